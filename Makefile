@@ -1,0 +1,31 @@
+# Builds the gfx950 kernel library (ctypes C ABI) and the native runtime (TFRecord IO, prefetcher).
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -munsafe-fp-atomics -Wno-unused-result
+CXXFLAGS ?= -O3 -std=c++17 -fPIC -Wall -Wno-unused-result
+PKG := homebrewnlp_mtf_amd
+KSRC := $(wildcard csrc/kernels/*.hip)
+KOBJ := $(patsubst csrc/kernels/%.hip,build/kernels/%.o,$(KSRC))
+RSRC := $(wildcard csrc/runtime/*.cpp)
+ROBJ := $(patsubst csrc/runtime/%.cpp,build/runtime/%.o,$(RSRC))
+
+all: $(PKG)/_kernels.so $(if $(RSRC),$(PKG)/_runtime.so,)
+
+build/kernels/%.o: csrc/kernels/%.hip csrc/kernels/common.h
+	@mkdir -p build/kernels
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(PKG)/_kernels.so: $(KOBJ)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(KOBJ)
+
+build/runtime/%.o: csrc/runtime/%.cpp $(wildcard csrc/runtime/*.h)
+	@mkdir -p build/runtime
+	g++ $(CXXFLAGS) -c $< -o $@
+
+$(PKG)/_runtime.so: $(ROBJ)
+	g++ $(CXXFLAGS) -shared -o $@ $(ROBJ) -lpthread
+
+clean:
+	rm -rf build $(PKG)/_kernels.so $(PKG)/_runtime.so
+
+.PHONY: all clean

@@ -1,0 +1,125 @@
+#!/usr/bin/env python3
+"""Headline benchmark: training tokens/sec for the whole node, GPT-Neo-1.3B-shaped model, seq 2048, bf16
+(BASELINE.json metric), one process per GPU over RCCL.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config configs/gpt_neo_1.3b.json] [--batch-per-gpu B]
+
+N > 1 is launched by the driver with ``torch.distributed.run`` (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* in the env).
+Weak scaling: every GPU processes ``batch-per-gpu`` sequences per step (global batch = B x N, DP over all ranks).
+Each timed step is a full training step: forward, backward, DP all-reduce, fused optimizer update. Data is synthetic
+(uniform random tokens, resident on the device) and the weights are randomly initialised.
+Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from homebrewnlp_mtf_amd.config import load_config  # noqa: E402
+from homebrewnlp_mtf_amd.models.model import count_flops_per_token  # noqa: E402
+from homebrewnlp_mtf_amd.parallel import state as pstate  # noqa: E402
+from homebrewnlp_mtf_amd.run.trainer import Trainer  # noqa: E402
+from homebrewnlp_mtf_amd.utils.log import log  # noqa: E402
+
+PEAK_BF16_DENSE = 2.5e15  # MI355X dense bf16 MFMA peak (spec, no sparsity)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default=os.path.join(os.path.dirname(os.path.abspath(__file__)), "configs",
+                                                     "gpt_neo_1.3b.json"))
+    ap.add_argument("--batch-per-gpu", type=int, default=0, help="default: config train_batch_size")
+    ap.add_argument("--depth", type=int, default=0, help="(debug only: invalidates the headline number)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one process per GPU)")
+        raise SystemExit(f"WORLD_SIZE={world} != --gpus {args.gpus}")
+    torch.cuda.set_device(local_rank)
+    device = torch.device("cuda", local_rank)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=device)
+    mesh = pstate.Mesh(dp=world, tp=1, rank=rank).build_groups()
+
+    overrides = {}
+    base = load_config(args.config)
+    per_gpu = args.batch_per_gpu or base.train_batch_size
+    overrides["train_batch_size"] = per_gpu * world
+    overrides["mesh"] = {"dp": world, "tp": 1}
+    if args.depth:
+        overrides["depth"] = args.depth
+    params = load_config(args.config, overrides)
+    torch.manual_seed(1234 + rank)
+    trainer = Trainer(params, device, mesh)
+
+    S = params.sequence_length
+    B = trainer.local_batch
+    gen = torch.Generator(device=device)
+    gen.manual_seed(4321 + rank)
+    batches = []
+    for _ in range(4):
+        toks = torch.randint(0, params.vocab_size, (B, S + 1, 1), device=device, generator=gen)
+        batches.append({"token_x": toks[:, :-1].contiguous(), "token_y": toks[:, 1:].contiguous()})
+
+    def barrier():
+        if world > 1:
+            dist.barrier(device_ids=[local_rank])
+
+    t_w = time.time()
+    for i in range(args.warmup):
+        m = trainer.step(batches[i % len(batches)])
+        if i == 0:
+            torch.cuda.synchronize()
+            log(f"first step done ({time.time() - t_w:.1f}s) loss={float(m['loss']):.4f}")
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        m = trainer.step(batches[i % len(batches)])
+    torch.cuda.synchronize()
+    barrier()
+    t1 = time.perf_counter()
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    elapsed = float(elapsed)
+    ms = 1000.0 * elapsed / max(args.steps, 1)
+    tokens = params.train_batch_size * S * args.steps
+    tps = tokens / elapsed
+    fpt = count_flops_per_token(params, trainer.store)
+    mfu = tps * fpt / (PEAK_BF16_DENSE * world)
+    if rank == 0:
+        log(f"loss={float(m['loss']):.4f} acc={float(m['accuracy']):.4f} step={ms:.1f}ms "
+            f"tokens/s={tps:.0f} MFU={mfu * 100:.1f}% ({fpt / 1e9:.2f} GFLOP/token)")
+        print(json.dumps({
+            "metric": "tokens/sec (whole node), GPT-Neo-1.3B seq2048 bf16",
+            "value": round(tps, 1), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "bf16", "data": "synthetic (uniform random tokens), random-init weights",
+            "mfu": round(mfu, 4), "final_loss": round(float(m["loss"]), 4),
+            "config": {"model": os.path.basename(args.config).replace(".json", "") +
+                                (f"-depth{args.depth}(debug)" if args.depth else ""),
+                       "global_batch": params.train_batch_size, "seq_len": S, "parallelism": f"dp{world}",
+                       "params": trainer.store.global_numel(), "optimizer": params.optimizer}}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,499 @@
+// K04: flash attention (causal / full) for gfx950 with v_mfma_f32_16x16x32_bf16.
+// Reference semantics (src/model/spatial.py:44-81): logits = q·kᵀ·scale (scale is a runtime argument: the
+// reference uses attention-dim length^-0.5, quirk A1), causal mask by -inf (ref adds -2e38), max-subtracted
+// softmax, ·v. Tensors are token-major [B, S, H, D] (row stride H*D) -- the layout the q/k/v linears write --
+// so no transposes are needed around the kernel. LSE/delta are fp32 [B, H, S].
+//
+// Orientation (cdna_hip_programming.md §3 "accumulator tile as the next MFMA's operand", Appendix B attention):
+//  * forward and dQ kernels compute Sᵀ = K·Qᵀ, so a lane owns one query column (lane&15) and 16 keys of a
+//    64-key block: the softmax row max/sum is 15 local ops + 2 xor-shuffles, and the rescale of Oᵀ is lane-uniform.
+//  * the P / dS accumulators feed the next MFMA directly as B operand (bf16-packed in registers) with a permuted
+//    k order; the matching A operand (V or K, [key][d] in LDS) is read with ds_read_b64_tr_b16 (T10).
+//  * the dK/dV kernel computes S = Q·Kᵀ (key on the lane) so dVᵀ += dOᵀ·P and dKᵀ += Qᵀ·dS reuse the registers.
+// dQ is produced by its own kernel (recomputing S and dP) instead of fp32 atomics: at S=2048 the atomic dQ sum
+// would move ~16x the dQ bytes through the ~1.3 TB/s atomic path (Guideline 12).
+#include "common.h"
+
+namespace {
+
+constexpr int NTH = 256;  // 4 waves
+
+template <int D>
+struct Geo {
+  static constexpr int CPR = D / 8;        // 16-byte chunks per row
+  static constexpr int DS = D / 32;        // k-steps over the head dim
+  static constexpr int DT = D / 16;        // 16-wide d tiles
+  static constexpr int ROWB = D * 2;       // bytes per row
+};
+
+// one XOR-swizzle per head dim, used for every tile (row reads via ds_read_b128 and transposed reads via
+// ds_read_b64_tr_b16); layout (b) of cdna_hip_programming.md T10 for D=128.
+template <int D>
+__device__ __forceinline__ int swz(int row) {
+  if (D == 128) return ((row & 3) << 2) | ((row >> 2) & 3);
+  if (D == 64) return ((row >> 1) & 3) << 1 | ((row >> 3) & 1);
+  return (row >> 2) & 3;
+}
+
+template <int D>
+__device__ __forceinline__ int lds_off(int row, int chunk) {
+  return row * Geo<D>::ROWB + ((chunk ^ swz<D>(row)) << 4);
+}
+
+// stage ROWS x D bf16 rows (token-major, row stride ld) into LDS; rows >= nvalid are zero-filled
+template <int D, int ROWS>
+__device__ __forceinline__ void stage_rows(char* lds, const bf16_t* g, long long ld, int nvalid, int tid) {
+  constexpr int CH = ROWS * Geo<D>::CPR;
+#pragma unroll
+  for (int i = 0; i < (CH + NTH - 1) / NTH; ++i) {
+    const int q = tid + i * NTH;
+    if (CH % NTH == 0 || q < CH) {
+      const int row = q / Geo<D>::CPR, c = q % Geo<D>::CPR;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (row < nvalid) v = *reinterpret_cast<const uint4*>(g + row * ld + c * 8);
+      *reinterpret_cast<uint4*>(lds + lds_off<D>(row, c)) = v;
+    }
+  }
+}
+
+// row fragment: lane holds X[row0 + (lane&15)][d = ds*32 + 8*(lane>>4) + 0..7]
+template <int D>
+__device__ __forceinline__ bf16x8_t row_frag(const char* lds, int row0, int ds, int lane) {
+  const int r = row0 + (lane & 15);
+  return *reinterpret_cast<const bf16x8_t*>(lds + lds_off<D>(r, ds * 4 + (lane >> 4)));
+}
+
+// transposed fragment over 32 rows starting at row0: lane (g, i) holds X[row0 + perm(g, jj)][d0 + i],
+// perm(g, jj) = (jj >> 2) * 16 + 4g + (jj & 3)
+template <int D>
+__device__ __forceinline__ bf16x8_t tr_frag(const char* lds, int row0, int d0, int lane) {
+  const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, pp = i16 & 3;
+  const int col = d0 + 4 * pp;
+  const int c = col >> 3;
+  const int r0 = row0 + 4 * g + q, r1 = r0 + 16;
+  const int o0 = r0 * Geo<D>::ROWB + ((c ^ swz<D>(r0)) << 4) + ((pp & 1) << 3);
+  const int o1 = r1 * Geo<D>::ROWB + ((c ^ swz<D>(r1)) << 4) + ((pp & 1) << 3);
+  s16x4_t v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4_t, lds + o0));
+  s16x4_t v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4_t, lds + o1));
+  s16x8_t v = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+
+// pack two 16x16 fp32 accumulator tiles (k-halves) into one bf16x8 B-operand with the perm() k order
+__device__ __forceinline__ bf16x8_t pack_p(const f32x4_t& a, const f32x4_t& b) {
+  s16x8_t v;
+  v[0] = (short)f2bf(a[0]); v[1] = (short)f2bf(a[1]); v[2] = (short)f2bf(a[2]); v[3] = (short)f2bf(a[3]);
+  v[4] = (short)f2bf(b[0]); v[5] = (short)f2bf(b[1]); v[6] = (short)f2bf(b[2]); v[7] = (short)f2bf(b[3]);
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+
+__device__ __forceinline__ bf16x8_t load_frag_g(const bf16_t* p, bool ok) {
+  if (!ok) return __builtin_bit_cast(bf16x8_t, s16x8_t{0, 0, 0, 0, 0, 0, 0, 0});
+  return *reinterpret_cast<const bf16x8_t*>(p);
+}
+
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr float NEG_BIG = -1e30f;
+
+struct AttnArgs {
+  const bf16_t *Q, *K, *V, *O, *dO;
+  bf16_t *Oout, *dQ, *dK, *dV;
+  float *LSE, *delta;
+  int B, S, H;
+  long long ld;   // token stride (elements), usually H*D
+  float scale;
+  int causal;
+};
+
+// ----------------------------------------------------------------------------------------------------------------
+// forward: block = 128 queries of one (b, h); wave w owns queries q0 + 32w + [0, 32)
+template <int D>
+__global__ __launch_bounds__(NTH, 2) void attn_fwd_kernel(AttnArgs a) {
+  using G = Geo<D>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* sK = smem;
+  char* sV = smem + 64 * G::ROWB;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, i = lane & 15;
+  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+  const int qblk = blockIdx.x * 128;
+  const int qw = qblk + w * 32;
+  const bf16_t* Qb = a.Q + (long long)b * a.S * a.ld + h * D;
+  const bf16_t* Kb = a.K + (long long)b * a.S * a.ld + h * D;
+  const bf16_t* Vb = a.V + (long long)b * a.S * a.ld + h * D;
+
+  bf16x8_t qf[2][G::DS];
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    const int q = qw + qt * 16 + i;
+#pragma unroll
+    for (int ds = 0; ds < G::DS; ++ds) qf[qt][ds] = load_frag_g(Qb + (long long)q * a.ld + ds * 32 + 8 * g, q < a.S);
+  }
+  f32x4_t o[G::DT][2];
+#pragma unroll
+  for (int dt = 0; dt < G::DT; ++dt) o[dt][0] = o[dt][1] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  float m[2] = {NEG_BIG, NEG_BIG}, l[2] = {0.f, 0.f};
+  const float c2 = a.scale * LOG2E;
+
+  const int kend = a.causal ? min(a.S, qblk + 128) : a.S;
+  for (int k0 = 0; k0 < kend; k0 += 64) {
+    __syncthreads();
+    stage_rows<D, 64>(sK, Kb + (long long)k0 * a.ld, a.ld, a.S - k0, tid);
+    stage_rows<D, 64>(sV, Vb + (long long)k0 * a.ld, a.ld, a.S - k0, tid);
+    __syncthreads();
+    if (a.causal && k0 > qw + 31) continue;  // wave-uniform: every key of this block is in this wave's future
+    f32x4_t s[2][4];
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) s[qt][kt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ds = 0; ds < G::DS; ++ds) {
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) {
+        bf16x8_t kf = row_frag<D>(sK, kt * 16, ds, lane);
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt) s[qt][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[qt][ds], s[qt][kt], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      const int q = qw + qt * 16 + i;
+      float mx = NEG_BIG;
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int key = k0 + kt * 16 + 4 * g + v;
+          float x = s[qt][kt][v] * c2;
+          if (key >= a.S || (a.causal && key > q)) x = -INFINITY;
+          s[qt][kt][v] = x;
+          mx = fmaxf(mx, x);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mn = fmaxf(m[qt], mx);
+      const float alpha = exp2f(m[qt] - mn);
+      float rs = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const float p = exp2f(s[qt][kt][v] - mn);
+          s[qt][kt][v] = p;
+          rs += p;
+        }
+      rs += __shfl_xor(rs, 16, 64);
+      rs += __shfl_xor(rs, 32, 64);
+      l[qt] = l[qt] * alpha + rs;
+      m[qt] = mn;
+#pragma unroll
+      for (int dt = 0; dt < G::DT; ++dt) o[dt][qt] *= alpha;
+    }
+    bf16x8_t pf[2][2];
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      pf[qt][0] = pack_p(s[qt][0], s[qt][1]);
+      pf[qt][1] = pack_p(s[qt][2], s[qt][3]);
+    }
+#pragma unroll
+    for (int dt = 0; dt < G::DT; ++dt) {
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        bf16x8_t vf = tr_frag<D>(sV, st * 32, dt * 16, lane);
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt) o[dt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[qt][st], o[dt][qt], 0, 0, 0);
+      }
+    }
+  }
+  // epilogue: lane holds O[q = qw + qt*16 + i][d = dt*16 + 4g + v]
+  bf16_t* Ob = a.Oout + (long long)b * a.S * a.ld + h * D;
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    const int q = qw + qt * 16 + i;
+    if (q >= a.S) continue;
+    const float inv = 1.f / l[qt];
+#pragma unroll
+    for (int dt = 0; dt < G::DT; ++dt) {
+      const int d = dt * 16 + 4 * g;
+      *reinterpret_cast<uint2*>(Ob + (long long)q * a.ld + d) =
+          make_uint2(pack_bf16x2(o[dt][qt][0] * inv, o[dt][qt][1] * inv), pack_bf16x2(o[dt][qt][2] * inv, o[dt][qt][3] * inv));
+    }
+    if (g == 0) a.LSE[((long long)b * a.H + h) * a.S + q] = (m[qt] + log2f(l[qt])) / LOG2E;
+  }
+}
+
+// ----------------------------------------------------------------------------------------------------------------
+// delta[b,h,q] = sum_d dO * O
+template <int D>
+__global__ __launch_bounds__(NTH) void attn_delta_kernel(AttnArgs a) {
+  const int lane = threadIdx.x & 63;
+  const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);  // row = (b*S + q)*H + h
+  const long long nrows = (long long)a.B * a.S * a.H;
+  if (row >= nrows) return;
+  const int h = row % a.H;
+  const long long bq = row / a.H;
+  const int q = bq % a.S, b = bq / a.S;
+  const bf16_t* o = a.O + bq * a.ld + h * D;
+  const bf16_t* d = a.dO + bq * a.ld + h * D;
+  float acc = 0.f;
+  for (int j = lane * 2; j < D; j += 128) {
+    uint32_t ov = *reinterpret_cast<const uint32_t*>(o + j);
+    uint32_t dv = *reinterpret_cast<const uint32_t*>(d + j);
+    acc += bf2f(ov & 0xffff) * bf2f(dv & 0xffff) + bf2f(ov >> 16) * bf2f(dv >> 16);
+  }
+  acc = wave_sum(acc);
+  if (lane == 0) a.delta[((long long)b * a.H + h) * a.S + q] = acc;
+}
+
+// ----------------------------------------------------------------------------------------------------------------
+// dQ: block = 128 queries; recompute Sᵀ, Pᵀ, dPᵀ = V·dOᵀ, dSᵀ, dQᵀ += Kᵀ·dSᵀ
+template <int D>
+__global__ __launch_bounds__(NTH, 2) void attn_bwd_dq_kernel(AttnArgs a) {
+  using G = Geo<D>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* sK = smem;
+  char* sV = smem + 64 * G::ROWB;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, i = lane & 15;
+  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+  const int qblk = blockIdx.x * 128;
+  const int qw = qblk + w * 32;
+  const long long base = (long long)b * a.S * a.ld + h * D;
+
+  bf16x8_t qf[2][G::DS], df[2][G::DS];
+  float lse2[2], dlt[2];
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    const int q = qw + qt * 16 + i;
+    const bool ok = q < a.S;
+#pragma unroll
+    for (int ds = 0; ds < G::DS; ++ds) {
+      qf[qt][ds] = load_frag_g(a.Q + base + (long long)q * a.ld + ds * 32 + 8 * g, ok);
+      df[qt][ds] = load_frag_g(a.dO + base + (long long)q * a.ld + ds * 32 + 8 * g, ok);
+    }
+    const long long si = ((long long)b * a.H + h) * a.S + (ok ? q : 0);
+    lse2[qt] = a.LSE[si] * LOG2E;
+    dlt[qt] = a.delta[si];
+  }
+  f32x4_t acc[G::DT][2];
+#pragma unroll
+  for (int dt = 0; dt < G::DT; ++dt) acc[dt][0] = acc[dt][1] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const float c2 = a.scale * LOG2E;
+  const int kend = a.causal ? min(a.S, qblk + 128) : a.S;
+  for (int k0 = 0; k0 < kend; k0 += 64) {
+    __syncthreads();
+    stage_rows<D, 64>(sK, a.K + base + (long long)k0 * a.ld, a.ld, a.S - k0, tid);
+    stage_rows<D, 64>(sV, a.V + base + (long long)k0 * a.ld, a.ld, a.S - k0, tid);
+    __syncthreads();
+    if (a.causal && k0 > qw + 31) continue;
+    f32x4_t s[2][4], dp[2][4];
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) s[qt][kt] = dp[qt][kt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ds = 0; ds < G::DS; ++ds) {
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) {
+        bf16x8_t kf = row_frag<D>(sK, kt * 16, ds, lane);
+        bf16x8_t vf = row_frag<D>(sV, kt * 16, ds, lane);
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt) {
+          s[qt][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[qt][ds], s[qt][kt], 0, 0, 0);
+          dp[qt][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, df[qt][ds], dp[qt][kt], 0, 0, 0);
+        }
+      }
+    }
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      const int q = qw + qt * 16 + i;
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int key = k0 + kt * 16 + 4 * g + v;
+          float p = exp2f(s[qt][kt][v] * c2 - lse2[qt]);
+          if (key >= a.S || (a.causal && key > q)) p = 0.f;
+          s[qt][kt][v] = p * (dp[qt][kt][v] - dlt[qt]);
+        }
+    }
+    bf16x8_t sf[2][2];
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      sf[qt][0] = pack_p(s[qt][0], s[qt][1]);
+      sf[qt][1] = pack_p(s[qt][2], s[qt][3]);
+    }
+#pragma unroll
+    for (int dt = 0; dt < G::DT; ++dt)
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        bf16x8_t kf = tr_frag<D>(sK, st * 32, dt * 16, lane);
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt) acc[dt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, sf[qt][st], acc[dt][qt], 0, 0, 0);
+      }
+  }
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    const int q = qw + qt * 16 + i;
+    if (q >= a.S) continue;
+#pragma unroll
+    for (int dt = 0; dt < G::DT; ++dt) {
+      const int d = dt * 16 + 4 * g;
+      const float sc = a.scale;
+      *reinterpret_cast<uint2*>(a.dQ + base + (long long)q * a.ld + d) =
+          make_uint2(pack_bf16x2(acc[dt][qt][0] * sc, acc[dt][qt][1] * sc), pack_bf16x2(acc[dt][qt][2] * sc, acc[dt][qt][3] * sc));
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------------------------------------------
+// dK/dV: block = 64 keys; wave w owns keys k0 + 16w + [0,16). Loop over 32-query chunks staged in LDS.
+template <int D>
+__global__ __launch_bounds__(NTH, 2) void attn_bwd_dkv_kernel(AttnArgs a) {
+  using G = Geo<D>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* sQ = smem;
+  char* sD = smem + 32 * G::ROWB;
+  float* sL = reinterpret_cast<float*>(smem + 64 * G::ROWB);
+  float* sDl = sL + 32;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, i = lane & 15;
+  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+  const int kblk = blockIdx.x * 64;
+  const int kw = kblk + w * 16;
+  const long long base = (long long)b * a.S * a.ld + h * D;
+  const long long sbase = ((long long)b * a.H + h) * a.S;
+
+  bf16x8_t kf[G::DS], vf[G::DS];
+  {
+    const int key = kw + i;
+    const bool ok = key < a.S;
+#pragma unroll
+    for (int ds = 0; ds < G::DS; ++ds) {
+      kf[ds] = load_frag_g(a.K + base + (long long)key * a.ld + ds * 32 + 8 * g, ok);
+      vf[ds] = load_frag_g(a.V + base + (long long)key * a.ld + ds * 32 + 8 * g, ok);
+    }
+  }
+  f32x4_t dk[G::DT], dv[G::DT];
+#pragma unroll
+  for (int dt = 0; dt < G::DT; ++dt) dk[dt] = dv[dt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const float c2 = a.scale * LOG2E;
+  const int qstart = a.causal ? (kblk / 32) * 32 : 0;
+  for (int q0 = qstart; q0 < a.S; q0 += 32) {
+    __syncthreads();
+    stage_rows<D, 32>(sQ, a.Q + base + (long long)q0 * a.ld, a.ld, a.S - q0, tid);
+    stage_rows<D, 32>(sD, a.dO + base + (long long)q0 * a.ld, a.ld, a.S - q0, tid);
+    if (tid < 32) {
+      const int q = q0 + tid;
+      sL[tid] = q < a.S ? a.LSE[sbase + q] * LOG2E : 0.f;
+      sDl[tid] = q < a.S ? a.delta[sbase + q] : 0.f;
+    }
+    __syncthreads();
+    if (a.causal && q0 + 31 < kw) continue;  // every query of this chunk precedes this wave's keys
+    f32x4_t s[2], dp[2];
+    s[0] = s[1] = dp[0] = dp[1] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ds = 0; ds < G::DS; ++ds) {
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) {
+        bf16x8_t qa = row_frag<D>(sQ, qt * 16, ds, lane);
+        bf16x8_t da = row_frag<D>(sD, qt * 16, ds, lane);
+        s[qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa, kf[ds], s[qt], 0, 0, 0);
+        dp[qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, vf[ds], dp[qt], 0, 0, 0);
+      }
+    }
+    // s[qt][v] = S[q = q0 + qt*16 + 4g + v][key = kw + i]
+    f32x4_t p[2], dsv[2];
+    const int key = kw + i;
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int ql = qt * 16 + 4 * g + v;
+        const int q = q0 + ql;
+        float pv = exp2f(s[qt][v] * c2 - sL[ql]);
+        if (q >= a.S || key >= a.S || (a.causal && key > q)) pv = 0.f;
+        p[qt][v] = pv;
+        dsv[qt][v] = pv * (dp[qt][v] - sDl[ql]);
+      }
+    const bf16x8_t pb = pack_p(p[0], p[1]);
+    const bf16x8_t sb = pack_p(dsv[0], dsv[1]);
+#pragma unroll
+    for (int dt = 0; dt < G::DT; ++dt) {
+      bf16x8_t dot = tr_frag<D>(sD, 0, dt * 16, lane);
+      bf16x8_t qtr = tr_frag<D>(sQ, 0, dt * 16, lane);
+      dv[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dot, pb, dv[dt], 0, 0, 0);
+      dk[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qtr, sb, dk[dt], 0, 0, 0);
+    }
+  }
+  const int key = kw + i;
+  if (key < a.S) {
+#pragma unroll
+    for (int dt = 0; dt < G::DT; ++dt) {
+      const int d = dt * 16 + 4 * g;
+      const float sc = a.scale;
+      *reinterpret_cast<uint2*>(a.dK + base + (long long)key * a.ld + d) =
+          make_uint2(pack_bf16x2(dk[dt][0] * sc, dk[dt][1] * sc), pack_bf16x2(dk[dt][2] * sc, dk[dt][3] * sc));
+      *reinterpret_cast<uint2*>(a.dV + base + (long long)key * a.ld + d) =
+          make_uint2(pack_bf16x2(dv[dt][0], dv[dt][1]), pack_bf16x2(dv[dt][2], dv[dt][3]));
+    }
+  }
+}
+
+template <int D>
+int launch_fwd(const AttnArgs& a, hipStream_t st) {
+  dim3 grid((a.S + 127) / 128, a.B * a.H);
+  hipLaunchKernelGGL(attn_fwd_kernel<D>, grid, dim3(NTH), 128 * Geo<D>::ROWB, st, a);
+  return (int)hipGetLastError();
+}
+
+template <int D>
+int launch_bwd(const AttnArgs& a, hipStream_t st) {
+  const long long rows = (long long)a.B * a.S * a.H;
+  hipLaunchKernelGGL(attn_delta_kernel<D>, dim3((unsigned)((rows + 3) / 4)), dim3(NTH), 0, st, a);
+  hipLaunchKernelGGL(attn_bwd_dkv_kernel<D>, dim3((a.S + 63) / 64, a.B * a.H), dim3(NTH), 64 * Geo<D>::ROWB + 256,
+                     st, a);
+  hipLaunchKernelGGL(attn_bwd_dq_kernel<D>, dim3((a.S + 127) / 128, a.B * a.H), dim3(NTH), 128 * Geo<D>::ROWB, st, a);
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+struct ObstAttnDesc {
+  const void *Q, *K, *V, *O, *dO;
+  void *Oout, *dQ, *dK, *dV;
+  float *LSE, *delta;
+  int B, S, H, D;
+  long long ld;
+  float scale;
+  int causal;
+};
+
+static bool fill(AttnArgs& a, const ObstAttnDesc* d) {
+  a.Q = (const bf16_t*)d->Q; a.K = (const bf16_t*)d->K; a.V = (const bf16_t*)d->V;
+  a.O = (const bf16_t*)d->O; a.dO = (const bf16_t*)d->dO;
+  a.Oout = (bf16_t*)d->Oout; a.dQ = (bf16_t*)d->dQ; a.dK = (bf16_t*)d->dK; a.dV = (bf16_t*)d->dV;
+  a.LSE = d->LSE; a.delta = d->delta;
+  a.B = d->B; a.S = d->S; a.H = d->H; a.ld = d->ld; a.scale = d->scale; a.causal = d->causal;
+  return d->B > 0 && d->S > 0 && d->H > 0 && d->ld % 8 == 0 && d->ld >= (long long)d->H * d->D;
+}
+
+OBST_API int obst_attn_fwd(const ObstAttnDesc* d, hipStream_t st) {
+  AttnArgs a;
+  if (!fill(a, d)) return -1;
+  switch (d->D) {
+    case 32: return launch_fwd<32>(a, st);
+    case 64: return launch_fwd<64>(a, st);
+    case 128: return launch_fwd<128>(a, st);
+    default: return -2;
+  }
+}
+
+OBST_API int obst_attn_bwd(const ObstAttnDesc* d, hipStream_t st) {
+  AttnArgs a;
+  if (!fill(a, d)) return -1;
+  switch (d->D) {
+    case 32: return launch_bwd<32>(a, st);
+    case 64: return launch_bwd<64>(a, st);
+    case 128: return launch_bwd<128>(a, st);
+    default: return -2;
+  }
+}

@@ -1,0 +1,185 @@
+// K06/K07/K08/K09/K13 and small memory-bound helpers. Every kernel moves bf16 as 16-byte vectors (8 elements
+// per lane, Guideline 13) with a grid-stride loop capped at 256 CUs x 8 blocks (Guideline 11).
+//  * activations fwd/bwd (src/model/activation.py: relu, sigmoid, tanh, gelu, lecun_tanh, silu, mish, softsign, exp)
+//  * residual add, rezero (x * g), dropout (counter-based hash RNG, keep-mask recomputed in backward)
+//  * embedding gather (K08, src/model/embedding.py:91-125) and scatter-add gradient (K09) into the fp32 grad buffer
+//  * cumsum / cummean along the sequence (K13, src/model/spatial.py:26-39) and its reverse-cumsum gradient
+#include "common.h"
+
+namespace {
+
+constexpr int NTH = 256;
+
+inline int grid_for(long long n_vec) {
+  long long g = (n_vec + NTH - 1) / NTH;
+  return (int)(g < 2048 ? (g < 1 ? 1 : g) : 2048);
+}
+
+__device__ __forceinline__ void unpack8(const uint4& u, float (&f)[8]) {
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { f[2 * j] = bf2f(w[j] & 0xffff); f[2 * j + 1] = bf2f(w[j] >> 16); }
+}
+
+__device__ __forceinline__ uint4 pack8(const float (&f)[8]) {
+  return make_uint4(pack_bf16x2(f[0], f[1]), pack_bf16x2(f[2], f[3]), pack_bf16x2(f[4], f[5]), pack_bf16x2(f[6], f[7]));
+}
+
+// op: 0 act fwd (y=act(x)), 1 act bwd (y = dy * act'(x)), 2 add (y = x + z), 3 mul scalar tensor (y = x * s[0]),
+//     4 dropout fwd/bwd (y = x * keep(i) / keep_prob), 5 axpby (y = alpha*x + beta*z), 6 mul (y = x*z)
+__global__ __launch_bounds__(NTH) void ew_kernel(int op, int act, const bf16_t* __restrict__ X,
+                                                 const bf16_t* __restrict__ Z, bf16_t* __restrict__ Y, long long nvec,
+                                                 const float* __restrict__ sptr, float alpha, float beta,
+                                                 unsigned long long seed, float keep) {
+  for (long long v = (long long)blockIdx.x * NTH + threadIdx.x; v < nvec; v += (long long)gridDim.x * NTH) {
+    float x[8], z[8];
+    unpack8(reinterpret_cast<const uint4*>(X)[v], x);
+    if (op == 1 || op == 2 || op == 5 || op == 6) unpack8(reinterpret_cast<const uint4*>(Z)[v], z);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float r;
+      switch (op) {
+        case 0: r = act_fwd(act, x[j]); break;
+        case 1: r = x[j] * 0.f + z[j] * act_grad(act, x[j]); break;  // X = saved input, Z = dy
+        case 2: r = x[j] + z[j]; break;
+        case 3: r = x[j] * sptr[0]; break;
+        case 4: {
+          unsigned long long h = (unsigned long long)(v * 8 + j) * 0x9E3779B97F4A7C15ull ^ seed;
+          h ^= h >> 33; h *= 0xff51afd7ed558ccdull; h ^= h >> 33; h *= 0xc4ceb9fe1a85ec53ull; h ^= h >> 33;
+          const float u = (float)(h >> 40) * (1.f / 16777216.f);
+          r = u < keep ? x[j] / keep : 0.f;
+          break;
+        }
+        case 5: r = alpha * x[j] + beta * z[j]; break;
+        case 6: r = x[j] * z[j]; break;
+        default: r = x[j];
+      }
+      x[j] = r;
+    }
+    reinterpret_cast<uint4*>(Y)[v] = pack8(x);
+  }
+}
+
+// sum of x*dy over all elements into out[0] (rezero gradient: d g = sum(x * dy))
+__global__ __launch_bounds__(NTH) void dot_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ DY,
+                                                  float* __restrict__ out, long long nvec) {
+  __shared__ float red[4];
+  float acc = 0.f;
+  for (long long v = (long long)blockIdx.x * NTH + threadIdx.x; v < nvec; v += (long long)gridDim.x * NTH) {
+    float x[8], d[8];
+    unpack8(reinterpret_cast<const uint4*>(X)[v], x);
+    unpack8(reinterpret_cast<const uint4*>(DY)[v], d);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc += x[j] * d[j];
+  }
+  acc = block_sum<4>(acc, red);
+  if (threadIdx.x == 0) atomicAdd(out, acc);
+}
+
+// out[t, :] = E[idx[t], :]   (E bf16 [V, F], F % 8 == 0)
+__global__ __launch_bounds__(NTH) void gather_kernel(const int* __restrict__ idx, const bf16_t* __restrict__ E,
+                                                     bf16_t* __restrict__ out, long long T, int F, int V) {
+  const int vpr = F / 8;
+  const long long n = T * vpr;
+  for (long long v = (long long)blockIdx.x * NTH + threadIdx.x; v < n; v += (long long)gridDim.x * NTH) {
+    const long long t = v / vpr;
+    const int c = v % vpr;
+    int r = idx[t];
+    r = r < 0 ? 0 : (r >= V ? V - 1 : r);
+    reinterpret_cast<uint4*>(out)[v] = reinterpret_cast<const uint4*>(E + (long long)r * F)[c];
+  }
+}
+
+// dE[idx[t], :] += dy[t, :]   (fp32 atomics; each wave-instruction covers 256 contiguous bytes of one row)
+__global__ __launch_bounds__(NTH) void scatter_add_kernel(const int* __restrict__ idx, const bf16_t* __restrict__ DY,
+                                                          float* __restrict__ dE, long long T, int F, int V) {
+  const long long n = T * F;
+  for (long long e = (long long)blockIdx.x * NTH + threadIdx.x; e < n; e += (long long)gridDim.x * NTH) {
+    const long long t = e / F;
+    const int c = e % F;
+    int r = idx[t];
+    r = r < 0 ? 0 : (r >= V ? V - 1 : r);
+    atomicAdd(dE + (long long)r * F + c, bf2f(DY[e]));
+  }
+}
+
+// cumulative sum over the sequence axis of x viewed as [outer, S, inner]; reverse for the gradient; cummean
+// divides by (position + 1) (backward of cummean = reverse-cumsum of dy / (pos+1)).
+__global__ __launch_bounds__(NTH) void cumsum_kernel(const bf16_t* __restrict__ X, bf16_t* __restrict__ Y,
+                                                     long long outer, int S, long long inner, int reverse, int mean,
+                                                     int grad) {
+  const long long n = outer * inner;
+  for (long long e = (long long)blockIdx.x * NTH + threadIdx.x; e < n; e += (long long)gridDim.x * NTH) {
+    const long long o = e / inner, in = e % inner;
+    const bf16_t* x = X + o * S * inner + in;
+    bf16_t* y = Y + o * S * inner + in;
+    float acc = 0.f;
+    for (int s = 0; s < S; ++s) {
+      const int p = reverse ? S - 1 - s : s;
+      float v = bf2f(x[(long long)p * inner]);
+      if (mean && grad) v /= (float)(p + 1);
+      acc += v;
+      float out = acc;
+      if (mean && !grad) out /= (float)(p + 1);
+      y[(long long)p * inner] = f2bf(out);
+    }
+  }
+}
+
+__global__ __launch_bounds__(NTH) void cast_f32_bf16_kernel(const float* __restrict__ X, bf16_t* __restrict__ Y,
+                                                            long long n) {
+  for (long long v = (long long)blockIdx.x * NTH + threadIdx.x; v * 4 < n; v += (long long)gridDim.x * NTH) {
+    if (v * 4 + 3 < n) {
+      float4 f = reinterpret_cast<const float4*>(X)[v];
+      reinterpret_cast<uint2*>(Y)[v] = make_uint2(pack_bf16x2(f.x, f.y), pack_bf16x2(f.z, f.w));
+    } else {
+      for (long long j = v * 4; j < n; ++j) Y[j] = f2bf(X[j]);
+    }
+  }
+}
+
+}  // namespace
+
+struct ObstEwDesc {
+  const void* X; const void* Z; void* Y; const float* sptr;
+  long long n; int op; int act; float alpha; float beta; unsigned long long seed; float keep;
+};
+
+OBST_API int obst_elementwise(const ObstEwDesc* d, hipStream_t st) {
+  if (d->n % 8) return -1;
+  if ((((uintptr_t)d->X) | ((uintptr_t)d->Y) | ((uintptr_t)d->Z)) & 15) return -2;
+  const long long nvec = d->n / 8;
+  hipLaunchKernelGGL(ew_kernel, dim3(grid_for(nvec)), dim3(NTH), 0, st, d->op, d->act, (const bf16_t*)d->X,
+                     (const bf16_t*)d->Z, (bf16_t*)d->Y, nvec, d->sptr, d->alpha, d->beta, d->seed, d->keep);
+  return (int)hipGetLastError();
+}
+
+OBST_API int obst_dot(const void* X, const void* DY, float* out, long long n, hipStream_t st) {
+  if (n % 8) return -1;
+  hipLaunchKernelGGL(dot_kernel, dim3(grid_for(n / 8)), dim3(NTH), 0, st, (const bf16_t*)X, (const bf16_t*)DY, out, n / 8);
+  return (int)hipGetLastError();
+}
+
+OBST_API int obst_gather(const int* idx, const void* E, void* out, long long T, int F, int V, hipStream_t st) {
+  if (F % 8) return -1;
+  hipLaunchKernelGGL(gather_kernel, dim3(grid_for(T * F / 8)), dim3(NTH), 0, st, idx, (const bf16_t*)E, (bf16_t*)out,
+                     T, F, V);
+  return (int)hipGetLastError();
+}
+
+OBST_API int obst_scatter_add(const int* idx, const void* DY, float* dE, long long T, int F, int V, hipStream_t st) {
+  hipLaunchKernelGGL(scatter_add_kernel, dim3(grid_for(T * F)), dim3(NTH), 0, st, idx, (const bf16_t*)DY, dE, T, F, V);
+  return (int)hipGetLastError();
+}
+
+OBST_API int obst_cumsum(const void* X, void* Y, long long outer, int S, long long inner, int reverse, int mean,
+                         int grad, hipStream_t st) {
+  hipLaunchKernelGGL(cumsum_kernel, dim3(grid_for(outer * inner)), dim3(NTH), 0, st, (const bf16_t*)X, (bf16_t*)Y,
+                     outer, S, inner, reverse, mean, grad);
+  return (int)hipGetLastError();
+}
+
+OBST_API int obst_cast_f32_bf16(const float* X, void* Y, long long n, hipStream_t st) {
+  hipLaunchKernelGGL(cast_f32_bf16_kernel, dim3(grid_for((n + 3) / 4)), dim3(NTH), 0, st, X, (bf16_t*)Y, n);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,281 @@
+// K01/K02: bf16 MFMA GEMM for gfx950 with fused epilogues. One kernel template serves the forward (X·W),
+// data-gradient (dY·Wᵀ) and weight-gradient (Xᵀ·dY) products of every linear in the block grammar
+// (reference einsum sites: src/model/backend.py:108-110, basic.py:33-126, spatial.py:45-81), as a
+// strided, two-level-batched GEMM (batch = heads for `group` linears, heads×batch for the token mixer).
+//
+//   C[m][n] = epilogue( alpha * sum_k A(m,k) * B(k,n) )
+//   A_T = 0 : A stored [M][K] (K contiguous)      A_T = 1 : A stored [K][M] (M contiguous)
+//   B_T = 0 : B stored [N][K] (K contiguous)      B_T = 1 : B stored [K][N] (N contiguous)
+//
+// Design (cdna_hip_programming.md §5): 128x128x64 block tile, 4 waves (2x2), each wave 64x64 = 4x4 tiles of
+// v_mfma_f32_16x16x32_bf16; register-staged double-buffered LDS with ONE barrier per K-step (loads for tile k+1
+// are issued before the MFMAs of tile k). K-contiguous operands are read with ds_read_b128 from an XOR-swizzled
+// [rows][64] image (conflict-free: chunk ^= (row>>1)&7); M/N-contiguous operands are stored [64][128] as loaded
+// (coalesced) and read through the CDNA4 hardware transpose ds_read_b64_tr_b16 with chunk ^= f(k) so both
+// 16-lane groups of a half-wave hit distinct banks. The MFMA is issued as mfma(B, A) so each lane ends with 4
+// consecutive output columns (8-byte bf16 / 16-byte fp32 stores). Block ids are remapped XCD-aware (T1) and
+// grouped 8 tiles along M so blocks that share an XCD share A panels in its L2.
+#include "common.h"
+
+namespace {
+
+constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
+constexpr int TILE_BYTES = 128 * 64 * 2;  // one operand tile, either image
+
+struct GemmArgs {
+  const bf16_t* A; const bf16_t* B; void* C;
+  const void* R;          // residual added before the activation (same dtype/layout as C) or null
+  bf16_t* Zout;           // pre-activation output (bf16, layout of C) or null
+  const bf16_t* Zin;      // saved pre-activation for the activation-backward epilogue (layout of C)
+  long long lda, ldb, ldc;
+  long long a_s1, a_s2, b_s1, b_s2, c_s1, c_s2;
+  int M, N, K, nb2;
+  int tiles_m, tiles_n;
+  float alpha, beta;      // beta: fp32 output only, C = alpha*acc + beta*C_old (gradient accumulation)
+  int act, mode;          // mode 0: out = act(alpha*acc + R); mode 1: out = (alpha*acc + R) * act'(Zin)
+};
+
+__device__ __forceinline__ int kswz(int k) { return ((k & 3) << 1) | (((k >> 3) & 1) << 3); }
+
+// --- staging: global -> registers -------------------------------------------------------------------------------
+template <int T>
+__device__ __forceinline__ void load_tile(uint4 (&reg)[4], const bf16_t* X, long long ld, int r0, int R, int k0,
+                                          int K, int tid) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int q = tid + i * NT;
+    int row, col;
+    bool ok;
+    const bf16_t* g;
+    if (T == 0) {  // [rows][K]
+      row = q >> 3; col = (q & 7) * 8;
+      ok = (r0 + row < R) && (k0 + col < K);
+      g = X + (long long)(r0 + row) * ld + (k0 + col);
+    } else {       // [K][rows]
+      row = q >> 4; col = (q & 15) * 8;
+      ok = (k0 + row < K) && (r0 + col < R);
+      g = X + (long long)(k0 + row) * ld + (r0 + col);
+    }
+    reg[i] = ok ? *reinterpret_cast<const uint4*>(g) : make_uint4(0, 0, 0, 0);
+  }
+}
+
+template <int T>
+__device__ __forceinline__ void store_tile(char* lds, const uint4 (&reg)[4], int tid) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int q = tid + i * NT;
+    int off;
+    if (T == 0) {
+      const int row = q >> 3, c = q & 7;
+      off = row * 128 + ((c ^ ((row >> 1) & 7)) << 4);
+    } else {
+      const int k = q >> 4, c = q & 15;
+      off = k * 256 + ((c ^ kswz(k)) << 4);
+    }
+    *reinterpret_cast<uint4*>(lds + off) = reg[i];
+  }
+}
+
+// --- LDS -> MFMA fragment (8 consecutive k of one row/col) -------------------------------------------------------
+template <int T>
+__device__ __forceinline__ bf16x8_t read_frag(const char* lds, int rbase, int kk, int lane) {
+  if (T == 0) {
+    const int r = rbase + (lane & 15);
+    const int c = kk * 4 + (lane >> 4);
+    return *reinterpret_cast<const bf16x8_t*>(lds + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
+  } else {
+    const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, pp = i16 & 3;
+    const int col = rbase + 4 * pp;
+    const int c = col >> 3;
+    const int k0 = kk * 32 + 8 * g + q;
+    const int k1 = k0 + 4;
+    const int off0 = k0 * 256 + ((c ^ kswz(k0)) << 4) + ((pp & 1) << 3);
+    const int off1 = k1 * 256 + ((c ^ kswz(k1)) << 4) + ((pp & 1) << 3);
+    s16x4_t v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4_t, lds + off0));
+    s16x4_t v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4_t, lds + off1));
+    s16x8_t v = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+    return __builtin_bit_cast(bf16x8_t, v);
+  }
+}
+
+template <int A_T, int B_T, bool OUT_F32>
+__global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(GemmArgs p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  // stage s: A image at smem + s*2*TILE_BYTES, B image right after it
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  // XCD-aware bijective remap (T1), then GROUP=8 ordering along M.
+  int bid = blockIdx.x;
+  {
+    const int nwg = gridDim.x, xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+    bid = base + (bid >> 3);
+  }
+  const int GROUP = 8;
+  const int per_group = GROUP * p.tiles_n;
+  const int first_m = (bid / per_group) * GROUP;
+  const int gsz = min(p.tiles_m - first_m, GROUP);
+  const int tm = first_m + (bid % per_group) % gsz;
+  const int tn = (bid % per_group) / gsz;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const int b1 = blockIdx.y / p.nb2, b2 = blockIdx.y % p.nb2;
+  const bf16_t* A = p.A + b1 * p.a_s1 + b2 * p.a_s2;
+  const bf16_t* B = p.B + b1 * p.b_s1 + b2 * p.b_s2;
+
+  f32x4_t acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  uint4 ra[4], rb[4];
+  const int nk = (p.K + BK - 1) / BK;
+  load_tile<A_T>(ra, A, p.lda, m0, p.M, 0, p.K, tid);
+  load_tile<B_T>(rb, B, p.ldb, n0, p.N, 0, p.K, tid);
+  store_tile<A_T>(smem, ra, tid);
+  store_tile<B_T>(smem + TILE_BYTES, rb, tid);
+  __syncthreads();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int s = kt & 1;
+    const bool more = kt + 1 < nk;
+    if (more) {
+      load_tile<A_T>(ra, A, p.lda, m0, p.M, (kt + 1) * BK, p.K, tid);
+      load_tile<B_T>(rb, B, p.ldb, n0, p.N, (kt + 1) * BK, p.K, tid);
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8_t af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = read_frag<A_T>(smem + s * 2 * TILE_BYTES, wm * 64 + i * 16, kk, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = read_frag<B_T>(smem + s * 2 * TILE_BYTES + TILE_BYTES, wn * 64 + j * 16, kk, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+    }
+    if (more) {
+      store_tile<A_T>(smem + (s ^ 1) * 2 * TILE_BYTES, ra, tid);
+      store_tile<B_T>(smem + (s ^ 1) * 2 * TILE_BYTES + TILE_BYTES, rb, tid);
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue: lane holds C[m][n..n+3] for each (i, j) tile -----------------------------------------------------
+  const long long coff = b1 * p.c_s1 + b2 * p.c_s2;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + wm * 64 + i * 16 + (lane & 15);
+    if (m >= p.M) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
+      if (n >= p.N) continue;
+      const long long idx = coff + (long long)m * p.ldc + n;
+      float v[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) v[t] = p.alpha * acc[i][j][t];
+      if (OUT_F32) {
+        float* C = reinterpret_cast<float*>(p.C) + idx;
+        if (p.beta != 0.f) {
+          float4 o = *reinterpret_cast<const float4*>(C);
+          v[0] += p.beta * o.x; v[1] += p.beta * o.y; v[2] += p.beta * o.z; v[3] += p.beta * o.w;
+        }
+        if (p.R) {
+          float4 r = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(p.R) + idx);
+          v[0] += r.x; v[1] += r.y; v[2] += r.z; v[3] += r.w;
+        }
+        if (p.act) {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) v[t] = act_fwd(p.act, v[t]);
+        }
+        *reinterpret_cast<float4*>(C) = make_float4(v[0], v[1], v[2], v[3]);
+      } else {
+        if (p.mode == 1) {
+          if (p.R) {
+            uint2 r = *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16_t*>(p.R) + idx);
+            v[0] += bf2f(r.x & 0xffff); v[1] += bf2f(r.x >> 16); v[2] += bf2f(r.y & 0xffff); v[3] += bf2f(r.y >> 16);
+          }
+          uint2 z = *reinterpret_cast<const uint2*>(p.Zin + idx);
+          v[0] *= act_grad(p.act, bf2f(z.x & 0xffff)); v[1] *= act_grad(p.act, bf2f(z.x >> 16));
+          v[2] *= act_grad(p.act, bf2f(z.y & 0xffff)); v[3] *= act_grad(p.act, bf2f(z.y >> 16));
+        } else {
+          if (p.R) {
+            uint2 r = *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16_t*>(p.R) + idx);
+            v[0] += bf2f(r.x & 0xffff); v[1] += bf2f(r.x >> 16); v[2] += bf2f(r.y & 0xffff); v[3] += bf2f(r.y >> 16);
+          }
+          if (p.Zout) {
+            *reinterpret_cast<uint2*>(p.Zout + idx) = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+          }
+          if (p.act) {
+#pragma unroll
+            for (int t = 0; t < 4; ++t) v[t] = act_fwd(p.act, v[t]);
+          }
+        }
+        *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.C) + idx) =
+            make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+      }
+    }
+  }
+}
+
+template <int A_T, int B_T, bool F32>
+hipError_t launch(const GemmArgs& a, int batch, hipStream_t stream) {
+  dim3 grid(a.tiles_m * a.tiles_n, batch);
+  const size_t lds = 4 * TILE_BYTES;
+  auto k = gemm_bf16_kernel<A_T, B_T, F32>;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr = true;
+  }
+  hipLaunchKernelGGL(k, grid, dim3(NT), lds, stream, a);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+struct ObstGemmDesc {
+  const void* A; const void* B; void* C; const void* R; void* Zout; const void* Zin;
+  long long lda, ldb, ldc;
+  long long a_s1, a_s2, b_s1, b_s2, c_s1, c_s2;
+  int M, N, K, batch1, batch2;
+  int a_t, b_t, out_f32, act, mode;
+  float alpha, beta;
+};
+
+// Returns 0 on success, <0 on a host-side shape/alignment violation, >0 for a HIP error.
+OBST_API int obst_gemm(const ObstGemmDesc* d, hipStream_t stream) {
+  if (d->M <= 0 || d->N <= 0 || d->K <= 0 || d->batch1 <= 0 || d->batch2 <= 0) return -1;
+  // 16-byte staging loads: the contiguous extent and every leading dimension must be multiples of 8 elements.
+  if (d->K % 8 || d->N % 8) return -2;
+  if (d->a_t == 1 && d->M % 8) return -3;
+  if (d->lda % 8 || d->ldb % 8 || d->ldc % 8) return -4;
+  if (((uintptr_t)d->A | (uintptr_t)d->B) & 15) return -5;
+  if (((uintptr_t)d->C) & 15) return -6;
+  GemmArgs a;
+  a.A = (const bf16_t*)d->A; a.B = (const bf16_t*)d->B; a.C = d->C; a.R = d->R;
+  a.Zout = (bf16_t*)d->Zout; a.Zin = (const bf16_t*)d->Zin;
+  a.lda = d->lda; a.ldb = d->ldb; a.ldc = d->ldc;
+  a.a_s1 = d->a_s1; a.a_s2 = d->a_s2; a.b_s1 = d->b_s1; a.b_s2 = d->b_s2; a.c_s1 = d->c_s1; a.c_s2 = d->c_s2;
+  a.M = d->M; a.N = d->N; a.K = d->K; a.nb2 = d->batch2;
+  a.tiles_m = (d->M + BM - 1) / BM; a.tiles_n = (d->N + BN - 1) / BN;
+  a.alpha = d->alpha; a.beta = d->beta; a.act = d->act; a.mode = d->mode;
+  const int batch = d->batch1 * d->batch2;
+  hipError_t e;
+#define OBST_GEMM_CASE(AT, BT, F)                                   \
+  if (d->a_t == AT && d->b_t == BT && (d->out_f32 != 0) == F) {    \
+    e = launch<AT, BT, F>(a, batch, stream);                         \
+    return e == hipSuccess ? 0 : (int)e;                             \
+  }
+  OBST_GEMM_CASE(0, 0, false) OBST_GEMM_CASE(0, 1, false) OBST_GEMM_CASE(1, 0, false) OBST_GEMM_CASE(1, 1, false)
+  OBST_GEMM_CASE(0, 0, true) OBST_GEMM_CASE(0, 1, true) OBST_GEMM_CASE(1, 0, true) OBST_GEMM_CASE(1, 1, true)
+#undef OBST_GEMM_CASE
+  return -7;
+}

@@ -1,0 +1,239 @@
+// K05: the reference `norm` layer (src/model/normalization.py:22-34):
+//   x -= mean(x);  x *= rsqrt(mean(x^2) + 1e-5);  x *= scale;  x += shift
+// statistics over the trailing F elements of each row (F = features, or features_per_head for `group`, where
+// rows are (token, head) pairs and the [heads, F] scale/shift is indexed by row % groups).
+// One wave per row, the row held in registers (16-byte bf16 vector loads, Guideline 13), two-pass statistics,
+// fp32 math. Backward: dx = rstd * (dxh - mean(dxh) - xh * mean(dxh * xh)); scale/shift gradients are summed per
+// block in registers and added to the fp32 gradient buffer with one atomic per element per block.
+// A split "row statistics" path (partial sums -> all-reduce over the TP group -> apply) serves the non-group
+// norm when `heads` is split across ranks (collective X05).
+#include "common.h"
+
+namespace {
+
+constexpr int NTH = 256;
+
+template <int NCH>  // 512-element chunks per row
+__device__ __forceinline__ void load_row(const bf16_t* x, int F, int lane, float (&v)[NCH][8]) {
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = c * 512 + lane * 8;
+    if (col < F) {
+      uint4 u = *reinterpret_cast<const uint4*>(x + col);
+      const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { v[c][2 * j] = bf2f(w[j] & 0xffff); v[c][2 * j + 1] = bf2f(w[j] >> 16); }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[c][j] = 0.f;
+    }
+  }
+}
+
+template <int NCH>
+__global__ __launch_bounds__(NTH) void norm_fwd_kernel(const bf16_t* __restrict__ X, const float* __restrict__ scale,
+                                                       const float* __restrict__ shift, bf16_t* __restrict__ Y,
+                                                       float* __restrict__ rstd_out, long long rows, int F,
+                                                       int groups, float eps, const float* __restrict__ ext_stats) {
+  const int lane = threadIdx.x & 63;
+  const long long nw = (long long)gridDim.x * 4;
+  for (long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6); row < rows; row += nw) {
+    float v[NCH][8];
+    load_row<NCH>(X + row * F, F, lane, v);
+    float mean, rstd;
+    if (ext_stats) {  // [rows, 2] = (mean, rstd) computed over the full (TP-gathered) feature set
+      mean = ext_stats[2 * row];
+      rstd = ext_stats[2 * row + 1];
+    } else {
+      float s = 0.f;
+#pragma unroll
+      for (int c = 0; c < NCH; ++c)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s += v[c][j];
+      mean = wave_sum(s) / F;
+      float q = 0.f;
+#pragma unroll
+      for (int c = 0; c < NCH; ++c)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int col = c * 512 + lane * 8 + j;
+          const float d = col < F ? v[c][j] - mean : 0.f;
+          q += d * d;
+        }
+      rstd = rsqrtf(wave_sum(q) / F + eps);
+    }
+    if (rstd_out && lane == 0) { rstd_out[2 * row] = mean; rstd_out[2 * row + 1] = rstd; }
+    const long long poff = (long long)(row % groups) * F;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = c * 512 + lane * 8;
+      if (col >= F) continue;
+      uint32_t o[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float y0 = (v[c][2 * j] - mean) * rstd, y1 = (v[c][2 * j + 1] - mean) * rstd;
+        if (scale) { y0 *= scale[poff + col + 2 * j]; y1 *= scale[poff + col + 2 * j + 1]; }
+        if (shift) { y0 += shift[poff + col + 2 * j]; y1 += shift[poff + col + 2 * j + 1]; }
+        o[j] = pack_bf16x2(y0, y1);
+      }
+      *reinterpret_cast<uint4*>(Y + row * F + col) = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+  }
+}
+
+// row partial sums for the TP path: out[row] = (sum x, sum x^2) over this rank's slice
+__global__ __launch_bounds__(NTH) void norm_partial_kernel(const bf16_t* __restrict__ X, float* __restrict__ out,
+                                                           long long rows, int F) {
+  const int lane = threadIdx.x & 63;
+  const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  float s = 0.f, q = 0.f;
+  for (int col = lane * 2; col < F; col += 128) {
+    uint32_t u = *reinterpret_cast<const uint32_t*>(X + row * F + col);
+    const float a = bf2f(u & 0xffff), b = bf2f(u >> 16);
+    s += a + b;
+    q += a * a + b * b;
+  }
+  s = wave_sum(s);
+  q = wave_sum(q);
+  if (lane == 0) { out[2 * row] = s; out[2 * row + 1] = q; }
+}
+
+// backward. stats = (mean, rstd) per row. If `partial_out` is set, only writes per-row partial
+// (sum dxh, sum dxh*xh) for the TP all-reduce and returns (phase 1); with `ext_dsum` (phase 2) uses them.
+template <int NCH>
+__global__ __launch_bounds__(NTH) void norm_bwd_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ DY,
+                                                       const float* __restrict__ scale, const float* __restrict__ stats,
+                                                       bf16_t* __restrict__ DX, float* __restrict__ dscale,
+                                                       float* __restrict__ dshift, long long rows, int F, int groups,
+                                                       int Ffull, float* __restrict__ partial_out,
+                                                       const float* __restrict__ ext_dsum) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* red_s = reinterpret_cast<float*>(smem);           // [4 waves][F] dscale partials, then dshift
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const bool want_param = (dscale || dshift) && partial_out == nullptr;
+  // per-lane parameter-gradient accumulators (only valid when groups == 1; grouped norms use atomics per row)
+  float gs[NCH][8], gb[NCH][8];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) gs[c][j] = gb[c][j] = 0.f;
+  const long long nw = (long long)gridDim.x * 4;
+  for (long long row = (long long)blockIdx.x * 4 + w; row < rows; row += nw) {
+    float x[NCH][8], dy[NCH][8];
+    load_row<NCH>(X + row * F, F, lane, x);
+    load_row<NCH>(DY + row * F, F, lane, dy);
+    const float mean = stats[2 * row], rstd = stats[2 * row + 1];
+    const long long poff = (long long)(row % groups) * F;
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int col = c * 512 + lane * 8 + j;
+        if (col < F) {
+          const float xh = (x[c][j] - mean) * rstd;
+          const float g = scale ? scale[poff + col] : 1.f;
+          const float dxh = dy[c][j] * g;
+          s1 += dxh;
+          s2 += dxh * xh;
+          if (want_param) {
+            if (groups == 1) { gs[c][j] += dy[c][j] * xh; gb[c][j] += dy[c][j]; }
+            else {
+              if (dscale) atomicAdd(dscale + poff + col, dy[c][j] * xh);
+              if (dshift) atomicAdd(dshift + poff + col, dy[c][j]);
+            }
+          }
+          x[c][j] = xh;
+          dy[c][j] = dxh;
+        }
+      }
+    s1 = wave_sum(s1);
+    s2 = wave_sum(s2);
+    if (partial_out) {
+      if (lane == 0) { partial_out[2 * row] = s1; partial_out[2 * row + 1] = s2; }
+      continue;
+    }
+    if (ext_dsum) { s1 = ext_dsum[2 * row]; s2 = ext_dsum[2 * row + 1]; }
+    const float m1 = s1 / Ffull, m2 = s2 / Ffull;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = c * 512 + lane * 8;
+      if (col >= F) continue;
+      uint32_t o[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        o[j] = pack_bf16x2(rstd * (dy[c][2 * j] - m1 - x[c][2 * j] * m2),
+                           rstd * (dy[c][2 * j + 1] - m1 - x[c][2 * j + 1] * m2));
+      *reinterpret_cast<uint4*>(DX + row * F + col) = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+  }
+  if (want_param && groups == 1) {
+    // reduce the 4 waves through LDS, then one atomic per element per block
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int col = c * 512 + lane * 8 + j;
+        if (col < F) { red_s[w * F + col] = gs[c][j]; red_s[(4 + w) * F + col] = gb[c][j]; }
+      }
+    __syncthreads();
+    for (int col = threadIdx.x; col < F; col += NTH) {
+      const float a = red_s[col] + red_s[F + col] + red_s[2 * F + col] + red_s[3 * F + col];
+      const float b = red_s[4 * F + col] + red_s[5 * F + col] + red_s[6 * F + col] + red_s[7 * F + col];
+      if (dscale) atomicAdd(dscale + col, a);
+      if (dshift) atomicAdd(dshift + col, b);
+    }
+  }
+}
+
+int grid_for(long long rows) {
+  long long g = (rows + 3) / 4;
+  return (int)(g < 2048 ? g : 2048);
+}
+
+}  // namespace
+
+struct ObstNormDesc {
+  const void* X; const float* scale; const float* shift; void* Y; float* stats;
+  const void* DY; void* DX; float* dscale; float* dshift;
+  float* partial; const float* ext;   // TP path
+  long long rows; int F; int groups; int Ffull; float eps;
+};
+
+#define NORM_DISPATCH(KERNEL, GRID, LDSB, ...)                                                      \
+  do {                                                                                              \
+    const int nch = (d->F + 511) / 512;                                                             \
+    if (nch <= 1) hipLaunchKernelGGL(KERNEL<1>, GRID, dim3(NTH), LDSB, st, __VA_ARGS__);            \
+    else if (nch <= 2) hipLaunchKernelGGL(KERNEL<2>, GRID, dim3(NTH), LDSB, st, __VA_ARGS__);       \
+    else if (nch <= 4) hipLaunchKernelGGL(KERNEL<4>, GRID, dim3(NTH), LDSB, st, __VA_ARGS__);       \
+    else if (nch <= 8) hipLaunchKernelGGL(KERNEL<8>, GRID, dim3(NTH), LDSB, st, __VA_ARGS__);       \
+    else if (nch <= 16) hipLaunchKernelGGL(KERNEL<16>, GRID, dim3(NTH), LDSB, st, __VA_ARGS__);     \
+    else return -2;                                                                                 \
+  } while (0)
+
+OBST_API int obst_norm_fwd(const ObstNormDesc* d, hipStream_t st) {
+  if (d->F % 8 || d->rows <= 0) return -1;
+  NORM_DISPATCH(norm_fwd_kernel, dim3(grid_for(d->rows)), 0, (const bf16_t*)d->X, d->scale, d->shift, (bf16_t*)d->Y,
+                d->stats, d->rows, d->F, d->groups, d->eps, d->ext);
+  return (int)hipGetLastError();
+}
+
+OBST_API int obst_norm_partial(const ObstNormDesc* d, hipStream_t st) {
+  if (d->F % 2 || d->rows <= 0) return -1;
+  hipLaunchKernelGGL(norm_partial_kernel, dim3((unsigned)((d->rows + 3) / 4)), dim3(NTH), 0, st, (const bf16_t*)d->X,
+                     d->partial, d->rows, d->F);
+  return (int)hipGetLastError();
+}
+
+OBST_API int obst_norm_bwd(const ObstNormDesc* d, hipStream_t st) {
+  if (d->F % 8 || d->rows <= 0) return -1;
+  const size_t lds = (d->groups == 1 && (d->dscale || d->dshift) && !d->partial) ? (size_t)8 * d->F * 4 : 0;
+  if (lds > 160 * 1024) return -3;
+  // more rows per block amortises the parameter-gradient atomics
+  long long g = (d->rows + 31) / 32;
+  const int grid = (int)(g < 1024 ? (g < 1 ? 1 : g) : 1024);
+  NORM_DISPATCH(norm_bwd_kernel, dim3(grid), lds, (const bf16_t*)d->X, (const bf16_t*)d->DY, d->scale, d->stats,
+                (bf16_t*)d->DX, d->dscale, d->dshift, d->rows, d->F, d->groups, d->Ffull, d->partial, d->ext);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,58 @@
+"""Block grammar: ``{"layer": ["name-extra-extra", ...], "skip": bool}`` (ref src/model/frontend.py:21-55).
+
+Layers run sequentially inside the block's scope; ``skip`` adds the block input back for the ``none`` and
+``checkpoint`` memory strategies. When the last layer has a fused fast path (feed_forward / dot-product attention)
+the residual add is folded into its final GEMM / attention epilogue instead of a separate elementwise pass.
+"""
+from __future__ import annotations
+
+import typing
+
+from ..config import BlockConfig
+from ..ops import functional as F
+from .context import Act, BlockArgs, Builder
+from .layers import LAYER_FUNCTIONS
+
+_FUSABLE_LAST = ("feed_forward", "attention")
+
+
+def run_layers(builder: Builder, layers: typing.List[str], x: Act, residual: typing.Optional[Act] = None
+               ) -> typing.Tuple[Act, bool]:
+    out = x
+    consumed = False
+    seen: typing.Dict[str, int] = {}
+    n = len(layers)
+    for idx, layer in enumerate(layers, 1):
+        name, *extras = layer.split('-')
+        if name not in LAYER_FUNCTIONS:
+            raise ValueError(f"unknown layer {name!r}; known: {sorted(LAYER_FUNCTIONS)}")
+        args = BlockArgs(builder, out, extras, idx == n)
+        args.fn_name = name
+        args.fn_occurrence = seen.get(name, 0)
+        seen[name] = args.fn_occurrence + 1
+        if idx == n and residual is not None and name in _FUSABLE_LAST:
+            args.residual = residual
+        with builder.scope(name + '_'):
+            out = LAYER_FUNCTIONS[name](args)
+        consumed = consumed or getattr(args, "residual_consumed", False)
+    return out, consumed
+
+
+def block_body(builder: Builder, config: BlockConfig, x: Act) -> Act:
+    """the block's layers (+ skip), run inside an already-entered block scope"""
+    skip = config.skip and config.memory_reduction_strategy in ("none", "checkpoint")
+    out, consumed = run_layers(builder, list(config.layer), x, residual=x if skip else None)
+    if skip and not consumed:
+        out = Act(F.add(out.t, x.t), out.dims)
+    return out
+
+
+def block_scope_name(depth: int, config_idx: int, prefix: str = "") -> str:
+    return f"{prefix}{depth}_{config_idx}"
+
+
+def block_part_fn(builder: Builder, config: BlockConfig, x: Act, depth: int, config_idx: int,
+                  prefix: str = "") -> Act:
+    builder.depth_idx, builder.config_idx = depth, config_idx
+    with builder.scope.exact(block_scope_name(depth, config_idx, prefix)):
+        return block_body(builder, config, x)

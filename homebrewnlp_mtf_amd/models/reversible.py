@@ -1,0 +1,137 @@
+"""Memory-reduction strategies of the body: ``revnet``, ``momentum``, ``checkpoint`` and ``none``
+(ref src/model/__init__.py:94-130, src/model/revnet.py:14-120, src/model/momentumnet.py:14-125).
+
+RevNet (reversible residual): state (x1, x2) -> (x2, x1 + F(x2)); the body returns x1 + x2. The whole depth stack
+is ONE autograd node: forward keeps no activations, backward walks the blocks in reverse, reconstructs
+x1 = y2 - F(x2), re-runs F(x2) with grad enabled and back-propagates through it (weight gradients land in the flat
+fp32 buffer via the ops' fused wgrad epilogues). Activation memory is O(1) in depth, as in the reference.
+
+MomentumNet: v' = a v + (1-a) F(x); x' = x + v'; inverse v = (v' - (1-a) F(x)) / a, x = x' - v'.
+
+Each block is re-entered in backward under the exact scope it ran in (``Scope.restore``) so it fetches the same
+variables by name (incl. ``shared`` cross-depth reuse).
+"""
+from __future__ import annotations
+
+import typing
+
+import torch
+
+from ..ops import raw
+from .context import Act, Builder
+from .frontend import block_body, block_scope_name
+
+
+class Block:
+    def __init__(self, builder: Builder, config, depth: int, config_idx: int, stack: typing.List[str], dims):
+        self.builder, self.config, self.depth, self.config_idx = builder, config, depth, config_idx
+        self.stack = stack + [block_scope_name(depth, config_idx)]
+        self.dims = dims
+
+    def __call__(self, x: torch.Tensor) -> torch.Tensor:
+        b = self.builder
+        b.depth_idx, b.config_idx = self.depth, self.config_idx
+        with b.scope.restore(self.stack):
+            return block_body(b, self.config, Act(x, self.dims)).t
+
+
+def _axpby(x, z, alpha, beta):
+    y = torch.empty_like(x)
+    raw.elementwise("axpby", x.contiguous(), y, z=z.contiguous(), alpha=alpha, beta=beta)
+    return y
+
+
+class _RevStack(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x1, x2, blocks: typing.List[Block], mode: str, alpha: float):
+        with torch.no_grad():
+            for f in blocks:
+                if mode == "revnet":
+                    x1, x2 = x2, _axpby(x1, f(x2), 1.0, 1.0)
+                else:  # momentum: (x, v) -> (x + v', v'), v' = a v + (1-a) F(x)
+                    v = _axpby(x2, f(x1), alpha, 1.0 - alpha)
+                    x1, x2 = _axpby(x1, v, 1.0, 1.0), v
+        ctx.blocks, ctx.mode, ctx.alpha = blocks, mode, alpha
+        ctx.save_for_backward(x1, x2)
+        return x1, x2
+
+    @staticmethod
+    def backward(ctx, g1, g2):
+        y1, y2 = ctx.saved_tensors
+        mode, alpha = ctx.mode, ctx.alpha
+        g1 = torch.zeros_like(y1) if g1 is None else g1.contiguous()
+        g2 = torch.zeros_like(y2) if g2 is None else g2.contiguous()
+        for f in reversed(ctx.blocks):
+            if mode == "revnet":
+                # y1 = x2, y2 = x1 + F(x2)
+                with torch.enable_grad():
+                    x2 = y1.detach().requires_grad_(True)
+                    fx = f(x2)
+                torch.autograd.backward(fx, g2)
+                x1 = _axpby(y2, fx.detach(), 1.0, -1.0)
+                dx2 = g1 if x2.grad is None else _axpby(g1, x2.grad, 1.0, 1.0)
+                y1, y2, g1, g2 = x1, x2.detach(), g2, dx2
+            else:
+                # y1 = x + v', y2 = v' ; v' = a v + (1-a) F(x)
+                x = _axpby(y1, y2, 1.0, -1.0)
+                gv_tot = _axpby(g2, g1, 1.0, 1.0)
+                with torch.enable_grad():
+                    xr = x.detach().requires_grad_(True)
+                    fx = f(xr)
+                torch.autograd.backward(fx, gv_tot * (1.0 - alpha))
+                v = _axpby(y2, fx.detach(), 1.0 / alpha, -(1.0 - alpha) / alpha)
+                gx = g1 if xr.grad is None else _axpby(g1, xr.grad, 1.0, 1.0)
+                gv = gv_tot * alpha
+                y1, y2, g1, g2 = x, v, gx, gv
+        return g1, g2, None, None, None
+
+
+class _Checkpoint(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, f: Block):
+        with torch.no_grad():
+            y = f(x)
+        ctx.f = f
+        ctx.save_for_backward(x)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        with torch.enable_grad():
+            xr = x.detach().requires_grad_(True)
+            y = ctx.f(xr)
+        torch.autograd.backward(y, dy)
+        return xr.grad, None
+
+
+def run_body(builder: Builder, src: Act, strategy: str, configs, depth: int) -> Act:
+    stack = builder.scope.snapshot()
+    dims = src.dims
+    blocks = [Block(builder, cfg, i, c, stack, dims) for i in range(depth) for c, cfg in enumerate(configs)]
+    if builder.register or not torch.is_grad_enabled() or not src.t.requires_grad:
+        # registration / inference: plain forward through the same blocks
+        if strategy in ("revnet", "momentum"):
+            x1, x2 = src.t, src.t
+            for f in blocks:
+                if strategy == "revnet":
+                    x1, x2 = x2, _axpby(x1, f(x2), 1.0, 1.0)
+                else:
+                    a = builder.params.momentumnet_alpha
+                    v = _axpby(x2, f(x1), a, 1.0 - a)
+                    x1, x2 = _axpby(x1, v, 1.0, 1.0), v
+            return Act(_axpby(x1, x2, 1.0, 1.0), dims)
+        x = src.t
+        for f in blocks:
+            x = f(x)
+        return Act(x, dims)
+    if strategy in ("revnet", "momentum"):
+        y1, y2 = _RevStack.apply(src.t, src.t, blocks, strategy, builder.params.momentumnet_alpha)
+        return Act(y1 + y2, dims)
+    x = src.t
+    for f in blocks:
+        if strategy == "checkpoint":
+            x = _Checkpoint.apply(x, f)
+        else:
+            x = f(x)
+    return Act(x, dims)

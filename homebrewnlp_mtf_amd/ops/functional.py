@@ -1,0 +1,586 @@
+"""Autograd ops of the model, written once against ``ops.raw`` (HIP on GPU, torch oracle on CPU).
+
+Weight gradients never go through autograd: every op adds its fp32 weight gradient straight into the flat gradient
+buffer (``weight.main_grad``, see ``models/variables.py``) with a beta=1 GEMM epilogue and returns ``None`` -- this
+is the MI355X-native replacement of the reference's per-variable gradient einsums (src/optimizer/__init__.py:128-174)
+and lets the DP all-reduce start on contiguous buckets while backward is still running.
+
+TP collectives are issued where the reference's ``heads`` layout implies them:
+  * linear contracting ``heads`` (row-parallel, X01/X03/X04): all-reduce the output in forward;
+  * linear creating ``heads`` from replicated input (column-parallel, X02): all-reduce dX in backward;
+  * non-group norm (X05): all-reduce row statistics in forward and backward.
+"""
+from __future__ import annotations
+
+import functools
+import math
+import typing
+
+import torch
+
+from . import raw
+from ..config import Dim
+from ..parallel import state as pstate
+
+DimList = typing.List[Dim]
+
+
+def _empty(shape, like: torch.Tensor, dtype=None):
+    return torch.empty(shape, dtype=dtype or like.dtype, device=like.device)
+
+
+GRAD_HOOK: typing.Optional[typing.Callable[[torch.Tensor], None]] = None   # set by parallel.grad_sync
+
+
+def _acc_grad(w: torch.Tensor) -> typing.Tuple[torch.Tensor, bool]:
+    """(fp32 buffer to accumulate the weight gradient into, whether it is the flat main_grad)"""
+    mg = getattr(w, "main_grad", None)
+    if mg is not None:
+        return mg, True
+    return torch.zeros(w.shape, dtype=torch.float32, device=w.device), False
+
+
+def _param32(t: typing.Optional[torch.Tensor]) -> typing.Optional[torch.Tensor]:
+    """small parameters (norm scale/shift, rezero gate) are read from the fp32 master copy; fp64 (gradient-check)
+    computations use the tensor itself"""
+    if t is None or t.dtype == torch.float64:
+        return t
+    m = getattr(t, "master", t)
+    return m if m.dtype == torch.float32 else m.float()
+
+
+def _done(w: torch.Tensor):
+    """a weight-gradient contribution has been accumulated (DP bucket bookkeeping)"""
+    if GRAD_HOOK is not None:
+        GRAD_HOOK(w)
+
+
+# ================================================================================================================
+# named linear  y[P, S, N] = sum_C x[P, S, C] * w[S, C, N]   (S = shared/batch dims, e.g. heads of `group`)
+class LinearPlan:
+    def __init__(self, xdims: DimList, wdims: DimList, odims: DimList, head_name: str = "heads"):
+        xs, ws, os_ = list(xdims), list(wdims), list(odims)
+        self.S = [d for d in ws if d in xs and d in os_]
+        self.C = [d for d in ws if d in xs and d not in os_]
+        self.Nn = [d for d in ws if d not in xs]
+        self.P = [d for d in xs if d not in ws]
+        if ws != self.S + self.C + self.Nn:
+            raise NotImplementedError(f"weight dims {ws} not in [shared, contracted, new] order")
+        canon_x = self.P + self.S + self.C
+        canon_o = self.P + self.S + self.Nn
+        if sorted(os_) != sorted(canon_o):
+            raise ValueError(f"output dims {os_} inconsistent with x {xs} / w {ws}")
+        self.x_perm = None if xs == canon_x else [xs.index(d) for d in canon_x]
+        self.o_perm = None if os_ == canon_o else [canon_o.index(d) for d in os_]
+        self.canon_o_shape = [d.size for d in canon_o]
+        self.out_shape = [d.size for d in os_]
+        prod = lambda ds: int(math.prod(d.size for d in ds))  # noqa: E731
+        self.M, self.H, self.K, self.N = prod(self.P), prod(self.S), prod(self.C), prod(self.Nn)
+        # TP roles (heads axis split over ranks)
+        names_c = [d.name for d in self.C]
+        names_n = [d.name for d in self.Nn]
+        self.row_parallel = head_name in names_c          # contracts heads -> partial sums
+        self.col_parallel = head_name in names_n          # creates heads from replicated input
+
+
+@functools.lru_cache(maxsize=4096)
+def linear_plan(xdims: tuple, wdims: tuple, odims: tuple) -> LinearPlan:
+    return LinearPlan(list(xdims), list(wdims), list(odims))
+
+
+def _fwd_gemm(x2, w, y2, plan: LinearPlan, act=None, R=None, Zout=None):
+    M, H, K, N = plan.M, plan.H, plan.K, plan.N
+    raw.gemm(raw.Operand(x2, 0, H * K, K), raw.Operand(w, 1, N, K * N), raw.Operand(y2, 0, H * N, N),
+             M, N, K, batch=(H, 1), act=act, R=R, Zout=Zout)
+
+
+def _dgrad_gemm(dy2, w, dx2, plan: LinearPlan, act=None, Zin=None, R=None):
+    M, H, K, N = plan.M, plan.H, plan.K, plan.N
+    raw.gemm(raw.Operand(dy2, 0, H * N, N), raw.Operand(w, 0, N, K * N), raw.Operand(dx2, 0, H * K, K),
+             M, K, N, batch=(H, 1), act=act, act_bwd=Zin is not None, Zin=Zin, R=R)
+
+
+def _wgrad_gemm(x2, dy2, gw, plan: LinearPlan):
+    M, H, K, N = plan.M, plan.H, plan.K, plan.N
+    raw.gemm(raw.Operand(x2, 1, H * K, K), raw.Operand(dy2, 1, H * N, N), raw.Operand(gw, 0, N, K * N),
+             K, N, M, batch=(H, 1), beta=1.0)
+
+
+class _Linear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, plan: LinearPlan, act):
+        xc = x.permute(plan.x_perm).contiguous() if plan.x_perm is not None else x.contiguous()
+        y = _empty(plan.canon_o_shape, xc)
+        z = _empty(plan.canon_o_shape, xc) if act else None
+        _fwd_gemm(xc, w, y, plan, act=act, Zout=z)
+        if plan.row_parallel and pstate.tp_size() > 1:
+            if act:
+                raise NotImplementedError("activation fused into a heads-contracting linear under TP")
+            pstate.tp_all_reduce(y)
+        ctx.save_for_backward(xc, w, z)
+        ctx.plan, ctx.act = plan, act
+        if plan.o_perm is not None:
+            y = y.permute(plan.o_perm)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xc, w, z = ctx.saved_tensors
+        plan, act = ctx.plan, ctx.act
+        if plan.o_perm is not None:
+            inv = [plan.o_perm.index(i) for i in range(len(plan.o_perm))]
+            dy = dy.permute(inv)
+        dy = dy.contiguous()
+        if act:
+            dz = torch.empty_like(dy)
+            raw.elementwise("act_bwd", z, dz, z=dy, act=act)
+            dy = dz
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = _empty(xc.shape, xc)
+            _dgrad_gemm(dy, w, dx, plan)
+            if plan.col_parallel and pstate.tp_size() > 1:
+                pstate.tp_all_reduce(dx)
+            if plan.x_perm is not None:
+                inv = [plan.x_perm.index(i) for i in range(len(plan.x_perm))]
+                dx = dx.permute(inv)
+        gw, is_main = _acc_grad(w)
+        _wgrad_gemm(xc, dy, gw, plan)
+        _done(w)
+        return dx, (None if is_main else gw.to(w.dtype)), None, None
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, xdims: DimList, wdims: DimList, odims: DimList,
+           act: typing.Optional[str] = None) -> torch.Tensor:
+    plan = linear_plan(tuple(xdims), tuple(wdims), tuple(odims))
+    return _Linear.apply(x, w, plan, act)
+
+
+class _TPReduce(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        return pstate.tp_all_reduce(x.contiguous().clone())
+
+    @staticmethod
+    def backward(ctx, dy):
+        return dy
+
+
+class _TPCopy(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        return x
+
+    @staticmethod
+    def backward(ctx, dy):
+        return pstate.tp_all_reduce(dy.contiguous().clone())
+
+
+def tp_reduce(x):
+    """all-reduce over the TP group in forward, identity in backward (row-parallel output)"""
+    return _TPReduce.apply(x) if pstate.tp_size() > 1 else x
+
+
+def tp_copy(x):
+    """identity in forward, all-reduce of the gradient in backward (column-parallel input)"""
+    return _TPCopy.apply(x) if pstate.tp_size() > 1 else x
+
+
+# ================================================================================================================
+# fused feed-forward: y = act(x W1) W2 (+ residual)   -- K01 x4 with fused epilogues, no separate elementwise pass
+class _FFN(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w1, w2, p1: LinearPlan, p2: LinearPlan, act, residual):
+        xc = x.contiguous()
+        z = _empty(p1.canon_o_shape, xc)
+        a = _empty(p1.canon_o_shape, xc) if act else z
+        _fwd_gemm(xc, w1, a, p1, act=act, Zout=z if act else None)
+        if p1.row_parallel and pstate.tp_size() > 1:
+            raise NotImplementedError
+        y = _empty(p2.canon_o_shape, xc)
+        _fwd_gemm(a, w2, y, p2, R=residual.contiguous() if residual is not None else None)
+        ctx.save_for_backward(xc, w1, w2, z, a if act else None)
+        ctx.p1, ctx.p2, ctx.act, ctx.has_res = p1, p2, act, residual is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xc, w1, w2, z, a = ctx.saved_tensors
+        p1, p2, act = ctx.p1, ctx.p2, ctx.act
+        a = z if a is None else a
+        dy = dy.contiguous()
+        # dZ = (dY W2^T) * act'(Z) in ONE gemm epilogue
+        dz = _empty(p1.canon_o_shape, dy)
+        _dgrad_gemm(dy, w2, dz, p2, act=act, Zin=z if act else None)
+        g2, m2 = _acc_grad(w2)
+        _wgrad_gemm(a, dy, g2, p2)
+        _done(w2)
+        dx = _empty(xc.shape, xc)
+        _dgrad_gemm(dz, w1, dx, p1)
+        g1, m1 = _acc_grad(w1)
+        _wgrad_gemm(xc, dz, g1, p1)
+        _done(w1)
+        return (dx, None if m1 else g1.to(w1.dtype), None if m2 else g2.to(w2.dtype), None, None, None,
+                dy if ctx.has_res else None)
+
+
+def ffn(x, w1, w2, xdims, w1dims, mdims, w2dims, odims, act, residual=None):
+    p1 = linear_plan(tuple(xdims), tuple(w1dims), tuple(mdims))
+    p2 = linear_plan(tuple(mdims), tuple(w2dims), tuple(odims))
+    if p1.x_perm is not None or p1.o_perm is not None or p2.x_perm is not None or p2.o_perm is not None:
+        raise NotImplementedError("fused FFN needs canonical layouts")
+    return _FFN.apply(x, w1, w2, p1, p2, act, residual)
+
+
+# ================================================================================================================
+# fused dot-product attention block (reference spatial.py:42-81 with 'dot_product', 'context'/'embedded' keys):
+#   base = act(x W_in);  k, q, v = base W_k, base W_q, base W_v;  out = softmax(q k^T * scale, causal) v (+ residual)
+class _DotAttention(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w_in, w_k, w_q, w_v, p_in: LinearPlan, p_out: LinearPlan, act, scale, causal, residual,
+                geo):
+        B, S, H, D = geo
+        xc = x.contiguous()
+        base = _empty(p_in.canon_o_shape, xc)
+        z = _empty(p_in.canon_o_shape, xc) if act else None
+        _fwd_gemm(xc, w_in, base, p_in, act=act, Zout=z)
+        if p_in.row_parallel and pstate.tp_size() > 1:
+            pstate.tp_all_reduce(base)
+        T = p_out.M
+        Nq = p_out.N
+        # q, k, v in one launch when the three weights are adjacent in the flat buffer
+        kqv = _empty([3] + p_out.canon_o_shape, xc)
+        _qkv_fwd(base, (w_k, w_q, w_v), kqv, p_out)
+        k, q, v = kqv[0], kqv[1], kqv[2]
+        o = _empty(p_out.canon_o_shape, xc)
+        lse = torch.empty(B * H * S, dtype=torch.float32, device=xc.device)
+        ld = H * D
+        raw.attn_fwd(q, k, v, o, lse, B, S, H, D, ld, scale, causal)
+        if residual is not None:
+            out = torch.empty_like(o)
+            raw.elementwise("add", o, out, z=residual.contiguous())
+        else:
+            out = o
+        ctx.save_for_backward(xc, w_in, w_k, w_q, w_v, z, base, kqv, o, lse)
+        ctx.cfg = (p_in, p_out, act, scale, causal, geo, residual is not None, T, Nq)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        xc, w_in, w_k, w_q, w_v, z, base, kqv, o, lse = ctx.saved_tensors
+        p_in, p_out, act, scale, causal, (B, S, H, D), has_res, T, Nq = ctx.cfg
+        dout = dout.contiguous()
+        k, q, v = kqv[0], kqv[1], kqv[2]
+        dkqv = torch.empty_like(kqv)
+        delta = torch.empty(B * H * S, dtype=torch.float32, device=xc.device)
+        raw.attn_bwd(q, k, v, o, dout, lse, delta, dkqv[1], dkqv[0], dkqv[2], B, S, H, D, H * D, scale, causal)
+        # weight grads of k/q/v and dbase = sum_j dj W_j^T (chained through the residual input, last one fuses act')
+        dbase = _empty(p_in.canon_o_shape, xc)
+        ws = (w_k, w_q, w_v)
+        outs = []
+        for j in range(3):
+            last = j == 2
+            _dgrad_gemm(dkqv[j], ws[j], dbase, p_out, act=act if last else None,
+                        Zin=z if (last and act) else None, R=dbase if j > 0 else None)
+            g, m = _acc_grad(ws[j])
+            _wgrad_gemm(base, dkqv[j], g, p_out)
+            _done(ws[j])
+            outs.append(None if m else g.to(ws[j].dtype))
+        if p_out.col_parallel and pstate.tp_size() > 1:
+            if act:
+                raise NotImplementedError("TP + activated attention input")
+            pstate.tp_all_reduce(dbase)
+        dx = _empty(xc.shape, xc)
+        _dgrad_gemm(dbase, w_in, dx, p_in)
+        g, m = _acc_grad(w_in)
+        _wgrad_gemm(xc, dbase, g, p_in)
+        _done(w_in)
+        return (dx, None if m else g.to(w_in.dtype), outs[0], outs[1], outs[2], None, None, None, None, None,
+                dout if has_res else None, None)
+
+
+def _qkv_fwd(base, ws, out, p: LinearPlan):
+    """k, q, v = base @ W_j. One batched launch if the three weights are equally spaced in memory."""
+    M, H, K, N = p.M, p.H, p.K, p.N
+    stride = ws[1].data_ptr() - ws[0].data_ptr()
+    es = ws[0].element_size()
+    same = (H == 1 and stride > 0 and stride % es == 0 and ws[2].data_ptr() - ws[1].data_ptr() == stride
+            and all(w.is_contiguous() for w in ws))
+    if same:
+        raw.gemm(raw.Operand(base, 0, K, 0), raw.Operand(ws[0], 1, N, stride // es), raw.Operand(out, 0, N, M * N),
+                 M, N, K, batch=(3, 1))
+    else:
+        for j in range(3):
+            _fwd_gemm(base, ws[j], out[j], p)
+
+
+def dot_attention(x, w_in, w_k, w_q, w_v, xdims, w_in_dims, base_dims, w_out_dims, act, scale, causal, geo,
+                  residual=None):
+    p_in = linear_plan(tuple(xdims), tuple(w_in_dims), tuple(base_dims))
+    p_out = linear_plan(tuple(base_dims), tuple(w_out_dims), tuple(xdims))
+    return _DotAttention.apply(x, w_in, w_k, w_q, w_v, p_in, p_out, act, scale, causal, residual, geo)
+
+
+# ================================================================================================================
+# general attention core on already-projected q, k, v [B, S, H, D] (used by the composable attention path)
+class _AttnCore(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, v, scale, causal):
+        B, S, H, D = q.shape
+        q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
+        o = torch.empty_like(q)
+        lse = torch.empty(B * H * S, dtype=torch.float32, device=q.device)
+        raw.attn_fwd(q, k, v, o, lse, B, S, H, D, H * D, scale, causal)
+        ctx.save_for_backward(q, k, v, o, lse)
+        ctx.cfg = (scale, causal)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, o, lse = ctx.saved_tensors
+        scale, causal = ctx.cfg
+        B, S, H, D = q.shape
+        dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+        delta = torch.empty(B * H * S, dtype=torch.float32, device=q.device)
+        raw.attn_bwd(q, k, v, o, do.contiguous(), lse, delta, dq, dk, dv, B, S, H, D, H * D, scale, causal)
+        return dq, dk, dv, None, None
+
+
+def attention_core(q, k, v, scale: float, causal: bool):
+    return _AttnCore.apply(q, k, v, scale, causal)
+
+
+# ================================================================================================================
+# norm
+class _Norm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, scale, shift, F, groups, tp_stats):
+        xc = x.contiguous()
+        rows = xc.numel() // F
+        y = torch.empty_like(xc)
+        stats = torch.empty(2 * rows, dtype=torch.float32, device=xc.device)
+        sm32 = _param32(scale)
+        sh32 = _param32(shift)
+        ext = None
+        Ffull = F
+        if tp_stats and pstate.tp_size() > 1:
+            part = torch.empty(2 * rows, dtype=torch.float32, device=xc.device)
+            raw.norm_partial(xc, part, rows, F)
+            pstate.tp_all_reduce(part)
+            Ffull = F * pstate.tp_size()
+            p = part.view(rows, 2)
+            mean = p[:, 0] / Ffull
+            var = (p[:, 1] / Ffull - mean * mean).clamp_min(0)
+            ext = torch.stack([mean, torch.rsqrt(var + raw.EPS)], -1).reshape(-1).contiguous()
+        raw.norm_fwd(xc, sm32, sh32, y, stats, rows, F, groups, ext_stats=ext)
+        ctx.save_for_backward(xc, scale, shift, stats)
+        ctx.cfg = (F, groups, rows, Ffull, tp_stats)
+        ctx.sm32 = sm32
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xc, scale, shift, stats = ctx.saved_tensors
+        F, groups, rows, Ffull, tp_stats = ctx.cfg
+        dy = dy.contiguous()
+        dx = torch.empty_like(xc)
+        gsc, msc = _acc_grad(scale) if scale is not None else (None, True)
+        gsh, msh = _acc_grad(shift) if shift is not None else (None, True)
+        ext = None
+        if tp_stats and pstate.tp_size() > 1:
+            part = torch.empty(2 * rows, dtype=torch.float32, device=xc.device)
+            raw.norm_bwd(xc, dy, ctx.sm32, stats, None, None, None, rows, F, groups, Ffull, partial=part)
+            pstate.tp_all_reduce(part)
+            ext = part
+        raw.norm_bwd(xc, dy, ctx.sm32, stats, dx, gsc, gsh, rows, F, groups, Ffull, ext_dsum=ext)
+        for t in (scale, shift):
+            if t is not None:
+                _done(t)
+        return (dx, None if msc else gsc.view(scale.shape).to(scale.dtype),
+                None if msh else gsh.view(shift.shape).to(shift.dtype), None, None, None)
+
+
+def norm(x, scale, shift, F: int, groups: int, tp_stats: bool = False):
+    return _Norm.apply(x, scale, shift, F, groups, tp_stats)
+
+
+# ================================================================================================================
+# elementwise autograd ops
+class _Act(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, act):
+        xc = x.contiguous()
+        y = torch.empty_like(xc)
+        raw.elementwise("act", xc, y, act=act)
+        ctx.save_for_backward(xc)
+        ctx.act = act
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (xc,) = ctx.saved_tensors
+        dx = torch.empty_like(xc)
+        raw.elementwise("act_bwd", xc, dx, z=dy.contiguous(), act=ctx.act)
+        return dx, None
+
+
+def activation(x, act: typing.Optional[str]):
+    if act in (None, "none", "identity"):
+        return x
+    return _Act.apply(x, act)
+
+
+class _Add(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a, b):
+        a, b = a.contiguous(), b.contiguous()
+        y = torch.empty_like(a)
+        raw.elementwise("add", a, y, z=b)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        return dy, dy
+
+
+def add(a, b):
+    if a.shape != b.shape:
+        return a + b
+    return _Add.apply(a, b)
+
+
+class _Rezero(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, g):
+        xc = x.contiguous()
+        y = torch.empty_like(xc)
+        sm = _param32(g).reshape(-1)
+        raw.elementwise("mul_scalar", xc, y, sptr=sm)
+        ctx.save_for_backward(xc, g)
+        ctx.sm = sm
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xc, g = ctx.saved_tensors
+        dy = dy.contiguous()
+        dx = torch.empty_like(dy)
+        raw.elementwise("mul_scalar", dy, dx, sptr=ctx.sm)
+        gg, m = _acc_grad(g)
+        raw.dot(xc, dy, gg.reshape(-1))
+        _done(g)
+        return dx, None if m else gg.to(g.dtype)
+
+
+def rezero(x, g):
+    return _Rezero.apply(x, g)
+
+
+class _Dropout(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, keep, seed):
+        xc = x.contiguous()
+        y = torch.empty_like(xc)
+        raw.elementwise("dropout", xc, y, keep=keep, seed=seed)
+        ctx.cfg = (keep, seed)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        keep, seed = ctx.cfg
+        dx = torch.empty_like(dy.contiguous())
+        raw.elementwise("dropout", dy.contiguous(), dx, keep=keep, seed=seed)
+        return dx, None, None
+
+
+def dropout(x, keep: float, seed: int, train: bool = True):
+    if not train or keep >= 1.0:
+        return x
+    return _Dropout.apply(x, keep, seed)
+
+
+class _Cumsum(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, axis, mean):
+        xc = x.contiguous()
+        shape = xc.shape
+        outer = int(math.prod(shape[:axis]))
+        S = shape[axis]
+        inner = int(math.prod(shape[axis + 1:]))
+        y = torch.empty_like(xc)
+        raw.cumsum(xc, y, outer, S, inner, reverse=False, mean=mean, grad=False)
+        ctx.cfg = (outer, S, inner, mean)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        outer, S, inner, mean = ctx.cfg
+        dy = dy.contiguous()
+        dx = torch.empty_like(dy)
+        raw.cumsum(dy, dx, outer, S, inner, reverse=True, mean=mean, grad=True)
+        return dx, None, None
+
+
+def cumsum(x, axis: int, mean: bool = False):
+    return _Cumsum.apply(x, axis, mean)
+
+
+# ================================================================================================================
+# embedding gather (K08) / scatter-add (K09)
+class _Gather(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, idx, table, V, F):
+        idx32 = idx.to(torch.int32).contiguous()
+        T = idx32.numel()
+        out = torch.empty(list(idx.shape) + [F], dtype=table.dtype, device=table.device)
+        raw.gather(idx32, table, out, T, F, V)
+        ctx.save_for_backward(idx32, table)
+        ctx.cfg = (T, F, V)
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        idx32, table = ctx.saved_tensors
+        T, F, V = ctx.cfg
+        g, m = _acc_grad(table)
+        raw.scatter_add(idx32, dy.contiguous(), g, T, F, V)
+        _done(table)
+        return None, None if m else g.to(table.dtype), None, None
+
+
+def gather(idx, table, V: int, F: int):
+    return _Gather.apply(idx, table, V, F)
+
+
+# ================================================================================================================
+# fused output projection + softmax cross-entropy + z-loss + accuracy (K01 + K10)
+class _SoftmaxXent(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, tgt, V, z_loss, n_total):
+        rows = tgt.numel()
+        Vp = logits.shape[-1]
+        lc = logits.contiguous()
+        t32 = tgt.to(torch.int32).contiguous()
+        sdt = torch.float64 if lc.dtype == torch.float64 else torch.float32
+        lse = torch.empty(rows, dtype=sdt, device=lc.device)
+        loss = torch.empty(rows, dtype=sdt, device=lc.device)
+        hit = torch.empty(rows, dtype=sdt, device=lc.device)
+        raw.xent_fwd(lc, t32, lse, loss, hit, rows, V, Vp, z_loss)
+        ctx.save_for_backward(lc, t32, lse)
+        ctx.cfg = (rows, V, Vp, z_loss, n_total)
+        ctx.mark_non_differentiable(hit)
+        return loss.sum() / n_total, hit.sum() / n_total
+
+    @staticmethod
+    def backward(ctx, dloss, dacc):
+        lc, t32, lse = ctx.saved_tensors
+        rows, V, Vp, z_loss, n_total = ctx.cfg
+        g = lc  # in-place: the logits buffer is dead after this point
+        gptr = dloss.reshape(1).to(lse.dtype).contiguous()
+        raw.xent_bwd(lc, t32, lse, g, gptr, 1.0 / n_total, rows, V, Vp, z_loss)
+        return g, None, None, None, None
+
+
+def softmax_xent(logits, tgt, V: int, z_loss: float, n_total: int):
+    """(mean loss incl. z-loss, accuracy). `logits` may be vocab-padded (columns >= V ignored)."""
+    return _SoftmaxXent.apply(logits, tgt, V, z_loss, n_total)

@@ -1,0 +1,493 @@
+"""Raw (non-autograd) compute primitives. Each has two implementations with identical semantics:
+
+* CUDA tensors → the hand-written gfx950 HIP kernels in ``csrc/kernels`` (never a silent PyTorch fallback);
+* CPU / meta tensors → a plain PyTorch fp32 oracle (the CPU plumbing path, and the numerics reference the
+  GPU tests compare against).
+
+The autograd ops (``ops/functional.py``) and the model are written once against these primitives, so the CPU
+test-suite exercises exactly the orchestration (strides, batching, fusion flags) the GPU path runs.
+Before every launch the host checks that the largest element each operand descriptor can touch lies inside the
+tensor's storage (a kernel fault can reset every GPU of the node).
+"""
+from __future__ import annotations
+
+import math
+import typing
+
+import torch
+
+from . import _lib as L
+
+ACTS = {None: 0, "none": 0, "identity": 0, "relu": 1, "gelu": 2, "silu": 3, "sigmoid": 4, "tanh": 5,
+        "lecun_tanh": 6, "mish": 7, "softsign": 8, "exp": 9}
+
+
+def _f(t: torch.Tensor) -> torch.Tensor:
+    return t if t.dtype == torch.float64 else t.float()
+
+
+def on_gpu(t: torch.Tensor) -> bool:
+    return t.device.type == "cuda"
+
+
+def _room(t: torch.Tensor) -> int:
+    """elements addressable from t.data_ptr() to the end of its storage"""
+    return t.untyped_storage().nbytes() // t.element_size() - t.storage_offset()
+
+
+def _need(t: typing.Optional[torch.Tensor], max_index: int, name: str):
+    if t is None:
+        return
+    if max_index >= _room(t):
+        raise L.KernelError(f"operand {name}: descriptor reaches element {max_index} but storage holds {_room(t)}")
+
+
+# ----------------------------------------------------------------------------------------------------------------
+# activations (torch oracle; the kernels implement the same formulas in csrc/kernels/common.h)
+def act_fwd_t(act: typing.Optional[str], x: torch.Tensor) -> torch.Tensor:
+    if act in (None, "none", "identity"):
+        return x
+    if act == "relu":
+        return torch.relu(x)
+    if act == "gelu":
+        return 0.5 * x * (1 + torch.tanh(math.sqrt(2 / math.pi) * (x + 0.044715 * x ** 3)))
+    if act == "silu":
+        return x * torch.sigmoid(x)
+    if act == "sigmoid":
+        return torch.sigmoid(x)
+    if act == "tanh":
+        return torch.tanh(x)
+    if act == "lecun_tanh":
+        return torch.tanh(x) + 0.1 * x
+    if act == "mish":
+        return x * torch.tanh(torch.nn.functional.softplus(x))
+    if act == "softsign":
+        return x / (1 + x.abs())
+    if act == "exp":
+        return torch.exp(x)
+    raise ValueError(act)
+
+
+def act_grad_t(act: typing.Optional[str], x: torch.Tensor) -> torch.Tensor:
+    if act in (None, "none", "identity"):
+        return torch.ones_like(x)
+    if act == "relu":
+        return (x > 0).to(x.dtype)
+    if act == "gelu":
+        k0, k1 = math.sqrt(2 / math.pi), 0.044715
+        t = torch.tanh(k0 * (x + k1 * x ** 3))
+        return 0.5 * (1 + t) + 0.5 * x * (1 - t * t) * k0 * (1 + 3 * k1 * x * x)
+    if act == "silu":
+        s = torch.sigmoid(x)
+        return s * (1 + x * (1 - s))
+    if act == "sigmoid":
+        s = torch.sigmoid(x)
+        return s * (1 - s)
+    if act == "tanh":
+        return 1 - torch.tanh(x) ** 2
+    if act == "lecun_tanh":
+        return 1.1 - torch.tanh(x) ** 2
+    if act == "mish":
+        sp = torch.nn.functional.softplus(x)
+        tsp = torch.tanh(sp)
+        return tsp + x * (1 - tsp * tsp) * torch.sigmoid(x)
+    if act == "softsign":
+        return 1 / (1 + x.abs()) ** 2
+    if act == "exp":
+        return torch.exp(x)
+    raise ValueError(act)
+
+
+# ----------------------------------------------------------------------------------------------------------------
+# GEMM
+class Operand(typing.NamedTuple):
+    t: torch.Tensor
+    trans: int            # A: 0 = [M][K], 1 = [K][M];  B: 0 = [N][K], 1 = [K][N]
+    ld: int
+    s1: int = 0
+    s2: int = 0
+
+
+def gemm(a: Operand, b: Operand, c: Operand, M: int, N: int, K: int, batch: typing.Tuple[int, int] = (1, 1),
+         alpha: float = 1.0, beta: float = 0.0, act: typing.Optional[str] = None, act_bwd: bool = False,
+         R: typing.Optional[torch.Tensor] = None, Zout: typing.Optional[torch.Tensor] = None,
+         Zin: typing.Optional[torch.Tensor] = None):
+    """C = epilogue(alpha * A·B). R, Zout, Zin share C's leading dims / batch strides.
+
+    epilogue (act_bwd False): v = alpha*acc (+ beta*C if C is fp32) (+ R); Zout <- v; C <- act(v)
+    epilogue (act_bwd True) : C <- (alpha*acc + R) * act'(Zin)"""
+    if c.t.device.type == "meta":
+        return c.t
+    b1, b2 = batch
+    if on_gpu(c.t):
+        out_f32 = c.t.dtype == torch.float32
+        for nm, t in (("A", a.t), ("B", b.t)):
+            if t.dtype != torch.bfloat16:
+                raise L.KernelError(f"gemm operand {nm} must be bfloat16 on the GPU, got {t.dtype}")
+        if not out_f32 and c.t.dtype != torch.bfloat16:
+            raise L.KernelError(f"gemm output must be bf16 or fp32, got {c.t.dtype}")
+        if (R is not None or Zout is not None or Zin is not None) and out_f32 and (Zout is not None or act_bwd):
+            raise L.KernelError("pre-activation output / activation-backward epilogue need a bf16 output")
+        bo = (b1 - 1) * a.s1 + (b2 - 1) * a.s2
+        _need(a.t, bo + ((M - 1) * a.ld + K - 1 if a.trans == 0 else (K - 1) * a.ld + M - 1), "A")
+        bo = (b1 - 1) * b.s1 + (b2 - 1) * b.s2
+        _need(b.t, bo + ((N - 1) * b.ld + K - 1 if b.trans == 0 else (K - 1) * b.ld + N - 1), "B")
+        cmax = (b1 - 1) * c.s1 + (b2 - 1) * c.s2 + (M - 1) * c.ld + N - 1
+        for nm, t in (("C", c.t), ("R", R), ("Zout", Zout), ("Zin", Zin)):
+            _need(t, cmax, nm)
+        d = L.GemmDesc(a.t.data_ptr(), b.t.data_ptr(), c.t.data_ptr(), L.ptr(R), L.ptr(Zout), L.ptr(Zin),
+                       a.ld, b.ld, c.ld, a.s1, a.s2, b.s1, b.s2, c.s1, c.s2, M, N, K, b1, b2,
+                       a.trans, b.trans, int(out_f32), ACTS[act], int(act_bwd), float(alpha), float(beta))
+        L.check(L.lib().obst_gemm(d, L.stream_ptr()), "gemm")
+        return c.t
+    # ---- torch oracle
+    av = torch.as_strided(a.t, (b1, b2, M, K), (a.s1, a.s2, a.ld, 1) if a.trans == 0 else (a.s1, a.s2, 1, a.ld),
+                          a.t.storage_offset())
+    bv = torch.as_strided(b.t, (b1, b2, K, N), (b.s1, b.s2, 1, b.ld) if b.trans == 0 else (b.s1, b.s2, b.ld, 1),
+                          b.t.storage_offset())
+    shape, strides = (b1, b2, M, N), (c.s1, c.s2, c.ld, 1)
+
+    def view(t):
+        return None if t is None else torch.as_strided(t, shape, strides, t.storage_offset())
+
+    cv = view(c.t)
+    acc = torch.matmul(_f(av), _f(bv)) * alpha
+    if act_bwd:
+        if R is not None:
+            acc = acc + _f(view(R))
+        acc = acc * act_grad_t(act, _f(view(Zin)))
+    else:
+        if beta != 0.0:
+            acc = acc + beta * _f(cv)
+        if R is not None:
+            acc = acc + _f(view(R))
+        if Zout is not None:
+            view(Zout).copy_(acc)
+        acc = act_fwd_t(act, acc)
+    cv.copy_(acc)
+    return c.t
+
+
+# ----------------------------------------------------------------------------------------------------------------
+# flash attention on token-major [B, S, H, D] tensors with row stride ld (elements)
+def _bshd(t: torch.Tensor, B, S, H, D, ld):
+    return torch.as_strided(t, (B, S, H, D), (S * ld, ld, D, 1), t.storage_offset())
+
+
+def attn_fwd(q, k, v, o, lse, B, S, H, D, ld, scale: float, causal: bool):
+    if q.device.type == "meta":
+        return None
+    if on_gpu(q):
+        if D not in (32, 64, 128):
+            raise L.KernelError(f"attention head dim {D} not supported by the HIP kernel (32/64/128)")
+        for nm, t in (("q", q), ("k", k), ("v", v), ("o", o)):
+            if t.dtype != torch.bfloat16:
+                raise L.KernelError(f"attention {nm} must be bf16")
+            _need(t, (B * S - 1) * ld + (H - 1) * D + D - 1, nm)
+        _need(lse, B * H * S - 1, "lse")
+        d = L.AttnDesc(q.data_ptr(), k.data_ptr(), v.data_ptr(), 0, 0, o.data_ptr(), 0, 0, 0, lse.data_ptr(), 0,
+                       B, S, H, D, ld, float(scale), int(causal))
+        L.check(L.lib().obst_attn_fwd(d, L.stream_ptr()), "attn_fwd")
+        return
+    qv, kv, vv = (_f(_bshd(t, B, S, H, D, ld)) for t in (q, k, v))
+    s = torch.einsum("bqhd,bkhd->bhqk", qv, kv) * scale
+    if causal:
+        s = s.masked_fill(torch.ones(S, S, dtype=torch.bool, device=s.device).triu(1), float("-inf"))
+    m = s.logsumexp(-1)
+    p = torch.exp(s - m.unsqueeze(-1))
+    _bshd(o, B, S, H, D, ld).copy_(torch.einsum("bhqk,bkhd->bqhd", p, vv))
+    lse.view(B, H, S).copy_(m)
+
+
+def attn_bwd(q, k, v, o, do, lse, delta, dq, dk, dv, B, S, H, D, ld, scale: float, causal: bool):
+    if q.device.type == "meta":
+        return None
+    if on_gpu(q):
+        if D not in (32, 64, 128):
+            raise L.KernelError(f"attention head dim {D} not supported by the HIP kernel (32/64/128)")
+        for nm, t in (("q", q), ("k", k), ("v", v), ("o", o), ("do", do), ("dq", dq), ("dk", dk), ("dv", dv)):
+            if t.dtype != torch.bfloat16:
+                raise L.KernelError(f"attention {nm} must be bf16")
+            _need(t, (B * S - 1) * ld + (H - 1) * D + D - 1, nm)
+        _need(lse, B * H * S - 1, "lse")
+        _need(delta, B * H * S - 1, "delta")
+        d = L.AttnDesc(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), do.data_ptr(), 0, dq.data_ptr(),
+                       dk.data_ptr(), dv.data_ptr(), lse.data_ptr(), delta.data_ptr(), B, S, H, D, ld, float(scale),
+                       int(causal))
+        L.check(L.lib().obst_attn_bwd(d, L.stream_ptr()), "attn_bwd")
+        return
+    qv, kv, vv, ov, dov = (_f(_bshd(t, B, S, H, D, ld)) for t in (q, k, v, o, do))
+    s = torch.einsum("bqhd,bkhd->bhqk", qv, kv) * scale
+    if causal:
+        s = s.masked_fill(torch.ones(S, S, dtype=torch.bool, device=s.device).triu(1), float("-inf"))
+    p = torch.exp(s - lse.view(B, H, S).unsqueeze(-1))
+    dlt = (dov * ov).sum(-1).permute(0, 2, 1)  # [B,H,S]
+    delta.view(B, H, S).copy_(dlt)
+    _bshd(dv, B, S, H, D, ld).copy_(torch.einsum("bhqk,bqhd->bkhd", p, dov))
+    dp = torch.einsum("bqhd,bkhd->bhqk", dov, vv)
+    ds = p * (dp - dlt.unsqueeze(-1))
+    _bshd(dq, B, S, H, D, ld).copy_(torch.einsum("bhqk,bkhd->bqhd", ds, kv) * scale)
+    _bshd(dk, B, S, H, D, ld).copy_(torch.einsum("bhqk,bqhd->bkhd", ds, qv) * scale)
+
+
+# ----------------------------------------------------------------------------------------------------------------
+# norm (reference normalization.py:22-34); x viewed as [rows, F], params indexed by row % groups
+EPS = 1e-5
+
+
+def norm_fwd(x, scale, shift, y, stats, rows: int, F: int, groups: int, ext_stats=None):
+    if x.device.type == "meta":
+        return None
+    if on_gpu(x):
+        if x.dtype != torch.bfloat16:
+            raise L.KernelError("norm input must be bf16 on the GPU")
+        for nm, t in (("x", x), ("y", y)):
+            _need(t, rows * F - 1, nm)
+        _need(stats, 2 * rows - 1, "stats")
+        for nm, t in (("scale", scale), ("shift", shift)):
+            if t is not None:
+                if t.dtype != torch.float32:
+                    raise L.KernelError("norm scale/shift must be fp32 master views")
+                _need(t, groups * F - 1, nm)
+        d = L.NormDesc(x.data_ptr(), L.ptr(scale), L.ptr(shift), y.data_ptr(), L.ptr(stats), 0, 0, 0, 0, 0,
+                       L.ptr(ext_stats), rows, F, groups, F, EPS)
+        L.check(L.lib().obst_norm_fwd(d, L.stream_ptr()), "norm_fwd")
+        return
+    xv = _f(x.reshape(rows, F))
+    if ext_stats is not None:
+        mean, rstd = ext_stats.view(rows, 2)[:, 0:1], ext_stats.view(rows, 2)[:, 1:2]
+    else:
+        mean = xv.mean(-1, keepdim=True)
+        rstd = torch.rsqrt(((xv - mean) ** 2).mean(-1, keepdim=True) + EPS)
+    out = (xv - mean) * rstd
+    g = torch.arange(rows, device=x.device) % groups
+    if scale is not None:
+        out = out * scale.reshape(groups, F)[g]
+    if shift is not None:
+        out = out + shift.reshape(groups, F)[g]
+    y.reshape(rows, F).copy_(out)
+    if stats is not None:
+        stats.view(rows, 2).copy_(torch.cat([mean, rstd], -1))
+
+
+def norm_partial(x, out, rows: int, F: int):
+    """per-row (sum x, sum x^2) of this rank's slice (TP statistics, collective X05)"""
+    if x.device.type == "meta":
+        return None
+    if on_gpu(x):
+        _need(x, rows * F - 1, "x")
+        _need(out, 2 * rows - 1, "out")
+        d = L.NormDesc(x.data_ptr(), 0, 0, 0, 0, 0, 0, 0, 0, out.data_ptr(), 0, rows, F, 1, F, EPS)
+        L.check(L.lib().obst_norm_partial(d, L.stream_ptr()), "norm_partial")
+        return
+    xv = _f(x.reshape(rows, F))
+    out.view(rows, 2).copy_(torch.stack([xv.sum(-1), (xv * xv).sum(-1)], -1))
+
+
+def norm_bwd(x, dy, scale, stats, dx, dscale, dshift, rows: int, F: int, groups: int, Ffull: int = 0,
+             partial=None, ext_dsum=None):
+    """dx (and parameter grads accumulated into fp32 dscale/dshift). With `partial` set, only the per-row partial
+    sums (sum dxh, sum dxh*xh) are written (TP phase 1); phase 2 passes them back as `ext_dsum`."""
+    if x.device.type == "meta":
+        return None
+    Ffull = Ffull or F
+    if on_gpu(x):
+        _need(x, rows * F - 1, "x")
+        _need(dy, rows * F - 1, "dy")
+        if dx is not None:
+            _need(dx, rows * F - 1, "dx")
+        _need(stats, 2 * rows - 1, "stats")
+        for nm, t in (("scale", scale), ("dscale", dscale), ("dshift", dshift)):
+            if t is not None:
+                _need(t, groups * F - 1, nm)
+        d = L.NormDesc(x.data_ptr(), L.ptr(scale), 0, 0, stats.data_ptr(), dy.data_ptr(), L.ptr(dx), L.ptr(dscale),
+                       L.ptr(dshift), L.ptr(partial), L.ptr(ext_dsum), rows, F, groups, Ffull, EPS)
+        L.check(L.lib().obst_norm_bwd(d, L.stream_ptr()), "norm_bwd")
+        return
+    xv = _f(x.reshape(rows, F))
+    dyv = _f(dy.reshape(rows, F))
+    st = stats.view(rows, 2)
+    xh = (xv - st[:, 0:1]) * st[:, 1:2]
+    g = torch.arange(rows, device=x.device) % groups
+    gs = _f(scale.reshape(groups, F)[g]) if scale is not None else 1.0
+    dxh = dyv * gs
+    if partial is not None:
+        partial.view(rows, 2).copy_(torch.stack([dxh.sum(-1), (dxh * xh).sum(-1)], -1))
+        return
+    if dscale is not None:
+        dscale.reshape(groups, F).index_add_(0, g, (dyv * xh).to(dscale.dtype))
+    if dshift is not None:
+        dshift.reshape(groups, F).index_add_(0, g, dyv.to(dshift.dtype))
+    if ext_dsum is not None:
+        s1, s2 = ext_dsum.view(rows, 2)[:, 0:1], ext_dsum.view(rows, 2)[:, 1:2]
+    else:
+        s1, s2 = dxh.sum(-1, keepdim=True), (dxh * xh).sum(-1, keepdim=True)
+    dx.reshape(rows, F).copy_(st[:, 1:2] * (dxh - s1 / Ffull - xh * s2 / Ffull))
+
+
+# ----------------------------------------------------------------------------------------------------------------
+# elementwise
+_EW = {"act": 0, "act_bwd": 1, "add": 2, "mul_scalar": 3, "dropout": 4, "axpby": 5, "mul": 6}
+
+
+def elementwise(op: str, x, y, z=None, act=None, sptr=None, alpha=1.0, beta=1.0, seed=0, keep=1.0):
+    """act: y=act(x); act_bwd: y = z * act'(x); add: y = x + z; mul_scalar: y = x * sptr[0];
+    dropout: y = x * keep_mask / keep; axpby: y = alpha x + beta z; mul: y = x * z"""
+    if x.device.type == "meta":
+        return y
+    n = x.numel()
+    if on_gpu(x):
+        for t in (x, y, z):
+            if t is not None and (t.dtype != torch.bfloat16 or not t.is_contiguous()):
+                raise L.KernelError("elementwise operands must be contiguous bf16 on the GPU")
+            if t is not None:
+                _need(t, n - 1, "ew")
+        if n % 8:
+            raise L.KernelError(f"elementwise size {n} must be a multiple of 8")
+        d = L.EwDesc(x.data_ptr(), L.ptr(z), y.data_ptr(), L.ptr(sptr), n, _EW[op], ACTS[act], float(alpha),
+                     float(beta), int(seed) & (2 ** 64 - 1), float(keep))
+        L.check(L.lib().obst_elementwise(d, L.stream_ptr()), "elementwise")
+        return y
+    xf = _f(x)
+    if op == "act":
+        r = act_fwd_t(act, xf)
+    elif op == "act_bwd":
+        r = _f(z) * act_grad_t(act, xf)
+    elif op == "add":
+        r = xf + _f(z)
+    elif op == "mul_scalar":
+        r = xf * _f(sptr.reshape(-1)[0])
+    elif op == "dropout":
+        r = xf * (dropout_mask(n, seed, keep, x.device).view_as(xf)) / keep
+    elif op == "axpby":
+        r = alpha * xf + beta * _f(z)
+    elif op == "mul":
+        r = xf * _f(z)
+    else:
+        raise ValueError(op)
+    y.copy_(r.view_as(y))
+    return y
+
+
+def dropout_mask(n: int, seed: int, keep: float, device) -> torch.Tensor:
+    """The same counter-based hash as the kernel (splitmix64 finaliser), so CPU and GPU masks agree."""
+    i = torch.arange(n, dtype=torch.int64, device=device)
+    m64 = (1 << 64) - 1
+
+    def _u(v):
+        return torch.tensor(v - (1 << 64) if v >= (1 << 63) else v, dtype=torch.int64, device=device)
+
+    h = (i * _u(0x9E3779B97F4A7C15)) ^ _u(seed & m64)
+
+    def srl(v, k):  # logical shift right on int64
+        return (v >> k) & ((1 << (64 - k)) - 1)
+    h = h ^ srl(h, 33)
+    h = h * _u(0xff51afd7ed558ccd)
+    h = h ^ srl(h, 33)
+    h = h * _u(0xc4ceb9fe1a85ec53)
+    h = h ^ srl(h, 33)
+    u = srl(h, 40).double() / 16777216.0
+    return (u < keep).to(torch.float32)
+
+
+def dot(x, dy, out):
+    """out[0] += sum(x * dy)"""
+    if x.device.type == "meta":
+        return None
+    if on_gpu(x):
+        n = x.numel()
+        if n % 8:
+            raise L.KernelError("dot size must be a multiple of 8")
+        L.check(L.lib().obst_dot(x.data_ptr(), dy.data_ptr(), out.data_ptr(), n, L.stream_ptr()), "dot")
+        return
+    out.view(-1)[0] += (_f(x) * _f(dy)).sum()
+
+
+def gather(idx, table, out, T: int, F: int, V: int):
+    if table.device.type == "meta":
+        return None
+    if on_gpu(table):
+        if idx.dtype != torch.int32:
+            raise L.KernelError("gather indices must be int32")
+        _need(idx, T - 1, "idx")
+        _need(table, V * F - 1, "table")
+        _need(out, T * F - 1, "out")
+        L.check(L.lib().obst_gather(idx.data_ptr(), table.data_ptr(), out.data_ptr(), T, F, V, L.stream_ptr()),
+                "gather")
+        return
+    out.reshape(T, F).copy_(table.reshape(V, F)[idx.reshape(T).long().clamp(0, V - 1)])
+
+
+def scatter_add(idx, dy, dtable, T: int, F: int, V: int):
+    if dy.device.type == "meta":
+        return None
+    if on_gpu(dy):
+        _need(idx, T - 1, "idx")
+        _need(dy, T * F - 1, "dy")
+        _need(dtable, V * F - 1, "dtable")
+        L.check(L.lib().obst_scatter_add(idx.data_ptr(), dy.data_ptr(), dtable.data_ptr(), T, F, V, L.stream_ptr()),
+                "scatter_add")
+        return
+    dtable.reshape(V, F).index_add_(0, idx.reshape(T).long().clamp(0, V - 1), _f(dy.reshape(T, F)).to(dtable.dtype))
+
+
+def cumsum(x, y, outer: int, S: int, inner: int, reverse: bool, mean: bool, grad: bool):
+    if x.device.type == "meta":
+        return None
+    if on_gpu(x):
+        _need(x, outer * S * inner - 1, "x")
+        _need(y, outer * S * inner - 1, "y")
+        L.check(L.lib().obst_cumsum(x.data_ptr(), y.data_ptr(), outer, S, inner, int(reverse), int(mean), int(grad),
+                                    L.stream_ptr()), "cumsum")
+        return
+    xv = _f(x.reshape(outer, S, inner))
+    pos = torch.arange(1, S + 1, device=x.device, dtype=torch.float32).view(1, S, 1)
+    if mean and grad:
+        xv = xv / pos
+    if reverse:
+        r = xv.flip(1).cumsum(1).flip(1)
+    else:
+        r = xv.cumsum(1)
+    if mean and not grad:
+        r = r / pos
+    y.reshape(outer, S, inner).copy_(r)
+
+
+def xent_fwd(logits, tgt, lse, loss, hit, rows: int, V: int, Vp: int, z_loss: float):
+    if logits.device.type == "meta":
+        return None
+    if on_gpu(logits):
+        if tgt.dtype != torch.int32:
+            raise L.KernelError("targets must be int32")
+        _need(logits, rows * Vp - 1, "logits")
+        for nm, t in (("tgt", tgt), ("lse", lse), ("loss", loss), ("hit", hit)):
+            _need(t, rows - 1, nm)
+        L.check(L.lib().obst_xent_fwd(logits.data_ptr(), tgt.data_ptr(), lse.data_ptr(), loss.data_ptr(),
+                                      hit.data_ptr(), rows, V, Vp, float(z_loss), L.stream_ptr()), "xent_fwd")
+        return
+    lv = _f(logits.reshape(rows, Vp)[:, :V])
+    t = tgt.reshape(rows).long()
+    m = lv.logsumexp(-1)
+    ly = lv.gather(1, t.clamp(0, V - 1).unsqueeze(1)).squeeze(1)
+    lse.copy_(m)
+    loss.copy_(-(ly - m) + z_loss * m * m)
+    hit.copy_((lv.argmax(-1) == t).to(hit.dtype))
+
+
+def xent_bwd(logits, tgt, lse, grad, gscale_ptr, gscale: float, rows: int, V: int, Vp: int, z_loss: float):
+    if logits.device.type == "meta":
+        return None
+    if on_gpu(logits):
+        _need(logits, rows * Vp - 1, "logits")
+        _need(grad, rows * Vp - 1, "grad")
+        L.check(L.lib().obst_xent_bwd(logits.data_ptr(), tgt.data_ptr(), lse.data_ptr(), grad.data_ptr(),
+                                      L.ptr(gscale_ptr), float(gscale), rows, V, Vp, float(z_loss), L.stream_ptr()),
+                "xent_bwd")
+        return
+    lv = _f(logits.reshape(rows, Vp))
+    p = torch.exp(lv - lse.view(rows, 1))
+    p[:, V:] = 0
+    g = gscale * (_f(gscale_ptr.reshape(-1)[0]) if gscale_ptr is not None else 1.0)
+    d = p * (1 + 2 * z_loss * lse.view(rows, 1))
+    d[torch.arange(rows, device=lv.device), tgt.reshape(rows).long()] -= 1
+    grad.reshape(rows, Vp).copy_(d * g)

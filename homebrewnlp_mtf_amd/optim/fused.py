@@ -1,0 +1,277 @@
+"""Fused multi-tensor optimizer step on the GPU (K20, csrc/kernels/optim.hip).
+
+The chain is compiled into *segments*: a segment is one ``opt_apply`` launch over every tensor (chunk table ->
+tensor table), and starts at each stage that needs a per-tensor reduction of its input (adaptive/l2/global clip,
+gradient centralisation, NovoGrad, Adafactor). Reductions of the raw gradient / weights come from one ``opt_stats``
+pass; later ones are accumulated by the previous segment's launch (``emit_stats``). A one-block ``opt_scalar``
+launch turns statistics into per-tensor factors. The last segment applies rezero / weight decay, ``w -= u`` and
+writes the bf16 compute copy. For the shipped chain ``adaptive_clip-sm3-momentum-learning_rate`` this is three
+launches for all parameters together.
+
+Under TP, statistics of sharded tensors are summed over the TP group and SM3 accumulators of non-head dims are
+max-reduced (collectives X10-X12), each as ONE packed RCCL call per step.
+"""
+from __future__ import annotations
+
+import math
+import struct
+import typing
+
+import torch
+import torch.distributed as dist
+
+from ..ops import _lib as L
+from ..parallel import state as pstate
+from .chain import parse_chain
+
+OP = dict(none=0, adaptive_clip=1, l2norm_clip=2, global_l2norm_clip=3, value_clip=4, gradient_centralisation=5,
+          weight_centralisation=6, sm3=7, momentum=8, adam=9, novograd=10, learning_rate=11, adafactor=12,
+          adafactor_clip=13, scale=14)
+REDUCTIONS = {"adaptive_clip", "l2norm_clip", "global_l2norm_clip", "gradient_centralisation", "novograd",
+              "adafactor", "adafactor_clip"}
+CHUNK = 16384
+
+
+def _f2i(x: float) -> int:
+    return struct.unpack("<i", struct.pack("<f", float(x)))[0]
+
+
+class Segment:
+    def __init__(self):
+        self.opener: typing.Optional[typing.Tuple[str, tuple]] = None
+        self.stages: typing.List[typing.Tuple[str, tuple]] = []
+        self.emit_stats = False
+        self.emit_factored = False
+
+
+def supported(chain: str) -> bool:
+    return all(n != "graft" for n, _ in parse_chain(chain))
+
+
+def compile_chain(chain: str) -> typing.Tuple[typing.List[Segment], bool, bool]:
+    """-> (segments, needs a pre-pass that materialises factored stats of the raw grad, weight_centralisation)"""
+    stages = []
+    for n, a in parse_chain(chain):
+        stages.append((n, a))
+        if n == "adafactor":
+            stages.append(("adafactor_clip", ()))
+    segs = [Segment()]
+    pre_factored = False
+    wc = any(n == "weight_centralisation" for n, _ in stages)
+    first = True
+    for n, a in stages:
+        if n in REDUCTIONS:
+            if first and n != "adafactor":
+                segs[0].opener = (n, a)          # statistics of the raw gradient come from the stats pass
+            else:
+                if first and n == "adafactor":
+                    pre_factored = True           # identity pre-pass emits row/col sums of g^2
+                elif n == "adafactor":
+                    segs[-1].emit_factored = True
+                else:
+                    segs[-1].emit_stats = True
+                s = Segment()
+                s.opener = (n, a)
+                segs.append(s)
+        segs[-1].stages.append((n, a))
+        first = False
+    if pre_factored:
+        segs[0].emit_factored = True
+    return segs, pre_factored, wc
+
+
+class FusedOptimizer:
+    def __init__(self, store, params):
+        L.lib()
+        self.store, self.params = store, params
+        self.chain = params.optimizer
+        self.segments, self.pre_factored, self.wc = compile_chain(self.chain)
+        names = [n for n in store.order if store.specs[n].trainable]
+        self.names = names
+        dev = store.device
+        self.tp = pstate.tp_size()
+        chain_names = {n for n, _ in parse_chain(self.chain)}
+        need_sm3 = "sm3" in chain_names
+        need_mom = "momentum" in chain_names or "novograd" in chain_names
+        need_adam = "adam" in chain_names
+        need_af = "adafactor" in chain_names
+        # --- tensor table ----------------------------------------------------------------------------------------
+        recs, chunks = [], []
+        sm3_local, sm3_red = [], []     # (tensor idx, dim) lists for the two SM3 regions
+        fac_total = 0
+        self.sharded = []
+        for ti, n in enumerate(names):
+            s = store.specs[n]
+            shape = list(s.local_shape)
+            if len(shape) > 4:  # merge leading dims (SM3 then keeps one accumulator for the merged prefix)
+                shape = [int(math.prod(shape[:len(shape) - 3]))] + shape[-3:]
+            self.sharded.append(s.tp_dim is not None)
+            for d in range(len(shape)):
+                local = self.tp == 1 or (s.tp_dim is not None and d == s.tp_dim)
+                (sm3_local if local else sm3_red).append((ti, d, shape[d]))
+            recs.append([s.offset, s.numel, len(shape), shape])
+            for st in range(0, s.numel, CHUNK):
+                chunks.append(struct.pack("<iiqq", ti, 0, st, min(CHUNK, s.numel - st)))
+        # SM3 offsets: local region first, then the region that is max-reduced over TP
+        sm3_off = {}
+        off = 0
+        for ti, d, sz in sm3_local:
+            sm3_off[(ti, d)] = off
+            off += sz
+        self.sm3_red_start = off
+        for ti, d, sz in sm3_red:
+            sm3_off[(ti, d)] = off
+            off += sz
+        self.sm3_total = max(off, 1)
+        packed = []
+        self.fac = {}
+        for ti, (offset, numel, ndim, shape) in enumerate(recs):
+            flags = 0
+            n = names[ti]
+            if store.specs[n].weight_decay_eligible(params):
+                flags |= 1
+            if store.specs[n].is_rezero:
+                flags |= 2
+            if self.sharded[ti]:
+                flags |= 4
+            dims = (shape + [1, 1, 1, 1])[:4]
+            so = [sm3_off.get((ti, d), 0) for d in range(4)]
+            frows = fcols = 0
+            foff = 0
+            if need_af and ndim >= 2:
+                fcols = shape[-1]
+                frows = numel // fcols
+                foff = fac_total
+                fac_total += frows + fcols
+            packed.append(struct.pack("<qqii4i4qqii", offset, numel, ndim, flags, *dims, *so, foff, frows, fcols))
+        self.ntensors = len(packed)
+        self.nchunks = len(chunks)
+        self.t_tensors = torch.tensor(bytearray(b"".join(packed)), dtype=torch.uint8, device=dev)
+        self.t_chunks = torch.tensor(bytearray(b"".join(chunks)), dtype=torch.uint8, device=dev)
+        f32 = dict(dtype=torch.float32, device=dev)
+        self.stats = torch.zeros(self.ntensors * 8, **f32)
+        self.facs = torch.zeros(self.ntensors * 8, **f32)
+        self.sstate = torch.zeros(self.ntensors * 4, **f32)
+        self.shard_mask = torch.tensor([1.0 if s else 0.0 for s in self.sharded], **f32).view(-1, 1)
+        total = store.total
+        self.mom = torch.zeros(total, **f32) if need_mom else None
+        self.adam_m = torch.zeros(total, **f32) if need_adam else None
+        self.adam_v = torch.zeros(total, **f32) if (need_adam or need_af) else None
+        self.sm3 = [torch.zeros(self.sm3_total, **f32), torch.zeros(self.sm3_total, **f32)] if need_sm3 else None
+        self.af_state = torch.zeros(max(fac_total, 1), **f32) if need_af else None
+        self.af_sums = torch.zeros(max(fac_total, 1), **f32) if need_af else None
+        nseg = len(self.segments) + int(self.pre_factored)
+        self.u = torch.empty(total, **f32) if nseg > 1 else None
+        self.u2 = torch.empty(total, **f32) if nseg > 2 else None
+        self.flip = 0
+
+    # ------------------------------------------------------------------------------------------------------------
+    def _desc(self, lr, step_count, grad_scale):
+        s = self.store
+        d = L.OptDesc()
+        d.tensors, d.chunks = self.t_tensors.data_ptr(), self.t_chunks.data_ptr()
+        d.ntensors, d.nchunks = self.ntensors, self.nchunks
+        d.grad, d.master = s.grad.data_ptr(), s.master.data_ptr()
+        d.compute = s.compute.data_ptr() if s.compute is not s.master else 0
+        d.stats, d.fac, d.sstate = self.stats.data_ptr(), self.facs.data_ptr(), self.sstate.data_ptr()
+        d.mom = L.ptr(self.mom)
+        d.adam_m, d.adam_v = L.ptr(self.adam_m), L.ptr(self.adam_v)
+        if self.sm3 is not None:
+            d.sm3_old, d.sm3_new = self.sm3[self.flip].data_ptr(), self.sm3[1 - self.flip].data_ptr()
+        d.af_state = L.ptr(self.af_state)
+        d.af_rows_sum = d.af_cols_sum = L.ptr(self.af_sums)
+        p = self.params
+        d.lr, d.wd, d.rezero_mult, d.grad_scale = lr, p.weight_decay, p.rezero_lr_multiplier, grad_scale
+        d.beta1, d.beta2, d.step_count = p.opt_beta1, p.opt_beta2, float(step_count)
+        d.tp_size = self.tp
+        return d
+
+    def _set_stages(self, d, stages):
+        if len(stages) > 8:
+            raise ValueError("at most 8 stages per fused segment")
+        arr = [0] * 32
+        for i, (n, a) in enumerate(stages):
+            vals = [float(x) for x in a[:3]] + [0.0] * (3 - len(a[:3]))
+            if n == "adafactor":
+                vals = [float(a[0]) if a else 0.0, 0.0, 0.0]
+            arr[4 * i:4 * i + 4] = [OP[n], _f2i(vals[0]), _f2i(vals[1]), _f2i(vals[2])]
+        d.stages = (L.c_i * 32)(*arr)
+        d.nst = len(stages)
+
+    def _reduce_stats(self):
+        if self.tp > 1:
+            st = self.stats.view(-1, 8)
+            part = st * self.shard_mask
+            pstate.tp_all_reduce(part)
+            st.copy_(part + st * (1 - self.shard_mask))
+
+    def _scalar(self, d, stage):
+        self._set_stages(d, [stage])
+        L.check(L.lib().obst_opt_scalar(d, L.stream_ptr()), "opt_scalar")
+
+    @torch.no_grad()
+    def step(self, lr: float, step_count: int, grad_scale: float = 1.0):
+        lib = L.lib()
+        sp = L.stream_ptr()
+        d = self._desc(lr, step_count, grad_scale)
+        self.stats.zero_()
+        L.check(lib.obst_opt_stats(d, sp), "opt_stats")
+        self._reduce_stats()
+        if self.wc:
+            self._scalar(d, ("weight_centralisation", ()))
+        if self.sm3 is not None:
+            self.sm3[1 - self.flip].zero_()
+        src = None    # None = raw gradient
+        bufs = [self.u, self.u2]
+        bi = 0
+        if self.pre_factored:
+            self.af_sums.zero_()
+            d.uin, d.uout = 0, bufs[bi].data_ptr()
+            self._set_stages(d, [])
+            d.final_seg, d.emit_stats, d.emit_factored = 0, 0, 1
+            L.check(lib.obst_opt_apply(d, sp), "opt_apply(pre)")
+            if self.tp > 1:
+                raise NotImplementedError("adafactor under TP")
+            src, bi = bufs[bi], 1 - bi
+        segs = self.segments[1:] if (self.pre_factored and not self.segments[0].stages) else self.segments
+        for k, seg in enumerate(segs):
+            if seg.opener is not None:
+                self._scalar(d, seg.opener)
+            last = k == len(segs) - 1
+            d.uin = 0 if src is None else src.data_ptr()
+            if seg.emit_stats:
+                self.stats.view(-1, 8)[:, 0:2].zero_()
+            if seg.emit_factored:
+                self.af_sums.zero_()
+            d.uout = 0 if last else bufs[bi].data_ptr()
+            self._set_stages(d, seg.stages)
+            d.final_seg, d.emit_stats, d.emit_factored = int(last), int(seg.emit_stats), int(seg.emit_factored)
+            L.check(lib.obst_opt_apply(d, sp), "opt_apply")
+            if seg.emit_stats:
+                self._reduce_stats()
+            if not last:
+                src, bi = bufs[bi], 1 - bi
+        if self.sm3 is not None:
+            if self.tp > 1 and self.sm3_red_start < self.sm3_total:
+                dist.all_reduce(self.sm3[1 - self.flip][self.sm3_red_start:], op=dist.ReduceOp.MAX,
+                                group=pstate.mesh().tp_group)
+            self.flip = 1 - self.flip
+
+    # ------------------------------------------------------------------------------------------------------------
+    def state_dict(self) -> typing.Dict[str, torch.Tensor]:
+        out = {"flip": torch.tensor(self.flip)}
+        for k in ("mom", "adam_m", "adam_v", "af_state", "sstate"):
+            v = getattr(self, k)
+            if v is not None:
+                out[k] = v
+        if self.sm3 is not None:
+            out["sm3"] = self.sm3[self.flip]
+        return out
+
+    def load_state_dict(self, sd):
+        for k in ("mom", "adam_m", "adam_v", "af_state", "sstate"):
+            if k in sd and getattr(self, k) is not None:
+                getattr(self, k).copy_(sd[k])
+        if self.sm3 is not None and "sm3" in sd:
+            self.flip = 0
+            self.sm3[0].copy_(sd["sm3"])

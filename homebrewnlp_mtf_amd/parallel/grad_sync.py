@@ -1,0 +1,106 @@
+"""Data-parallel gradient all-reduce over RCCL, bucketed and overlapped with backward (collective X08/X09).
+
+The flat fp32 gradient buffer is cut into contiguous buckets of ``grad_bucket_mb`` in *reverse* registration
+order (the order backward produces them: output projection first, input embedding last). Every op that writes a
+weight gradient calls ``grad_ready(weight)``; when the last use of every variable in a bucket has reported, the
+bucket's all-reduce is queued on RCCL's stream (``async_op=True`` orders it after the current compute stream's
+work without blocking it). ``finish()`` flushes the remaining buckets (incl. variables whose gradients arrive via
+plain autograd) and makes the compute stream wait for all of them before the optimizer step.
+
+Bucket sizing for xGMI: a ring all-reduce is per-link bound (~153 GB/s per link); 64 MiB buckets keep
+each ring step well above the latency floor while ~20 buckets of a 1.4B-parameter model still overlap with the
+last layers' backward. The embedding gradient (reference bug A5: no DP reduction) is part of the buffer, so it is
+reduced like every other gradient.
+"""
+from __future__ import annotations
+
+import typing
+
+import torch
+import torch.distributed as dist
+
+from ..ops import functional as F
+
+
+class GradSync:
+    def __init__(self, store, group, world: int, bucket_mb: float = 64.0, dtype: torch.dtype = torch.float32,
+                 use_counts: typing.Optional[typing.Dict[str, int]] = None):
+        self.store = store
+        self.group = group
+        self.world = world
+        self.dtype = dtype
+        self.enabled = world > 1
+        self.use_counts = dict(use_counts or {})
+        cap = max(int(bucket_mb * 2 ** 20 // 4), 1)
+        self.buckets: typing.List[typing.Tuple[int, int, typing.List[str]]] = []
+        names = list(reversed(store.order))
+        cur: typing.List[str] = []
+        for n in names:
+            cur.append(n)
+            lo = min(store.specs[m].offset for m in cur)
+            hi = max(store.specs[m].offset + store.specs[m].numel for m in cur)
+            if hi - lo >= cap:
+                self.buckets.append((lo, hi, cur))
+                cur = []
+        if cur:
+            lo = min(store.specs[m].offset for m in cur)
+            hi = max(store.specs[m].offset + store.specs[m].numel for m in cur)
+            self.buckets.append((lo, hi, cur))
+        # make buckets tile the buffer without gaps (alignment padding belongs to a neighbour)
+        self.var_bucket = {}
+        for bi, (_, _, vs) in enumerate(self.buckets):
+            for v in vs:
+                self.var_bucket[v] = bi
+        self.reset()
+
+    def reset(self):
+        self.remaining = {n: self.use_counts.get(n, 1) for n in self.store.order}
+        self.pending = [len(vs) for _, _, vs in self.buckets]
+        self.launched = [False] * len(self.buckets)
+        self.works = []
+
+    def _launch(self, bi: int):
+        if self.launched[bi]:
+            return
+        self.launched[bi] = True
+        lo, hi, _ = self.buckets[bi]
+        t = self.store.grad[lo:hi]
+        if self.dtype != torch.float32:
+            low = t.to(self.dtype)
+            work = dist.all_reduce(low, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+            self.works.append((work, t, low))
+        else:
+            work = dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+            self.works.append((work, None, None))
+
+    def grad_ready(self, w: torch.Tensor):
+        name = getattr(w, "var_name", None)
+        if name is None or not self.enabled:
+            return
+        r = self.remaining.get(name, 0) - 1
+        self.remaining[name] = r
+        if r == 0:
+            bi = self.var_bucket[name]
+            self.pending[bi] -= 1
+            if self.pending[bi] == 0:
+                self._launch(bi)
+
+    def attach(self):
+        F.GRAD_HOOK = self.grad_ready if self.enabled else None
+
+    def detach(self):
+        F.GRAD_HOOK = None
+
+    def finish(self, average: bool = True):
+        """flush every bucket not yet launched, wait for all, scale to the mean over the DP group"""
+        if not self.enabled:
+            return
+        for bi in range(len(self.buckets)):
+            self._launch(bi)
+        for work, full, low in self.works:
+            work.wait()
+            if full is not None:
+                full.copy_(low)
+        if average:
+            self.store.grad.mul_(1.0 / self.world)
+        self.reset()

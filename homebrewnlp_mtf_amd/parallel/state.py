@@ -1,0 +1,67 @@
+"""Process-wide parallel state: the ``Mesh(dp, tp)`` of the current job.
+
+The reference derives a TPU mesh ``b:{tpu/heads}, h:{heads}`` and lets Mesh-TensorFlow insert every collective
+(``src/dataclass.py:247-252``). Here the grid is explicit: ``world = dp x tp`` with TP groups of
+contiguous ranks (on one 8-GPU node every rank pair has a direct xGMI link, contiguous groups keep a TP group
+inside a node when the job grows past one). Collectives are explicit RCCL calls (backend ``nccl`` is RCCL on
+ROCm) issued from the autograd ops at the sites the reference's layout implied (X01-X12).
+"""
+from __future__ import annotations
+
+import typing
+
+import torch
+import torch.distributed as dist
+
+
+class Mesh:
+    def __init__(self, dp: int = 1, tp: int = 1, rank: int = 0):
+        self.dp, self.tp, self.rank = dp, tp, rank
+        self.world = dp * tp
+        self.tp_rank = rank % tp
+        self.dp_rank = rank // tp
+        self.tp_group: typing.Optional[dist.ProcessGroup] = None
+        self.dp_group: typing.Optional[dist.ProcessGroup] = None
+        self.world_group = None
+
+    def build_groups(self):
+        if not dist.is_initialized() or self.world == 1:
+            return self
+        self.world_group = dist.group.WORLD
+        for d in range(self.dp):
+            ranks = list(range(d * self.tp, (d + 1) * self.tp))
+            g = dist.new_group(ranks)
+            if self.rank in ranks:
+                self.tp_group = g
+        for t in range(self.tp):
+            ranks = list(range(t, self.world, self.tp))
+            g = dist.new_group(ranks)
+            if self.rank in ranks:
+                self.dp_group = g
+        return self
+
+    def __repr__(self):
+        return f"Mesh(dp={self.dp}, tp={self.tp}, rank={self.rank})"
+
+
+_MESH = Mesh()
+
+
+def set_mesh(mesh: Mesh):
+    global _MESH
+    _MESH = mesh
+
+
+def mesh() -> Mesh:
+    return _MESH
+
+
+def tp_size() -> int:
+    return _MESH.tp
+
+
+def tp_all_reduce(t: torch.Tensor, op=None) -> torch.Tensor:
+    """In-place sum (or `op`) over the TP group; identity when tp == 1."""
+    if _MESH.tp > 1:
+        dist.all_reduce(t, op=op or dist.ReduceOp.SUM, group=_MESH.tp_group)
+    return t

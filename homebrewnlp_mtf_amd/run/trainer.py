@@ -1,0 +1,107 @@
+"""Training runtime: model + optimizer + DP gradient sync + step loop (ref src/run/run.py:27-262, train.py:19-77).
+
+One process per GPU. ``Trainer.step(batches)`` runs one optimizer step over ``grad_accumulation`` micro-batches
+(gradient accumulation, bug A11 fixed): forward, backward (weight gradients land in the flat fp32 buffer, DP
+buckets all-reduce while backward runs), then the fused optimizer. ``macro_batching`` (K optimizer steps per host
+call, ref train.py:21-74) is ``train_steps``. Metrics stay on device; the host syncs only when it logs.
+"""
+from __future__ import annotations
+
+import os
+import time
+import typing
+
+import torch
+import torch.distributed as dist
+
+from ..config import ModelParameter
+from ..models.model import Model
+from ..optim import fused as fused_opt
+from ..optim.chain import learning_rate
+from ..optim.reference import ReferenceOptimizer
+from ..parallel import state as pstate
+from ..parallel.grad_sync import GradSync
+from ..utils.log import log
+
+
+class Trainer:
+    def __init__(self, params: ModelParameter, device: typing.Union[str, torch.device] = "cpu",
+                 mesh: typing.Optional[pstate.Mesh] = None, dtype: typing.Optional[torch.dtype] = None,
+                 use_fused: typing.Optional[bool] = None):
+        self.params = params
+        self.device = torch.device(device)
+        self.mesh = mesh or pstate.mesh()
+        pstate.set_mesh(self.mesh)
+        if params.train_batch_size % self.mesh.dp:
+            raise ValueError("train_batch_size must be divisible by dp")
+        self.local_batch = params.train_batch_size // self.mesh.dp
+        t0 = time.time()
+        self.model = Model(params, self.device, self.mesh.tp_rank, self.mesh.tp, dtype=dtype,
+                           local_batch=self.local_batch)
+        self.store = self.model.store
+        log(f"model built in {time.time() - t0:.1f}s: {self.store.global_numel() / 1e6:.2f}M parameters "
+            f"({len(self.store.specs)} tensors), local {self.store.numel() / 1e6:.2f}M")
+        if use_fused is None:
+            use_fused = self.device.type == "cuda" and fused_opt.supported(params.optimizer)
+        self.opt = fused_opt.FusedOptimizer(self.store, params) if use_fused else ReferenceOptimizer(self.store,
+                                                                                                        params)
+        self.grad_sync = GradSync(self.store, self.mesh.dp_group, self.mesh.dp, params.grad_bucket_mb,
+                                  {"float32": torch.float32, "bfloat16": torch.bfloat16}[params.allreduce_dtype],
+                                  use_counts=self.model.builder.use_counts)
+        self.global_step = int(params.current_step)
+
+    # ---------------------------------------------------------------------------------------------------------------
+    def _micro_batches(self, batch: typing.Dict[str, torch.Tensor]) -> typing.List[typing.Dict[str, torch.Tensor]]:
+        n = int(self.params.grad_accumulation)
+        if n == 1:
+            return [batch]
+        out = []
+        for i in range(n):
+            out.append({k: (None if v is None else v.chunk(n, 0)[i]) for k, v in batch.items()})
+        return out
+
+    def step(self, batch: typing.Dict[str, torch.Tensor]) -> typing.Dict[str, torch.Tensor]:
+        """one optimizer step; returns device-side metrics"""
+        self.store.zero_grad()
+        micro = self._micro_batches(batch)
+        metrics: typing.Dict[str, torch.Tensor] = {}
+        for i, mb in enumerate(micro):
+            last = i == len(micro) - 1
+            if last:
+                self.grad_sync.attach()
+            try:
+                out = self.model(**mb, train=True, step_seed=self.global_step * 131 + i)
+                loss = out["loss"] / len(micro)
+                loss.backward()
+            finally:
+                self.grad_sync.detach()
+            self.store.fold_leaf_grads()
+            for k, v in out.items():
+                v = v.detach().float()
+                metrics[k] = metrics.get(k, 0) + v / len(micro)
+        self.grad_sync.finish(average=True)
+        lr = learning_rate(self.params, self.global_step)
+        self.opt.step(lr, self.global_step + 1)
+        self.global_step += 1
+        metrics["learning_rate"] = torch.tensor(lr)
+        return metrics
+
+    def train_steps(self, batches: typing.Iterable[typing.Dict[str, torch.Tensor]]):
+        """macro-batching: several optimizer steps per host call (first/last/mean loss, ref run.py:123-132)"""
+        losses = []
+        last = None
+        for b in batches:
+            last = self.step(b)
+            losses.append(last["loss"])
+        if not losses:
+            return {}
+        st = torch.stack(losses)
+        out = dict(last)
+        out.update(first_loss=st[0], last_loss=st[-1], mean_loss=st.mean())
+        return out
+
+    # ---------------------------------------------------------------------------------------------------------------
+    @torch.no_grad()
+    def evaluate(self, batch) -> typing.Dict[str, torch.Tensor]:
+        out = self.model(**batch, train=False)
+        return {k: v.float() for k, v in out.items()}
