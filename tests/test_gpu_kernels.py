@@ -1,0 +1,198 @@
+"""HIP kernel numerics vs the PyTorch fp32 oracle of the same op (ops/raw.py CPU path).
+
+Every test builds inputs on the CPU, runs the CPU oracle, copies the inputs to the GPU, runs the gfx950 kernel
+through the same ``raw`` entry point, and compares.
+"""
+import math
+
+import pytest
+import torch
+
+from homebrewnlp_mtf_amd.ops import raw
+from homebrewnlp_mtf_amd.ops import functional as F
+
+pytestmark = pytest.mark.gpu
+BF = torch.bfloat16
+
+
+def _close(gpu, ref, atol, rtol, what=""):
+    g = gpu.float().cpu()
+    r = ref.float()
+    err = (g - r).abs()
+    tol = atol + rtol * r.abs()
+    bad = (err > tol).sum().item()
+    assert bad == 0, f"{what}: {bad}/{r.numel()} out of tolerance, max err {err.max().item():.4g}"
+
+
+# ----------------------------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("a_t,b_t", [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (200, 136, 72), (512, 384, 256), (64, 8, 8)])
+def test_gemm_layouts(cuda, a_t, b_t, M, N, K):
+    torch.manual_seed(M + N + K + 10 * a_t + b_t)
+    A = (torch.randn(M * K) * 0.5).to(BF)
+    B = (torch.randn(N * K) * 0.5).to(BF)
+    lda = K if a_t == 0 else M
+    ldb = K if b_t == 0 else N
+    C = torch.zeros(M * N, dtype=BF)
+    raw.gemm(raw.Operand(A, a_t, lda), raw.Operand(B, b_t, ldb), raw.Operand(C, 0, N), M, N, K)
+    Cg = torch.zeros(M * N, dtype=BF, device=cuda)
+    raw.gemm(raw.Operand(A.to(cuda), a_t, lda), raw.Operand(B.to(cuda), b_t, ldb), raw.Operand(Cg, 0, N), M, N, K)
+    torch.cuda.synchronize()
+    _close(Cg, C, 2e-2 * math.sqrt(K / 64), 2e-2, f"gemm {a_t}{b_t} {M}x{N}x{K}")
+
+
+def test_gemm_identity_asymmetric(cuda):
+    """A = I with an asymmetric B catches a transposed C write (cdna guide §3)."""
+    n = 128
+    A = torch.eye(n).to(BF)
+    B = torch.arange(n * n, dtype=torch.float32).view(n, n).remainder(97).to(BF)  # stored [K][N]
+    Cg = torch.zeros(n * n, dtype=BF, device=cuda)
+    raw.gemm(raw.Operand(A.reshape(-1).to(cuda), 0, n), raw.Operand(B.reshape(-1).to(cuda), 1, n),
+             raw.Operand(Cg, 0, n), n, n, n)
+    torch.cuda.synchronize()
+    assert torch.equal(Cg.view(n, n).cpu(), B)
+
+
+def test_gemm_batched_epilogues(cuda):
+    torch.manual_seed(3)
+    H, M, K, N = 3, 96, 64, 40
+    A = (torch.randn(M, H, K) * 0.5).to(BF)            # [M][H][K] -> batch stride K, ld H*K
+    B = (torch.randn(H, K, N) * 0.5).to(BF)            # [H][K][N]
+    R = (torch.randn(M, H, N) * 0.5).to(BF)
+    outs = {}
+    for dev in ("cpu", cuda):
+        C = torch.zeros(M, H, N, dtype=BF, device=dev)
+        Z = torch.zeros(M, H, N, dtype=BF, device=dev)
+        raw.gemm(raw.Operand(A.to(dev), 0, H * K, K), raw.Operand(B.to(dev), 1, N, K * N),
+                 raw.Operand(C, 0, H * N, N), M, N, K, batch=(H, 1), act="gelu", R=R.to(dev), Zout=Z)
+        D = torch.zeros(M, H, N, dtype=BF, device=dev)   # activation-backward epilogue: (acc + R) * gelu'(Z)
+        raw.gemm(raw.Operand(A.to(dev), 0, H * K, K), raw.Operand(B.to(dev), 1, N, K * N),
+                 raw.Operand(D, 0, H * N, N), M, N, K, batch=(H, 1), act="gelu", act_bwd=True, Zin=Z, R=R.to(dev))
+        G = torch.ones(H, K, N, dtype=torch.float32, device=dev)   # fp32 accumulate (beta = 1)
+        raw.gemm(raw.Operand(A.to(dev), 1, H * K, K), raw.Operand(R.to(dev), 1, H * N, N),
+                 raw.Operand(G, 0, N, K * N), K, N, M, batch=(H, 1), beta=1.0)
+        outs[str(dev)] = (C, Z, D, G)
+    torch.cuda.synchronize()
+    for name, g, c in zip("CZDG", outs[str(cuda)], outs["cpu"]):
+        _close(g, c, 5e-2, 3e-2, f"batched epilogue {name}")
+
+
+def test_gemm_oob_rejected(cuda):
+    A = torch.zeros(64 * 64, dtype=BF, device=cuda)
+    B = torch.zeros(64 * 64, dtype=BF, device=cuda)
+    C = torch.zeros(64 * 64, dtype=BF, device=cuda)
+    with pytest.raises(Exception):
+        raw.gemm(raw.Operand(A, 0, 64), raw.Operand(B, 0, 64), raw.Operand(C, 0, 64), 128, 64, 64)
+
+
+# ----------------------------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("D", [32, 64, 128])
+@pytest.mark.parametrize("S,causal", [(128, True), (200, True), (256, False), (64, True)])
+def test_attention_fwd_bwd(cuda, D, S, causal):
+    torch.manual_seed(D + S)
+    B, H = 2, 3
+    ld = H * D
+    scale = D ** -0.5
+    q, k, v, do = [(torch.randn(B * S * ld) * 0.8).to(BF) for _ in range(4)]
+    res = {}
+    for dev in ("cpu", cuda):
+        t = [x.to(dev) for x in (q, k, v, do)]
+        o = torch.zeros(B * S * ld, dtype=BF, device=dev)
+        lse = torch.zeros(B * H * S, dtype=torch.float32, device=dev)
+        raw.attn_fwd(t[0], t[1], t[2], o, lse, B, S, H, D, ld, scale, causal)
+        dq, dk, dv = [torch.zeros(B * S * ld, dtype=BF, device=dev) for _ in range(3)]
+        delta = torch.zeros(B * H * S, dtype=torch.float32, device=dev)
+        raw.attn_bwd(t[0], t[1], t[2], o, t[3], lse, delta, dq, dk, dv, B, S, H, D, ld, scale, causal)
+        res[str(dev)] = (o, lse, dq, dk, dv)
+    torch.cuda.synchronize()
+    for name, g, c in zip(["o", "lse", "dq", "dk", "dv"], res[str(cuda)], res["cpu"]):
+        _close(g, c, 3e-2, 3e-2, f"attention D={D} S={S} causal={causal} {name}")
+
+
+# ----------------------------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("F_,groups", [(2048, 1), (128, 16), (64, 1), (1000, 1)])
+def test_norm(cuda, F_, groups):
+    torch.manual_seed(F_)
+    rows = 96 * groups
+    x = (torch.randn(rows * F_) * 2 + 0.3).to(BF)
+    dy = torch.randn(rows * F_).to(BF)
+    sc = torch.randn(groups * F_) * 0.1 + 1
+    sh = torch.randn(groups * F_) * 0.1
+    res = {}
+    for dev in ("cpu", cuda):
+        y = torch.zeros(rows * F_, dtype=BF, device=dev)
+        st = torch.zeros(2 * rows, device=dev)
+        raw.norm_fwd(x.to(dev), sc.to(dev), sh.to(dev), y, st, rows, F_, groups)
+        dx = torch.zeros(rows * F_, dtype=BF, device=dev)
+        dsc = torch.zeros(groups * F_, device=dev)
+        dsh = torch.zeros(groups * F_, device=dev)
+        raw.norm_bwd(x.to(dev), dy.to(dev), sc.to(dev), st, dx, dsc, dsh, rows, F_, groups)
+        res[str(dev)] = (y, st, dx, dsc, dsh)
+    torch.cuda.synchronize()
+    for name, g, c in zip(["y", "stats", "dx", "dscale", "dshift"], res[str(cuda)], res["cpu"]):
+        _close(g, c, 3e-2, 2e-2, f"norm F={F_} {name}")
+
+
+@pytest.mark.parametrize("op,act", [("act", "gelu"), ("act", "relu"), ("act_bwd", "gelu"), ("act_bwd", "mish"),
+                                    ("act", "silu"), ("act", "lecun_tanh"), ("add", None), ("axpby", None),
+                                    ("mul", None), ("dropout", None), ("act_bwd", "softsign")])
+def test_elementwise(cuda, op, act):
+    torch.manual_seed(7)
+    n = 4096 + 8
+    x = torch.randn(n).to(BF)
+    z = torch.randn(n).to(BF)
+    out = {}
+    for dev in ("cpu", cuda):
+        y = torch.zeros(n, dtype=BF, device=dev)
+        raw.elementwise(op, x.to(dev), y, z=z.to(dev), act=act, alpha=0.7, beta=-1.3, seed=1234, keep=0.8)
+        out[str(dev)] = y
+    torch.cuda.synchronize()
+    _close(out[str(cuda)], out["cpu"], 2e-2, 2e-2, f"{op}/{act}")
+
+
+def test_xent(cuda):
+    torch.manual_seed(11)
+    rows, V, Vp = 64, 1000, 1024
+    logits = (torch.randn(rows * Vp) * 3).to(BF)
+    tgt = torch.randint(0, V, (rows,), dtype=torch.int32)
+    res = {}
+    for dev in ("cpu", cuda):
+        lse, loss, hit = [torch.zeros(rows, device=dev) for _ in range(3)]
+        raw.xent_fwd(logits.to(dev), tgt.to(dev), lse, loss, hit, rows, V, Vp, 1e-4)
+        g = torch.zeros(rows * Vp, dtype=BF, device=dev)
+        raw.xent_bwd(logits.to(dev), tgt.to(dev), lse, g, None, 1.0 / rows, rows, V, Vp, 1e-4)
+        res[str(dev)] = (lse, loss, hit, g)
+    torch.cuda.synchronize()
+    for name, g, c in zip(["lse", "loss", "hit", "grad"], res[str(cuda)], res["cpu"]):
+        _close(g, c, 2e-2, 1e-2, f"xent {name}")
+
+
+def test_gather_scatter(cuda):
+    torch.manual_seed(5)
+    V, Fd, T = 300, 64, 1000
+    table = torch.randn(V * Fd).to(BF)
+    idx = torch.randint(0, V, (T,), dtype=torch.int32)
+    dy = torch.randn(T * Fd).to(BF)
+    res = {}
+    for dev in ("cpu", cuda):
+        out = torch.zeros(T * Fd, dtype=BF, device=dev)
+        raw.gather(idx.to(dev), table.to(dev), out, T, Fd, V)
+        dt = torch.zeros(V * Fd, device=dev)
+        raw.scatter_add(idx.to(dev), dy.to(dev), dt, T, Fd, V)
+        res[str(dev)] = (out, dt)
+    torch.cuda.synchronize()
+    _close(res[str(cuda)][0], res["cpu"][0], 0, 0, "gather")
+    _close(res[str(cuda)][1], res["cpu"][1], 1e-3, 1e-3, "scatter_add")
+
+
+def test_cumsum(cuda):
+    torch.manual_seed(9)
+    x = torch.randn(2, 50, 3, 8).to(BF)
+    for rev, mean, grad in [(False, False, False), (True, True, True), (False, True, False)]:
+        out = {}
+        for dev in ("cpu", cuda):
+            y = torch.zeros_like(x, device=dev)
+            raw.cumsum(x.to(dev), y, 2, 50, 24, rev, mean, grad)
+            out[str(dev)] = y
+        torch.cuda.synchronize()
+        _close(out[str(cuda)], out["cpu"], 5e-2, 2e-2, f"cumsum {rev}{mean}{grad}")
