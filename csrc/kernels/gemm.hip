@@ -16,6 +16,7 @@
 // consecutive output columns (8-byte bf16 / 16-byte fp32 stores). Block ids are remapped XCD-aware (T1) and
 // grouped 8 tiles along M so blocks that share an XCD share A panels in its L2.
 #include "common.h"
+#include <stdlib.h>
 
 namespace {
 
@@ -239,7 +240,202 @@ hipError_t launch(const GemmArgs& a, int batch, hipStream_t stream) {
   return hipGetLastError();
 }
 
+
+// ================================================================================================================
+// 256x256x64 tile, 8 waves (2 M x 4 N, 128x64 per wave), staged by direct global->LDS DMA
+// (global_load_lds_dwordx4: each wave-instruction writes 1 KiB of LDS lane-linearly). The XOR swizzle of the LDS
+// image is applied to the per-lane SOURCE address (cdna guide §5.4 rule 21), the ds_read side applies the same
+// XOR. Two LDS stages (2 x 64 KiB), one barrier per K-step; 1 block per CU. Requires K % 64 == 0; rows/columns
+// beyond M/N are clamped to valid memory (their results are never stored).
+constexpr int BM2 = 256, BN2 = 256, NT2 = 512;
+constexpr int IMG2 = 256 * 64 * 2;  // 32 KiB per operand image
+
+__device__ __forceinline__ void glds16(const bf16_t* src, char* lds_base) {
+  __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
+                                   (void __attribute__((address_space(3)))*)lds_base, 16, 0, 0);
+}
+
+template <int T>
+__device__ __forceinline__ void stage256(char* img, const bf16_t* X, long long ld, int r0, int R, int k0, int wave,
+                                         int lane) {
+#pragma unroll
+  for (int rd = 0; rd < 4; ++rd) {
+    const int j = wave * 4 + rd;           // 1 KiB piece of the 32 KiB image
+    const bf16_t* src;
+    if (T == 0) {                          // [256 rows][64 k], 128-B rows, 8 rows per piece
+      const int rr = j * 8 + (lane >> 3), p = lane & 7;
+      const int c = p ^ ((rr >> 1) & 7);
+      const int row = min(r0 + rr, R - 1);
+      src = X + (long long)row * ld + k0 + c * 8;
+    } else {                               // [64 k][256 rows], 512-B rows, 2 k-rows per piece
+      const int kr = j * 2 + (lane >> 5), p = lane & 31;
+      const int c = p ^ kswz(kr);
+      const int col = min(r0 + c * 8, R - 8);
+      src = X + (long long)(k0 + kr) * ld + col;
+    }
+    glds16(src, img + j * 1024);
+  }
+}
+
+template <int T>
+__device__ __forceinline__ bf16x8_t read_frag256(const char* lds, int rbase, int kk, int lane) {
+  if (T == 0) {
+    const int r = rbase + (lane & 15);
+    const int c = kk * 4 + (lane >> 4);
+    return *reinterpret_cast<const bf16x8_t*>(lds + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
+  } else {
+    const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, pp = i16 & 3;
+    const int c = (rbase + 4 * pp) >> 3;
+    const int k0 = kk * 32 + 8 * g + q;
+    const int k1 = k0 + 4;
+    const int off0 = k0 * 512 + ((c ^ kswz(k0)) << 4) + ((pp & 1) << 3);
+    const int off1 = k1 * 512 + ((c ^ kswz(k1)) << 4) + ((pp & 1) << 3);
+    s16x4_t v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4_t, lds + off0));
+    s16x4_t v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4_t, lds + off1));
+    s16x8_t v = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+    return __builtin_bit_cast(bf16x8_t, v);
+  }
+}
+
+template <bool OUT_F32>
+__device__ __forceinline__ void epilogue_store(const GemmArgs& p, long long idx, float (&v)[4]) {
+  if (OUT_F32) {
+    float* C = reinterpret_cast<float*>(p.C) + idx;
+    if (p.beta != 0.f) {
+      float4 o = *reinterpret_cast<const float4*>(C);
+      v[0] += p.beta * o.x; v[1] += p.beta * o.y; v[2] += p.beta * o.z; v[3] += p.beta * o.w;
+    }
+    if (p.R) {
+      float4 r = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(p.R) + idx);
+      v[0] += r.x; v[1] += r.y; v[2] += r.z; v[3] += r.w;
+    }
+    if (p.act) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) v[t] = act_fwd(p.act, v[t]);
+    }
+    *reinterpret_cast<float4*>(C) = make_float4(v[0], v[1], v[2], v[3]);
+  } else {
+    if (p.R) {
+      uint2 r = *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16_t*>(p.R) + idx);
+      v[0] += bf2f(r.x & 0xffff); v[1] += bf2f(r.x >> 16); v[2] += bf2f(r.y & 0xffff); v[3] += bf2f(r.y >> 16);
+    }
+    if (p.mode == 1) {
+      uint2 z = *reinterpret_cast<const uint2*>(p.Zin + idx);
+      v[0] *= act_grad(p.act, bf2f(z.x & 0xffff)); v[1] *= act_grad(p.act, bf2f(z.x >> 16));
+      v[2] *= act_grad(p.act, bf2f(z.y & 0xffff)); v[3] *= act_grad(p.act, bf2f(z.y >> 16));
+    } else {
+      if (p.Zout) {
+        *reinterpret_cast<uint2*>(p.Zout + idx) = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+      }
+      if (p.act) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) v[t] = act_fwd(p.act, v[t]);
+      }
+    }
+    *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.C) + idx) =
+        make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+  }
+}
+
+template <int A_T, int B_T, bool OUT_F32>
+__global__ __launch_bounds__(NT2, 1) void gemm256_kernel(GemmArgs p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  int bid = blockIdx.x;
+  {
+    const int nwg = gridDim.x, xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+    bid = base + (bid >> 3);
+  }
+  const int GROUP = 4;
+  const int per_group = GROUP * p.tiles_n;
+  const int first_m = (bid / per_group) * GROUP;
+  const int gsz = min(p.tiles_m - first_m, GROUP);
+  const int tm = first_m + (bid % per_group) % gsz;
+  const int tn = (bid % per_group) / gsz;
+  const int m0 = tm * BM2, n0 = tn * BN2;
+  const int b1 = blockIdx.y / p.nb2, b2 = blockIdx.y % p.nb2;
+  const bf16_t* A = p.A + b1 * p.a_s1 + b2 * p.a_s2;
+  const bf16_t* B = p.B + b1 * p.b_s1 + b2 * p.b_s2;
+
+  f32x4_t acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = p.K / BK;
+  stage256<A_T>(smem, A, p.lda, m0, p.M, 0, wave, lane);
+  stage256<B_T>(smem + IMG2, B, p.ldb, n0, p.N, 0, wave, lane);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int s = kt & 1;
+    if (kt + 1 < nk) {
+      char* nxt = smem + (s ^ 1) * 2 * IMG2;
+      stage256<A_T>(nxt, A, p.lda, m0, p.M, (kt + 1) * BK, wave, lane);
+      stage256<B_T>(nxt + IMG2, B, p.ldb, n0, p.N, (kt + 1) * BK, wave, lane);
+    }
+    const char* ca = smem + s * 2 * IMG2;
+    const char* cb = ca + IMG2;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8_t bfr[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = read_frag256<B_T>(cb, wn * 64 + j * 16, kk, lane);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const bf16x8_t af = read_frag256<A_T>(ca, wm * 128 + i * 16, kk, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af, acc[i][j], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+  const long long coff = b1 * p.c_s1 + b2 * p.c_s2;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = m0 + wm * 128 + i * 16 + (lane & 15);
+    if (m >= p.M) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
+      if (n >= p.N) continue;
+      float v[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) v[t] = p.alpha * acc[i][j][t];
+      epilogue_store<OUT_F32>(p, coff + (long long)m * p.ldc + n, v);
+    }
+  }
+}
+
+template <int A_T, int B_T, bool F32>
+hipError_t launch256(GemmArgs a, int batch, hipStream_t stream) {
+  a.tiles_m = (a.M + BM2 - 1) / BM2;
+  a.tiles_n = (a.N + BN2 - 1) / BN2;
+  dim3 grid(a.tiles_m * a.tiles_n, batch);
+  const size_t lds = 4 * IMG2;
+  auto k = gemm256_kernel<A_T, B_T, F32>;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr = true;
+  }
+  hipLaunchKernelGGL(k, grid, dim3(NT2), lds, stream, a);
+  return hipGetLastError();
+}
+
 }  // namespace
+
+static bool getenv_big() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("OBST_GEMM_BIG");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v == 1;
+}
 
 struct ObstGemmDesc {
   const void* A; const void* B; void* C; const void* R; void* Zout; const void* Zin;
@@ -269,6 +465,21 @@ OBST_API int obst_gemm(const ObstGemmDesc* d, hipStream_t stream) {
   a.alpha = d->alpha; a.beta = d->beta; a.act = d->act; a.mode = d->mode;
   const int batch = d->batch1 * d->batch2;
   hipError_t e;
+  // big-tile path: needs K % 64 == 0, M/N >= 256 and enough 256x256 tiles to fill the 256 CUs twice
+  const long long big_tiles = (long long)((d->M + 255) / 256) * ((d->N + 255) / 256) * batch;
+  const bool big = getenv_big() && d->K % 64 == 0 && d->M >= 256 && d->N >= 256 && big_tiles >= 512 &&
+                   (d->a_t == 0 || d->M % 8 == 0) && (d->b_t == 0 || d->N % 8 == 0);
+  if (big) {
+#define OBST_GEMM256_CASE(AT, BT, F)                               \
+    if (d->a_t == AT && d->b_t == BT && (d->out_f32 != 0) == F) {  \
+      e = launch256<AT, BT, F>(a, batch, stream);                    \
+      return e == hipSuccess ? 0 : (int)e;                           \
+    }
+    OBST_GEMM256_CASE(0, 0, false) OBST_GEMM256_CASE(0, 1, false) OBST_GEMM256_CASE(1, 0, false)
+    OBST_GEMM256_CASE(1, 1, false) OBST_GEMM256_CASE(0, 0, true) OBST_GEMM256_CASE(0, 1, true)
+    OBST_GEMM256_CASE(1, 0, true) OBST_GEMM256_CASE(1, 1, true)
+#undef OBST_GEMM256_CASE
+  }
 #define OBST_GEMM_CASE(AT, BT, F)                                   \
   if (d->a_t == AT && d->b_t == BT && (d->out_f32 != 0) == F) {    \
     e = launch<AT, BT, F>(a, batch, stream);                         \

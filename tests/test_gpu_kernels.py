@@ -196,3 +196,21 @@ def test_cumsum(cuda):
             out[str(dev)] = y
         torch.cuda.synchronize()
         _close(out[str(cuda)], out["cpu"], 5e-2, 2e-2, f"cumsum {rev}{mean}{grad}")
+
+
+@pytest.mark.parametrize("a_t,b_t", [(0, 0), (0, 1), (1, 0), (1, 1)])
+def test_gemm_big_tile(cuda, a_t, b_t):
+    """shapes that take the 256x256 LDS-DMA kernel (>= 512 tiles), incl. ragged M/N edges"""
+    torch.manual_seed(21 + a_t + 2 * b_t)
+    M, N, K = 4160, 8128, 128
+    A = (torch.randn(M * K) * 0.5).to(BF)
+    B = (torch.randn(N * K) * 0.5).to(BF)
+    lda = K if a_t == 0 else M
+    ldb = K if b_t == 0 else N
+    av = A.view(M, K) if a_t == 0 else A.view(K, M).t()
+    bv = B.view(N, K).t() if b_t == 0 else B.view(K, N)
+    ref = av.float() @ bv.float()
+    Cg = torch.zeros(M * N, dtype=BF, device=cuda)
+    raw.gemm(raw.Operand(A.to(cuda), a_t, lda), raw.Operand(B.to(cuda), b_t, ldb), raw.Operand(Cg, 0, N), M, N, K)
+    torch.cuda.synchronize()
+    _close(Cg.view(M, N), ref, 4e-2, 2e-2, f"gemm256 {a_t}{b_t}")
