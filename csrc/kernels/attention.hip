@@ -40,19 +40,36 @@ __device__ __forceinline__ int lds_off(int row, int chunk) {
   return row * Geo<D>::ROWB + ((chunk ^ swz<D>(row)) << 4);
 }
 
-// stage ROWS x D bf16 rows (token-major, row stride ld) into LDS; rows >= nvalid are zero-filled
+// stage ROWS x D bf16 rows (token-major, row stride ld) into an LDS image with direct global->LDS DMA
+// (global_load_lds_dwordx4, one 1 KiB piece per wave-instruction, lane-linear in LDS): the per-lane SOURCE chunk is
+// pre-swizzled so the image matches lds_off(). Rows >= nvalid are clamped to the last valid row (masked later).
 template <int D, int ROWS>
 __device__ __forceinline__ void stage_rows(char* lds, const bf16_t* g, long long ld, int nvalid, int tid) {
-  constexpr int CH = ROWS * Geo<D>::CPR;
+  constexpr int CPR = Geo<D>::CPR;
+  constexpr int PIECES = ROWS * CPR * 16 / 1024;   // 1 KiB pieces in the image
+  constexpr int RPP = 64 / CPR;                    // rows per piece
+  const int wave = tid >> 6, lane = tid & 63;
+  const int last = nvalid - 1;
 #pragma unroll
-  for (int i = 0; i < (CH + NTH - 1) / NTH; ++i) {
-    const int q = tid + i * NTH;
-    if (CH % NTH == 0 || q < CH) {
-      const int row = q / Geo<D>::CPR, c = q % Geo<D>::CPR;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (row < nvalid) v = *reinterpret_cast<const uint4*>(g + row * ld + c * 8);
-      *reinterpret_cast<uint4*>(lds + lds_off<D>(row, c)) = v;
+  for (int i = 0; i < (PIECES + 3) / 4; ++i) {
+    const int j = wave + 4 * i;
+    if (PIECES % 4 == 0 || j < PIECES) {
+      const int row = j * RPP + lane / CPR;
+      const int p = lane % CPR;
+      const int c = p ^ swz<D>(row);
+      const int srow = row < last ? row : last;
+      __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(g + srow * ld + c * 8),
+                                       (void __attribute__((address_space(3)))*)(lds + j * 1024), 16, 0, 0);
     }
+  }
+}
+
+// 4-byte values (lse / delta rows) for `n` consecutive queries, n*4 <= 1 KiB: one piece from wave 0
+__device__ __forceinline__ void stage_f32(char* lds, const float* g, int n, int nvalid, int tid) {
+  if (tid < n) {
+    const int q = tid < nvalid ? tid : nvalid - 1;
+    __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(g + q),
+                                     (void __attribute__((address_space(3)))*)(lds), 4, 0, 0);
   }
 }
 
@@ -106,13 +123,13 @@ struct AttnArgs {
 };
 
 // ----------------------------------------------------------------------------------------------------------------
-// forward: block = 128 queries of one (b, h); wave w owns queries q0 + 32w + [0, 32)
+// forward: block = 128 queries of one (b, h); wave w owns queries q0 + 32w + [0, 32). K/V tiles of 64 keys are
+// double-buffered in LDS and filled by LDS-DMA one tile ahead; one barrier per tile.
 template <int D>
 __global__ __launch_bounds__(NTH, 2) void attn_fwd_kernel(AttnArgs a) {
   using G = Geo<D>;
+  constexpr int TILE = 64 * G::ROWB;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* sK = smem;
-  char* sV = smem + 64 * G::ROWB;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, i = lane & 15;
   const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
   const int qblk = blockIdx.x * 128;
@@ -120,6 +137,11 @@ __global__ __launch_bounds__(NTH, 2) void attn_fwd_kernel(AttnArgs a) {
   const bf16_t* Qb = a.Q + (long long)b * a.S * a.ld + h * D;
   const bf16_t* Kb = a.K + (long long)b * a.S * a.ld + h * D;
   const bf16_t* Vb = a.V + (long long)b * a.S * a.ld + h * D;
+
+  const int kend = a.causal ? min(a.S, qblk + 128) : a.S;
+  const int nkb = (kend + 63) / 64;
+  stage_rows<D, 64>(smem, Kb, a.ld, a.S, tid);
+  stage_rows<D, 64>(smem + TILE, Vb, a.ld, a.S, tid);
 
   bf16x8_t qf[2][G::DS];
 #pragma unroll
@@ -133,77 +155,88 @@ __global__ __launch_bounds__(NTH, 2) void attn_fwd_kernel(AttnArgs a) {
   for (int dt = 0; dt < G::DT; ++dt) o[dt][0] = o[dt][1] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   float m[2] = {NEG_BIG, NEG_BIG}, l[2] = {0.f, 0.f};
   const float c2 = a.scale * LOG2E;
+  __syncthreads();
 
-  const int kend = a.causal ? min(a.S, qblk + 128) : a.S;
-  for (int k0 = 0; k0 < kend; k0 += 64) {
-    __syncthreads();
-    stage_rows<D, 64>(sK, Kb + (long long)k0 * a.ld, a.ld, a.S - k0, tid);
-    stage_rows<D, 64>(sV, Vb + (long long)k0 * a.ld, a.ld, a.S - k0, tid);
-    __syncthreads();
-    if (a.causal && k0 > qw + 31) continue;  // wave-uniform: every key of this block is in this wave's future
-    f32x4_t s[2][4];
+  for (int kb = 0; kb < nkb; ++kb) {
+    const int k0 = kb * 64;
+    const char* sK = smem + (kb & 1) * 2 * TILE;
+    const char* sV = sK + TILE;
+    if (kb + 1 < nkb) {
+      char* nxt = smem + ((kb + 1) & 1) * 2 * TILE;
+      stage_rows<D, 64>(nxt, Kb + (long long)(k0 + 64) * a.ld, a.ld, a.S - k0 - 64, tid);
+      stage_rows<D, 64>(nxt + TILE, Vb + (long long)(k0 + 64) * a.ld, a.ld, a.S - k0 - 64, tid);
+    }
+    if (!(a.causal && k0 > qw + 31)) {  // wave-uniform: skip blocks entirely in this wave's future
+      f32x4_t s[2][4];
 #pragma unroll
-    for (int qt = 0; qt < 2; ++qt)
+      for (int qt = 0; qt < 2; ++qt)
 #pragma unroll
-      for (int kt = 0; kt < 4; ++kt) s[qt][kt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        for (int kt = 0; kt < 4; ++kt) s[qt][kt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int ds = 0; ds < G::DS; ++ds) {
+      for (int ds = 0; ds < G::DS; ++ds) {
 #pragma unroll
-      for (int kt = 0; kt < 4; ++kt) {
-        bf16x8_t kf = row_frag<D>(sK, kt * 16, ds, lane);
+        for (int kt = 0; kt < 4; ++kt) {
+          bf16x8_t kf = row_frag<D>(sK, kt * 16, ds, lane);
 #pragma unroll
-        for (int qt = 0; qt < 2; ++qt) s[qt][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[qt][ds], s[qt][kt], 0, 0, 0);
+          for (int qt = 0; qt < 2; ++qt)
+            s[qt][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[qt][ds], s[qt][kt], 0, 0, 0);
+        }
+      }
+      const bool need_mask = (a.causal && k0 + 63 > qw) || k0 + 64 > a.S;
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) {
+        const int q = qw + qt * 16 + i;
+        float mx = NEG_BIG;
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+          for (int v = 0; v < 4; ++v) {
+            float x = s[qt][kt][v] * c2;
+            if (need_mask) {
+              const int key = k0 + kt * 16 + 4 * g + v;
+              if (key >= a.S || (a.causal && key > q)) x = -INFINITY;
+            }
+            s[qt][kt][v] = x;
+            mx = fmaxf(mx, x);
+          }
+        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        const float mn = fmaxf(m[qt], mx);
+        const float alpha = exp2f(m[qt] - mn);
+        float rs = 0.f;
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+          for (int v = 0; v < 4; ++v) {
+            const float p = exp2f(s[qt][kt][v] - mn);
+            s[qt][kt][v] = p;
+            rs += p;
+          }
+        rs += __shfl_xor(rs, 16, 64);
+        rs += __shfl_xor(rs, 32, 64);
+        l[qt] = l[qt] * alpha + rs;
+        m[qt] = mn;
+#pragma unroll
+        for (int dt = 0; dt < G::DT; ++dt) o[dt][qt] *= alpha;
+      }
+      bf16x8_t pf[2][2];
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) {
+        pf[qt][0] = pack_p(s[qt][0], s[qt][1]);
+        pf[qt][1] = pack_p(s[qt][2], s[qt][3]);
+      }
+#pragma unroll
+      for (int dt = 0; dt < G::DT; ++dt) {
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+          bf16x8_t vf = tr_frag<D>(sV, st * 32, dt * 16, lane);
+#pragma unroll
+          for (int qt = 0; qt < 2; ++qt)
+            o[dt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[qt][st], o[dt][qt], 0, 0, 0);
+        }
       }
     }
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt) {
-      const int q = qw + qt * 16 + i;
-      float mx = NEG_BIG;
-#pragma unroll
-      for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {
-          const int key = k0 + kt * 16 + 4 * g + v;
-          float x = s[qt][kt][v] * c2;
-          if (key >= a.S || (a.causal && key > q)) x = -INFINITY;
-          s[qt][kt][v] = x;
-          mx = fmaxf(mx, x);
-        }
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mn = fmaxf(m[qt], mx);
-      const float alpha = exp2f(m[qt] - mn);
-      float rs = 0.f;
-#pragma unroll
-      for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {
-          const float p = exp2f(s[qt][kt][v] - mn);
-          s[qt][kt][v] = p;
-          rs += p;
-        }
-      rs += __shfl_xor(rs, 16, 64);
-      rs += __shfl_xor(rs, 32, 64);
-      l[qt] = l[qt] * alpha + rs;
-      m[qt] = mn;
-#pragma unroll
-      for (int dt = 0; dt < G::DT; ++dt) o[dt][qt] *= alpha;
-    }
-    bf16x8_t pf[2][2];
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt) {
-      pf[qt][0] = pack_p(s[qt][0], s[qt][1]);
-      pf[qt][1] = pack_p(s[qt][2], s[qt][3]);
-    }
-#pragma unroll
-    for (int dt = 0; dt < G::DT; ++dt) {
-#pragma unroll
-      for (int st = 0; st < 2; ++st) {
-        bf16x8_t vf = tr_frag<D>(sV, st * 32, dt * 16, lane);
-#pragma unroll
-        for (int qt = 0; qt < 2; ++qt) o[dt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[qt][st], o[dt][qt], 0, 0, 0);
-      }
-    }
+    __syncthreads();
   }
   // epilogue: lane holds O[q = qw + qt*16 + i][d = dt*16 + 4g + v]
   bf16_t* Ob = a.Oout + (long long)b * a.S * a.ld + h * D;
@@ -246,18 +279,21 @@ __global__ __launch_bounds__(NTH) void attn_delta_kernel(AttnArgs a) {
 }
 
 // ----------------------------------------------------------------------------------------------------------------
-// dQ: block = 128 queries; recompute Sᵀ, Pᵀ, dPᵀ = V·dOᵀ, dSᵀ, dQᵀ += Kᵀ·dSᵀ
+// dQ: block = 128 queries; recompute Sᵀ, Pᵀ, dPᵀ = V·dOᵀ, dSᵀ, dQᵀ += Kᵀ·dSᵀ. K/V tiles double-buffered (LDS-DMA).
 template <int D>
 __global__ __launch_bounds__(NTH, 2) void attn_bwd_dq_kernel(AttnArgs a) {
   using G = Geo<D>;
+  constexpr int TILE = 64 * G::ROWB;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* sK = smem;
-  char* sV = smem + 64 * G::ROWB;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, i = lane & 15;
   const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
   const int qblk = blockIdx.x * 128;
   const int qw = qblk + w * 32;
   const long long base = (long long)b * a.S * a.ld + h * D;
+  const int kend = a.causal ? min(a.S, qblk + 128) : a.S;
+  const int nkb = (kend + 63) / 64;
+  stage_rows<D, 64>(smem, a.K + base, a.ld, a.S, tid);
+  stage_rows<D, 64>(smem + TILE, a.V + base, a.ld, a.S, tid);
 
   bf16x8_t qf[2][G::DS], df[2][G::DS];
   float lse2[2], dlt[2];
@@ -278,58 +314,68 @@ __global__ __launch_bounds__(NTH, 2) void attn_bwd_dq_kernel(AttnArgs a) {
 #pragma unroll
   for (int dt = 0; dt < G::DT; ++dt) acc[dt][0] = acc[dt][1] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   const float c2 = a.scale * LOG2E;
-  const int kend = a.causal ? min(a.S, qblk + 128) : a.S;
-  for (int k0 = 0; k0 < kend; k0 += 64) {
-    __syncthreads();
-    stage_rows<D, 64>(sK, a.K + base + (long long)k0 * a.ld, a.ld, a.S - k0, tid);
-    stage_rows<D, 64>(sV, a.V + base + (long long)k0 * a.ld, a.ld, a.S - k0, tid);
-    __syncthreads();
-    if (a.causal && k0 > qw + 31) continue;
-    f32x4_t s[2][4], dp[2][4];
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt)
-#pragma unroll
-      for (int kt = 0; kt < 4; ++kt) s[qt][kt] = dp[qt][kt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int ds = 0; ds < G::DS; ++ds) {
-#pragma unroll
-      for (int kt = 0; kt < 4; ++kt) {
-        bf16x8_t kf = row_frag<D>(sK, kt * 16, ds, lane);
-        bf16x8_t vf = row_frag<D>(sV, kt * 16, ds, lane);
-#pragma unroll
-        for (int qt = 0; qt < 2; ++qt) {
-          s[qt][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[qt][ds], s[qt][kt], 0, 0, 0);
-          dp[qt][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, df[qt][ds], dp[qt][kt], 0, 0, 0);
-        }
-      }
+  __syncthreads();
+  for (int kb = 0; kb < nkb; ++kb) {
+    const int k0 = kb * 64;
+    const char* sK = smem + (kb & 1) * 2 * TILE;
+    const char* sV = sK + TILE;
+    if (kb + 1 < nkb) {
+      char* nxt = smem + ((kb + 1) & 1) * 2 * TILE;
+      stage_rows<D, 64>(nxt, a.K + base + (long long)(k0 + 64) * a.ld, a.ld, a.S - k0 - 64, tid);
+      stage_rows<D, 64>(nxt + TILE, a.V + base + (long long)(k0 + 64) * a.ld, a.ld, a.S - k0 - 64, tid);
     }
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt) {
-      const int q = qw + qt * 16 + i;
-#pragma unroll
-      for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {
-          const int key = k0 + kt * 16 + 4 * g + v;
-          float p = exp2f(s[qt][kt][v] * c2 - lse2[qt]);
-          if (key >= a.S || (a.causal && key > q)) p = 0.f;
-          s[qt][kt][v] = p * (dp[qt][kt][v] - dlt[qt]);
-        }
-    }
-    bf16x8_t sf[2][2];
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt) {
-      sf[qt][0] = pack_p(s[qt][0], s[qt][1]);
-      sf[qt][1] = pack_p(s[qt][2], s[qt][3]);
-    }
-#pragma unroll
-    for (int dt = 0; dt < G::DT; ++dt)
+    if (!(a.causal && k0 > qw + 31)) {
+      const bool need_mask = (a.causal && k0 + 63 > qw) || k0 + 64 > a.S;
+      // two 32-key halves: P needs only the stored LSE, so no state crosses the halves
 #pragma unroll
       for (int st = 0; st < 2; ++st) {
-        bf16x8_t kf = tr_frag<D>(sK, st * 32, dt * 16, lane);
+        f32x4_t s[2][2], dp[2][2];
 #pragma unroll
-        for (int qt = 0; qt < 2; ++qt) acc[dt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, sf[qt][st], acc[dt][qt], 0, 0, 0);
+        for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk) s[qt][kk] = dp[qt][kk] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ds = 0; ds < G::DS; ++ds) {
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk) {
+            const int kt = 2 * st + kk;
+            bf16x8_t kf = row_frag<D>(sK, kt * 16, ds, lane);
+            bf16x8_t vf = row_frag<D>(sV, kt * 16, ds, lane);
+#pragma unroll
+            for (int qt = 0; qt < 2; ++qt) {
+              s[qt][kk] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[qt][ds], s[qt][kk], 0, 0, 0);
+              dp[qt][kk] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, df[qt][ds], dp[qt][kk], 0, 0, 0);
+            }
+          }
+        }
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt) {
+          const int q = qw + qt * 16 + i;
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+              float p = exp2f(s[qt][kk][v] * c2 - lse2[qt]);
+              if (need_mask) {
+                const int key = k0 + (2 * st + kk) * 16 + 4 * g + v;
+                if (key >= a.S || (a.causal && key > q)) p = 0.f;
+              }
+              s[qt][kk][v] = p * (dp[qt][kk][v] - dlt[qt]);
+            }
+        }
+        bf16x8_t sf[2];
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt) sf[qt] = pack_p(s[qt][0], s[qt][1]);
+#pragma unroll
+        for (int dt = 0; dt < G::DT; ++dt) {
+          bf16x8_t kf = tr_frag<D>(sK, st * 32, dt * 16, lane);
+#pragma unroll
+          for (int qt = 0; qt < 2; ++qt)
+            acc[dt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, sf[qt], acc[dt][qt], 0, 0, 0);
+        }
       }
+    }
+    __syncthreads();
   }
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
@@ -346,21 +392,31 @@ __global__ __launch_bounds__(NTH, 2) void attn_bwd_dq_kernel(AttnArgs a) {
 }
 
 // ----------------------------------------------------------------------------------------------------------------
-// dK/dV: block = 64 keys; wave w owns keys k0 + 16w + [0,16). Loop over 32-query chunks staged in LDS.
+// dK/dV: block = 64 keys; wave w owns keys k0 + 16w + [0,16). Loop over 64-query chunks (Q, dO, lse, delta)
+// double-buffered in LDS via LDS-DMA.
 template <int D>
 __global__ __launch_bounds__(NTH, 2) void attn_bwd_dkv_kernel(AttnArgs a) {
   using G = Geo<D>;
+  constexpr int QC = 64;
+  constexpr int TILE = QC * G::ROWB;
+  constexpr int STAGE = 2 * TILE + 2 * 256;   // Q, dO, lse[64], delta[64]
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* sQ = smem;
-  char* sD = smem + 32 * G::ROWB;
-  float* sL = reinterpret_cast<float*>(smem + 64 * G::ROWB);
-  float* sDl = sL + 32;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, i = lane & 15;
   const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
   const int kblk = blockIdx.x * 64;
   const int kw = kblk + w * 16;
   const long long base = (long long)b * a.S * a.ld + h * D;
   const long long sbase = ((long long)b * a.H + h) * a.S;
+  const int qstart = a.causal ? (kblk / QC) * QC : 0;
+  const int nqc = (a.S - qstart + QC - 1) / QC;
+
+  auto stage = [&](char* st, int q0) {
+    stage_rows<D, QC>(st, a.Q + base + (long long)q0 * a.ld, a.ld, a.S - q0, tid);
+    stage_rows<D, QC>(st + TILE, a.dO + base + (long long)q0 * a.ld, a.ld, a.S - q0, tid);
+    stage_f32(st + 2 * TILE, a.LSE + sbase + q0, QC, a.S - q0, tid);
+    stage_f32(st + 2 * TILE + 256, a.delta + sbase + q0, QC, a.S - q0, tid);
+  };
+  if (nqc > 0) stage(smem, qstart);
 
   bf16x8_t kf[G::DS], vf[G::DS];
   {
@@ -376,55 +432,59 @@ __global__ __launch_bounds__(NTH, 2) void attn_bwd_dkv_kernel(AttnArgs a) {
 #pragma unroll
   for (int dt = 0; dt < G::DT; ++dt) dk[dt] = dv[dt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   const float c2 = a.scale * LOG2E;
-  const int qstart = a.causal ? (kblk / 32) * 32 : 0;
-  for (int q0 = qstart; q0 < a.S; q0 += 32) {
-    __syncthreads();
-    stage_rows<D, 32>(sQ, a.Q + base + (long long)q0 * a.ld, a.ld, a.S - q0, tid);
-    stage_rows<D, 32>(sD, a.dO + base + (long long)q0 * a.ld, a.ld, a.S - q0, tid);
-    if (tid < 32) {
-      const int q = q0 + tid;
-      sL[tid] = q < a.S ? a.LSE[sbase + q] * LOG2E : 0.f;
-      sDl[tid] = q < a.S ? a.delta[sbase + q] : 0.f;
-    }
-    __syncthreads();
-    if (a.causal && q0 + 31 < kw) continue;  // every query of this chunk precedes this wave's keys
-    f32x4_t s[2], dp[2];
-    s[0] = s[1] = dp[0] = dp[1] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int ds = 0; ds < G::DS; ++ds) {
-#pragma unroll
-      for (int qt = 0; qt < 2; ++qt) {
-        bf16x8_t qa = row_frag<D>(sQ, qt * 16, ds, lane);
-        bf16x8_t da = row_frag<D>(sD, qt * 16, ds, lane);
-        s[qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa, kf[ds], s[qt], 0, 0, 0);
-        dp[qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, vf[ds], dp[qt], 0, 0, 0);
-      }
-    }
-    // s[qt][v] = S[q = q0 + qt*16 + 4g + v][key = kw + i]
-    f32x4_t p[2], dsv[2];
-    const int key = kw + i;
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt)
-#pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const int ql = qt * 16 + 4 * g + v;
-        const int q = q0 + ql;
-        float pv = exp2f(s[qt][v] * c2 - sL[ql]);
-        if (q >= a.S || key >= a.S || (a.causal && key > q)) pv = 0.f;
-        p[qt][v] = pv;
-        dsv[qt][v] = pv * (dp[qt][v] - sDl[ql]);
-      }
-    const bf16x8_t pb = pack_p(p[0], p[1]);
-    const bf16x8_t sb = pack_p(dsv[0], dsv[1]);
-#pragma unroll
-    for (int dt = 0; dt < G::DT; ++dt) {
-      bf16x8_t dot = tr_frag<D>(sD, 0, dt * 16, lane);
-      bf16x8_t qtr = tr_frag<D>(sQ, 0, dt * 16, lane);
-      dv[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dot, pb, dv[dt], 0, 0, 0);
-      dk[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qtr, sb, dk[dt], 0, 0, 0);
-    }
-  }
   const int key = kw + i;
+  __syncthreads();
+  for (int c = 0; c < nqc; ++c) {
+    const int q0 = qstart + c * QC;
+    const char* sQ = smem + (c & 1) * STAGE;
+    const char* sD = sQ + TILE;
+    const float* sL = reinterpret_cast<const float*>(sQ + 2 * TILE);
+    const float* sDl = sL + 64;
+    if (c + 1 < nqc) stage(smem + ((c + 1) & 1) * STAGE, q0 + QC);
+    if (!(a.causal && q0 + QC - 1 < kw)) {  // every query of this chunk precedes this wave's keys
+      f32x4_t s[4], dp[4];
+#pragma unroll
+      for (int qt = 0; qt < 4; ++qt) s[qt] = dp[qt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ds = 0; ds < G::DS; ++ds) {
+#pragma unroll
+        for (int qt = 0; qt < 4; ++qt) {
+          bf16x8_t qa = row_frag<D>(sQ, qt * 16, ds, lane);
+          bf16x8_t da = row_frag<D>(sD, qt * 16, ds, lane);
+          s[qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa, kf[ds], s[qt], 0, 0, 0);
+          dp[qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, vf[ds], dp[qt], 0, 0, 0);
+        }
+      }
+      // s[qt][v] = S[q = q0 + qt*16 + 4g + v][key]
+      const bool need_mask = (a.causal && q0 < kw + 15) || q0 + QC > a.S || kw + 16 > a.S;
+#pragma unroll
+      for (int qt = 0; qt < 4; ++qt)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int ql = qt * 16 + 4 * g + v;
+          float pv = exp2f(s[qt][v] * c2 - sL[ql] * LOG2E);
+          if (need_mask) {
+            const int q = q0 + ql;
+            if (q >= a.S || key >= a.S || (a.causal && key > q)) pv = 0.f;
+          }
+          s[qt][v] = pv;
+          dp[qt][v] = pv * (dp[qt][v] - sDl[ql]);
+        }
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        const bf16x8_t pb = pack_p(s[2 * st], s[2 * st + 1]);
+        const bf16x8_t sb = pack_p(dp[2 * st], dp[2 * st + 1]);
+#pragma unroll
+        for (int dt = 0; dt < G::DT; ++dt) {
+          bf16x8_t dot = tr_frag<D>(sD, st * 32, dt * 16, lane);
+          bf16x8_t qtr = tr_frag<D>(sQ, st * 32, dt * 16, lane);
+          dv[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dot, pb, dv[dt], 0, 0, 0);
+          dk[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qtr, sb, dk[dt], 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();
+  }
   if (key < a.S) {
 #pragma unroll
     for (int dt = 0; dt < G::DT; ++dt) {
@@ -441,7 +501,7 @@ __global__ __launch_bounds__(NTH, 2) void attn_bwd_dkv_kernel(AttnArgs a) {
 template <int D>
 int launch_fwd(const AttnArgs& a, hipStream_t st) {
   dim3 grid((a.S + 127) / 128, a.B * a.H);
-  hipLaunchKernelGGL(attn_fwd_kernel<D>, grid, dim3(NTH), 128 * Geo<D>::ROWB, st, a);
+  hipLaunchKernelGGL(attn_fwd_kernel<D>, grid, dim3(NTH), 4 * 64 * Geo<D>::ROWB, st, a);
   return (int)hipGetLastError();
 }
 
@@ -449,9 +509,9 @@ template <int D>
 int launch_bwd(const AttnArgs& a, hipStream_t st) {
   const long long rows = (long long)a.B * a.S * a.H;
   hipLaunchKernelGGL(attn_delta_kernel<D>, dim3((unsigned)((rows + 3) / 4)), dim3(NTH), 0, st, a);
-  hipLaunchKernelGGL(attn_bwd_dkv_kernel<D>, dim3((a.S + 63) / 64, a.B * a.H), dim3(NTH), 64 * Geo<D>::ROWB + 256,
-                     st, a);
-  hipLaunchKernelGGL(attn_bwd_dq_kernel<D>, dim3((a.S + 127) / 128, a.B * a.H), dim3(NTH), 128 * Geo<D>::ROWB, st, a);
+  hipLaunchKernelGGL(attn_bwd_dkv_kernel<D>, dim3((a.S + 63) / 64, a.B * a.H), dim3(NTH),
+                     2 * (2 * 64 * Geo<D>::ROWB + 512), st, a);
+  hipLaunchKernelGGL(attn_bwd_dq_kernel<D>, dim3((a.S + 127) / 128, a.B * a.H), dim3(NTH), 4 * 64 * Geo<D>::ROWB, st, a);
   return (int)hipGetLastError();
 }
 
