@@ -30,6 +30,7 @@ def run_layers(builder: Builder, layers: typing.List[str], x: Act, residual: typ
         args.fn_name = name
         args.fn_occurrence = seen.get(name, 0)
         seen[name] = args.fn_occurrence + 1
+        builder.shared.begin_layer((builder.config_idx, name, args.fn_occurrence))
         if idx == n and residual is not None and name in _FUSABLE_LAST:
             args.residual = residual
         with builder.scope(name + '_'):

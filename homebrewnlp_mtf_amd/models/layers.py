@@ -249,7 +249,9 @@ def group_linear(args: BlockArgs) -> Act:
     p = args.params
     new = [anonymize_dim(p.key_dim) if d == p.key_dim else d for d in p.feature_dims]
     out = linear(args('group'), p.feature_dims, new)
-    return Act(out.t.reshape([d.size for d in args.tensor.dims]), args.tensor.dims)
+    # the reference reshapes back to the input shape; for a head-less input (reduced_half_linear) that reshape is
+    # size-inconsistent in the reference, so here the head dim is kept and `_features_per_head` renamed back
+    return Act(out.t, [unanonymize_dim(d) if d.name == "_" + p.key_dim.name else d for d in out.dims])
 
 
 def sum_heads(args: BlockArgs) -> Act:

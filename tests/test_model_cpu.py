@@ -1,0 +1,252 @@
+"""CPU tests of the model layer: config derivations, the named-dim weight-shape rules, every layer of the block
+grammar, initialisation statistics (the reference's own tests: tests/basic_linear_square_test.py,
+tests/basic_pointwise_test.py, tests/variable_test.py), and exact fp64 gradient checks of every body variant."""
+import math
+
+import pytest
+import torch
+
+from homebrewnlp_mtf_amd.config import Dim, ModelParameter, load_config
+from homebrewnlp_mtf_amd.models import dims as D
+from homebrewnlp_mtf_amd.models.context import Act, BlockArgs, Builder
+from homebrewnlp_mtf_amd.models.model import Model, padded_vocab
+from homebrewnlp_mtf_amd.models.layers import LAYER_FUNCTIONS
+
+BASE = dict(model_mode="gpt", use_video=False, use_language=True, heads=2, features_per_head=8, depth=2,
+            sequence_length=8, train_batch_size=2, vocab_size=50, intermediate_feed_forward_multiplier=2,
+            memory_reduction_strategy="none", calculation_dtype="float32")
+
+
+# ---------------------------------------------------------------------------------------------------------------
+def test_config_derivations():
+    p = ModelParameter(dict(heads=8, features_per_head=256, intermediate_feed_forward_multiplier_multiplier=0.5, train_batch_size=8,
+                            group_linear_factor=2, use_video=False, sequence_length=2048))
+    assert p.features == 2048
+    assert p.intermediate[0].size == int(8 * 256 * (2 * 0.5 / 8))   # ref dataclass.py:221-234
+    assert p.feature_dims == [Dim("heads", 8), Dim("features_per_head", 256)]
+    assert p.language_token_per_frame == 2048
+    assert p["heads"] == 8                                          # A13 fixed
+    with pytest.raises(ValueError):
+        ModelParameter(dict(heads=8))                               # neither features nor features_per_head
+    assert p.resolve_mesh(8) == (8, 1)
+    p2 = ModelParameter(dict(heads=8, features_per_head=16, use_video=False, mesh={"dp": 4, "tp": 2},
+                             train_batch_size=8))
+    assert p2.resolve_mesh(8) == (4, 2)
+
+
+def test_shipped_configs_load():
+    for name in ("gpt_neo_125m_cpu", "gpt_neo_1.3b", "gpt_neo_2.7b", "gpt_neo_20b_scale", "ctx32_mixer",
+                 "big32_mixer", "group32_mixer"):
+        p = load_config(name)
+        assert p.features == p.heads * p.features_per_head
+
+
+def test_linear_shapes_rules():
+    p = ModelParameter(dict(heads=4, features_per_head=8, use_video=False, intermediate_feed_forward_multiplier=2))
+    x = [Dim("batch", 2), Dim("sequence", 8), p.head_dim, p.key_dim]
+    old, new = D.linear_shapes(p, [], x)
+    assert old == [p.head_dim, p.key_dim] and new == p.intermediate
+    old, new = D.linear_shapes(p, ["group"], x)      # block-diagonal over heads
+    assert old == [p.head_dim, p.key_dim]
+    assert new == [p.head_dim, Dim("_features_per_head", 16)]
+    xi = [Dim("batch", 2), Dim("sequence", 8), p.intermediate[0]]
+    old, new = D.linear_shapes(p, [], xi)
+    assert old == p.intermediate and new == [p.head_dim, p.key_dim]
+    old, new = D.linear_shapes(p, ["group"], xi)     # bottleneck 'mid:' with intermediate input
+    assert old == p.intermediate and new == [p.head_dim, Dim("_features_per_head", 16)]
+
+
+def test_gpt_neo_1_3b_parameter_count():
+    p = load_config("gpt_neo_1.3b")
+    b = Builder(p)
+    b.params.vocab_dim = Dim("vocab", padded_vocab(p))
+    m = Model.__new__(Model)
+    m.params, m.builder, m.dtype, m.local_batch = p, b, torch.bfloat16, 1
+    b.register, b.dtype = True, torch.bfloat16
+    with torch.no_grad():
+        m._forward(m._dummy_inputs("meta"))
+    n = b.store.global_numel()
+    assert 1.3e9 < n < 1.4e9, n     # 12 d^2 per layer x 24 + embeddings
+
+
+# ---------------------------------------------------------------------------------------------------------------
+LAYER_STRINGS = [
+    "feed_forward-in:relu", "feed_forward-in:gelu-in:glu", "feed_forward-in:silu-in:glu_add-in:norm",
+    "feed_forward-in:mixture_of_experts", "attention-dot_product-context", "attention-dot_product-embedded-absolute",
+    "attention-dot_product-positional-relative-shared_key_value", "attention-biased_attention_map-absolute-input_as_value",
+    "attention-biased_softmax-dot_product-context-absolute", "attention-dot_product-embedded-axial", "attention-scale_attention_map-dot_product-context-absolute",
+    "norm-group-shift-scale", "norm-shift-scale", "activation-lecun_tanh", "activation-mish", "rezero",
+    "dropout-dropout_rate0.1", "group_linear", "cumsum", "cummean",
+    "bottleneck_group_linear-in:relu-mid:relu-mid:norm-mid:shift-mid:scale-mid:features",
+    "reduced_half_linear", "product_key_memory", "feed_forward_product_key_memory-in:relu",
+    "split_path-add;norm-shift,feed_forward-in:relu;activation-gelu",
+]
+
+
+@pytest.mark.parametrize("layer", LAYER_STRINGS)
+def test_every_layer_forward_backward(layer):
+    cfg = dict(BASE, experts=4, block_config=[{"layer": [layer], "skip": True}])
+    m = Model(ModelParameter(cfg), "cpu")
+    x = torch.randint(0, 50, (2, 8, 1))
+    out = m(x, x)
+    out["loss"].backward()
+    m.store.fold_leaf_grads()
+    assert torch.isfinite(out["loss"])
+    assert torch.isfinite(m.store.grad).all()
+
+
+def test_layer_registry_complete():
+    ref = {'feed_forward', 'attention', 'cummean', 'cumsum', 'norm', 'rezero', 'activation', 'convolution', 'dropout',
+           'group_linear', 'split_path', 'feed_forward_product_key_memory', 'product_key_memory',
+           'reduced_half_linear', 'transpose_sequence_features', 'bottleneck_group_linear', 'sum_heads'}
+    assert ref == set(LAYER_FUNCTIONS)
+
+
+def test_convolution_disabled_like_reference():
+    cfg = dict(BASE, block_config=[{"layer": ["convolution-3"], "skip": True}])
+    with pytest.raises(ValueError):
+        Model(ModelParameter(cfg), "cpu")
+
+
+def test_shared_parameters_across_depth():
+    cfg = dict(BASE, depth=3, memory_reduction_strategy="revnet",
+               block_config=[{"layer": ["attention-biased_attention_map-absolute-input_as_value-shared"]},
+                             {"layer": ["feed_forward-in:relu"]}])
+    m = Model(ModelParameter(cfg), "cpu")
+    mixer = [n for n in m.store.order if "attention" in n]
+    ffn = [n for n in m.store.order if "feed_forward" in n]
+    assert len(mixer) == 1, mixer          # one map shared by all depths
+    assert len(ffn) == 3 * 2               # two linears per depth, not shared
+    assert m.builder.use_counts[mixer[0]] == 3
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# initialisation statistics (reference tests/variable_test.py, basic_linear_square_test.py)
+def test_orthogonal_linear_stack_preserves_std():
+    """group_linear's weight [heads, fph, fph'] is initialised as ONE orthogonal (heads*fph, fph') matrix (fan-in =
+    all `old` dims, ref backend.py:18-40,109) -- so a chain through the flattened weights preserves the norm."""
+    torch.manual_seed(0)
+    cfg = dict(BASE, heads=8, features_per_head=64, depth=6, sequence_length=64, scale_by_depth=False,
+               block_config=[{"layer": ["group_linear"]}])
+    m = Model(ModelParameter(cfg), "cpu")
+    names = [n for n in m.store.order if "body" in n]
+    assert len(names) == 6
+    for n in names:
+        w = m.store.master_view(n).reshape(8 * 64, 64)
+        assert torch.allclose(w.t() @ w, torch.eye(64), atol=1e-5)
+    x = torch.randn(4096, 8 * 64)
+    for n in names:
+        w = m.store.master_view(n).reshape(8 * 64, 64)
+        x = (x @ w).repeat(1, 8)     # broadcast back over heads
+    assert abs(x.std().item() - 1.0) < 0.05
+
+
+def test_orthogonal_is_orthogonal_and_scale_by_depth():
+    cfg = dict(BASE, heads=4, features_per_head=16, depth=4, scale_by_depth=True,
+               block_config=[{"layer": ["feed_forward-in:relu"]}])
+    m = Model(ModelParameter(cfg), "cpu")
+    w_in = m.store.master_view("gpt0/body0/0_0/feed_forward_0/linear0/orthogonal_var0").reshape(64, -1)
+    # every variable created by the block's last layer is divided by sqrt(depth) (quirk A3, ref backend.py:30):
+    # feed_forward is that layer, so both of its linears are orthogonal * 1/2
+    for w in (w_in, m.store.master_view("gpt0/body0/0_0/feed_forward_0/linear1/orthogonal_var0").reshape(-1, 64)):
+        s = torch.linalg.svdvals(w)
+        assert torch.allclose(s, torch.full_like(s, 1 / 2), atol=1e-4)
+    cfg["block_config"] = [{"layer": ["feed_forward-in:relu", "rezero"]}]
+    m = Model(ModelParameter(cfg), "cpu")
+    w = m.store.master_view("gpt0/body0/0_0/feed_forward_0/linear0/orthogonal_var0").reshape(64, -1)
+    s = torch.linalg.svdvals(w)
+    assert torch.allclose(s, torch.ones_like(s), atol=1e-4)
+
+
+def test_normal_init_statistics():
+    cfg = dict(BASE, heads=16, features_per_head=256, block_config=[{"layer": ["norm-shift-scale"]}])
+    m = Model(ModelParameter(cfg), "cpu")
+    scale = m.store.master_view("gpt0/body0/0_0/norm_0/norm0/normal_var0")
+    shift = m.store.master_view("gpt0/body0/0_0/norm_0/norm1/normal_var0")
+    assert abs(scale.mean().item() - 1) < 0.01 and abs(scale.std().item() - 0.02) < 0.002
+    assert abs(shift.mean().item()) < 0.01 and abs(shift.std().item() - 0.02) < 0.002
+
+
+def test_output_embedding_is_unit_vector_quirk_a2():
+    m = Model(ModelParameter(dict(BASE, block_config=[{"layer": ["feed_forward-in:relu"]}])), "cpu")
+    w = m.store.master_view("gpt0/output0/embed0/orthogonal_var0")
+    assert abs(w.norm().item() - 1.0) < 1e-4
+
+
+def test_rezero_starts_at_zero_and_dropout_rate():
+    cfg = dict(BASE, block_config=[{"layer": ["rezero"], "skip": False}])
+    m = Model(ModelParameter(cfg), "cpu")
+    assert m.store.master_view("gpt0/body0/0_0/rezero_0/rezero0/constant_var0").item() == 0.0
+    from homebrewnlp_mtf_amd.ops import functional as F
+    x = torch.ones(100000)
+    y = F.dropout(x, 0.7, seed=3)
+    assert abs((y == 0).float().mean().item() - 0.3) < 0.01
+    assert abs(y.mean().item() - 1.0) < 0.02
+
+
+# ---------------------------------------------------------------------------------------------------------------
+VARIANTS = {
+    "none": dict(block_config=[{"layer": ["norm-shift-scale", "attention-dot_product-context"], "skip": True},
+                               {"layer": ["norm-shift-scale", "feed_forward-in:gelu"], "skip": True}]),
+    "revnet": dict(memory_reduction_strategy="revnet",
+                   block_config=[{"layer": ["norm-shift-scale", "attention-dot_product-context"]},
+                                 {"layer": ["norm-shift-scale-group", "feed_forward-in:gelu"]}]),
+    "momentum": dict(memory_reduction_strategy="momentum",
+                     block_config=[{"layer": ["norm-shift-scale-group", "feed_forward-in:relu-in:glu"]}]),
+    "checkpoint": dict(memory_reduction_strategy="checkpoint",
+                       block_config=[{"layer": ["norm-shift-scale", "feed_forward-in:tanh"], "skip": True}]),
+    "mixer": dict(memory_reduction_strategy="revnet",
+                  block_config=[{"layer": ["norm-shift-scale-group",
+                                           "attention-biased_attention_map-absolute-input_as_value-shared",
+                                           "rezero"]},
+                                {"layer": ["bottleneck_group_linear-in:relu-mid:relu-mid:norm-mid:shift-mid:scale"]}]),
+}
+
+
+@pytest.mark.parametrize("variant", sorted(VARIANTS))
+def test_gradients_match_finite_differences_fp64(variant):
+    torch.manual_seed(0)
+    cfg = dict(BASE, calculation_dtype="float64", **VARIANTS[variant])
+    m = Model(ModelParameter(cfg), "cpu")
+    st = m.store
+    st.master = st.master.double()
+    st.grad = st.grad.double()
+    st.compute = st.master
+    st._leaves = {}
+    st.master.copy_(torch.randn_like(st.master) * 0.3)
+    x = torch.randint(0, 50, (2, 8, 1))
+    y = torch.randint(0, 50, (2, 8, 1))
+    out = m(x, y)
+    out["loss"].backward()
+    st.fold_leaf_grads()
+    g = st.grad.clone()
+    for name in st.order:
+        s = st.specs[name]
+        d = torch.zeros_like(st.master)
+        d[s.offset:s.offset + s.numel] = torch.randn(s.numel, dtype=torch.float64)
+        eps = 1e-5
+        with torch.no_grad():
+            base = st.master.clone()
+            st.master.copy_(base + eps * d)
+            lp = float(m(x, y)["loss"])
+            st.master.copy_(base - eps * d)
+            lm = float(m(x, y)["loss"])
+            st.master.copy_(base)
+        fd = (lp - lm) / (2 * eps)
+        an = float((g * d).sum())
+        assert abs(fd - an) <= 1e-5 + 1e-4 * max(abs(fd), abs(an)), f"{variant}/{name}: fd={fd} analytic={an}"
+
+
+def test_gpt_cpu_plumbing_trains():
+    """BASELINE config 1 in miniature: the GPT-Neo-small CPU path learns a fixed batch"""
+    from homebrewnlp_mtf_amd.run.trainer import Trainer
+    p = load_config("gpt_neo_125m_cpu", {"depth": 2, "heads": 4, "features_per_head": 16, "vocab_size": 128,
+                                         "sequence_length": 32, "learning_rate_config": {},
+                                         "learning_rate": 0.003, "optimizer": "adam-learning_rate"})
+    tr = Trainer(p, "cpu")
+    toks = torch.randint(0, 128, (4, 33, 1), generator=torch.Generator().manual_seed(1))
+    b = {"token_x": toks[:, :-1], "token_y": toks[:, 1:]}
+    first = float(tr.step(b)["loss"])
+    for _ in range(30):
+        last = float(tr.step(b)["loss"])
+    assert last < first - 1.0, (first, last)
