@@ -23,7 +23,7 @@ build/runtime/%.o: csrc/runtime/%.cpp $(wildcard csrc/runtime/*.h)
 	g++ $(CXXFLAGS) -c $< -o $@
 
 $(PKG)/_runtime.so: $(ROBJ)
-	g++ $(CXXFLAGS) -shared -o $@ $(ROBJ) -lpthread
+	g++ $(CXXFLAGS) -shared -o $@ $(ROBJ) -lpthread -lz -ldl
 
 clean:
 	rm -rf build $(PKG)/_kernels.so $(PKG)/_runtime.so
