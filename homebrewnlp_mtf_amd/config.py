@@ -97,6 +97,11 @@ _DEFAULTS: typing.Dict[str, typing.Any] = dict(
     allreduce_dtype="float32",   # dtype gradients travel in over RCCL
     use_hip_graphs=False,        # capture the optimizer step in a hipGraph
     log_every=10, metrics_path=None, pad_vocab_to=128,
+    tokenizer_path=None,         # tokenizers JSON for vocab_size > 256 (the reference downloads GPT-2's)
+    web_host="0.0.0.0", web_port=62220, serve_max_batch=8,
+    heartbeat_path=None,         # file touched every logged step (watchdog liveness)
+    tensorboard=False,           # also write TensorBoard scalars (if the tensorboard package is importable)
+    dist_timeout_s=1800,         # torch.distributed collective timeout
 )
 
 # keys the reference reads nowhere outside dataclass.py -- accepted silently

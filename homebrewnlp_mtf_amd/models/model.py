@@ -75,7 +75,23 @@ class Model:
 
     __call__ = forward
 
-    def _forward(self, batch: dict) -> typing.Dict[str, torch.Tensor]:
+    @torch.no_grad()
+    def logits(self, token_x: torch.Tensor, positions: typing.Optional[torch.Tensor] = None,
+               frame: typing.Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Inference forward (ref src/run/inference.py:77-85 ``build`` inside the sampling loop).
+
+        Returns fp32 logits [batch, sequence, patch, vocab_size]; with ``positions`` ([batch] int) only the
+        hidden state of those positions goes through the output projection -> [batch, 1, patch, vocab_size]
+        (exact for causal bodies; the reference computes every position and then uses one)."""
+        self.builder.train = False
+        self._positions = positions
+        try:
+            out = self._forward({"token_x": token_x, "token_y": None, "frame": frame}, logits_only=True)
+        finally:
+            self._positions = None
+        return out[..., :self.params.vocab_size].float()
+
+    def _forward(self, batch: dict, logits_only: bool = False):
         b = self.builder
         p = b.params
         b.begin_forward()
@@ -84,8 +100,19 @@ class Model:
                 src, vid_tgt = self._input(batch)
             with b.scope("body"):
                 out = run_body(b, src, p.memory_reduction_strategy, p.block_configs, p.depth)
+            pos = getattr(self, "_positions", None)
+            if logits_only and pos is not None and not p.output_block_configs:
+                if out.dims[0].name != "batch" or out.dims[1].name != "sequence":
+                    raise NotImplementedError(f"position slicing needs [batch, sequence, ...], got {out.dims}")
+                t = out.t[torch.arange(out.t.shape[0], device=out.t.device), pos.to(out.t.device).long()]
+                out = Act(t.unsqueeze(1).contiguous(), [out.dims[0], Dim("sequence", 1)] + list(out.dims[2:]))
             with b.scope("output"):
                 frame_out, token_out = self._output(out)
+            if logits_only:
+                if pos is not None and p.output_block_configs:
+                    idx = pos.to(token_out.t.device).long()
+                    return token_out.t[torch.arange(token_out.t.shape[0], device=idx.device), idx].unsqueeze(1)
+                return token_out.t
             with b.scope("loss"):
                 return self._loss(frame_out, token_out, batch, vid_tgt)
 

@@ -125,6 +125,7 @@ class FusedOptimizer:
         self.sm3_total = max(off, 1)
         packed = []
         self.fac = {}
+        self.tinfo = []
         for ti, (offset, numel, ndim, shape) in enumerate(recs):
             flags = 0
             n = names[ti]
@@ -144,6 +145,7 @@ class FusedOptimizer:
                 foff = fac_total
                 fac_total += frows + fcols
             packed.append(struct.pack("<qqii4i4qqii", offset, numel, ndim, flags, *dims, *so, foff, frows, fcols))
+            self.tinfo.append((offset, numel, shape, [sm3_off.get((ti, d)) for d in range(ndim)], foff, frows, fcols))
         self.ntensors = len(packed)
         self.nchunks = len(chunks)
         self.t_tensors = torch.tensor(bytearray(b"".join(packed)), dtype=torch.uint8, device=dev)
@@ -258,6 +260,44 @@ class FusedOptimizer:
             self.flip = 1 - self.flip
 
     # ------------------------------------------------------------------------------------------------------------
+    def named_slots(self) -> typing.Dict[str, torch.Tensor]:
+        """views of the optimizer state per variable, keyed like the reference's slot variables
+        (``<var>/<optimizer string with : -> _>/<slot>``, src/optimizer/backend.py:23-25) and like
+        ``ReferenceOptimizer.state_dict`` -- so checkpoints move between the fused and the reference optimizer."""
+        chain = {n for n, _ in parse_chain(self.chain)}
+        opt_str = self.chain.replace(':', '_')
+        out: typing.Dict[str, torch.Tensor] = {}
+        for ti, name in enumerate(self.names):
+            offset, numel, shape, sm3o, foff, frows, fcols = self.tinfo[ti]
+            full = list(self.store.specs[name].local_shape)
+            key = f"{name}/{opt_str}/"
+            flat = lambda buf: buf[offset:offset + numel].view(full)  # noqa: E731
+            if not full:       # 0-dim: sm3/novograd/adam all fall back to scalar adam state
+                if chain & {"sm3", "novograd", "adam"}:
+                    out[key + "exp_avg_p1"] = self.sstate[ti * 4:ti * 4 + 1].view(())
+                    out[key + "exp_avg_p2"] = self.sstate[ti * 4 + 1:ti * 4 + 2].view(())
+                if "momentum" in chain:
+                    out[key + "momentum"] = flat(self.mom)
+                continue
+            if "sm3" in chain:
+                for d, o in enumerate(sm3o):
+                    out[key + f"dim{d}"] = self.sm3[self.flip][o:o + shape[d]]
+            if "adam" in chain:
+                out[key + "exp_avg_p1"] = flat(self.adam_m)
+                out[key + "exp_avg_p2"] = flat(self.adam_v)
+            if "novograd" in chain:
+                out[key + "exp_avg_p1"] = flat(self.mom)
+                out[key + "exp_avg_p2"] = self.sstate[ti * 4 + 2:ti * 4 + 3].view(())
+            elif "momentum" in chain:
+                out[key + "momentum"] = flat(self.mom)
+            if "adafactor" in chain:
+                if frows:
+                    out[key + "af_rows"] = self.af_state[foff:foff + frows]
+                    out[key + "af_cols"] = self.af_state[foff + frows:foff + frows + fcols]
+                else:
+                    out[key + "af_v"] = flat(self.adam_v)
+        return out
+
     def state_dict(self) -> typing.Dict[str, torch.Tensor]:
         out = {"flip": torch.tensor(self.flip)}
         for k in ("mom", "adam_m", "adam_v", "af_state", "sstate"):

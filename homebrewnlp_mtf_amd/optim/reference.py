@@ -184,6 +184,10 @@ class ReferenceOptimizer:
                 out[f"{name}/{opt_str}/{k}"] = v   # ref slot naming src/optimizer/backend.py:23-25
         return out
 
+    def named_slots(self) -> typing.Dict[str, torch.Tensor]:
+        """every slot tensor under its reference name; slots are created lazily, so untouched ones are absent"""
+        return self.state_dict()
+
     def load_state_dict(self, sd: typing.Dict[str, torch.Tensor]):
         opt_str = self.params.optimizer.replace(':', '_')
         for key, v in sd.items():

@@ -1,0 +1,220 @@
+"""Autoregressive sampling and the interactive run modes (ref src/run/inference.py:15-133, src/interface.py;
+SURVEY C08/C31, §3.4).
+
+Sampling semantics follow the reference's language loop: for ``position`` in ``[initial_pos, end_iterations)``
+the model reads the whole (causal) context, the logits get Gumbel noise scaled by the temperature
+(``logits - T * log(-log(u))``, u ~ U[1e-9, 1)), ``argmax`` over the vocabulary, and the prediction made at
+``position - 1`` is written into ``token_x[position]`` (the shift-by-one of inference.py:94-96). Only the one needed
+position goes through the output projection (``Model.logits(positions=...)``), which gives the same tokens as the
+reference's full-sequence projection for causal bodies.
+
+``CompletionEngine`` replaces the reference's Manager-dict ``InterfaceWrapper`` (interface.py:231-280): requests go
+into an in-process queue and one GPU thread serves them in batches of up to ``max_batch`` prompts.
+"""
+from __future__ import annotations
+
+import queue
+import random
+import threading
+import typing
+
+import numpy as np
+import torch
+
+from ..config import ModelParameter
+from ..utils.log import log
+
+
+class ContextExhaustedError(ValueError):
+    pass
+
+
+class InvalidTokenError(ValueError):
+    pass
+
+
+# ---------------------------------------------------------------------------------------------------------------
+class Tokenizer:
+    """Byte/char-level for vocabularies <= 256 (the reference's `chr`/`ord` path), otherwise a local HF
+    ``tokenizers`` JSON file (``params.tokenizer_path``; the reference downloads GPT-2's, impossible offline)."""
+
+    def __init__(self, params: ModelParameter):
+        self.params = params
+        self.bpe = None
+        path = getattr(params, "tokenizer_path", None)
+        if params.vocab_size > 256:
+            if not path:
+                raise ValueError("vocab_size > 256 needs `tokenizer_path` (a tokenizers JSON file)")
+            from tokenizers import Tokenizer as HFTokenizer
+            self.bpe = HFTokenizer.from_file(path)
+
+    def encode(self, text: str) -> typing.List[int]:
+        if self.bpe is None:
+            return list(text.encode()) if self.params.vocab_size == 256 else [ord(c) for c in text]
+        return self.bpe.encode(text).ids
+
+    def decode(self, tokens: typing.Sequence[int]) -> str:
+        if self.bpe is None:
+            if self.params.vocab_size == 256:
+                return bytes(int(t) & 0xff for t in tokens).decode(errors="replace")
+            return "".join(chr(int(t)) for t in tokens)
+        return self.bpe.decode([int(t) for t in tokens])
+
+
+def process_token_output(tokens: np.ndarray, padding_token: int = -1,
+                         tokenizer: typing.Optional[Tokenizer] = None) -> typing.List[str]:
+    """ref interface.py:61-88 (without argmax: callers pass token ids)"""
+    tokens = np.asarray(tokens).reshape(tokens.shape[0], -1)
+    out = []
+    for row in tokens:
+        row = row.tolist()
+        if padding_token > -1 and padding_token in row:
+            row = row[:row.index(padding_token)]
+        if tokenizer is None or tokenizer.bpe is None:
+            out.append("".join(chr(t) if t > 31 and t != 127 and t != 10 else " " for t in row))
+        else:
+            out.append(tokenizer.decode(row))
+    return out
+
+
+# ---------------------------------------------------------------------------------------------------------------
+class Sampler:
+    def __init__(self, model, params: ModelParameter, device):
+        self.model, self.params, self.device = model, params, torch.device(device)
+        self.gen = torch.Generator(device=self.device)
+        self.gen.manual_seed(int(params.seed) if getattr(params, "seed", None) is not None else 0)
+
+    @torch.no_grad()
+    def sample(self, token_x: torch.Tensor, initial_pos, temperature, end_iterations) -> torch.Tensor:
+        """token_x [B, S, patch] int; per-row initial position / temperature / end (scalars or [B] tensors)."""
+        x = token_x.to(self.device, torch.int32).clone()
+        B, S = x.shape[0], x.shape[1]
+
+        def vec(v, dtype):
+            t = torch.as_tensor(v, dtype=dtype, device=self.device)
+            return t.expand(B).clone() if t.dim() == 0 else t.clone()
+        pos = vec(initial_pos, torch.long).clamp(min=1)
+        temp = vec(temperature, torch.float32)
+        end = vec(end_iterations, torch.long).clamp(max=S)
+        rows = torch.arange(B, device=self.device)
+        while bool((pos < end).any()):
+            active = pos < end
+            src = (pos - 1).clamp(max=S - 1)
+            logits = self.model.logits(x, positions=src)[:, 0]          # [B, patch, V]
+            u = torch.rand(logits.shape, generator=self.gen, device=self.device) * (1 - 1e-9) + 1e-9
+            noisy = logits - temp.view(B, 1, 1) * torch.log(-torch.log(u))
+            pred = noisy.argmax(-1).to(torch.int32)                      # [B, patch]
+            wpos = pos.clamp(max=S - 1)
+            cur = x[rows, wpos]
+            x[rows, wpos] = torch.where(active.view(B, 1), pred, cur)
+            pos = torch.where(active, pos + 1, pos)
+        return x
+
+
+# ---------------------------------------------------------------------------------------------------------------
+class CompletionEngine:
+    """Thread-safe completion service over one model (``complete`` blocks; ``submit`` returns a future)."""
+
+    def __init__(self, sampler: Sampler, params: ModelParameter, max_batch: int = 8):
+        self.sampler, self.params, self.max_batch = sampler, params, max_batch
+        self.q: "queue.Queue" = queue.Queue()
+        self._stop = False
+        self.thread = threading.Thread(target=self._loop, daemon=True)
+        self.thread.start()
+
+    def submit(self, query: typing.List[int], temperature: float, response_len: int):
+        p = self.params
+        iter_pos = len(query)
+        if iter_pos >= p.sequence_length:
+            raise ContextExhaustedError(f"context of {iter_pos} tokens exceeds {p.sequence_length}")
+        if query and (max(query) >= p.vocab_size or min(query) < 0):
+            raise InvalidTokenError(f"tokens must be in [0, {p.vocab_size})")
+        fill = [random.randint(0, p.vocab_size - 1) for _ in range(p.sequence_length - iter_pos)]
+        fut: "queue.Queue" = queue.Queue(maxsize=1)
+        end = min(response_len + iter_pos, p.sequence_length)
+        self.q.put((query + fill, iter_pos, float(temperature), end, fut))
+        return fut
+
+    def complete(self, query, temperature: float, response_len: int) -> np.ndarray:
+        out = self.submit(query, temperature, response_len).get()
+        if isinstance(out, BaseException):
+            raise out
+        return out
+
+    def _loop(self):
+        while not self._stop:
+            try:
+                first = self.q.get(timeout=0.1)
+            except queue.Empty:
+                continue
+            items = [first]
+            while len(items) < self.max_batch:
+                try:
+                    items.append(self.q.get_nowait())
+                except queue.Empty:
+                    break
+            try:
+                p = self.params
+                toks = torch.tensor([it[0] for it in items], dtype=torch.int32).view(len(items), p.sequence_length, 1)
+                out = self.sampler.sample(toks, [it[1] for it in items], [it[2] for it in items],
+                                          [it[3] for it in items]).cpu().numpy()
+                for it, row in zip(items, out):
+                    it[4].put(row.reshape(-1)[it[1]:it[3]].astype(np.int64))
+            except BaseException as e:  # noqa: BLE001 -- handed to the waiting caller
+                for it in items:
+                    it[4].put(e)
+
+    def close(self):
+        self._stop = True
+        self.thread.join(timeout=5)
+
+
+# ---------------------------------------------------------------------------------------------------------------
+def run_query(engine: CompletionEngine, tokenizer: Tokenizer, params: ModelParameter, stream=None):
+    """`query` run mode: prompts from stdin (ref interface.py:177-220)"""
+    import sys
+    stream = stream or sys.stdin
+    while True:
+        print("Enter Query:", flush=True)
+        line = stream.readline()
+        if not line:
+            return
+        q = tokenizer.encode(line.rstrip("\n"))
+        if len(q) >= params.sequence_length:
+            print(f"Query is too long: at most {params.sequence_length - 1} tokens, got {len(q)}.")
+            continue
+        out = engine.complete(q, params.sampling_temperature, params.sequence_length)
+        print("Response:")
+        print(process_token_output(out[None], tokenizer=tokenizer)[0].rstrip(), flush=True)
+
+
+def run_debug(engine: CompletionEngine, params: ModelParameter) -> typing.List[float]:
+    """`debug` run mode: the same random prompt N times at temperature 0 must give identical completions
+    (ref interface.py:283-302)."""
+    scores = []
+    for idx in range(params.num_of_sample):
+        query = [random.randint(0, params.vocab_size - 1) for _ in range(min(32, params.sequence_length - 8))]
+        futs = [engine.submit(query, 0.0, params.sequence_length)
+                for _ in range(int(params.equal_debugging_items_per_check))]
+        base, *rest = [f.get() for f in futs]
+        score = float(np.mean([np.mean(np.equal(base, o)) * 100 for o in rest])) if rest else 100.0
+        print(f"test:{idx} similarity score: {score:6.2f}%")
+        scores.append(score)
+    return scores
+
+
+def run_sample(sampler: Sampler, tokenizer: Tokenizer, params: ModelParameter, batches: typing.Iterable[dict]):
+    """`sample` / `debug_old` run modes: complete dataset prompts after `initial_autoregressive_position`
+    (ref interface.py:101-174)."""
+    pos = int(params.initial_autoregressive_position)
+    for i, b in enumerate(batches):
+        if i >= params.num_of_sample:
+            return
+        x = b["token_x"][:1]
+        out = sampler.sample(x, pos, params.sampling_temperature, params.sequence_length).cpu().numpy()
+        print(f"sample_idx: {i}")
+        print("Prompt:")
+        print(process_token_output(x[:, :pos - 1].cpu().numpy(), tokenizer=tokenizer)[0])
+        print("Output:")
+        print(process_token_output(out[:, pos:], tokenizer=tokenizer)[0].rstrip(), flush=True)
+        log(f"sample {i} done")

@@ -46,6 +46,8 @@ def write_blobs(path: str, bufs: typing.Sequence[Buffer], threads: typing.Option
 
 def read_blobs(path: str, bufs: typing.Sequence[Buffer], meta: dict, verify: bool = True,
                threads: typing.Optional[int] = None):
+    """``meta``: {"offsets": [...], "sizes": [...], "crcs": [...]} for exactly these blobs, in order (the CRC list is
+    the concatenation of every blob's piece CRCs, see ``piece_crcs``)."""
     n = len(bufs)
     ps = [_ptr_size(b) for b in bufs]
     sizes = np.array(meta["sizes"], dtype=np.int64)
@@ -58,3 +60,14 @@ def read_blobs(path: str, bufs: typing.Sequence[Buffer], meta: dict, verify: boo
                              crcs.ctypes.data_as(N.P_u32) if crcs is not None else None, threads or _threads())
     if r != 0:
         N.fail("checkpoint read")
+
+
+def piece_crcs(meta: dict) -> typing.List[typing.List[int]]:
+    """splits the flat CRC list of ``write_blobs`` into one list per blob"""
+    chunk = int(N.lib().rt_blob_chunk())
+    out, k = [], 0
+    for s in meta["sizes"]:
+        c = max(1, -(-int(s) // chunk))
+        out.append(meta["crcs"][k:k + c])
+        k += c
+    return out
