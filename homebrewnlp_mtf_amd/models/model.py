@@ -38,6 +38,9 @@ class Model:
         self.params = params
         self.device = torch.device(device)
         self.dtype = dtype or params.torch_calculation_dtype
+        if self.device.type == "cuda" and self.dtype != torch.bfloat16:
+            raise ValueError(f"the gfx950 kernels compute in bfloat16 (fp32 accumulate); calculation_dtype "
+                             f"{self.dtype} is only supported by the CPU oracle")
         self.builder = Builder(params, tp_rank, tp_size)
         p = self.builder.params
         p.vocab_dim = Dim("vocab", padded_vocab(params))

@@ -1,0 +1,100 @@
+"""Runtime paths on the GPU: fused-optimizer checkpoints restore into the reference optimizer (same slot names),
+sampling through the HIP kernels, the pinned-memory side-stream feeder."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from homebrewnlp_mtf_amd.config import ModelParameter
+from homebrewnlp_mtf_amd.parallel import state as pstate
+from homebrewnlp_mtf_amd.run.trainer import Trainer
+from homebrewnlp_mtf_amd.utils import checkpoint as ckpt
+
+pytestmark = pytest.mark.gpu
+
+CFG = dict(model_mode="gpt", use_video=False, use_language=True, heads=4, features_per_head=64, depth=2,
+           sequence_length=128, train_batch_size=2, vocab_size=500, intermediate_feed_forward_multiplier=2,
+           memory_reduction_strategy="revnet", learning_rate=0.01, calculation_dtype="bfloat16",
+           optimizer="adaptive_clip:0.003-sm3-momentum:0.9:1:1-learning_rate",
+           block_config=[{"layer": ["norm-shift-scale", "attention-dot_product-context"]},
+                         {"layer": ["norm-shift-scale", "feed_forward-in:gelu"]}])
+
+
+def _batch(seed, device):
+    g = torch.Generator().manual_seed(seed)
+    t = torch.randint(0, 500, (2, 129, 1), generator=g)
+    return {"token_x": t[:, :-1].contiguous().to(device), "token_y": t[:, 1:].contiguous().to(device)}
+
+
+@pytest.mark.parametrize("optimizer", ["adaptive_clip:0.003-sm3-momentum:0.9:1:1-learning_rate",
+                                       "adam-learning_rate", "adafactor-learning_rate"])
+def test_fused_checkpoint_restores_into_reference_optimizer(cuda, tmp_path, optimizer):
+    pstate.set_mesh(pstate.Mesh())
+    p = ModelParameter(dict(CFG, optimizer=optimizer))
+    torch.manual_seed(0)
+    fused = Trainer(p, cuda)                       # fused HIP optimizer
+    assert type(fused.opt).__name__ == "FusedOptimizer"
+    for i in range(3):
+        fused.step(_batch(i, cuda))
+    ckpt.save(fused, str(tmp_path), 3)
+    ref = Trainer(p, cuda, use_fused=False)        # torch reference optimizer, lazily created slots
+    ckpt.restore(ref, ckpt.latest(str(tmp_path)))
+    assert torch.equal(ref.store.master, fused.store.master)
+    live = fused.opt.named_slots()
+    got = ref.opt.named_slots()
+    assert set(live) == set(got)
+    for k in live:
+        assert torch.equal(live[k].float().cpu(), got[k].float().cpu()), k
+    # one more step with identical grads: both optimizers land on nearly the same weights
+    fused.step(_batch(7, cuda))
+    ref.step(_batch(7, cuda))
+    diff = (fused.store.master - ref.store.master).abs().max().item()
+    assert diff < 1e-3, diff
+    # and back: reference checkpoint → fused optimizer
+    ckpt.save(ref, str(tmp_path / "b"), 4)
+    fused2 = Trainer(p, cuda)
+    ckpt.restore(fused2, ckpt.latest(str(tmp_path / "b")))
+    for k, v in fused2.opt.named_slots().items():
+        assert torch.equal(v.float().cpu(), got[k].float().cpu()), k
+
+
+def test_gpu_sampling_greedy_is_reproducible(cuda):
+    from homebrewnlp_mtf_amd.models.model import Model
+    from homebrewnlp_mtf_amd.run.infer import Sampler
+    pstate.set_mesh(pstate.Mesh())
+    torch.manual_seed(0)
+    p = ModelParameter(dict(CFG, train_batch_size=1, memory_reduction_strategy="none"))
+    m = Model(p, cuda)
+    x = torch.randint(0, 500, (3, 128, 1), device=cuda)
+    s = Sampler(m, p, cuda)
+    a = s.sample(x, 100, 0.0, 128)
+    b = s.sample(x, 100, 0.0, 128)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+    assert torch.equal(a[:, :100], x[:, :100].int())
+    # the last written token is the argmax of the full-sequence logits at position 126
+    full = m.logits(a)
+    assert torch.equal(full[:, 126].argmax(-1).int(), a[:, 127])
+
+
+def test_device_feeder_pinned_side_stream(cuda, tmp_path):
+    from homebrewnlp_mtf_amd.data import pipeline as P
+    from homebrewnlp_mtf_amd.data import tfrecord as T
+    rng = np.random.default_rng(0)
+    for i in range(3):
+        with T.TFRecordWriter(str(tmp_path / f"int64_x_{i:_>6d}_1_2000.tfrecord")) as w:
+            w.write_example({"text": rng.integers(0, 500, 2000)})
+    p = ModelParameter(dict(CFG, dataset_configs=[{"type": "text", "path": str(tmp_path / "*.tfrecord"),
+                                                   "weight": 1}], interleaved_datasets=2))
+    cpu = P.text_input(p, 2, 0, 1, "cpu", prefetch=2)
+    gpu = P.text_input(p, 2, 0, 1, cuda, prefetch=3)
+    for _ in range(10):
+        a, b = cpu.next(), gpu.next()
+        if a is None:
+            assert b is None
+            break
+        assert b["token_x"].device.type == "cuda"
+        assert torch.equal(a["token_x"], b["token_x"].cpu()) and torch.equal(a["token_y"], b["token_y"].cpu())
+    cpu.close()
+    gpu.close()
