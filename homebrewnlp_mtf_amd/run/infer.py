@@ -58,7 +58,7 @@ class Tokenizer:
             if self.params.vocab_size == 256:
                 return bytes(int(t) & 0xff for t in tokens).decode(errors="replace")
             return "".join(chr(int(t)) for t in tokens)
-        return self.bpe.decode([int(t) for t in tokens])
+        return self.bpe.decode([int(t) for t in tokens], skip_special_tokens=False)
 
 
 def process_token_output(tokens: np.ndarray, padding_token: int = -1,
