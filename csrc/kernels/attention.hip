@@ -123,6 +123,101 @@ struct AttnArgs {
 };
 
 // ----------------------------------------------------------------------------------------------------------------
+// raw v_exp_f32 (2^x): no denormal range fix-up (exp2f adds a compare + 2 ldexp per call); -inf -> 0
+__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// The running max only moves when a row's max grew by more than 2^RESCALE_TH (P stays <= 2^8 in bf16, l and O in
+// fp32), so the O rescale -- 64 multiplies per tile at D=128 -- runs on a few early tiles instead of every tile.
+constexpr float RESCALE_TH = 8.f;
+
+// one 64-key tile of the forward for a wave's 32 queries. MASK: diagonal / ragged tiles (causal + bounds), branch
+// free; unmasked tiles carry no mask arithmetic at all.
+template <int D, bool MASK>
+__device__ __forceinline__ void fwd_tile(const char* sK, const char* sV, const bf16x8_t (&qf)[2][Geo<D>::DS],
+                                         f32x4_t (&o)[Geo<D>::DT][2], float (&m)[2], float (&l)[2], int k0, int qw,
+                                         int S, int causal, float c2, int lane) {
+  using G = Geo<D>;
+  const int g = lane >> 4, i = lane & 15;
+  f32x4_t s[2][4];
+  {
+    bf16x8_t kf[4];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) kf[kt] = row_frag<D>(sK, kt * 16, 0, lane);
+#pragma unroll
+    for (int ds = 0; ds < G::DS; ++ds) {
+      bf16x8_t kn[4];
+      if (ds + 1 < G::DS) {
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt) kn[kt] = row_frag<D>(sK, kt * 16, ds + 1, lane);
+      }
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt)
+          s[qt][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kt], qf[qt][ds],
+                                                              ds == 0 ? f32x4_t{0.f, 0.f, 0.f, 0.f} : s[qt][kt], 0, 0, 0);
+      if (ds + 1 < G::DS) {
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt) kf[kt] = kn[kt];
+      }
+    }
+  }
+  bf16x8_t pf[2][2];
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    const int q = qw + qt * 16 + i;
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        if (MASK) {
+          const int key = k0 + kt * 16 + 4 * g + v;
+          const bool dead = key >= S || (causal && key > q);
+          s[qt][kt][v] = dead ? -INFINITY : s[qt][kt][v];
+        }
+        mx = fmaxf(mx, s[qt][kt][v]);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float ms = mx * c2;                       // row max in the scaled log2 domain (c2 > 0)
+    const bool bump = ms > m[qt] + RESCALE_TH;
+    if (__builtin_amdgcn_ballot_w64(bump)) {        // wave-uniform: rare after the first tile
+      const float mn = bump ? ms : m[qt];
+      const float alpha = fexp2(m[qt] - mn);
+      l[qt] *= alpha;
+#pragma unroll
+      for (int dt = 0; dt < G::DT; ++dt) o[dt][qt] *= alpha;
+      m[qt] = mn;
+    }
+    const float nm = -m[qt];
+    float rs = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const float p = fexp2(__builtin_fmaf(s[qt][kt][v], c2, nm));
+        s[qt][kt][v] = p;
+        rs += p;
+      }
+    rs += __shfl_xor(rs, 16, 64);
+    rs += __shfl_xor(rs, 32, 64);
+    l[qt] += rs;
+    pf[qt][0] = pack_p(s[qt][0], s[qt][1]);
+    pf[qt][1] = pack_p(s[qt][2], s[qt][3]);
+  }
+#pragma unroll
+  for (int dt = 0; dt < G::DT; ++dt) {
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      bf16x8_t vf = tr_frag<D>(sV, st * 32, dt * 16, lane);
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt)
+        o[dt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[qt][st], o[dt][qt], 0, 0, 0);
+    }
+  }
+}
+
 // forward: block = 128 queries of one (b, h); wave w owns queries q0 + 32w + [0, 32). K/V tiles of 64 keys are
 // double-buffered in LDS and filled by LDS-DMA one tile ahead; one barrier per tile.
 template <int D>
@@ -132,7 +227,8 @@ __global__ __launch_bounds__(NTH, 2) void attn_fwd_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, i = lane & 15;
   const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
-  const int qblk = blockIdx.x * 128;
+  // heaviest causal blocks first: the tail of the grid then fills with short blocks
+  const int qblk = (a.causal ? (gridDim.x - 1 - blockIdx.x) : blockIdx.x) * 128;
   const int qw = qblk + w * 32;
   const bf16_t* Qb = a.Q + (long long)b * a.S * a.ld + h * D;
   const bf16_t* Kb = a.K + (long long)b * a.S * a.ld + h * D;
@@ -167,74 +263,9 @@ __global__ __launch_bounds__(NTH, 2) void attn_fwd_kernel(AttnArgs a) {
       stage_rows<D, 64>(nxt + TILE, Vb + (long long)(k0 + 64) * a.ld, a.ld, a.S - k0 - 64, tid);
     }
     if (!(a.causal && k0 > qw + 31)) {  // wave-uniform: skip blocks entirely in this wave's future
-      f32x4_t s[2][4];
-#pragma unroll
-      for (int qt = 0; qt < 2; ++qt)
-#pragma unroll
-        for (int kt = 0; kt < 4; ++kt) s[qt][kt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int ds = 0; ds < G::DS; ++ds) {
-#pragma unroll
-        for (int kt = 0; kt < 4; ++kt) {
-          bf16x8_t kf = row_frag<D>(sK, kt * 16, ds, lane);
-#pragma unroll
-          for (int qt = 0; qt < 2; ++qt)
-            s[qt][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[qt][ds], s[qt][kt], 0, 0, 0);
-        }
-      }
       const bool need_mask = (a.causal && k0 + 63 > qw) || k0 + 64 > a.S;
-#pragma unroll
-      for (int qt = 0; qt < 2; ++qt) {
-        const int q = qw + qt * 16 + i;
-        float mx = NEG_BIG;
-#pragma unroll
-        for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-          for (int v = 0; v < 4; ++v) {
-            float x = s[qt][kt][v] * c2;
-            if (need_mask) {
-              const int key = k0 + kt * 16 + 4 * g + v;
-              if (key >= a.S || (a.causal && key > q)) x = -INFINITY;
-            }
-            s[qt][kt][v] = x;
-            mx = fmaxf(mx, x);
-          }
-        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-        const float mn = fmaxf(m[qt], mx);
-        const float alpha = exp2f(m[qt] - mn);
-        float rs = 0.f;
-#pragma unroll
-        for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-          for (int v = 0; v < 4; ++v) {
-            const float p = exp2f(s[qt][kt][v] - mn);
-            s[qt][kt][v] = p;
-            rs += p;
-          }
-        rs += __shfl_xor(rs, 16, 64);
-        rs += __shfl_xor(rs, 32, 64);
-        l[qt] = l[qt] * alpha + rs;
-        m[qt] = mn;
-#pragma unroll
-        for (int dt = 0; dt < G::DT; ++dt) o[dt][qt] *= alpha;
-      }
-      bf16x8_t pf[2][2];
-#pragma unroll
-      for (int qt = 0; qt < 2; ++qt) {
-        pf[qt][0] = pack_p(s[qt][0], s[qt][1]);
-        pf[qt][1] = pack_p(s[qt][2], s[qt][3]);
-      }
-#pragma unroll
-      for (int dt = 0; dt < G::DT; ++dt) {
-#pragma unroll
-        for (int st = 0; st < 2; ++st) {
-          bf16x8_t vf = tr_frag<D>(sV, st * 32, dt * 16, lane);
-#pragma unroll
-          for (int qt = 0; qt < 2; ++qt)
-            o[dt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[qt][st], o[dt][qt], 0, 0, 0);
-        }
-      }
+      if (need_mask) fwd_tile<D, true>(sK, sV, qf, o, m, l, k0, qw, a.S, a.causal, c2, lane);
+      else fwd_tile<D, false>(sK, sV, qf, o, m, l, k0, qw, a.S, a.causal, c2, lane);
     }
     __syncthreads();
   }
@@ -251,7 +282,7 @@ __global__ __launch_bounds__(NTH, 2) void attn_fwd_kernel(AttnArgs a) {
       *reinterpret_cast<uint2*>(Ob + (long long)q * a.ld + d) =
           make_uint2(pack_bf16x2(o[dt][qt][0] * inv, o[dt][qt][1] * inv), pack_bf16x2(o[dt][qt][2] * inv, o[dt][qt][3] * inv));
     }
-    if (g == 0) a.LSE[((long long)b * a.H + h) * a.S + q] = (m[qt] + log2f(l[qt])) / LOG2E;
+    if (g == 0) a.LSE[((long long)b * a.H + h) * a.S + q] = (m[qt] + __log2f(l[qt])) / LOG2E;
   }
 }
 

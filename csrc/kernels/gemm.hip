@@ -410,6 +410,183 @@ __global__ __launch_bounds__(NT2, 1) void gemm256_kernel(GemmArgs p) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// Phase-pipelined 256x256 kernel (cdna_hip_programming.md §5 "256² 8-phase template", re-derived here).
+// 8 waves = 2 (M) x 4 (N) groups, each wave 128x64 of C = 2x2 quadrants of 64x32. A K-tile (BK = 64) is computed
+// in 4 phases, one quadrant each, in the order (qm,qn) = (0,0) (0,1) (1,1) (1,0); fragments are loaded at the
+// START of a phase: p0 A[qm=0] + B[qn=0], p1 B[qn=1], p2 A[qm=1], p3 nothing (B[qn=0] still in registers).
+// LDS holds 8 "pieces" of 16 KiB: {A0, A1, B0, B1} x K-tile parity, where A_q = the 64-row halves qm = q of BOTH
+// M wave groups and B_q the 32-column quarters qn = q of all four N groups, so a piece is dead as soon as its
+// quadrant phase retired. Each phase stages ONE piece by LDS-DMA (2 x 16 B per thread), 4-6 phases ahead:
+//   phase 4t+0: B1(t+1)   4t+1: A1(t+1)   4t+2: A0(t+2)   4t+3: B0(t+2)
+// and waits with a COUNTED vmcnt(8) (4 pieces may stay in flight), never vmcnt(0) in the steady state.
+// The two M wave groups run one barrier apart (group 1 takes an extra barrier up front) so one group's ds_reads
+// and LDS-DMA issue overlap the other group's 16 MFMAs; each phase = reads, stage, wait, barrier, lgkmcnt(0),
+// MFMAs (setprio 1), barrier. Derived hazard rules (intervals between barriers, stagger included):
+//   RAW: a piece read in phase Q was waited for in phase <= Q-1 by every thread (vmcnt counts above);
+//   WAR: a piece's slot is restaged >= 2 phases after its last read phase (A0: +2, B0: +3, B1: +3, A1: +3).
+constexpr int PIECE = 16384;
+
+__device__ __forceinline__ void bar() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int T, bool IS_A>
+__device__ __forceinline__ void stage_piece(char* img, const bf16_t* X, long long ld, int base0, int R, int k0,
+                                            int q, int wave, int lane) {
+#pragma unroll
+  for (int rd = 0; rd < 2; ++rd) {
+    const int jj = rd * 8 + wave;            // 1 KiB sub-piece
+    const bf16_t* src;
+    if (T == 0) {                            // [128 rows][64 k], 128-B rows
+      const int lr = jj * 8 + (lane >> 3), pc = lane & 7;
+      const int c = pc ^ ((lr >> 1) & 7);
+      const int grow = IS_A ? (lr >> 6) * 128 + q * 64 + (lr & 63) : (lr >> 5) * 64 + q * 32 + (lr & 31);
+      const int row = min(base0 + grow, R - 1);
+      src = X + (long long)row * ld + k0 + c * 8;
+    } else {                                 // [64 k][128 cols], 256-B rows
+      const int kr = jj * 4 + (lane >> 4), pc = lane & 15;
+      const int lc = (pc ^ kswz(kr)) * 8;
+      const int gcol = IS_A ? (lc >> 6) * 128 + q * 64 + (lc & 63) : (lc >> 5) * 64 + q * 32 + (lc & 31);
+      const int col = min(base0 + gcol, R - 8);
+      src = X + (long long)(k0 + kr) * ld + col;
+    }
+    glds16(src, img + jj * 1024);
+  }
+}
+
+template <int A_T, int B_T, bool OUT_F32>
+__global__ __launch_bounds__(NT2, 1) void gemm_ph_kernel(GemmArgs p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+  int bid = blockIdx.x;
+  {
+    const int nwg = gridDim.x, xcd = bid & 7, qq = nwg >> 3, r = nwg & 7;
+    const int base = xcd < r ? xcd * (qq + 1) : r * (qq + 1) + (xcd - r) * qq;
+    bid = base + (bid >> 3);
+  }
+  const int GROUP = 4;
+  const int per_group = GROUP * p.tiles_n;
+  const int first_m = (bid / per_group) * GROUP;
+  const int gsz = min(p.tiles_m - first_m, GROUP);
+  const int tm = first_m + (bid % per_group) % gsz;
+  const int tn = (bid % per_group) / gsz;
+  const int m0 = tm * BM2, n0 = tn * BN2;
+  const int b1 = blockIdx.y / p.nb2, b2 = blockIdx.y % p.nb2;
+  const bf16_t* A = p.A + b1 * p.a_s1 + b2 * p.a_s2;
+  const bf16_t* B = p.B + b1 * p.b_s1 + b2 * p.b_s2;
+  const int nk = p.K / BK;
+
+  // piece slots: (parity * 4 + {A0, A1, B0, B1}) * 16 KiB
+  auto slot = [&](int t, int pc) -> char* { return smem + ((t & 1) * 4 + pc) * PIECE; };
+  auto stageA = [&](int t, int q) { stage_piece<A_T, true>(slot(t, q), A, p.lda, m0, p.M, t * BK, q, wave, lane); };
+  auto stageB = [&](int t, int q) { stage_piece<B_T, false>(slot(t, 2 + q), B, p.ldb, n0, p.N, t * BK, q, wave, lane); };
+
+  f32x4_t acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: the pieces phases -6..-1 would have staged
+  stageA(0, 0); stageB(0, 0); stageB(0, 1); stageA(0, 1);
+  if (nk > 1) { stageA(1, 0); stageB(1, 0); asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); }
+  else { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+  if (wr == 1) bar();
+  bar();
+
+  bf16x8_t af[4][2], bq0[2][2], bq1[2][2];
+  for (int t = 0; t < nk; ++t) {
+    const bool tail = t + 2 >= nk;
+#pragma unroll
+    for (int ph = 0; ph < 4; ++ph) {
+      const int qm = (ph == 0 || ph == 1) ? 0 : 1;
+      const int qn = (ph == 0 || ph == 3) ? 0 : 1;
+      // 1. fragments of this phase
+      if (ph == 0) {
+        const char* ib = slot(t, 2);
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk) bq0[j][kk] = read_frag<B_T>(ib, wc * 32 + j * 16, kk, lane);
+      }
+      if (ph == 0 || ph == 2) {
+        const char* ia = slot(t, qm);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk) af[i][kk] = read_frag<A_T>(ia, wr * 64 + i * 16, kk, lane);
+      }
+      if (ph == 1) {
+        const char* ib = slot(t, 3);
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk) bq1[j][kk] = read_frag<B_T>(ib, wc * 32 + j * 16, kk, lane);
+      }
+      // 2. one piece of LDS-DMA
+      if (ph == 0 && t + 1 < nk) stageB(t + 1, 1);
+      if (ph == 1 && t + 1 < nk) stageA(t + 1, 1);
+      if (ph == 2 && t + 2 < nk) stageA(t + 2, 0);
+      if (ph == 3 && t + 2 < nk) stageB(t + 2, 0);
+      // 3. counted wait, barrier, MFMAs, barrier
+      if (tail) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      bar();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk) {
+            const bf16x8_t bb = qn == 0 ? bq0[j][kk] : bq1[j][kk];
+            acc[qm * 4 + i][qn * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bb, af[i][kk],
+                                                                                  acc[qm * 4 + i][qn * 2 + j], 0, 0, 0);
+          }
+      __builtin_amdgcn_s_setprio(0);
+      bar();
+    }
+  }
+  if (wr == 0) bar();
+
+  const long long coff = b1 * p.c_s1 + b2 * p.c_s2;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = m0 + wr * 128 + i * 16 + (lane & 15);
+    if (m >= p.M) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + wc * 64 + j * 16 + 4 * (lane >> 4);
+      if (n >= p.N) continue;
+      float v[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) v[t] = p.alpha * acc[i][j][t];
+      epilogue_store<OUT_F32>(p, coff + (long long)m * p.ldc + n, v);
+    }
+  }
+}
+
+template <int A_T, int B_T, bool F32>
+hipError_t launch_ph(GemmArgs a, int batch, hipStream_t stream) {
+  a.tiles_m = (a.M + BM2 - 1) / BM2;
+  a.tiles_n = (a.N + BN2 - 1) / BN2;
+  dim3 grid(a.tiles_m * a.tiles_n, batch);
+  const size_t lds = 8 * PIECE;
+  auto k = gemm_ph_kernel<A_T, B_T, F32>;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr = true;
+  }
+  hipLaunchKernelGGL(k, grid, dim3(NT2), lds, stream, a);
+  return hipGetLastError();
+}
+
 template <int A_T, int B_T, bool F32>
 hipError_t launch256(GemmArgs a, int batch, hipStream_t stream) {
   a.tiles_m = (a.M + BM2 - 1) / BM2;
@@ -428,13 +605,13 @@ hipError_t launch256(GemmArgs a, int batch, hipStream_t stream) {
 
 }  // namespace
 
-static bool getenv_big() {
+static int getenv_big() {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("OBST_GEMM_BIG");
-    v = (e && e[0] == '0') ? 0 : 1;
+    v = e ? (e[0] - '0') : 2;
   }
-  return v == 1;
+  return v;
 }
 
 struct ObstGemmDesc {
@@ -467,13 +644,14 @@ OBST_API int obst_gemm(const ObstGemmDesc* d, hipStream_t stream) {
   hipError_t e;
   // big-tile path: needs K % 64 == 0, M/N >= 256 and enough 256x256 tiles to fill the 256 CUs twice
   const long long big_tiles = (long long)((d->M + 255) / 256) * ((d->N + 255) / 256) * batch;
-  const bool big = getenv_big() && d->K % 64 == 0 && d->M >= 256 && d->N >= 256 && big_tiles >= 512 &&
+  const int impl = getenv_big();
+  const bool big = impl > 0 && d->K % 64 == 0 && d->M >= 256 && d->N >= 256 && big_tiles >= 512 &&
                    (d->a_t == 0 || d->M % 8 == 0) && (d->b_t == 0 || d->N % 8 == 0);
   if (big) {
-#define OBST_GEMM256_CASE(AT, BT, F)                               \
-    if (d->a_t == AT && d->b_t == BT && (d->out_f32 != 0) == F) {  \
-      e = launch256<AT, BT, F>(a, batch, stream);                    \
-      return e == hipSuccess ? 0 : (int)e;                           \
+#define OBST_GEMM256_CASE(AT, BT, F)                                                             \
+    if (d->a_t == AT && d->b_t == BT && (d->out_f32 != 0) == F) {                                \
+      e = impl >= 2 ? launch_ph<AT, BT, F>(a, batch, stream) : launch256<AT, BT, F>(a, batch, stream); \
+      return e == hipSuccess ? 0 : (int)e;                                                         \
     }
     OBST_GEMM256_CASE(0, 0, false) OBST_GEMM256_CASE(0, 1, false) OBST_GEMM256_CASE(1, 0, false)
     OBST_GEMM256_CASE(1, 1, false) OBST_GEMM256_CASE(0, 0, true) OBST_GEMM256_CASE(0, 1, true)

@@ -198,11 +198,13 @@ def test_cumsum(cuda):
         _close(out[str(cuda)], out["cpu"], 5e-2, 2e-2, f"cumsum {rev}{mean}{grad}")
 
 
+@pytest.mark.parametrize("K", [64, 128, 576])
 @pytest.mark.parametrize("a_t,b_t", [(0, 0), (0, 1), (1, 0), (1, 1)])
-def test_gemm_big_tile(cuda, a_t, b_t):
-    """shapes that take the 256x256 LDS-DMA kernel (>= 512 tiles), incl. ragged M/N edges"""
-    torch.manual_seed(21 + a_t + 2 * b_t)
-    M, N, K = 4160, 8128, 128
+def test_gemm_big_tile(cuda, a_t, b_t, K):
+    """shapes that take the 256x256 LDS-DMA kernels (>= 512 tiles), incl. ragged M/N edges; K = 576 runs the
+    phase kernel's steady state (counted vmcnt) for 7 K-tiles. Repeats must be bitwise identical (race screen)."""
+    torch.manual_seed(21 + a_t + 2 * b_t + K)
+    M, N = 4160, 8128
     A = (torch.randn(M * K) * 0.5).to(BF)
     B = (torch.randn(N * K) * 0.5).to(BF)
     lda = K if a_t == 0 else M
@@ -210,7 +212,18 @@ def test_gemm_big_tile(cuda, a_t, b_t):
     av = A.view(M, K) if a_t == 0 else A.view(K, M).t()
     bv = B.view(N, K).t() if b_t == 0 else B.view(K, N)
     ref = av.float() @ bv.float()
-    Cg = torch.zeros(M * N, dtype=BF, device=cuda)
-    raw.gemm(raw.Operand(A.to(cuda), a_t, lda), raw.Operand(B.to(cuda), b_t, ldb), raw.Operand(Cg, 0, N), M, N, K)
+    Ad, Bd = A.to(cuda), B.to(cuda)
+    outs = []
+    for _ in range(4):
+        Cg = torch.zeros(M * N, dtype=BF, device=cuda)
+        raw.gemm(raw.Operand(Ad, a_t, lda), raw.Operand(Bd, b_t, ldb), raw.Operand(Cg, 0, N), M, N, K)
+        outs.append(Cg)
     torch.cuda.synchronize()
-    _close(Cg.view(M, N), ref, 4e-2, 2e-2, f"gemm256 {a_t}{b_t}")
+    _close(outs[0].view(M, N), ref, 4e-2, 2e-2, f"gemm256 {a_t}{b_t} K{K}")
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0]), "run-to-run difference: LDS race"
+    # fp32 output with accumulation (the wgrad epilogue)
+    Cf = torch.ones(M * N, dtype=torch.float32, device=cuda)
+    raw.gemm(raw.Operand(Ad, a_t, lda), raw.Operand(Bd, b_t, ldb), raw.Operand(Cf, 0, N), M, N, K, beta=1.0)
+    torch.cuda.synchronize()
+    _close(Cf.view(M, N), ref + 1, 2e-2, 2e-2, f"gemm256 f32 {a_t}{b_t} K{K}")
