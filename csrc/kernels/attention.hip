@@ -309,6 +309,67 @@ __global__ __launch_bounds__(NTH) void attn_delta_kernel(AttnArgs a) {
   if (lane == 0) a.delta[((long long)b * a.H + h) * a.S + q] = acc;
 }
 
+// one 64-key tile of the dQ kernel for a wave's 32 queries (two 32-key halves: P needs only the stored LSE, so no
+// state crosses the halves). dP starts from -delta (the accumulator init), so dS = P * dP.
+template <int D, bool MASK>
+__device__ __forceinline__ void dq_tile(const char* sK, const char* sV, const bf16x8_t (&qf)[2][Geo<D>::DS],
+                                        const bf16x8_t (&df)[2][Geo<D>::DS], const float (&lse2)[2],
+                                        const float (&dlt)[2], f32x4_t (&acc)[Geo<D>::DT][2], int k0, int qw, int S,
+                                        int causal, float c2, int lane) {
+  using G = Geo<D>;
+  const int g = lane >> 4, i = lane & 15;
+#pragma unroll
+  for (int st = 0; st < 2; ++st) {
+    f32x4_t sc[2][2], dp[2][2];
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        sc[qt][kk] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        dp[qt][kk] = f32x4_t{-dlt[qt], -dlt[qt], -dlt[qt], -dlt[qt]};
+      }
+#pragma unroll
+    for (int ds = 0; ds < G::DS; ++ds) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int kt = 2 * st + kk;
+        bf16x8_t kf = row_frag<D>(sK, kt * 16, ds, lane);
+        bf16x8_t vf = row_frag<D>(sV, kt * 16, ds, lane);
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt) {
+          sc[qt][kk] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[qt][ds], sc[qt][kk], 0, 0, 0);
+          dp[qt][kk] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, df[qt][ds], dp[qt][kk], 0, 0, 0);
+        }
+      }
+    }
+    bf16x8_t sf[2];
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      const int q = qw + qt * 16 + i;
+      const float nl = -lse2[qt];
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          float p = fexp2(__builtin_fmaf(sc[qt][kk][v], c2, nl));
+          if (MASK) {
+            const int key = k0 + (2 * st + kk) * 16 + 4 * g + v;
+            p = (key >= S || (causal && key > q)) ? 0.f : p;
+          }
+          sc[qt][kk][v] = p * dp[qt][kk][v];
+        }
+      sf[qt] = pack_p(sc[qt][0], sc[qt][1]);
+    }
+#pragma unroll
+    for (int dt = 0; dt < G::DT; ++dt) {
+      bf16x8_t kf = tr_frag<D>(sK, st * 32, dt * 16, lane);
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt)
+        acc[dt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, sf[qt], acc[dt][qt], 0, 0, 0);
+    }
+  }
+}
+
 // ----------------------------------------------------------------------------------------------------------------
 // dQ: block = 128 queries; recompute Sᵀ, Pᵀ, dPᵀ = V·dOᵀ, dSᵀ, dQᵀ += Kᵀ·dSᵀ. K/V tiles double-buffered (LDS-DMA).
 template <int D>
@@ -318,7 +379,7 @@ __global__ __launch_bounds__(NTH, 2) void attn_bwd_dq_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, i = lane & 15;
   const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
-  const int qblk = blockIdx.x * 128;
+  const int qblk = (a.causal ? (gridDim.x - 1 - blockIdx.x) : blockIdx.x) * 128;  // heaviest first
   const int qw = qblk + w * 32;
   const long long base = (long long)b * a.S * a.ld + h * D;
   const int kend = a.causal ? min(a.S, qblk + 128) : a.S;
@@ -357,54 +418,8 @@ __global__ __launch_bounds__(NTH, 2) void attn_bwd_dq_kernel(AttnArgs a) {
     }
     if (!(a.causal && k0 > qw + 31)) {
       const bool need_mask = (a.causal && k0 + 63 > qw) || k0 + 64 > a.S;
-      // two 32-key halves: P needs only the stored LSE, so no state crosses the halves
-#pragma unroll
-      for (int st = 0; st < 2; ++st) {
-        f32x4_t s[2][2], dp[2][2];
-#pragma unroll
-        for (int qt = 0; qt < 2; ++qt)
-#pragma unroll
-          for (int kk = 0; kk < 2; ++kk) s[qt][kk] = dp[qt][kk] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int ds = 0; ds < G::DS; ++ds) {
-#pragma unroll
-          for (int kk = 0; kk < 2; ++kk) {
-            const int kt = 2 * st + kk;
-            bf16x8_t kf = row_frag<D>(sK, kt * 16, ds, lane);
-            bf16x8_t vf = row_frag<D>(sV, kt * 16, ds, lane);
-#pragma unroll
-            for (int qt = 0; qt < 2; ++qt) {
-              s[qt][kk] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[qt][ds], s[qt][kk], 0, 0, 0);
-              dp[qt][kk] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, df[qt][ds], dp[qt][kk], 0, 0, 0);
-            }
-          }
-        }
-#pragma unroll
-        for (int qt = 0; qt < 2; ++qt) {
-          const int q = qw + qt * 16 + i;
-#pragma unroll
-          for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-            for (int v = 0; v < 4; ++v) {
-              float p = exp2f(s[qt][kk][v] * c2 - lse2[qt]);
-              if (need_mask) {
-                const int key = k0 + (2 * st + kk) * 16 + 4 * g + v;
-                if (key >= a.S || (a.causal && key > q)) p = 0.f;
-              }
-              s[qt][kk][v] = p * (dp[qt][kk][v] - dlt[qt]);
-            }
-        }
-        bf16x8_t sf[2];
-#pragma unroll
-        for (int qt = 0; qt < 2; ++qt) sf[qt] = pack_p(s[qt][0], s[qt][1]);
-#pragma unroll
-        for (int dt = 0; dt < G::DT; ++dt) {
-          bf16x8_t kf = tr_frag<D>(sK, st * 32, dt * 16, lane);
-#pragma unroll
-          for (int qt = 0; qt < 2; ++qt)
-            acc[dt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, sf[qt], acc[dt][qt], 0, 0, 0);
-        }
-      }
+      if (need_mask) dq_tile<D, true>(sK, sV, qf, df, lse2, dlt, acc, k0, qw, a.S, a.causal, c2, lane);
+      else dq_tile<D, false>(sK, sV, qf, df, lse2, dlt, acc, k0, qw, a.S, a.causal, c2, lane);
     }
     __syncthreads();
   }
@@ -418,6 +433,62 @@ __global__ __launch_bounds__(NTH, 2) void attn_bwd_dq_kernel(AttnArgs a) {
       const float sc = a.scale;
       *reinterpret_cast<uint2*>(a.dQ + base + (long long)q * a.ld + d) =
           make_uint2(pack_bf16x2(acc[dt][qt][0] * sc, acc[dt][qt][1] * sc), pack_bf16x2(acc[dt][qt][2] * sc, acc[dt][qt][3] * sc));
+    }
+  }
+}
+
+// one 64-query chunk of the dK/dV kernel for a wave's 16 keys (key on the lane: S = Q·Kᵀ, P and dS feed dVᵀ and
+// dKᵀ as B operands straight from the accumulators). dP starts from -delta[q] (read from LDS as one f32x4 per tile).
+template <int D, bool MASK>
+__device__ __forceinline__ void dkv_chunk(const char* sQ, const char* sD, const float* sL, const float* sDl,
+                                          const bf16x8_t (&kf)[Geo<D>::DS], const bf16x8_t (&vf)[Geo<D>::DS],
+                                          f32x4_t (&dk)[Geo<D>::DT], f32x4_t (&dv)[Geo<D>::DT], int q0, int key, int S,
+                                          int causal, float c2, int lane) {
+  using G = Geo<D>;
+  const int g = lane >> 4;
+  f32x4_t sc[4], dp[4];
+#pragma unroll
+  for (int qt = 0; qt < 4; ++qt) {
+    const float4 dl = *reinterpret_cast<const float4*>(sDl + qt * 16 + 4 * g);
+    sc[qt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    dp[qt] = f32x4_t{-dl.x, -dl.y, -dl.z, -dl.w};
+  }
+#pragma unroll
+  for (int ds = 0; ds < G::DS; ++ds) {
+#pragma unroll
+    for (int qt = 0; qt < 4; ++qt) {
+      bf16x8_t qa = row_frag<D>(sQ, qt * 16, ds, lane);
+      bf16x8_t da = row_frag<D>(sD, qt * 16, ds, lane);
+      sc[qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa, kf[ds], sc[qt], 0, 0, 0);
+      dp[qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, vf[ds], dp[qt], 0, 0, 0);
+    }
+  }
+  // sc[qt][v] = S[q = q0 + qt*16 + 4g + v][key]
+#pragma unroll
+  for (int qt = 0; qt < 4; ++qt) {
+    const float4 lv = *reinterpret_cast<const float4*>(sL + qt * 16 + 4 * g);
+    const float nl[4] = {-lv.x * LOG2E, -lv.y * LOG2E, -lv.z * LOG2E, -lv.w * LOG2E};
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      float pv = fexp2(__builtin_fmaf(sc[qt][v], c2, nl[v]));
+      if (MASK) {
+        const int q = q0 + qt * 16 + 4 * g + v;
+        pv = (q >= S || key >= S || (causal && key > q)) ? 0.f : pv;
+      }
+      sc[qt][v] = pv;
+      dp[qt][v] = pv * dp[qt][v];
+    }
+  }
+#pragma unroll
+  for (int st = 0; st < 2; ++st) {
+    const bf16x8_t pb = pack_p(sc[2 * st], sc[2 * st + 1]);
+    const bf16x8_t sb = pack_p(dp[2 * st], dp[2 * st + 1]);
+#pragma unroll
+    for (int dt = 0; dt < G::DT; ++dt) {
+      bf16x8_t dot = tr_frag<D>(sD, st * 32, dt * 16, lane);
+      bf16x8_t qtr = tr_frag<D>(sQ, st * 32, dt * 16, lane);
+      dv[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dot, pb, dv[dt], 0, 0, 0);
+      dk[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qtr, sb, dk[dt], 0, 0, 0);
     }
   }
 }
@@ -473,46 +544,9 @@ __global__ __launch_bounds__(NTH, 2) void attn_bwd_dkv_kernel(AttnArgs a) {
     const float* sDl = sL + 64;
     if (c + 1 < nqc) stage(smem + ((c + 1) & 1) * STAGE, q0 + QC);
     if (!(a.causal && q0 + QC - 1 < kw)) {  // every query of this chunk precedes this wave's keys
-      f32x4_t s[4], dp[4];
-#pragma unroll
-      for (int qt = 0; qt < 4; ++qt) s[qt] = dp[qt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int ds = 0; ds < G::DS; ++ds) {
-#pragma unroll
-        for (int qt = 0; qt < 4; ++qt) {
-          bf16x8_t qa = row_frag<D>(sQ, qt * 16, ds, lane);
-          bf16x8_t da = row_frag<D>(sD, qt * 16, ds, lane);
-          s[qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa, kf[ds], s[qt], 0, 0, 0);
-          dp[qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, vf[ds], dp[qt], 0, 0, 0);
-        }
-      }
-      // s[qt][v] = S[q = q0 + qt*16 + 4g + v][key]
       const bool need_mask = (a.causal && q0 < kw + 15) || q0 + QC > a.S || kw + 16 > a.S;
-#pragma unroll
-      for (int qt = 0; qt < 4; ++qt)
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {
-          const int ql = qt * 16 + 4 * g + v;
-          float pv = exp2f(s[qt][v] * c2 - sL[ql] * LOG2E);
-          if (need_mask) {
-            const int q = q0 + ql;
-            if (q >= a.S || key >= a.S || (a.causal && key > q)) pv = 0.f;
-          }
-          s[qt][v] = pv;
-          dp[qt][v] = pv * (dp[qt][v] - sDl[ql]);
-        }
-#pragma unroll
-      for (int st = 0; st < 2; ++st) {
-        const bf16x8_t pb = pack_p(s[2 * st], s[2 * st + 1]);
-        const bf16x8_t sb = pack_p(dp[2 * st], dp[2 * st + 1]);
-#pragma unroll
-        for (int dt = 0; dt < G::DT; ++dt) {
-          bf16x8_t dot = tr_frag<D>(sD, st * 32, dt * 16, lane);
-          bf16x8_t qtr = tr_frag<D>(sQ, st * 32, dt * 16, lane);
-          dv[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dot, pb, dv[dt], 0, 0, 0);
-          dk[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qtr, sb, dk[dt], 0, 0, 0);
-        }
-      }
+      if (need_mask) dkv_chunk<D, true>(sQ, sD, sL, sDl, kf, vf, dk, dv, q0, key, a.S, a.causal, c2, lane);
+      else dkv_chunk<D, false>(sQ, sD, sL, sDl, kf, vf, dk, dv, q0, key, a.S, a.causal, c2, lane);
     }
     __syncthreads();
   }

@@ -412,12 +412,13 @@ __global__ __launch_bounds__(NT2, 1) void gemm256_kernel(GemmArgs p) {
 
 // ---------------------------------------------------------------------------------------------------------------
 // Phase-pipelined 256x256 kernel (cdna_hip_programming.md §5 "256² 8-phase template", re-derived here).
-// 8 waves = 2 (M) x 4 (N) groups, each wave 128x64 of C = 2x2 quadrants of 64x32. A K-tile (BK = 64) is computed
-// in 4 phases, one quadrant each, in the order (qm,qn) = (0,0) (0,1) (1,1) (1,0); fragments are loaded at the
-// START of a phase: p0 A[qm=0] + B[qn=0], p1 B[qn=1], p2 A[qm=1], p3 nothing (B[qn=0] still in registers).
-// LDS holds 8 "pieces" of 16 KiB: {A0, A1, B0, B1} x K-tile parity, where A_q = the 64-row halves qm = q of BOTH
-// M wave groups and B_q the 32-column quarters qn = q of all four N groups, so a piece is dead as soon as its
-// quadrant phase retired. Each phase stages ONE piece by LDS-DMA (2 x 16 B per thread), 4-6 phases ahead:
+// 8 waves = 2 (M) x 4 (N) groups; C is cut into quadrants (qm, qn) of 128 x 128, and wave (wr, wc) owns the
+// 64 x 32 sub-block (wr, wc) of every quadrant (so its 128 x 64 of C are 2 x 2 sub-blocks 128 apart). A K-tile
+// (BK = 64) is computed in 4 phases, one quadrant each, in the order (qm,qn) = (0,0) (0,1) (1,1) (1,0); fragments
+// are loaded at the START of a phase: p0 A[qm=0] + B[qn=0], p1 B[qn=1], p2 A[qm=1], p3 nothing (B[qn=0] still in
+// registers). LDS holds 8 "pieces" of 16 KiB: {A0, A1, B0, B1} x K-tile parity, A_q = rows q*128..+128 and
+// B_q = columns q*128..+128 of the block tile -- contiguous, so an M/N-contiguous operand streams whole 256-B
+// rows -- and a piece is dead as soon as its quadrant phase retired. Each phase stages ONE piece by LDS-DMA (2 x 16 B per thread), 4-6 phases ahead:
 //   phase 4t+0: B1(t+1)   4t+1: A1(t+1)   4t+2: A0(t+2)   4t+3: B0(t+2)
 // and waits with a COUNTED vmcnt(8) (4 pieces may stay in flight), never vmcnt(0) in the steady state.
 // The two M wave groups run one barrier apart (group 1 takes an extra barrier up front) so one group's ds_reads
@@ -443,14 +444,12 @@ __device__ __forceinline__ void stage_piece(char* img, const bf16_t* X, long lon
     if (T == 0) {                            // [128 rows][64 k], 128-B rows
       const int lr = jj * 8 + (lane >> 3), pc = lane & 7;
       const int c = pc ^ ((lr >> 1) & 7);
-      const int grow = IS_A ? (lr >> 6) * 128 + q * 64 + (lr & 63) : (lr >> 5) * 64 + q * 32 + (lr & 31);
-      const int row = min(base0 + grow, R - 1);
+      const int row = min(base0 + q * 128 + lr, R - 1);
       src = X + (long long)row * ld + k0 + c * 8;
     } else {                                 // [64 k][128 cols], 256-B rows
       const int kr = jj * 4 + (lane >> 4), pc = lane & 15;
       const int lc = (pc ^ kswz(kr)) * 8;
-      const int gcol = IS_A ? (lc >> 6) * 128 + q * 64 + (lc & 63) : (lc >> 5) * 64 + q * 32 + (lc & 31);
-      const int col = min(base0 + gcol, R - 8);
+      const int col = min(base0 + q * 128 + lc, R - 8);
       src = X + (long long)(k0 + kr) * ld + col;
     }
     glds16(src, img + jj * 1024);
@@ -557,11 +556,11 @@ __global__ __launch_bounds__(NT2, 1) void gemm_ph_kernel(GemmArgs p) {
   const long long coff = b1 * p.c_s1 + b2 * p.c_s2;
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    const int m = m0 + wr * 128 + i * 16 + (lane & 15);
+    const int m = m0 + (i >> 2) * 128 + wr * 64 + (i & 3) * 16 + (lane & 15);
     if (m >= p.M) continue;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int n = n0 + wc * 64 + j * 16 + 4 * (lane >> 4);
+      const int n = n0 + (j >> 1) * 128 + wc * 32 + (j & 1) * 16 + 4 * (lane >> 4);
       if (n >= p.N) continue;
       float v[4];
 #pragma unroll

@@ -17,6 +17,8 @@ SHAPES = [  # (name, M, N, K, a_t, b_t, out_f32)
     ("wgrad d x I", 2048, 4096, T, 1, 1, True), ("wgrad I x d", 4096, 2048, T, 1, 1, True),
     ("logits fwd", T, 50304, 2048, 0, 1, False), ("logits dgrad", T, 2048, 50304, 0, 0, False),
     ("logits wgrad", 2048, 50304, T, 1, 1, True),
+    ("sq8k NT", 8192, 8192, 8192, 0, 0, False), ("sq8k NN", 8192, 8192, 8192, 0, 1, False),
+    ("sq8k TT f32", 8192, 8192, 8192, 1, 1, True), ("sq8k TN", 8192, 8192, 8192, 1, 0, False),
 ]
 
 
