@@ -34,6 +34,8 @@ struct GemmArgs {
   int tiles_m, tiles_n;
   float alpha, beta;      // beta: fp32 output only, C = alpha*acc + beta*C_old (gradient accumulation)
   int act, mode;          // mode 0: out = act(alpha*acc + R); mode 1: out = (alpha*acc + R) * act'(Zin)
+  int ksplit;             // phase kernel only: K split over blockIdx.y; partial tiles go to `ws` [split][M][N]
+  float* ws;              // split-K workspace (fp32), summed into C by splitk_reduce_kernel
 };
 
 __device__ __forceinline__ int kswz(int k) { return ((k & 3) << 1) | (((k >> 3) & 1) << 3); }
@@ -474,10 +476,12 @@ __global__ __launch_bounds__(NT2, 1) void gemm_ph_kernel(GemmArgs p) {
   const int tm = first_m + (bid % per_group) % gsz;
   const int tn = (bid % per_group) / gsz;
   const int m0 = tm * BM2, n0 = tn * BN2;
-  const int b1 = blockIdx.y / p.nb2, b2 = blockIdx.y % p.nb2;
-  const bf16_t* A = p.A + b1 * p.a_s1 + b2 * p.a_s2;
-  const bf16_t* B = p.B + b1 * p.b_s1 + b2 * p.b_s2;
-  const int nk = p.K / BK;
+  const int split = blockIdx.y % p.ksplit, bidx = blockIdx.y / p.ksplit;
+  const int b1 = bidx / p.nb2, b2 = bidx % p.nb2;
+  const int kspan = p.K / p.ksplit, kbeg = split * kspan;
+  const bf16_t* A = p.A + b1 * p.a_s1 + b2 * p.a_s2 + (A_T == 0 ? (long long)kbeg : (long long)kbeg * p.lda);
+  const bf16_t* B = p.B + b1 * p.b_s1 + b2 * p.b_s2 + (B_T == 0 ? (long long)kbeg : (long long)kbeg * p.ldb);
+  const int nk = kspan / BK;
 
   // piece slots: (parity * 4 + {A0, A1, B0, B1}) * 16 KiB
   auto slot = [&](int t, int pc) -> char* { return smem + ((t & 1) * 4 + pc) * PIECE; };
@@ -565,16 +569,52 @@ __global__ __launch_bounds__(NT2, 1) void gemm_ph_kernel(GemmArgs p) {
       float v[4];
 #pragma unroll
       for (int t = 0; t < 4; ++t) v[t] = p.alpha * acc[i][j][t];
-      epilogue_store<OUT_F32>(p, coff + (long long)m * p.ldc + n, v);
+      if (OUT_F32 && p.ksplit > 1) {
+        *reinterpret_cast<float4*>(p.ws + (long long)split * p.M * p.N + (long long)m * p.N + n) =
+            make_float4(v[0], v[1], v[2], v[3]);
+      } else {
+        epilogue_store<OUT_F32>(p, coff + (long long)m * p.ldc + n, v);
+      }
     }
   }
+}
+
+// C[m][n] = beta * C[m][n] + sum_s ws[s][m][n]   (float4 per lane)
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(float* __restrict__ C, const float* __restrict__ ws,
+                                                             long long mn, long long ldc, int N, int ks, float beta) {
+  const long long nv = mn / 4;
+  for (long long v = (long long)blockIdx.x * 256 + threadIdx.x; v < nv; v += (long long)gridDim.x * 256) {
+    const long long e = v * 4, m = e / N, n = e % N;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int s = 0; s < ks; ++s) {
+      const float4 w = reinterpret_cast<const float4*>(ws + s * mn)[v];
+      acc.x += w.x; acc.y += w.y; acc.z += w.z; acc.w += w.w;
+    }
+    float4* c = reinterpret_cast<float4*>(C + m * ldc + n);
+    if (beta != 0.f) {
+      const float4 o = *c;
+      acc.x += beta * o.x; acc.y += beta * o.y; acc.z += beta * o.z; acc.w += beta * o.w;
+    }
+    *c = acc;
+  }
+}
+
+float* splitk_workspace(size_t bytes) {
+  static float* buf = nullptr;
+  static size_t cap = 0;
+  if (bytes > cap) {
+    if (buf) (void)hipFree(buf);
+    if (hipMalloc(&buf, bytes) != hipSuccess) { buf = nullptr; cap = 0; return nullptr; }
+    cap = bytes;
+  }
+  return buf;
 }
 
 template <int A_T, int B_T, bool F32>
 hipError_t launch_ph(GemmArgs a, int batch, hipStream_t stream) {
   a.tiles_m = (a.M + BM2 - 1) / BM2;
   a.tiles_n = (a.N + BN2 - 1) / BN2;
-  dim3 grid(a.tiles_m * a.tiles_n, batch);
+  dim3 grid(a.tiles_m * a.tiles_n, batch * a.ksplit);
   const size_t lds = 8 * PIECE;
   auto k = gemm_ph_kernel<A_T, B_T, F32>;
   static bool attr = false;
@@ -583,6 +623,11 @@ hipError_t launch_ph(GemmArgs a, int batch, hipStream_t stream) {
     attr = true;
   }
   hipLaunchKernelGGL(k, grid, dim3(NT2), lds, stream, a);
+  if (F32 && a.ksplit > 1) {
+    const long long mn = (long long)a.M * a.N;
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(2048), dim3(256), 0, stream, reinterpret_cast<float*>(a.C), a.ws,
+                       mn, a.ldc, a.N, a.ksplit, a.beta);
+  }
   return hipGetLastError();
 }
 
@@ -644,7 +689,27 @@ OBST_API int obst_gemm(const ObstGemmDesc* d, hipStream_t stream) {
   // big-tile path: needs K % 64 == 0, M/N >= 256 and enough 256x256 tiles to fill the 256 CUs twice
   const long long big_tiles = (long long)((d->M + 255) / 256) * ((d->N + 255) / 256) * batch;
   const int impl = getenv_big();
-  const bool big = impl > 0 && d->K % 64 == 0 && d->M >= 256 && d->N >= 256 && big_tiles >= 512 &&
+  a.ksplit = 1;
+  // split-K (fp32 accumulate-into-C GEMMs with few output tiles, i.e. the weight gradients): atomic-add epilogue
+  static int ksplit_env = -1;
+  if (ksplit_env < 0) {
+    const char* e = getenv("OBST_GEMM_KSPLIT");
+    ksplit_env = e ? atoi(e) : 1;
+  }
+  a.ws = nullptr;
+  if (ksplit_env > 0 && impl >= 2 && big_tiles < 512 && d->out_f32 && !d->R && !d->act && d->mode == 0 &&
+      batch == 1 && d->M >= 256 && d->N >= 256 && d->N % 4 == 0) {
+    int ks = 1;
+    const long long want = 256LL * ksplit_env;   // blocks: one (or ksplit_env) per CU
+    while (big_tiles * ks < want && d->K % (64 * ks * 2) == 0 && d->K / (ks * 2) >= 1024) ks *= 2;
+    if (ks > 1) {
+      a.ws = splitk_workspace((size_t)ks * d->M * d->N * sizeof(float));
+      if (!a.ws) ks = 1;
+    }
+    a.ksplit = ks;
+  }
+  const bool big = impl > 0 && d->K % 64 == 0 && d->M >= 256 && d->N >= 256 &&
+                   big_tiles * a.ksplit >= (a.ksplit > 1 ? 256 : 512) &&
                    (d->a_t == 0 || d->M % 8 == 0) && (d->b_t == 0 || d->N % 8 == 0);
   if (big) {
 #define OBST_GEMM256_CASE(AT, BT, F)                                                             \

@@ -182,6 +182,7 @@ class ParamStore:
             t.main_grad = self.grad_view(name)
             t.master = self.master_view(name)
             t.var_name = name
+            t.store = self
             self._leaves[name] = t
         return t
 
@@ -189,6 +190,27 @@ class ParamStore:
         """master (fp32) → compute (bf16) copy; the fused optimizer kernel does this itself on the GPU."""
         if self.compute is not self.master:
             self.compute.copy_(self.master)
+        self.bump()
+
+    def bump(self):
+        """the compute copy changed (optimizer step, restore): cached transposed weights are stale"""
+        self.version = getattr(self, "version", 0) + 1
+
+    def transposed(self, name: str, H: int, K: int, N: int) -> torch.Tensor:
+        """bf16 copy of a linear weight with every [K][N] block stored as [N][K] (same flat offsets as ``compute``,
+        so weights adjacent in ``compute`` stay adjacent here). Re-transposed lazily after each ``bump``."""
+        from ..ops import raw
+        s = self.specs[name]
+        if getattr(self, "compute_t", None) is None:
+            self.compute_t = torch.empty_like(self.compute)
+            self._t_version: typing.Dict[str, int] = {}
+        out = self.compute_t[s.offset:s.offset + s.numel]
+        ver = getattr(self, "version", 0)
+        if self._t_version.get(name) != ver:
+            src = self.compute[s.offset:s.offset + s.numel]
+            raw.transpose(src, out, K, N, N, K, H, K * N, K * N)
+            self._t_version[name] = ver
+        return out
 
     def zero_grad(self):
         self.grad.zero_()

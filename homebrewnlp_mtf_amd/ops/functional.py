@@ -88,10 +88,36 @@ def linear_plan(xdims: tuple, wdims: tuple, odims: tuple) -> LinearPlan:
     return LinearPlan(list(xdims), list(wdims), list(odims))
 
 
+# K-contiguous operands only on the GPU (ds_read_b128 fragments; the transposed-read path is 25-35 % slower):
+# the forward GEMM reads a cached [N][K] copy of each weight, the weight gradient reads token-contiguous
+# transposes of x and dy (`OBST_TRANSPOSED_OPERANDS=0` turns both off for A/B measurements).
+_KCONTIG = __import__("os").environ.get("OBST_TRANSPOSED_OPERANDS", "1") != "0"
+
+
+def _wT(w, plan: LinearPlan):
+    store = getattr(w, "store", None)
+    if not _KCONTIG or store is None or not raw.on_gpu(w) or w.dtype != torch.bfloat16:
+        return None
+    if plan.K % 8 or plan.N % 8:
+        return None
+    return store.transposed(w.var_name, plan.H, plan.K, plan.N)
+
+
 def _fwd_gemm(x2, w, y2, plan: LinearPlan, act=None, R=None, Zout=None):
     M, H, K, N = plan.M, plan.H, plan.K, plan.N
-    raw.gemm(raw.Operand(x2, 0, H * K, K), raw.Operand(w, 1, N, K * N), raw.Operand(y2, 0, H * N, N),
+    wt = _wT(w, plan)
+    bop = raw.Operand(wt, 0, K, K * N) if wt is not None else raw.Operand(w, 1, N, K * N)
+    raw.gemm(raw.Operand(x2, 0, H * K, K), bop, raw.Operand(y2, 0, H * N, N),
              M, N, K, batch=(H, 1), act=act, R=R, Zout=Zout)
+
+
+def tokens_transposed(x2, rows: int, cols: int) -> typing.Optional[torch.Tensor]:
+    """[rows][cols] bf16 -> [cols][rows] (None where the plain transposed-read GEMM is used instead)"""
+    if not _KCONTIG or not raw.on_gpu(x2) or x2.dtype != torch.bfloat16 or rows % 8 or cols % 8:
+        return None
+    out = torch.empty(cols * rows, dtype=x2.dtype, device=x2.device)
+    raw.transpose(x2, out, rows, cols, cols, rows)
+    return out
 
 
 def _dgrad_gemm(dy2, w, dx2, plan: LinearPlan, act=None, Zin=None, R=None):
@@ -100,8 +126,18 @@ def _dgrad_gemm(dy2, w, dx2, plan: LinearPlan, act=None, Zin=None, R=None):
              M, K, N, batch=(H, 1), act=act, act_bwd=Zin is not None, Zin=Zin, R=R)
 
 
-def _wgrad_gemm(x2, dy2, gw, plan: LinearPlan):
+def _wgrad_gemm(x2, dy2, gw, plan: LinearPlan, xT=None, dyT=None):
+    """gw[H][K][N] += x[M][H][K]ᵀ · dy[M][H][N]; with token-contiguous transposes (xT [H*K][M], dyT [H*N][M]) both
+    operands are K-contiguous"""
     M, H, K, N = plan.M, plan.H, plan.K, plan.N
+    if xT is None:
+        xT = tokens_transposed(x2, M, H * K)
+    if xT is not None and dyT is None:
+        dyT = tokens_transposed(dy2, M, H * N)
+    if xT is not None and dyT is not None:
+        raw.gemm(raw.Operand(xT, 0, M, K * M), raw.Operand(dyT, 0, M, N * M), raw.Operand(gw, 0, N, K * N),
+                 K, N, M, batch=(H, 1), beta=1.0)
+        return
     raw.gemm(raw.Operand(x2, 1, H * K, K), raw.Operand(dy2, 1, H * N, N), raw.Operand(gw, 0, N, K * N),
              K, N, M, batch=(H, 1), beta=1.0)
 
@@ -278,12 +314,19 @@ class _DotAttention(torch.autograd.Function):
         dbase = _empty(p_in.canon_o_shape, xc)
         ws = (w_k, w_q, w_v)
         outs = []
+        Mo, Ko, No = p_out.M, p_out.H * p_out.K, p_out.H * p_out.N
+        baseT = tokens_transposed(base, Mo, Ko)
+        dkqvT = None
+        if baseT is not None and Mo % 8 == 0 and No % 8 == 0:
+            dkqvT = torch.empty(3 * No * Mo, dtype=dkqv.dtype, device=dkqv.device)
+            raw.transpose(dkqv, dkqvT, Mo, No, No, Mo, 3, Mo * No, Mo * No)
         for j in range(3):
             last = j == 2
             _dgrad_gemm(dkqv[j], ws[j], dbase, p_out, act=act if last else None,
                         Zin=z if (last and act) else None, R=dbase if j > 0 else None)
             g, m = _acc_grad(ws[j])
-            _wgrad_gemm(base, dkqv[j], g, p_out)
+            _wgrad_gemm(base, dkqv[j], g, p_out, xT=baseT,
+                        dyT=None if dkqvT is None else dkqvT[j * No * Mo:(j + 1) * No * Mo])
             _done(ws[j])
             outs.append(None if m else g.to(ws[j].dtype))
         if p_out.col_parallel and pstate.tp_size() > 1:
@@ -307,8 +350,14 @@ def _qkv_fwd(base, ws, out, p: LinearPlan):
     same = (H == 1 and stride > 0 and stride % es == 0 and ws[2].data_ptr() - ws[1].data_ptr() == stride
             and all(w.is_contiguous() for w in ws))
     if same:
-        raw.gemm(raw.Operand(base, 0, K, 0), raw.Operand(ws[0], 1, N, stride // es), raw.Operand(out, 0, N, M * N),
-                 M, N, K, batch=(3, 1))
+        wt = _wT(ws[0], p)
+        if wt is not None:
+            for j in (1, 2):
+                _wT(ws[j], p)           # refresh the neighbours' transposed copies too
+            bop = raw.Operand(wt, 0, K, stride // es)
+        else:
+            bop = raw.Operand(ws[0], 1, N, stride // es)
+        raw.gemm(raw.Operand(base, 0, K, 0), bop, raw.Operand(out, 0, N, M * N), M, N, K, batch=(3, 1))
     else:
         for j in range(3):
             _fwd_gemm(base, ws[j], out[j], p)

@@ -403,6 +403,23 @@ def dot(x, dy, out):
     out.view(-1)[0] += (_f(x) * _f(dy)).sum()
 
 
+def transpose(x, y, rows: int, cols: int, ldx: int, ldy: int, batch: int = 1, sx: int = 0, sy: int = 0):
+    """y[b][c][r] = x[b][r][c] (bf16 on the GPU; any dtype on the CPU)"""
+    if x.device.type == "meta":
+        return None
+    if on_gpu(x):
+        if x.dtype != torch.bfloat16 or y.dtype != torch.bfloat16:
+            raise L.KernelError("transpose is bf16")
+        _need(x, (batch - 1) * sx + (rows - 1) * ldx + cols - 1, "x")
+        _need(y, (batch - 1) * sy + (cols - 1) * ldy + rows - 1, "y")
+        L.check(L.lib().obst_transpose(x.data_ptr(), y.data_ptr(), rows, cols, ldx, ldy, batch, sx, sy,
+                                       L.stream_ptr()), "transpose")
+        return
+    xv = torch.as_strided(x, (batch, rows, cols), (sx, ldx, 1), x.storage_offset())
+    yv = torch.as_strided(y, (batch, cols, rows), (sy, ldy, 1), y.storage_offset())
+    yv.copy_(xv.transpose(1, 2))
+
+
 def gather(idx, table, out, T: int, F: int, V: int):
     if table.device.type == "meta":
         return None

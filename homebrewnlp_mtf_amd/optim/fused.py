@@ -253,6 +253,7 @@ class FusedOptimizer:
                 self._reduce_stats()
             if not last:
                 src, bi = bufs[bi], 1 - bi
+        self.store.bump()
         if self.sm3 is not None:
             if self.tp > 1 and self.sm3_red_start < self.sm3_total:
                 dist.all_reduce(self.sm3[1 - self.flip][self.sm3_red_start:], op=dist.ReduceOp.MAX,

@@ -227,3 +227,22 @@ def test_gemm_big_tile(cuda, a_t, b_t, K):
     raw.gemm(raw.Operand(Ad, a_t, lda), raw.Operand(Bd, b_t, ldb), raw.Operand(Cf, 0, N), M, N, K, beta=1.0)
     torch.cuda.synchronize()
     _close(Cf.view(M, N), ref + 1, 2e-2, 2e-2, f"gemm256 f32 {a_t}{b_t} K{K}")
+
+
+@pytest.mark.parametrize("a_t,b_t", [(0, 0), (1, 1)])
+def test_gemm_splitk_wgrad(cuda, a_t, b_t):
+    """few output tiles + long K + fp32 accumulate: the phase kernel splits K into a workspace and reduces"""
+    torch.manual_seed(5)
+    M, N, K = 1024, 1536, 16384
+    A = (torch.randn(M * K) * 0.5).to(BF)
+    B = (torch.randn(N * K) * 0.5).to(BF)
+    lda = K if a_t == 0 else M
+    ldb = K if b_t == 0 else N
+    av = A.view(M, K) if a_t == 0 else A.view(K, M).t()
+    bv = B.view(N, K).t() if b_t == 0 else B.view(K, N)
+    ref = av.float() @ bv.float() + 2.0
+    Cf = torch.full((M * N,), 2.0, dtype=torch.float32, device=cuda)
+    raw.gemm(raw.Operand(A.to(cuda), a_t, lda), raw.Operand(B.to(cuda), b_t, ldb), raw.Operand(Cf, 0, N), M, N, K,
+             beta=1.0)
+    torch.cuda.synchronize()
+    _close(Cf.view(M, N), ref, 5e-2, 1e-2, f"splitk {a_t}{b_t}")

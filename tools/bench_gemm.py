@@ -17,6 +17,7 @@ SHAPES = [  # (name, M, N, K, a_t, b_t, out_f32)
     ("wgrad d x I", 2048, 4096, T, 1, 1, True), ("wgrad I x d", 4096, 2048, T, 1, 1, True),
     ("logits fwd", T, 50304, 2048, 0, 1, False), ("logits dgrad", T, 2048, 50304, 0, 0, False),
     ("logits wgrad", 2048, 50304, T, 1, 1, True),
+    ("wgradNT d x I", 2048, 4096, T, 0, 0, True), ("wgradNT I x d", 4096, 2048, T, 0, 0, True),
     ("sq8k NT", 8192, 8192, 8192, 0, 0, False), ("sq8k NN", 8192, 8192, 8192, 0, 1, False),
     ("sq8k TT f32", 8192, 8192, 8192, 1, 1, True), ("sq8k TN", 8192, 8192, 8192, 1, 0, False),
 ]
@@ -45,7 +46,7 @@ def main():
             torch.cuda.synchronize()
             dt = (time.perf_counter() - t) / n
             res[name].append(2 * M * N * K / dt / 1e12)
-    tag = os.environ.get("OBST_GEMM_BIG", "1")
+    tag = os.environ.get("OBST_GEMM_BIG", "2") + "/ks" + os.environ.get("OBST_GEMM_KSPLIT", "1")
     for name, *_ in SHAPES:
         v = sorted(res[name])
         print(f"[big={tag}] {name:14s} median {v[len(v) // 2]:7.1f} TFLOP/s  max {v[-1]:7.1f}")
