@@ -56,156 +56,274 @@ __device__ __forceinline__ void atomic_max_nonneg(float* addr, float v) {
   atomicMax(reinterpret_cast<int*>(addr), __float_as_int(v));   // valid for v >= 0 (IEEE ordering of non-negatives)
 }
 
-constexpr int SM3_WIN = 1024;  // per-dim LDS window of accumulator slots reduced inside the block
+// SM3 accumulator max (and Adafactor row/col sums) per chunk: every dim whose index takes few enough values inside
+// the chunk is reduced in an LDS window and flushed with one global atomic per slot; leading-dim updates are first
+// max-reduced across the wave when all its lanes share the index (the common case: a wave's 256 elements lie in one
+// row), so LDS atomics do not serialise on one address.
+constexpr int NTA = 512;          // apply threads (16 waves per CU at 2 blocks)
+constexpr int WIN_LEAD = 1024;    // LDS slots per leading dim
+constexpr int WIN_LAST = 16384;   // LDS slots for the contiguous trailing dim (>= any chunk's distinct indices)
 
-__global__ __launch_bounds__(NTH) void opt_apply_kernel(ApplyArgs a) {
+struct Windows {
+  int lo[4], cnt[4];              // cnt = 0: window unusable -> global atomics
+};
+
+__device__ __forceinline__ float* win_slot(float* lead, float* last, int d, int ndim) {
+  return d == ndim - 1 ? last : lead + d * WIN_LEAD;
+}
+
+__device__ __forceinline__ float wave_max_f(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// V consecutive elements of one tensor, starting at tensor-relative element e (multi-index idx of e; for V > 1 the
+// trailing dim is a multiple of V so all V share the leading indices)
+template <int V>
+__device__ __forceinline__ void apply_elems(const ApplyArgs& a, const OptTensor& T, const float* F, int tix, int e,
+                                            const int (&idx)[4], bool sm3_on, const Windows& W, float* wlead,
+                                            float* wlast, bool af, long long af_r0, bool af_rows_win,
+                                            bool af_cols_win, float deb1, float deb2, float& s1, float& s2) {
+  const long long gi = T.off + e;
+  float g[V], w[V];
+  if (V == 4) {
+    const float4 gv = a.uin ? *reinterpret_cast<const float4*>(a.uin + gi) : *reinterpret_cast<const float4*>(a.grad + gi);
+    const float4 wv = *reinterpret_cast<const float4*>(a.master + gi);
+    g[0] = gv.x; g[1] = gv.y; g[2] = gv.z; g[3] = gv.w;
+    w[0] = wv.x; w[1] = wv.y; w[2] = wv.z; w[3] = wv.w;
+    if (!a.uin) {
+#pragma unroll
+      for (int j = 0; j < V; ++j) g[j] *= a.grad_scale;
+    }
+  } else {
+    g[0] = a.uin ? a.uin[gi] : a.grad[gi] * a.grad_scale;
+    w[0] = a.master[gi];
+  }
+  const int last = T.ndim - 1;
+  for (int s = 0; s < a.nst; ++s) {
+    const Stage S = a.st[s];
+    switch (S.op) {
+      case OP_ADAPTIVE_CLIP: case OP_L2_CLIP: case OP_GLOBAL_L2_CLIP: case OP_ADAFACTOR_CLIP: case OP_SCALE:
+#pragma unroll
+        for (int j = 0; j < V; ++j) g[j] *= F[0];
+        break;
+      case OP_VALUE_CLIP:
+#pragma unroll
+        for (int j = 0; j < V; ++j) g[j] = fmaxf(fminf(g[j], S.a), -S.a);
+        break;
+      case OP_GRAD_CENTRAL:
+#pragma unroll
+        for (int j = 0; j < V; ++j) g[j] -= F[0];
+        break;
+      case OP_WEIGHT_CENTRAL:
+#pragma unroll
+        for (int j = 0; j < V; ++j) g[j] += F[1];
+        break;
+      case OP_SM3: {
+        if (T.ndim == 0) goto scalar_adam;
+        float lead = 3.4e38f;
+        for (int d = 0; d < last; ++d) lead = fminf(lead, a.sm3_old[T.sm3_off[d] + idx[d]]);
+        float nu[V], numax = 0.f;
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+          nu[j] = fminf(lead, a.sm3_old[T.sm3_off[last] + idx[last] + j]) + g[j] * g[j];
+          numax = fmaxf(numax, nu[j]);
+        }
+        // leading dims: one value per vector
+        for (int d = 0; d < last; ++d) {
+          const int i0 = __shfl(idx[d], 0, 64);
+          const bool uni = __builtin_amdgcn_ballot_w64(idx[d] != i0) == 0 &&
+                           __builtin_amdgcn_ballot_w64(1) == ~0ull;
+          float v = numax;
+          if (uni) v = wave_max_f(v);
+          if (!uni || (threadIdx.x & 63) == 0) {
+            if (W.cnt[d]) {
+              int slot = idx[d] - W.lo[d];
+              if (slot < 0) slot += T.dims[d];
+              atomicMax(reinterpret_cast<int*>(wlead + d * WIN_LEAD + slot), __float_as_int(v));
+            } else {
+              atomic_max_nonneg(a.sm3_new + T.sm3_off[d] + idx[d], v);
+            }
+          }
+        }
+        // trailing dim: V distinct slots
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+          if (W.cnt[last]) {
+            int slot = idx[last] + j - W.lo[last];
+            if (slot < 0) slot += T.dims[last];
+            atomicMax(reinterpret_cast<int*>(wlast + slot), __float_as_int(nu[j]));
+          } else {
+            atomic_max_nonneg(a.sm3_new + T.sm3_off[last] + idx[last] + j, nu[j]);
+          }
+          g[j] *= opt_rsqrt(nu[j]);
+        }
+        break;
+      }
+      case OP_MOMENTUM: {
+        float m[V];
+        if (V == 4) {
+          const float4 mv = *reinterpret_cast<const float4*>(a.mom + gi);
+          m[0] = mv.x; m[1] = mv.y; m[2] = mv.z; m[3] = mv.w;
+        } else {
+          m[0] = a.mom[gi];
+        }
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+          m[j] = S.a * m[j] + g[j] * S.b;
+          g[j] = S.c != 0.f ? g[j] + S.a * m[j] : m[j];
+        }
+        if (V == 4) *reinterpret_cast<float4*>(a.mom + gi) = make_float4(m[0], m[1], m[2], m[3]);
+        else a.mom[gi] = m[0];
+        break;
+      }
+      case OP_ADAM: {
+        if (T.ndim == 0) goto scalar_adam;
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+          const float v = a.adam_v[gi + j] * a.beta2 + g[j] * g[j] * (1.f - a.beta2);
+          const float m = a.adam_m[gi + j] * a.beta1 + g[j] * (1.f - a.beta1);
+          a.adam_v[gi + j] = v; a.adam_m[gi + j] = m;
+          g[j] = opt_rsqrt(v * deb2) * m * deb1;
+        }
+        break;
+      }
+      case OP_NOVOGRAD: {
+        if (T.ndim == 0) goto scalar_adam;
+        // F[2] = rsqrt-term of the OLD p2, F[3] = rsqrt-term of the debiased NEW p2 (scalar kernel)
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+          const float p1 = a.beta1 * a.mom[gi + j] + g[j] * F[2];
+          a.mom[gi + j] = p1;
+          g[j] = a.beta1 * p1 + g[j] * F[3];
+        }
+        break;
+      }
+      case OP_ADAFACTOR: {
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+          if (T.fac_rows == 0) {  // unfactored (<= 1-D): per-element second moment in adam_v
+            const float v = a.adam_v[gi + j] * F[4] + (g[j] * g[j] + 1e-30f) * (1.f - F[4]);
+            a.adam_v[gi + j] = v;
+            g[j] = g[j] * rsqrtf(v);
+          } else {
+            const int rr = (e + j) / T.fac_cols, cc = (e + j) % T.fac_cols;
+            const float R = a.af_old[T.fac_off + rr], C = a.af_old[T.fac_off + T.fac_rows + cc];
+            const float vhat = R * C * F[5];       // F[5] = 1 / mean(R)
+            g[j] = g[j] * rsqrtf(fmaxf(vhat, 1e-30f));
+          }
+        }
+        break;
+      }
+      case OP_LR:
+#pragma unroll
+        for (int j = 0; j < V; ++j) g[j] *= a.lr;
+        break;
+      default: break;
+    }
+    continue;
+  scalar_adam: {   // 0-dim tensors (always the scalar path, V == 1)
+      float* ss = a.sstate + tix * 4;
+      const float v = ss[1] * a.beta2 + g[0] * g[0] * (1.f - a.beta2);
+      const float m = ss[0] * a.beta1 + g[0] * (1.f - a.beta1);
+      ss[1] = v; ss[0] = m;
+      g[0] = opt_rsqrt(v * deb2) * m * deb1;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < V; ++j) {
+    if (a.emit_stats) { s2 += g[j] * g[j]; s1 += g[j]; }
+    if (af) {
+      const float v = g[j] * g[j] + 1e-30f;
+      const int r = (e + j) / T.fac_cols, c = (e + j) % T.fac_cols;
+      if (af_rows_win) atomicAdd(wlead + (r - af_r0), v);
+      else atomicAdd(a.af_rows_sum + T.fac_off + r, v);
+      if (af_cols_win) atomicAdd(wlast + c, v);
+      else atomicAdd(a.af_cols_sum + T.fac_off + T.fac_rows + c, v);
+    }
+  }
+  if (a.final_seg) {
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      if (T.flags & 2) g[j] *= a.rezero_mult;
+      if ((T.flags & 1) && a.wd > 0.f) g[j] += w[j] * a.lr * a.wd;
+      w[j] -= g[j];
+    }
+    if (V == 4) {
+      *reinterpret_cast<float4*>(a.master + gi) = make_float4(w[0], w[1], w[2], w[3]);
+      if (a.compute)
+        *reinterpret_cast<uint2*>(a.compute + gi) = make_uint2(pack_bf16x2(w[0], w[1]), pack_bf16x2(w[2], w[3]));
+    } else {
+      a.master[gi] = w[0];
+      if (a.compute) a.compute[gi] = f2bf(w[0]);
+    }
+  } else {
+    if (V == 4) *reinterpret_cast<float4*>(a.uout + gi) = make_float4(g[0], g[1], g[2], g[3]);
+    else a.uout[gi] = g[0];
+  }
+}
+
+__global__ __launch_bounds__(NTA) void opt_apply_kernel(ApplyArgs a) {
   const Chunk ck = a.chunks[blockIdx.x];
   const OptTensor T = a.tensors[ck.t];
   const float* F = a.fac + ck.t * 8;
   float s2 = 0.f, s1 = 0.f;
-  // SM3 accumulator max: dims whose index takes few values inside this chunk (leading dims) are max-reduced in
-  // LDS and flushed with one global atomic per slot; dims with many distinct indices (the contiguous trailing
-  // dim) go straight to global atomics, whose addresses are then all different (no contention).
-  __shared__ float sm3_lds[4][SM3_WIN];
-  int win_lo[4] = {0, 0, 0, 0}, win_cnt[4] = {0, 0, 0, 0};
-  bool has_sm3 = false;
-  for (int s = 0; s < a.nst; ++s) has_sm3 |= a.st[s].op == OP_SM3;
-  has_sm3 &= T.ndim > 0;
-  if (has_sm3) {
-    long long stride = 1;
+  __shared__ float wlead[3 * WIN_LEAD];
+  __shared__ float wlast[WIN_LAST];
+  Windows W;
+  for (int d = 0; d < 4; ++d) W.lo[d] = W.cnt[d] = 0;
+  bool sm3_on = false;
+  for (int s = 0; s < a.nst; ++s) sm3_on |= a.st[s].op == OP_SM3;
+  sm3_on &= T.ndim > 0;
+  const int start = (int)ck.start, len = (int)ck.len;
+  if (sm3_on) {
+    int stride = 1;
     for (int d = T.ndim - 1; d >= 0; --d) {
-      const long long span = (ck.len - 1) / stride + 2;
-      const int cnt = (int)(span < T.dims[d] ? span : T.dims[d]);
-      win_lo[d] = (int)((ck.start / stride) % T.dims[d]);
-      win_cnt[d] = cnt <= SM3_WIN ? cnt : 0;
+      const int span = (len - 1) / stride + 2;
+      const int cnt = span < T.dims[d] ? span : T.dims[d];
+      W.lo[d] = (start / stride) % T.dims[d];
+      W.cnt[d] = cnt <= (d == T.ndim - 1 ? WIN_LAST : WIN_LEAD) ? cnt : 0;
       stride *= T.dims[d];
+      float* wb = win_slot(wlead, wlast, d, T.ndim);
+      for (int i = threadIdx.x; i < W.cnt[d]; i += NTA) wb[i] = 0.f;
     }
-    for (int d = 0; d < 4; ++d)
-      for (int i = threadIdx.x; i < SM3_WIN; i += NTH) sm3_lds[d][i] = 0.f;
-    __syncthreads();
   }
-  // adafactor row/column sums of g^2: same LDS-window treatment (rows of this chunk, and all columns when few)
+  // adafactor row/column sums of g^2: rows of this chunk in wlead, all columns in wlast (when they fit)
   const bool af = a.emit_factored && T.fac_rows > 0;
   const long long af_r0 = af ? ck.start / T.fac_cols : 0;
-  const bool af_rows_win = af && ((ck.start + ck.len - 1) / T.fac_cols - af_r0 + 1) <= SM3_WIN;
-  const bool af_cols_win = af && T.fac_cols <= SM3_WIN;
+  const int af_nr = af ? (int)((ck.start + ck.len - 1) / T.fac_cols - af_r0 + 1) : 0;
+  const bool af_rows_win = af && af_nr <= 3 * WIN_LEAD;
+  const bool af_cols_win = af && T.fac_cols <= WIN_LAST;
   if (af) {
-    for (int d = 0; d < 2; ++d)
-      for (int i = threadIdx.x; i < SM3_WIN; i += NTH) sm3_lds[d][i] = 0.f;
-    __syncthreads();
+    for (int i = threadIdx.x; i < (af_rows_win ? af_nr : 0); i += NTA) wlead[i] = 0.f;
+    for (int i = threadIdx.x; i < (af_cols_win ? T.fac_cols : 0); i += NTA) wlast[i] = 0.f;
   }
+  __syncthreads();
   const float deb1 = 1.f / (1.f - powf(a.beta1, a.step_count));
   const float deb2 = 1.f / (1.f - powf(a.beta2, a.step_count));
-  for (long long e = ck.start + threadIdx.x; e < ck.start + ck.len; e += NTH) {
-    const long long gi = T.off + e;
-    float g = a.uin ? a.uin[gi] : a.grad[gi] * a.grad_scale;
-    const float w = a.master[gi];
-    // multi-index for SM3 / adafactor
+  const bool vec = T.ndim > 0 && (T.off & 3) == 0 && (start & 3) == 0 && (len & 3) == 0 &&
+                   (T.dims[T.ndim - 1] & 3) == 0 && (!af || (T.fac_cols & 3) == 0);
+  const int V = vec ? 4 : 1;
+  for (int e = start + threadIdx.x * V; e < start + len; e += NTA * V) {
     int idx[4] = {0, 0, 0, 0};
     {
-      long long r = e;
-      for (int d = T.ndim - 1; d >= 0; --d) { idx[d] = (int)(r % T.dims[d]); r /= T.dims[d]; }
+      int r = e;
+      for (int d = T.ndim - 1; d >= 0; --d) { idx[d] = r % T.dims[d]; r /= T.dims[d]; }
     }
-    for (int s = 0; s < a.nst; ++s) {
-      const Stage S = a.st[s];
-      switch (S.op) {
-        case OP_ADAPTIVE_CLIP: case OP_L2_CLIP: case OP_GLOBAL_L2_CLIP: case OP_ADAFACTOR_CLIP: case OP_SCALE:
-          g *= F[0]; break;
-        case OP_VALUE_CLIP: g = fmaxf(fminf(g, S.a), -S.a); break;
-        case OP_GRAD_CENTRAL: g -= F[0]; break;
-        case OP_WEIGHT_CENTRAL: g += F[1]; break;
-        case OP_SM3: {
-          if (T.ndim == 0) goto scalar_adam;
-          float nu = a.sm3_old[T.sm3_off[0] + idx[0]];
-          for (int d = 1; d < T.ndim; ++d) nu = fminf(nu, a.sm3_old[T.sm3_off[d] + idx[d]]);
-          nu += g * g;
-          for (int d = 0; d < T.ndim; ++d) {
-            if (win_cnt[d]) {
-              int slot = idx[d] - win_lo[d];
-              if (slot < 0) slot += T.dims[d];
-              atomicMax(reinterpret_cast<int*>(&sm3_lds[d][slot]), __float_as_int(nu));
-            } else {
-              atomic_max_nonneg(a.sm3_new + T.sm3_off[d] + idx[d], nu);
-            }
-          }
-          g *= opt_rsqrt(nu);
-          break;
-        }
-        case OP_MOMENTUM: {
-          const float st = S.a * a.mom[gi] + g * S.b;
-          a.mom[gi] = st;
-          g = S.c != 0.f ? g + S.a * st : st;
-          break;
-        }
-        case OP_ADAM: {
-          if (T.ndim == 0) goto scalar_adam;
-          const float v = a.adam_v[gi] * a.beta2 + g * g * (1.f - a.beta2);
-          const float m = a.adam_m[gi] * a.beta1 + g * (1.f - a.beta1);
-          a.adam_v[gi] = v; a.adam_m[gi] = m;
-          g = opt_rsqrt(v * deb2) * m * deb1;
-          break;
-        }
-        case OP_NOVOGRAD: {
-          if (T.ndim == 0) goto scalar_adam;
-          // F[2] = rsqrt-term of the OLD p2, F[3] = rsqrt-term of the debiased NEW p2 (scalar kernel)
-          const float p1 = a.beta1 * a.mom[gi] + g * F[2];
-          a.mom[gi] = p1;
-          g = a.beta1 * p1 + g * F[3];
-          break;
-        }
-        case OP_ADAFACTOR: {
-          if (T.fac_rows == 0) {  // unfactored (<= 1-D): per-element second moment in adam_v
-            const float v = a.adam_v[gi] * F[4] + (g * g + 1e-30f) * (1.f - F[4]);
-            a.adam_v[gi] = v;
-            g = g * rsqrtf(v);
-          } else {
-            const long long inner = T.fac_cols;
-            const long long rr = e / inner, cc = e % inner;
-            const float R = a.af_old[T.fac_off + rr], C = a.af_old[T.fac_off + T.fac_rows + cc];
-            const float vhat = R * C * F[5];       // F[5] = 1 / mean(R)
-            g = g * rsqrtf(fmaxf(vhat, 1e-30f));
-          }
-          break;
-        }
-        case OP_LR: g *= a.lr; break;
-        default: break;
-      }
-      continue;
-    scalar_adam: {
-        float* ss = a.sstate + ck.t * 4;
-        const float v = ss[1] * a.beta2 + g * g * (1.f - a.beta2);
-        const float m = ss[0] * a.beta1 + g * (1.f - a.beta1);
-        ss[1] = v; ss[0] = m;
-        g = opt_rsqrt(v * deb2) * m * deb1;
-      }
-    }
-    if (a.emit_stats) { s2 += g * g; s1 += g; }
-    if (a.emit_factored && T.fac_rows > 0) {
-      const long long inner = T.fac_cols;
-      const float v = g * g + 1e-30f;
-      const long long r = e / inner, c = e % inner;
-      if (af_rows_win) atomicAdd(&sm3_lds[0][r - af_r0], v);
-      else atomicAdd(a.af_rows_sum + T.fac_off + r, v);
-      if (af_cols_win) atomicAdd(&sm3_lds[1][c], v);
-      else atomicAdd(a.af_cols_sum + T.fac_off + T.fac_rows + c, v);
-    }
-    if (a.final_seg) {
-      if (T.flags & 2) g *= a.rezero_mult;
-      if ((T.flags & 1) && a.wd > 0.f) g += w * a.lr * a.wd;
-      const float nw = w - g;
-      a.master[gi] = nw;
-      if (a.compute) a.compute[gi] = f2bf(nw);
-    } else {
-      a.uout[gi] = g;
-    }
+    if (vec) apply_elems<4>(a, T, F, ck.t, e, idx, sm3_on, W, wlead, wlast, af, af_r0, af_rows_win, af_cols_win, deb1,
+                            deb2, s1, s2);
+    else apply_elems<1>(a, T, F, ck.t, e, idx, sm3_on, W, wlead, wlast, af, af_r0, af_rows_win, af_cols_win, deb1,
+                        deb2, s1, s2);
   }
-  if (has_sm3) {
+  if (sm3_on) {
     __syncthreads();
     for (int d = 0; d < T.ndim; ++d) {
-      for (int i = threadIdx.x; i < win_cnt[d]; i += NTH) {
-        const float v = sm3_lds[d][i];
+      const float* wb = win_slot(wlead, wlast, d, T.ndim);
+      for (int i = threadIdx.x; i < W.cnt[d]; i += NTA) {
+        const float v = wb[i];
         if (v > 0.f) {
-          int j = win_lo[d] + i;
+          int j = W.lo[d] + i;
           if (j >= T.dims[d]) j -= T.dims[d];
           atomic_max_nonneg(a.sm3_new + T.sm3_off[d] + j, v);
         }
@@ -214,32 +332,41 @@ __global__ __launch_bounds__(NTH) void opt_apply_kernel(ApplyArgs a) {
   }
   if (af) {
     __syncthreads();
-    if (af_rows_win) {
-      const int nr = (int)((ck.start + ck.len - 1) / T.fac_cols - af_r0 + 1);
-      for (int i = threadIdx.x; i < nr; i += NTH) atomicAdd(a.af_rows_sum + T.fac_off + af_r0 + i, sm3_lds[0][i]);
-    }
+    if (af_rows_win)
+      for (int i = threadIdx.x; i < af_nr; i += NTA) atomicAdd(a.af_rows_sum + T.fac_off + af_r0 + i, wlead[i]);
     if (af_cols_win)
-      for (int i = threadIdx.x; i < T.fac_cols; i += NTH)
-        atomicAdd(a.af_cols_sum + T.fac_off + T.fac_rows + i, sm3_lds[1][i]);
+      for (int i = threadIdx.x; i < T.fac_cols; i += NTA) atomicAdd(a.af_cols_sum + T.fac_off + T.fac_rows + i, wlast[i]);
   }
   if (a.emit_stats) {
-    __shared__ float red[4];
-    s2 = block_sum<4>(s2, red);
-    s1 = block_sum<4>(s1, red);
+    __shared__ float red[8];
+    s2 = block_sum<8>(s2, red);
+    s1 = block_sum<8>(s1, red);
     if (threadIdx.x == 0) { atomicAdd(a.stats + ck.t * 8 + 0, s2); atomicAdd(a.stats + ck.t * 8 + 1, s1); }
   }
 }
 
-// pass 0: sum g^2, sum g of the (scaled) raw gradient, sum w^2, sum w of the weights
+// pass 0: sum g^2, sum g of the (scaled) raw gradient, sum w^2, sum w of the weights (float4 when aligned)
 __global__ __launch_bounds__(NTH) void opt_stats_kernel(const OptTensor* tensors, const Chunk* chunks,
                                                         const float* grad, const float* master, float* stats,
                                                         float grad_scale) {
   const Chunk ck = chunks[blockIdx.x];
   const OptTensor T = tensors[ck.t];
   float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-  for (long long e = ck.start + threadIdx.x; e < ck.start + ck.len; e += NTH) {
-    const float g = grad[T.off + e] * grad_scale, w = master[T.off + e];
-    a0 += g * g; a1 += g; a2 += w * w; a3 += w;
+  const long long base = T.off + ck.start;
+  if ((base & 3) == 0 && (ck.len & 3) == 0) {
+    const float4* g4 = reinterpret_cast<const float4*>(grad + base);
+    const float4* w4 = reinterpret_cast<const float4*>(master + base);
+    for (long long v = threadIdx.x; v < ck.len / 4; v += NTH) {
+      const float4 g = g4[v], w = w4[v];
+      const float gx = g.x * grad_scale, gy = g.y * grad_scale, gz = g.z * grad_scale, gw = g.w * grad_scale;
+      a0 += gx * gx + gy * gy + gz * gz + gw * gw; a1 += gx + gy + gz + gw;
+      a2 += w.x * w.x + w.y * w.y + w.z * w.z + w.w * w.w; a3 += w.x + w.y + w.z + w.w;
+    }
+  } else {
+    for (long long e = threadIdx.x; e < ck.len; e += NTH) {
+      const float g = grad[base + e] * grad_scale, w = master[base + e];
+      a0 += g * g; a1 += g; a2 += w * w; a3 += w;
+    }
   }
   __shared__ float red[4];
   a0 = block_sum<4>(a0, red); a1 = block_sum<4>(a1, red); a2 = block_sum<4>(a2, red); a3 = block_sum<4>(a3, red);
@@ -364,6 +491,6 @@ OBST_API int obst_opt_apply(const ObstOptDesc* d, hipStream_t s) {
   a.nst = d->nst; a.final_seg = d->final_seg; a.emit_stats = d->emit_stats; a.emit_factored = d->emit_factored;
   a.lr = d->lr; a.wd = d->wd; a.rezero_mult = d->rezero_mult; a.grad_scale = d->grad_scale;
   a.beta1 = d->beta1; a.beta2 = d->beta2; a.step_count = d->step_count;
-  hipLaunchKernelGGL(opt_apply_kernel, dim3(d->nchunks), dim3(NTH), 0, s, a);
+  hipLaunchKernelGGL(opt_apply_kernel, dim3(d->nchunks), dim3(NTA), 0, s, a);
   return (int)hipGetLastError();
 }

@@ -29,7 +29,7 @@ OP = dict(none=0, adaptive_clip=1, l2norm_clip=2, global_l2norm_clip=3, value_cl
           adafactor_clip=13, scale=14)
 REDUCTIONS = {"adaptive_clip", "l2norm_clip", "global_l2norm_clip", "gradient_centralisation", "novograd",
               "adafactor", "adafactor_clip"}
-CHUNK = 16384
+CHUNK = 65536
 
 
 def _f2i(x: float) -> int:
