@@ -59,22 +59,27 @@ class Model:
     def _dummy_inputs(self, device):
         p = self.params
         B = self.local_batch
-        x = torch.zeros([B, p.sequence_length // p.token_patch_size, p.token_patch_size], dtype=torch.int64,
-                        device=device) if p.use_language else None
+        x = None
+        if p.use_language:
+            shape = [B, p.sequence_length // p.token_patch_size, p.token_patch_size]
+            if p.use_video:   # jannet: [batch, time, language_token_patch, token_patch]
+                shape = [B, p.time_patch_size, p.language_token_patch, p.token_patch_size]
+            x = torch.zeros(shape, dtype=torch.int64, device=device)
         vid = None
         if p.use_video:
             shape = [B, p.time_patch_size + 1, p.frame_height_patch, p.frame_width_patch, p.channel_color_size]
             if not p.three_axes:
                 shape = [B, p.time_patch_size + 1, p.frame_height_patch * p.frame_width_patch, p.channel_color_size]
-            vid = torch.zeros(shape, dtype=self.dtype, device=device)
+            vid = torch.zeros(shape, dtype=torch.uint8, device=device)
         return {"token_x": x, "token_y": x, "frame": vid}
 
-    def forward(self, token_x=None, token_y=None, frame=None, vid_msk_src=None, vid_msk_tgt=None, train=True,
-                step_seed: int = 0) -> typing.Dict[str, torch.Tensor]:
+    def forward(self, token_x=None, token_y=None, frame=None, vid_msk_src=None, vid_msk_tgt=None, cat_mask_x=None,
+                cat_mask_y=None, txt_msk=None, train=True, step_seed: int = 0) -> typing.Dict[str, torch.Tensor]:
         self.builder.train = train
         self.builder.step_seed = step_seed
         return self._forward({"token_x": token_x, "token_y": token_y, "frame": frame,
-                              "vid_msk_src": vid_msk_src, "vid_msk_tgt": vid_msk_tgt})
+                              "vid_msk_src": vid_msk_src, "vid_msk_tgt": vid_msk_tgt,
+                              "cat_mask_x": cat_mask_x, "cat_mask_y": cat_mask_y})
 
     __call__ = forward
 
@@ -120,7 +125,19 @@ class Model:
                 return self._loss(frame_out, token_out, batch, vid_tgt)
 
     # ---------------------------------------------------------------------------------------------------------------
+    def _frames(self, vid: torch.Tensor) -> torch.Tensor:
+        """uint8 (or bit-folded int) frames -> activation dtype in [0, 1] (ref __init__.py:37-55)"""
+        p = self.builder.params
+        if p.use_bit_fold_input_pipeline:
+            v = vid.long()
+            base = 2 ** p.bit_fold_value
+            parts = [((v // base ** i) % base).to(torch.uint8) for i in range(p.fold_count)]
+            vid = torch.cat(parts, -1)
+        return vid.to(self.builder.dtype) / 255.0
+
     def _input(self, batch):
+        """ref src/model/__init__.py:32-91: video patches and/or language tokens -> features; jannet concatenates
+        language tokens and frame patches along the spatial ("height") axis."""
         b = self.builder
         p = b.params
         tgt = None
@@ -129,26 +146,30 @@ class Model:
             vid = batch["frame"]
             vdims = [Dim("batch", vid.shape[0]), Dim("_sequence", vid.shape[1])]
             vdims += [Dim("height", vid.shape[2])] + ([Dim("width", vid.shape[3])] if p.three_axes else [])
-            vdims += [p.color_channel_dim]
-            v = vid.to(b.dtype) / 255.0
+            v = self._frames(vid)
+            vdims += [Dim(p.color_channel_dim.name, v.shape[-1])]
+            v = dropout(BlockArgs(b, Act(v, vdims), [f"dropout_rate{p.input_dropout}"])).t
             seq = Dim("sequence", vid.shape[1] - 1)
-            src_t, tgt_t = v[:, :-1], v[:, 1:]
             sdims = [vdims[0], seq] + vdims[2:]
-            src = Act(src_t.contiguous(), sdims)
-            tgt = Act(tgt_t.contiguous(), sdims)
+            src = Act(v[:, :-1].contiguous(), sdims)
+            tgt = Act(v[:, 1:].contiguous(), sdims)
             args = BlockArgs(b, src, [''])
             if p.empty_frame_embedding is not None:
                 e = embed(args(list(p.empty_frame_embedding)), sdims[2:])
-                msk = batch.get("vid_msk_src")
-                if msk is not None:
-                    m = msk.to(b.dtype).view(list(msk.shape) + [1] * (len(sdims) - 2))
-                    src = Act(src.t * m + e.t * (1 - m), sdims)
-            src = linear_to_features(args(src), [p.color_channel_dim])
+                for key in ("vid_msk_src", "cat_mask_x"):       # weighted_add(src, embed, mask) twice (ref :60-62)
+                    msk = batch.get(key)
+                    if msk is not None:
+                        m = msk.to(b.dtype).view(list(msk.shape) + [1] * (len(sdims) - 2))
+                        src = Act(src.t * m + e.t.unsqueeze(0).unsqueeze(0) * (1 - m), sdims)
+            src = linear_to_features(args(src), [sdims[-1]])
             for ci, cfg in enumerate(p.input_block_configs):
                 src = block_part_fn(b, cfg, src, 0, ci, prefix="vid_inp")
         if p.use_language:
             tok = batch["token_x"]
-            tdims = [Dim("batch", tok.shape[0]), Dim("sequence", tok.shape[1]), p.token_patch_dim]
+            tdims = [Dim("batch", tok.shape[0]), Dim("sequence", tok.shape[1])]
+            if tok.dim() == 4:                                    # jannet: [batch, time, lang_patch, token_patch]
+                tdims.append(Dim("height", tok.shape[2]))
+            tdims.append(p.token_patch_dim)
             args = BlockArgs(b, Act(tok, tdims), [''])
             inter = Dim(p.intermediate[0].name, int(p.intermediate[0].size * p.vocab_weight_factorization))
             txt = gather_embed(args(list(p.token_embedding)), [p.vocab_dim, inter], tok, tdims)
@@ -157,9 +178,9 @@ class Model:
             for ci, cfg in enumerate(p.input_block_configs):
                 txt = block_part_fn(b, cfg, txt, 0, ci, prefix="lang_inp")
             if src is not None:
-                # language tokens concatenated with video on the spatial axis (ref __init__.py:87-88)
-                raise NotImplementedError("joint language+video input concatenation")
-            src = txt
+                src = _concat_height(txt, src)
+            else:
+                src = txt
         if p.use_initial_position_embedding:
             args = BlockArgs(b, src, [''])
             for dim in D.subtract(src.dims, p.feature_dims)[1:]:
@@ -168,14 +189,17 @@ class Model:
         return src, tgt
 
     def _output(self, out: Act):
+        """ref src/model/__init__.py:133-156: the first language_token_patch spatial slots are tokens, the rest frames"""
         b = self.builder
         p = b.params
         token_out = frame_out = None
-        args = BlockArgs(b, out, [''])
+        joint = p.use_video and p.use_language
+        lp = p.language_token_patch
         if p.use_language:
-            x = out
+            x = _slice_height(out, 0, lp) if joint else out
             for ci, cfg in enumerate(p.output_block_configs):
                 x = block_part_fn(b, cfg, x, 0, ci, prefix="lang_out")
+            args = BlockArgs(b, x, [''])
             new = [p.token_patch_dim, p.vocab_dim]
             w = embed(args(x, list(p.output_embedding)), list(p.feature_dims) + new)
             odims = D.subtract(x.dims, p.feature_dims) + new
@@ -185,10 +209,10 @@ class Model:
                 y = F.tp_reduce(named_einsum([x, w], odims).t)
             token_out = Act(y, odims)
         if p.use_video:
-            x = out
+            x = _slice_height(out, lp, None) if joint else out
             for ci, cfg in enumerate(p.output_block_configs):
                 x = block_part_fn(b, cfg, x, 0, ci, prefix="vid_out")
-            y = linear(args(x), p.feature_dims, [p.color_channel_dim])
+            y = linear(BlockArgs(b, x, ['']), p.feature_dims, [p.color_channel_dim])
             frame_out = Act(torch.sigmoid(y.t.float()).to(y.t.dtype), y.dims)
         return frame_out, token_out
 
@@ -208,19 +232,52 @@ class Model:
             res["accuracy"] = acc
             losses.append(loss)
         if p.use_video:
-            out = frame_out.t.float() - vid_tgt.t.float()
-            msk = batch.get("vid_msk_tgt")
-            if msk is not None:
-                m = msk.float().view(list(msk.shape) + [1] * (out.dim() - msk.dim()))
-                out = out * m
-            vloss = (out * torch.sign(out.detach())).sum() / out.numel()   # ref __init__.py:189-192
-            res["video_loss"] = vloss
-            losses.append(vloss)
+            if self.builder.register:
+                vloss = torch.zeros([], device="meta")
+                res["video_loss"] = vloss
+                losses.append(vloss)
+            else:
+                out = frame_out.t.float() - vid_tgt.t.float()
+                scale = 1.0
+                for key in ("vid_msk_tgt", "cat_mask_y"):
+                    msk = batch.get(key)
+                    if msk is not None:
+                        m = msk.float().view(list(msk.shape) + [1] * (out.dim() - msk.dim()))
+                        out = out * m
+                        scale *= msk.numel() / msk.float().sum().clamp(min=1.0)
+                vloss = (out * torch.sign(out.detach())).sum() / out.numel()   # ref __init__.py:187-199
+                losses.append(vloss)
+                res["video_loss"] = vloss.detach() * scale                  # reported loss rescaled by the masks
+        if not losses:
+            raise ValueError("neither use_language nor use_video")
         total = losses[0]
         for extra in losses[1:]:
             total = total + extra
         res["loss"] = total
         return res
+
+
+def _concat_height(a: Act, b: Act) -> Act:
+    """concatenate two activations along their "height" axis (all other dims equal)"""
+    ia = [d.name for d in a.dims].index("height")
+    ib = [d.name for d in b.dims].index("height")
+    rest_a = [d for d in a.dims if d.name != "height"]
+    rest_b = [d for d in b.dims if d.name != "height"]
+    if rest_a != rest_b or ia != ib:
+        raise ValueError(f"cannot concatenate {a.dims} and {b.dims} along height (jannet needs three_axes=false)")
+    t = torch.cat([a.t, b.t], ia)
+    dims = list(a.dims)
+    dims[ia] = Dim("height", a.dims[ia].size + b.dims[ib].size)
+    return Act(t, dims)
+
+
+def _slice_height(x: Act, start: int, stop: typing.Optional[int]) -> Act:
+    i = [d.name for d in x.dims].index("height")
+    stop = x.dims[i].size if stop is None else stop
+    t = x.t.narrow(i, start, stop - start).contiguous()
+    dims = list(x.dims)
+    dims[i] = Dim("height", stop - start)
+    return Act(t, dims)
 
 
 def _bcast(pe: Act, like: Act) -> torch.Tensor:

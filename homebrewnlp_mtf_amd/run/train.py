@@ -51,7 +51,15 @@ def train(params: ModelParameter, debug_grad: bool = False, synthetic: bool = Fa
             step, data_state = ckpt.restore(trainer, path)
             log(f"resumed from {path} at step {step}")
     trainer.global_step = step
-    if synthetic or not params.dataset_configs:
+    if params.model_mode == "jannet":
+        from ..data import video
+        if synthetic or not params.dataset_configs:
+            feeder = video.SyntheticVideo(params, trainer.local_batch, dev, seed=1000 * mesh.dp_rank + step)
+        else:
+            feeder = video.jannet_input(params, trainer.local_batch, mesh.dp_rank, mesh.dp, dev)
+            if data_state is not None and hasattr(feeder, "restore"):
+                feeder.restore(data_state)
+    elif synthetic or not params.dataset_configs:
         feeder = data.SyntheticText(params, trainer.local_batch, dev, seed=1000 * mesh.dp_rank + step)
     else:
         feeder = data.text_input(params, trainer.local_batch, mesh.dp_rank, mesh.dp, dev, state=data_state,

@@ -93,3 +93,33 @@ def test_fused_optimizer_matches_reference(cuda, chain):
     scale = ref_store.master.abs().max().item()
     assert diff < 1e-4 * max(scale, 1.0), f"{chain}: fused vs reference max diff {diff}"
     assert torch.equal(m.store.compute, m.store.master.to(torch.bfloat16))
+
+
+def test_jannet_gpu_matches_cpu(cuda):
+    """video + language (jannet) through the HIP kernels vs the fp32 CPU oracle"""
+    cfg = dict(model_mode="jannet", use_video=True, use_language=True, three_axes=False, frame_width=64,
+               frame_height=32, patch_size=8, color_channels=3, time_patch=1, sequence_length=16,
+               language_token_per_frame=8, token_patch_size=1, vocab_size=256, experts=4, heads=4,
+               features_per_head=32, depth=2, train_batch_size=2, intermediate_feed_forward_multiplier=2,
+               memory_reduction_strategy="revnet", attention_scale="head",
+               block_config=[{"layer": ["norm-shift-scale", "attention-dot_product-context"]},
+                             {"layer": ["norm-shift-scale", "feed_forward-in:gelu"]}])
+    torch.manual_seed(0)
+    m_cpu, m_gpu = _pair(cfg, cuda)
+    p = m_cpu.params
+    frame = torch.randint(0, 256, (2, 17, 32, 3 * 64), dtype=torch.uint8)
+    tok = torch.randint(0, 256, (2, 17, 8, 1))
+    kw = dict(frame=frame, token_x=tok[:, :-1], token_y=tok[:, 1:])
+    out_c = m_cpu(**kw)
+    out_g = m_gpu(**{k: v.to(cuda) for k, v in kw.items()})
+    out_c["loss"].backward()
+    out_g["loss"].backward()
+    torch.cuda.synchronize()
+    for k in ("token_loss", "video_loss"):
+        a, b = float(out_c[k]), float(out_g[k])
+        assert abs(a - b) < 3e-2 * max(1.0, abs(a)), (k, a, b)
+    m_cpu.store.fold_leaf_grads()
+    m_gpu.store.fold_leaf_grads()
+    gc, gg = m_cpu.store.grad, m_gpu.store.grad.cpu()
+    cos = torch.nn.functional.cosine_similarity(gc, gg, dim=0).item()
+    assert cos > 0.98, cos

@@ -250,3 +250,33 @@ def test_gpt_cpu_plumbing_trains():
     for _ in range(30):
         last = float(tr.step(b)["loss"])
     assert last < first - 1.0, (first, last)
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# jannet (video) mode: frame patches, optional language tokens concatenated on the spatial axis
+@pytest.mark.parametrize("joint", [False, True])
+def test_jannet_forward_backward(joint):
+    torch.manual_seed(0)
+    cfg = dict(model_mode="jannet", use_video=True, use_language=joint, heads=2, features_per_head=8, depth=1,
+               sequence_length=4, time_patch=1, frame_width=16, frame_height=8, patch_size=4, color_channels=3,
+               three_axes=not joint, language_token_per_frame=4 if joint else 0, token_patch_size=1, vocab_size=32,
+               train_batch_size=2, intermediate_feed_forward_multiplier=2, memory_reduction_strategy="none",
+               calculation_dtype="float32", experts=4,
+               block_config=[{"layer": ["norm-shift-scale", "feed_forward-in:relu"], "skip": True},
+                             {"layer": ["norm-shift-scale", "attention-dot_product-context"], "skip": True}])
+    p = ModelParameter(cfg)
+    m = Model(p, "cpu")
+    hw = [p.frame_height_patch, p.frame_width_patch] if p.three_axes else [p.frame_height_patch * p.frame_width_patch]
+    frame = torch.randint(0, 256, [2, p.time_patch_size + 1] + hw + [p.channel_color_size], dtype=torch.uint8)
+    batch = {"frame": frame, "vid_msk_src": torch.ones(2, p.time_patch_size, dtype=torch.bool),
+             "vid_msk_tgt": torch.tensor([[1, 1, 0, 1], [1, 1, 1, 1]], dtype=torch.bool)}
+    if joint:
+        tok = torch.randint(0, 32, (2, p.time_patch_size + 1, p.language_token_patch, 1))
+        batch.update(token_x=tok[:, :-1], token_y=tok[:, 1:])
+    out = m(**batch)
+    assert torch.isfinite(out["loss"]) and "video_loss" in out
+    assert ("token_loss" in out) == joint
+    out["loss"].backward()
+    m.store.fold_leaf_grads()
+    names = [n for n in m.store.order if m.store.grad_view(n).abs().sum() > 0]
+    assert len(names) >= len(m.store.order) - 1, set(m.store.order) - set(names)

@@ -81,3 +81,59 @@ def test_text_prep_bytes_and_int64(tmp_path):
     assert tok.decode(ids.tolist(), skip_special_tokens=False).replace(" ", "")[:40] == open(txt).read().replace(" ", "")[:40]
     assert all(P._element_count(f) == len(T.Example(next(T.read_records(str(tmp_path / "i" / f)))).int64("text"))
                for f in files)
+
+
+def test_video_json_split_and_chunk(tmp_path):
+    import video_json
+    src = tmp_path / "v.json"
+    src.write_text(json.dumps({"id": list(range(10)), "duration": [100, 5, 300, 50, 70, 20, 400, 10, 60, 90]}))
+    ids, dur = video_json.split_equal([[i] for i in range(10)], [100, 5, 300, 50, 70, 20, 400, 10, 60, 90], 3, -1)
+    sums = [sum(d) for d in dur]
+    assert sum(sums) == 1105 and max(sums) - min(sums) <= 100
+    assert sorted(i for part in ids for (i,) in part) == list(range(10))
+    ci, cd = video_json.chunk(list(range(10)), [100, 5, 300, 50, 70, 20, 400, 10, 60, 90], 200)
+    assert sorted(i for c in ci for i in c) == list(range(10))
+    assert all(sum(d) >= 200 for d in cd[:-1])
+    assert video_json.main(["split", str(src), "2", "--prefix", str(tmp_path) + "/"]) == 0
+    assert (tmp_path / "work_split_1.json").exists()
+
+
+def test_video2tfrecord_and_jannet_loader(tmp_path):
+    pytest.importorskip("PIL")
+    import torch
+    import video2tfrecord
+    from homebrewnlp_mtf_amd.config import ModelParameter
+    from homebrewnlp_mtf_amd.data import video as V
+    rng = np.random.default_rng(0)
+    vids = []
+    for k in range(2):
+        arr = rng.integers(0, 256, (7, 8, 16, 3), dtype=np.uint8)
+        path = tmp_path / f"v{k}.npy"
+        np.save(path, arr)
+        vids.append(str(path))
+    texts = {"v0.npy": ["hi"] * 7, "v1.npy": ["there", "x"]}
+    (tmp_path / "t.json").write_text(json.dumps(texts))
+    out = tmp_path / "tfr"
+    assert video2tfrecord.main(["--out", str(out), "--name", "demo", "--width", "16", "--height", "8",
+                                "--text", str(tmp_path / "t.json"), "--language-token-per-frame", "4",
+                                "--videos-per-file", "1"] + vids) == 0
+    files = sorted(str(out / f) for f in os.listdir(out))
+    assert len(files) == 2
+    ex = T.Example(next(T.read_records(files[0])))
+    assert ex.int64("tokens").tolist() == [104, 105, 0, 0] and ex.int64("mask").tolist() == [2]
+    p = ModelParameter(dict(model_mode="jannet", use_video=True, use_language=True, heads=2, features_per_head=8,
+                            sequence_length=2, time_patch=1, frame_width=16, frame_height=8, patch_size=4,
+                            color_channels=3, three_axes=False, language_token_per_frame=4, token_patch_size=1,
+                            vocab_size=256, experts=4, interleaved_datasets=2))
+    src = V.VideoSource(files, p, batch=2, device="cpu", workers=2)
+    b = src.next()
+    assert b["frame"].shape == (2, 3, 8, 48) and b["frame"].dtype == torch.uint8
+    assert b["token_x"].shape == (2, 2, 4, 1) and b["vid_msk_src"].all()
+    # the first window of file 0 decodes back to the (JPEG-approximate) patches of frame 0
+    ref = V.decode_frame(video2tfrecord.encode_jpeg(np.load(vids[0])[0], 16, 8), p)
+    assert np.array_equal(b["frame"][0, 0].numpy(), ref)
+    st = src.consumed_state
+    nxt = src.next()
+    src2 = V.VideoSource(files, p, batch=2, device="cpu", workers=2)
+    src2.restore(st)
+    assert torch.equal(src2.next()["frame"], nxt["frame"])
