@@ -247,6 +247,7 @@ class Model:
                         scale *= msk.numel() / msk.float().sum().clamp(min=1.0)
                 vloss = (out * torch.sign(out.detach())).sum() / out.numel()   # ref __init__.py:187-199
                 losses.append(vloss)
+                res["video_loss_raw"] = vloss
                 res["video_loss"] = vloss.detach() * scale                  # reported loss rescaled by the masks
         if not losses:
             raise ValueError("neither use_language nor use_video")

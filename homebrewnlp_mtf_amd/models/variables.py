@@ -186,6 +186,11 @@ class ParamStore:
             self._leaves[name] = t
         return t
 
+    def grad_view_of(self, flat: torch.Tensor, name: str) -> torch.Tensor:
+        """view of variable `name` inside any flat buffer laid out like ``grad``"""
+        s = self.specs[name]
+        return flat[s.offset:s.offset + s.numel].view(s.local_shape)
+
     def sync_compute(self):
         """master (fp32) → compute (bf16) copy; the fused optimizer kernel does this itself on the GPU."""
         if self.compute is not self.master:

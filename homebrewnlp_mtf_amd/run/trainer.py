@@ -62,6 +62,9 @@ class Trainer:
 
     def step(self, batch: typing.Dict[str, torch.Tensor]) -> typing.Dict[str, torch.Tensor]:
         """one optimizer step; returns device-side metrics"""
+        p = self.params
+        if p.multi_loss_strategy in ("pcgrad", "mgda") and p.use_video and p.use_language:
+            return self._multi_loss_step(batch)
         self.store.zero_grad()
         micro = self._micro_batches(batch)
         metrics: typing.Dict[str, torch.Tensor] = {}
@@ -80,6 +83,65 @@ class Trainer:
                 v = v.detach().float()
                 metrics[k] = metrics.get(k, 0) + v / len(micro)
         self.grad_sync.finish(average=True)
+        lr = learning_rate(self.params, self.global_step)
+        self.opt.step(lr, self.global_step + 1)
+        self.global_step += 1
+        metrics["learning_rate"] = torch.tensor(lr)
+        return metrics
+
+    # ---------------------------------------------------------------------------------------------------------------
+    def _multi_loss_step(self, batch):
+        """token and video losses get separate (DP-averaged) gradients, combined per SURVEY A8 -- the reference
+        wires pcgrad/mgda but never calls them (src/optimizer/gradients.py:65-66, __init__.py:102-126):
+          pcgrad: g_i <- g_i - min(g_i . g_j, 0) / |g_j|^2 g_j per body variable (Yu et al. 2020), then summed;
+          mgda:   two-task min-norm weight gamma from the body-gradient dot products (Sener & Koltun 2018; the
+                  reference's min_gamma clamps), g = gamma g_token + (1 - gamma) g_video for every variable."""
+        store = self.store
+        micro = self._micro_batches(batch)
+        parts = []
+        metrics: typing.Dict[str, torch.Tensor] = {}
+        for li, key in enumerate(("token_loss", "video_loss_raw")):
+            store.zero_grad()
+            for i, mb in enumerate(micro):
+                out = self.model(**mb, train=True, step_seed=self.global_step * 131 + i)
+                (out[key] / len(micro)).backward()
+                store.fold_leaf_grads()
+                if li == 0:
+                    for k, v in out.items():
+                        metrics[k] = metrics.get(k, 0) + v.detach().float() / len(micro)
+            self.grad_sync.finish(average=True)
+            parts.append(store.grad.clone())
+        g1, g2 = parts
+        body = [n for n in store.order if "body" in n]
+
+        def dots(a, b):
+            out = torch.stack([(store.grad_view_of(a, n) * store.grad_view_of(b, n)).sum() for n in body]) \
+                if body else torch.zeros(0, device=a.device)
+            sharded = torch.tensor([store.specs[n].tp_dim is not None for n in body], device=a.device)
+            if pstate.tp_size() > 1 and body:
+                part = out * sharded
+                pstate.tp_all_reduce(part)
+                out = torch.where(sharded, part, out)
+            return out
+        if self.params.multi_loss_strategy == "pcgrad":
+            d12, d11, d22 = dots(g1, g2), dots(g1, g1), dots(g2, g2)
+            out = g1 + g2
+            for k, n in enumerate(body):
+                c = torch.clamp(d12[k], max=0.0)
+                v = store.grad_view_of(out, n)
+                v.sub_(c / (d22[k] + 1e-20) * store.grad_view_of(g2, n) + c / (d11[k] + 1e-20) * store.grad_view_of(g1, n))
+            store.grad.copy_(out)
+        else:
+            v11, v12, v22 = dots(g1, g1).sum(), dots(g1, g2).sum(), dots(g2, g2).sum()
+            min_gamma = 0.001
+            if float(v12) >= float(v11):
+                gamma = 1 - min_gamma
+            elif float(v12) >= float(v22):
+                gamma = min_gamma
+            else:
+                gamma = float((v22 - v12) / (v11 + v22 - 2 * v12))
+            store.grad.copy_(gamma * g1 + (1 - gamma) * g2)
+            metrics["mgda_gamma"] = torch.tensor(gamma)
         lr = learning_rate(self.params, self.global_step)
         self.opt.step(lr, self.global_step + 1)
         self.global_step += 1

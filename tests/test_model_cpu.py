@@ -280,3 +280,46 @@ def test_jannet_forward_backward(joint):
     m.store.fold_leaf_grads()
     names = [n for n in m.store.order if m.store.grad_view(n).abs().sum() > 0]
     assert len(names) >= len(m.store.order) - 1, set(m.store.order) - set(names)
+
+
+@pytest.mark.parametrize("strategy", ["pcgrad", "mgda"])
+def test_multi_loss_strategies(strategy):
+    from homebrewnlp_mtf_amd.run.trainer import Trainer
+    torch.manual_seed(0)
+    cfg = dict(model_mode="jannet", use_video=True, use_language=True, heads=2, features_per_head=8, depth=1,
+               sequence_length=4, time_patch=1, frame_width=16, frame_height=8, patch_size=4, color_channels=3,
+               three_axes=False, language_token_per_frame=4, token_patch_size=1, vocab_size=32, train_batch_size=2,
+               intermediate_feed_forward_multiplier=2, memory_reduction_strategy="none", calculation_dtype="float32",
+               experts=4, multi_loss_strategy=strategy, optimizer="learning_rate", learning_rate=0.1,
+               weight_decay=0.0, block_config=[{"layer": ["norm-shift-scale", "feed_forward-in:relu"], "skip": True}])
+    tr = Trainer(ModelParameter(cfg), "cpu")
+    frame = torch.randint(0, 256, (2, 5, 8, 48), dtype=torch.uint8)
+    tok = torch.randint(0, 32, (2, 5, 4, 1))
+    batch = dict(frame=frame, token_x=tok[:, :-1], token_y=tok[:, 1:])
+    # reference gradients of each loss
+    store = tr.store
+    grads = []
+    for key in ("token_loss", "video_loss_raw"):
+        store.zero_grad()
+        tr.model(**batch, train=True, step_seed=0)[key].backward()
+        store.fold_leaf_grads()
+        grads.append(store.grad.clone())
+    w0 = store.master.clone()
+    m = tr.step(batch)
+    upd = (w0 - store.master) / 0.1                       # plain SGD: the combined gradient
+    body = [n for n in store.order if "body" in n]
+    g1, g2 = grads
+    if strategy == "mgda":
+        gamma = float(m["mgda_gamma"])
+        assert 0.0 < gamma < 1.0
+        assert torch.allclose(upd, gamma * g1 + (1 - gamma) * g2, atol=1e-5)
+    else:
+        for n in store.order:
+            a, b, u = store.grad_view_of(g1, n), store.grad_view_of(g2, n), store.grad_view_of(upd, n)
+            if n in body:
+                d = (a * b).sum()
+                exp = a + b - min(float(d), 0) / float((b * b).sum() + 1e-20) * b - min(float(d), 0) / float(
+                    (a * a).sum() + 1e-20) * a
+            else:
+                exp = a + b
+            assert torch.allclose(u, exp, atol=1e-5), n
