@@ -629,6 +629,7 @@ def gather_embed(args: BlockArgs, shape: typing.List[Dim], idx: torch.Tensor, id
     """ref embedding.py:230-231: table [vocab, ...] gathered by integer indices."""
     with args.builder.scope("gather"):
         table = embed(args, shape)
+    args.builder.last_gather_table = table.t
     V = shape[0].size
     Fsz = D.size(shape[1:])
     if table.t.dim() != 2:

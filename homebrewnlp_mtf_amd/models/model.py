@@ -125,6 +125,19 @@ class Model:
                 return self._loss(frame_out, token_out, batch, vid_tgt)
 
     # ---------------------------------------------------------------------------------------------------------------
+    def _contrastive_samples(self, token_out: Act) -> torch.Tensor:
+        return _contrastive_samples_impl(token_out.t, token_out.dims, self.builder.params)
+
+    def _contrastive_embeddings(self, token_out: Act, tgt: torch.Tensor) -> torch.Tensor:
+        """ref __init__.py:172-179 taken literally: the features and the embedding table share no named dim, so both
+        einsums reduce to products of sums: (sum(out) * sum(E) - 2 * sum(out) * sum(E[tgt])) / (|out| * vocab)"""
+        p = self.builder.params
+        table = self._text_table
+        gathered = table[tgt.reshape(-1).long().clamp(0, table.shape[0] - 1)].float()
+        so = token_out.t.sum()
+        loss = so * table.float().sum() - 2 * so * gathered.sum()
+        return loss / (token_out.t.numel() * p.vocab_size)
+
     def _frames(self, vid: torch.Tensor) -> torch.Tensor:
         """uint8 (or bit-folded int) frames -> activation dtype in [0, 1] (ref __init__.py:37-55)"""
         p = self.builder.params
@@ -173,6 +186,7 @@ class Model:
             args = BlockArgs(b, Act(tok, tdims), [''])
             inter = Dim(p.intermediate[0].name, int(p.intermediate[0].size * p.vocab_weight_factorization))
             txt = gather_embed(args(list(p.token_embedding)), [p.vocab_dim, inter], tok, tdims)
+            self._text_table = b.last_gather_table
             txt = dropout(args(txt, [f"dropout_rate{p.input_dropout}"]))
             txt = linear_to_features(args(txt), [p.token_patch_dim, inter])
             for ci, cfg in enumerate(p.input_block_configs):
@@ -195,7 +209,15 @@ class Model:
         token_out = frame_out = None
         joint = p.use_video and p.use_language
         lp = p.language_token_patch
-        if p.use_language:
+        contrastive = p.contrastive_across_samples or p.contrastive_across_token_embeddings
+        if p.use_language and contrastive:
+            # ref __init__.py:138-139,165: the contrastive losses work on the body's features (no output embedding)
+            x = _slice_height(out, 0, lp) if joint else out
+            fi = [x.dims.index(d) for d in p.feature_dims]
+            t = x.t.float()
+            t = t / t.pow(2).sum(fi, keepdim=True).sqrt()
+            token_out = Act(t, x.dims)
+        elif p.use_language:
             x = _slice_height(out, 0, lp) if joint else out
             for ci, cfg in enumerate(p.output_block_configs):
                 x = block_part_fn(b, cfg, x, 0, ci, prefix="lang_out")
@@ -226,10 +248,15 @@ class Model:
             if self.builder.register:
                 loss = torch.zeros([], device="meta")
                 acc = torch.zeros([], device="meta")
+            elif p.contrastive_across_samples:
+                loss, acc = self._contrastive_samples(token_out), None
+            elif p.contrastive_across_token_embeddings:
+                loss, acc = self._contrastive_embeddings(token_out, tgt), None
             else:
                 loss, acc = F.softmax_xent(token_out.t, tgt, p.vocab_size, p.z_loss, n)
             res["token_loss"] = loss
-            res["accuracy"] = acc
+            if acc is not None:
+                res["accuracy"] = acc
             losses.append(loss)
         if p.use_video:
             if self.builder.register:
@@ -256,6 +283,17 @@ class Model:
             total = total + extra
         res["loss"] = total
         return res
+
+
+def _contrastive_samples_impl(t: torch.Tensor, dims, p) -> torch.Tensor:
+    """ref __init__.py:167-171: (|sum over batch|^2 / B - |sum over sequence|^2 / S) / (B S)"""
+    names = [d.name for d in dims]
+    bi, si = names.index("batch"), names.index("sequence")
+    over_samples = t.sum(si)
+    over_batch = t.sum(bi)
+    B, S = t.shape[bi], t.shape[si]
+    loss = over_batch.pow(2).sum() / B - over_samples.pow(2).sum() / S
+    return loss / (B * S)
 
 
 def _concat_height(a: Act, b: Act) -> Act:

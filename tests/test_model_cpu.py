@@ -323,3 +323,23 @@ def test_multi_loss_strategies(strategy):
             else:
                 exp = a + b
             assert torch.allclose(u, exp, atol=1e-5), n
+
+
+@pytest.mark.parametrize("kind", ["contrastive_across_samples", "contrastive_across_token_embeddings"])
+def test_contrastive_losses(kind):
+    torch.manual_seed(0)
+    cfg = dict(BASE, **{kind: True}, block_config=[{"layer": ["norm-shift-scale", "feed_forward-in:relu"],
+                                                    "skip": True}])
+    m = Model(ModelParameter(cfg), "cpu")
+    x = torch.randint(0, 50, (2, 8, 1))
+    out = m(x, x)
+    assert torch.isfinite(out["loss"]) and "accuracy" not in out
+    out["loss"].backward()
+    m.store.fold_leaf_grads()
+    assert m.store.grad.abs().sum() > 0
+    if kind == "contrastive_across_samples":
+        from homebrewnlp_mtf_amd.models.model import _contrastive_samples_impl
+        t = torch.randn(3, 5, 2, 4)
+        dims = [type("D", (), {"name": n})() for n in ("batch", "sequence", "heads", "features_per_head")]
+        ref = (t.sum(0).pow(2).sum() / 3 - t.sum(1).pow(2).sum() / 5) / 15
+        assert torch.allclose(_contrastive_samples_impl(t, dims, None), ref)
