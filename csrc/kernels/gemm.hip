@@ -34,6 +34,8 @@ struct GemmArgs {
   int tiles_m, tiles_n;
   float alpha, beta;      // beta: fp32 output only, C = alpha*acc + beta*C_old (gradient accumulation)
   int act, mode;          // mode 0: out = act(alpha*acc + R); mode 1: out = (alpha*acc + R) * act'(Zin)
+  int tri;                // 0 dense; 1 A lower-triangular (A[m][k] = 0 for k > m); 2 A upper-triangular (k < m);
+                          // 3 only C[m][n] with n <= m is produced (strictly-upper outputs get no contribution)
   int ksplit;             // phase kernel only: K split over blockIdx.y; partial tiles go to `ws` [split][M][N]
   float* ws;              // split-K workspace (fp32), summed into C by splitk_reduce_kernel
 };
@@ -184,6 +186,10 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(GemmArgs p) {
       float v[4];
 #pragma unroll
       for (int t = 0; t < 4; ++t) v[t] = p.alpha * acc[i][j][t];
+          if (p.tri == 3) {
+#pragma unroll
+            for (int t = 0; t < 4; ++t) if (n + t > m) v[t] = 0.f;
+          }
       if (OUT_F32) {
         float* C = reinterpret_cast<float*>(p.C) + idx;
         if (p.beta != 0.f) {
@@ -407,6 +413,10 @@ __global__ __launch_bounds__(NT2, 1) void gemm256_kernel(GemmArgs p) {
       float v[4];
 #pragma unroll
       for (int t = 0; t < 4; ++t) v[t] = p.alpha * acc[i][j][t];
+      if (p.tri == 3) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) if (n + t > m) v[t] = 0.f;
+      }
       epilogue_store<OUT_F32>(p, coff + (long long)m * p.ldc + n, v);
     }
   }
@@ -478,7 +488,10 @@ __global__ __launch_bounds__(NT2, 1) void gemm_ph_kernel(GemmArgs p) {
   const int m0 = tm * BM2, n0 = tn * BN2;
   const int split = blockIdx.y % p.ksplit, bidx = blockIdx.y / p.ksplit;
   const int b1 = bidx / p.nb2, b2 = bidx % p.nb2;
-  const int kspan = p.K / p.ksplit, kbeg = split * kspan;
+  int kspan = p.K / p.ksplit, kbeg = split * kspan;
+  if (p.tri == 1) kspan = min(p.K, (m0 + BM2 + BK - 1) / BK * BK);             // A[m][k] = 0 for k > m
+  if (p.tri == 2) { kbeg = min(m0 / BK * BK, p.K - BK); kspan = p.K - kbeg; }   // A[m][k] = 0 for k < m
+  if (p.tri == 3 && OUT_F32 && p.beta == 1.f && n0 > m0 + BM2 - 1) return;     // no output in this tile
   const bf16_t* A = p.A + b1 * p.a_s1 + b2 * p.a_s2 + (A_T == 0 ? (long long)kbeg : (long long)kbeg * p.lda);
   const bf16_t* B = p.B + b1 * p.b_s1 + b2 * p.b_s2 + (B_T == 0 ? (long long)kbeg : (long long)kbeg * p.ldb);
   const int nk = kspan / BK;
@@ -569,6 +582,10 @@ __global__ __launch_bounds__(NT2, 1) void gemm_ph_kernel(GemmArgs p) {
       float v[4];
 #pragma unroll
       for (int t = 0; t < 4; ++t) v[t] = p.alpha * acc[i][j][t];
+      if (p.tri == 3) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) if (n + t > m) v[t] = 0.f;
+      }
       if (OUT_F32 && p.ksplit > 1) {
         *reinterpret_cast<float4*>(p.ws + (long long)split * p.M * p.N + (long long)m * p.N + n) =
             make_float4(v[0], v[1], v[2], v[3]);
@@ -665,6 +682,7 @@ struct ObstGemmDesc {
   int M, N, K, batch1, batch2;
   int a_t, b_t, out_f32, act, mode;
   float alpha, beta;
+  int tri;
 };
 
 // Returns 0 on success, <0 on a host-side shape/alignment violation, >0 for a HIP error.
@@ -683,7 +701,9 @@ OBST_API int obst_gemm(const ObstGemmDesc* d, hipStream_t stream) {
   a.a_s1 = d->a_s1; a.a_s2 = d->a_s2; a.b_s1 = d->b_s1; a.b_s2 = d->b_s2; a.c_s1 = d->c_s1; a.c_s2 = d->c_s2;
   a.M = d->M; a.N = d->N; a.K = d->K; a.nb2 = d->batch2;
   a.tiles_m = (d->M + BM - 1) / BM; a.tiles_n = (d->N + BN - 1) / BN;
-  a.alpha = d->alpha; a.beta = d->beta; a.act = d->act; a.mode = d->mode;
+  a.alpha = d->alpha; a.beta = d->beta; a.act = d->act; a.mode = d->mode; a.tri = d->tri;
+  if (d->tri < 0 || d->tri > 3 || ((d->tri == 1 || d->tri == 2) && d->M != d->K) || (d->tri == 3 && d->M != d->N))
+    return -8;
   const int batch = d->batch1 * d->batch2;
   hipError_t e;
   // big-tile path: needs K % 64 == 0, M/N >= 256 and enough 256x256 tiles to fill the 256 CUs twice
@@ -697,7 +717,7 @@ OBST_API int obst_gemm(const ObstGemmDesc* d, hipStream_t stream) {
     ksplit_env = e ? atoi(e) : 1;
   }
   a.ws = nullptr;
-  if (ksplit_env > 0 && impl >= 2 && big_tiles < 512 && d->out_f32 && !d->R && !d->act && d->mode == 0 &&
+  if (ksplit_env > 0 && impl >= 2 && big_tiles < 512 && d->tri == 0 && d->out_f32 && !d->R && !d->act && d->mode == 0 &&
       batch == 1 && d->M >= 256 && d->N >= 256 && d->N % 4 == 0) {
     int ks = 1;
     const long long want = 256LL * ksplit_env;   // blocks: one (or ksplit_env) per CU

@@ -425,6 +425,17 @@ def _attention_fast_ok(args: BlockArgs, ins, outs) -> bool:
     return True
 
 
+def _mixer_fast_ok(args: BlockArgs, x: Act, dim: Dim) -> bool:
+    """the learned causal token mixer (biased_attention_map on the input as value) as one batched GEMM (K03)"""
+    p = args.params
+    if 'biased_attention_map' not in args or 'input_as_value' not in args:
+        return False
+    if any(k in args for k in ('dot_product', 'biased_softmax', 'scale_attention_map')):
+        return False
+    return (len(x.dims) == 4 and x.dims[0].name == "batch" and x.dims[1] == dim and
+            x.dims[2:] == list(p.feature_dims))
+
+
 def attention(args: BlockArgs) -> Act:
     """ref spatial.py:42-81 (all variants). Fast path: dot_product + context (causal flash attention)."""
     p = args.params
@@ -460,6 +471,10 @@ def attention(args: BlockArgs) -> Act:
             return Act(y, x.dims)
         except NotImplementedError:
             pass
+
+    if _mixer_fast_ok(args, x, dim):
+        bias = embed(args, [p.head_dim, dim, tmp])
+        return Act(F.token_mixer(x.t, bias.t, causal), x.dims)
 
     base = None
     if 'dot_product' in args or 'input_as_value' not in args:

@@ -371,6 +371,52 @@ def dot_attention(x, w_in, w_k, w_q, w_v, xdims, w_in_dims, base_dims, w_out_dim
 
 
 # ================================================================================================================
+# K03: learned token mixer (reference `attention-biased_attention_map-...-input_as_value`, spatial.py:19-23,72-81)
+#   y[b,s,h,f] = sum_{s'} (W[h,s,s'] * M[s,s']) x[b,s',h,f],   M = lower triangle incl. the diagonal when causal
+# One strided two-level-batched GEMM per pass (batch = batch x heads); the causal triangle is skipped tile-wise
+# (tri flags of the GEMM), so forward and dgrad run ~half the dense FLOPs and dW only fills the lower triangle.
+class _TokenMixer(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, causal: bool):
+        B, S, H, Fd = x.shape
+        xc = x.contiguous()
+        wm = torch.tril(w) if causal else w.contiguous()
+        y = torch.empty_like(xc)
+        hf = H * Fd
+        raw.gemm(raw.Operand(wm, 0, S, 0, S * S), raw.Operand(xc, 1, hf, S * hf, Fd), raw.Operand(y, 0, hf, S * hf, Fd),
+                 S, Fd, S, batch=(B, H), tri=1 if causal else 0)
+        ctx.save_for_backward(xc, wm, w)
+        ctx.causal = causal
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xc, wm, w = ctx.saved_tensors
+        B, S, H, Fd = xc.shape
+        hf = H * Fd
+        dy = dy.contiguous()
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(xc)
+            raw.gemm(raw.Operand(wm, 1, S, 0, S * S), raw.Operand(dy, 1, hf, S * hf, Fd),
+                     raw.Operand(dx, 0, hf, S * hf, Fd), S, Fd, S, batch=(B, H), tri=2 if ctx.causal else 0)
+        g, m = _acc_grad(w)
+        # dW[h] = dy_h · x_hᵀ over (batch, features): both operands as [H][S][B*F] (K-contiguous)
+        dyp = dy.permute(2, 1, 0, 3).reshape(H, S, B * Fd).contiguous()
+        xp = xc.permute(2, 1, 0, 3).reshape(H, S, B * Fd).contiguous()
+        kk = B * Fd
+        raw.gemm(raw.Operand(dyp, 0, kk, 0, S * kk), raw.Operand(xp, 0, kk, 0, S * kk), raw.Operand(g, 0, S, 0, S * S),
+                 S, S, kk, batch=(1, H), beta=1.0, tri=3 if ctx.causal else 0)
+        _done(w)
+        return dx, (None if m else g.to(w.dtype)), None
+
+
+def token_mixer(x, w, causal: bool):
+    """x [B, S, H, F], w [H, S, S] (query, key)"""
+    return _TokenMixer.apply(x, w, causal)
+
+
+# ================================================================================================================
 # general attention core on already-projected q, k, v [B, S, H, D] (used by the composable attention path)
 class _AttnCore(torch.autograd.Function):
     @staticmethod

@@ -111,8 +111,10 @@ class Operand(typing.NamedTuple):
 def gemm(a: Operand, b: Operand, c: Operand, M: int, N: int, K: int, batch: typing.Tuple[int, int] = (1, 1),
          alpha: float = 1.0, beta: float = 0.0, act: typing.Optional[str] = None, act_bwd: bool = False,
          R: typing.Optional[torch.Tensor] = None, Zout: typing.Optional[torch.Tensor] = None,
-         Zin: typing.Optional[torch.Tensor] = None):
+         Zin: typing.Optional[torch.Tensor] = None, tri: int = 0):
     """C = epilogue(alpha * A·B). R, Zout, Zin share C's leading dims / batch strides.
+    tri: 1/2 = A is lower/upper triangular (zero tiles are skipped, A must hold the zeros), 3 = only the lower
+    triangle (n <= m) of C receives the product (M == N).
 
     epilogue (act_bwd False): v = alpha*acc (+ beta*C if C is fp32) (+ R); Zout <- v; C <- act(v)
     epilogue (act_bwd True) : C <- (alpha*acc + R) * act'(Zin)"""
@@ -137,7 +139,7 @@ def gemm(a: Operand, b: Operand, c: Operand, M: int, N: int, K: int, batch: typi
             _need(t, cmax, nm)
         d = L.GemmDesc(a.t.data_ptr(), b.t.data_ptr(), c.t.data_ptr(), L.ptr(R), L.ptr(Zout), L.ptr(Zin),
                        a.ld, b.ld, c.ld, a.s1, a.s2, b.s1, b.s2, c.s1, c.s2, M, N, K, b1, b2,
-                       a.trans, b.trans, int(out_f32), ACTS[act], int(act_bwd), float(alpha), float(beta))
+                       a.trans, b.trans, int(out_f32), ACTS[act], int(act_bwd), float(alpha), float(beta), int(tri))
         L.check(L.lib().obst_gemm(d, L.stream_ptr()), "gemm")
         return c.t
     # ---- torch oracle
@@ -152,6 +154,8 @@ def gemm(a: Operand, b: Operand, c: Operand, M: int, N: int, K: int, batch: typi
 
     cv = view(c.t)
     acc = torch.matmul(_f(av), _f(bv)) * alpha
+    if tri == 3:
+        acc = acc * torch.ones(M, N, dtype=acc.dtype, device=acc.device).tril()
     if act_bwd:
         if R is not None:
             acc = acc + _f(view(R))

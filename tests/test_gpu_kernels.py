@@ -246,3 +246,25 @@ def test_gemm_splitk_wgrad(cuda, a_t, b_t):
              beta=1.0)
     torch.cuda.synchronize()
     _close(Cf.view(M, N), ref, 5e-2, 1e-2, f"splitk {a_t}{b_t}")
+
+
+@pytest.mark.parametrize("causal", [True, False])
+def test_token_mixer_big_tiles(cuda, causal):
+    """K03 through the 256x256 phase kernel (>= 512 tiles) incl. the triangular tile skipping (tri = 1/2/3)"""
+    from homebrewnlp_mtf_amd.ops import functional as F
+    torch.manual_seed(3)
+    B, S, H, Fd = 16, 1024, 8, 256
+    x = (torch.randn(B, S, H, Fd) * 0.5).to(BF)
+    w = (torch.randn(H, S, S) * 0.05).to(BF)
+    dy = (torch.randn(B, S, H, Fd) * 0.5).to(BF)
+    xg, wg = x.to(cuda).requires_grad_(True), w.to(cuda).requires_grad_(True)
+    y = F.token_mixer(xg, wg, causal)
+    y.backward(dy.to(cuda))
+    torch.cuda.synchronize()
+    xf, wf = x.float().requires_grad_(True), w.float().requires_grad_(True)
+    wm = torch.tril(wf) if causal else wf
+    ref = torch.einsum("hst,bthf->bshf", wm, xf)
+    ref.backward(dy.float())
+    _close(y, ref, 5e-2, 3e-2, "mixer y")
+    _close(xg.grad, xf.grad, 5e-2, 3e-2, "mixer dx")
+    _close(wg.grad, wf.grad, 1e-1, 3e-2, "mixer dw")

@@ -343,3 +343,23 @@ def test_contrastive_losses(kind):
         dims = [type("D", (), {"name": n})() for n in ("batch", "sequence", "heads", "features_per_head")]
         ref = (t.sum(0).pow(2).sum() / 3 - t.sum(1).pow(2).sum() / 5) / 15
         assert torch.allclose(_contrastive_samples_impl(t, dims, None), ref)
+
+
+@pytest.mark.parametrize("causal", [True, False])
+def test_token_mixer_op_matches_einsum(causal):
+    from homebrewnlp_mtf_amd.ops import functional as F
+    torch.manual_seed(0)
+    B, S, H, Fd = 2, 8, 3, 4
+    x = torch.randn(B, S, H, Fd, dtype=torch.float64, requires_grad=True)
+    w = torch.randn(H, S, S, dtype=torch.float64, requires_grad=True)
+    dy = torch.randn(B, S, H, Fd, dtype=torch.float64)
+    y = F.token_mixer(x, w, causal)
+    y.backward(dy)
+    x2 = x.detach().clone().requires_grad_(True)
+    w2 = w.detach().clone().requires_grad_(True)
+    wm = torch.tril(w2) if causal else w2
+    ref = torch.einsum("hst,bthf->bshf", wm, x2)
+    ref.backward(dy)
+    assert torch.allclose(y, ref, atol=1e-10)
+    assert torch.allclose(x.grad, x2.grad, atol=1e-10)
+    assert torch.allclose(w.grad, w2.grad, atol=1e-10)
