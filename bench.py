@@ -58,6 +58,8 @@ def main():
     mesh = pstate.Mesh(dp=world, tp=1, rank=rank).build_groups()
 
     overrides = {}
+    if not os.path.exists(args.config):   # relative to the repository (profilers run from elsewhere)
+        args.config = os.path.join(os.path.dirname(os.path.abspath(__file__)), args.config)
     base = load_config(args.config)
     per_gpu = args.batch_per_gpu or base.train_batch_size
     overrides["train_batch_size"] = per_gpu * world

@@ -138,7 +138,33 @@ __global__ __launch_bounds__(NTH) void cast_f32_bf16_kernel(const float* __restr
   }
 }
 
+// y(fp32) = alpha * x(fp32) + beta * z(bf16); optional bf16 copy of y (the reversible bodies' residual streams)
+__global__ __launch_bounds__(NTH) void mix_f32_kernel(const float* __restrict__ X, const bf16_t* __restrict__ Z,
+                                                      float* __restrict__ Y, bf16_t* __restrict__ Yb, long long nvec,
+                                                      float alpha, float beta) {
+  for (long long v = (long long)blockIdx.x * NTH + threadIdx.x; v < nvec; v += (long long)gridDim.x * NTH) {
+    float z[8];
+    unpack8(reinterpret_cast<const uint4*>(Z)[v], z);
+    const float4 a = reinterpret_cast<const float4*>(X)[2 * v], b = reinterpret_cast<const float4*>(X)[2 * v + 1];
+    float r[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = alpha * r[j] + beta * z[j];
+    reinterpret_cast<float4*>(Y)[2 * v] = make_float4(r[0], r[1], r[2], r[3]);
+    reinterpret_cast<float4*>(Y)[2 * v + 1] = make_float4(r[4], r[5], r[6], r[7]);
+    if (Yb) reinterpret_cast<uint4*>(Yb)[v] = pack8(r);
+  }
+}
+
 }  // namespace
+
+OBST_API int obst_mix_f32(const float* X, const void* Z, float* Y, void* Yb, long long n, float alpha, float beta,
+                          hipStream_t st) {
+  if (n % 8) return -1;
+  if ((((uintptr_t)X) | ((uintptr_t)Y) | ((uintptr_t)Z) | ((uintptr_t)Yb)) & 15) return -2;
+  hipLaunchKernelGGL(mix_f32_kernel, dim3(grid_for(n / 8)), dim3(NTH), 0, st, X, (const bf16_t*)Z, Y, (bf16_t*)Yb,
+                     n / 8, alpha, beta);
+  return (int)hipGetLastError();
+}
 
 struct ObstEwDesc {
   const void* X; const void* Z; void* Y; const float* sptr;

@@ -13,12 +13,28 @@ namespace {
 
 constexpr int NTH = 256;
 
-template <int NCH>  // 512-element chunks per row
-__device__ __forceinline__ void load_row(const bf16_t* x, int F, int lane, float (&v)[NCH][8]) {
+// LPR lanes per row (64 for F > 256; 32 / 16 / 8 for short rows so a wave covers 64/LPR rows at once),
+// NCH chunks of LPR*8 elements per row
+template <int LPR>
+__device__ __forceinline__ float row_sum(float v) {
+#pragma unroll
+  for (int o = LPR / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <int LPR>
+__device__ __forceinline__ float sub_sum(float v) {   // across the row-groups of a wave (same column)
+#pragma unroll
+  for (int o = LPR; o < 64; o <<= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <int NCH, int LPR>
+__device__ __forceinline__ void load_row(const bf16_t* x, int F, int sl, bool ok, float (&v)[NCH][8]) {
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
-    const int col = c * 512 + lane * 8;
-    if (col < F) {
+    const int col = c * LPR * 8 + sl * 8;
+    if (ok && col < F) {
       uint4 u = *reinterpret_cast<const uint4*>(x + col);
       const uint32_t w[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
@@ -30,43 +46,47 @@ __device__ __forceinline__ void load_row(const bf16_t* x, int F, int lane, float
   }
 }
 
-template <int NCH>
+template <int NCH, int LPR>
 __global__ __launch_bounds__(NTH) void norm_fwd_kernel(const bf16_t* __restrict__ X, const float* __restrict__ scale,
                                                        const float* __restrict__ shift, bf16_t* __restrict__ Y,
                                                        float* __restrict__ rstd_out, long long rows, int F,
                                                        int groups, float eps, const float* __restrict__ ext_stats) {
-  const int lane = threadIdx.x & 63;
-  const long long nw = (long long)gridDim.x * 4;
-  for (long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6); row < rows; row += nw) {
+  constexpr int RPW = 64 / LPR;
+  const int lane = threadIdx.x & 63, sub = lane / LPR, sl = lane % LPR;
+  const long long nw = (long long)gridDim.x * 4 * RPW;
+  for (long long r0 = ((long long)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW; r0 < rows; r0 += nw) {
+    const long long row = r0 + sub;
+    const bool ok = row < rows;
     float v[NCH][8];
-    load_row<NCH>(X + row * F, F, lane, v);
+    load_row<NCH, LPR>(X + row * F, F, sl, ok, v);
     float mean, rstd;
     if (ext_stats) {  // [rows, 2] = (mean, rstd) computed over the full (TP-gathered) feature set
-      mean = ext_stats[2 * row];
-      rstd = ext_stats[2 * row + 1];
+      mean = ok ? ext_stats[2 * row] : 0.f;
+      rstd = ok ? ext_stats[2 * row + 1] : 0.f;
     } else {
       float s = 0.f;
 #pragma unroll
       for (int c = 0; c < NCH; ++c)
 #pragma unroll
         for (int j = 0; j < 8; ++j) s += v[c][j];
-      mean = wave_sum(s) / F;
+      mean = row_sum<LPR>(s) / F;
       float q = 0.f;
 #pragma unroll
       for (int c = 0; c < NCH; ++c)
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const int col = c * 512 + lane * 8 + j;
+          const int col = c * LPR * 8 + sl * 8 + j;
           const float d = col < F ? v[c][j] - mean : 0.f;
           q += d * d;
         }
-      rstd = rsqrtf(wave_sum(q) / F + eps);
+      rstd = rsqrtf(row_sum<LPR>(q) / F + eps);
     }
-    if (rstd_out && lane == 0) { rstd_out[2 * row] = mean; rstd_out[2 * row + 1] = rstd; }
+    if (!ok) continue;
+    if (rstd_out && sl == 0) { rstd_out[2 * row] = mean; rstd_out[2 * row + 1] = rstd; }
     const long long poff = (long long)(row % groups) * F;
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
-      const int col = c * 512 + lane * 8;
+      const int col = c * LPR * 8 + sl * 8;
       if (col >= F) continue;
       uint32_t o[4];
 #pragma unroll
@@ -101,64 +121,64 @@ __global__ __launch_bounds__(NTH) void norm_partial_kernel(const bf16_t* __restr
 
 // backward. stats = (mean, rstd) per row. If `partial_out` is set, only writes per-row partial
 // (sum dxh, sum dxh*xh) for the TP all-reduce and returns (phase 1); with `ext_dsum` (phase 2) uses them.
-template <int NCH>
+// Parameter gradients: per-lane register sums; the host sizes the grid so that (rows per grid step) % groups == 0,
+// so every lane only ever sees rows of one group (row % groups is fixed along the grid-stride loop).
+template <int NCH, int LPR>
 __global__ __launch_bounds__(NTH) void norm_bwd_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ DY,
                                                        const float* __restrict__ scale, const float* __restrict__ stats,
                                                        bf16_t* __restrict__ DX, float* __restrict__ dscale,
                                                        float* __restrict__ dshift, long long rows, int F, int groups,
                                                        int Ffull, float* __restrict__ partial_out,
                                                        const float* __restrict__ ext_dsum) {
+  constexpr int RPW = 64 / LPR;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* red_s = reinterpret_cast<float*>(smem);           // [4 waves][F] dscale partials, then dshift
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, sub = lane / LPR, sl = lane % LPR;
   const bool want_param = (dscale || dshift) && partial_out == nullptr;
-  // per-lane parameter-gradient accumulators (only valid when groups == 1; grouped norms use atomics per row)
   float gs[NCH][8], gb[NCH][8];
 #pragma unroll
   for (int c = 0; c < NCH; ++c)
 #pragma unroll
     for (int j = 0; j < 8; ++j) gs[c][j] = gb[c][j] = 0.f;
-  const long long nw = (long long)gridDim.x * 4;
-  for (long long row = (long long)blockIdx.x * 4 + w; row < rows; row += nw) {
+  const long long nw = (long long)gridDim.x * 4 * RPW;
+  const long long first = ((long long)blockIdx.x * 4 + w) * RPW + sub;
+  for (long long r0 = ((long long)blockIdx.x * 4 + w) * RPW; r0 < rows; r0 += nw) {
+    const long long row = r0 + sub;
+    const bool ok = row < rows;
     float x[NCH][8], dy[NCH][8];
-    load_row<NCH>(X + row * F, F, lane, x);
-    load_row<NCH>(DY + row * F, F, lane, dy);
-    const float mean = stats[2 * row], rstd = stats[2 * row + 1];
+    load_row<NCH, LPR>(X + row * F, F, sl, ok, x);
+    load_row<NCH, LPR>(DY + row * F, F, sl, ok, dy);
+    const float mean = ok ? stats[2 * row] : 0.f, rstd = ok ? stats[2 * row + 1] : 0.f;
     const long long poff = (long long)(row % groups) * F;
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int c = 0; c < NCH; ++c)
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const int col = c * 512 + lane * 8 + j;
-        if (col < F) {
+        const int col = c * LPR * 8 + sl * 8 + j;
+        if (ok && col < F) {
           const float xh = (x[c][j] - mean) * rstd;
           const float g = scale ? scale[poff + col] : 1.f;
           const float dxh = dy[c][j] * g;
           s1 += dxh;
           s2 += dxh * xh;
-          if (want_param) {
-            if (groups == 1) { gs[c][j] += dy[c][j] * xh; gb[c][j] += dy[c][j]; }
-            else {
-              if (dscale) atomicAdd(dscale + poff + col, dy[c][j] * xh);
-              if (dshift) atomicAdd(dshift + poff + col, dy[c][j]);
-            }
-          }
+          if (want_param) { gs[c][j] += dy[c][j] * xh; gb[c][j] += dy[c][j]; }
           x[c][j] = xh;
           dy[c][j] = dxh;
         }
       }
-    s1 = wave_sum(s1);
-    s2 = wave_sum(s2);
+    s1 = row_sum<LPR>(s1);
+    s2 = row_sum<LPR>(s2);
+    if (!ok) continue;
     if (partial_out) {
-      if (lane == 0) { partial_out[2 * row] = s1; partial_out[2 * row + 1] = s2; }
+      if (sl == 0) { partial_out[2 * row] = s1; partial_out[2 * row + 1] = s2; }
       continue;
     }
     if (ext_dsum) { s1 = ext_dsum[2 * row]; s2 = ext_dsum[2 * row + 1]; }
     const float m1 = s1 / Ffull, m2 = s2 / Ffull;
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
-      const int col = c * 512 + lane * 8;
+      const int col = c * LPR * 8 + sl * 8;
       if (col >= F) continue;
       uint32_t o[4];
 #pragma unroll
@@ -168,14 +188,31 @@ __global__ __launch_bounds__(NTH) void norm_bwd_kernel(const bf16_t* __restrict_
       *reinterpret_cast<uint4*>(DX + row * F + col) = make_uint4(o[0], o[1], o[2], o[3]);
     }
   }
+  if (want_param && groups > 1) {
+    // one atomic per element per lane group into its group of the [groups, F] parameters
+    if (first < rows) {
+      const long long poff = (long long)(first % groups) * F;
+#pragma unroll
+      for (int c = 0; c < NCH; ++c)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int col = c * LPR * 8 + sl * 8 + j;
+          if (col < F) {
+            if (dscale) atomicAdd(dscale + poff + col, gs[c][j]);
+            if (dshift) atomicAdd(dshift + poff + col, gb[c][j]);
+          }
+        }
+    }
+  }
   if (want_param && groups == 1) {
-    // reduce the 4 waves through LDS, then one atomic per element per block
+    // fold the row-groups of the wave, reduce the 4 waves through LDS, then one atomic per element per block
 #pragma unroll
     for (int c = 0; c < NCH; ++c)
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const int col = c * 512 + lane * 8 + j;
-        if (col < F) { red_s[w * F + col] = gs[c][j]; red_s[(4 + w) * F + col] = gb[c][j]; }
+        const float a = sub_sum<LPR>(gs[c][j]), b = sub_sum<LPR>(gb[c][j]);
+        const int col = c * LPR * 8 + sl * 8 + j;
+        if (sub == 0 && col < F) { red_s[w * F + col] = a; red_s[(4 + w) * F + col] = b; }
       }
     __syncthreads();
     for (int col = threadIdx.x; col < F; col += NTH) {
@@ -201,15 +238,27 @@ struct ObstNormDesc {
   long long rows; int F; int groups; int Ffull; float eps;
 };
 
+#define NORM_DISPATCH_L(KERNEL, LPR, GRID, LDSB, ...)                                               \
+  do {                                                                                              \
+    const int nch = (d->F + LPR * 8 - 1) / (LPR * 8);                                               \
+    if (nch <= 1) hipLaunchKernelGGL((KERNEL<1, LPR>), GRID, dim3(NTH), LDSB, st, __VA_ARGS__);     \
+    else if (nch <= 2) hipLaunchKernelGGL((KERNEL<2, LPR>), GRID, dim3(NTH), LDSB, st, __VA_ARGS__);\
+    else if (nch <= 4) hipLaunchKernelGGL((KERNEL<4, LPR>), GRID, dim3(NTH), LDSB, st, __VA_ARGS__);\
+    else if (nch <= 8) hipLaunchKernelGGL((KERNEL<8, LPR>), GRID, dim3(NTH), LDSB, st, __VA_ARGS__);\
+    else if (nch <= 16) hipLaunchKernelGGL((KERNEL<16, LPR>), GRID, dim3(NTH), LDSB, st, __VA_ARGS__);\
+    else return -2;                                                                                 \
+  } while (0)
+
+static int lanes_per_row(int F) { return F <= 64 ? 8 : F <= 128 ? 16 : F <= 256 ? 32 : 64; }
+
 #define NORM_DISPATCH(KERNEL, GRID, LDSB, ...)                                                      \
   do {                                                                                              \
-    const int nch = (d->F + 511) / 512;                                                             \
-    if (nch <= 1) hipLaunchKernelGGL(KERNEL<1>, GRID, dim3(NTH), LDSB, st, __VA_ARGS__);            \
-    else if (nch <= 2) hipLaunchKernelGGL(KERNEL<2>, GRID, dim3(NTH), LDSB, st, __VA_ARGS__);       \
-    else if (nch <= 4) hipLaunchKernelGGL(KERNEL<4>, GRID, dim3(NTH), LDSB, st, __VA_ARGS__);       \
-    else if (nch <= 8) hipLaunchKernelGGL(KERNEL<8>, GRID, dim3(NTH), LDSB, st, __VA_ARGS__);       \
-    else if (nch <= 16) hipLaunchKernelGGL(KERNEL<16>, GRID, dim3(NTH), LDSB, st, __VA_ARGS__);     \
-    else return -2;                                                                                 \
+    switch (lanes_per_row(d->F)) {                                                                  \
+      case 8: NORM_DISPATCH_L(KERNEL, 8, GRID, LDSB, __VA_ARGS__); break;                           \
+      case 16: NORM_DISPATCH_L(KERNEL, 16, GRID, LDSB, __VA_ARGS__); break;                         \
+      case 32: NORM_DISPATCH_L(KERNEL, 32, GRID, LDSB, __VA_ARGS__); break;                         \
+      default: NORM_DISPATCH_L(KERNEL, 64, GRID, LDSB, __VA_ARGS__); break;                         \
+    }                                                                                               \
   } while (0)
 
 OBST_API int obst_norm_fwd(const ObstNormDesc* d, hipStream_t st) {
@@ -232,7 +281,13 @@ OBST_API int obst_norm_bwd(const ObstNormDesc* d, hipStream_t st) {
   if (lds > 160 * 1024) return -3;
   // more rows per block amortises the parameter-gradient atomics
   long long g = (d->rows + 31) / 32;
-  const int grid = (int)(g < 1024 ? (g < 1 ? 1 : g) : 1024);
+  int grid = (int)(g < 1024 ? (g < 1 ? 1 : g) : 1024);
+  if (d->groups > 1) {   // rows per grid step (4 waves x 64/LPR rows per block) must be a multiple of groups
+    int a = d->groups, b = 4 * (64 / lanes_per_row(d->F));
+    while (b) { const int t = a % b; a = b; b = t; }
+    const int q = d->groups / a;                 // blocks per group period
+    grid = grid < q ? q : grid / q * q;
+  }
   NORM_DISPATCH(norm_bwd_kernel, dim3(grid), lds, (const bf16_t*)d->X, (const bf16_t*)d->DY, d->scale, d->stats,
                 (bf16_t*)d->DX, d->dscale, d->dshift, d->rows, d->F, d->groups, d->Ffull, d->partial, d->ext);
   return (int)hipGetLastError();

@@ -55,13 +55,21 @@ class _RevStack(torch.autograd.Function):
         dt = x1.dtype
         sd = _stream_dtype(dt)
         x1, x2 = x1.to(sd), x2.to(sd)
+        low = dt != sd                      # fused fp32 <- fp32 + bf16 kernels on the GPU
         with torch.no_grad():
-            for f in blocks:
-                if mode == "revnet":
-                    x1, x2 = x2, x1 + f(x2.to(dt)).to(sd)
-                else:  # momentum: (x, v) -> (x + v', v'), v' = a v + (1-a) F(x)
-                    v = x2 * alpha + f(x1.to(dt)).to(sd) * (1.0 - alpha)
-                    x1, x2 = x1 + v, v
+            if mode == "revnet" and low:
+                x2b = raw.to_bf16(x2)
+                for f in blocks:
+                    nb = torch.empty_like(x2b)
+                    nx2 = raw.mix_f32(x1, f(x2b), 1.0, 1.0, yb=nb)   # y2 = x1 + F(x2), plus its bf16 copy
+                    x1, x2, x2b = x2, nx2, nb
+            else:
+                for f in blocks:
+                    if mode == "revnet":
+                        x1, x2 = x2, x1 + f(x2.to(dt)).to(sd)
+                    else:  # momentum: (x, v) -> (x + v', v'), v' = a v + (1-a) F(x)
+                        v = x2 * alpha + f(x1.to(dt)).to(sd) * (1.0 - alpha)
+                        x1, x2 = x1 + v, v
         ctx.blocks, ctx.mode, ctx.alpha, ctx.dt = blocks, mode, alpha, dt
         ctx.save_for_backward(x1, x2)
         return x1, x2
@@ -77,11 +85,15 @@ class _RevStack(torch.autograd.Function):
             if mode == "revnet":
                 # y1 = x2, y2 = x1 + F(x2)
                 with torch.enable_grad():
-                    x2 = y1.to(dt).detach().requires_grad_(True)
+                    x2 = (raw.to_bf16(y1) if dt == torch.bfloat16 else y1.to(dt)).detach().requires_grad_(True)
                     fx = f(x2)
-                torch.autograd.backward(fx, g2.to(dt))
-                x1 = y2 - fx.detach().to(sd)
-                dx2 = g1 if x2.grad is None else g1 + x2.grad.to(sd)
+                torch.autograd.backward(fx, raw.to_bf16(g2) if dt == torch.bfloat16 else g2.to(dt))
+                if dt == torch.bfloat16:
+                    x1 = raw.mix_f32(y2, fx.detach(), 1.0, -1.0)
+                    dx2 = g1 if x2.grad is None else raw.mix_f32(g1, x2.grad, 1.0, 1.0)
+                else:
+                    x1 = y2 - fx.detach().to(sd)
+                    dx2 = g1 if x2.grad is None else g1 + x2.grad.to(sd)
                 y1, y2, g1, g2 = x1, y1, g2, dx2
             else:
                 # y1 = x + v', y2 = v' ; v' = a v + (1-a) F(x)

@@ -407,6 +407,37 @@ def dot(x, dy, out):
     out.view(-1)[0] += (_f(x) * _f(dy)).sum()
 
 
+def mix_f32(x, z, alpha: float, beta: float, y=None, yb=None):
+    """y(fp32) = alpha * x(fp32) + beta * z(low precision); optionally also writes the bf16 copy `yb`"""
+    if y is None:
+        y = torch.empty_like(x)
+    if x.device.type == "meta":
+        return y
+    if on_gpu(x) and z.dtype == torch.bfloat16 and x.dtype == torch.float32 and x.numel() % 8 == 0:
+        x, z = x.contiguous(), z.contiguous()       # raw pointers below: block outputs may be permuted views
+        if z.shape != x.shape:
+            z = z.reshape(x.shape)
+        L.check(L.lib().obst_mix_f32(x.data_ptr(), z.data_ptr(), y.data_ptr(), L.ptr(yb), x.numel(), float(alpha),
+                                     float(beta), L.stream_ptr()), "mix_f32")
+        return y
+    torch.add(x * alpha, z.to(x.dtype), alpha=beta, out=y)
+    if yb is not None:
+        yb.copy_(y)
+    return y
+
+
+def to_bf16(x, out=None):
+    """fp32 -> bf16 copy through the HIP cast kernel on the GPU"""
+    if out is None:
+        out = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)
+    if on_gpu(x) and x.dtype == torch.float32:
+        x = x.contiguous()
+        L.check(L.lib().obst_cast_f32_bf16(x.data_ptr(), out.data_ptr(), x.numel(), L.stream_ptr()), "cast")
+        return out
+    out.copy_(x)
+    return out
+
+
 def transpose(x, y, rows: int, cols: int, ldx: int, ldy: int, batch: int = 1, sx: int = 0, sy: int = 0):
     """y[b][c][r] = x[b][r][c] (bf16 on the GPU; any dtype on the CPU)"""
     if x.device.type == "meta":

@@ -110,10 +110,11 @@ def test_attention_fwd_bwd(cuda, D, S, causal):
 
 
 # ----------------------------------------------------------------------------------------------------------------
-@pytest.mark.parametrize("F_,groups", [(2048, 1), (128, 16), (64, 1), (1000, 1)])
-def test_norm(cuda, F_, groups):
+@pytest.mark.parametrize("F_,groups,nrows", [(2048, 1, 96), (128, 16, 96), (64, 1, 96), (1000, 1, 96),
+                                           (128, 1, 5000), (256, 8, 4000), (32, 4, 3001)])
+def test_norm(cuda, F_, groups, nrows):
     torch.manual_seed(F_)
-    rows = 96 * groups
+    rows = nrows * groups
     x = (torch.randn(rows * F_) * 2 + 0.3).to(BF)
     dy = torch.randn(rows * F_).to(BF)
     sc = torch.randn(groups * F_) * 0.1 + 1
