@@ -99,7 +99,14 @@ class Model:
             self._positions = None
         return out[..., :self.params.vocab_size].float()
 
-    def _forward(self, batch: dict, logits_only: bool = False):
+    @torch.no_grad()
+    def predict(self, batch: dict) -> typing.Tuple[typing.Optional[torch.Tensor], typing.Optional[torch.Tensor]]:
+        """Inference forward returning (frame_out [B, T, ..., C] in [0, 1], token logits) for the video sampling loop
+        (ref src/run/inference.py:27-36)."""
+        self.builder.train = False
+        return self._forward(dict(batch, token_y=None), logits_only="outputs")
+
+    def _forward(self, batch: dict, logits_only: typing.Union[bool, str] = False):
         b = self.builder
         p = b.params
         b.begin_forward()
@@ -116,6 +123,8 @@ class Model:
                 out = Act(t.unsqueeze(1).contiguous(), [out.dims[0], Dim("sequence", 1)] + list(out.dims[2:]))
             with b.scope("output"):
                 frame_out, token_out = self._output(out)
+            if logits_only == "outputs":
+                return (None if frame_out is None else frame_out.t), (None if token_out is None else token_out.t)
             if logits_only:
                 if pos is not None and p.output_block_configs:
                     idx = pos.to(token_out.t.device).long()

@@ -18,6 +18,7 @@ import typing
 import torch
 
 from ..ops import raw
+from ..utils import debug
 from .context import Act, Builder
 from .frontend import block_body, block_scope_name
 
@@ -31,7 +32,7 @@ class Block:
     def __call__(self, x: torch.Tensor) -> torch.Tensor:
         b = self.builder
         b.depth_idx, b.config_idx = self.depth, self.config_idx
-        with b.scope.restore(self.stack):
+        with b.scope.restore(self.stack), debug.range_(self.stack[-1]):
             return block_body(b, self.config, Act(x, self.dims)).t
 
 

@@ -19,6 +19,8 @@ import typing
 import torch
 import torch.distributed as dist
 
+from ..utils import debug
+
 from ..ops import functional as F
 
 
@@ -65,6 +67,7 @@ class GradSync:
         self.launched[bi] = True
         lo, hi, _ = self.buckets[bi]
         t = self.store.grad[lo:hi]
+        debug.record("dp_all_reduce", t)
         if self.dtype != torch.float32:
             low = t.to(self.dtype)
             work = dist.all_reduce(low, op=dist.ReduceOp.SUM, group=self.group, async_op=True)

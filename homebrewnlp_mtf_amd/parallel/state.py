@@ -63,5 +63,7 @@ def tp_size() -> int:
 def tp_all_reduce(t: torch.Tensor, op=None) -> torch.Tensor:
     """In-place sum (or `op`) over the TP group; identity when tp == 1."""
     if _MESH.tp > 1 and t.device.type != "meta":   # the registration pass runs on meta tensors
+        from ..utils import debug
+        debug.record("tp_all_reduce", t)
         dist.all_reduce(t, op=op or dist.ReduceOp.SUM, group=_MESH.tp_group)
     return t

@@ -112,6 +112,92 @@ class Sampler:
 
 
 # ---------------------------------------------------------------------------------------------------------------
+class VideoSampler:
+    """Autoregressive jannet sampling with frame feedback (ref src/run/inference.py:22-64).
+
+    For ``position`` in ``[initial_pos, end)`` the model reads the frames (and per-frame tokens) so far; the frame
+    predicted at ``position`` (the model's estimate of frame ``position + 1``) is quantised back to the uint8 input
+    encoding (re-folding bits when ``use_bit_fold_input_pipeline``) and written into slot ``position + 1``, and the
+    Gumbel-argmax tokens of ``position`` into ``token_x[position + 1]``. The reference writes both into slot
+    ``position`` (its own "todo: fix token shift for video"), which overwrites the prompt frame it just read; the
+    rebuild shifts by one so prompt frames are never modified."""
+
+    def __init__(self, model, params: ModelParameter, device):
+        self.model, self.params, self.device = model, params, torch.device(device)
+        self.gen = torch.Generator(device=self.device)
+        self.gen.manual_seed(int(params.seed) if getattr(params, "seed", None) is not None else 0)
+
+    def _to_input(self, frame_out: torch.Tensor) -> torch.Tensor:
+        p = self.params
+        q = (frame_out.float() * 255.0).round().clamp(0, 255)
+        if p.use_bit_fold_input_pipeline:
+            base = 2 ** p.bit_fold_value
+            parts = q.clamp(max=base - 1).chunk(p.fold_count, -1)
+            q = sum(part * base ** i for i, part in enumerate(parts))
+        return q.to(torch.uint8)
+
+    @torch.no_grad()
+    def sample(self, batch: dict, initial_pos: int, temperature: float, end: typing.Optional[int] = None) -> dict:
+        p = self.params
+        frame = batch["frame"].to(self.device).clone()
+        tok = batch.get("token_x")
+        tok = tok.to(self.device).clone() if tok is not None else None
+        T = frame.shape[1] - 1
+        end = T if end is None else min(int(end), T)
+        inputs = {k: v.to(self.device) for k, v in batch.items() if k not in ("frame", "token_x", "token_y")
+                  and isinstance(v, torch.Tensor)}
+        for pos in range(max(0, int(initial_pos)), end):
+            frame_out, logits = self.model.predict(dict(inputs, frame=frame, token_x=tok))
+            if pos + 1 <= T:
+                frame[:, pos + 1] = self._to_input(frame_out[:, pos])
+            if tok is not None and logits is not None and pos + 1 < tok.shape[1]:
+                lg = logits[:, pos, ..., :p.vocab_size].float()
+                u = torch.rand(lg.shape, generator=self.gen, device=self.device) * (1 - 1e-9) + 1e-9
+                tok[:, pos + 1] = (lg - temperature * torch.log(-torch.log(u))).argmax(-1).to(tok.dtype)
+        out = {"frame": frame}
+        if tok is not None:
+            out["token_x"] = tok
+        return out
+
+
+def render_video(samples: typing.Sequence[typing.Tuple[np.ndarray, typing.Optional[typing.List[str]]]],
+                 count: int, params: ModelParameter, save_prefix: str = "", upscale: int = 4,
+                 line_split: int = 2, text_color=(255, 0, 255), prompt_sample_color=(0, 128, 255)) -> str:
+    """Side-by-side animated GIF of sampled videos (ref src/interface.py:13-58, which writes an MJPG .avi through
+    OpenCV; OpenCV is not part of this stack, PIL is). ``samples`` is a list of (frames [T, H, W, C] in [0, 1],
+    per-frame texts or None); frames are upscaled by nearest neighbour, per-frame text is drawn in
+    ``language_token_per_frame // line_split`` character lines and, with autoregressive sampling, each frame is
+    labelled "prompt" or "sample". Returns the written path."""
+    from PIL import Image, ImageDraw
+    images = []
+    n_frames = len(samples[0][0])
+    for idx in range(n_frames):
+        cols = []
+        for frames, texts in samples:
+            f = np.asarray(frames[idx], dtype=np.float32)
+            if f.ndim == 2:
+                f = f[..., None]
+            f = np.clip(f * (params.color_quantization_value - 1), 0, 255).astype(np.uint8)
+            f = f.repeat(upscale, 0).repeat(upscale, 1)
+            img = Image.fromarray(f[..., 0] if f.shape[-1] == 1 else f[..., :3])
+            img = img.convert("RGB")
+            draw = ImageDraw.Draw(img)
+            if texts is not None and idx < len(texts):
+                width = max(1, params.language_token_per_frame // line_split)
+                for li, k in enumerate(range(0, len(texts[idx]), width)):
+                    draw.text((10, img.height - 12 * (len(texts[idx]) // width + 1) + 12 * li),
+                              texts[idx][k:k + width], fill=tuple(text_color))
+            if params.use_autoregressive_sampling:
+                label = "prompt" if idx < params.initial_autoregressive_position else "sample"
+                draw.text((10, 10), label, fill=tuple(prompt_sample_color))
+            cols.append(np.asarray(img))
+        images.append(Image.fromarray(np.concatenate(cols, axis=1)))
+    path = f"{save_prefix}_{count}.gif"
+    images[0].save(path, save_all=True, append_images=images[1:], duration=1000, loop=0)
+    return path
+
+
+# ---------------------------------------------------------------------------------------------------------------
 class CompletionEngine:
     """Thread-safe completion service over one model (``complete`` blocks; ``submit`` returns a future)."""
 
@@ -201,6 +287,44 @@ def run_debug(engine: CompletionEngine, params: ModelParameter) -> typing.List[f
         print(f"test:{idx} similarity score: {score:6.2f}%")
         scores.append(score)
     return scores
+
+
+def run_video_sample(sampler: VideoSampler, tokenizer: Tokenizer, params: ModelParameter,
+                     batches: typing.Iterable[dict], save_prefix: str = "") -> typing.List[str]:
+    """`sample` run mode for jannet (ref interface.py:101-150): sample after `initial_autoregressive_position` and
+    render prompt + samples next to the ground truth."""
+    pos = int(params.initial_autoregressive_position)
+    paths = []
+    for i, b in enumerate(batches):
+        if i >= params.num_of_sample:
+            break
+        b1 = {k: v[:1] for k, v in b.items() if isinstance(v, torch.Tensor)}
+        out = sampler.sample(b1, pos, params.sampling_temperature)
+        model = sampler.model
+
+        def frames(f):     # frame targets [T, ...] in the decoder's quantised scale, mapped to [0, 1]
+            v = model._frames(f[0, 1:]).float() * 255.0
+            return (v / max(1, params.color_quantization_value - 1)).cpu().numpy()
+
+        def texts(t):
+            if t is None:
+                return None
+            return [process_token_output(t[0, k].reshape(1, -1).cpu().numpy(), params.padding_token,
+                                         tokenizer)[0] for k in range(t.shape[1])]
+        cols = [(frames(b1["frame"]), texts(b1.get("token_x"))), (frames(out["frame"]), texts(out.get("token_x")))]
+        cols = [(_unpatch(f, params), t) for f, t in cols]
+        paths.append(render_video(cols, i, params, save_prefix=save_prefix))
+        log(f"video sample {i} written to {paths[-1]}")
+    return paths
+
+
+def _unpatch(f: np.ndarray, params: ModelParameter) -> np.ndarray:
+    """decoder frames [T, Hp(, Wp), C*p*p] -> images [T, H, W, C]: inverse of decode_frame's reshape/transpose
+    (whose memory order is [p, p, Hp, Wp, C], ref src/inputs.py:181-198)"""
+    T, p = f.shape[0], params.patch_size
+    hp, wp, c = params.frame_height_patch, params.frame_width_patch, params.color_channels
+    flat = f.reshape(T, -1)[:, :p * p * hp * wp * c]
+    return flat.reshape(T, p, p, hp, wp, c).transpose(0, 3, 1, 4, 2, 5).reshape(T, hp * p, wp * p, c)
 
 
 def run_sample(sampler: Sampler, tokenizer: Tokenizer, params: ModelParameter, batches: typing.Iterable[dict]):

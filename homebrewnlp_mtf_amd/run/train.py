@@ -32,6 +32,21 @@ def _sync(dev):
         torch.cuda.synchronize(dev)
 
 
+def _mean_over_ranks(vals: dict, dev) -> dict:
+    import torch.distributed as dist
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return vals
+    keys = [k for k, v in vals.items() if isinstance(v, torch.Tensor) and v.numel() == 1]
+    if not keys:
+        return vals
+    t = torch.stack([vals[k].detach().float().reshape(()).to(dev) for k in keys])
+    dist.all_reduce(t)
+    t /= dist.get_world_size()
+    out = dict(vals)
+    out.update({k: t[i] for i, k in enumerate(keys)})
+    return out
+
+
 def train(params: ModelParameter, debug_grad: bool = False, synthetic: bool = False, device: str = "auto",
           max_steps: typing.Optional[int] = None) -> dict:
     mesh, dev = launch.init(params, device)
@@ -96,7 +111,7 @@ def train(params: ModelParameter, debug_grad: bool = False, synthetic: bool = Fa
             _sync(dev)
             now = time.time()
             tps = (step - last_log_step) * tokens_per_step / max(now - last_log_t, 1e-9)
-            vals = {k2: v for k2, v in m.items()}
+            vals = _mean_over_ranks({k2: v for k2, v in m.items()}, dev)     # X07: losses averaged over ranks
             vals.update(tokens_per_s=tps, tflops_per_gpu=tps * flops_tok / mesh.world / 1e12,
                         mfu=tps * flops_tok / mesh.world / PEAK_BF16_DENSE if dev.type == "cuda" else 0.0)
             metrics.write(step, vals)

@@ -21,6 +21,7 @@ from ..optim.chain import learning_rate
 from ..optim.reference import ReferenceOptimizer
 from ..parallel import state as pstate
 from ..parallel.grad_sync import GradSync
+from ..utils import debug
 from ..utils.log import log
 
 
@@ -82,11 +83,15 @@ class Trainer:
             for k, v in out.items():
                 v = v.detach().float()
                 metrics[k] = metrics.get(k, 0) + v / len(micro)
-        self.grad_sync.finish(average=True)
+        with debug.range_("dp_sync"):
+            self.grad_sync.finish(average=True)
         lr = learning_rate(self.params, self.global_step)
-        self.opt.step(lr, self.global_step + 1)
+        with debug.range_("optimizer"):
+            self.opt.step(lr, self.global_step + 1)
         self.global_step += 1
         metrics["learning_rate"] = torch.tensor(lr)
+        if debug.CHECK:
+            debug.verify()
         return metrics
 
     # ---------------------------------------------------------------------------------------------------------------

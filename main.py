@@ -95,6 +95,9 @@ def _inference(params, args) -> int:
     if params.debug_sample:
         params.use_autoregressive_sampling = True
         params.sampling_temperature = 0
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:   # A17: the inference batch is 1-2 sequences, so extra ranks split heads (TP), not the batch
+        params.mesh = {"dp": 1, "tp": world}
     params = ModelParameter(params)
     mesh, dev = launch.init(params, args.device)
     tr = Trainer(params, dev, mesh, use_fused=False)
@@ -105,6 +108,14 @@ def _inference(params, args) -> int:
         print(f"warning: no checkpoint under {params.model_path}; sampling from random weights", flush=True)
     tok = infer.Tokenizer(params)
     sampler = infer.Sampler(tr.model, params, dev)
+    if args.run_mode == "sample" and params.use_video:
+        from homebrewnlp_mtf_amd.data import video
+        src = video.SyntheticVideo(params, 1, dev) if (args.synthetic or not params.dataset_configs) else \
+            video.jannet_input(params, 1, 0, 1, dev)
+        vs = infer.VideoSampler(tr.model, params, dev)
+        infer.run_video_sample(vs, tok, params, iter(src.next, None),
+                               save_prefix=os.path.join(params.model_path, "sample"))
+        return 0
     if args.run_mode in ("sample", "debug_old"):
         from homebrewnlp_mtf_amd.data import pipeline as data
         src = data.SyntheticText(params, 1, dev) if (args.synthetic or not params.dataset_configs) else \

@@ -107,3 +107,33 @@ def test_tp_matches_single_rank(strategy):
             got = torch.cat([p.view(shp) for p in parts], tp_dim)
         diff = (got - full).abs().max().item()
         assert diff < 5e-5, f"TP weight {name} differs by {diff}"
+
+
+def _check_worker(rank, world, port, out_dir):
+    from homebrewnlp_mtf_amd.utils import debug
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    debug.CHECK = True
+    torch.manual_seed(0)
+    mesh = pstate.Mesh(dp=1, tp=world, rank=rank).build_groups()
+    tr = Trainer(ModelParameter(dict(CFG, mesh={"dp": 1, "tp": world})), "cpu", mesh)
+    tr.step(_batch())                       # Trainer.step verifies the sequence itself
+    n_ok = debug._count
+    debug.record("extra", torch.zeros(3 + rank))   # ranks now disagree
+    try:
+        debug.verify()
+        err = ""
+    except RuntimeError as e:
+        err = str(e)
+    torch.save({"n_ok": n_ok, "err": err}, os.path.join(out_dir, f"c{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def test_collective_sequence_check():
+    """diverging collective sequences (the TP+RevNet deadlock hazard) raise instead of hanging"""
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_check_worker, args=(2, _free_port(), d), nprocs=2, join=True)
+        res = [torch.load(os.path.join(d, f"c{r}.pt"), weights_only=True) for r in range(2)]
+    for r in res:
+        assert r["n_ok"] == 0, "verify() at the end of the step resets the sequence"
+        assert "diverged" in r["err"]

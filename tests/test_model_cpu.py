@@ -363,3 +363,40 @@ def test_token_mixer_op_matches_einsum(causal):
     assert torch.allclose(y, ref, atol=1e-10)
     assert torch.allclose(x.grad, x2.grad, atol=1e-10)
     assert torch.allclose(w.grad, w2.grad, atol=1e-10)
+
+
+def test_video_sampling_and_render(tmp_path):
+    """jannet sampling with frame feedback (ref inference.py:22-64) and the GIF renderer (ref interface.py:13-58)"""
+    from homebrewnlp_mtf_amd.data.video import decode_frame
+    from homebrewnlp_mtf_amd.run import infer
+    torch.manual_seed(0)
+    cfg = dict(model_mode="jannet", use_video=True, use_language=True, heads=2, features_per_head=8, depth=1,
+               sequence_length=4, time_patch=1, frame_width=16, frame_height=8, patch_size=4, color_channels=3,
+               three_axes=False, language_token_per_frame=4, token_patch_size=1, vocab_size=32,
+               train_batch_size=1, intermediate_feed_forward_multiplier=2, memory_reduction_strategy="none",
+               calculation_dtype="float32", experts=4, initial_autoregressive_position=2, num_of_sample=1,
+               use_autoregressive_sampling=True, sampling_temperature=0.0,
+               block_config=[{"layer": ["norm-shift-scale", "attention-dot_product-context"], "skip": True}])
+    p = ModelParameter(cfg)
+    m = Model(p, "cpu")
+    frame = torch.randint(0, 256, (1, 5, 8, 48), dtype=torch.uint8)
+    tok = torch.randint(0, 32, (1, 5, 4, 1))
+    vs = infer.VideoSampler(m, p, "cpu")
+    out = vs.sample({"frame": frame, "token_x": tok[:, :-1]}, 2, 0.0)
+    assert torch.equal(out["frame"][:, :3], frame[:, :3]), "prompt frames must not change"
+    fo, _ = m.predict({"frame": frame, "token_x": tok[:, :-1]})
+    assert torch.equal(out["frame"][:, 3], vs._to_input(fo[:, 2])), "frame 3 is the prediction made at position 2"
+    assert torch.equal(out["token_x"][:, :3], tok[:, :3])
+    # the renderer's un-patching inverts the decoder's patch layout
+    import io
+    import numpy as np
+    from PIL import Image
+    img = np.random.RandomState(0).randint(0, 256, (8, 16, 3)).astype(np.uint8)
+    buf = io.BytesIO()
+    Image.fromarray(img).save(buf, format="PNG")
+    patched = decode_frame(buf.getvalue(), p)
+    assert np.array_equal(infer._unpatch(patched[None], p)[0], img)
+    paths = infer.run_video_sample(vs, infer.Tokenizer(p), p, iter([{"frame": frame, "token_x": tok[:, :-1]}]),
+                                   save_prefix=str(tmp_path / "s"))
+    gif = Image.open(paths[0])
+    assert gif.n_frames == 4 and gif.size == (2 * 16 * 4, 8 * 4)
