@@ -133,3 +133,27 @@ def test_fused_chain_compilation():
     segs, pre, wc = fused.compile_chain("adafactor-learning_rate")
     assert pre and [s.opener[0] if s.opener else None for s in segs] == [None, "adafactor", "adafactor_clip"]
     assert not fused.supported("graft:adam-learning_rate")
+
+
+def test_grad_accumulation_matches_full_batch():
+    """grad_accumulation=2 (reference raises for >1): two half-batch micro-steps == one full-batch step"""
+    from homebrewnlp_mtf_amd.config import ModelParameter
+    from homebrewnlp_mtf_amd.parallel import state as pstate
+    from homebrewnlp_mtf_amd.run.trainer import Trainer
+    cfg = dict(model_mode="gpt", use_video=False, use_language=True, heads=2, features_per_head=8, depth=1,
+               sequence_length=8, train_batch_size=4, vocab_size=32, intermediate_feed_forward_multiplier=2,
+               memory_reduction_strategy="none", calculation_dtype="float32", learning_rate=0.01,
+               optimizer="adaptive_clip:0.003-sm3-momentum:0.9:1:1-learning_rate",
+               block_config=[{"layer": ["norm-shift-scale", "feed_forward-in:gelu"], "skip": True}])
+    pstate.set_mesh(pstate.Mesh())
+    g = torch.Generator().manual_seed(3)
+    toks = torch.randint(0, 32, (4, 9, 1), generator=g)
+    batch = {"token_x": toks[:, :-1].contiguous(), "token_y": toks[:, 1:].contiguous()}
+    res = []
+    for n in (1, 2):
+        torch.manual_seed(0)
+        tr = Trainer(ModelParameter(dict(cfg, grad_accumulation=n)), "cpu")
+        m = tr.step(batch)
+        res.append((float(m["loss"]), tr.store.master.clone()))
+    assert abs(res[0][0] - res[1][0]) < 1e-5
+    assert (res[0][1] - res[1][1]).abs().max().item() < 1e-5
