@@ -13,6 +13,8 @@
 // dQ is produced by its own kernel (recomputing S and dP) instead of fp32 atomics: at S=2048 the atomic dQ sum
 // would move ~16x the dQ bytes through the ~1.3 TB/s atomic path (Guideline 12).
 #include "common.h"
+#include <stdlib.h>
+#include <type_traits>
 
 namespace {
 
@@ -563,9 +565,399 @@ __global__ __launch_bounds__(NTH, 2) void attn_bwd_dkv_kernel(AttnArgs a) {
   }
 }
 
+// ================================================================================================================
+// D = 128 forward with v_mfma_f32_32x32x16_bf16 (cdna_hip_programming.md Appendix B "Fused attention prefill").
+// A 32x32x16 MFMA holds the SIMD's vector issue for 8 of its 32 cycles (16x16x32: 8 of 16), so the softmax VALU
+// work of one wave fits in the MFMA gaps of its partner; the per-query row reductions shrink to 31 local ops + one
+// v_permlane32_swap. Sᵀ = K·Qᵀ keeps the query on the lane: lane (h = lane>>5, n = lane&31) holds, for query n,
+// keys 8a + 4h + b (register 4a + b) of every 32-key sub-tile. Those registers, bf16-packed 8 at a time, are the
+// B operand of P·V directly (k-step s of a sub-tile = registers 8s..8s+7); the A operand Vᵀ is read from the same
+// swizzled [key][d] LDS image with ds_read_b64_tr_b16 in that key order, so P never crosses lanes.
+typedef __attribute__((ext_vector_type(16))) float f32x16_t;
+
+__device__ __forceinline__ float xh_max(float v) {   // max over lanes l and l^32
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+
+__device__ __forceinline__ float xh_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+__device__ __forceinline__ bf16x8_t pack8(const f32x16_t& a, int off) {
+  s16x8_t v;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = (short)f2bf(a[off + j]);
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+
+// per-lane LDS byte offsets of the fragments, tile-relative (row n of K for k-step ks; Vᵀ rows r0 / r0 + 8 for d-tile
+// dt). The swizzle depends on row & 15 only, so every 16-row shift of a fragment is a constant (immediate) offset.
+struct Frag32 {
+  int k[8];
+  int v[4][2];
+};
+
+__device__ __forceinline__ void frag32_offsets(Frag32& f, int lane) {
+  const int h = lane >> 5, n = lane & 31, hi = (lane >> 4) & 1, i16 = lane & 15, q = i16 >> 2, pp = i16 & 3;
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks) f.k[ks] = lds_off<128>(n, ks * 2 + h);
+  const int r0 = 4 * h + q, r1 = r0 + 8;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) {
+    const int c = (dt * 32 + hi * 16 + 4 * pp) >> 3;
+    f.v[dt][0] = r0 * 256 + ((c ^ swz<128>(r0)) << 4) + ((pp & 1) << 3);
+    f.v[dt][1] = r1 * 256 + ((c ^ swz<128>(r1)) << 4) + ((pp & 1) << 3);
+  }
+}
+
+__device__ __forceinline__ bf16x8_t tr_pair(const char* lds, int o0, int o1) {
+  const s16x4_t v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4_t, lds + o0));
+  const s16x4_t v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4_t, lds + o1));
+  const s16x8_t v = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+
+// one 64-key tile for a wave's 32 queries (query n = lane&31 is `q`); l is this lane's partial row sum
+template <bool MASK>
+__device__ __forceinline__ void fwd32_tile(const char* sK, const char* sV, const bf16x8_t (&qf)[8],
+                                           f32x16_t (&o)[4], float& m, float& l, int k0, int q, int S, int causal,
+                                           float c2, int lane) {
+  const int h = lane >> 5;
+  Frag32 fo;
+  frag32_offsets(fo, lane);
+  f32x16_t s[2];
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt) {
+    s[kt] = f32x16_t{};
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      const bf16x8_t kf = *reinterpret_cast<const bf16x8_t*>(sK + fo.k[ks] + kt * 32 * 256);
+      s[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], s[kt], 0, 0, 0);
+    }
+  }
+  float mx = -INFINITY;
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      if (MASK) {
+        const int key = k0 + kt * 32 + 8 * (r >> 2) + 4 * h + (r & 3);
+        s[kt][r] = (key >= S || (causal && key > q)) ? -INFINITY : s[kt][r];
+      }
+      mx = fmaxf(mx, s[kt][r]);
+    }
+  mx = xh_max(mx);
+  const float ms = mx * c2;
+  const bool bump = ms > m + RESCALE_TH;
+  if (__builtin_amdgcn_ballot_w64(bump)) {
+    const float mn = bump ? ms : m;
+    const float alpha = fexp2(m - mn);
+    l *= alpha;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
+    m = mn;
+  }
+  const float nm = -m;
+  float rs = 0.f;
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float p = fexp2(__builtin_fmaf(s[kt][r], c2, nm));
+      s[kt][r] = p;
+      rs += p;
+    }
+  l += rs;
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      const bf16x8_t pf = pack8(s[kt], 8 * st);
+      const int kb = (kt * 32 + 16 * st) * 256;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+        o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_pair(sV, fo.v[dt][0] + kb, fo.v[dt][1] + kb), pf, o[dt],
+                                                        0, 0, 0);
+    }
+}
+
+// LDS-DMA of a full 64-row tile: wave-uniform global base + 32-bit per-lane byte offsets computed once (soff), so
+// the loads take the saddr + voffset form and the LDS base (M0) is scalar
+__device__ __forceinline__ void stage_full64(char* lds, const bf16_t* g, const unsigned (&soff)[4], int w) {
+  const char* gb = reinterpret_cast<const char*>(g);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) glds16_asm(gb + soff[i], lds + (w + 4 * i) * 1024);
+}
+
+// stage_rows with the asm DMA (ragged last tile: rows >= nvalid clamped to the last valid row)
+__device__ __forceinline__ void stage_rows64_asm(char* lds, const bf16_t* g, long long ld, int nvalid, int w,
+                                                 int lane) {
+  const int last = nvalid - 1;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int j = w + 4 * i;
+    const int row = j * 4 + (lane >> 4);
+    const int c = (lane & 15) ^ swz<128>(row);
+    const int srow = row < last ? row : last;
+    glds16_asm(g + srow * ld + c * 8, lds + j * 1024);
+  }
+}
+
+// block = 128 queries of one (b, h), wave w owns 32; K/V 64-key tiles double-buffered by LDS-DMA, one barrier/tile;
+// the tile loop is unrolled by two so both buffers' fragment addresses are immediates
+__global__ __launch_bounds__(NTH, 2) void attn_fwd32_kernel(AttnArgs a) {
+  constexpr int D = 128;
+  constexpr int TILE = 64 * 256;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, n = lane & 31;
+  const int bh = blockIdx.y, b = bh / a.H, hd = bh % a.H;
+  const int qblk = (a.causal ? (gridDim.x - 1 - blockIdx.x) : blockIdx.x) * 128;
+  const int qw = qblk + w * 32;
+  const int q = qw + n;
+  const long long base = (long long)b * a.S * a.ld + hd * D;
+  const bf16_t* Kb = a.K + base;
+  const bf16_t* Vb = a.V + base;
+  const int kend = a.causal ? min(a.S, qblk + 128) : a.S;
+  const int nkb = (kend + 63) / 64;
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  unsigned soff[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = (wu + 4 * i) * 4 + (lane >> 4);
+    soff[i] = (unsigned)(row * (int)a.ld + (((lane & 15) ^ swz<128>(row)) << 3)) * 2u;
+  }
+  auto stage = [&](char* buf, int k0) {
+    k0 = __builtin_amdgcn_readfirstlane(k0);
+    if (k0 + 64 <= a.S) {
+      stage_full64(buf, Kb + (long long)k0 * a.ld, soff, wu);
+      stage_full64(buf + TILE, Vb + (long long)k0 * a.ld, soff, wu);
+    } else {
+      stage_rows64_asm(buf, Kb + (long long)k0 * a.ld, a.ld, a.S - k0, wu, lane);
+      stage_rows64_asm(buf + TILE, Vb + (long long)k0 * a.ld, a.ld, a.S - k0, wu, lane);
+    }
+  };
+  stage(smem, 0);
+  bf16x8_t qf[8];
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks) qf[ks] = load_frag_g(a.Q + base + (long long)q * a.ld + ks * 16 + 8 * h, q < a.S);
+  // consume Q here so the compiler's own vmcnt wait for it lands in the prologue, not in front of the first MFMA
+  // of every tile (where it would also wait for the next tile's in-flight DMA)
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks) asm volatile("" ::"v"(qf[ks]));
+  f32x16_t o[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) o[dt] = f32x16_t{};
+  float m = NEG_BIG, l = 0.f;
+  const float c2 = a.scale * LOG2E;
+  vm_wait<0>();
+  __syncthreads();
+  for (int kb = 0; kb < nkb; ++kb) {
+    const int k0 = kb * 64;
+    const char* sK = smem + (kb & 1) * 2 * TILE;
+    const char* sV = sK + TILE;
+    if (kb + 1 < nkb) stage(smem + ((kb + 1) & 1) * 2 * TILE, k0 + 64);
+    if (!(a.causal && k0 > qw + 31)) {
+      const bool need_mask = (a.causal && k0 + 63 > qw) || k0 + 64 > a.S;
+      if (need_mask) fwd32_tile<true>(sK, sV, qf, o, m, l, k0, q, a.S, a.causal, c2, lane);
+      else fwd32_tile<false>(sK, sV, qf, o, m, l, k0, q, a.S, a.causal, c2, lane);
+    }
+    vm_wait<0>();        // the next tile's DMA (issued before this tile's compute) has landed
+    __syncthreads();
+  }
+  l = xh_sum(l);
+  if (q < a.S) {
+    const float inv = 1.f / l;
+    bf16_t* orow = a.Oout + base + (long long)q * a.ld;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d = dt * 32 + 8 * g4 + 4 * h;
+        *reinterpret_cast<uint2*>(orow + d) =
+            make_uint2(pack_bf16x2(o[dt][4 * g4] * inv, o[dt][4 * g4 + 1] * inv),
+                       pack_bf16x2(o[dt][4 * g4 + 2] * inv, o[dt][4 * g4 + 3] * inv));
+      }
+    if (h == 0) a.LSE[((long long)b * a.H + hd) * a.S + q] = (m + __log2f(l)) / LOG2E;
+  }
+}
+
+// ----------------------------------------------------------------------------------------------------------------
+// Forward v3: software-pipelined over 32-key sub-tiles. Iteration j issues the QKᵀ MFMAs of sub-tile j+1 (into a
+// second score register block) while the VALU does the softmax of sub-tile j, then P·V of sub-tile j -- each wave
+// always has independent MFMA work beside its own softmax instead of relying on the partner wave. K and V live in
+// separate double buffers with staggered lifetimes so one barrier per sub-tile suffices and each 16 KiB DMA has two
+// sub-tile iterations to land:
+//   iteration 2t   : wait V(t), barrier, DMA V(t+1) -> Vbuf[(t+1)&1];  QK(2t+1) on K(t), softmax+PV(2t) on V(t)
+//   iteration 2t+1 : wait K(t+1), barrier, DMA K(t+2) -> Kbuf[t&1];     QK(2t+2) on K(t+1), softmax+PV(2t+1) on V(t)
+// (WAR: K(t) was last read by QK(2t+1) in iteration 2t, V(t-1) by PV(2t-1) in iteration 2t-1, both before the
+// barrier that precedes their buffer's refill; RAW: the counted vmcnt leaves only the most recent DMA in flight.)
+__device__ __forceinline__ void qk_sub(f32x16_t& sc, const char* sK, int sub, const bf16x8_t (&qf)[8], int lane) {
+  const int h = lane >> 5, n = lane & 31;
+  sc = f32x16_t{};
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks) {
+    const bf16x8_t kf = *reinterpret_cast<const bf16x8_t*>(sK + sub * 32 * 256 + lds_off<128>(n, ks * 2 + h));
+    sc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], sc, 0, 0, 0);
+  }
+}
+
+template <bool MASK>
+__device__ __forceinline__ void softmax_pv_sub(f32x16_t& sc, const char* sV, int sub, f32x16_t (&o)[4], float& m,
+                                               float& l, int key0, int q, int S, float c2, int lane) {
+  const int h = lane >> 5, hi = (lane >> 4) & 1, i16 = lane & 15, qq = i16 >> 2, pp = i16 & 3;
+  float mx = -INFINITY;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    if (MASK) {
+      const int key = key0 + 8 * (r >> 2) + 4 * h + (r & 3);
+      sc[r] = (key >= S || key > q) ? -INFINITY : sc[r];
+    }
+    mx = fmaxf(mx, sc[r]);
+  }
+  mx = xh_max(mx);
+  const float ms = mx * c2;
+  const bool bump = ms > m + RESCALE_TH;
+  if (__builtin_amdgcn_ballot_w64(bump)) {
+    const float mn = bump ? ms : m;
+    const float alpha = fexp2(m - mn);
+    l *= alpha;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
+    m = mn;
+  }
+  const float nm = -m;
+  float rs = 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const float p = fexp2(__builtin_fmaf(sc[r], c2, nm));
+    sc[r] = p;
+    rs += p;
+  }
+  l += rs;
+  const int r0 = 4 * h + qq, r1 = r0 + 8;
+#pragma unroll
+  for (int st = 0; st < 2; ++st) {
+    const bf16x8_t pf = pack8(sc, 8 * st);
+    const int kb = (sub * 32 + 16 * st) * 256;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const int c = (dt * 32 + hi * 16 + 4 * pp) >> 3;
+      const int o0 = r0 * 256 + ((c ^ swz<128>(r0)) << 4) + ((pp & 1) << 3);
+      const int o1 = r1 * 256 + ((c ^ swz<128>(r1)) << 4) + ((pp & 1) << 3);
+      o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_pair(sV, o0 + kb, o1 + kb), pf, o[dt], 0, 0, 0);
+    }
+  }
+}
+
+__global__ __launch_bounds__(NTH, 2) void attn_fwd3_kernel(AttnArgs a) {
+  constexpr int D = 128;
+  constexpr int TILE = 64 * 256;
+  extern __shared__ __attribute__((aligned(16))) char smem[];   // Kbuf[2] then Vbuf[2]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, n = lane & 31;
+  const int bh = blockIdx.y, b = bh / a.H, hd = bh % a.H;
+  const int qblk = (a.causal ? (gridDim.x - 1 - blockIdx.x) : blockIdx.x) * 128;
+  const int qw = qblk + w * 32;
+  const int q = qw + n;
+  const long long base = (long long)b * a.S * a.ld + hd * D;
+  const bf16_t* Kb = a.K + base;
+  const bf16_t* Vb = a.V + base;
+  const int kend = a.causal ? min(a.S, qblk + 128) : a.S;
+  const int ntile = (kend + 63) / 64, nsub = (kend + 31) / 32;
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  unsigned soff[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = (wu + 4 * i) * 4 + (lane >> 4);
+    soff[i] = (unsigned)(row * (int)a.ld + (((lane & 15) ^ swz<128>(row)) << 3)) * 2u;
+  }
+  char* Kbuf = smem;
+  char* Vbuf = smem + 2 * TILE;
+  auto stage = [&](char* buf, const bf16_t* src, int t) {
+    const int k0 = __builtin_amdgcn_readfirstlane(t * 64);
+    if (k0 + 64 <= a.S) stage_full64(buf, src + (long long)k0 * a.ld, soff, wu);
+    else stage_rows64_asm(buf, src + (long long)k0 * a.ld, a.ld, a.S - k0, wu, lane);
+  };
+  stage(Kbuf, Kb, 0);
+  stage(Vbuf, Vb, 0);
+  if (ntile > 1) stage(Kbuf + TILE, Kb, 1);
+  bf16x8_t qf[8];
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks) qf[ks] = load_frag_g(a.Q + base + (long long)q * a.ld + ks * 16 + 8 * h, q < a.S);
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks) asm volatile("" ::"v"(qf[ks]));
+  f32x16_t o[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) o[dt] = f32x16_t{};
+  float m = NEG_BIG, l = 0.f;
+  const float c2 = a.scale * LOG2E;
+  const bool causal = a.causal;
+  vm_wait<0>();
+  __syncthreads();
+  f32x16_t sc, sn;
+  if (!(causal && 0 > qw + 31)) qk_sub(sc, Kbuf, 0, qf, lane);
+  bool pendK = false, pendV = false;
+  for (int j = 0; j < nsub; ++j) {
+    const int t = j >> 1, half = j & 1;
+    if (!half) {                         // even: V(t) must have landed; refill Vbuf[(t+1)&1] with V(t+1)
+      if (j > 0) {
+        if (pendK) vm_wait<4>(); else vm_wait<0>();
+        __syncthreads();
+      }
+      pendV = t + 1 < ntile;
+      if (pendV) stage(Vbuf + ((t + 1) & 1) * TILE, Vb, t + 1);
+    } else {                             // odd: K(t+1) must have landed; refill Kbuf[t&1] with K(t+2)
+      if (pendV) vm_wait<4>(); else vm_wait<0>();
+      __syncthreads();
+      pendK = t + 2 < ntile;
+      if (pendK) stage(Kbuf + (t & 1) * TILE, Kb, t + 2);
+    }
+    const int jn = j + 1;
+    const int key0 = j * 32;
+    const bool next_live = jn < nsub && !(causal && jn * 32 > qw + 31);
+    if (next_live) qk_sub(sn, Kbuf + ((jn >> 1) & 1) * TILE, jn & 1, qf, lane);
+    if (!(causal && key0 > qw + 31)) {
+      const char* sV = Vbuf + (t & 1) * TILE;
+      const bool need_mask = (causal && key0 + 31 > qw) || key0 + 32 > a.S;
+      if (need_mask) softmax_pv_sub<true>(sc, sV, half, o, m, l, key0, causal ? q : 0x7fffffff, a.S, c2, lane);
+      else softmax_pv_sub<false>(sc, sV, half, o, m, l, key0, q, a.S, c2, lane);
+    }
+    sc = sn;
+  }
+  l = xh_sum(l);
+  if (q < a.S) {
+    const float inv = 1.f / l;
+    bf16_t* orow = a.Oout + base + (long long)q * a.ld;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d = dt * 32 + 8 * g4 + 4 * h;
+        *reinterpret_cast<uint2*>(orow + d) =
+            make_uint2(pack_bf16x2(o[dt][4 * g4] * inv, o[dt][4 * g4 + 1] * inv),
+                       pack_bf16x2(o[dt][4 * g4 + 2] * inv, o[dt][4 * g4 + 3] * inv));
+      }
+    if (h == 0) a.LSE[((long long)b * a.H + hd) * a.S + q] = (m + __log2f(l)) / LOG2E;
+  }
+}
+
+static int attn_impl() {   // OBST_ATTN_IMPL=1 forces the 16x16x32 kernels (A/B comparisons)
+  static int v = [] { const char* e = getenv("OBST_ATTN_IMPL"); return e ? atoi(e) : 2; }();
+  return v;
+}
+
 template <int D>
 int launch_fwd(const AttnArgs& a, hipStream_t st) {
   dim3 grid((a.S + 127) / 128, a.B * a.H);
+  if (D == 128 && attn_impl() >= 3) {
+    hipLaunchKernelGGL(attn_fwd3_kernel, grid, dim3(NTH), 4 * 64 * 256, st, a);
+    return (int)hipGetLastError();
+  }
+  if (D == 128 && attn_impl() == 2) {
+    hipLaunchKernelGGL(attn_fwd32_kernel, grid, dim3(NTH), 4 * 64 * 256, st, a);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(attn_fwd_kernel<D>, grid, dim3(NTH), 4 * 64 * Geo<D>::ROWB, st, a);
   return (int)hipGetLastError();
 }

@@ -14,6 +14,26 @@ typedef __attribute__((ext_vector_type(8))) short s16x8_t;
 
 #define LDS_PTR(T, p) ((__attribute__((address_space(3))) T*)(p))
 
+// LDS-DMA of 16 bytes per lane (1 KiB per wave-instruction) issued from inline asm: the compiler then does not know
+// an LDS write is in flight, so it inserts no conservative `s_waitcnt vmcnt(0)` in front of every later LDS read
+// (it cannot prove the DMA's destination buffer differs from the one being read, and that wait collapses any
+// multi-stage pipeline). The price: every consumer must wait explicitly -- `vm_wait<N>()` before the barrier that
+// publishes a staged tile (a fence/__syncthreads alone is not enough, the compiler believes nothing is pending).
+// M0 is written here and used by no compiler-generated instruction in kernels that stage only through this helper.
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+__device__ __forceinline__ void glds16_asm(const void* g, const void* lds_wave_base) {
+  const unsigned m0 = __builtin_amdgcn_readfirstlane(
+      (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)lds_wave_base);
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(m0) : "memory", "m0");
+}
+#pragma clang diagnostic pop
+
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
 __device__ __forceinline__ float bf2f(bf16_t v) {
   return __uint_as_float(((uint32_t)v) << 16);
 }
