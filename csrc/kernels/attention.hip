@@ -111,6 +111,16 @@ __device__ __forceinline__ bf16x8_t load_frag_g(const bf16_t* p, bool ok) {
   return *reinterpret_cast<const bf16x8_t*>(p);
 }
 
+// XCD-aware block coordinates for a 1-D grid of nx * (B*H) blocks (T1): the bijective XCD remap puts consecutive
+// logical blocks -- the nx blocks of one (b, h), which all stream the same K/V (forward, dQ) or Q/dO (dK/dV) -- on
+// the same XCD, so those re-reads hit that XCD's L2 instead of MALL/HBM.
+__device__ __forceinline__ void attn_block(int nx, int& bx, int& bh) {
+  const int nwg = gridDim.x, bid = blockIdx.x, xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int L = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  bx = L % nx;
+  bh = L / nx;
+}
+
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr float NEG_BIG = -1e30f;
 
@@ -228,9 +238,12 @@ __global__ __launch_bounds__(NTH, 2) void attn_fwd_kernel(AttnArgs a) {
   constexpr int TILE = 64 * G::ROWB;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, i = lane & 15;
-  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+  const int nx = (a.S + 127) / 128;
+  int bx, bh;
+  attn_block(nx, bx, bh);
+  const int b = bh / a.H, h = bh % a.H;
   // heaviest causal blocks first: the tail of the grid then fills with short blocks
-  const int qblk = (a.causal ? (gridDim.x - 1 - blockIdx.x) : blockIdx.x) * 128;
+  const int qblk = (a.causal ? (nx - 1 - bx) : bx) * 128;
   const int qw = qblk + w * 32;
   const bf16_t* Qb = a.Q + (long long)b * a.S * a.ld + h * D;
   const bf16_t* Kb = a.K + (long long)b * a.S * a.ld + h * D;
@@ -380,8 +393,11 @@ __global__ __launch_bounds__(NTH, 2) void attn_bwd_dq_kernel(AttnArgs a) {
   constexpr int TILE = 64 * G::ROWB;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, i = lane & 15;
-  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
-  const int qblk = (a.causal ? (gridDim.x - 1 - blockIdx.x) : blockIdx.x) * 128;  // heaviest first
+  const int nx = (a.S + 127) / 128;
+  int bx, bh;
+  attn_block(nx, bx, bh);
+  const int b = bh / a.H, h = bh % a.H;
+  const int qblk = (a.causal ? (nx - 1 - bx) : bx) * 128;  // heaviest first
   const int qw = qblk + w * 32;
   const long long base = (long long)b * a.S * a.ld + h * D;
   const int kend = a.causal ? min(a.S, qblk + 128) : a.S;
@@ -506,8 +522,10 @@ __global__ __launch_bounds__(NTH, 2) void attn_bwd_dkv_kernel(AttnArgs a) {
   constexpr int STAGE = 2 * TILE + 2 * 256;   // Q, dO, lse[64], delta[64]
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, i = lane & 15;
-  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
-  const int kblk = blockIdx.x * 64;
+  int bx, bh;
+  attn_block((a.S + 63) / 64, bx, bh);
+  const int b = bh / a.H, h = bh % a.H;
+  const int kblk = bx * 64;
   const int kw = kblk + w * 16;
   const long long base = (long long)b * a.S * a.ld + h * D;
   const long long sbase = ((long long)b * a.H + h) * a.S;
@@ -712,8 +730,11 @@ __global__ __launch_bounds__(NTH, 2) void attn_fwd32_kernel(AttnArgs a) {
   constexpr int TILE = 64 * 256;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, n = lane & 31;
-  const int bh = blockIdx.y, b = bh / a.H, hd = bh % a.H;
-  const int qblk = (a.causal ? (gridDim.x - 1 - blockIdx.x) : blockIdx.x) * 128;
+  const int nx = (a.S + 127) / 128;
+  int bx, bh;
+  attn_block(nx, bx, bh);
+  const int b = bh / a.H, hd = bh % a.H;
+  const int qblk = (a.causal ? (nx - 1 - bx) : bx) * 128;
   const int qw = qblk + w * 32;
   const int q = qw + n;
   const long long base = (long long)b * a.S * a.ld + hd * D;
@@ -856,8 +877,11 @@ __global__ __launch_bounds__(NTH, 2) void attn_fwd3_kernel(AttnArgs a) {
   constexpr int TILE = 64 * 256;
   extern __shared__ __attribute__((aligned(16))) char smem[];   // Kbuf[2] then Vbuf[2]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, n = lane & 31;
-  const int bh = blockIdx.y, b = bh / a.H, hd = bh % a.H;
-  const int qblk = (a.causal ? (gridDim.x - 1 - blockIdx.x) : blockIdx.x) * 128;
+  const int nx = (a.S + 127) / 128;
+  int bx, bh;
+  attn_block(nx, bx, bh);
+  const int b = bh / a.H, hd = bh % a.H;
+  const int qblk = (a.causal ? (nx - 1 - bx) : bx) * 128;
   const int qw = qblk + w * 32;
   const int q = qw + n;
   const long long base = (long long)b * a.S * a.ld + hd * D;
@@ -942,14 +966,189 @@ __global__ __launch_bounds__(NTH, 2) void attn_fwd3_kernel(AttnArgs a) {
   }
 }
 
+// ----------------------------------------------------------------------------------------------------------------
+// D = 128 dK/dV with v_mfma_f32_32x32x16_bf16: block = 128 keys, wave w owns keys kw = kblk + 32w + [0, 32) (key
+// n = lane&31 on the lane, K and V of that key held in registers as B operands for the whole block). Per 32-query
+// sub-chunk: S = Q·Kᵀ and dP = dO·Vᵀ (queries on the 16 accumulator registers, A operands = Q / dO rows from LDS),
+// P = exp2(S·c2 - lse), dS = P·(dP - delta) (dP's accumulator starts at -delta), then dVᵀ += dOᵀ·P and dKᵀ += Qᵀ·dS
+// sum over the accumulators' ROW index, so P / dS feed the MFMA as B operands straight from the registers (permuted
+// k order) and the matching dOᵀ / Qᵀ A operands are read from the [q][d] LDS images with ds_read_b64_tr_b16.
+// Against the 16-keys-per-wave kernel this halves the LDS bytes per MFMA (every Q / dO fragment read from LDS now
+// serves 32 keys). Q, dO (64 rows), lse and delta (64 values) are double-buffered by LDS-DMA one chunk ahead.
+
+// S = Q·Kᵀ and dP = dO·Vᵀ - delta for one 32-query sub-chunk (accumulator register r <-> query row
+// 8(r>>2) + 4h + (r&3) of the sub-chunk)
+__device__ __forceinline__ void dkv32_scores(const char* sQ, const char* sD, const float* sDl, const Frag32& fo,
+                                             const bf16x8_t (&kf)[8], const bf16x8_t (&vf)[8], f32x16_t& s,
+                                             f32x16_t& dp, int sub, int lane) {
+  const int h = lane >> 5;
+  const int rb = sub * 32 * 256;
+  s = f32x16_t{};
+#pragma unroll
+  for (int a4 = 0; a4 < 4; ++a4) {
+    const float4 dl = *reinterpret_cast<const float4*>(sDl + sub * 32 + 8 * a4 + 4 * h);
+    dp[4 * a4 + 0] = -dl.x; dp[4 * a4 + 1] = -dl.y; dp[4 * a4 + 2] = -dl.z; dp[4 * a4 + 3] = -dl.w;
+  }
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks) {
+    const bf16x8_t qa = *reinterpret_cast<const bf16x8_t*>(sQ + fo.k[ks] + rb);
+    const bf16x8_t da = *reinterpret_cast<const bf16x8_t*>(sD + fo.k[ks] + rb);
+    s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, kf[ks], s, 0, 0, 0);
+    dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da, vf[ks], dp, 0, 0, 0);
+  }
+}
+
+// P = exp2(S·c2 - lse·log2e), dS = P·dP; then dVᵀ += dOᵀ·P, dKᵀ += Qᵀ·dS. Branch-free masking (a branch around
+// the MFMAs makes the compiler carry the dK/dV accumulators through VGPR<->AGPR copies): element r of the lane is
+// query row j = 8(r>>2) + (r&3) (+ the lane's 4h), so "key > q" is "j < tc" and "q >= S" is "j >= tq" with two
+// per-lane thresholds tc, tq and a compile-time j.
+__device__ __forceinline__ void dkv32_update(const char* sQ, const char* sD, const float* sL, const Frag32& fo,
+                                             f32x16_t& s, f32x16_t& dp, f32x16_t (&dk)[4], f32x16_t (&dv)[4],
+                                             int sub, int tc, int tq, float c2, int lane) {
+  const int h = lane >> 5;
+  const int rb = sub * 32 * 256;
+#pragma unroll
+  for (int a4 = 0; a4 < 4; ++a4) {
+    const float4 lv = *reinterpret_cast<const float4*>(sL + sub * 32 + 8 * a4 + 4 * h);
+    const float nl[4] = {-lv.x * LOG2E, -lv.y * LOG2E, -lv.z * LOG2E, -lv.w * LOG2E};
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int r = 4 * a4 + b, j = 8 * a4 + b;
+      float p = fexp2(__builtin_fmaf(s[r], c2, nl[b]));
+      p = (j < tc || j >= tq) ? 0.f : p;
+      s[r] = p;
+      dp[r] = p * dp[r];
+    }
+  }
+#pragma unroll
+  for (int st = 0; st < 2; ++st) {
+    const bf16x8_t pb = pack8(s, 8 * st);
+    const bf16x8_t sb = pack8(dp, 8 * st);
+    const int kb = rb + 16 * st * 256;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      dv[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_pair(sD, fo.v[dt][0] + kb, fo.v[dt][1] + kb), pb, dv[dt],
+                                                       0, 0, 0);
+      dk[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_pair(sQ, fo.v[dt][0] + kb, fo.v[dt][1] + kb), sb, dk[dt],
+                                                       0, 0, 0);
+    }
+  }
+}
+
+__global__ __launch_bounds__(NTH, 1) void attn_bwd_dkv32_kernel(AttnArgs a) {
+  constexpr int D = 128;
+  constexpr int QC = 64;
+  constexpr int TILE = QC * 256;
+  constexpr int STAGE = 2 * TILE + 2 * 256;   // Q, dO, lse[64], delta[64]
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  // an AGPR named in inline asm keeps the compiler from inferring "no AGPRs": the MFMAs are then selected in the
+  // AGPR-accumulator form, so the 128 dK/dV accumulator registers live in AGPRs instead of being shuttled between
+  // the VGPR and AGPR files (v_accvgpr_read/write) when the kernel's >256 live registers overflow the VGPRs
+  asm volatile("" ::: "a255");
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, n = lane & 31;
+  int bx, bh;
+  attn_block((a.S + 127) / 128, bx, bh);
+  const int b = bh / a.H, hd = bh % a.H;
+  const int kblk = bx * 128;
+  const int kw = kblk + w * 32;
+  const int key = kw + n;
+  const long long base = (long long)b * a.S * a.ld + hd * D;
+  const long long sbase = ((long long)b * a.H + hd) * a.S;
+  const bf16_t* Qb = a.Q + base;
+  const bf16_t* Db = a.dO + base;
+  const int qstart = a.causal ? (kblk / QC) * QC : 0;
+  const int nqc = (a.S - qstart + QC - 1) / QC;
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  unsigned soff[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = (wu + 4 * i) * 4 + (lane >> 4);
+    soff[i] = (unsigned)(row * (int)a.ld + (((lane & 15) ^ swz<128>(row)) << 3)) * 2u;
+  }
+  auto stage = [&](char* buf, int q0) {
+    q0 = __builtin_amdgcn_readfirstlane(q0);
+    if (q0 + QC <= a.S) {
+      stage_full64(buf, Qb + (long long)q0 * a.ld, soff, wu);
+      stage_full64(buf + TILE, Db + (long long)q0 * a.ld, soff, wu);
+    } else {
+      stage_rows64_asm(buf, Qb + (long long)q0 * a.ld, a.ld, a.S - q0, wu, lane);
+      stage_rows64_asm(buf + TILE, Db + (long long)q0 * a.ld, a.ld, a.S - q0, wu, lane);
+    }
+    if (wu < 2) {   // wave 0: lse, wave 1: delta (64 x 4 B, lane-linear)
+      const float* src = (wu == 0 ? a.LSE : a.delta) + sbase;
+      const int qq = min(q0 + lane, a.S - 1);
+      glds4_asm(src + qq, buf + 2 * TILE + wu * 256);
+    }
+  };
+  if (nqc > 0) stage(smem, qstart);
+
+  bf16x8_t kf[8], vf[8];
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks) {
+    kf[ks] = load_frag_g(a.K + base + (long long)key * a.ld + ks * 16 + 8 * h, key < a.S);
+    vf[ks] = load_frag_g(a.V + base + (long long)key * a.ld + ks * 16 + 8 * h, key < a.S);
+  }
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks) asm volatile("" ::"v"(kf[ks]), "v"(vf[ks]));
+  Frag32 fo;
+  frag32_offsets(fo, lane);
+  f32x16_t dk[4], dv[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) dk[dt] = dv[dt] = f32x16_t{};
+  const float c2 = a.scale * LOG2E;
+  vm_wait<0>();
+  __syncthreads();
+  for (int c = 0; c < nqc; ++c) {
+    const int q0 = qstart + c * QC;
+    const char* sQ = smem + (c & 1) * STAGE;
+    const char* sD = sQ + TILE;
+    const float* sL = reinterpret_cast<const float*>(sQ + 2 * TILE);
+    const float* sDl = sL + 64;
+    if (c + 1 < nqc) stage(smem + ((c + 1) & 1) * STAGE, q0 + QC);
+    {   // both sub-chunks straight-line: the score MFMAs of sub-chunk 1 overlap the softmax VALU of sub-chunk 0
+      f32x16_t s0, dp0, s1, dp1;
+      dkv32_scores(sQ, sD, sDl, fo, kf, vf, s0, dp0, 0, lane);
+      dkv32_scores(sQ, sD, sDl, fo, kf, vf, s1, dp1, 1, lane);
+      const int rel = q0 + 4 * h;                 // query of element j in sub-chunk u: rel + 32u + j
+      const int tc0 = a.causal ? key - rel : -1000000, tc1 = tc0 - 32;
+      const int tq0 = a.S - rel, tq1 = tq0 - 32;
+      dkv32_update(sQ, sD, sL, fo, s0, dp0, dk, dv, 0, tc0, tq0, c2, lane);
+      dkv32_update(sQ, sD, sL, fo, s1, dp1, dk, dv, 1, tc1, tq1, c2, lane);
+    }
+    vm_wait<0>();
+    __syncthreads();
+  }
+  if (key < a.S) {
+    bf16_t* krow = a.dK + base + (long long)key * a.ld;
+    bf16_t* vrow = a.dV + base + (long long)key * a.ld;
+    const float sc = a.scale;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d = dt * 32 + 8 * g4 + 4 * h;
+        *reinterpret_cast<uint2*>(krow + d) =
+            make_uint2(pack_bf16x2(dk[dt][4 * g4] * sc, dk[dt][4 * g4 + 1] * sc),
+                       pack_bf16x2(dk[dt][4 * g4 + 2] * sc, dk[dt][4 * g4 + 3] * sc));
+        *reinterpret_cast<uint2*>(vrow + d) =
+            make_uint2(pack_bf16x2(dv[dt][4 * g4], dv[dt][4 * g4 + 1]), pack_bf16x2(dv[dt][4 * g4 + 2], dv[dt][4 * g4 + 3]));
+      }
+  }
+}
+
 static int attn_impl() {   // OBST_ATTN_IMPL=1 forces the 16x16x32 kernels (A/B comparisons)
   static int v = [] { const char* e = getenv("OBST_ATTN_IMPL"); return e ? atoi(e) : 2; }();
   return v;
 }
 
+static int attn_bwd_impl() {   // OBST_ATTN_BWD=2 selects the 32x32x16 dK/dV kernel (slower so far: A/B only)
+  static int v = [] { const char* e = getenv("OBST_ATTN_BWD"); return e ? atoi(e) : 1; }();
+  return v;
+}
+
 template <int D>
 int launch_fwd(const AttnArgs& a, hipStream_t st) {
-  dim3 grid((a.S + 127) / 128, a.B * a.H);
+  dim3 grid((a.S + 127) / 128 * a.B * a.H);
   if (D == 128 && attn_impl() >= 3) {
     hipLaunchKernelGGL(attn_fwd3_kernel, grid, dim3(NTH), 4 * 64 * 256, st, a);
     return (int)hipGetLastError();
@@ -966,9 +1165,13 @@ template <int D>
 int launch_bwd(const AttnArgs& a, hipStream_t st) {
   const long long rows = (long long)a.B * a.S * a.H;
   hipLaunchKernelGGL(attn_delta_kernel<D>, dim3((unsigned)((rows + 3) / 4)), dim3(NTH), 0, st, a);
-  hipLaunchKernelGGL(attn_bwd_dkv_kernel<D>, dim3((a.S + 63) / 64, a.B * a.H), dim3(NTH),
-                     2 * (2 * 64 * Geo<D>::ROWB + 512), st, a);
-  hipLaunchKernelGGL(attn_bwd_dq_kernel<D>, dim3((a.S + 127) / 128, a.B * a.H), dim3(NTH), 4 * 64 * Geo<D>::ROWB, st, a);
+  if (D == 128 && attn_bwd_impl() == 2)
+    hipLaunchKernelGGL(attn_bwd_dkv32_kernel, dim3((a.S + 127) / 128 * a.B * a.H), dim3(NTH), 2 * (2 * 64 * 256 + 512),
+                       st, a);
+  else
+    hipLaunchKernelGGL(attn_bwd_dkv_kernel<D>, dim3((a.S + 63) / 64 * a.B * a.H), dim3(NTH),
+                       2 * (2 * 64 * Geo<D>::ROWB + 512), st, a);
+  hipLaunchKernelGGL(attn_bwd_dq_kernel<D>, dim3((a.S + 127) / 128 * a.B * a.H), dim3(NTH), 4 * 64 * Geo<D>::ROWB, st, a);
   return (int)hipGetLastError();
 }
 

@@ -27,6 +27,12 @@ __device__ __forceinline__ void glds16_asm(const void* g, const void* lds_wave_b
       (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)lds_wave_base);
   asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(m0) : "memory", "m0");
 }
+// 4 bytes per lane (256 B per wave-instruction, lane-linear in LDS), same contract as glds16_asm
+__device__ __forceinline__ void glds4_asm(const void* g, const void* lds_wave_base) {
+  const unsigned m0 = __builtin_amdgcn_readfirstlane(
+      (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)lds_wave_base);
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off" ::"v"(g), "s"(m0) : "memory", "m0");
+}
 #pragma clang diagnostic pop
 
 template <int N>

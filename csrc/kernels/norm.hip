@@ -29,6 +29,31 @@ __device__ __forceinline__ float sub_sum(float v) {   // across the row-groups o
   return v;
 }
 
+// 8 consecutive fp32 parameters (scale / shift) as two 16-byte loads (col % 8 == 0, F % 8 == 0)
+__device__ __forceinline__ void load8f(const float* p, float (&o)[8]) {
+  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w; o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
+}
+
+template <int NCH, int LPR>
+__device__ __forceinline__ void load_raw(const bf16_t* x, int F, int sl, bool ok, uint4 (&u)[NCH]) {
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = c * LPR * 8 + sl * 8;
+    u[c] = (ok && col < F) ? *reinterpret_cast<const uint4*>(x + col) : make_uint4(0, 0, 0, 0);
+  }
+}
+
+template <int NCH>
+__device__ __forceinline__ void unpack_row(const uint4 (&u)[NCH], float (&v)[NCH][8]) {
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const uint32_t w[4] = {u[c].x, u[c].y, u[c].z, u[c].w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { v[c][2 * j] = bf2f(w[j] & 0xffff); v[c][2 * j + 1] = bf2f(w[j] >> 16); }
+  }
+}
+
 template <int NCH, int LPR>
 __device__ __forceinline__ void load_row(const bf16_t* x, int F, int sl, bool ok, float (&v)[NCH][8]) {
 #pragma unroll
@@ -54,11 +79,15 @@ __global__ __launch_bounds__(NTH) void norm_fwd_kernel(const bf16_t* __restrict_
   constexpr int RPW = 64 / LPR;
   const int lane = threadIdx.x & 63, sub = lane / LPR, sl = lane % LPR;
   const long long nw = (long long)gridDim.x * 4 * RPW;
-  for (long long r0 = ((long long)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW; r0 < rows; r0 += nw) {
+  long long r0 = ((long long)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
+  uint4 nxt[NCH];   // the next row's data is in flight while this row is reduced and written
+  load_raw<NCH, LPR>(X + (r0 + sub) * F, F, sl, r0 + sub < rows, nxt);
+  for (; r0 < rows; r0 += nw) {
     const long long row = r0 + sub;
     const bool ok = row < rows;
     float v[NCH][8];
-    load_row<NCH, LPR>(X + row * F, F, sl, ok, v);
+    unpack_row<NCH>(nxt, v);
+    load_raw<NCH, LPR>(X + (row + nw) * F, F, sl, row + nw < rows, nxt);
     float mean, rstd;
     if (ext_stats) {  // [rows, 2] = (mean, rstd) computed over the full (TP-gathered) feature set
       mean = ok ? ext_stats[2 * row] : 0.f;
@@ -88,12 +117,15 @@ __global__ __launch_bounds__(NTH) void norm_fwd_kernel(const bf16_t* __restrict_
     for (int c = 0; c < NCH; ++c) {
       const int col = c * LPR * 8 + sl * 8;
       if (col >= F) continue;
+      float sc[8], sh[8];
+      if (scale) load8f(scale + poff + col, sc);
+      if (shift) load8f(shift + poff + col, sh);
       uint32_t o[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         float y0 = (v[c][2 * j] - mean) * rstd, y1 = (v[c][2 * j + 1] - mean) * rstd;
-        if (scale) { y0 *= scale[poff + col + 2 * j]; y1 *= scale[poff + col + 2 * j + 1]; }
-        if (shift) { y0 += shift[poff + col + 2 * j]; y1 += shift[poff + col + 2 * j + 1]; }
+        if (scale) { y0 *= sc[2 * j]; y1 *= sc[2 * j + 1]; }
+        if (shift) { y0 += sh[2 * j]; y1 += sh[2 * j + 1]; }
         o[j] = pack_bf16x2(y0, y1);
       }
       *reinterpret_cast<uint4*>(Y + row * F + col) = make_uint4(o[0], o[1], o[2], o[3]);
@@ -142,23 +174,34 @@ __global__ __launch_bounds__(NTH) void norm_bwd_kernel(const bf16_t* __restrict_
     for (int j = 0; j < 8; ++j) gs[c][j] = gb[c][j] = 0.f;
   const long long nw = (long long)gridDim.x * 4 * RPW;
   const long long first = ((long long)blockIdx.x * 4 + w) * RPW + sub;
+  uint4 nx[NCH], nd[NCH];   // next row in flight while this one is processed
+  {
+    const long long row = ((long long)blockIdx.x * 4 + w) * RPW + sub;
+    load_raw<NCH, LPR>(X + row * F, F, sl, row < rows, nx);
+    load_raw<NCH, LPR>(DY + row * F, F, sl, row < rows, nd);
+  }
   for (long long r0 = ((long long)blockIdx.x * 4 + w) * RPW; r0 < rows; r0 += nw) {
     const long long row = r0 + sub;
     const bool ok = row < rows;
     float x[NCH][8], dy[NCH][8];
-    load_row<NCH, LPR>(X + row * F, F, sl, ok, x);
-    load_row<NCH, LPR>(DY + row * F, F, sl, ok, dy);
+    unpack_row<NCH>(nx, x);
+    unpack_row<NCH>(nd, dy);
+    load_raw<NCH, LPR>(X + (row + nw) * F, F, sl, row + nw < rows, nx);
+    load_raw<NCH, LPR>(DY + (row + nw) * F, F, sl, row + nw < rows, nd);
     const float mean = ok ? stats[2 * row] : 0.f, rstd = ok ? stats[2 * row + 1] : 0.f;
     const long long poff = (long long)(row % groups) * F;
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-    for (int c = 0; c < NCH; ++c)
+    for (int c = 0; c < NCH; ++c) {
+      float gsc[8];
+      const int col0 = c * LPR * 8 + sl * 8;
+      if (scale && ok && col0 < F) load8f(scale + poff + col0, gsc);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const int col = c * LPR * 8 + sl * 8 + j;
+        const int col = col0 + j;
         if (ok && col < F) {
           const float xh = (x[c][j] - mean) * rstd;
-          const float g = scale ? scale[poff + col] : 1.f;
+          const float g = scale ? gsc[j] : 1.f;
           const float dxh = dy[c][j] * g;
           s1 += dxh;
           s2 += dxh * xh;
@@ -167,6 +210,7 @@ __global__ __launch_bounds__(NTH) void norm_bwd_kernel(const bf16_t* __restrict_
           dy[c][j] = dxh;
         }
       }
+    }
     s1 = row_sum<LPR>(s1);
     s2 = row_sum<LPR>(s2);
     if (!ok) continue;
@@ -205,21 +249,27 @@ __global__ __launch_bounds__(NTH) void norm_bwd_kernel(const bf16_t* __restrict_
     }
   }
   if (want_param && groups == 1) {
-    // fold the row-groups of the wave, reduce the 4 waves through LDS, then one atomic per element per block
+    // fold the row-groups of the wave, then per chunk reduce the 4 waves through LDS ([2][4][LPR*8] floats) and
+    // issue one atomic per element per block
+    constexpr int CW = LPR * 8;
 #pragma unroll
-    for (int c = 0; c < NCH; ++c)
+    for (int c = 0; c < NCH; ++c) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float a = sub_sum<LPR>(gs[c][j]), b = sub_sum<LPR>(gb[c][j]);
-        const int col = c * LPR * 8 + sl * 8 + j;
-        if (sub == 0 && col < F) { red_s[w * F + col] = a; red_s[(4 + w) * F + col] = b; }
+        if (sub == 0) { red_s[w * CW + sl * 8 + j] = a; red_s[(4 + w) * CW + sl * 8 + j] = b; }
       }
-    __syncthreads();
-    for (int col = threadIdx.x; col < F; col += NTH) {
-      const float a = red_s[col] + red_s[F + col] + red_s[2 * F + col] + red_s[3 * F + col];
-      const float b = red_s[4 * F + col] + red_s[5 * F + col] + red_s[6 * F + col] + red_s[7 * F + col];
-      if (dscale) atomicAdd(dscale + col, a);
-      if (dshift) atomicAdd(dshift + col, b);
+      __syncthreads();
+      for (int k = threadIdx.x; k < CW; k += NTH) {
+        const int col = c * CW + k;
+        if (col < F) {
+          const float a = red_s[k] + red_s[CW + k] + red_s[2 * CW + k] + red_s[3 * CW + k];
+          const float b = red_s[4 * CW + k] + red_s[5 * CW + k] + red_s[6 * CW + k] + red_s[7 * CW + k];
+          if (dscale) atomicAdd(dscale + col, a);
+          if (dshift) atomicAdd(dshift + col, b);
+        }
+      }
+      __syncthreads();
     }
   }
 }
@@ -277,11 +327,11 @@ OBST_API int obst_norm_partial(const ObstNormDesc* d, hipStream_t st) {
 
 OBST_API int obst_norm_bwd(const ObstNormDesc* d, hipStream_t st) {
   if (d->F % 8 || d->rows <= 0) return -1;
-  const size_t lds = (d->groups == 1 && (d->dscale || d->dshift) && !d->partial) ? (size_t)8 * d->F * 4 : 0;
-  if (lds > 160 * 1024) return -3;
-  // more rows per block amortises the parameter-gradient atomics
-  long long g = (d->rows + 31) / 32;
-  int grid = (int)(g < 1024 ? (g < 1 ? 1 : g) : 1024);
+  const size_t lds = (d->groups == 1 && (d->dscale || d->dshift) && !d->partial)
+                         ? (size_t)8 * lanes_per_row(d->F) * 8 * 4 : 0;   // <= 16 KiB
+  // more rows per block amortises the parameter-gradient atomics; 2048 blocks keep ~8 waves per SIMD in flight
+  long long g = (d->rows + 15) / 16;
+  int grid = (int)(g < 2048 ? (g < 1 ? 1 : g) : 2048);
   if (d->groups > 1) {   // rows per grid step (4 waves x 64/LPR rows per block) must be a multiple of groups
     int a = d->groups, b = 4 * (64 / lanes_per_row(d->F));
     while (b) { const int t = a % b; a = b; b = t; }

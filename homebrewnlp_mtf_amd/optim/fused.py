@@ -14,6 +14,7 @@ max-reduced (collectives X10-X12), each as ONE packed RCCL call per step.
 from __future__ import annotations
 
 import math
+import os
 import struct
 import typing
 
@@ -29,7 +30,7 @@ OP = dict(none=0, adaptive_clip=1, l2norm_clip=2, global_l2norm_clip=3, value_cl
           adafactor_clip=13, scale=14)
 REDUCTIONS = {"adaptive_clip", "l2norm_clip", "global_l2norm_clip", "gradient_centralisation", "novograd",
               "adafactor", "adafactor_clip"}
-CHUNK = 65536
+CHUNK = int(os.environ.get("OBST_OPT_CHUNK", 65536))   # elements per apply block (A/B knob)
 
 
 def _f2i(x: float) -> int:
