@@ -5,18 +5,23 @@ HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -munsafe-fp-atomics -Wno
 CXXFLAGS ?= -O3 -std=c++17 -fPIC -Wall -Wno-unused-result
 PKG := homebrewnlp_mtf_amd
 KSRC := $(wildcard csrc/kernels/*.hip)
-KOBJ := $(patsubst csrc/kernels/%.hip,build/kernels/%.o,$(KSRC))
+KCPP := $(wildcard csrc/kernels/*.cpp)
+KOBJ := $(patsubst csrc/kernels/%.hip,build/kernels/%.o,$(KSRC)) $(patsubst csrc/kernels/%.cpp,build/kernels/%.o,$(KCPP))
 RSRC := $(wildcard csrc/runtime/*.cpp)
 ROBJ := $(patsubst csrc/runtime/%.cpp,build/runtime/%.o,$(RSRC))
 
 all: $(PKG)/_kernels.so $(if $(RSRC),$(PKG)/_runtime.so,)
 
-build/kernels/%.o: csrc/kernels/%.hip csrc/kernels/common.h
+build/kernels/%.o: csrc/kernels/%.hip $(wildcard csrc/kernels/*.h)
 	@mkdir -p build/kernels
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
+build/kernels/%.o: csrc/kernels/%.cpp $(wildcard csrc/kernels/*.h)
+	@mkdir -p build/kernels
+	$(HIPCC) -O3 -std=c++17 -fPIC -Wall -Wno-unused-result -c $< -o $@
+
 $(PKG)/_kernels.so: $(KOBJ)
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(KOBJ)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(KOBJ) -L/opt/rocm/lib -lhipblaslt -Wl,-rpath,/opt/rocm/lib
 
 build/runtime/%.o: csrc/runtime/%.cpp $(wildcard csrc/runtime/*.h)
 	@mkdir -p build/runtime

@@ -418,7 +418,19 @@ __global__ __launch_bounds__(NTH, 2) void attn_bwd_dq_kernel(AttnArgs a) {
     }
     const long long si = ((long long)b * a.H + h) * a.S + (ok ? q : 0);
     lse2[qt] = a.LSE[si] * LOG2E;
-    dlt[qt] = a.delta[si];
+    // delta = rowsum(dO * O), fused here (the dK/dV kernel runs after this one and reads it back): this lane holds
+    // d = ds*32 + 8g + [0, 8) of query q; the 4 lanes g = 0..3 of the query are i, i+16, i+32, i+48
+    float part = 0.f;
+#pragma unroll
+    for (int ds = 0; ds < G::DS; ++ds) {
+      const bf16x8_t of = load_frag_g(a.O + base + (long long)q * a.ld + ds * 32 + 8 * g, ok);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) part += (float)of[j] * (float)df[qt][ds][j];
+    }
+    part += __shfl_xor(part, 16, 64);
+    part += __shfl_xor(part, 32, 64);
+    dlt[qt] = part;
+    if (ok && g == 0) a.delta[si] = part;
   }
   f32x4_t acc[G::DT][2];
 #pragma unroll
@@ -1163,15 +1175,14 @@ int launch_fwd(const AttnArgs& a, hipStream_t st) {
 
 template <int D>
 int launch_bwd(const AttnArgs& a, hipStream_t st) {
-  const long long rows = (long long)a.B * a.S * a.H;
-  hipLaunchKernelGGL(attn_delta_kernel<D>, dim3((unsigned)((rows + 3) / 4)), dim3(NTH), 0, st, a);
+  // dQ first: it also produces delta = rowsum(dO * O), which the dK/dV kernel reads
+  hipLaunchKernelGGL(attn_bwd_dq_kernel<D>, dim3((a.S + 127) / 128 * a.B * a.H), dim3(NTH), 4 * 64 * Geo<D>::ROWB, st, a);
   if (D == 128 && attn_bwd_impl() == 2)
     hipLaunchKernelGGL(attn_bwd_dkv32_kernel, dim3((a.S + 127) / 128 * a.B * a.H), dim3(NTH), 2 * (2 * 64 * 256 + 512),
                        st, a);
   else
     hipLaunchKernelGGL(attn_bwd_dkv_kernel<D>, dim3((a.S + 63) / 64 * a.B * a.H), dim3(NTH),
                        2 * (2 * 64 * Geo<D>::ROWB + 512), st, a);
-  hipLaunchKernelGGL(attn_bwd_dq_kernel<D>, dim3((a.S + 127) / 128 * a.B * a.H), dim3(NTH), 4 * 64 * Geo<D>::ROWB, st, a);
   return (int)hipGetLastError();
 }
 

@@ -1,0 +1,175 @@
+// Plain GEMMs (no activation / activation-backward epilogue, no triangular skipping) through hipBLASLt.
+//
+// Division of labour on MI355X: the GEMMs that carry fused epilogues (activation with pre-activation side output,
+// activation-backward, triangular token mixer) stay on the hand-written MFMA kernels in gemm.hip; the plain
+// products -- data gradients, weight gradients (bf16 x bf16 -> fp32 accumulated into the flat gradient buffer),
+// residual-add projections, logits -- are library GEMMs and go to hipBLASLt, whose gfx950 kernels sustain
+// 1.45-1.6 PFLOP/s on the model's shapes (tools/bench_gemm_k.py). hipBLASLt also reads every operand layout at
+// full rate, so the weight gradient needs no token-contiguous transposes and the forward needs no cached
+// transposed weight copies.
+//
+// Row-major C[M][N] = A·B is issued as the column-major product Cᵀ[N][M] = Bᵀ·Aᵀ:
+//   hipBLASLt "A" (N x K) = our B:  B_T = 0 ([N][K] row-major) -> op T, B_T = 1 ([K][N]) -> op N, ld = ldb
+//   hipBLASLt "B" (K x M) = our A:  A_T = 0 ([M][K] row-major) -> op N, A_T = 1 ([K][M]) -> op T, ld = lda
+//   hipBLASLt "C"/"D" (N x M, ld = ldc) = our C (R, when given, is hipBLASLt's C with beta = 1 and D = our C).
+// Descriptors and the heuristic's algorithm are cached per call signature; one workspace per process.
+#include <hip/hip_runtime.h>
+#include <hipblaslt/hipblaslt.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "gemm_desc.h"
+
+#include <mutex>
+#include <unordered_map>
+
+#define OBST_API extern "C" __attribute__((visibility("default")))
+
+namespace {
+
+struct Key {
+  int M, N, K, a_t, b_t, out_f32, has_r, has_beta, batch;
+  long long lda, ldb, ldc, sa, sb, sc;
+  bool operator==(const Key& o) const { return memcmp(this, &o, sizeof(Key)) == 0; }
+};
+
+struct KeyHash {
+  size_t operator()(const Key& k) const {
+    const unsigned char* p = reinterpret_cast<const unsigned char*>(&k);
+    size_t h = 1469598103934665603ull;
+    for (size_t i = 0; i < sizeof(Key); ++i) h = (h ^ p[i]) * 1099511628211ull;
+    return h;
+  }
+};
+
+struct Plan {
+  hipblasLtMatmulDesc_t op = nullptr;
+  hipblasLtMatrixLayout_t la = nullptr, lb = nullptr, lc = nullptr, ld = nullptr;
+  hipblasLtMatmulAlgo_t algo;
+  bool ok = false;
+};
+
+constexpr size_t WS_BYTES = 64ull << 20;
+
+struct State {
+  hipblasLtHandle_t handle = nullptr;
+  void* ws = nullptr;
+  int device = -1;
+  std::unordered_map<Key, Plan, KeyHash> plans;
+  std::mutex mu;
+};
+
+State& state() {
+  static State s;
+  return s;
+}
+
+int g_enabled = -1;
+
+int enabled() {
+  if (g_enabled < 0) {
+    const char* e = getenv("OBST_GEMM_LT");
+    g_enabled = e ? atoi(e) : 1;
+  }
+  return g_enabled;
+}
+
+hipblasLtMatrixLayout_t layout(hipDataType t, uint64_t rows, uint64_t cols, int64_t ld, int batch, long long stride) {
+  hipblasLtMatrixLayout_t l = nullptr;
+  if (hipblasLtMatrixLayoutCreate(&l, t, rows, cols, ld) != HIPBLAS_STATUS_SUCCESS) return nullptr;
+  if (batch > 1) {
+    int32_t bc = batch;
+    int64_t st = stride;
+    hipblasLtMatrixLayoutSetAttribute(l, HIPBLASLT_MATRIX_LAYOUT_BATCH_COUNT, &bc, sizeof(bc));
+    hipblasLtMatrixLayoutSetAttribute(l, HIPBLASLT_MATRIX_LAYOUT_STRIDED_BATCH_OFFSET, &st, sizeof(st));
+  }
+  return l;
+}
+
+Plan make_plan(State& S, const Key& k) {
+  Plan p;
+  if (hipblasLtMatmulDescCreate(&p.op, HIPBLAS_COMPUTE_32F, HIP_R_32F) != HIPBLAS_STATUS_SUCCESS) return p;
+  hipblasOperation_t ta = k.b_t == 0 ? HIPBLAS_OP_T : HIPBLAS_OP_N;
+  hipblasOperation_t tb = k.a_t == 0 ? HIPBLAS_OP_N : HIPBLAS_OP_T;
+  hipblasLtMatmulDescSetAttribute(p.op, HIPBLASLT_MATMUL_DESC_TRANSA, &ta, sizeof(ta));
+  hipblasLtMatmulDescSetAttribute(p.op, HIPBLASLT_MATMUL_DESC_TRANSB, &tb, sizeof(tb));
+  const hipDataType out = k.out_f32 ? HIP_R_32F : HIP_R_16BF;
+  // stored (column-major) shapes: op N -> rows x cols as used, op T -> transposed storage
+  p.la = ta == HIPBLAS_OP_N ? layout(HIP_R_16BF, k.N, k.K, k.ldb, k.batch, k.sb)
+                            : layout(HIP_R_16BF, k.K, k.N, k.ldb, k.batch, k.sb);
+  p.lb = tb == HIPBLAS_OP_N ? layout(HIP_R_16BF, k.K, k.M, k.lda, k.batch, k.sa)
+                            : layout(HIP_R_16BF, k.M, k.K, k.lda, k.batch, k.sa);
+  p.lc = layout(out, k.N, k.M, k.ldc, k.batch, k.sc);
+  p.ld = layout(out, k.N, k.M, k.ldc, k.batch, k.sc);
+  if (!p.la || !p.lb || !p.lc || !p.ld) return p;
+  hipblasLtMatmulPreference_t pref = nullptr;
+  if (hipblasLtMatmulPreferenceCreate(&pref) != HIPBLAS_STATUS_SUCCESS) return p;
+  uint64_t wsb = WS_BYTES;
+  hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsb, sizeof(wsb));
+  hipblasLtMatmulHeuristicResult_t res[1];
+  int n = 0;
+  const hipblasStatus_t st =
+      hipblasLtMatmulAlgoGetHeuristic(S.handle, p.op, p.la, p.lb, p.lc, p.ld, pref, 1, res, &n);
+  hipblasLtMatmulPreferenceDestroy(pref);
+  if (st != HIPBLAS_STATUS_SUCCESS || n < 1 || res[0].state != HIPBLAS_STATUS_SUCCESS ||
+      res[0].workspaceSize > WS_BYTES)
+    return p;
+  p.algo = res[0].algo;
+  p.ok = true;
+  return p;
+}
+
+}  // namespace
+
+
+// 0: done; 1: not eligible (caller runs its own kernel); < 0: hipBLASLt error
+int obst_blaslt_gemm(const ObstGemmDesc* d, hipStream_t stream) {
+  if (!enabled() || d->act != 0 || d->mode != 0 || d->tri != 0 || d->Zout || d->Zin) return 1;
+  if (d->R && d->out_f32) return 1;                 // residual + fp32 accumulate: not a single C input
+  int batch = d->batch1 * d->batch2;
+  long long sa = 0, sb = 0, sc = 0;
+  if (batch > 1) {
+    if (d->batch2 == 1) { sa = d->a_s1; sb = d->b_s1; sc = d->c_s1; }
+    else if (d->batch1 == 1) { sa = d->a_s2; sb = d->b_s2; sc = d->c_s2; }
+    else if (d->a_s1 == d->batch2 * d->a_s2 && d->b_s1 == d->batch2 * d->b_s2 && d->c_s1 == d->batch2 * d->c_s2) {
+      sa = d->a_s2; sb = d->b_s2; sc = d->c_s2;
+    } else {
+      return 1;
+    }
+  }
+  State& S = state();
+  std::lock_guard<std::mutex> g(S.mu);
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return -101;
+  if (!S.handle || S.device != dev) {
+    if (S.handle) return 1;                         // one device per process in this framework
+    if (hipblasLtCreate(&S.handle) != HIPBLAS_STATUS_SUCCESS) return -102;
+    if (hipMalloc(&S.ws, WS_BYTES) != hipSuccess) return -103;
+    S.device = dev;
+  }
+  Key k;
+  memset(&k, 0, sizeof(k));
+  k.M = d->M; k.N = d->N; k.K = d->K; k.a_t = d->a_t; k.b_t = d->b_t; k.out_f32 = d->out_f32;
+  k.has_r = d->R != nullptr; k.has_beta = d->out_f32 && d->beta != 0.f; k.batch = batch;
+  k.lda = d->lda; k.ldb = d->ldb; k.ldc = d->ldc; k.sa = sa; k.sb = sb; k.sc = sc;
+  auto it = S.plans.find(k);
+  if (it == S.plans.end()) it = S.plans.emplace(k, make_plan(S, k)).first;
+  const Plan& p = it->second;
+  if (!p.ok) return 1;
+  const float alpha = d->alpha;
+  const float beta = d->R ? 1.f : (d->out_f32 ? d->beta : 0.f);
+  const void* cin = d->R ? d->R : d->C;
+  const hipblasStatus_t st = hipblasLtMatmul(S.handle, p.op, &alpha, d->B, p.la, d->A, p.lb, &beta, cin, p.lc, d->C,
+                                             p.ld, &p.algo, S.ws, WS_BYTES, stream);
+  return st == HIPBLAS_STATUS_SUCCESS ? 0 : -(int)st - 200;
+}
+
+OBST_API int obst_blaslt_enabled() { return enabled(); }
+
+// runtime switch (tests run the plain GEMM cases on both paths); returns the previous setting
+OBST_API int obst_blaslt_set(int on) {
+  const int old = enabled();
+  g_enabled = on;
+  return old;
+}

@@ -16,6 +16,7 @@
 // consecutive output columns (8-byte bf16 / 16-byte fp32 stores). Block ids are remapped XCD-aware (T1) and
 // grouped 8 tiles along M so blocks that share an XCD share A panels in its L2.
 #include "common.h"
+#include "gemm_desc.h"
 #include <stdlib.h>
 
 namespace {
@@ -675,15 +676,6 @@ static int getenv_big() {
   return v;
 }
 
-struct ObstGemmDesc {
-  const void* A; const void* B; void* C; const void* R; void* Zout; const void* Zin;
-  long long lda, ldb, ldc;
-  long long a_s1, a_s2, b_s1, b_s2, c_s1, c_s2;
-  int M, N, K, batch1, batch2;
-  int a_t, b_t, out_f32, act, mode;
-  float alpha, beta;
-  int tri;
-};
 
 // Returns 0 on success, <0 on a host-side shape/alignment violation, >0 for a HIP error.
 OBST_API int obst_gemm(const ObstGemmDesc* d, hipStream_t stream) {
@@ -694,6 +686,10 @@ OBST_API int obst_gemm(const ObstGemmDesc* d, hipStream_t stream) {
   if (d->lda % 8 || d->ldb % 8 || d->ldc % 8) return -4;
   if (((uintptr_t)d->A | (uintptr_t)d->B) & 15) return -5;
   if (((uintptr_t)d->C) & 15) return -6;
+  {
+    const int r = obst_blaslt_gemm(d, stream);
+    if (r <= 0) return r;
+  }
   GemmArgs a;
   a.A = (const bf16_t*)d->A; a.B = (const bf16_t*)d->B; a.C = d->C; a.R = d->R;
   a.Zout = (bf16_t*)d->Zout; a.Zin = (const bf16_t*)d->Zin;

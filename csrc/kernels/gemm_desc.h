@@ -1,0 +1,15 @@
+// Host-side GEMM descriptor shared by the MFMA kernels (gemm.hip) and the hipBLASLt path (blaslt.cpp); the ctypes
+// mirror is GemmDesc in homebrewnlp_mtf_amd/ops/_lib.py.
+#pragma once
+struct ObstGemmDesc {
+  const void* A; const void* B; void* C; const void* R; void* Zout; const void* Zin;
+  long long lda, ldb, ldc;
+  long long a_s1, a_s2, b_s1, b_s2, c_s1, c_s2;
+  int M, N, K, batch1, batch2;
+  int a_t, b_t, out_f32, act, mode;
+  float alpha, beta;
+  int tri;
+};
+
+// plain GEMMs through hipBLASLt: 0 done, 1 not eligible (run the MFMA kernels), < 0 hipBLASLt error
+int obst_blaslt_gemm(const ObstGemmDesc* d, hipStream_t stream);

@@ -88,15 +88,19 @@ def linear_plan(xdims: tuple, wdims: tuple, odims: tuple) -> LinearPlan:
     return LinearPlan(list(xdims), list(wdims), list(odims))
 
 
-# K-contiguous operands only on the GPU (ds_read_b128 fragments; the transposed-read path is 25-35 % slower):
-# the forward GEMM reads a cached [N][K] copy of each weight, the weight gradient reads token-contiguous
-# transposes of x and dy (`OBST_TRANSPOSED_OPERANDS=0` turns both off for A/B measurements).
+# Operand layouts on the GPU. Plain GEMMs run on hipBLASLt (raw.lt_enabled()), which reads every layout at full
+# rate: no copies. The fused-epilogue GEMMs run on the MFMA kernels, whose K-contiguous (ds_read_b128) path is
+# 25-35 % faster than the transposed-read path, so for those the forward reads a cached [N][K] copy of the weight;
+# with hipBLASLt off, the weight gradient also reads token-contiguous transposes of x and dy
+# (`OBST_TRANSPOSED_OPERANDS=0` turns the copies off for A/B measurements).
 _KCONTIG = __import__("os").environ.get("OBST_TRANSPOSED_OPERANDS", "1") != "0"
 
 
-def _wT(w, plan: LinearPlan):
+def _wT(w, plan: LinearPlan, fused: bool = False):
     store = getattr(w, "store", None)
     if not _KCONTIG or store is None or not raw.on_gpu(w) or w.dtype != torch.bfloat16:
+        return None
+    if not fused and raw.lt_enabled():
         return None
     if plan.K % 8 or plan.N % 8:
         return None
@@ -105,7 +109,7 @@ def _wT(w, plan: LinearPlan):
 
 def _fwd_gemm(x2, w, y2, plan: LinearPlan, act=None, R=None, Zout=None):
     M, H, K, N = plan.M, plan.H, plan.K, plan.N
-    wt = _wT(w, plan)
+    wt = _wT(w, plan, fused=act is not None or Zout is not None)
     bop = raw.Operand(wt, 0, K, K * N) if wt is not None else raw.Operand(w, 1, N, K * N)
     raw.gemm(raw.Operand(x2, 0, H * K, K), bop, raw.Operand(y2, 0, H * N, N),
              M, N, K, batch=(H, 1), act=act, R=R, Zout=Zout)
@@ -114,6 +118,8 @@ def _fwd_gemm(x2, w, y2, plan: LinearPlan, act=None, R=None, Zout=None):
 def tokens_transposed(x2, rows: int, cols: int) -> typing.Optional[torch.Tensor]:
     """[rows][cols] bf16 -> [cols][rows] (None where the plain transposed-read GEMM is used instead)"""
     if not _KCONTIG or not raw.on_gpu(x2) or x2.dtype != torch.bfloat16 or rows % 8 or cols % 8:
+        return None
+    if raw.lt_enabled():
         return None
     out = torch.empty(cols * rows, dtype=x2.dtype, device=x2.device)
     raw.transpose(x2, out, rows, cols, cols, rows)

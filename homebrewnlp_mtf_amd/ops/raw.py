@@ -30,6 +30,25 @@ def on_gpu(t: torch.Tensor) -> bool:
     return t.device.type == "cuda"
 
 
+_LT = None
+
+
+def lt_enabled() -> bool:
+    """plain GEMMs run on hipBLASLt (csrc/kernels/blaslt.cpp; OBST_GEMM_LT=0 keeps every GEMM on the MFMA kernels)"""
+    global _LT
+    if _LT is None:
+        _LT = bool(L.lib().obst_blaslt_enabled())
+    return _LT
+
+
+def lt_set(on: bool) -> bool:
+    """switch the hipBLASLt path at run time (tests); returns the previous setting"""
+    global _LT
+    old = bool(L.lib().obst_blaslt_set(int(on)))
+    _LT = bool(on)
+    return old
+
+
 def _room(t: torch.Tensor) -> int:
     """elements addressable from t.data_ptr() to the end of its storage"""
     return t.untyped_storage().nbytes() // t.element_size() - t.storage_offset()

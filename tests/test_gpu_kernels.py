@@ -24,10 +24,18 @@ def _close(gpu, ref, atol, rtol, what=""):
     assert bad == 0, f"{what}: {bad}/{r.numel()} out of tolerance, max err {err.max().item():.4g}"
 
 
+@pytest.fixture(params=[0, 1], ids=["mfma", "hipblaslt"])
+def lt(request, cuda):
+    """plain GEMMs on the MFMA kernels (0) or on hipBLASLt (1)"""
+    old = raw.lt_set(bool(request.param))
+    yield request.param
+    raw.lt_set(old)
+
+
 # ----------------------------------------------------------------------------------------------------------------
 @pytest.mark.parametrize("a_t,b_t", [(0, 0), (0, 1), (1, 0), (1, 1)])
 @pytest.mark.parametrize("M,N,K", [(128, 128, 64), (200, 136, 72), (512, 384, 256), (64, 8, 8)])
-def test_gemm_layouts(cuda, a_t, b_t, M, N, K):
+def test_gemm_layouts(cuda, lt, a_t, b_t, M, N, K):
     torch.manual_seed(M + N + K + 10 * a_t + b_t)
     A = (torch.randn(M * K) * 0.5).to(BF)
     B = (torch.randn(N * K) * 0.5).to(BF)
@@ -75,6 +83,36 @@ def test_gemm_batched_epilogues(cuda):
     torch.cuda.synchronize()
     for name, g, c in zip("CZDG", outs[str(cuda)], outs["cpu"]):
         _close(g, c, 5e-2, 3e-2, f"batched epilogue {name}")
+
+
+@pytest.mark.parametrize("case", ["residual", "f32_accumulate", "shared_A_batch", "two_level_batch"])
+def test_gemm_plain_paths(cuda, lt, case):
+    """the plain-GEMM shapes the model issues (residual input, fp32 accumulate, q/k/v batch over one input)"""
+    torch.manual_seed(5)
+    M, K, N, H = 256, 192, 136, 3
+    outs = {}
+    A = (torch.randn(M * H * K) * 0.5).to(BF)
+    B = (torch.randn(H * K * N) * 0.5).to(BF)
+    R = (torch.randn(M * H * N) * 0.5).to(BF)
+    for dev in ("cpu", cuda):
+        a, b, r = A.to(dev), B.to(dev), R.to(dev)
+        if case == "residual":
+            C = torch.zeros(M * N, dtype=BF, device=dev)
+            raw.gemm(raw.Operand(a, 0, K), raw.Operand(b, 1, N), raw.Operand(C, 0, N), M, N, K, R=r)
+        elif case == "f32_accumulate":   # weight gradient: C[K][N] += A[M][K]^T B[M][N]
+            C = torch.ones(K * N, dtype=torch.float32, device=dev)
+            raw.gemm(raw.Operand(a, 1, K), raw.Operand(r, 1, N), raw.Operand(C, 0, N), K, N, M, beta=1.0)
+        elif case == "shared_A_batch":   # out[j] = A · B_j  (A batch stride 0)
+            C = torch.zeros(H * M * N, dtype=BF, device=dev)
+            raw.gemm(raw.Operand(a, 0, K, 0), raw.Operand(b, 1, N, K * N), raw.Operand(C, 0, N, M * N), M, N, K,
+                     batch=(H, 1))
+        else:                            # batch = (2, H) with compatible strides
+            C = torch.zeros(2 * H * 64 * N, dtype=BF, device=dev)
+            raw.gemm(raw.Operand(a, 0, K, H * 64 * K, 64 * K), raw.Operand(b, 1, N, 0, K * N),
+                     raw.Operand(C, 0, N, H * 64 * N, 64 * N), 64, N, K, batch=(2, H))
+        outs[str(dev)] = C
+    torch.cuda.synchronize()
+    _close(outs[str(cuda)], outs["cpu"], 5e-2, 3e-2, f"plain gemm {case}")
 
 
 def test_gemm_oob_rejected(cuda):
