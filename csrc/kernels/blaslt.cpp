@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 #include <hipblaslt/hipblaslt.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -29,7 +30,7 @@
 namespace {
 
 struct Key {
-  int M, N, K, a_t, b_t, out_f32, has_r, has_beta, batch;
+  int M, N, K, a_t, b_t, out_f32, has_r, has_beta, batch, epi;   // epi: 0 none, 1 GELU_AUX, 2 DGELU
   long long lda, ldb, ldc, sa, sb, sc;
   bool operator==(const Key& o) const { return memcmp(this, &o, sizeof(Key)) == 0; }
 };
@@ -66,6 +67,16 @@ State& state() {
 }
 
 int g_enabled = -1;
+long long g_calls = 0, g_declined = 0;   // dispatches taken / eligible calls hipBLASLt had no algorithm for
+
+bool debug() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("OBST_LT_DEBUG");
+    v = e ? atoi(e) : 0;
+  }
+  return v > 0;
+}
 
 int enabled() {
   if (g_enabled < 0) {
@@ -95,6 +106,16 @@ Plan make_plan(State& S, const Key& k) {
   hipblasLtMatmulDescSetAttribute(p.op, HIPBLASLT_MATMUL_DESC_TRANSA, &ta, sizeof(ta));
   hipblasLtMatmulDescSetAttribute(p.op, HIPBLASLT_MATMUL_DESC_TRANSB, &tb, sizeof(tb));
   const hipDataType out = k.out_f32 ? HIP_R_32F : HIP_R_16BF;
+  if (k.epi) {
+    const uint32_t e = k.epi == 1 ? HIPBLASLT_EPILOGUE_GELU_AUX : HIPBLASLT_EPILOGUE_DGELU;
+    const int64_t ald = k.ldc, ast = k.sc;
+    const int32_t adt = HIP_R_16BF;
+    hipblasLtMatmulDescSetAttribute(p.op, HIPBLASLT_MATMUL_DESC_EPILOGUE, &e, sizeof(e));
+    hipblasLtMatmulDescSetAttribute(p.op, HIPBLASLT_MATMUL_DESC_EPILOGUE_AUX_LD, &ald, sizeof(ald));
+    hipblasLtMatmulDescSetAttribute(p.op, HIPBLASLT_MATMUL_DESC_EPILOGUE_AUX_DATA_TYPE, &adt, sizeof(adt));
+    if (k.batch > 1)
+      hipblasLtMatmulDescSetAttribute(p.op, HIPBLASLT_MATMUL_DESC_EPILOGUE_AUX_BATCH_STRIDE, &ast, sizeof(ast));
+  }
   // stored (column-major) shapes: op N -> rows x cols as used, op T -> transposed storage
   p.la = ta == HIPBLAS_OP_N ? layout(HIP_R_16BF, k.N, k.K, k.ldb, k.batch, k.sb)
                             : layout(HIP_R_16BF, k.K, k.N, k.ldb, k.batch, k.sb);
@@ -113,8 +134,12 @@ Plan make_plan(State& S, const Key& k) {
       hipblasLtMatmulAlgoGetHeuristic(S.handle, p.op, p.la, p.lb, p.lc, p.ld, pref, 1, res, &n);
   hipblasLtMatmulPreferenceDestroy(pref);
   if (st != HIPBLAS_STATUS_SUCCESS || n < 1 || res[0].state != HIPBLAS_STATUS_SUCCESS ||
-      res[0].workspaceSize > WS_BYTES)
+      res[0].workspaceSize > WS_BYTES) {
+    if (debug())
+      fprintf(stderr, "[blaslt] no algorithm (status %d, n %d): M %d N %d K %d a_t %d b_t %d f32 %d R %d epi %d batch %d\n",
+              (int)st, n, k.M, k.N, k.K, k.a_t, k.b_t, k.out_f32, k.has_r, k.epi, k.batch);
     return p;
+  }
   p.algo = res[0].algo;
   p.ok = true;
   return p;
@@ -123,9 +148,23 @@ Plan make_plan(State& S, const Key& k) {
 }  // namespace
 
 
-// 0: done; 1: not eligible (caller runs its own kernel); < 0: hipBLASLt error
+// 0: done; 1: not eligible (caller runs its own kernel); < 0: hipBLASLt error.
+// Plain GEMMs only by default. With OBST_GEMM_LT=2 also gelu with the pre-activation side output (GELU_AUX:
+// Zout = acc, C = gelu(acc)) and gelu-backward (DGELU: C = (acc + R) * gelu'(Zin)) when the installed hipBLASLt
+// has kernels for them (hipBLASLt's GELU is the tanh form, the reference's: src/model/activation.py). Otherwise the
+// Python layer (ops/raw.py) splits an activation GEMM into a plain hipBLASLt GEMM plus the elementwise kernel.
 int obst_blaslt_gemm(const ObstGemmDesc* d, hipStream_t stream) {
-  if (!enabled() || d->act != 0 || d->mode != 0 || d->tri != 0 || d->Zout || d->Zin) return 1;
+  if (!enabled() || d->tri != 0) return 1;
+  int epi = 0;
+  if (d->act == 0) {
+    if (d->mode != 0 || d->Zout || d->Zin) return 1;
+  } else if (enabled() >= 2 && d->act == 2 && d->mode == 0 && d->Zout && !d->R && !d->out_f32) {
+    epi = 1;   // OBST_GEMM_LT=2: try hipBLASLt's own epilogues (gfx950 builds ship few GELU_AUX/DGELU kernels)
+  } else if (enabled() >= 2 && d->act == 2 && d->mode == 1 && d->Zin && !d->out_f32) {
+    epi = 2;
+  } else {
+    return 1;
+  }
   if (d->R && d->out_f32) return 1;                 // residual + fp32 accumulate: not a single C input
   int batch = d->batch1 * d->batch2;
   long long sa = 0, sb = 0, sc = 0;
@@ -152,11 +191,19 @@ int obst_blaslt_gemm(const ObstGemmDesc* d, hipStream_t stream) {
   memset(&k, 0, sizeof(k));
   k.M = d->M; k.N = d->N; k.K = d->K; k.a_t = d->a_t; k.b_t = d->b_t; k.out_f32 = d->out_f32;
   k.has_r = d->R != nullptr; k.has_beta = d->out_f32 && d->beta != 0.f; k.batch = batch;
-  k.lda = d->lda; k.ldb = d->ldb; k.ldc = d->ldc; k.sa = sa; k.sb = sb; k.sc = sc;
+  k.lda = d->lda; k.ldb = d->ldb; k.ldc = d->ldc; k.sa = sa; k.sb = sb; k.sc = sc; k.epi = epi;
   auto it = S.plans.find(k);
   if (it == S.plans.end()) it = S.plans.emplace(k, make_plan(S, k)).first;
   const Plan& p = it->second;
-  if (!p.ok) return 1;
+  if (!p.ok) {
+    ++g_declined;
+    return 1;
+  }
+  ++g_calls;
+  if (epi) {
+    const void* aux = epi == 1 ? (const void*)d->Zout : d->Zin;
+    hipblasLtMatmulDescSetAttribute(p.op, HIPBLASLT_MATMUL_DESC_EPILOGUE_AUX_POINTER, &aux, sizeof(aux));
+  }
   const float alpha = d->alpha;
   const float beta = d->R ? 1.f : (d->out_f32 ? d->beta : 0.f);
   const void* cin = d->R ? d->R : d->C;
@@ -166,6 +213,13 @@ int obst_blaslt_gemm(const ObstGemmDesc* d, hipStream_t stream) {
 }
 
 OBST_API int obst_blaslt_enabled() { return enabled(); }
+
+// counters for tests / diagnostics: out[0] = hipBLASLt dispatches, out[1] = eligible calls it declined
+OBST_API int obst_blaslt_stats(long long* out) {
+  out[0] = g_calls;
+  out[1] = g_declined;
+  return 0;
+}
 
 // runtime switch (tests run the plain GEMM cases on both paths); returns the previous setting
 OBST_API int obst_blaslt_set(int on) {

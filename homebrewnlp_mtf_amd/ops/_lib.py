@@ -96,6 +96,7 @@ _SIGS = {
     "obst_opt_apply": [ctypes.POINTER(OptDesc), c_p],
     "obst_blaslt_enabled": [],
     "obst_blaslt_set": [c_i],
+    "obst_blaslt_stats": [c_p],
 }
 
 

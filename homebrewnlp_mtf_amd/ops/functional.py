@@ -96,11 +96,11 @@ def linear_plan(xdims: tuple, wdims: tuple, odims: tuple) -> LinearPlan:
 _KCONTIG = __import__("os").environ.get("OBST_TRANSPOSED_OPERANDS", "1") != "0"
 
 
-def _wT(w, plan: LinearPlan, fused: bool = False):
+def _wT(w, plan: LinearPlan, act=None, has_r: bool = False):
     store = getattr(w, "store", None)
     if not _KCONTIG or store is None or not raw.on_gpu(w) or w.dtype != torch.bfloat16:
         return None
-    if not fused and raw.lt_enabled():
+    if raw.lt_enabled() and (act is None or (act == "gelu" and not has_r)):   # runs on hipBLASLt (blaslt.cpp)
         return None
     if plan.K % 8 or plan.N % 8:
         return None
@@ -109,7 +109,7 @@ def _wT(w, plan: LinearPlan, fused: bool = False):
 
 def _fwd_gemm(x2, w, y2, plan: LinearPlan, act=None, R=None, Zout=None):
     M, H, K, N = plan.M, plan.H, plan.K, plan.N
-    wt = _wT(w, plan, fused=act is not None or Zout is not None)
+    wt = _wT(w, plan, act, R is not None)
     bop = raw.Operand(wt, 0, K, K * N) if wt is not None else raw.Operand(w, 1, N, K * N)
     raw.gemm(raw.Operand(x2, 0, H * K, K), bop, raw.Operand(y2, 0, H * N, N),
              M, N, K, batch=(H, 1), act=act, R=R, Zout=Zout)

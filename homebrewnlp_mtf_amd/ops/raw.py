@@ -12,6 +12,7 @@ tensor's storage (a kernel fault can reset every GPU of the node).
 from __future__ import annotations
 
 import math
+import ctypes
 import typing
 
 import torch
@@ -33,19 +34,27 @@ def on_gpu(t: torch.Tensor) -> bool:
 _LT = None
 
 
-def lt_enabled() -> bool:
-    """plain GEMMs run on hipBLASLt (csrc/kernels/blaslt.cpp; OBST_GEMM_LT=0 keeps every GEMM on the MFMA kernels)"""
+def lt_enabled() -> int:
+    """plain GEMMs run on hipBLASLt (csrc/kernels/blaslt.cpp; OBST_GEMM_LT=0 keeps every GEMM on the MFMA kernels,
+    2 tries hipBLASLt's own GELU epilogues instead of the plain GEMM + elementwise split)"""
     global _LT
     if _LT is None:
-        _LT = bool(L.lib().obst_blaslt_enabled())
+        _LT = int(L.lib().obst_blaslt_enabled())
     return _LT
+
+
+def lt_stats() -> typing.Tuple[int, int]:
+    """(GEMMs dispatched to hipBLASLt, eligible GEMMs it declined -- those ran on the MFMA kernels)"""
+    out = (ctypes.c_longlong * 2)()
+    L.lib().obst_blaslt_stats(ctypes.addressof(out))
+    return int(out[0]), int(out[1])
 
 
 def lt_set(on: bool) -> bool:
     """switch the hipBLASLt path at run time (tests); returns the previous setting"""
     global _LT
-    old = bool(L.lib().obst_blaslt_set(int(on)))
-    _LT = bool(on)
+    old = int(L.lib().obst_blaslt_set(int(on)))
+    _LT = int(on)
     return old
 
 
@@ -140,6 +149,17 @@ def gemm(a: Operand, b: Operand, c: Operand, M: int, N: int, K: int, batch: typi
     if c.t.device.type == "meta":
         return c.t
     b1, b2 = batch
+    if (on_gpu(c.t) and act is not None and tri == 0 and lt_enabled() == 1 and c.t.dtype == torch.bfloat16
+            and b1 * b2 == 1 and c.ld == N and (M * N) % 8 == 0 and c.t.is_contiguous() and c.t.numel() == M * N):
+        # activation GEMM on hipBLASLt: plain product, then the elementwise kernel (pre-activation kept in Zout)
+        if not act_bwd:
+            z = Zout if Zout is not None else torch.empty(M * N, dtype=torch.bfloat16, device=c.t.device)
+            gemm(a, b, Operand(z, 0, N), M, N, K, alpha=alpha, R=R)
+            elementwise("act", z, c.t, act=act)
+        else:
+            gemm(a, b, c, M, N, K, alpha=alpha, R=R)
+            elementwise("act_bwd", Zin, c.t, z=c.t, act=act)    # in place: C = C * act'(Zin)
+        return c.t
     if on_gpu(c.t):
         out_f32 = c.t.dtype == torch.float32
         for nm, t in (("A", a.t), ("B", b.t)):

@@ -27,7 +27,7 @@ def _close(gpu, ref, atol, rtol, what=""):
 @pytest.fixture(params=[0, 1], ids=["mfma", "hipblaslt"])
 def lt(request, cuda):
     """plain GEMMs on the MFMA kernels (0) or on hipBLASLt (1)"""
-    old = raw.lt_set(bool(request.param))
+    old = raw.lt_set(request.param)
     yield request.param
     raw.lt_set(old)
 
@@ -61,13 +61,14 @@ def test_gemm_identity_asymmetric(cuda):
     assert torch.equal(Cg.view(n, n).cpu(), B)
 
 
-def test_gemm_batched_epilogues(cuda):
+def test_gemm_batched_epilogues(cuda, lt):
     torch.manual_seed(3)
     H, M, K, N = 3, 96, 64, 40
     A = (torch.randn(M, H, K) * 0.5).to(BF)            # [M][H][K] -> batch stride K, ld H*K
     B = (torch.randn(H, K, N) * 0.5).to(BF)            # [H][K][N]
     R = (torch.randn(M, H, N) * 0.5).to(BF)
     outs = {}
+    n0 = raw.lt_stats()
     for dev in ("cpu", cuda):
         C = torch.zeros(M, H, N, dtype=BF, device=dev)
         Z = torch.zeros(M, H, N, dtype=BF, device=dev)
@@ -79,10 +80,20 @@ def test_gemm_batched_epilogues(cuda):
         G = torch.ones(H, K, N, dtype=torch.float32, device=dev)   # fp32 accumulate (beta = 1)
         raw.gemm(raw.Operand(A.to(dev), 1, H * K, K), raw.Operand(R.to(dev), 1, H * N, N),
                  raw.Operand(G, 0, N, K * N), K, N, M, batch=(H, 1), beta=1.0)
-        outs[str(dev)] = (C, Z, D, G)
+        C2 = torch.zeros(M, H, N, dtype=BF, device=dev)   # activation + pre-activation output, no residual
+        Z2 = torch.zeros(M, H, N, dtype=BF, device=dev)
+        raw.gemm(raw.Operand(A.to(dev), 0, H * K, K), raw.Operand(B.to(dev), 1, N, K * N),
+                 raw.Operand(C2, 0, H * N, N), M, N, K, batch=(H, 1), act="gelu", Zout=Z2)
+        D2 = torch.zeros(M, H, N, dtype=BF, device=dev)   # activation backward without residual
+        raw.gemm(raw.Operand(A.to(dev), 0, H * K, K), raw.Operand(B.to(dev), 1, N, K * N),
+                 raw.Operand(D2, 0, H * N, N), M, N, K, batch=(H, 1), act="gelu", act_bwd=True, Zin=Z)
+        outs[str(dev)] = (C, Z, D, G, C2, Z2, D2)
     torch.cuda.synchronize()
-    for name, g, c in zip("CZDG", outs[str(cuda)], outs["cpu"]):
+    for name, g, c in zip(["C", "Z", "D", "G", "C2", "Z2", "D2"], outs[str(cuda)], outs["cpu"]):
         _close(g, c, 5e-2, 3e-2, f"batched epilogue {name}")
+    n1 = raw.lt_stats()
+    if lt:   # G on hipBLASLt (the batched activation GEMMs C, D, C2, D2 stay on the fused MFMA kernel)
+        assert n1[0] == n0[0] + 1 and n1[1] == n0[1], (n0, n1)
 
 
 @pytest.mark.parametrize("case", ["residual", "f32_accumulate", "shared_A_batch", "two_level_batch"])
@@ -91,6 +102,7 @@ def test_gemm_plain_paths(cuda, lt, case):
     torch.manual_seed(5)
     M, K, N, H = 256, 192, 136, 3
     outs = {}
+    n0 = raw.lt_stats()
     A = (torch.randn(M * H * K) * 0.5).to(BF)
     B = (torch.randn(H * K * N) * 0.5).to(BF)
     R = (torch.randn(M * H * N) * 0.5).to(BF)
@@ -113,6 +125,36 @@ def test_gemm_plain_paths(cuda, lt, case):
         outs[str(dev)] = C
     torch.cuda.synchronize()
     _close(outs[str(cuda)], outs["cpu"], 5e-2, 3e-2, f"plain gemm {case}")
+    n1 = raw.lt_stats()
+    if lt and case != "two_level_batch":   # the path under test really ran on hipBLASLt
+        assert n1[0] == n0[0] + 1 and n1[1] == n0[1], (n0, n1)
+
+
+@pytest.mark.parametrize("act_bwd", [False, True])
+@pytest.mark.parametrize("with_r", [False, True])
+def test_gemm_activation_split(cuda, lt, act_bwd, with_r):
+    """activation GEMMs as the model issues them (contiguous, unbatched): hipBLASLt + elementwise or fused MFMA"""
+    torch.manual_seed(9)
+    M, K, N = 384, 256, 520
+    A = (torch.randn(M * K) * 0.5).to(BF)
+    B = (torch.randn(N * K) * 0.5).to(BF)
+    R = (torch.randn(M * N) * 0.5).to(BF)
+    Zi = (torch.randn(M * N) * 1.5).to(BF)
+    outs = {}
+    n0 = raw.lt_stats()
+    for dev in ("cpu", cuda):
+        C = torch.zeros(M * N, dtype=BF, device=dev)
+        Z = torch.zeros(M * N, dtype=BF, device=dev)
+        raw.gemm(raw.Operand(A.to(dev), 0, K), raw.Operand(B.to(dev), 0, K), raw.Operand(C, 0, N), M, N, K,
+                 act="gelu", act_bwd=act_bwd, R=R.to(dev) if with_r else None,
+                 Zout=None if act_bwd else Z, Zin=Zi.to(dev) if act_bwd else None)
+        outs[str(dev)] = (C, Z)
+    torch.cuda.synchronize()
+    for name, g, c in zip("CZ", outs[str(cuda)], outs["cpu"]):
+        _close(g, c, 5e-2, 3e-2, f"activation gemm {name} bwd={act_bwd} R={with_r}")
+    n1 = raw.lt_stats()
+    if lt:
+        assert n1[0] == n0[0] + 1, (n0, n1)
 
 
 def test_gemm_oob_rejected(cuda):

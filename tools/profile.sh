@@ -11,6 +11,7 @@ rc=$?
 cd $GRAFT_REPO_ROOT
 STATS=$(find gpurun_out/prof_$TAG -name "*kernel_stats.csv" | head -1)
 python3 tools/prof_summary.py "$STATS" ${PROF_STEPS:-1} > gpurun_out/prof_$TAG/summary.md
-cat gpurun_out/prof_$TAG/summary.md | head -40
+TRACE=$(find gpurun_out/prof_$TAG -name "*kernel_trace.csv" | head -1)
+python3 tools/prof_steps.py "$TRACE" > gpurun_out/prof_$TAG/steps.md && head -30 gpurun_out/prof_$TAG/steps.md
 find gpurun_out/prof_$TAG -name "*kernel_trace.csv" -delete
 exit $rc
