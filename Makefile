@@ -18,7 +18,7 @@ build/kernels/%.o: csrc/kernels/%.hip $(wildcard csrc/kernels/*.h)
 
 build/kernels/%.o: csrc/kernels/%.cpp $(wildcard csrc/kernels/*.h)
 	@mkdir -p build/kernels
-	$(HIPCC) -O3 -std=c++17 -fPIC -Wall -Wno-unused-result -c $< -o $@
+	$(HIPCC) -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-result -c $< -o $@
 
 $(PKG)/_kernels.so: $(KOBJ)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(KOBJ) -L/opt/rocm/lib -lhipblaslt -Wl,-rpath,/opt/rocm/lib

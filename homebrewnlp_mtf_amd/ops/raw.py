@@ -32,6 +32,7 @@ def on_gpu(t: torch.Tensor) -> bool:
 
 
 _LT = None
+_RSPLIT = __import__("os").environ.get("OBST_LT_RSPLIT", "0") == "1"   # A/B knob: measured 1 % slower
 
 
 def lt_enabled() -> int:
@@ -159,6 +160,14 @@ def gemm(a: Operand, b: Operand, c: Operand, M: int, N: int, K: int, batch: typi
         else:
             gemm(a, b, c, M, N, K, alpha=alpha, R=R)
             elementwise("act_bwd", Zin, c.t, z=c.t, act=act)    # in place: C = C * act'(Zin)
+        return c.t
+    if (on_gpu(c.t) and R is not None and act is None and tri == 0 and lt_enabled() == 1 and _RSPLIT
+            and c.t.dtype == torch.bfloat16 and b1 * b2 == 1 and c.ld == N and (M * N) % 8 == 0
+            and c.t.is_contiguous() and c.t.numel() == M * N and R.is_contiguous() and R.numel() == M * N):
+        # residual input: hipBLASLt's out-of-place beta*C path runs 2-3x slower than the plain product on some
+        # layouts (tools/bench_gemm_k.py), so the plain product plus the elementwise add is faster
+        gemm(a, b, c, M, N, K, alpha=alpha)
+        elementwise("add", c.t, c.t, z=R)
         return c.t
     if on_gpu(c.t):
         out_f32 = c.t.dtype == torch.float32
