@@ -345,6 +345,309 @@ __global__ __launch_bounds__(NTA) void opt_apply_kernel(ApplyArgs a) {
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------------------------
+// Row-tiled apply for every chain without Adafactor (the shipped SM3 chain among them). A tensor is viewed as
+// [rows][C] (C = trailing dim); a chunk is a tile of whole rows x a column range (<= RW_COLS). Each thread owns the
+// same columns in every row, so:
+//   * no per-element multi-index arithmetic: the leading-dim indices are derived once per row;
+//   * the SM3 trailing-dim max is a thread-private running max in LDS (no atomics), flushed with one global atomic
+//     per column per chunk; the leading-dim max is one wave reduction + one global atomic per wave per row.
+// (The generic opt_apply_kernel above derived a 4-D index per element and reduced through LDS atomics: ~620 VALU
+// instructions per 4 elements, measured with rocprofv3 --pmc.)
+constexpr int RW_NT = 256;
+constexpr int RW_COLS = 8192;
+
+struct RChunk { int t, row0, nrows, col0, ncols, vec; };
+
+// the segment's stage program on V consecutive elements of one row (gi: flat index; acc_last: the trailing-dim SM3
+// accumulators of those V columns; lead: min over the row's leading-dim accumulators). tm: running trailing-dim max
+// of these columns, rmax: running max of this lane's part of the row.
+template <int V>
+__device__ __forceinline__ void row_program(const ApplyArgs& a, const float* F, long long gi, const float* acc_last,
+                                            float lead, float (&g)[V], const float (&w)[V], float (&tm)[V],
+                                            float& rmax, float deb1, float deb2) {
+      for (int s = 0; s < a.nst; ++s) {
+    const Stage S = a.st[s];
+    switch (S.op) {
+      case OP_ADAPTIVE_CLIP: case OP_L2_CLIP: case OP_GLOBAL_L2_CLIP: case OP_SCALE:
+#pragma unroll
+        for (int j = 0; j < V; ++j) g[j] *= F[0];
+        break;
+      case OP_VALUE_CLIP:
+#pragma unroll
+        for (int j = 0; j < V; ++j) g[j] = fmaxf(fminf(g[j], S.a), -S.a);
+        break;
+      case OP_GRAD_CENTRAL:
+#pragma unroll
+        for (int j = 0; j < V; ++j) g[j] -= F[0];
+        break;
+      case OP_WEIGHT_CENTRAL:
+#pragma unroll
+        for (int j = 0; j < V; ++j) g[j] += F[1];
+        break;
+      case OP_SM3: {
+        float al[V];
+        if (V == 4) {
+          const float4 v = *reinterpret_cast<const float4*>(acc_last);
+          al[0] = v.x; al[1] = v.y; al[2] = v.z; al[3] = v.w;
+        } else {
+          al[0] = acc_last[0];
+        }
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+          const float nu = fminf(lead, al[j]) + g[j] * g[j];
+          tm[j] = fmaxf(tm[j], nu);
+          rmax = fmaxf(rmax, nu);
+          g[j] *= opt_rsqrt(nu);
+        }
+        break;
+      }
+      case OP_MOMENTUM: {
+        float m[V];
+        if (V == 4) {
+          const float4 mv = *reinterpret_cast<const float4*>(a.mom + gi);
+          m[0] = mv.x; m[1] = mv.y; m[2] = mv.z; m[3] = mv.w;
+        } else {
+          m[0] = a.mom[gi];
+        }
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+          m[j] = S.a * m[j] + g[j] * S.b;
+          g[j] = S.c != 0.f ? g[j] + S.a * m[j] : m[j];
+        }
+        if (V == 4) *reinterpret_cast<float4*>(a.mom + gi) = make_float4(m[0], m[1], m[2], m[3]);
+        else a.mom[gi] = m[0];
+        break;
+      }
+      case OP_ADAM:
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+          const float v = a.adam_v[gi + j] * a.beta2 + g[j] * g[j] * (1.f - a.beta2);
+          const float m = a.adam_m[gi + j] * a.beta1 + g[j] * (1.f - a.beta1);
+          a.adam_v[gi + j] = v; a.adam_m[gi + j] = m;
+          g[j] = opt_rsqrt(v * deb2) * m * deb1;
+        }
+        break;
+      case OP_NOVOGRAD:
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+          const float p1 = a.beta1 * a.mom[gi + j] + g[j] * F[2];
+          a.mom[gi + j] = p1;
+          g[j] = a.beta1 * p1 + g[j] * F[3];
+        }
+        break;
+      case OP_LR:
+#pragma unroll
+        for (int j = 0; j < V; ++j) g[j] *= a.lr;
+        break;
+      default: break;
+    }
+  }
+}
+
+// segment output for V elements: statistics, then either the final weight update (+ bf16 compute copy) or the
+// intermediate update buffer
+template <int V>
+__device__ __forceinline__ void finish_elems(const ApplyArgs& a, const OptTensor& T, long long gi, float (&g)[V],
+                                             float (&w)[V], float& s1, float& s2) {
+      if (a.emit_stats) {
+#pragma unroll
+    for (int j = 0; j < V; ++j) { s2 += g[j] * g[j]; s1 += g[j]; }
+  }
+  if (a.final_seg) {
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      if (T.flags & 2) g[j] *= a.rezero_mult;
+      if ((T.flags & 1) && a.wd > 0.f) g[j] += w[j] * a.lr * a.wd;
+      w[j] -= g[j];
+    }
+    if (V == 4) {
+      *reinterpret_cast<float4*>(a.master + gi) = make_float4(w[0], w[1], w[2], w[3]);
+      if (a.compute)
+        *reinterpret_cast<uint2*>(a.compute + gi) = make_uint2(pack_bf16x2(w[0], w[1]), pack_bf16x2(w[2], w[3]));
+    } else {
+      a.master[gi] = w[0];
+      if (a.compute) a.compute[gi] = f2bf(w[0]);
+    }
+  } else {
+    if (V == 4) *reinterpret_cast<float4*>(a.uout + gi) = make_float4(g[0], g[1], g[2], g[3]);
+    else a.uout[gi] = g[0];
+  }
+    }
+
+// exact n / d for 0 <= n < 2^31 from a precomputed m = floor((2^32 - 1) / d) + 1 (d >= 2): the estimate is floor(n/d)
+// or one more
+__device__ __forceinline__ int fast_div(int n, int d, unsigned m) {
+  if (d == 1) return n;
+  int q = (int)__umulhi((unsigned)n, m);
+  if (q * d > n) --q;
+  return q;
+}
+
+// narrow rows (C / V lanes per row, a power of two <= 64): the block covers RW_NT * V / C whole rows per iteration,
+// each lane keeps the same V columns in every iteration (register running max of the trailing-dim accumulator),
+// the row max is a shuffle reduction over the row's lanes
+template <int V>
+__device__ __forceinline__ void rows_packed(const ApplyArgs& a, const OptTensor& T, const float* F, const RChunk& ck,
+                                            float* tmax, bool sm3_on, float deb1, float deb2, float& s1, float& s2) {
+  const int tid = threadIdx.x;
+  const int last = T.ndim - 1;
+  const int C = T.dims[last];
+  const int lpr = C / V;
+  const int rpi = RW_NT / lpr;
+  const int sub = tid / lpr, col = (tid % lpr) * V;
+  const float* acc_last = a.sm3_old + T.sm3_off[last] + col;
+  unsigned mg[3] = {0u, 0u, 0u};
+  for (int d = 0; d < last && d < 3; ++d) mg[d] = T.dims[d] > 1 ? 0xFFFFFFFFu / (unsigned)T.dims[d] + 1u : 0u;
+  float tm[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) tm[j] = 0.f;
+  for (int r0 = 0; r0 < ck.nrows; r0 += rpi) {
+    const int rr = r0 + sub;
+    const bool ok = rr < ck.nrows;
+    const int row = ck.row0 + rr;
+    float lead = 3.4e38f;
+    int lidx[3] = {0, 0, 0};
+    if (sm3_on && ok) {
+      int r = row;
+      for (int d = last - 1; d >= 0; --d) {
+        const int q = fast_div(r, T.dims[d], mg[d]);
+        lidx[d] = r - q * T.dims[d];
+        r = q;
+        lead = fminf(lead, a.sm3_old[T.sm3_off[d] + lidx[d]]);
+      }
+    }
+    float rmax = 0.f;
+    if (ok) {
+      const long long gi = T.off + (long long)row * C + col;
+      float g[V], w[V];
+      if (V == 4) {
+        const float4 gv = a.uin ? *reinterpret_cast<const float4*>(a.uin + gi) : *reinterpret_cast<const float4*>(a.grad + gi);
+        const float4 wv = *reinterpret_cast<const float4*>(a.master + gi);
+        g[0] = gv.x; g[1] = gv.y; g[2] = gv.z; g[3] = gv.w;
+        w[0] = wv.x; w[1] = wv.y; w[2] = wv.z; w[3] = wv.w;
+      } else {
+        g[0] = a.uin ? a.uin[gi] : a.grad[gi];
+        w[0] = a.master[gi];
+      }
+      if (!a.uin) {
+#pragma unroll
+        for (int j = 0; j < V; ++j) g[j] *= a.grad_scale;
+      }
+      row_program<V>(a, F, gi, acc_last, lead, g, w, tm, rmax, deb1, deb2);
+      finish_elems<V>(a, T, gi, g, w, s1, s2);
+    }
+    if (sm3_on && last > 0) {
+      for (int o = lpr / 2; o > 0; o >>= 1) rmax = fmaxf(rmax, __shfl_xor(rmax, o, 64));
+      if (ok && (tid % lpr) == 0 && rmax > 0.f)
+        for (int d = 0; d < last; ++d) atomic_max_nonneg(a.sm3_new + T.sm3_off[d] + lidx[d], rmax);
+    }
+  }
+  if (sm3_on) {   // combine the rpi lanes that share each column, then one global atomic per column
+    for (int i = tid; i < C; i += RW_NT) tmax[i] = 0.f;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < V; ++j)
+      if (tm[j] > 0.f) atomicMax(reinterpret_cast<int*>(tmax + col + j), __float_as_int(tm[j]));
+    __syncthreads();
+    for (int i = tid; i < C; i += RW_NT)
+      if (tmax[i] > 0.f) atomic_max_nonneg(a.sm3_new + T.sm3_off[last] + i, tmax[i]);
+  }
+}
+
+template <int V>
+__device__ __forceinline__ void rows_body(const ApplyArgs& a, const OptTensor& T, const float* F, const RChunk& ck,
+                                          float* tmax, bool sm3_on, float deb1, float deb2, float& s1, float& s2) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int last = T.ndim - 1;
+  const int C = T.dims[last];
+  const float* acc_last = a.sm3_old + T.sm3_off[last] + ck.col0;
+  if (sm3_on)
+    for (int c = tid * V; c < ck.ncols; c += RW_NT * V)
+#pragma unroll
+      for (int j = 0; j < V; ++j) tmax[c + j] = 0.f;
+  for (int rr = 0; rr < ck.nrows; ++rr) {
+    const int row = ck.row0 + rr;
+    float lead = 3.4e38f;
+    int lidx[3] = {0, 0, 0};
+    if (sm3_on) {
+      int r = row;
+      for (int d = last - 1; d >= 0; --d) {
+        lidx[d] = r % T.dims[d];
+        r /= T.dims[d];
+        lead = fminf(lead, a.sm3_old[T.sm3_off[d] + lidx[d]]);
+      }
+    }
+    float rmax = 0.f;
+    const long long rbase = T.off + (long long)row * C + ck.col0;
+    for (int c = tid * V; c < ck.ncols; c += RW_NT * V) {
+      const long long gi = rbase + c;
+      float g[V], w[V];
+      if (V == 4) {
+        const float4 gv = a.uin ? *reinterpret_cast<const float4*>(a.uin + gi) : *reinterpret_cast<const float4*>(a.grad + gi);
+        const float4 wv = *reinterpret_cast<const float4*>(a.master + gi);
+        g[0] = gv.x; g[1] = gv.y; g[2] = gv.z; g[3] = gv.w;
+        w[0] = wv.x; w[1] = wv.y; w[2] = wv.z; w[3] = wv.w;
+      } else {
+        g[0] = a.uin ? a.uin[gi] : a.grad[gi];
+        w[0] = a.master[gi];
+      }
+      if (!a.uin) {
+#pragma unroll
+        for (int j = 0; j < V; ++j) g[j] *= a.grad_scale;
+      }
+      float tmx[V];
+#pragma unroll
+      for (int j = 0; j < V; ++j) tmx[j] = sm3_on ? tmax[c + j] : 0.f;
+      row_program<V>(a, F, gi, acc_last + c, lead, g, w, tmx, rmax, deb1, deb2);
+      if (sm3_on) {
+#pragma unroll
+        for (int j = 0; j < V; ++j) tmax[c + j] = tmx[j];
+      }
+      finish_elems<V>(a, T, gi, g, w, s1, s2);
+    }
+    if (sm3_on && last > 0) {
+      rmax = wave_max_f(rmax);
+      if (lane == 0 && rmax > 0.f)
+        for (int d = 0; d < last; ++d) atomic_max_nonneg(a.sm3_new + T.sm3_off[d] + lidx[d], rmax);
+    }
+  }
+  if (sm3_on)
+    for (int c = tid * V; c < ck.ncols; c += RW_NT * V)
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        const float v = tmax[c + j];
+        if (v > 0.f) atomic_max_nonneg(a.sm3_new + T.sm3_off[last] + ck.col0 + c + j, v);
+      }
+}
+
+__global__ __launch_bounds__(RW_NT) void opt_rows_kernel(ApplyArgs a, const RChunk* chunks) {
+  __shared__ float tmax[RW_COLS];
+  const RChunk ck = chunks[blockIdx.x];
+  const OptTensor T = a.tensors[ck.t];
+  const float* F = a.fac + ck.t * 8;
+  bool sm3_on = false;
+  for (int s = 0; s < a.nst; ++s) sm3_on |= a.st[s].op == OP_SM3;
+  const float deb1 = 1.f / (1.f - powf(a.beta1, a.step_count));
+  const float deb2 = 1.f / (1.f - powf(a.beta2, a.step_count));
+  float s1 = 0.f, s2 = 0.f;
+  // vec bit 0: float4 (offset and C multiples of 4); bit 1: narrow rows (C / V lanes per row, power of two <= 64)
+  if (ck.vec & 2) {
+    if (ck.vec & 1) rows_packed<4>(a, T, F, ck, tmax, sm3_on, deb1, deb2, s1, s2);
+    else rows_packed<1>(a, T, F, ck, tmax, sm3_on, deb1, deb2, s1, s2);
+  } else {
+    if (ck.vec & 1) rows_body<4>(a, T, F, ck, tmax, sm3_on, deb1, deb2, s1, s2);
+    else rows_body<1>(a, T, F, ck, tmax, sm3_on, deb1, deb2, s1, s2);
+  }
+  if (a.emit_stats) {
+    __shared__ float red[4];
+    s2 = block_sum<4>(s2, red);
+    s1 = block_sum<4>(s1, red);
+    if (threadIdx.x == 0) { atomicAdd(a.stats + ck.t * 8 + 0, s2); atomicAdd(a.stats + ck.t * 8 + 1, s1); }
+  }
+}
+
 // pass 0: sum g^2, sum g of the (scaled) raw gradient, sum w^2, sum w of the weights (float4 when aligned)
 __global__ __launch_bounds__(NTH) void opt_stats_kernel(const OptTensor* tensors, const Chunk* chunks,
                                                         const float* grad, const float* master, float* stats,
@@ -455,6 +758,7 @@ struct ObstOptDesc {
 
 static_assert(sizeof(OptTensor) == 88, "OptTensor layout is mirrored in python (optim/fused.py)");
 static_assert(sizeof(Chunk) == 24, "Chunk layout is mirrored in python (optim/fused.py)");
+static_assert(sizeof(RChunk) == 24, "RChunk layout is mirrored in python (optim/fused.py)");
 
 OBST_API int obst_opt_stats(const ObstOptDesc* d, hipStream_t s) {
   hipLaunchKernelGGL(opt_stats_kernel, dim3(d->nchunks), dim3(NTH), 0, s, (const OptTensor*)d->tensors,
@@ -474,8 +778,7 @@ OBST_API int obst_opt_scalar(const ObstOptDesc* d, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
-OBST_API int obst_opt_apply(const ObstOptDesc* d, hipStream_t s) {
-  if (d->nst > MAXST) return -1;
+static ApplyArgs apply_args(const ObstOptDesc* d) {
   ApplyArgs a;
   a.tensors = (const OptTensor*)d->tensors; a.chunks = (const Chunk*)d->chunks;
   a.grad = d->grad; a.uin = d->uin; a.uout = d->uout; a.master = d->master; a.compute = (bf16_t*)d->compute;
@@ -491,6 +794,22 @@ OBST_API int obst_opt_apply(const ObstOptDesc* d, hipStream_t s) {
   a.nst = d->nst; a.final_seg = d->final_seg; a.emit_stats = d->emit_stats; a.emit_factored = d->emit_factored;
   a.lr = d->lr; a.wd = d->wd; a.rezero_mult = d->rezero_mult; a.grad_scale = d->grad_scale;
   a.beta1 = d->beta1; a.beta2 = d->beta2; a.step_count = d->step_count;
-  hipLaunchKernelGGL(opt_apply_kernel, dim3(d->nchunks), dim3(NTA), 0, s, a);
+  return a;
+}
+
+OBST_API int obst_opt_apply(const ObstOptDesc* d, hipStream_t s) {
+  if (d->nst > MAXST) return -1;
+  if (d->nchunks <= 0) return 0;
+  hipLaunchKernelGGL(opt_apply_kernel, dim3(d->nchunks), dim3(NTA), 0, s, apply_args(d));
+  return (int)hipGetLastError();
+}
+
+// row-tiled apply (no Adafactor stages, no factored-stat emission); rchunks: RChunk[nrchunks]
+OBST_API int obst_opt_apply_rows(const ObstOptDesc* d, const void* rchunks, int nrchunks, hipStream_t s) {
+  if (d->nst > MAXST || d->emit_factored) return -1;
+  for (int i = 0; i < d->nst; ++i)
+    if (d->stages[4 * i] == OP_ADAFACTOR || d->stages[4 * i] == OP_ADAFACTOR_CLIP) return -2;
+  if (nrchunks <= 0) return 0;
+  hipLaunchKernelGGL(opt_rows_kernel, dim3(nrchunks), dim3(RW_NT), 0, s, apply_args(d), (const RChunk*)rchunks);
   return (int)hipGetLastError();
 }

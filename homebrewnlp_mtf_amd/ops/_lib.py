@@ -94,6 +94,7 @@ _SIGS = {
     "obst_opt_stats": [ctypes.POINTER(OptDesc), c_p],
     "obst_opt_scalar": [ctypes.POINTER(OptDesc), c_p],
     "obst_opt_apply": [ctypes.POINTER(OptDesc), c_p],
+    "obst_opt_apply_rows": [ctypes.POINTER(OptDesc), c_p, c_i, c_p],
     "obst_blaslt_enabled": [],
     "obst_blaslt_set": [c_i],
     "obst_blaslt_stats": [c_p],

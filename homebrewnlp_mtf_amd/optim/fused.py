@@ -30,7 +30,9 @@ OP = dict(none=0, adaptive_clip=1, l2norm_clip=2, global_l2norm_clip=3, value_cl
           adafactor_clip=13, scale=14)
 REDUCTIONS = {"adaptive_clip", "l2norm_clip", "global_l2norm_clip", "gradient_centralisation", "novograd",
               "adafactor", "adafactor_clip"}
-CHUNK = int(os.environ.get("OBST_OPT_CHUNK", 65536))   # elements per apply block (A/B knob)
+CHUNK = int(os.environ.get("OBST_OPT_CHUNK", 65536))   # elements per stats / generic-apply block
+RW_COLS = 8192                                           # row-tiled apply: column range per chunk (optim.hip)
+RW_ELEMS = int(os.environ.get("OBST_OPT_RW_ELEMS", 262144))   # row-tiled apply: elements per chunk (whole rows)
 
 
 def _f2i(x: float) -> int:
@@ -149,8 +151,34 @@ class FusedOptimizer:
             self.tinfo.append((offset, numel, shape, [sm3_off.get((ti, d)) for d in range(ndim)], foff, frows, fcols))
         self.ntensors = len(packed)
         self.nchunks = len(chunks)
+        # row-tiled apply (optim.hip opt_rows_kernel) for every >= 1-D tensor when the chain has no Adafactor;
+        # the generic apply then only runs the 0-dim tensors
+        self.use_rows = not need_af and os.environ.get("OBST_OPT_ROWS", "1") != "0"
+        rchunks, schunks = [], []
+        for ti, (offset, numel, ndim, shape) in enumerate(recs):
+            if not self.use_rows or ndim == 0:
+                schunks.extend(c for c in chunks if struct.unpack_from("<i", c)[0] == ti)
+                continue
+            C = shape[-1]
+            R = numel // C
+            vec = int(offset % 4 == 0 and C % 4 == 0)
+            lpr = C // (4 if vec else 1)
+            if lpr <= 64 and lpr & (lpr - 1) == 0:      # narrow rows: several whole rows per block iteration
+                vec |= 2
+                per = max(1, RW_ELEMS // C)
+                for row0 in range(0, R, per):
+                    rchunks.append(struct.pack("<6i", ti, row0, min(per, R - row0), 0, C, vec))
+                continue
+            for col0 in range(0, C, RW_COLS):
+                ncols = min(RW_COLS, C - col0)
+                per = max(1, RW_ELEMS // ncols)
+                for row0 in range(0, R, per):
+                    rchunks.append(struct.pack("<6i", ti, row0, min(per, R - row0), col0, ncols, vec))
+        self.nrchunks, self.nschunks = len(rchunks), len(schunks)
         self.t_tensors = torch.tensor(bytearray(b"".join(packed)), dtype=torch.uint8, device=dev)
         self.t_chunks = torch.tensor(bytearray(b"".join(chunks)), dtype=torch.uint8, device=dev)
+        self.t_rchunks = torch.tensor(bytearray(b"".join(rchunks) or b"\0" * 24), dtype=torch.uint8, device=dev)
+        self.t_schunks = torch.tensor(bytearray(b"".join(schunks) or b"\0" * 24), dtype=torch.uint8, device=dev)
         f32 = dict(dtype=torch.float32, device=dev)
         self.stats = torch.zeros(self.ntensors * 8, **f32)
         self.facs = torch.zeros(self.ntensors * 8, **f32)
@@ -249,7 +277,13 @@ class FusedOptimizer:
             d.uout = 0 if last else bufs[bi].data_ptr()
             self._set_stages(d, seg.stages)
             d.final_seg, d.emit_stats, d.emit_factored = int(last), int(seg.emit_stats), int(seg.emit_factored)
-            L.check(lib.obst_opt_apply(d, sp), "opt_apply")
+            if self.use_rows:
+                L.check(lib.obst_opt_apply_rows(d, self.t_rchunks.data_ptr(), self.nrchunks, sp), "opt_apply_rows")
+                d.chunks, d.nchunks = self.t_schunks.data_ptr(), self.nschunks
+                L.check(lib.obst_opt_apply(d, sp), "opt_apply")
+                d.chunks, d.nchunks = self.t_chunks.data_ptr(), self.nchunks
+            else:
+                L.check(lib.obst_opt_apply(d, sp), "opt_apply")
             if seg.emit_stats:
                 self._reduce_stats()
             if not last:

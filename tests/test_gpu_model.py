@@ -70,7 +70,9 @@ def test_model_forward_backward(cuda, variant):
                                    "sm3-l2norm_clip:0.1-momentum:0.9:1:0-learning_rate",
                                    "adafactor-learning_rate", "gradient_centralisation-value_clip:0.01-adam-"
                                                               "learning_rate-weight_centralisation"])
-def test_fused_optimizer_matches_reference(cuda, chain):
+@pytest.mark.parametrize("rows", ["1", "0"], ids=["row_tiled", "generic"])
+def test_fused_optimizer_matches_reference(cuda, chain, rows, monkeypatch):
+    monkeypatch.setenv("OBST_OPT_ROWS", rows)
     cfg = dict(GPT, optimizer=chain, calculation_dtype="bfloat16", weight_decay=0.01,
                block_config=GPT["block_config"] + [{"layer": ["rezero"], "skip": True}])
     torch.manual_seed(1)
