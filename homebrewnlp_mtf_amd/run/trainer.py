@@ -84,10 +84,11 @@ class Trainer:
                 v = v.detach().float()
                 metrics[k] = metrics.get(k, 0) + v / len(micro)
         with debug.range_("dp_sync"):
-            self.grad_sync.finish(average=True)
+            # the 1/dp mean is folded into the optimizer's gradient scale (no extra pass over the gradient buffer)
+            self.grad_sync.finish(average=False)
         lr = learning_rate(self.params, self.global_step)
         with debug.range_("optimizer"):
-            self.opt.step(lr, self.global_step + 1)
+            self.opt.step(lr, self.global_step + 1, grad_scale=1.0 / max(self.mesh.dp, 1))
         self.global_step += 1
         metrics["learning_rate"] = torch.tensor(lr)
         if debug.CHECK:
