@@ -144,6 +144,10 @@ def _wgrad_gemm(x2, dy2, gw, plan: LinearPlan, xT=None, dyT=None):
         raw.gemm(raw.Operand(xT, 0, M, K * M), raw.Operand(dyT, 0, M, N * M), raw.Operand(gw, 0, N, K * N),
                  K, N, M, batch=(H, 1), beta=1.0)
         return
+    if xT is not None:      # shared token-contiguous x (hipBLASLt: NT runs ~25 % faster than TT at T = 32k)
+        raw.gemm(raw.Operand(xT, 0, M, K * M), raw.Operand(dy2, 1, H * N, N), raw.Operand(gw, 0, N, K * N),
+                 K, N, M, batch=(H, 1), beta=1.0)
+        return
     raw.gemm(raw.Operand(x2, 1, H * K, K), raw.Operand(dy2, 1, H * N, N), raw.Operand(gw, 0, N, K * N),
              K, N, M, batch=(H, 1), beta=1.0)
 
@@ -322,8 +326,13 @@ class _DotAttention(torch.autograd.Function):
         outs = []
         Mo, Ko, No = p_out.M, p_out.H * p_out.K, p_out.H * p_out.N
         baseT = tokens_transposed(base, Mo, Ko)
+        if baseT is None and raw.on_gpu(base) and raw.lt_enabled() and Mo % 8 == 0 and Ko % 8 == 0:
+            # one transpose of base serves the three q/k/v weight gradients (tools/bench_wgrad.py: -118 us each
+            # against the token-strided layout, for one 122 us transpose)
+            baseT = torch.empty(Ko * Mo, dtype=base.dtype, device=base.device)
+            raw.transpose(base, baseT, Mo, Ko, Ko, Mo)
         dkqvT = None
-        if baseT is not None and Mo % 8 == 0 and No % 8 == 0:
+        if baseT is not None and Mo % 8 == 0 and No % 8 == 0 and not raw.lt_enabled():
             dkqvT = torch.empty(3 * No * Mo, dtype=dkqv.dtype, device=dkqv.device)
             raw.transpose(dkqv, dkqvT, Mo, No, No, Mo, 3, Mo * No, Mo * No)
         for j in range(3):
