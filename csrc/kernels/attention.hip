@@ -42,8 +42,28 @@ __device__ __forceinline__ int lds_off(int row, int chunk) {
   return row * Geo<D>::ROWB + ((chunk ^ swz<D>(row)) << 4);
 }
 
+// swizzle of the images the 16x16x32 kernels (dQ, dK/dV, forward v1) stage and read. D = 128: chunk ^= (row & 7) << 1.
+// Their row read (lanes 0-15 rows r..r+15 of chunk c, lanes 16-31 chunk c+1) meets the ds_read_b128 lane groups
+// {0-3,12-15,20-27} / {4-11,16-19,28-31}: rows {0-3,12-15} of c with rows 4-11 of c+1 -- (row & 7) << 1 is one-to-one
+// on each of those row sets and leaves bit 0 to the chunk, so the 16 slots of a group are distinct. Their transposed
+// read (one 32-lane half = rows r..r+7, chunks c, c+1) gets 8 distinct bit-1..3 values and the chunk bit: also
+// conflict-free. The (row&3)<<2 | (row>>2)&3 swizzle of the 32x32x16 kernels is 2-way on both reads here
+// (cdna_hip_programming.md T10: SQ_LDS_BANK_CONFLICT 138M per dK/dV launch, profiles/r1e_pmc_attn_dkv16.txt).
+template <int D>
+__device__ __forceinline__ int swz16(int row) {
+  if (D == 128) return (row & 7) << 1;
+  return swz<D>(row);
+}
+
+template <int D>
+__device__ __forceinline__ int lds_off16(int row, int chunk) {
+  return row * Geo<D>::ROWB + ((chunk ^ swz16<D>(row)) << 4);
+}
+
 // stage ROWS x D bf16 rows (token-major, row stride ld) into an LDS image with direct global->LDS DMA
-// (global_load_lds_dwordx4, one 1 KiB piece per wave-instruction, lane-linear in LDS): the per-lane SOURCE chunk is
+// (global_load_lds_dwordx4 from inline asm, one 1 KiB piece per wave-instruction, lane-linear in LDS; the consumer
+// waits with vm_wait<0>() before the publishing barrier -- the builtin made the compiler put vmcnt(0) in front of
+// every LDS read, so the next tile's DMA could never overlap the current tile's MFMAs): the per-lane SOURCE chunk is
 // pre-swizzled so the image matches lds_off(). Rows >= nvalid are clamped to the last valid row (masked later).
 template <int D, int ROWS>
 __device__ __forceinline__ void stage_rows(char* lds, const bf16_t* g, long long ld, int nvalid, int tid) {
@@ -58,20 +78,18 @@ __device__ __forceinline__ void stage_rows(char* lds, const bf16_t* g, long long
     if (PIECES % 4 == 0 || j < PIECES) {
       const int row = j * RPP + lane / CPR;
       const int p = lane % CPR;
-      const int c = p ^ swz<D>(row);
+      const int c = p ^ swz16<D>(row);
       const int srow = row < last ? row : last;
-      __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(g + srow * ld + c * 8),
-                                       (void __attribute__((address_space(3)))*)(lds + j * 1024), 16, 0, 0);
+      glds16_asm(g + srow * ld + c * 8, lds + j * 1024);
     }
   }
 }
 
-// 4-byte values (lse / delta rows) for `n` consecutive queries, n*4 <= 1 KiB: one piece from wave 0
+// 4-byte values (lse / delta rows) for `n` <= 64 consecutive queries: one 256-B piece from wave 0
 __device__ __forceinline__ void stage_f32(char* lds, const float* g, int n, int nvalid, int tid) {
-  if (tid < n) {
-    const int q = tid < nvalid ? tid : nvalid - 1;
-    __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(g + q),
-                                     (void __attribute__((address_space(3)))*)(lds), 4, 0, 0);
+  if (tid < 64) {   // wave 0, all lanes (n <= 64: lanes past n re-read the last value)
+    const int q = min(min(tid, n - 1), nvalid - 1);
+    glds4_asm(g + q, lds);
   }
 }
 
@@ -79,7 +97,7 @@ __device__ __forceinline__ void stage_f32(char* lds, const float* g, int n, int 
 template <int D>
 __device__ __forceinline__ bf16x8_t row_frag(const char* lds, int row0, int ds, int lane) {
   const int r = row0 + (lane & 15);
-  return *reinterpret_cast<const bf16x8_t*>(lds + lds_off<D>(r, ds * 4 + (lane >> 4)));
+  return *reinterpret_cast<const bf16x8_t*>(lds + lds_off16<D>(r, ds * 4 + (lane >> 4)));
 }
 
 // transposed fragment over 32 rows starting at row0: lane (g, i) holds X[row0 + perm(g, jj)][d0 + i],
@@ -90,8 +108,8 @@ __device__ __forceinline__ bf16x8_t tr_frag(const char* lds, int row0, int d0, i
   const int col = d0 + 4 * pp;
   const int c = col >> 3;
   const int r0 = row0 + 4 * g + q, r1 = r0 + 16;
-  const int o0 = r0 * Geo<D>::ROWB + ((c ^ swz<D>(r0)) << 4) + ((pp & 1) << 3);
-  const int o1 = r1 * Geo<D>::ROWB + ((c ^ swz<D>(r1)) << 4) + ((pp & 1) << 3);
+  const int o0 = r0 * Geo<D>::ROWB + ((c ^ swz16<D>(r0)) << 4) + ((pp & 1) << 3);
+  const int o1 = r1 * Geo<D>::ROWB + ((c ^ swz16<D>(r1)) << 4) + ((pp & 1) << 3);
   s16x4_t v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4_t, lds + o0));
   s16x4_t v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4_t, lds + o1));
   s16x8_t v = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
@@ -266,6 +284,7 @@ __global__ __launch_bounds__(NTH, 2) void attn_fwd_kernel(AttnArgs a) {
   for (int dt = 0; dt < G::DT; ++dt) o[dt][0] = o[dt][1] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   float m[2] = {NEG_BIG, NEG_BIG}, l[2] = {0.f, 0.f};
   const float c2 = a.scale * LOG2E;
+  vm_wait<0>();   // staged tiles (asm LDS-DMA: the compiler does not track them) have landed
   __syncthreads();
 
   for (int kb = 0; kb < nkb; ++kb) {
@@ -282,6 +301,7 @@ __global__ __launch_bounds__(NTH, 2) void attn_fwd_kernel(AttnArgs a) {
       if (need_mask) fwd_tile<D, true>(sK, sV, qf, o, m, l, k0, qw, a.S, a.causal, c2, lane);
       else fwd_tile<D, false>(sK, sV, qf, o, m, l, k0, qw, a.S, a.causal, c2, lane);
     }
+    vm_wait<0>();   // staged tiles (asm LDS-DMA: the compiler does not track them) have landed
     __syncthreads();
   }
   // epilogue: lane holds O[q = qw + qt*16 + i][d = dt*16 + 4g + v]
@@ -436,6 +456,7 @@ __global__ __launch_bounds__(NTH, 2) void attn_bwd_dq_kernel(AttnArgs a) {
 #pragma unroll
   for (int dt = 0; dt < G::DT; ++dt) acc[dt][0] = acc[dt][1] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   const float c2 = a.scale * LOG2E;
+  vm_wait<0>();   // staged tiles (asm LDS-DMA: the compiler does not track them) have landed
   __syncthreads();
   for (int kb = 0; kb < nkb; ++kb) {
     const int k0 = kb * 64;
@@ -451,6 +472,7 @@ __global__ __launch_bounds__(NTH, 2) void attn_bwd_dq_kernel(AttnArgs a) {
       if (need_mask) dq_tile<D, true>(sK, sV, qf, df, lse2, dlt, acc, k0, qw, a.S, a.causal, c2, lane);
       else dq_tile<D, false>(sK, sV, qf, df, lse2, dlt, acc, k0, qw, a.S, a.causal, c2, lane);
     }
+    vm_wait<0>();   // staged tiles (asm LDS-DMA: the compiler does not track them) have landed
     __syncthreads();
   }
 #pragma unroll
@@ -567,6 +589,7 @@ __global__ __launch_bounds__(NTH, 2) void attn_bwd_dkv_kernel(AttnArgs a) {
   for (int dt = 0; dt < G::DT; ++dt) dk[dt] = dv[dt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   const float c2 = a.scale * LOG2E;
   const int key = kw + i;
+  vm_wait<0>();   // staged tiles (asm LDS-DMA: the compiler does not track them) have landed
   __syncthreads();
   for (int c = 0; c < nqc; ++c) {
     const int q0 = qstart + c * QC;
@@ -580,6 +603,7 @@ __global__ __launch_bounds__(NTH, 2) void attn_bwd_dkv_kernel(AttnArgs a) {
       if (need_mask) dkv_chunk<D, true>(sQ, sD, sL, sDl, kf, vf, dk, dv, q0, key, a.S, a.causal, c2, lane);
       else dkv_chunk<D, false>(sQ, sD, sL, sDl, kf, vf, dk, dv, q0, key, a.S, a.causal, c2, lane);
     }
+    vm_wait<0>();   // staged tiles (asm LDS-DMA: the compiler does not track them) have landed
     __syncthreads();
   }
   if (key < a.S) {

@@ -88,13 +88,17 @@ enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_SILU = 3, ACT_SIG
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
 __device__ __forceinline__ float softplusf_(float x) { return x > 20.f ? x : log1pf(__expf(x)); }
 
+// tanh-form gelu through the identity 0.5 (1 + tanh(u)) = sigmoid(2u): one v_exp_f32 + one reciprocal instead of
+// the libm tanhf (~30 VALU with range branches) -- the elementwise gelu passes were VALU-bound
+__device__ __forceinline__ float gelu_s(float x) {   // sigmoid(2u), u = k0 (x + k1 x^3)
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  return __frcp_rn(1.f + __expf(-2.f * k0 * (x + k1 * x * x * x)));
+}
+
 __device__ __forceinline__ float act_fwd(int act, float x) {
   switch (act) {
     case ACT_RELU: return fmaxf(x, 0.f);
-    case ACT_GELU: {
-      const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-      return 0.5f * x * (1.f + tanhf(k0 * (x + k1 * x * x * x)));
-    }
+    case ACT_GELU: return x * gelu_s(x);
     case ACT_SILU: return x * sigmoidf_(x);
     case ACT_SIGMOID: return sigmoidf_(x);
     case ACT_TANH: return tanhf(x);
@@ -110,11 +114,10 @@ __device__ __forceinline__ float act_fwd(int act, float x) {
 __device__ __forceinline__ float act_grad(int act, float x) {
   switch (act) {
     case ACT_RELU: return x > 0.f ? 1.f : 0.f;
-    case ACT_GELU: {
+    case ACT_GELU: {   // d/dx x s(2u) = s + 2 x s (1 - s) u'(x), s = sigmoid(2u) = 0.5 (1 + tanh u)
       const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-      float u = k0 * (x + k1 * x * x * x);
-      float t = tanhf(u);
-      return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x * x);
+      const float s = gelu_s(x);
+      return s + 2.f * x * s * (1.f - s) * k0 * (1.f + 3.f * k1 * x * x);
     }
     case ACT_SILU: { float s = sigmoidf_(x); return s * (1.f + x * (1.f - s)); }
     case ACT_SIGMOID: { float s = sigmoidf_(x); return s * (1.f - s); }
