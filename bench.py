@@ -41,6 +41,7 @@ def main():
                                                      "gpt_neo_1.3b.json"))
     ap.add_argument("--batch-per-gpu", type=int, default=0, help="default: config train_batch_size")
     ap.add_argument("--depth", type=int, default=0, help="(debug only: invalidates the headline number)")
+    ap.add_argument("--hip-graphs", type=int, default=0, help="1: replay the captured training step (1 GPU)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -66,6 +67,8 @@ def main():
     overrides["mesh"] = {"dp": world, "tp": 1}
     if args.depth:
         overrides["depth"] = args.depth
+    if args.hip_graphs:
+        overrides["use_hip_graphs"] = True
     params = load_config(args.config, overrides)
     torch.manual_seed(1234 + rank)
     trainer = Trainer(params, device, mesh)
@@ -88,7 +91,8 @@ def main():
         m = trainer.step(batches[i % len(batches)])
         if i == 0:
             torch.cuda.synchronize()
-            log(f"first step done ({time.time() - t_w:.1f}s) loss={float(m['loss']):.4f}")
+            log(f"first step done ({time.time() - t_w:.1f}s) loss={float(m['loss']):.4f} "
+                f"peak mem {torch.cuda.max_memory_allocated(device) / 2**30:.1f} GiB")
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -118,7 +122,8 @@ def main():
             "config": {"model": os.path.basename(args.config).replace(".json", "") +
                                 (f"-depth{args.depth}(debug)" if args.depth else ""),
                        "global_batch": params.train_batch_size, "seq_len": S, "parallelism": f"dp{world}",
-                       "params": trainer.store.global_numel(), "optimizer": params.optimizer}}), flush=True)
+                       "params": trainer.store.global_numel(), "optimizer": params.optimizer,
+                       "hip_graphs": bool(params.use_hip_graphs and trainer._graphs_ok())}}), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

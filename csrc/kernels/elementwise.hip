@@ -27,10 +27,15 @@ __device__ __forceinline__ uint4 pack8(const float (&f)[8]) {
 
 // op: 0 act fwd (y=act(x)), 1 act bwd (y = dy * act'(x)), 2 add (y = x + z), 3 mul scalar tensor (y = x * s[0]),
 //     4 dropout fwd/bwd (y = x * keep(i) / keep_prob), 5 axpby (y = alpha*x + beta*z), 6 mul (y = x*z)
-__global__ __launch_bounds__(NTH) void ew_kernel(int op, int act, const bf16_t* __restrict__ X,
+// OP / ACT as template parameters (-1: taken from the runtime arguments) so the hot instances -- gelu forward and
+// backward, residual add -- carry no per-element dispatch
+template <int OP, int ACT>
+__global__ __launch_bounds__(NTH) void ew_kernel(int op_rt, int act_rt, const bf16_t* __restrict__ X,
                                                  const bf16_t* __restrict__ Z, bf16_t* __restrict__ Y, long long nvec,
                                                  const float* __restrict__ sptr, float alpha, float beta,
                                                  unsigned long long seed, float keep) {
+  const int op = OP >= 0 ? OP : op_rt;
+  const int act = ACT >= 0 ? ACT : act_rt;
   for (long long v = (long long)blockIdx.x * NTH + threadIdx.x; v < nvec; v += (long long)gridDim.x * NTH) {
     float x[8], z[8];
     unpack8(reinterpret_cast<const uint4*>(X)[v], x);
@@ -40,7 +45,7 @@ __global__ __launch_bounds__(NTH) void ew_kernel(int op, int act, const bf16_t* 
       float r;
       switch (op) {
         case 0: r = act_fwd(act, x[j]); break;
-        case 1: r = x[j] * 0.f + z[j] * act_grad(act, x[j]); break;  // X = saved input, Z = dy
+        case 1: r = z[j] * act_grad(act, x[j]); break;  // X = saved input, Z = dy
         case 2: r = x[j] + z[j]; break;
         case 3: r = x[j] * sptr[0]; break;
         case 4: {
@@ -175,7 +180,11 @@ OBST_API int obst_elementwise(const ObstEwDesc* d, hipStream_t st) {
   if (d->n % 8) return -1;
   if ((((uintptr_t)d->X) | ((uintptr_t)d->Y) | ((uintptr_t)d->Z)) & 15) return -2;
   const long long nvec = d->n / 8;
-  hipLaunchKernelGGL(ew_kernel, dim3(grid_for(nvec)), dim3(NTH), 0, st, d->op, d->act, (const bf16_t*)d->X,
+  auto k = ew_kernel<-1, -1>;
+  if (d->act == ACT_GELU && d->op == 0) k = ew_kernel<0, ACT_GELU>;
+  else if (d->act == ACT_GELU && d->op == 1) k = ew_kernel<1, ACT_GELU>;
+  else if (d->op == 2) k = ew_kernel<2, 0>;
+  hipLaunchKernelGGL(k, dim3(grid_for(nvec)), dim3(NTH), 0, st, d->op, d->act, (const bf16_t*)d->X,
                      (const bf16_t*)d->Z, (bf16_t*)d->Y, nvec, d->sptr, d->alpha, d->beta, d->seed, d->keep);
   return (int)hipGetLastError();
 }

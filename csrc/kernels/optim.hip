@@ -48,7 +48,11 @@ struct ApplyArgs {
   Stage st[MAXST]; int nst;
   int final_seg, emit_stats, emit_factored;
   float lr, wd, rezero_mult, grad_scale, beta1, beta2, step_count;
+  const float* dyn;           // device [lr, step_count] (graph replay: the host values change every step) or null
 };
+
+__device__ __forceinline__ float lr_of(const ApplyArgs& a) { return a.dyn ? a.dyn[0] : a.lr; }
+__device__ __forceinline__ float step_of(const ApplyArgs& a) { return a.dyn ? a.dyn[1] : a.step_count; }
 
 __device__ __forceinline__ float opt_rsqrt(float x) { return 1.f / fmaxf(sqrtf(x), 1e-5f); }
 
@@ -218,7 +222,7 @@ __device__ __forceinline__ void apply_elems(const ApplyArgs& a, const OptTensor&
       }
       case OP_LR:
 #pragma unroll
-        for (int j = 0; j < V; ++j) g[j] *= a.lr;
+        for (int j = 0; j < V; ++j) g[j] *= lr_of(a);
         break;
       default: break;
     }
@@ -247,7 +251,7 @@ __device__ __forceinline__ void apply_elems(const ApplyArgs& a, const OptTensor&
 #pragma unroll
     for (int j = 0; j < V; ++j) {
       if (T.flags & 2) g[j] *= a.rezero_mult;
-      if ((T.flags & 1) && a.wd > 0.f) g[j] += w[j] * a.lr * a.wd;
+      if ((T.flags & 1) && a.wd > 0.f) g[j] += w[j] * lr_of(a) * a.wd;
       w[j] -= g[j];
     }
     if (V == 4) {
@@ -300,8 +304,8 @@ __global__ __launch_bounds__(NTA) void opt_apply_kernel(ApplyArgs a) {
     for (int i = threadIdx.x; i < (af_cols_win ? T.fac_cols : 0); i += NTA) wlast[i] = 0.f;
   }
   __syncthreads();
-  const float deb1 = 1.f / (1.f - powf(a.beta1, a.step_count));
-  const float deb2 = 1.f / (1.f - powf(a.beta2, a.step_count));
+  const float deb1 = 1.f / (1.f - powf(a.beta1, step_of(a)));
+  const float deb2 = 1.f / (1.f - powf(a.beta2, step_of(a)));
   const bool vec = T.ndim > 0 && (T.off & 3) == 0 && (start & 3) == 0 && (len & 3) == 0 &&
                    (T.dims[T.ndim - 1] & 3) == 0 && (!af || (T.fac_cols & 3) == 0);
   const int V = vec ? 4 : 1;
@@ -439,7 +443,7 @@ __device__ __forceinline__ void row_program(const ApplyArgs& a, const float* F, 
         break;
       case OP_LR:
 #pragma unroll
-        for (int j = 0; j < V; ++j) g[j] *= a.lr;
+        for (int j = 0; j < V; ++j) g[j] *= lr_of(a);
         break;
       default: break;
     }
@@ -459,7 +463,7 @@ __device__ __forceinline__ void finish_elems(const ApplyArgs& a, const OptTensor
 #pragma unroll
     for (int j = 0; j < V; ++j) {
       if (T.flags & 2) g[j] *= a.rezero_mult;
-      if ((T.flags & 1) && a.wd > 0.f) g[j] += w[j] * a.lr * a.wd;
+      if ((T.flags & 1) && a.wd > 0.f) g[j] += w[j] * lr_of(a) * a.wd;
       w[j] -= g[j];
     }
     if (V == 4) {
@@ -629,8 +633,8 @@ __global__ __launch_bounds__(RW_NT) void opt_rows_kernel(ApplyArgs a, const RChu
   const float* F = a.fac + ck.t * 8;
   bool sm3_on = false;
   for (int s = 0; s < a.nst; ++s) sm3_on |= a.st[s].op == OP_SM3;
-  const float deb1 = 1.f / (1.f - powf(a.beta1, a.step_count));
-  const float deb2 = 1.f / (1.f - powf(a.beta2, a.step_count));
+  const float deb1 = 1.f / (1.f - powf(a.beta1, step_of(a)));
+  const float deb2 = 1.f / (1.f - powf(a.beta2, step_of(a)));
   float s1 = 0.f, s2 = 0.f;
   // vec bit 0: float4 (offset and C multiples of 4); bit 1: narrow rows (C / V lanes per row, power of two <= 64)
   if (ck.vec & 2) {
@@ -684,7 +688,9 @@ __global__ __launch_bounds__(NTH) void opt_stats_kernel(const OptTensor* tensors
 __global__ __launch_bounds__(NTH) void opt_scalar_kernel(const OptTensor* tensors, int ntensors, const float* stats,
                                                          float* fac, float* sstate, float* af_state,
                                                          const float* af_rows_sum, const float* af_cols_sum, Stage st,
-                                                         float beta1, float beta2, float step_count, int tp_size) {
+                                                         float beta1, float beta2, float step_count, int tp_size,
+                                                         const float* dyn) {
+  if (dyn) step_count = dyn[1];
   __shared__ float red[4];
   float gl = 0.f;
   for (int t = threadIdx.x; t < ntensors; t += NTH) gl += stats[t * 8 + 0];
@@ -754,6 +760,7 @@ struct ObstOptDesc {
   int nst; int final_seg; int emit_stats; int emit_factored;
   float lr, wd, rezero_mult, grad_scale, beta1, beta2, step_count;
   int tp_size;
+  const float* dyn;        // device [lr, step_count] or null (then lr / step_count above)
 };
 
 static_assert(sizeof(OptTensor) == 88, "OptTensor layout is mirrored in python (optim/fused.py)");
@@ -774,7 +781,7 @@ OBST_API int obst_opt_scalar(const ObstOptDesc* d, hipStream_t s) {
   st.c = __builtin_bit_cast(float, d->stages[3]);
   hipLaunchKernelGGL(opt_scalar_kernel, dim3(1), dim3(NTH), 0, s, (const OptTensor*)d->tensors, d->ntensors, d->stats,
                      d->fac, d->sstate, d->af_state, d->af_rows_sum, d->af_cols_sum, st, d->beta1, d->beta2,
-                     d->step_count, d->tp_size);
+                     d->step_count, d->tp_size, d->dyn);
   return (int)hipGetLastError();
 }
 
@@ -793,7 +800,7 @@ static ApplyArgs apply_args(const ObstOptDesc* d) {
   }
   a.nst = d->nst; a.final_seg = d->final_seg; a.emit_stats = d->emit_stats; a.emit_factored = d->emit_factored;
   a.lr = d->lr; a.wd = d->wd; a.rezero_mult = d->rezero_mult; a.grad_scale = d->grad_scale;
-  a.beta1 = d->beta1; a.beta2 = d->beta2; a.step_count = d->step_count;
+  a.beta1 = d->beta1; a.beta2 = d->beta2; a.step_count = d->step_count; a.dyn = d->dyn;
   return a;
 }
 

@@ -225,6 +225,7 @@ class ParamStore:
         fold them into the flat fp32 buffer so the optimizer/all-reduce see one gradient."""
         for t in self._leaves.values():
             if t.grad is not None:
+                self.leaf_grads_seen = True     # a plain-autograd path is active: no whole-step hipGraph
                 t.main_grad.add_(t.grad.float())
                 t.grad = None
 

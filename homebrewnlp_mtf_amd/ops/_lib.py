@@ -71,7 +71,7 @@ class OptDesc(ctypes.Structure):
                 ("sm3_old", c_p), ("sm3_new", c_p), ("af_state", c_p), ("af_rows_sum", c_p), ("af_cols_sum", c_p),
                 ("stages", c_i * 32), ("nst", c_i), ("final_seg", c_i), ("emit_stats", c_i), ("emit_factored", c_i),
                 ("lr", c_f), ("wd", c_f), ("rezero_mult", c_f), ("grad_scale", c_f), ("beta1", c_f), ("beta2", c_f),
-                ("step_count", c_f), ("tp_size", c_i)]
+                ("step_count", c_f), ("tp_size", c_i), ("dyn", c_p)]
 
 
 _SIGS = {

@@ -195,6 +195,10 @@ class FusedOptimizer:
         self.u = torch.empty(total, **f32) if nseg > 1 else None
         self.u2 = torch.empty(total, **f32) if nseg > 2 else None
         self.flip = 0
+        # [lr, step_count] on the device: the kernels read them from here, so a captured step (hipGraph replay,
+        # Trainer with use_hip_graphs) sees each step's values; ``external_dyn``: the caller fills them
+        self.dyn = torch.zeros(2, **f32)
+        self.external_dyn = False
 
     # ------------------------------------------------------------------------------------------------------------
     def _desc(self, lr, step_count, grad_scale):
@@ -215,7 +219,13 @@ class FusedOptimizer:
         d.lr, d.wd, d.rezero_mult, d.grad_scale = lr, p.weight_decay, p.rezero_lr_multiplier, grad_scale
         d.beta1, d.beta2, d.step_count = p.opt_beta1, p.opt_beta2, float(step_count)
         d.tp_size = self.tp
+        d.dyn = self.dyn.data_ptr()
         return d
+
+    def set_dyn(self, lr: float, step_count: int):
+        """stream-ordered fills of the device-side learning rate / step (outside any captured region)"""
+        self.dyn[0].fill_(float(lr))
+        self.dyn[1].fill_(float(step_count))
 
     def _set_stages(self, d, stages):
         if len(stages) > 8:
@@ -244,6 +254,8 @@ class FusedOptimizer:
     def step(self, lr: float, step_count: int, grad_scale: float = 1.0):
         lib = L.lib()
         sp = L.stream_ptr()
+        if not self.external_dyn:
+            self.set_dyn(lr, step_count)
         d = self._desc(lr, step_count, grad_scale)
         self.stats.zero_()
         L.check(lib.obst_opt_stats(d, sp), "opt_stats")

@@ -66,6 +66,18 @@ class Trainer:
         p = self.params
         if p.multi_loss_strategy in ("pcgrad", "mgda") and p.use_video and p.use_language:
             return self._multi_loss_step(batch)
+        if p.use_hip_graphs and self._graphs_ok():
+            return self._graph_step(batch)
+        lr = learning_rate(self.params, self.global_step)
+        metrics = self._step_body(batch, lr)
+        self.global_step += 1
+        metrics["learning_rate"] = torch.tensor(lr)
+        if debug.CHECK:
+            debug.verify()
+        return metrics
+
+    def _step_body(self, batch: typing.Dict[str, torch.Tensor], lr: float) -> typing.Dict[str, torch.Tensor]:
+        """zero grads, forward + backward over the micro-batches, DP sync, optimizer -- all device work of a step"""
         self.store.zero_grad()
         micro = self._micro_batches(batch)
         metrics: typing.Dict[str, torch.Tensor] = {}
@@ -86,13 +98,56 @@ class Trainer:
         with debug.range_("dp_sync"):
             # the 1/dp mean is folded into the optimizer's gradient scale (no extra pass over the gradient buffer)
             self.grad_sync.finish(average=False)
-        lr = learning_rate(self.params, self.global_step)
         with debug.range_("optimizer"):
             self.opt.step(lr, self.global_step + 1, grad_scale=1.0 / max(self.mesh.dp, 1))
+        return metrics
+
+    # ---------------------------------------------------------------------------------------------------------------
+    # Whole-step hipGraph (``use_hip_graphs``): the device work of a training step -- forward, backward (every HIP
+    # kernel, hipBLASLt GEMM and allocation of the step), the fused optimizer -- is captured once and replayed, so
+    # the host issues one graph launch per step instead of ~1000 kernel launches. The values that change between
+    # steps live on the device (input tokens copied into static buffers, [lr, step] read by the optimizer kernels);
+    # the SM3 accumulators alternate between two buffers, so one graph is captured per parity.
+    def _graphs_ok(self) -> bool:
+        p = self.params
+        dropout = p.input_dropout > 0 or "dropout" in str(p.block_config)
+        return (self.device.type == "cuda" and isinstance(self.opt, fused_opt.FusedOptimizer)
+                and self.mesh.world == 1 and int(p.grad_accumulation) == 1 and not dropout
+                and not getattr(self.store, "leaf_grads_seen", False) and not debug.CHECK)
+
+    def _graph_step(self, batch: typing.Dict[str, torch.Tensor]) -> typing.Dict[str, torch.Tensor]:
+        g = getattr(self, "_graph", None)
+        if g is None:
+            g = self._graph = {"inputs": {k: v.clone() for k, v in batch.items() if v is not None},
+                               "graphs": {}, "warm": 0, "pool": torch.cuda.graph_pool_handle()}
+            self.opt.external_dyn = True
+        for k, v in batch.items():
+            if v is not None:
+                g["inputs"][k].copy_(v, non_blocking=True)
+        lr = learning_rate(self.params, self.global_step)
+        self.opt.set_dyn(lr, self.global_step + 1)
+        parity = self.opt.flip
+        if parity not in g["graphs"]:
+            if g["warm"] < 2:     # eager warm-up: first-use GEMM plans, workspaces, allocator growth
+                g["warm"] += 1
+                metrics = self._step_body(g["inputs"], lr)
+                self.global_step += 1
+                metrics["learning_rate"] = torch.tensor(lr)
+                return metrics
+            graph = torch.cuda.CUDAGraph()
+            torch.cuda.synchronize(self.device)
+            with torch.cuda.graph(graph, pool=g["pool"]):
+                out = self._step_body(g["inputs"], lr)
+            self.opt.flip = parity   # capture ran the host side of the step (buffer flip) but executed nothing
+            g["graphs"][parity] = (graph, out)
+            log(f"captured the training step in a hipGraph (SM3 parity {parity})")
+        graph, out = g["graphs"][parity]
+        graph.replay()
+        self.opt.flip = 1 - parity
+        self.store.bump()
         self.global_step += 1
+        metrics = {k: v.clone() for k, v in out.items()}
         metrics["learning_rate"] = torch.tensor(lr)
-        if debug.CHECK:
-            debug.verify()
         return metrics
 
     # ---------------------------------------------------------------------------------------------------------------

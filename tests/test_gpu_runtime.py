@@ -98,3 +98,30 @@ def test_device_feeder_pinned_side_stream(cuda, tmp_path):
         assert torch.equal(a["token_x"], b["token_x"].cpu()) and torch.equal(a["token_y"], b["token_y"].cpu())
     cpu.close()
     gpu.close()
+
+
+@pytest.mark.parametrize("strategy", ["none", "revnet"])
+def test_hip_graph_step_matches_eager(cuda, strategy):
+    """the captured/replayed training step (both SM3 buffer parities, lr warm-up changing every step) tracks the
+    eager step as closely as two eager runs track each other (atomics make runs differ in the last bits)"""
+    pstate.set_mesh(pstate.Mesh())
+    cfg = dict(CFG, memory_reduction_strategy=strategy, learning_rate=1e-3,
+               learning_rate_config={"linear_warmup": {"final_step": 10}})
+    runs = []
+    for graphs in (False, False, True):
+        torch.manual_seed(0)
+        runs.append(Trainer(ModelParameter(dict(cfg, use_hip_graphs=graphs)), cuda))
+    losses = [[], [], []]
+    for i in range(7):
+        b = _batch(i, cuda)
+        for r, t in enumerate(runs):
+            losses[r].append(float(t.step(b)["loss"]))
+    torch.cuda.synchronize()
+    a, b, g = runs
+    assert len(g._graph["graphs"]) == 2 and g.global_step == a.global_step == 7
+    assert not hasattr(a, "_graph")
+    base = (a.store.master - b.store.master).abs().max().item()
+    diff = (a.store.master - g.store.master).abs().max().item()
+    assert diff <= 4 * base + 1e-5, (diff, base)
+    for la, lg in zip(losses[0], losses[2]):
+        assert abs(la - lg) < 2e-3 * abs(la), (losses[0], losses[2])
