@@ -367,10 +367,37 @@ struct RChunk { int t, row0, nrows, col0, ncols, vec; };
 // the segment's stage program on V consecutive elements of one row (gi: flat index; acc_last: the trailing-dim SM3
 // accumulators of those V columns; lead: min over the row's leading-dim accumulators). tm: running trailing-dim max
 // of these columns, rmax: running max of this lane's part of the row.
-template <int V>
+template <int V, int PROG>
 __device__ __forceinline__ void row_program(const ApplyArgs& a, const float* F, long long gi, const float* acc_last,
                                             float lead, float (&g)[V], const float (&w)[V], float (&tm)[V],
                                             float& rmax, float deb1, float deb2) {
+  if (PROG == 1) {   // the shipped chain, stages fixed at compile time: [norm clip] - sm3 - momentum - learning_rate
+    const Stage M = a.st[2];
+    const float lr = lr_of(a);
+    float al[V], m[V];
+    if (V == 4) {
+      const float4 v = *reinterpret_cast<const float4*>(acc_last);
+      const float4 mv = *reinterpret_cast<const float4*>(a.mom + gi);
+      al[0] = v.x; al[1] = v.y; al[2] = v.z; al[3] = v.w;
+      m[0] = mv.x; m[1] = mv.y; m[2] = mv.z; m[3] = mv.w;
+    } else {
+      al[0] = acc_last[0];
+      m[0] = a.mom[gi];
+    }
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      g[j] *= F[0];
+      const float nu = fminf(lead, al[j]) + g[j] * g[j];
+      tm[j] = fmaxf(tm[j], nu);
+      rmax = fmaxf(rmax, nu);
+      g[j] *= opt_rsqrt(nu);
+      m[j] = M.a * m[j] + g[j] * M.b;
+      g[j] = (M.c != 0.f ? g[j] + M.a * m[j] : m[j]) * lr;
+    }
+    if (V == 4) *reinterpret_cast<float4*>(a.mom + gi) = make_float4(m[0], m[1], m[2], m[3]);
+    else a.mom[gi] = m[0];
+    return;
+  }
       for (int s = 0; s < a.nst; ++s) {
     const Stage S = a.st[s];
     switch (S.op) {
@@ -492,7 +519,7 @@ __device__ __forceinline__ int fast_div(int n, int d, unsigned m) {
 // narrow rows (C / V lanes per row, a power of two <= 64): the block covers RW_NT * V / C whole rows per iteration,
 // each lane keeps the same V columns in every iteration (register running max of the trailing-dim accumulator),
 // the row max is a shuffle reduction over the row's lanes
-template <int V>
+template <int V, int PROG>
 __device__ __forceinline__ void rows_packed(const ApplyArgs& a, const OptTensor& T, const float* F, const RChunk& ck,
                                             float* tmax, bool sm3_on, float deb1, float deb2, float& s1, float& s2) {
   const int tid = threadIdx.x;
@@ -539,7 +566,7 @@ __device__ __forceinline__ void rows_packed(const ApplyArgs& a, const OptTensor&
 #pragma unroll
         for (int j = 0; j < V; ++j) g[j] *= a.grad_scale;
       }
-      row_program<V>(a, F, gi, acc_last, lead, g, w, tm, rmax, deb1, deb2);
+      row_program<V, PROG>(a, F, gi, acc_last, lead, g, w, tm, rmax, deb1, deb2);
       finish_elems<V>(a, T, gi, g, w, s1, s2);
     }
     if (sm3_on && last > 0) {
@@ -560,7 +587,7 @@ __device__ __forceinline__ void rows_packed(const ApplyArgs& a, const OptTensor&
   }
 }
 
-template <int V>
+template <int V, int PROG>
 __device__ __forceinline__ void rows_body(const ApplyArgs& a, const OptTensor& T, const float* F, const RChunk& ck,
                                           float* tmax, bool sm3_on, float deb1, float deb2, float& s1, float& s2) {
   const int tid = threadIdx.x, lane = tid & 63;
@@ -604,7 +631,7 @@ __device__ __forceinline__ void rows_body(const ApplyArgs& a, const OptTensor& T
       float tmx[V];
 #pragma unroll
       for (int j = 0; j < V; ++j) tmx[j] = sm3_on ? tmax[c + j] : 0.f;
-      row_program<V>(a, F, gi, acc_last + c, lead, g, w, tmx, rmax, deb1, deb2);
+      row_program<V, PROG>(a, F, gi, acc_last + c, lead, g, w, tmx, rmax, deb1, deb2);
       if (sm3_on) {
 #pragma unroll
         for (int j = 0; j < V; ++j) tmax[c + j] = tmx[j];
@@ -626,6 +653,7 @@ __device__ __forceinline__ void rows_body(const ApplyArgs& a, const OptTensor& T
       }
 }
 
+template <int PROG>
 __global__ __launch_bounds__(RW_NT) void opt_rows_kernel(ApplyArgs a, const RChunk* chunks) {
   __shared__ float tmax[RW_COLS];
   const RChunk ck = chunks[blockIdx.x];
@@ -638,11 +666,11 @@ __global__ __launch_bounds__(RW_NT) void opt_rows_kernel(ApplyArgs a, const RChu
   float s1 = 0.f, s2 = 0.f;
   // vec bit 0: float4 (offset and C multiples of 4); bit 1: narrow rows (C / V lanes per row, power of two <= 64)
   if (ck.vec & 2) {
-    if (ck.vec & 1) rows_packed<4>(a, T, F, ck, tmax, sm3_on, deb1, deb2, s1, s2);
-    else rows_packed<1>(a, T, F, ck, tmax, sm3_on, deb1, deb2, s1, s2);
+    if (ck.vec & 1) rows_packed<4, PROG>(a, T, F, ck, tmax, sm3_on, deb1, deb2, s1, s2);
+    else rows_packed<1, PROG>(a, T, F, ck, tmax, sm3_on, deb1, deb2, s1, s2);
   } else {
-    if (ck.vec & 1) rows_body<4>(a, T, F, ck, tmax, sm3_on, deb1, deb2, s1, s2);
-    else rows_body<1>(a, T, F, ck, tmax, sm3_on, deb1, deb2, s1, s2);
+    if (ck.vec & 1) rows_body<4, PROG>(a, T, F, ck, tmax, sm3_on, deb1, deb2, s1, s2);
+    else rows_body<1, PROG>(a, T, F, ck, tmax, sm3_on, deb1, deb2, s1, s2);
   }
   if (a.emit_stats) {
     __shared__ float red[4];
@@ -817,6 +845,14 @@ OBST_API int obst_opt_apply_rows(const ObstOptDesc* d, const void* rchunks, int 
   for (int i = 0; i < d->nst; ++i)
     if (d->stages[4 * i] == OP_ADAFACTOR || d->stages[4 * i] == OP_ADAFACTOR_CLIP) return -2;
   if (nrchunks <= 0) return 0;
-  hipLaunchKernelGGL(opt_rows_kernel, dim3(nrchunks), dim3(RW_NT), 0, s, apply_args(d), (const RChunk*)rchunks);
+  const int* st = d->stages;
+  const bool shipped = d->nst == 4 && d->final_seg && !d->emit_stats && !d->uin &&
+                       (st[0] == OP_ADAPTIVE_CLIP || st[0] == OP_L2_CLIP || st[0] == OP_GLOBAL_L2_CLIP ||
+                        st[0] == OP_SCALE) &&
+                       st[4] == OP_SM3 && st[8] == OP_MOMENTUM && st[12] == OP_LR;
+  if (shipped)
+    hipLaunchKernelGGL(opt_rows_kernel<1>, dim3(nrchunks), dim3(RW_NT), 0, s, apply_args(d), (const RChunk*)rchunks);
+  else
+    hipLaunchKernelGGL(opt_rows_kernel<0>, dim3(nrchunks), dim3(RW_NT), 0, s, apply_args(d), (const RChunk*)rchunks);
   return (int)hipGetLastError();
 }
