@@ -161,7 +161,8 @@ __global__ __launch_bounds__(NTH) void norm_bwd_kernel(const bf16_t* __restrict_
                                                        bf16_t* __restrict__ DX, float* __restrict__ dscale,
                                                        float* __restrict__ dshift, long long rows, int F, int groups,
                                                        int Ffull, float* __restrict__ partial_out,
-                                                       const float* __restrict__ ext_dsum) {
+                                                       const float* __restrict__ ext_dsum,
+                                                       const bf16_t* __restrict__ R) {
   constexpr int RPW = 64 / LPR;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* red_s = reinterpret_cast<float*>(smem);           // [4 waves][F] dscale partials, then dshift
@@ -224,11 +225,18 @@ __global__ __launch_bounds__(NTH) void norm_bwd_kernel(const bf16_t* __restrict_
     for (int c = 0; c < NCH; ++c) {
       const int col = c * LPR * 8 + sl * 8;
       if (col >= F) continue;
+      float r[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (R) {   // the block's residual-input gradient, summed here instead of in a separate elementwise pass
+        const uint4 u = *reinterpret_cast<const uint4*>(R + row * F + col);
+        const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { r[2 * j] = bf2f(w[j] & 0xffff); r[2 * j + 1] = bf2f(w[j] >> 16); }
+      }
       uint32_t o[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        o[j] = pack_bf16x2(rstd * (dy[c][2 * j] - m1 - x[c][2 * j] * m2),
-                           rstd * (dy[c][2 * j + 1] - m1 - x[c][2 * j + 1] * m2));
+        o[j] = pack_bf16x2(rstd * (dy[c][2 * j] - m1 - x[c][2 * j] * m2) + r[2 * j],
+                           rstd * (dy[c][2 * j + 1] - m1 - x[c][2 * j + 1] * m2) + r[2 * j + 1]);
       *reinterpret_cast<uint4*>(DX + row * F + col) = make_uint4(o[0], o[1], o[2], o[3]);
     }
   }
@@ -286,6 +294,7 @@ struct ObstNormDesc {
   const void* DY; void* DX; float* dscale; float* dshift;
   float* partial; const float* ext;   // TP path
   long long rows; int F; int groups; int Ffull; float eps;
+  const void* R;                      // backward: gradient added to DX (residual input of the block) or null
 };
 
 #define NORM_DISPATCH_L(KERNEL, LPR, GRID, LDSB, ...)                                               \
@@ -339,6 +348,7 @@ OBST_API int obst_norm_bwd(const ObstNormDesc* d, hipStream_t st) {
     grid = grid < q ? q : grid / q * q;
   }
   NORM_DISPATCH(norm_bwd_kernel, dim3(grid), lds, (const bf16_t*)d->X, (const bf16_t*)d->DY, d->scale, d->stats,
-                (bf16_t*)d->DX, d->dscale, d->dshift, d->rows, d->F, d->groups, d->Ffull, d->partial, d->ext);
+                (bf16_t*)d->DX, d->dscale, d->dshift, d->rows, d->F, d->groups, d->Ffull, d->partial, d->ext,
+                (const bf16_t*)d->R);
   return (int)hipGetLastError();
 }

@@ -22,6 +22,12 @@ def run_layers(builder: Builder, layers: typing.List[str], x: Act, residual: typ
     consumed = False
     seen: typing.Dict[str, int] = {}
     n = len(layers)
+    # pre-norm block whose last layer takes the residual in its epilogue: that layer's residual gradient goes to
+    # the opening norm (same input tensor x), which adds it inside its backward kernel (F.ResidualGrad)
+    carrier = None
+    if (residual is not None and residual is x and n > 1 and layers[0].split('-')[0] == "norm"
+            and layers[-1].split('-')[0] in _FUSABLE_LAST):
+        carrier = F.ResidualGrad()
     for idx, layer in enumerate(layers, 1):
         name, *extras = layer.split('-')
         if name not in LAYER_FUNCTIONS:
@@ -33,6 +39,9 @@ def run_layers(builder: Builder, layers: typing.List[str], x: Act, residual: typ
         builder.shared.begin_layer((builder.config_idx, name, args.fn_occurrence))
         if idx == n and residual is not None and name in _FUSABLE_LAST:
             args.residual = residual
+            args.residual_carrier = carrier
+        if idx == 1 and carrier is not None:
+            args.norm_carrier = carrier
         with builder.scope(name + '_'):
             out = LAYER_FUNCTIONS[name](args)
         consumed = consumed or getattr(args, "residual_consumed", False)

@@ -237,7 +237,8 @@ def feed_forward(args: BlockArgs) -> Act:
             w2 = _scoped(a_out, "linear", orthogonal_var, a_out, list(old2) + list(new2), list(old2))
             res = args.residual if (args.residual is not None and args.residual.dims == odims) else None
             y = F.ffn(x.t, w1, w2, x.dims, D.deduplicate(old1 + new1), mdims, D.deduplicate(old2 + new2), odims,
-                      act_in, residual=res.t if res is not None else None)
+                      act_in, residual=res.t if res is not None else None,
+                      carrier=getattr(args, "residual_carrier", None) if res is not None else None)
             if res is not None:
                 args.residual_consumed = True
             return Act(y, odims)
@@ -353,7 +354,8 @@ def norm(args: BlockArgs, feature_shape: typing.Optional[typing.List[Dim]] = Non
         Fsz = int(math.prod(d.size for d in normalized))
         groups = p.head_dim.size if group else 1
         tp_stats = (not group) and p.head_dim in normalized and pstate.tp_size() > 1
-        y = F.norm(x.t, scale, shift, Fsz, groups, tp_stats=tp_stats)
+        y = F.norm(x.t, scale, shift, Fsz, groups, tp_stats=tp_stats,
+                   carrier=getattr(args, "norm_carrier", None))
         return Act(y, x.dims)
     # general path (torch autograd)
     axes = [x.dims.index(d) for d in normalized]
@@ -465,7 +467,8 @@ def attention(args: BlockArgs) -> Act:
         try:
             y = F.dot_attention(x.t, w_in, ws[0], ws[1], ws[2], x.dims, D.deduplicate(old1 + new1), base_dims,
                                 D.deduplicate(old2 + new2), act_in, scale, causal, geo,
-                                residual=res.t if res is not None else None)
+                                residual=res.t if res is not None else None,
+                                carrier=getattr(args, "residual_carrier", None) if res is not None else None)
             if res is not None:
                 args.residual_consumed = True
             return Act(y, x.dims)

@@ -56,7 +56,7 @@ class AttnDesc(ctypes.Structure):
 class NormDesc(ctypes.Structure):
     _fields_ = [("X", c_p), ("scale", c_p), ("shift", c_p), ("Y", c_p), ("stats", c_p),
                 ("DY", c_p), ("DX", c_p), ("dscale", c_p), ("dshift", c_p), ("partial", c_p), ("ext", c_p),
-                ("rows", c_ll), ("F", c_i), ("groups", c_i), ("Ffull", c_i), ("eps", c_f)]
+                ("rows", c_ll), ("F", c_i), ("groups", c_i), ("Ffull", c_i), ("eps", c_f), ("R", c_p)]
 
 
 class EwDesc(ctypes.Structure):

@@ -242,7 +242,7 @@ def tp_copy(x):
 # fused feed-forward: y = act(x W1) W2 (+ residual)   -- K01 x4 with fused epilogues, no separate elementwise pass
 class _FFN(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w1, w2, p1: LinearPlan, p2: LinearPlan, act, residual):
+    def forward(ctx, x, w1, w2, p1: LinearPlan, p2: LinearPlan, act, residual, carrier=None):
         xc = x.contiguous()
         z = _empty(p1.canon_o_shape, xc)
         a = _empty(p1.canon_o_shape, xc) if act else z
@@ -253,6 +253,7 @@ class _FFN(torch.autograd.Function):
         _fwd_gemm(a, w2, y, p2, R=residual.contiguous() if residual is not None else None)
         ctx.save_for_backward(xc, w1, w2, z, a if act else None)
         ctx.p1, ctx.p2, ctx.act, ctx.has_res = p1, p2, act, residual is not None
+        ctx.carrier = carrier
         return y
 
     @staticmethod
@@ -272,16 +273,18 @@ class _FFN(torch.autograd.Function):
         g1, m1 = _acc_grad(w1)
         _wgrad_gemm(xc, dz, g1, p1)
         _done(w1)
-        return (dx, None if m1 else g1.to(w1.dtype), None if m2 else g2.to(w2.dtype), None, None, None,
-                dy if ctx.has_res else None)
+        dres = dy if ctx.has_res else None
+        if dres is not None and ctx.carrier is not None:   # handed to the block's opening norm (ResidualGrad)
+            ctx.carrier.grad, dres = dres, None
+        return (dx, None if m1 else g1.to(w1.dtype), None if m2 else g2.to(w2.dtype), None, None, None, dres, None)
 
 
-def ffn(x, w1, w2, xdims, w1dims, mdims, w2dims, odims, act, residual=None):
+def ffn(x, w1, w2, xdims, w1dims, mdims, w2dims, odims, act, residual=None, carrier=None):
     p1 = linear_plan(tuple(xdims), tuple(w1dims), tuple(mdims))
     p2 = linear_plan(tuple(mdims), tuple(w2dims), tuple(odims))
     if p1.x_perm is not None or p1.o_perm is not None or p2.x_perm is not None or p2.o_perm is not None:
         raise NotImplementedError("fused FFN needs canonical layouts")
-    return _FFN.apply(x, w1, w2, p1, p2, act, residual)
+    return _FFN.apply(x, w1, w2, p1, p2, act, residual, carrier)
 
 
 # ================================================================================================================
@@ -290,7 +293,7 @@ def ffn(x, w1, w2, xdims, w1dims, mdims, w2dims, odims, act, residual=None):
 class _DotAttention(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w_in, w_k, w_q, w_v, p_in: LinearPlan, p_out: LinearPlan, act, scale, causal, residual,
-                geo):
+                geo, carrier=None):
         B, S, H, D = geo
         xc = x.contiguous()
         base = _empty(p_in.canon_o_shape, xc)
@@ -315,6 +318,7 @@ class _DotAttention(torch.autograd.Function):
             out = o
         ctx.save_for_backward(xc, w_in, w_k, w_q, w_v, z, base, kqv, o, lse)
         ctx.cfg = (p_in, p_out, act, scale, causal, geo, residual is not None, T, Nq)
+        ctx.carrier = carrier
         return out
 
     @staticmethod
@@ -359,8 +363,11 @@ class _DotAttention(torch.autograd.Function):
         g, m = _acc_grad(w_in)
         _wgrad_gemm(xc, dbase, g, p_in)
         _done(w_in)
+        dres = dout if has_res else None
+        if dres is not None and ctx.carrier is not None:   # handed to the block's opening norm (ResidualGrad)
+            ctx.carrier.grad, dres = dres, None
         return (dx, None if m else g.to(w_in.dtype), outs[0], outs[1], outs[2], None, None, None, None, None,
-                dout if has_res else None, None)
+                dres, None, None)
 
 
 def _qkv_fwd(base, ws, out, p: LinearPlan):
@@ -385,10 +392,10 @@ def _qkv_fwd(base, ws, out, p: LinearPlan):
 
 
 def dot_attention(x, w_in, w_k, w_q, w_v, xdims, w_in_dims, base_dims, w_out_dims, act, scale, causal, geo,
-                  residual=None):
+                  residual=None, carrier=None):
     p_in = linear_plan(tuple(xdims), tuple(w_in_dims), tuple(base_dims))
     p_out = linear_plan(tuple(base_dims), tuple(w_out_dims), tuple(xdims))
-    return _DotAttention.apply(x, w_in, w_k, w_q, w_v, p_in, p_out, act, scale, causal, residual, geo)
+    return _DotAttention.apply(x, w_in, w_k, w_q, w_v, p_in, p_out, act, scale, causal, residual, geo, carrier)
 
 
 # ================================================================================================================
@@ -468,9 +475,20 @@ def attention_core(q, k, v, scale: float, causal: bool):
 
 # ================================================================================================================
 # norm
+class ResidualGrad:
+    """Carries a pre-norm block's residual-input gradient from the fused op that consumed the residual (FFN /
+    attention epilogue) to the norm that opens the block on the same input tensor: the norm backward adds it into dx
+    inside its kernel, so autograd does not sum the two gradients of the block input with a separate elementwise
+    pass. The consumer's backward always runs first (the norm's output feeds it)."""
+    __slots__ = ("grad",)
+
+    def __init__(self):
+        self.grad = None
+
+
 class _Norm(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, scale, shift, F, groups, tp_stats):
+    def forward(ctx, x, scale, shift, F, groups, tp_stats, carrier=None):
         xc = x.contiguous()
         rows = xc.numel() // F
         y = torch.empty_like(xc)
@@ -492,6 +510,7 @@ class _Norm(torch.autograd.Function):
         ctx.save_for_backward(xc, scale, shift, stats)
         ctx.cfg = (F, groups, rows, Ffull, tp_stats)
         ctx.sm32 = sm32
+        ctx.carrier = carrier
         return y
 
     @staticmethod
@@ -508,16 +527,20 @@ class _Norm(torch.autograd.Function):
             raw.norm_bwd(xc, dy, ctx.sm32, stats, None, None, None, rows, F, groups, Ffull, partial=part)
             pstate.tp_all_reduce(part)
             ext = part
-        raw.norm_bwd(xc, dy, ctx.sm32, stats, dx, gsc, gsh, rows, F, groups, Ffull, ext_dsum=ext)
+        R = None
+        if ctx.carrier is not None and ctx.carrier.grad is not None:
+            R = ctx.carrier.grad.contiguous()
+            ctx.carrier.grad = None
+        raw.norm_bwd(xc, dy, ctx.sm32, stats, dx, gsc, gsh, rows, F, groups, Ffull, ext_dsum=ext, R=R)
         for t in (scale, shift):
             if t is not None:
                 _done(t)
         return (dx, None if msc else gsc.view(scale.shape).to(scale.dtype),
-                None if msh else gsh.view(shift.shape).to(shift.dtype), None, None, None)
+                None if msh else gsh.view(shift.shape).to(shift.dtype), None, None, None, None)
 
 
-def norm(x, scale, shift, F: int, groups: int, tp_stats: bool = False):
-    return _Norm.apply(x, scale, shift, F, groups, tp_stats)
+def norm(x, scale, shift, F: int, groups: int, tp_stats: bool = False, carrier: typing.Optional[ResidualGrad] = None):
+    return _Norm.apply(x, scale, shift, F, groups, tp_stats, carrier)
 
 
 # ================================================================================================================

@@ -337,9 +337,10 @@ def norm_partial(x, out, rows: int, F: int):
 
 
 def norm_bwd(x, dy, scale, stats, dx, dscale, dshift, rows: int, F: int, groups: int, Ffull: int = 0,
-             partial=None, ext_dsum=None):
+             partial=None, ext_dsum=None, R=None):
     """dx (and parameter grads accumulated into fp32 dscale/dshift). With `partial` set, only the per-row partial
-    sums (sum dxh, sum dxh*xh) are written (TP phase 1); phase 2 passes them back as `ext_dsum`."""
+    sums (sum dxh, sum dxh*xh) are written (TP phase 1); phase 2 passes them back as `ext_dsum`. R (same layout as
+    dx) is added to dx."""
     if x.device.type == "meta":
         return None
     Ffull = Ffull or F
@@ -352,8 +353,12 @@ def norm_bwd(x, dy, scale, stats, dx, dscale, dshift, rows: int, F: int, groups:
         for nm, t in (("scale", scale), ("dscale", dscale), ("dshift", dshift)):
             if t is not None:
                 _need(t, groups * F - 1, nm)
+        if R is not None:
+            if R.dtype != torch.bfloat16 or not R.is_contiguous():
+                raise L.KernelError("norm_bwd residual gradient must be contiguous bf16")
+            _need(R, rows * F - 1, "R")
         d = L.NormDesc(x.data_ptr(), L.ptr(scale), 0, 0, stats.data_ptr(), dy.data_ptr(), L.ptr(dx), L.ptr(dscale),
-                       L.ptr(dshift), L.ptr(partial), L.ptr(ext_dsum), rows, F, groups, Ffull, EPS)
+                       L.ptr(dshift), L.ptr(partial), L.ptr(ext_dsum), rows, F, groups, Ffull, EPS, L.ptr(R))
         L.check(L.lib().obst_norm_bwd(d, L.stream_ptr()), "norm_bwd")
         return
     xv = _f(x.reshape(rows, F))
@@ -374,7 +379,10 @@ def norm_bwd(x, dy, scale, stats, dx, dscale, dshift, rows: int, F: int, groups:
         s1, s2 = ext_dsum.view(rows, 2)[:, 0:1], ext_dsum.view(rows, 2)[:, 1:2]
     else:
         s1, s2 = dxh.sum(-1, keepdim=True), (dxh * xh).sum(-1, keepdim=True)
-    dx.reshape(rows, F).copy_(st[:, 1:2] * (dxh - s1 / Ffull - xh * s2 / Ffull))
+    out = st[:, 1:2] * (dxh - s1 / Ffull - xh * s2 / Ffull)
+    if R is not None:
+        out = out + _f(R.reshape(rows, F))
+    dx.reshape(rows, F).copy_(out)
 
 
 # ----------------------------------------------------------------------------------------------------------------
