@@ -150,6 +150,7 @@ struct AttnArgs {
   long long ld;   // token stride (elements), usually H*D
   float scale;
   int causal;
+  int prio;       // s_setprio(1) around the MFMA clusters: bit 0 dK/dV kernel (default on: -2 %), bit 1 dQ (+1 %: off)
 };
 
 // ----------------------------------------------------------------------------------------------------------------
@@ -350,7 +351,7 @@ template <int D, bool MASK>
 __device__ __forceinline__ void dq_tile(const char* sK, const char* sV, const bf16x8_t (&qf)[2][Geo<D>::DS],
                                         const bf16x8_t (&df)[2][Geo<D>::DS], const float (&lse2)[2],
                                         const float (&dlt)[2], f32x4_t (&acc)[Geo<D>::DT][2], int k0, int qw, int S,
-                                        int causal, float c2, int lane) {
+                                        int causal, float c2, int lane, int prio = 0) {
   using G = Geo<D>;
   const int g = lane >> 4, i = lane & 15;
 #pragma unroll
@@ -363,6 +364,7 @@ __device__ __forceinline__ void dq_tile(const char* sK, const char* sV, const bf
         sc[qt][kk] = f32x4_t{0.f, 0.f, 0.f, 0.f};
         dp[qt][kk] = f32x4_t{-dlt[qt], -dlt[qt], -dlt[qt], -dlt[qt]};
       }
+    if (prio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int ds = 0; ds < G::DS; ++ds) {
 #pragma unroll
@@ -377,6 +379,7 @@ __device__ __forceinline__ void dq_tile(const char* sK, const char* sV, const bf
         }
       }
     }
+    if (prio) __builtin_amdgcn_s_setprio(0);
     bf16x8_t sf[2];
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) {
@@ -395,6 +398,7 @@ __device__ __forceinline__ void dq_tile(const char* sK, const char* sV, const bf
         }
       sf[qt] = pack_p(sc[qt][0], sc[qt][1]);
     }
+    if (prio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int dt = 0; dt < G::DT; ++dt) {
       bf16x8_t kf = tr_frag<D>(sK, st * 32, dt * 16, lane);
@@ -402,6 +406,7 @@ __device__ __forceinline__ void dq_tile(const char* sK, const char* sV, const bf
       for (int qt = 0; qt < 2; ++qt)
         acc[dt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, sf[qt], acc[dt][qt], 0, 0, 0);
     }
+    if (prio) __builtin_amdgcn_s_setprio(0);
   }
 }
 
@@ -469,8 +474,8 @@ __global__ __launch_bounds__(NTH, 2) void attn_bwd_dq_kernel(AttnArgs a) {
     }
     if (!(a.causal && k0 > qw + 31)) {
       const bool need_mask = (a.causal && k0 + 63 > qw) || k0 + 64 > a.S;
-      if (need_mask) dq_tile<D, true>(sK, sV, qf, df, lse2, dlt, acc, k0, qw, a.S, a.causal, c2, lane);
-      else dq_tile<D, false>(sK, sV, qf, df, lse2, dlt, acc, k0, qw, a.S, a.causal, c2, lane);
+      if (need_mask) dq_tile<D, true>(sK, sV, qf, df, lse2, dlt, acc, k0, qw, a.S, a.causal, c2, lane, a.prio & 2);
+      else dq_tile<D, false>(sK, sV, qf, df, lse2, dlt, acc, k0, qw, a.S, a.causal, c2, lane, a.prio & 2);
     }
     vm_wait<0>();   // staged tiles (asm LDS-DMA: the compiler does not track them) have landed
     __syncthreads();
@@ -495,7 +500,7 @@ template <int D, bool MASK>
 __device__ __forceinline__ void dkv_chunk(const char* sQ, const char* sD, const float* sL, const float* sDl,
                                           const bf16x8_t (&kf)[Geo<D>::DS], const bf16x8_t (&vf)[Geo<D>::DS],
                                           f32x4_t (&dk)[Geo<D>::DT], f32x4_t (&dv)[Geo<D>::DT], int q0, int key, int S,
-                                          int causal, float c2, int lane) {
+                                          int causal, float c2, int lane, int prio) {
   using G = Geo<D>;
   const int g = lane >> 4;
   f32x4_t sc[4], dp[4];
@@ -505,6 +510,7 @@ __device__ __forceinline__ void dkv_chunk(const char* sQ, const char* sD, const 
     sc[qt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
     dp[qt] = f32x4_t{-dl.x, -dl.y, -dl.z, -dl.w};
   }
+  if (prio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
   for (int ds = 0; ds < G::DS; ++ds) {
 #pragma unroll
@@ -515,6 +521,7 @@ __device__ __forceinline__ void dkv_chunk(const char* sQ, const char* sD, const 
       dp[qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, vf[ds], dp[qt], 0, 0, 0);
     }
   }
+  if (prio) __builtin_amdgcn_s_setprio(0);
   // sc[qt][v] = S[q = q0 + qt*16 + 4g + v][key]
 #pragma unroll
   for (int qt = 0; qt < 4; ++qt) {
@@ -531,6 +538,7 @@ __device__ __forceinline__ void dkv_chunk(const char* sQ, const char* sD, const 
       dp[qt][v] = pv * dp[qt][v];
     }
   }
+  if (prio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
   for (int st = 0; st < 2; ++st) {
     const bf16x8_t pb = pack_p(sc[2 * st], sc[2 * st + 1]);
@@ -543,6 +551,7 @@ __device__ __forceinline__ void dkv_chunk(const char* sQ, const char* sD, const 
       dk[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qtr, sb, dk[dt], 0, 0, 0);
     }
   }
+  if (prio) __builtin_amdgcn_s_setprio(0);
 }
 
 // ----------------------------------------------------------------------------------------------------------------
@@ -600,8 +609,8 @@ __global__ __launch_bounds__(NTH, 2) void attn_bwd_dkv_kernel(AttnArgs a) {
     if (c + 1 < nqc) stage(smem + ((c + 1) & 1) * STAGE, q0 + QC);
     if (!(a.causal && q0 + QC - 1 < kw)) {  // every query of this chunk precedes this wave's keys
       const bool need_mask = (a.causal && q0 < kw + 15) || q0 + QC > a.S || kw + 16 > a.S;
-      if (need_mask) dkv_chunk<D, true>(sQ, sD, sL, sDl, kf, vf, dk, dv, q0, key, a.S, a.causal, c2, lane);
-      else dkv_chunk<D, false>(sQ, sD, sL, sDl, kf, vf, dk, dv, q0, key, a.S, a.causal, c2, lane);
+      if (need_mask) dkv_chunk<D, true>(sQ, sD, sL, sDl, kf, vf, dk, dv, q0, key, a.S, a.causal, c2, lane, a.prio & 1);
+      else dkv_chunk<D, false>(sQ, sD, sL, sDl, kf, vf, dk, dv, q0, key, a.S, a.causal, c2, lane, a.prio & 1);
     }
     vm_wait<0>();   // staged tiles (asm LDS-DMA: the compiler does not track them) have landed
     __syncthreads();
@@ -1228,6 +1237,8 @@ static bool fill(AttnArgs& a, const ObstAttnDesc* d) {
   a.Oout = (bf16_t*)d->Oout; a.dQ = (bf16_t*)d->dQ; a.dK = (bf16_t*)d->dK; a.dV = (bf16_t*)d->dV;
   a.LSE = d->LSE; a.delta = d->delta;
   a.B = d->B; a.S = d->S; a.H = d->H; a.ld = d->ld; a.scale = d->scale; a.causal = d->causal;
+  static const int prio = [] { const char* e = getenv("OBST_ATTN_PRIO"); return e ? atoi(e) : 1; }();
+  a.prio = prio;
   return d->B > 0 && d->S > 0 && d->H > 0 && d->ld % 8 == 0 && d->ld >= (long long)d->H * d->D;
 }
 
