@@ -850,168 +850,6 @@ __global__ __launch_bounds__(NTH, 2) void attn_fwd32_kernel(AttnArgs a) {
 }
 
 // ----------------------------------------------------------------------------------------------------------------
-// Forward v3: software-pipelined over 32-key sub-tiles. Iteration j issues the QKᵀ MFMAs of sub-tile j+1 (into a
-// second score register block) while the VALU does the softmax of sub-tile j, then P·V of sub-tile j -- each wave
-// always has independent MFMA work beside its own softmax instead of relying on the partner wave. K and V live in
-// separate double buffers with staggered lifetimes so one barrier per sub-tile suffices and each 16 KiB DMA has two
-// sub-tile iterations to land:
-//   iteration 2t   : wait V(t), barrier, DMA V(t+1) -> Vbuf[(t+1)&1];  QK(2t+1) on K(t), softmax+PV(2t) on V(t)
-//   iteration 2t+1 : wait K(t+1), barrier, DMA K(t+2) -> Kbuf[t&1];     QK(2t+2) on K(t+1), softmax+PV(2t+1) on V(t)
-// (WAR: K(t) was last read by QK(2t+1) in iteration 2t, V(t-1) by PV(2t-1) in iteration 2t-1, both before the
-// barrier that precedes their buffer's refill; RAW: the counted vmcnt leaves only the most recent DMA in flight.)
-__device__ __forceinline__ void qk_sub(f32x16_t& sc, const char* sK, int sub, const bf16x8_t (&qf)[8], int lane) {
-  const int h = lane >> 5, n = lane & 31;
-  sc = f32x16_t{};
-#pragma unroll
-  for (int ks = 0; ks < 8; ++ks) {
-    const bf16x8_t kf = *reinterpret_cast<const bf16x8_t*>(sK + sub * 32 * 256 + lds_off<128>(n, ks * 2 + h));
-    sc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], sc, 0, 0, 0);
-  }
-}
-
-template <bool MASK>
-__device__ __forceinline__ void softmax_pv_sub(f32x16_t& sc, const char* sV, int sub, f32x16_t (&o)[4], float& m,
-                                               float& l, int key0, int q, int S, float c2, int lane) {
-  const int h = lane >> 5, hi = (lane >> 4) & 1, i16 = lane & 15, qq = i16 >> 2, pp = i16 & 3;
-  float mx = -INFINITY;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    if (MASK) {
-      const int key = key0 + 8 * (r >> 2) + 4 * h + (r & 3);
-      sc[r] = (key >= S || key > q) ? -INFINITY : sc[r];
-    }
-    mx = fmaxf(mx, sc[r]);
-  }
-  mx = xh_max(mx);
-  const float ms = mx * c2;
-  const bool bump = ms > m + RESCALE_TH;
-  if (__builtin_amdgcn_ballot_w64(bump)) {
-    const float mn = bump ? ms : m;
-    const float alpha = fexp2(m - mn);
-    l *= alpha;
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
-    m = mn;
-  }
-  const float nm = -m;
-  float rs = 0.f;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const float p = fexp2(__builtin_fmaf(sc[r], c2, nm));
-    sc[r] = p;
-    rs += p;
-  }
-  l += rs;
-  const int r0 = 4 * h + qq, r1 = r0 + 8;
-#pragma unroll
-  for (int st = 0; st < 2; ++st) {
-    const bf16x8_t pf = pack8(sc, 8 * st);
-    const int kb = (sub * 32 + 16 * st) * 256;
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      const int c = (dt * 32 + hi * 16 + 4 * pp) >> 3;
-      const int o0 = r0 * 256 + ((c ^ swz<128>(r0)) << 4) + ((pp & 1) << 3);
-      const int o1 = r1 * 256 + ((c ^ swz<128>(r1)) << 4) + ((pp & 1) << 3);
-      o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_pair(sV, o0 + kb, o1 + kb), pf, o[dt], 0, 0, 0);
-    }
-  }
-}
-
-__global__ __launch_bounds__(NTH, 2) void attn_fwd3_kernel(AttnArgs a) {
-  constexpr int D = 128;
-  constexpr int TILE = 64 * 256;
-  extern __shared__ __attribute__((aligned(16))) char smem[];   // Kbuf[2] then Vbuf[2]
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, n = lane & 31;
-  const int nx = (a.S + 127) / 128;
-  int bx, bh;
-  attn_block(nx, bx, bh);
-  const int b = bh / a.H, hd = bh % a.H;
-  const int qblk = (a.causal ? (nx - 1 - bx) : bx) * 128;
-  const int qw = qblk + w * 32;
-  const int q = qw + n;
-  const long long base = (long long)b * a.S * a.ld + hd * D;
-  const bf16_t* Kb = a.K + base;
-  const bf16_t* Vb = a.V + base;
-  const int kend = a.causal ? min(a.S, qblk + 128) : a.S;
-  const int ntile = (kend + 63) / 64, nsub = (kend + 31) / 32;
-  const int wu = __builtin_amdgcn_readfirstlane(w);
-  unsigned soff[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int row = (wu + 4 * i) * 4 + (lane >> 4);
-    soff[i] = (unsigned)(row * (int)a.ld + (((lane & 15) ^ swz<128>(row)) << 3)) * 2u;
-  }
-  char* Kbuf = smem;
-  char* Vbuf = smem + 2 * TILE;
-  auto stage = [&](char* buf, const bf16_t* src, int t) {
-    const int k0 = __builtin_amdgcn_readfirstlane(t * 64);
-    if (k0 + 64 <= a.S) stage_full64(buf, src + (long long)k0 * a.ld, soff, wu);
-    else stage_rows64_asm(buf, src + (long long)k0 * a.ld, a.ld, a.S - k0, wu, lane);
-  };
-  stage(Kbuf, Kb, 0);
-  stage(Vbuf, Vb, 0);
-  if (ntile > 1) stage(Kbuf + TILE, Kb, 1);
-  bf16x8_t qf[8];
-#pragma unroll
-  for (int ks = 0; ks < 8; ++ks) qf[ks] = load_frag_g(a.Q + base + (long long)q * a.ld + ks * 16 + 8 * h, q < a.S);
-#pragma unroll
-  for (int ks = 0; ks < 8; ++ks) asm volatile("" ::"v"(qf[ks]));
-  f32x16_t o[4];
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt) o[dt] = f32x16_t{};
-  float m = NEG_BIG, l = 0.f;
-  const float c2 = a.scale * LOG2E;
-  const bool causal = a.causal;
-  vm_wait<0>();
-  __syncthreads();
-  f32x16_t sc, sn;
-  if (!(causal && 0 > qw + 31)) qk_sub(sc, Kbuf, 0, qf, lane);
-  bool pendK = false, pendV = false;
-  for (int j = 0; j < nsub; ++j) {
-    const int t = j >> 1, half = j & 1;
-    if (!half) {                         // even: V(t) must have landed; refill Vbuf[(t+1)&1] with V(t+1)
-      if (j > 0) {
-        if (pendK) vm_wait<4>(); else vm_wait<0>();
-        __syncthreads();
-      }
-      pendV = t + 1 < ntile;
-      if (pendV) stage(Vbuf + ((t + 1) & 1) * TILE, Vb, t + 1);
-    } else {                             // odd: K(t+1) must have landed; refill Kbuf[t&1] with K(t+2)
-      if (pendV) vm_wait<4>(); else vm_wait<0>();
-      __syncthreads();
-      pendK = t + 2 < ntile;
-      if (pendK) stage(Kbuf + (t & 1) * TILE, Kb, t + 2);
-    }
-    const int jn = j + 1;
-    const int key0 = j * 32;
-    const bool next_live = jn < nsub && !(causal && jn * 32 > qw + 31);
-    if (next_live) qk_sub(sn, Kbuf + ((jn >> 1) & 1) * TILE, jn & 1, qf, lane);
-    if (!(causal && key0 > qw + 31)) {
-      const char* sV = Vbuf + (t & 1) * TILE;
-      const bool need_mask = (causal && key0 + 31 > qw) || key0 + 32 > a.S;
-      if (need_mask) softmax_pv_sub<true>(sc, sV, half, o, m, l, key0, causal ? q : 0x7fffffff, a.S, c2, lane);
-      else softmax_pv_sub<false>(sc, sV, half, o, m, l, key0, q, a.S, c2, lane);
-    }
-    sc = sn;
-  }
-  l = xh_sum(l);
-  if (q < a.S) {
-    const float inv = 1.f / l;
-    bf16_t* orow = a.Oout + base + (long long)q * a.ld;
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const int d = dt * 32 + 8 * g4 + 4 * h;
-        *reinterpret_cast<uint2*>(orow + d) =
-            make_uint2(pack_bf16x2(o[dt][4 * g4] * inv, o[dt][4 * g4 + 1] * inv),
-                       pack_bf16x2(o[dt][4 * g4 + 2] * inv, o[dt][4 * g4 + 3] * inv));
-      }
-    if (h == 0) a.LSE[((long long)b * a.H + hd) * a.S + q] = (m + __log2f(l)) / LOG2E;
-  }
-}
-
-// ----------------------------------------------------------------------------------------------------------------
 // D = 128 dK/dV with v_mfma_f32_32x32x16_bf16: block = 128 keys, wave w owns keys kw = kblk + 32w + [0, 32) (key
 // n = lane&31 on the lane, K and V of that key held in registers as B operands for the whole block). Per 32-query
 // sub-chunk: S = Q·Kᵀ and dP = dO·Vᵀ (queries on the 16 accumulator registers, A operands = Q / dO rows from LDS),
@@ -1194,10 +1032,6 @@ static int attn_bwd_impl() {   // OBST_ATTN_BWD=2 selects the 32x32x16 dK/dV ker
 template <int D>
 int launch_fwd(const AttnArgs& a, hipStream_t st) {
   dim3 grid((a.S + 127) / 128 * a.B * a.H);
-  if (D == 128 && attn_impl() >= 3) {
-    hipLaunchKernelGGL(attn_fwd3_kernel, grid, dim3(NTH), 4 * 64 * 256, st, a);
-    return (int)hipGetLastError();
-  }
   if (D == 128 && attn_impl() == 2) {
     hipLaunchKernelGGL(attn_fwd32_kernel, grid, dim3(NTH), 4 * 64 * 256, st, a);
     return (int)hipGetLastError();
