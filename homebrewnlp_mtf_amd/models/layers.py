@@ -17,6 +17,7 @@ import typing
 import torch
 
 from ..config import Dim, anonymize_dim, unanonymize_dim
+from ..ops import aux as X
 from ..ops import functional as F
 from ..parallel import state as pstate
 from . import dims as D
@@ -162,12 +163,20 @@ def mixture_of_experts(args: BlockArgs) -> Act:
     p = args.params
     old, new = D.linear_shapes(p, args, args.tensor.dims)
     gate = linear(args, old, [p.expert_dim])
-    g = gate.t.float()
-    ei = gate.dims.index(p.expert_dim)
-    g = torch.softmax(g - g.amax(ei, keepdim=True).detach(), ei).to(args.tensor.t.dtype)
     w = _scoped(args, "moe", orthogonal_var, args, list(old) + list(new) + [p.expert_dim])
     wdims = D.deduplicate(list(old) + list(new) + [p.expert_dim])
     odims = D.deduplicate(D.subtract(args.tensor.dims, old) + list(new))
+    x = args.tensor
+    rest = D.subtract(x.dims, old)
+    T, K, N, E = D.size(rest), D.size(old), D.size(new), p.expert_dim.size
+    if (list(x.dims) == rest + list(old) and list(gate.dims) == rest + [p.expert_dim] and odims == rest + list(new)
+            and wdims == list(old) + list(new) + [p.expert_dim] and pstate.tp_size() == 1 and X.moe_ok(x.t, E, K)):
+        # one GEMM over the expert-minor weight + the fused softmax / expert contraction kernel (K15)
+        y = X.moe(x.t, gate.t, w, T, K, N, E)
+        return Act(y.view([d.size for d in odims]), odims)
+    g = gate.t.float()
+    ei = gate.dims.index(p.expert_dim)
+    g = torch.softmax(g - g.amax(ei, keepdim=True).detach(), ei).to(args.tensor.t.dtype)
     return named_einsum([args.tensor, Act(g, gate.dims), Act(w, wdims)], odims)
 
 
@@ -184,7 +193,7 @@ def activated_linear(args: BlockArgs, prefix: str) -> Act:
     out = dropout(args(out))
     if 'glu' in args or 'glu_add' in args:
         gate = ff(args)
-        out = Act(out.t * F.activation(gate.t, "sigmoid"), out.dims)
+        out = Act(X.glu(out.t, gate.t), out.dims)
     if 'glu_add' in args:
         extra = activate(args(ff(args)))
         out = Act(F.add(out.t, extra.t), out.dims)
@@ -260,7 +269,7 @@ def sum_heads(args: BlockArgs) -> Act:
     x = args.tensor
     hd = args.params.head_dim
     i = x.dims.index(hd)
-    y = _TPSum.apply(x.t.sum(i))
+    y = _TPSum.apply(X.sum_axis(x.t, i))
     return Act(y, [d for d in x.dims if d != hd])
 
 
@@ -281,7 +290,7 @@ def transpose_sequence_features(args: BlockArgs) -> Act:
     x = args.tensor
     si = next(i for i, d in enumerate(x.dims) if d.name == "sequence")
     fi = x.dims.index(p.key_dim)
-    return Act(x.t.transpose(si, fi).contiguous(), x.dims)
+    return Act(X.swap_axes(x.t, si, fi), x.dims)
 
 
 def reduced_half_linear(args: BlockArgs) -> Act:
@@ -298,6 +307,13 @@ def product_key_memory(args: BlockArgs) -> Act:
     old = D.linear_shapes(p, args, x.dims).old
     assign = linear(args, old, [p.head_dim] + features)
     assign = norm(args(assign), features)
+    table = _scoped(args, "embed", normal_var, args, [p.product_key_value_dim] + list(p.feature_dims),
+                    p.embedding_stddev)
+    lead = [d for d in assign.dims if d not in (p.head_dim, p.pkm_dim, anon_key)]
+    if (assign.dims[-3:] == [p.head_dim, p.pkm_dim, anon_key] and list(p.feature_dims) == [p.head_dim, p.key_dim]
+            and X.product_key_ok(assign.t, table)):
+        # fused top-1 / index combine + value-weighted gather kernels (K14)
+        return Act(X.product_key(assign.t, table), lead + [p.head_dim, p.key_dim])
     a = assign.t.double()
     ki = assign.dims.index(anon_key)
     pi = assign.dims.index(p.pkm_dim)
@@ -312,8 +328,6 @@ def product_key_memory(args: BlockArgs) -> Act:
     keep = [d for d in assign.dims if d not in (anon_key, p.pkm_dim)]
     idx = idx.reshape([d.size for d in keep])
     val = val.reshape([d.size for d in keep]).to(x.t.dtype)
-    table = _scoped(args, "embed", normal_var, args, [p.product_key_value_dim] + list(p.feature_dims),
-                    p.embedding_stddev)
     # gather per head: out[..., h, f] = table[idx[..., h], h, f]
     hi = keep.index(p.head_dim)
     flat_idx = idx.movedim(hi, -1)                                   # [..., h]
@@ -571,6 +585,11 @@ def _relative(args: BlockArgs, shape: typing.List[Dim]) -> torch.Tensor:
     position_count = D.size(position_dims)
     cosine = 'cosine' in p.position_embedding
     dev = args.builder.device if not args.builder.register else "meta"
+    # a constant of the shapes: generated once per (shape, features, dtype, device) and kept on the device (K11)
+    cache = args.builder.__dict__.setdefault("_relative_cache", {})
+    key = (tuple(shape), tuple(feature_dims), cosine, float(p.embedding_stddev), args.builder.dtype, str(dev))
+    if key in cache:
+        return cache[key]
 
     def multi_range(dims):
         sizes = [d.size for d in dims]
@@ -599,7 +618,10 @@ def _relative(args: BlockArgs, shape: typing.List[Dim]) -> torch.Tensor:
     sl = "".join(string.ascii_lowercase[i] for i in range(len(shape)))
     out = torch.einsum(f"{pl},{fl}->{sl}", positions, features)
     out = torch.sin(out) * p.embedding_stddev
-    return out.to(dtype=args.builder.dtype, device=dev)
+    out = out.to(dtype=args.builder.dtype, device=dev)
+    if str(dev) != "meta":
+        cache[key] = out
+    return out
 
 
 def _embed(args: BlockArgs, shape: typing.List[Dim]) -> Act:

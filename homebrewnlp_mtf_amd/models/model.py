@@ -18,7 +18,9 @@ import typing
 import torch
 
 from ..config import Dim, ModelParameter
+from ..ops import aux as X
 from ..ops import functional as F
+from ..ops import raw as R
 from . import dims as D
 from .context import Act, BlockArgs, Builder
 from .frontend import block_part_fn
@@ -150,6 +152,15 @@ class Model:
     def _frames(self, vid: torch.Tensor) -> torch.Tensor:
         """uint8 (or bit-folded int) frames -> activation dtype in [0, 1] (ref __init__.py:37-55)"""
         p = self.builder.params
+        folds = p.fold_count if p.use_bit_fold_input_pipeline else 1
+        if (R.on_gpu(vid) and self.builder.dtype == torch.bfloat16 and vid.dtype in (torch.uint8, torch.int32)
+                and not self.builder.register):
+            # one pass: bit unfold + scale to [0, 1] in the frame kernel (K24)
+            C = vid.shape[-1]
+            y = torch.empty(list(vid.shape[:-1]) + [C * folds], dtype=torch.bfloat16, device=vid.device)
+            R.frames(vid.contiguous(), y, vid.numel() // C, C, folds,
+                     2 ** p.bit_fold_value if p.use_bit_fold_input_pipeline else 256)
+            return y
         if p.use_bit_fold_input_pipeline:
             v = vid.long()
             base = 2 ** p.bit_fold_value
@@ -244,7 +255,10 @@ class Model:
             for ci, cfg in enumerate(p.output_block_configs):
                 x = block_part_fn(b, cfg, x, 0, ci, prefix="vid_out")
             y = linear(BlockArgs(b, x, ['']), p.feature_dims, [p.color_channel_dim])
-            frame_out = Act(torch.sigmoid(y.t.float()).to(y.t.dtype), y.dims)
+            if R.on_gpu(y.t) and (y.t.dtype != torch.bfloat16 or y.t.numel() % 8):
+                frame_out = Act(torch.sigmoid(y.t.float()).to(y.t.dtype), y.dims)
+            else:
+                frame_out = Act(F.activation(y.t, "sigmoid"), y.dims)
         return frame_out, token_out
 
     def _loss(self, frame_out, token_out, batch, vid_tgt) -> typing.Dict[str, torch.Tensor]:
@@ -273,15 +287,23 @@ class Model:
                 res["video_loss"] = vloss
                 losses.append(vloss)
             else:
-                out = frame_out.t.float() - vid_tgt.t.float()
+                fo, tg = frame_out.t, vid_tgt.t
                 scale = 1.0
+                masks = []
                 for key in ("vid_msk_tgt", "cat_mask_y"):
                     msk = batch.get(key)
                     if msk is not None:
-                        m = msk.float().view(list(msk.shape) + [1] * (out.dim() - msk.dim()))
-                        out = out * m
-                        scale *= msk.numel() / msk.float().sum().clamp(min=1.0)
-                vloss = (out * torch.sign(out.detach())).sum() / out.numel()   # ref __init__.py:187-199
+                        masks.append(msk.float())
+                        scale *= msk.numel() / masks[-1].sum().clamp(min=1.0)
+                mask = None
+                if masks:        # masks cover leading dims of the frames (ref: mask broadcast over the trailing dims)
+                    r = max(m.dim() for m in masks)
+                    for m in masks:
+                        m = m.view(list(m.shape) + [1] * (r - m.dim()))
+                        mask = m if mask is None else mask * m
+                    mask = mask.expand(list(fo.shape[:r]))
+                # masked L1 (sum |d| with gradient sign(d) * mask) in one pass (K24), ref __init__.py:187-199
+                vloss = X.masked_l1(fo, tg, mask) / fo.numel()
                 losses.append(vloss)
                 res["video_loss_raw"] = vloss
                 res["video_loss"] = vloss.detach() * scale                  # reported loss rescaled by the masks

@@ -98,6 +98,17 @@ _SIGS = {
     "obst_blaslt_enabled": [],
     "obst_blaslt_set": [c_i],
     "obst_blaslt_stats": [c_p],
+    "obst_glu": [c_p, c_p, c_p, c_p, c_p, c_ll, c_p],
+    "obst_pkm_top1": [c_p, c_p, c_p, c_p, c_p, c_ll, c_i, c_i, c_p],
+    "obst_pkm_top1_bwd": [c_p, c_p, c_p, c_p, c_p, c_p, c_ll, c_i, c_i, c_p],
+    "obst_pkm_gather": [c_p, c_p, c_p, c_p, c_ll, c_i, c_i, c_i, c_p],
+    "obst_pkm_gather_bwd": [c_p, c_p, c_p, c_p, c_p, c_p, c_ll, c_i, c_i, c_i, c_p],
+    "obst_moe_fwd": [c_p, c_p, c_p, c_p, c_ll, c_i, c_i, c_p],
+    "obst_moe_bwd": [c_p, c_p, c_p, c_p, c_p, c_ll, c_i, c_i, c_p],
+    "obst_sum_axis": [c_p, c_p, c_ll, c_i, c_ll, c_p],
+    "obst_sample": [c_p, c_ll, c_i, c_i, c_p, c_p, c_p, c_p, c_i, c_p, ctypes.c_ulonglong, c_p],
+    "obst_frames": [c_p, c_i, c_p, c_ll, c_i, c_i, c_i, c_p],
+    "obst_l1": [c_p, c_p, c_p, c_ll, c_ll, c_p, c_p, c_p, c_f, c_p],
 }
 
 

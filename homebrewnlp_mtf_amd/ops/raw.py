@@ -431,7 +431,13 @@ def elementwise(op: str, x, y, z=None, act=None, sptr=None, alpha=1.0, beta=1.0,
 
 def dropout_mask(n: int, seed: int, keep: float, device) -> torch.Tensor:
     """The same counter-based hash as the kernel (splitmix64 finaliser), so CPU and GPU masks agree."""
-    i = torch.arange(n, dtype=torch.int64, device=device)
+    u = hash_u24(torch.arange(n, dtype=torch.int64, device=device), seed).double() / 16777216.0
+    return (u < keep).to(torch.float32)
+
+
+def hash_u24(i: torch.Tensor, seed: int) -> torch.Tensor:
+    """top 24 bits of the splitmix64 finaliser of (i * golden ^ seed): the kernels' counter RNG (int64 tensor)"""
+    device = i.device
     m64 = (1 << 64) - 1
 
     def _u(v):
@@ -446,8 +452,7 @@ def dropout_mask(n: int, seed: int, keep: float, device) -> torch.Tensor:
     h = h ^ srl(h, 33)
     h = h * _u(0xc4ceb9fe1a85ec53)
     h = h ^ srl(h, 33)
-    u = srl(h, 40).double() / 16777216.0
-    return (u < keep).to(torch.float32)
+    return srl(h, 40)
 
 
 def dot(x, dy, out):
@@ -599,3 +604,272 @@ def xent_bwd(logits, tgt, lse, grad, gscale_ptr, gscale: float, rows: int, V: in
     d = p * (1 + 2 * z_loss * lse.view(rows, 1))
     d[torch.arange(rows, device=lv.device), tgt.reshape(rows).long()] -= 1
     grad.reshape(rows, Vp).copy_(d * g)
+
+
+# ----------------------------------------------------------------------------------------------------------------
+# block-grammar ops off the GPT-Neo hot path (csrc/kernels/aux_ops.hip); bf16 on the GPU, torch oracles elsewhere
+def _bf16_contig(name: str, *ts):
+    for t in ts:
+        if t is not None and (t.dtype != torch.bfloat16 or not t.is_contiguous()):
+            raise L.KernelError(f"{name} operands must be contiguous bf16 on the GPU")
+
+
+def glu(a, g, y, dy=None, dg=None):
+    """dy None: y = a * sigmoid(g); else y = da = dy * s(g), dg = dy * a * s (1 - s)"""
+    if a.device.type == "meta":
+        return None
+    n = a.numel()
+    if on_gpu(a):
+        _bf16_contig("glu", a, g, y, dy, dg)
+        for nm, t in (("a", a), ("g", g), ("y", y), ("dy", dy), ("dg", dg)):
+            _need(t, n - 1, nm)
+        if n % 8:
+            raise L.KernelError(f"glu size {n} must be a multiple of 8")
+        L.check(L.lib().obst_glu(a.data_ptr(), g.data_ptr(), L.ptr(dy), y.data_ptr(), L.ptr(dg), n,
+                                 L.stream_ptr()), "glu")
+        return None
+    s = torch.sigmoid(_f(g))
+    if dy is None:
+        y.copy_(_f(a) * s)
+        return None
+    d = _f(dy)
+    y.copy_(d * s)
+    dg.copy_(d * _f(a) * s * (1 - s))
+    return None
+
+
+def pkm_top1(x, idx, val, stats, aidx, R: int, A: int, F: int):
+    """x [R][A][F]: idx[r] = sum_a argmax_a * F^a, val[r] = prod_a softmax_a(argmax_a); stats [R][A][2] = (max, sum
+    exp), aidx [R][A] kept for pkm_top1_bwd"""
+    if x.device.type == "meta":
+        return None
+    if on_gpu(x):
+        _bf16_contig("pkm_top1", x)
+        _need(x, R * A * F - 1, "x")
+        _need(stats, R * A * 2 - 1, "stats")
+        _need(aidx, R * A - 1, "aidx")
+        for nm, t in (("idx", idx), ("val", val)):
+            _need(t, R - 1, nm)
+        if idx.dtype != torch.int32 or aidx.dtype != torch.int32 or val.dtype != torch.float32:
+            raise L.KernelError("pkm_top1: int32 indices and fp32 values")
+        L.check(L.lib().obst_pkm_top1(x.data_ptr(), idx.data_ptr(), val.data_ptr(), stats.data_ptr(),
+                                      aidx.data_ptr(), R, A, F, L.stream_ptr()), "pkm_top1")
+        return None
+    xv = _f(x.reshape(R, A, F))
+    m, mi = xv.max(-1)
+    s = torch.exp(xv - m.unsqueeze(-1)).sum(-1)
+    mult = F ** torch.arange(A, device=x.device, dtype=torch.int64)
+    idx.reshape(R).copy_((mi * mult).sum(-1))
+    val.reshape(R).copy_((1.0 / s).prod(-1))
+    stats.reshape(R, A, 2).copy_(torch.stack([m, s], -1))
+    aidx.reshape(R, A).copy_(mi)
+    return None
+
+
+def pkm_top1_bwd(x, val, dval, stats, aidx, dx, R: int, A: int, F: int):
+    if x.device.type == "meta":
+        return None
+    if on_gpu(x):
+        _bf16_contig("pkm_top1_bwd", x, dx)
+        _need(dx, R * A * F - 1, "dx")
+        L.check(L.lib().obst_pkm_top1_bwd(x.data_ptr(), val.data_ptr(), dval.data_ptr(), stats.data_ptr(),
+                                          aidx.data_ptr(), dx.data_ptr(), R, A, F, L.stream_ptr()), "pkm_top1_bwd")
+        return None
+    xv = _f(x.reshape(R, A, F))
+    st = stats.reshape(R, A, 2).to(xv.dtype)
+    p = torch.exp(xv - st[..., :1]) / st[..., 1:]
+    hot = torch.nn.functional.one_hot(aidx.reshape(R, A).long(), F).to(xv.dtype)
+    g = (dval.reshape(R) * val.reshape(R)).to(xv.dtype).view(R, 1, 1)
+    dx.reshape(R, A, F).copy_(g * (hot - p))
+    return None
+
+
+def pkm_gather(idx, val, table, out, R: int, H: int, Fk: int, P: int):
+    """out[r] = table[idx[r], r % H] * val[r]   (table [P][H][Fk])"""
+    if table.device.type == "meta":
+        return None
+    if on_gpu(table):
+        _bf16_contig("pkm_gather", table, out)
+        _need(table, P * H * Fk - 1, "table")
+        _need(out, R * Fk - 1, "out")
+        _need(idx, R - 1, "idx")
+        _need(val, R - 1, "val")
+        L.check(L.lib().obst_pkm_gather(idx.data_ptr(), val.data_ptr(), table.data_ptr(), out.data_ptr(), R, H, Fk,
+                                        P, L.stream_ptr()), "pkm_gather")
+        return None
+    rows = idx.reshape(R).long().clamp(0, P - 1) * H + torch.arange(R, device=idx.device) % H
+    out.reshape(R, Fk).copy_(_f(table.reshape(P * H, Fk))[rows] * val.reshape(R, 1).to(_f(table).dtype))
+    return None
+
+
+def pkm_gather_bwd(idx, val, table, dy, dtable, dval, R: int, H: int, Fk: int, P: int):
+    """dtable[idx[r], r % H] += dy[r] * val[r] (fp32); dval[r] = <dy[r], table[idx[r], r % H]>"""
+    if table.device.type == "meta":
+        return None
+    if on_gpu(table):
+        _bf16_contig("pkm_gather_bwd", table, dy)
+        _need(dtable, P * H * Fk - 1, "dtable")
+        _need(dy, R * Fk - 1, "dy")
+        _need(dval, R - 1, "dval")
+        L.check(L.lib().obst_pkm_gather_bwd(idx.data_ptr(), val.data_ptr(), table.data_ptr(), dy.data_ptr(),
+                                            dtable.data_ptr(), dval.data_ptr(), R, H, Fk, P, L.stream_ptr()),
+                "pkm_gather_bwd")
+        return None
+    rows = idx.reshape(R).long().clamp(0, P - 1) * H + torch.arange(R, device=idx.device) % H
+    d = _f(dy.reshape(R, Fk))
+    dval.reshape(R).copy_((d * _f(table.reshape(P * H, Fk))[rows]).sum(-1))
+    dtable.reshape(P * H, Fk).index_add_(0, rows, (d * val.reshape(R, 1).to(d.dtype)).to(dtable.dtype))
+    return None
+
+
+def moe_ok(E: int) -> bool:
+    lanes = E // 8
+    return E % 8 == 0 and 1 <= lanes <= 64 and lanes & (lanes - 1) == 0
+
+
+def moe_fwd(u, lg, p, y, T: int, N: int, E: int):
+    """p[t] = softmax(lg[t]) (fp32), y[t][n] = sum_e u[t][n][e] p[t][e]"""
+    if u.device.type == "meta":
+        return None
+    if on_gpu(u):
+        _bf16_contig("moe_fwd", u, lg, y)
+        if not moe_ok(E):
+            raise L.KernelError(f"moe kernel: experts {E} must be 8 * 2^k <= 512")
+        _need(u, T * N * E - 1, "u")
+        _need(lg, T * E - 1, "lg")
+        _need(p, T * E - 1, "p")
+        _need(y, T * N - 1, "y")
+        L.check(L.lib().obst_moe_fwd(u.data_ptr(), lg.data_ptr(), p.data_ptr(), y.data_ptr(), T, N, E,
+                                     L.stream_ptr()), "moe_fwd")
+        return None
+    lv = _f(lg.reshape(T, E))
+    pv = torch.softmax(lv - lv.amax(-1, keepdim=True), -1)
+    p.reshape(T, E).copy_(pv)
+    y.reshape(T, N).copy_(torch.einsum("tne,te->tn", _f(u.reshape(T, N, E)), pv.to(_f(u).dtype)))
+    return None
+
+
+def moe_bwd(dy, u, p, du, dlg, T: int, N: int, E: int):
+    """du = dy ⊗ p; dlg = p (dp - <p, dp>), dp[t][e] = sum_n dy[t][n] u[t][n][e]"""
+    if u.device.type == "meta":
+        return None
+    if on_gpu(u):
+        _bf16_contig("moe_bwd", dy, u, du, dlg)
+        _need(du, T * N * E - 1, "du")
+        _need(dlg, T * E - 1, "dlg")
+        L.check(L.lib().obst_moe_bwd(dy.data_ptr(), u.data_ptr(), p.data_ptr(), du.data_ptr(), dlg.data_ptr(), T, N,
+                                     E, L.stream_ptr()), "moe_bwd")
+        return None
+    d = _f(dy.reshape(T, N))
+    pv = p.reshape(T, E).to(d.dtype)
+    du.reshape(T, N, E).copy_(d.unsqueeze(-1) * pv.unsqueeze(1))
+    dp = torch.einsum("tn,tne->te", d, _f(u.reshape(T, N, E)))
+    dlg.reshape(T, E).copy_(pv * (dp - (pv * dp).sum(-1, keepdim=True)))
+    return None
+
+
+def sum_axis(x, y, outer: int, H: int, inner: int):
+    """y[o][i] = sum_h x[o][h][i]"""
+    if x.device.type == "meta":
+        return None
+    if on_gpu(x):
+        _bf16_contig("sum_axis", x, y)
+        if inner % 8:
+            raise L.KernelError("sum_axis inner size must be a multiple of 8")
+        _need(x, outer * H * inner - 1, "x")
+        _need(y, outer * inner - 1, "y")
+        L.check(L.lib().obst_sum_axis(x.data_ptr(), y.data_ptr(), outer, H, inner, L.stream_ptr()), "sum_axis")
+        return None
+    y.reshape(outer, inner).copy_(_f(x.reshape(outer, H, inner)).sum(1))
+    return None
+
+
+def gumbel_scores(logits, temp, seed: int):
+    """torch oracle of the sampling kernel's noisy scores: logit - T log(-log u), u = (hash24(r V + v) + 0.5) / 2^24"""
+    rows, V = logits.shape
+    i = torch.arange(rows * V, dtype=torch.int64, device=logits.device)
+    u = (hash_u24(i, seed).to(torch.float32) + 0.5) / 16777216.0
+    noise = torch.log(-torch.log(u)).view(rows, V)
+    return logits.float() - temp.view(rows, 1).float() * noise
+
+
+def sample(logits, temp, pred, seed: int, x=None, pos=None, end=None, patch: int = 1):
+    """pred[r] = argmax_v(logits[r][v] - temp[r // patch] log(-log u)); with x [B][S][patch] (int32) the winner is
+    also written to x[b][min(pos_b, S-1)][r % patch] for rows whose pos_b < end_b"""
+    rows, V = logits.shape
+    B = rows // patch
+    if on_gpu(logits):
+        if logits.dtype != torch.float32 or not logits.is_contiguous():
+            raise L.KernelError("sample: contiguous fp32 logits")
+        if temp.dtype != torch.float32 or temp.numel() < B or pred.dtype != torch.int32 or pred.numel() < rows:
+            raise L.KernelError("sample: fp32 temperatures [B], int32 predictions [rows]")
+        S = 0
+        if x is not None:
+            if (x.dtype != torch.int32 or not x.is_contiguous() or x.numel() % (B * patch) or pos.dtype != torch.int64
+                    or end.dtype != torch.int64 or pos.numel() < B or end.numel() < B):
+                raise L.KernelError("sample: int32 token buffer, int64 pos / end")
+            S = x.numel() // (B * patch)
+        L.check(L.lib().obst_sample(logits.data_ptr(), rows, V, patch, temp.data_ptr(), L.ptr(pos), L.ptr(end),
+                                    L.ptr(x), S, pred.data_ptr(), int(seed) & (2 ** 64 - 1), L.stream_ptr()),
+                "sample")
+        return pred
+    t = temp.reshape(-1)[:B].repeat_interleave(patch)
+    scores = gumbel_scores(logits, t, seed)
+    scores = torch.where(t.view(rows, 1) == 0, logits.float(), scores)
+    pred.copy_(scores.argmax(-1).to(pred.dtype))
+    if x is not None:
+        S = x.numel() // (B * patch)
+        xv = x.view(B, S, patch)
+        rb = torch.arange(B, device=x.device)
+        wpos = pos.clamp(max=S - 1)
+        cur = xv[rb, wpos]
+        xv[rb, wpos] = torch.where((pos < end).view(B, 1), pred.view(B, patch).to(x.dtype), cur)
+    return pred
+
+
+def frames(v, y, rows: int, C: int, folds: int = 1, base: int = 256):
+    """y[r][i * C + c] = ((v[r][c] // base^i) % base) / 255  (folds == 1: v / 255); v uint8 or int32"""
+    if v.device.type == "meta":
+        return None
+    if on_gpu(v):
+        if y.dtype != torch.bfloat16 or not y.is_contiguous() or not v.is_contiguous():
+            raise L.KernelError("frames: contiguous input, bf16 output")
+        nb = {torch.uint8: 1, torch.int32: 4}.get(v.dtype)
+        if nb is None:
+            raise L.KernelError(f"frames: uint8 or int32 input, got {v.dtype}")
+        _need(v, rows * C - 1, "v")
+        _need(y, rows * C * folds - 1, "y")
+        L.check(L.lib().obst_frames(v.data_ptr(), nb, y.data_ptr(), rows, C, folds, base, L.stream_ptr()), "frames")
+        return None
+    vv = v.reshape(rows, C).long()
+    if folds == 1:
+        parts = [vv]
+    else:
+        parts = [(vv // base ** i) % base for i in range(folds)]
+    y.reshape(rows, C * folds).copy_(torch.cat(parts, -1).to(y.dtype) / 255.0)
+    return None
+
+
+def l1(fo, g, mask, inner: int, loss=None, dfo=None, gptr=None, gscale: float = 1.0):
+    """d = (fo - g) * mask[e // inner]; loss[0] += sum |d|  or (dfo given) dfo = sign(d) mask gscale (* gptr[0])"""
+    if fo.device.type == "meta":
+        return None
+    n = fo.numel()
+    if on_gpu(fo):
+        _bf16_contig("l1", fo, g, dfo)
+        _need(g, n - 1, "g")
+        if mask is not None:
+            if mask.dtype != torch.float32 or not mask.is_contiguous():
+                raise L.KernelError("l1 mask must be contiguous fp32")
+            _need(mask, (n - 1) // inner, "mask")
+        L.check(L.lib().obst_l1(fo.data_ptr(), g.data_ptr(), L.ptr(mask), inner, n, L.ptr(loss), L.ptr(dfo),
+                                L.ptr(gptr), float(gscale), L.stream_ptr()), "l1")
+        return None
+    m = 1.0 if mask is None else _f(mask).reshape(-1, 1)
+    d = (_f(fo).reshape(-1, inner) - _f(g).reshape(-1, inner)) * m
+    if dfo is None:
+        loss.view(-1)[0] += d.abs().sum().to(loss.dtype)
+        return None
+    gs = gscale * (_f(gptr.reshape(-1)[0]) if gptr is not None else 1.0)
+    dfo.reshape(-1, inner).copy_(torch.sign(d) * m * gs)
+    return None

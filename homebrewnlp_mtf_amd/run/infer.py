@@ -3,7 +3,7 @@ SURVEY C08/C31, §3.4).
 
 Sampling semantics follow the reference's language loop: for ``position`` in ``[initial_pos, end_iterations)``
 the model reads the whole (causal) context, the logits get Gumbel noise scaled by the temperature
-(``logits - T * log(-log(u))``, u ~ U[1e-9, 1)), ``argmax`` over the vocabulary, and the prediction made at
+(``logits - T * log(-log(u))``, u from a counter-hash RNG, see ``_NoiseSeeds``), ``argmax`` over the vocabulary, and the prediction made at
 ``position - 1`` is written into ``token_x[position]`` (the shift-by-one of inference.py:94-96). Only the one needed
 position goes through the output projection (``Model.logits(positions=...)``), which gives the same tokens as the
 reference's full-sequence projection for causal bodies.
@@ -22,6 +22,7 @@ import numpy as np
 import torch
 
 from ..config import ModelParameter
+from ..ops import raw as R
 from ..utils.log import log
 
 
@@ -78,16 +79,28 @@ def process_token_output(tokens: np.ndarray, padding_token: int = -1,
 
 
 # ---------------------------------------------------------------------------------------------------------------
+class _NoiseSeeds:
+    """Per-call seeds of the sampling kernel's counter RNG (splitmix64 of a 64-bit counter: no generator state on
+    the device, and the CPU oracle draws the same noise)"""
+
+    def __init__(self, params: ModelParameter):
+        self.base = int(params.seed) if getattr(params, "seed", None) is not None else 0
+        self.calls = 0
+
+    def next(self) -> int:
+        self.calls += 1
+        return (self.base * 0x9E3779B97F4A7C15 + self.calls * 0xD1B54A32D192ED03) & (2 ** 64 - 1)
+
+
 class Sampler:
     def __init__(self, model, params: ModelParameter, device):
         self.model, self.params, self.device = model, params, torch.device(device)
-        self.gen = torch.Generator(device=self.device)
-        self.gen.manual_seed(int(params.seed) if getattr(params, "seed", None) is not None else 0)
+        self.seeds = _NoiseSeeds(params)
 
     @torch.no_grad()
     def sample(self, token_x: torch.Tensor, initial_pos, temperature, end_iterations) -> torch.Tensor:
         """token_x [B, S, patch] int; per-row initial position / temperature / end (scalars or [B] tensors)."""
-        x = token_x.to(self.device, torch.int32).clone()
+        x = token_x.to(self.device, torch.int32).contiguous().clone()
         B, S = x.shape[0], x.shape[1]
 
         def vec(v, dtype):
@@ -96,17 +109,15 @@ class Sampler:
         pos = vec(initial_pos, torch.long).clamp(min=1)
         temp = vec(temperature, torch.float32)
         end = vec(end_iterations, torch.long).clamp(max=S)
-        rows = torch.arange(B, device=self.device)
         while bool((pos < end).any()):
             active = pos < end
             src = (pos - 1).clamp(max=S - 1)
-            logits = self.model.logits(x, positions=src)[:, 0]          # [B, patch, V]
-            u = torch.rand(logits.shape, generator=self.gen, device=self.device) * (1 - 1e-9) + 1e-9
-            noisy = logits - temp.view(B, 1, 1) * torch.log(-torch.log(u))
-            pred = noisy.argmax(-1).to(torch.int32)                      # [B, patch]
-            wpos = pos.clamp(max=S - 1)
-            cur = x[rows, wpos]
-            x[rows, wpos] = torch.where(active.view(B, 1), pred, cur)
+            logits = self.model.logits(x, positions=src)[:, 0]          # [B, patch, V] fp32
+            P, V = logits.shape[1], logits.shape[2]
+            pred = torch.empty(B * P, dtype=torch.int32, device=self.device)
+            # Gumbel-argmax + write of the token at min(pos, S-1) for rows with pos < end: one kernel (K21)
+            R.sample(logits.reshape(B * P, V).contiguous(), temp, pred, self.seeds.next(), x=x, pos=pos, end=end,
+                     patch=P)
             pos = torch.where(active, pos + 1, pos)
         return x
 
@@ -124,8 +135,7 @@ class VideoSampler:
 
     def __init__(self, model, params: ModelParameter, device):
         self.model, self.params, self.device = model, params, torch.device(device)
-        self.gen = torch.Generator(device=self.device)
-        self.gen.manual_seed(int(params.seed) if getattr(params, "seed", None) is not None else 0)
+        self.seeds = _NoiseSeeds(params)
 
     def _to_input(self, frame_out: torch.Tensor) -> torch.Tensor:
         p = self.params
@@ -152,8 +162,11 @@ class VideoSampler:
                 frame[:, pos + 1] = self._to_input(frame_out[:, pos])
             if tok is not None and logits is not None and pos + 1 < tok.shape[1]:
                 lg = logits[:, pos, ..., :p.vocab_size].float()
-                u = torch.rand(lg.shape, generator=self.gen, device=self.device) * (1 - 1e-9) + 1e-9
-                tok[:, pos + 1] = (lg - temperature * torch.log(-torch.log(u))).argmax(-1).to(tok.dtype)
+                rows = lg.numel() // lg.shape[-1]
+                pred = torch.empty(rows, dtype=torch.int32, device=self.device)
+                temp = torch.full((rows,), float(temperature), dtype=torch.float32, device=self.device)
+                R.sample(lg.reshape(rows, lg.shape[-1]).contiguous(), temp, pred, self.seeds.next())
+                tok[:, pos + 1] = pred.view(lg.shape[:-1]).to(tok.dtype)
         out = {"frame": frame}
         if tok is not None:
             out["token_x"] = tok
