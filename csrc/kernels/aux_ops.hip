@@ -9,6 +9,7 @@
 //  K21 Gumbel-argmax sampling with the token write (ref src/run/inference.py:87-97), counter-hash RNG
 //  K24 frame unpack (uint8 or bit-folded ints -> bf16 / 255, ref src/model/__init__.py:37-55) and the masked
 //      L1 video loss with its gradient (ref src/model/__init__.py:187-199)
+//  serving: single-query attention over a KV cache (incremental decoding; the reference recomputes the context)
 #include "common.h"
 
 namespace {
@@ -356,6 +357,91 @@ __global__ __launch_bounds__(NTH) void l1_kernel(const bf16_t* __restrict__ Fo, 
   }
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// KV-cache decode attention (serving): one new query per (b, h) against the cached keys / values of that row,
+// o[b][h] = softmax_j(scale q.K[b][j][h], j < len[b]) . V[b][j][h]. Q/O are [B][H][D], the caches [B][S][H][D]
+// (token-major, the layout the k/v linears write). Block = (b, h), 4 waves stride over the keys 4 at a time (4
+// independent dot-product reductions in flight per wave), lanes over the head dim (2 elements per lane, D <= 128,
+// 256-byte coalesced rows), online softmax per wave, the 4 partial states merged through LDS.
+__global__ __launch_bounds__(NTH) void decode_attn_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ Kn,
+                                                          const bf16_t* __restrict__ Vn, bf16_t* __restrict__ K,
+                                                          bf16_t* __restrict__ V, bf16_t* __restrict__ O,
+                                                          const long long* __restrict__ pos, int S, int H, int D,
+                                                          float scale) {
+  __shared__ float sm[NW], sl[NW];
+  __shared__ float sacc[NW][128];
+  const int bh = blockIdx.x, b = bh / H, h = bh % H;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int e0 = 2 * lane;
+  const bool act = e0 < D;
+  const long long P = pos[b];                            // the new token's position: keys [0, P]
+  long long L = P + 1;
+  L = L < 0 ? 0 : (L > S ? S : L);
+  float q0 = 0.f, q1 = 0.f;
+  uint32_t kn = 0, vn = 0;
+  if (act) {
+    const uint32_t u = *reinterpret_cast<const uint32_t*>(Q + (long long)bh * D + e0);
+    q0 = bf2f(u & 0xffff) * scale;
+    q1 = bf2f(u >> 16) * scale;
+    kn = *reinterpret_cast<const uint32_t*>(Kn + (long long)bh * D + e0);
+    vn = *reinterpret_cast<const uint32_t*>(Vn + (long long)bh * D + e0);
+  }
+  const long long rs = (long long)H * D;                 // cache row stride
+  bf16_t* Kb = K + (long long)b * S * rs + (long long)h * D + e0;
+  bf16_t* Vb = V + (long long)b * S * rs + (long long)h * D + e0;
+  if (w == 0 && act && P >= 0 && P < S) {                // append the new key / value (read below from registers)
+    *reinterpret_cast<uint32_t*>(Kb + P * rs) = kn;
+    *reinterpret_cast<uint32_t*>(Vb + P * rs) = vn;
+  }
+  float m = -INFINITY, l = 0.f, a0 = 0.f, a1 = 0.f;
+  for (long long j0 = 4 * w; j0 < L; j0 += 4 * NW) {
+    float s[4];
+    uint32_t vv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const long long j = j0 + u;
+      uint32_t kk = 0;
+      vv[u] = 0;
+      if (act && j < L) {
+        const bool cur = j == P;
+        kk = cur ? kn : *reinterpret_cast<const uint32_t*>(Kb + j * rs);
+        vv[u] = cur ? vn : *reinterpret_cast<const uint32_t*>(Vb + j * rs);
+      }
+      s[u] = q0 * bf2f(kk & 0xffff) + q1 * bf2f(kk >> 16);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) s[u] = wave_sum(s[u]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (j0 + u >= L) continue;                           // wave-uniform
+      const float mn = fmaxf(m, s[u]);
+      const float c = __expf(m - mn), p = __expf(s[u] - mn);
+      l = l * c + p;
+      a0 = a0 * c + p * bf2f(vv[u] & 0xffff);
+      a1 = a1 * c + p * bf2f(vv[u] >> 16);
+      m = mn;
+    }
+  }
+  if (lane == 0) { sm[w] = m; sl[w] = l; }
+  if (act) { sacc[w][e0] = a0; sacc[w][e0 + 1] = a1; }
+  __syncthreads();
+  if (w == 0 && act) {
+    float M = sm[0];
+#pragma unroll
+    for (int i = 1; i < NW; ++i) M = fmaxf(M, sm[i]);
+    float Lt = 0.f, o0 = 0.f, o1 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) {
+      const float c = sm[i] == -INFINITY ? 0.f : __expf(sm[i] - M);
+      Lt += sl[i] * c;
+      o0 += sacc[i][e0] * c;
+      o1 += sacc[i][e0 + 1] * c;
+    }
+    const float inv = Lt > 0.f ? 1.f / Lt : 0.f;
+    *reinterpret_cast<uint32_t*>(O + (long long)bh * D + e0) = pack_bf16x2(o0 * inv, o1 * inv);
+  }
+}
+
 inline bool aligned16(const void* p) { return (((uintptr_t)p) & 15) == 0; }
 
 }  // namespace
@@ -465,5 +551,17 @@ OBST_API int obst_l1(const void* Fo, const void* G, const float* M, long long in
   if (n <= 0 || inner <= 0 || (!DF && !loss)) return -1;
   hipLaunchKernelGGL(l1_kernel, dim3(grid_for(n)), dim3(NTH), 0, st, (const bf16_t*)Fo, (const bf16_t*)G, M, inner, n,
                      loss, (bf16_t*)DF, gptr, gscale);
+  return (int)hipGetLastError();
+}
+
+// Q, Kn, Vn, O [B][H][D] (the new token's q / k / v and the output); K, V caches [B][S][H][D] receive Kn / Vn at
+// pos[b]; row b attends over keys [0, pos[b]]. D even, <= 128
+OBST_API int obst_decode_attn(const void* Q, const void* Kn, const void* Vn, void* K, void* V, void* O,
+                              const long long* pos, int B, int S, int H, int D, float scale, hipStream_t st) {
+  if (B <= 0 || S <= 0 || H <= 0 || D <= 0 || D > 128 || D % 2) return -1;
+  if ((((uintptr_t)Q) | ((uintptr_t)Kn) | ((uintptr_t)Vn) | ((uintptr_t)K) | ((uintptr_t)V) | ((uintptr_t)O)) & 3)
+    return -2;
+  hipLaunchKernelGGL(decode_attn_kernel, dim3(B * H), dim3(NTH), 0, st, (const bf16_t*)Q, (const bf16_t*)Kn,
+                     (const bf16_t*)Vn, (bf16_t*)K, (bf16_t*)V, (bf16_t*)O, pos, S, H, D, scale);
   return (int)hipGetLastError();
 }

@@ -32,6 +32,18 @@ class Act:
         return f"Act({[f'{d.name}:{d.size}' for d in self.dims]})"
 
 
+class KVCache:
+    """Per-attention-layer key / value caches for incremental decoding (serving). ``mode`` "prefill": the attention
+    layers run over the whole context and keep k / v [B, S, H, D]; "decode": the input is one token per row at
+    position ``pos[b]``, whose k / v are appended to the caches and whose query attends over keys [0, pos[b]]."""
+
+    def __init__(self):
+        self.layers: typing.Dict[int, typing.Tuple[torch.Tensor, torch.Tensor, float]] = {}
+        self.mode = "prefill"
+        self.pos: typing.Optional[torch.Tensor] = None
+        self.idx = 0
+
+
 class Builder:
     def __init__(self, params: ModelParameter, tp_rank: int = 0, tp_size: int = 1):
         # local (TP-sharded) view of the config: `heads` has size heads / tp
@@ -57,6 +69,7 @@ class Builder:
         self.dropout_counter = 0
         self.step_seed = 0
         self.use_counts: typing.Dict[str, int] = {}
+        self.kv: typing.Optional[KVCache] = None
 
     # ---- per forward ------------------------------------------------------------------------------------------------
     def begin_forward(self):
@@ -64,6 +77,8 @@ class Builder:
         self.shared.reset()
         self.params.attention_idx = 0
         self.dropout_counter = 0
+        if self.kv is not None:
+            self.kv.idx = 0
         if self.register:
             self.use_counts = {}
 

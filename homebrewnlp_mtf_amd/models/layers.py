@@ -19,6 +19,7 @@ import torch
 from ..config import Dim, anonymize_dim, unanonymize_dim
 from ..ops import aux as X
 from ..ops import functional as F
+from ..ops import raw as R
 from ..parallel import state as pstate
 from . import dims as D
 from .context import Act, BlockArgs
@@ -441,6 +442,23 @@ def _attention_fast_ok(args: BlockArgs, ins, outs) -> bool:
     return True
 
 
+def _attention_kv(kv, x: Act, w_in, ws, w_in_dims, base_dims, w_out_dims, act_in, scale: float) -> Act:
+    """causal dot-product attention with a KV cache (serving): prefill keeps k / v of the whole context; a decode
+    step appends the new token's k / v and attends its query over the row's prefix in one kernel"""
+    base = F.linear(x.t, w_in, x.dims, w_in_dims, base_dims, act=act_in)
+    k, q, v = (F.linear(base, w, base_dims, w_out_dims, x.dims).contiguous() for w in ws)
+    i = kv.idx
+    kv.idx += 1
+    if kv.mode == "prefill":
+        kv.layers[i] = (k, v, scale)     # the scale may depend on the context length (attention_scale "sequence")
+        return Act(F.attention_core(q, k, v, scale, True), x.dims)
+    K, V, scale = kv.layers[i]
+    B, S, H, Dh = K.shape
+    o = torch.empty_like(q)
+    R.decode_attn(q, k, v, K, V, o, kv.pos, B, S, H, Dh, scale)
+    return Act(o, x.dims)
+
+
 def _mixer_fast_ok(args: BlockArgs, x: Act, dim: Dim) -> bool:
     """the learned causal token mixer (biased_attention_map on the input as value) as one batched GEMM (K03)"""
     p = args.params
@@ -476,6 +494,10 @@ def attention(args: BlockArgs) -> Act:
         old2, new2 = D.linear_shapes(p, a_out, base_dims)
         w_in = _scoped(a_in, "linear", orthogonal_var, a_in, list(old1) + list(new1), list(old1))
         ws = [_scoped(a_out, "linear", orthogonal_var, a_out, list(old2) + list(new2), list(old2)) for _ in range(3)]
+        kv = args.builder.kv
+        if kv is not None and causal and pstate.tp_size() == 1:
+            return _attention_kv(kv, x, w_in, ws, D.deduplicate(old1 + new1), base_dims, D.deduplicate(old2 + new2),
+                                 act_in, scale)
         res = args.residual if (args.residual is not None and args.residual.dims == x.dims) else None
         geo = (x.dims[0].size, x.dims[1].size, p.head_dim.size, p.key_dim.size)
         try:

@@ -22,7 +22,7 @@ from ..ops import aux as X
 from ..ops import functional as F
 from ..ops import raw as R
 from . import dims as D
-from .context import Act, BlockArgs, Builder
+from .context import Act, BlockArgs, Builder, KVCache
 from .frontend import block_part_fn
 from .layers import embed, gather_embed, linear, linear_to_features, named_einsum, dropout
 from .reversible import run_body
@@ -100,6 +100,50 @@ class Model:
         finally:
             self._positions = None
         return out[..., :self.params.vocab_size].float()
+
+    # ---- incremental decoding (serving) ----------------------------------------------------------------------------
+    def supports_kv_cache(self) -> bool:
+        """bodies whose only sequence mixing is causal dot-product attention on the fused path (GPT-style) decode
+        incrementally; everything else recomputes the context per token (as the reference does)"""
+        p = self.params
+        cfg = " ".join(str(c.layer) for c in list(p.block_configs) + list(p.input_block_configs) +
+                       list(p.output_block_configs))
+        mixing = ("cumsum", "cummean", "convolution", "transpose_sequence_features", "biased_", "scale_attention_map",
+                  "embedded", "positional", "input_as_value", "shared_key_value")
+        return (p.use_language and not p.use_video and not p.use_initial_position_embedding
+                and not p.input_block_configs and not p.output_block_configs and self.builder.tp_size == 1
+                and "attention" in cfg and not any(m in cfg for m in mixing)
+                and not (p.contrastive_across_samples or p.contrastive_across_token_embeddings))
+
+    @torch.no_grad()
+    def prefill(self, token_x: torch.Tensor, positions: torch.Tensor) -> torch.Tensor:
+        """Start incremental decoding: one forward over the whole context that fills the per-layer KV caches;
+        returns the logits at ``positions`` ([B, 1, patch, vocab])"""
+        kv = KVCache()
+        self.builder.kv = kv
+        try:
+            out = self.logits(token_x, positions=positions)
+        except BaseException:
+            self.builder.kv = None
+            raise
+        if kv.idx != self.builder.params.attention_idx or kv.idx == 0:
+            self.builder.kv = None          # an attention layer bypassed the cache: not decodable incrementally
+            raise NotImplementedError("body is not KV-cache decodable")
+        kv.mode = "decode"
+        return out
+
+    @torch.no_grad()
+    def decode(self, tokens: torch.Tensor, positions: torch.Tensor) -> torch.Tensor:
+        """One incremental step: ``tokens`` [B, 1, patch] sit at ``positions`` [B]; their k / v join the caches and
+        the logits of that position come back ([B, 1, patch, vocab])"""
+        kv = self.builder.kv
+        if kv is None or kv.mode != "decode":
+            raise RuntimeError("decode() needs prefill() first")
+        kv.pos = positions.to(self.device, torch.int64).contiguous()
+        return self.logits(tokens)
+
+    def end_decode(self):
+        self.builder.kv = None
 
     @torch.no_grad()
     def predict(self, batch: dict) -> typing.Tuple[typing.Optional[torch.Tensor], typing.Optional[torch.Tensor]]:

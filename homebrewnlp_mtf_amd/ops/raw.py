@@ -873,3 +873,33 @@ def l1(fo, g, mask, inner: int, loss=None, dfo=None, gptr=None, gscale: float = 
     gs = gscale * (_f(gptr.reshape(-1)[0]) if gptr is not None else 1.0)
     dfo.reshape(-1, inner).copy_(torch.sign(d) * m * gs)
     return None
+
+
+def decode_attn(q, kn, vn, k, v, o, pos, B: int, S: int, H: int, D: int, scale: float):
+    """KV-cache decode step: k[b][pos_b] = kn[b], v[b][pos_b] = vn[b], then
+    o[b][h] = softmax_j(scale q[b][h].k[b][j][h], j <= pos_b) . v[b][j][h]; q, kn, vn, o [B][H][D]; caches [B][S][H][D]"""
+    if q.device.type == "meta":
+        return None
+    if on_gpu(q):
+        _bf16_contig("decode_attn", q, kn, vn, k, v, o)
+        if pos.dtype != torch.int64 or pos.numel() < B:
+            raise L.KernelError("decode_attn: int64 positions [B]")
+        for nm, t, n in (("q", q, B * H * D), ("kn", kn, B * H * D), ("vn", vn, B * H * D), ("k", k, B * S * H * D),
+                         ("v", v, B * S * H * D), ("o", o, B * H * D)):
+            _need(t, n - 1, nm)
+        L.check(L.lib().obst_decode_attn(q.data_ptr(), kn.data_ptr(), vn.data_ptr(), k.data_ptr(), v.data_ptr(),
+                                         o.data_ptr(), pos.data_ptr(), B, S, H, D, float(scale), L.stream_ptr()),
+                "decode_attn")
+        return None
+    kc, vc = k.view(B, S, H, D), v.view(B, S, H, D)
+    rows = torch.arange(B, device=q.device)
+    ok = (pos >= 0) & (pos < S)
+    kc[rows[ok], pos[ok]] = kn.reshape(B, H, D)[ok].to(kc.dtype)
+    vc[rows[ok], pos[ok]] = vn.reshape(B, H, D)[ok].to(vc.dtype)
+    qv = _f(q.reshape(B, H, D)) * scale
+    s = torch.einsum("bhd,bjhd->bhj", qv, _f(kc))
+    valid = torch.arange(S, device=q.device).view(1, 1, S) <= pos.reshape(B, 1, 1)
+    s = s.masked_fill(~valid, float("-inf"))
+    p = torch.softmax(s, -1).nan_to_num(0.0)
+    o.reshape(B, H, D).copy_(torch.einsum("bhj,bjhd->bhd", p, _f(vc)))
+    return None

@@ -96,6 +96,7 @@ class Sampler:
     def __init__(self, model, params: ModelParameter, device):
         self.model, self.params, self.device = model, params, torch.device(device)
         self.seeds = _NoiseSeeds(params)
+        self.kv_cache = bool(getattr(params, "kv_cache", True))
 
     @torch.no_grad()
     def sample(self, token_x: torch.Tensor, initial_pos, temperature, end_iterations) -> torch.Tensor:
@@ -109,6 +110,8 @@ class Sampler:
         pos = vec(initial_pos, torch.long).clamp(min=1)
         temp = vec(temperature, torch.float32)
         end = vec(end_iterations, torch.long).clamp(max=S)
+        if self.kv_cache and self.model.supports_kv_cache():
+            return self._sample_cached(x, pos, temp, end)
         while bool((pos < end).any()):
             active = pos < end
             src = (pos - 1).clamp(max=S - 1)
@@ -119,6 +122,33 @@ class Sampler:
             R.sample(logits.reshape(B * P, V).contiguous(), temp, pred, self.seeds.next(), x=x, pos=pos, end=end,
                      patch=P)
             pos = torch.where(active, pos + 1, pos)
+        return x
+
+    def _sample_cached(self, x, pos, temp, end):
+        """Incremental decoding: one prefill forward over the context, then one single-token forward per step
+        (KV caches, csrc/kernels/aux_ops.hip::decode_attn_kernel) -- the same tokens as the full recompute."""
+        B, S = x.shape[0], x.shape[1]
+        m = self.model
+        try:
+            logits = m.prefill(x, (pos - 1).clamp(max=S - 1))
+        except NotImplementedError:
+            self.kv_cache = False
+            return self.sample(x, pos, temp, end)
+        try:
+            rows = torch.arange(B, device=self.device)
+            while True:
+                active = pos < end
+                P, V = logits.shape[2], logits.shape[3]
+                pred = torch.empty(B * P, dtype=torch.int32, device=self.device)
+                R.sample(logits.reshape(B * P, V).contiguous(), temp, pred, self.seeds.next(), x=x, pos=pos, end=end,
+                         patch=P)
+                pos = torch.where(active, pos + 1, pos)
+                if not bool((pos < end).any()):
+                    break
+                cur = (pos - 1).clamp(max=S - 1)           # the token just written; inactive rows rewrite theirs
+                logits = m.decode(x[rows, cur].unsqueeze(1), cur)
+        finally:
+            m.end_decode()
         return x
 
 
