@@ -442,6 +442,143 @@ __global__ __launch_bounds__(NTH) void decode_attn_kernel(const bf16_t* __restri
   }
 }
 
+// Split-K ("flash-decoding") variant for D % 8 == 0: grid (nsplit, B * H), block = 4 waves. A wave holds 4 keys at
+// a time, 16 lanes per key row with one 16-byte load each (8 dims per lane, D <= 128), so a score needs a 4-step
+// xor reduction inside the 16-lane group instead of 6 steps over the wave; 4 such groups are unrolled, i.e. 8
+// 16-byte K/V loads per lane are in flight. Each of the 16 (wave, group) states runs its own online softmax; the
+// block merges them through LDS and either writes the output (one split) or its unnormalised partial
+// (m, l, acc[D]) for decode_combine_kernel.
+__device__ __forceinline__ float group16_sum(float v) {
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__global__ __launch_bounds__(NTH) void decode_attn_split_kernel(
+    const bf16_t* __restrict__ Q, const bf16_t* __restrict__ Kn, const bf16_t* __restrict__ Vn,
+    bf16_t* __restrict__ K, bf16_t* __restrict__ V, bf16_t* __restrict__ O, float* __restrict__ part,
+    const long long* __restrict__ pos, int S, int H, int D, float scale, int chunk) {
+  __shared__ float sm[16], sl[16];
+  __shared__ float sacc[16][128];
+  const int sp = blockIdx.x, nsplit = gridDim.x, bh = blockIdx.y, b = bh / H, h = bh % H;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, e0 = 8 * (lane & 15);
+  const bool act = e0 < D;
+  const long long P = pos[b];
+  long long L = P + 1;
+  L = L < 0 ? 0 : (L > S ? S : L);
+  const long long jb = (long long)sp * chunk, je = jb + chunk < L ? jb + chunk : L;
+  float q[8];
+  uint4 kn = make_uint4(0, 0, 0, 0), vn = make_uint4(0, 0, 0, 0);
+  if (act) {
+    unpack8(*reinterpret_cast<const uint4*>(Q + (long long)bh * D + e0), q);
+    kn = *reinterpret_cast<const uint4*>(Kn + (long long)bh * D + e0);
+    vn = *reinterpret_cast<const uint4*>(Vn + (long long)bh * D + e0);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) q[i] = 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) q[i] *= scale;
+  const long long rs = (long long)H * D;
+  bf16_t* Kb = K + (long long)b * S * rs + (long long)h * D + e0;
+  bf16_t* Vb = V + (long long)b * S * rs + (long long)h * D + e0;
+  if (sp == 0 && w == 0 && g == 0 && act && P >= 0 && P < S) {   // append; read back below from registers
+    *reinterpret_cast<uint4*>(Kb + P * rs) = kn;
+    *reinterpret_cast<uint4*>(Vb + P * rs) = vn;
+  }
+  float m = -INFINITY, l = 0.f, acc[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) acc[i] = 0.f;
+  for (long long j0 = jb; j0 < je; j0 += 64) {
+    float s[4];
+    uint4 vv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const long long j = j0 + w * 16 + u * 4 + g;
+      uint4 kk = make_uint4(0, 0, 0, 0);
+      vv[u] = kk;
+      if (act && j < je) {
+        const bool cur = j == P;
+        kk = cur ? kn : *reinterpret_cast<const uint4*>(Kb + j * rs);
+        vv[u] = cur ? vn : *reinterpret_cast<const uint4*>(Vb + j * rs);
+      }
+      float kf[8];
+      unpack8(kk, kf);
+      float d = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) d += q[i] * kf[i];
+      s[u] = d;
+    }
+    float mx = m;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      s[u] = group16_sum(s[u]);
+      if (j0 + w * 16 + u * 4 + g >= je) s[u] = -INFINITY;
+      mx = fmaxf(mx, s[u]);
+    }
+    if (mx == -INFINITY) continue;
+    const float c = __expf(m - mx);
+    l *= c;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] *= c;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float p = __expf(s[u] - mx);
+      float vf[8];
+      unpack8(vv[u], vf);
+      l += p;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[i] += p * vf[i];
+    }
+    m = mx;
+  }
+  const int st = w * 4 + g;
+  if ((lane & 15) == 0) { sm[st] = m; sl[st] = l; }
+  if (act) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) sacc[st][e0 + i] = acc[i];
+  }
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (t < D) {
+    float M = sm[0];
+#pragma unroll
+    for (int i = 1; i < 16; ++i) M = fmaxf(M, sm[i]);
+    float Lt = 0.f, o = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float c = sm[i] == -INFINITY ? 0.f : __expf(sm[i] - M);
+      Lt += sl[i] * c;
+      o += sacc[i][t] * c;
+    }
+    if (nsplit == 1) {
+      O[(long long)bh * D + t] = f2bf(Lt > 0.f ? o / Lt : 0.f);
+    } else {
+      float* pp = part + ((long long)bh * nsplit + sp) * (D + 2);
+      pp[2 + t] = o;
+      if (t == 0) { pp[0] = M; pp[1] = Lt; }
+    }
+  }
+}
+
+// merges the nsplit partials of one (b, h): grid B * H, one thread per head dim
+__global__ __launch_bounds__(128) void decode_combine_kernel(const float* __restrict__ part, bf16_t* __restrict__ O,
+                                                            int D, int nsplit) {
+  const int bh = blockIdx.x, t = threadIdx.x;
+  if (t >= D) return;
+  const float* pp = part + (long long)bh * nsplit * (D + 2);
+  float M = -INFINITY;
+  for (int i = 0; i < nsplit; ++i) M = fmaxf(M, pp[i * (D + 2)]);
+  float Lt = 0.f, o = 0.f;
+  for (int i = 0; i < nsplit; ++i) {
+    const float mi = pp[i * (D + 2)];
+    const float c = mi == -INFINITY ? 0.f : __expf(mi - M);
+    Lt += pp[i * (D + 2) + 1] * c;
+    o += pp[i * (D + 2) + 2 + t] * c;
+  }
+  O[(long long)bh * D + t] = f2bf(Lt > 0.f ? o / Lt : 0.f);
+}
+
 inline bool aligned16(const void* p) { return (((uintptr_t)p) & 15) == 0; }
 
 }  // namespace
@@ -555,12 +692,25 @@ OBST_API int obst_l1(const void* Fo, const void* G, const float* M, long long in
 }
 
 // Q, Kn, Vn, O [B][H][D] (the new token's q / k / v and the output); K, V caches [B][S][H][D] receive Kn / Vn at
-// pos[b]; row b attends over keys [0, pos[b]]. D even, <= 128
+// pos[b]; row b attends over keys [0, pos[b]]. D even, <= 128. With D % 8 == 0, 16-byte aligned operands and a
+// workspace of B * H * nsplit * (D + 2) floats the split-K kernel runs (nsplit key chunks per (b, h) + a combine)
 OBST_API int obst_decode_attn(const void* Q, const void* Kn, const void* Vn, void* K, void* V, void* O,
-                              const long long* pos, int B, int S, int H, int D, float scale, hipStream_t st) {
+                              const long long* pos, int B, int S, int H, int D, float scale, int nsplit, float* ws,
+                              hipStream_t st) {
   if (B <= 0 || S <= 0 || H <= 0 || D <= 0 || D > 128 || D % 2) return -1;
   if ((((uintptr_t)Q) | ((uintptr_t)Kn) | ((uintptr_t)Vn) | ((uintptr_t)K) | ((uintptr_t)V) | ((uintptr_t)O)) & 3)
     return -2;
+  if (D % 8 == 0 && nsplit >= 1 && aligned16(Q) && aligned16(Kn) && aligned16(Vn) && aligned16(K) &&
+      aligned16(V) && (nsplit == 1 || ws != nullptr)) {
+    const int chunk = (S + nsplit - 1) / nsplit;
+    hipLaunchKernelGGL(decode_attn_split_kernel, dim3(nsplit, B * H), dim3(NTH), 0, st, (const bf16_t*)Q,
+                       (const bf16_t*)Kn, (const bf16_t*)Vn, (bf16_t*)K, (bf16_t*)V, (bf16_t*)O, ws, pos, S, H, D,
+                       scale, chunk);
+    if (nsplit > 1)
+      hipLaunchKernelGGL(decode_combine_kernel, dim3(B * H), dim3(128), 0, st, (const float*)ws, (bf16_t*)O, D,
+                         nsplit);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(decode_attn_kernel, dim3(B * H), dim3(NTH), 0, st, (const bf16_t*)Q, (const bf16_t*)Kn,
                      (const bf16_t*)Vn, (bf16_t*)K, (bf16_t*)V, (bf16_t*)O, pos, S, H, D, scale);
   return (int)hipGetLastError();

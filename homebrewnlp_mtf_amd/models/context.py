@@ -37,11 +37,25 @@ class KVCache:
     layers run over the whole context and keep k / v [B, S, H, D]; "decode": the input is one token per row at
     position ``pos[b]``, whose k / v are appended to the caches and whose query attends over keys [0, pos[b]]."""
 
-    def __init__(self):
+    def __init__(self, persist: typing.Optional[dict] = None):
         self.layers: typing.Dict[int, typing.Tuple[torch.Tensor, torch.Tensor, float]] = {}
         self.mode = "prefill"
         self.pos: typing.Optional[torch.Tensor] = None
         self.idx = 0
+        # state that outlives one request: cache buffers per layer (reused while the shape stays) and the decode
+        # step's hipGraph (Model._decode_graphed), which bakes their addresses in
+        self.persist = persist if persist is not None else {"bufs": {}, "graph": None}
+
+    def keep(self, i: int, k: torch.Tensor, v: torch.Tensor, scale: float):
+        bufs = self.persist["bufs"]
+        old = bufs.get(i)
+        if old is not None and old[0].shape == k.shape and old[0].dtype == k.dtype and old[0].device == k.device:
+            old[0].copy_(k)
+            old[1].copy_(v)
+        else:
+            old = bufs[i] = (k, v)
+            self.persist["graph"] = None
+        self.layers[i] = (old[0], old[1], scale)
 
 
 class Builder:

@@ -450,7 +450,7 @@ def _attention_kv(kv, x: Act, w_in, ws, w_in_dims, base_dims, w_out_dims, act_in
     i = kv.idx
     kv.idx += 1
     if kv.mode == "prefill":
-        kv.layers[i] = (k, v, scale)     # the scale may depend on the context length (attention_scale "sequence")
+        kv.keep(i, k, v, scale)          # the scale may depend on the context length (attention_scale "sequence")
         return Act(F.attention_core(q, k, v, scale, True), x.dims)
     K, V, scale = kv.layers[i]
     B, S, H, Dh = K.shape

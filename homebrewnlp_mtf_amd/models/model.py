@@ -119,7 +119,9 @@ class Model:
     def prefill(self, token_x: torch.Tensor, positions: torch.Tensor) -> torch.Tensor:
         """Start incremental decoding: one forward over the whole context that fills the per-layer KV caches;
         returns the logits at ``positions`` ([B, 1, patch, vocab])"""
-        kv = KVCache()
+        if not hasattr(self, "_kv_persist"):
+            self._kv_persist = {"bufs": {}, "graph": None}
+        kv = KVCache(self._kv_persist)
         self.builder.kv = kv
         try:
             out = self.logits(token_x, positions=positions)
@@ -139,8 +141,38 @@ class Model:
         kv = self.builder.kv
         if kv is None or kv.mode != "decode":
             raise RuntimeError("decode() needs prefill() first")
+        if self.device.type == "cuda" and getattr(self.params, "decode_hip_graphs", True):
+            return self._decode_graphed(kv, tokens, positions)
         kv.pos = positions.to(self.device, torch.int64).contiguous()
         return self.logits(tokens)
+
+    def _decode_graphed(self, kv: KVCache, tokens: torch.Tensor, positions: torch.Tensor) -> torch.Tensor:
+        """A decode step is ~25 small launches per layer at sequence length 1: launch-bound. It is captured once per
+        batch shape and cache layout in a hipGraph and replayed, across requests too (KVCache.persist); tokens /
+        positions go through static device buffers, the KV caches keep fixed addresses and the decode kernel reads
+        the positions from device memory. A re-run of a step is idempotent (the cache append rewrites the same
+        k / v), so the eager warm-up runs feed the very step they warm up. The returned logits are the graph's
+        static output: valid until the next step."""
+        g = kv.persist["graph"]
+        if g is None or g["shape"] != tuple(tokens.shape):
+            tok = tokens.to(self.device).clone()
+            kv.pos = positions.to(self.device, torch.int64).clone()
+            side = torch.cuda.Stream(self.device)
+            side.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(side):
+                for _ in range(2):     # first-use GEMM plans, workspaces, allocator growth
+                    self.logits(tok)
+            torch.cuda.current_stream(self.device).wait_stream(side)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                out = self.logits(tok)
+            g = kv.persist["graph"] = {"shape": tuple(tokens.shape), "graph": graph, "tok": tok, "pos": kv.pos,
+                                       "out": out}
+        else:
+            g["tok"].copy_(tokens, non_blocking=True)
+            g["pos"].copy_(positions, non_blocking=True)
+        g["graph"].replay()
+        return g["out"]
 
     def end_decode(self):
         self.builder.kv = None

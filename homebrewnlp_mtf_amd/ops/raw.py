@@ -887,8 +887,12 @@ def decode_attn(q, kn, vn, k, v, o, pos, B: int, S: int, H: int, D: int, scale: 
         for nm, t, n in (("q", q, B * H * D), ("kn", kn, B * H * D), ("vn", vn, B * H * D), ("k", k, B * S * H * D),
                          ("v", v, B * S * H * D), ("o", o, B * H * D)):
             _need(t, n - 1, nm)
+        # key splits so that the grid has >= ~2048 blocks (8 per CU), each split >= 64 keys
+        nsplit = max(1, min(-(-2048 // (B * H)), -(-S // 64))) if D % 8 == 0 else 1
+        ws = torch.empty(B * H * nsplit * (D + 2) if nsplit > 1 else 1, dtype=torch.float32, device=q.device)
         L.check(L.lib().obst_decode_attn(q.data_ptr(), kn.data_ptr(), vn.data_ptr(), k.data_ptr(), v.data_ptr(),
-                                         o.data_ptr(), pos.data_ptr(), B, S, H, D, float(scale), L.stream_ptr()),
+                                         o.data_ptr(), pos.data_ptr(), B, S, H, D, float(scale), nsplit,
+                                         ws.data_ptr(), L.stream_ptr()),
                 "decode_attn")
         return None
     kc, vc = k.view(B, S, H, D), v.view(B, S, H, D)

@@ -190,15 +190,17 @@ def test_layers_gpu_match_cpu(cuda, layer):
     assert cos > 0.97, (layer, cos)
 
 
-@pytest.mark.parametrize("D", [64, 128, 48])
-def test_decode_attn_kernel(cuda, D):
+@pytest.mark.parametrize("D", [64, 128, 48, 50])
+@pytest.mark.parametrize("S", [300, 40])
+def test_decode_attn_kernel(cuda, D, S):
     """KV-cache decode attention kernel vs the fp32 torch oracle: cache append at pos[b] and the softmax over
-    keys [0, pos[b]], with per-row positions (incl. an out-of-range row that must stay untouched)"""
+    keys [0, pos[b]], with per-row positions (incl. an out-of-range row that must stay untouched); S=300 runs the
+    split-K kernel + combine, S=40 a single split, D=50 the generic kernel"""
     torch.manual_seed(6)
-    B, S, H = 5, 300, 3
+    B, H = 5, 3
     q, kn, vn = (torch.randn(B, H, D).to(BF) for _ in range(3))
     K0, V0 = (torch.randn(B, S, H, D).to(BF) for _ in range(2))
-    pos = torch.tensor([0, 7, 299, 150, 300], dtype=torch.int64)
+    pos = torch.tensor([0, 7, S - 1, S // 2, S], dtype=torch.int64)
     res = {}
     for dev in ("cpu", cuda):
         K, V = K0.clone().to(dev), V0.clone().to(dev)
