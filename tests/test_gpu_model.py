@@ -125,3 +125,15 @@ def test_jannet_gpu_matches_cpu(cuda):
     gc, gg = m_cpu.store.grad, m_gpu.store.grad.cpu()
     cos = torch.nn.functional.cosine_similarity(gc, gg, dim=0).item()
     assert cos > 0.98, cos
+
+
+@pytest.mark.parametrize("shape", [(8192, 2048), (2048, 2048), (512, 64)])
+def test_gpu_orthogonal_init_matches_householder(cuda, shape):
+    """GPU init (CholeskyQR2, fp64) == the CPU sign-corrected Householder Q of the same Gaussian block."""
+    from homebrewnlp_mtf_amd.models.variables import orthonormal_columns
+    g = torch.randn(*shape, generator=torch.Generator().manual_seed(shape[1]))
+    ref = orthonormal_columns(g.double()).float()   # fp64 Householder: Q's sensitivity grows with cond(g)
+    q = orthonormal_columns(g.to(cuda)).cpu()
+    assert (q - ref).abs().max().item() < 1e-3
+    eye = torch.eye(shape[1])
+    assert (q.t() @ q - eye).abs().max().item() < 1e-4

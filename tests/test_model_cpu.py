@@ -400,3 +400,15 @@ def test_video_sampling_and_render(tmp_path):
                                    save_prefix=str(tmp_path / "s"))
     gif = Image.open(paths[0])
     assert gif.n_frames == 4 and gif.size == (2 * 16 * 4, 8 * 4)
+
+
+def test_cholesky_qr2_matches_sign_corrected_householder():
+    """The GPU init path (CholeskyQR2, fp64) returns the same Q as the reference's sign-corrected Householder QR."""
+    from homebrewnlp_mtf_amd.models.variables import cholesky_qr2, orthonormal_columns
+    for shape in ((512, 128), (256, 256)):
+        x = torch.randn(*shape, generator=torch.Generator().manual_seed(shape[1]))
+        ref = orthonormal_columns(x)          # CPU: Householder
+        q = cholesky_qr2(x)
+        assert q is not None
+        assert (q - ref).abs().max().item() < 1e-4
+        assert torch.allclose(q.t() @ q, torch.eye(shape[1]), atol=1e-5)
