@@ -349,3 +349,18 @@ def test_token_mixer_big_tiles(cuda, causal):
     _close(y, ref, 5e-2, 3e-2, "mixer y")
     _close(xg.grad, xf.grad, 5e-2, 3e-2, "mixer dx")
     _close(wg.grad, wf.grad, 1e-1, 3e-2, "mixer dw")
+
+
+@pytest.mark.parametrize("M,K,N", [(1, 2048, 2048), (7, 100, 64), (16, 2048, 8192), (32, 8192, 2048),
+                                   (32, 2048, 6144), (20, 1000, 1032)])
+def test_skinny_gemm_matches_fp32(cuda, M, K, N, monkeypatch):
+    """decode-step GEMM (M <= 32 tokens) on csrc/kernels/skinny.hip vs a PyTorch fp32 reference"""
+    monkeypatch.setattr(raw, "_SKINNY", True)
+    g = torch.Generator().manual_seed(M * 7 + K)
+    a = torch.randn(M, K, generator=g).bfloat16()
+    w = (torch.randn(K, N, generator=g) / math.sqrt(K)).bfloat16()
+    c = torch.full((M * N,), float("nan"), dtype=torch.bfloat16, device=cuda)
+    raw.gemm(raw.Operand(a.to(cuda).flatten(), 0, K), raw.Operand(w.to(cuda).flatten(), 1, N),
+             raw.Operand(c, 0, N), M, N, K)
+    ref = a.float() @ w.float()
+    _close(c.view(M, N).float().cpu(), ref, 2e-2, 2e-2, f"skinny {M}x{K}x{N}")
