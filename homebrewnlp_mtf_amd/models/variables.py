@@ -63,6 +63,11 @@ def _seed_for(name: str, base_seed: int) -> int:
     return int.from_bytes(hashlib.sha256(f"{base_seed}/{name}".encode()).digest()[:7], "little")
 
 
+# opt-in (OBST_CHOLQR_INIT=1): with it on, test_hip_graph_step_matches_eager[none] failed once (graph vs eager master
+# weights 5e-4 apart after 7 steps, eager vs eager 6e-8) -- cause not yet isolated, so Householder stays the default
+_CHOLQR = __import__("os").environ.get("OBST_CHOLQR_INIT", "0") == "1"
+
+
 def orthonormal_columns(g: torch.Tensor) -> torch.Tensor:
     """Q of the QR factorisation of a tall ``g`` [m, n] (m >= n) with R's diagonal made positive -- the unique
     orthonormal basis the reference's sign-corrected Householder QR returns.
@@ -71,8 +76,9 @@ def orthonormal_columns(g: torch.Tensor) -> torch.Tensor:
     Householder QR of a 8192x2048 block issues tens of thousands of tiny launches (1.58 M launches, 7.6 s of GPU time
     for GPT-Neo-1.3B init, profiles/r1h_decode_kv.md), whereas this is a handful of GEMM-shaped calls. Cholesky's R
     has a positive diagonal, so Q is the same matrix as the sign-corrected Householder Q up to rounding. Falls back to
-    Householder if the Gram matrix is numerically not positive definite. The CPU path keeps Householder QR."""
-    if g.device.type == "cuda":
+    Householder if the Gram matrix is numerically not positive definite. The CPU path keeps Householder QR.
+    GPU CholeskyQR2 is opt-in (``_CHOLQR``)."""
+    if g.device.type == "cuda" and _CHOLQR:
         q = cholesky_qr2(g)
         if q is not None:
             return q
