@@ -235,6 +235,9 @@ int obst_blaslt_gemm(const ObstGemmDesc* d, hipStream_t stream) {
     } else {
       return 1;
     }
+    // a K-contiguous ([N][K], hipBLASLt op T) B together with a broadcast (stride 0) A faulted with an illegal
+    // address on gfx950 / ROCm 7.2 (M 131072, N 2048, K 4096, batch 3): never issue it; the MFMA kernel runs it
+    if (d->b_t == 0 && (sa == 0 || sb == 0)) return 1;
   }
   State& S = state();
   std::lock_guard<std::mutex> g(S.mu);

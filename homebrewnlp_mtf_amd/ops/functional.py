@@ -94,6 +94,11 @@ def linear_plan(xdims: tuple, wdims: tuple, odims: tuple) -> LinearPlan:
 # with hipBLASLt off, the weight gradient also reads token-contiguous transposes of x and dy
 # (`OBST_TRANSPOSED_OPERANDS=0` turns the copies off for A/B measurements).
 _KCONTIG = __import__("os").environ.get("OBST_TRANSPOSED_OPERANDS", "1") != "0"
+# hipBLASLt forward GEMMs also read the cached [N][K] weight copy: on the GPT-Neo-1.3B step the same product runs
+# 1444 TF/s with the weight K-contiguous against 1256 TF/s on the stored [K][N] layout (tools/gemm_census.py,
+# profiles/r2_gemm_census.md); refreshing every copy costs one transpose pass over the bf16 weights per step (~1 ms).
+# Only token-rich products (training, prefill): a decode step streams each weight once either way.
+_FWD_WT = __import__("os").environ.get("OBST_FWD_WT", "1") != "0"
 
 
 def _wT(w, plan: LinearPlan, act=None, has_r: bool = False):
@@ -101,7 +106,8 @@ def _wT(w, plan: LinearPlan, act=None, has_r: bool = False):
     if not _KCONTIG or store is None or not raw.on_gpu(w) or w.dtype != torch.bfloat16:
         return None
     if raw.lt_enabled() and (act is None or (act == "gelu" and not has_r)):   # runs on hipBLASLt (blaslt.cpp)
-        return None
+        if not (_FWD_WT and plan.M >= 4096):
+            return None
     if plan.K % 8 or plan.N % 8:
         return None
     return store.transposed(w.var_name, plan.H, plan.K, plan.N)
@@ -379,6 +385,13 @@ def _qkv_fwd(base, ws, out, p: LinearPlan):
             and all(w.is_contiguous() for w in ws))
     if same:
         wt = _wT(ws[0], p)
+        if wt is not None and raw.lt_enabled():
+            # hipBLASLt on the K-contiguous copies: three plain products (1478 TF/s each on GPT-Neo-1.3B against
+            # 1307 TF/s for the batched product on the [K][N] weights; hipBLASLt faults on a batched [N][K] B with
+            # a shared A, so that combination is never issued -- blaslt.cpp declines it)
+            for j in range(3):
+                _fwd_gemm(base, ws[j], out[j], p)
+            return
         if wt is not None:
             for j in (1, 2):
                 _wT(ws[j], p)           # refresh the neighbours' transposed copies too

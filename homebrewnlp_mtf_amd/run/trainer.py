@@ -134,13 +134,7 @@ class Trainer:
                 self.global_step += 1
                 metrics["learning_rate"] = torch.tensor(lr)
                 return metrics
-            graph = torch.cuda.CUDAGraph()
-            torch.cuda.synchronize(self.device)
-            with torch.cuda.graph(graph, pool=g["pool"]):
-                out = self._step_body(g["inputs"], lr)
-            self.opt.flip = parity   # capture ran the host side of the step (buffer flip) but executed nothing
-            g["graphs"][parity] = (graph, out)
-            log(f"captured the training step in a hipGraph (SM3 parity {parity})")
+            self._capture(parity, lr)
         graph, out = g["graphs"][parity]
         graph.replay()
         self.opt.flip = 1 - parity
@@ -149,6 +143,30 @@ class Trainer:
         metrics = {k: v.clone() for k, v in out.items()}
         metrics["learning_rate"] = torch.tensor(lr)
         return metrics
+
+    def _capture(self, parity: int, lr: float):
+        """record the step for SM3 buffer parity ``parity`` (capture executes nothing on the device)"""
+        g = self._graph
+        keep = self.opt.flip
+        self.opt.flip = parity
+        graph = torch.cuda.CUDAGraph()
+        torch.cuda.synchronize(self.device)
+        with torch.cuda.graph(graph, pool=g["pool"]):
+            out = self._step_body(g["inputs"], lr)
+        self.opt.flip = keep     # capture ran the host side of the step (buffer flip) but executed nothing
+        g["graphs"][parity] = (graph, out)
+        log(f"captured the training step in a hipGraph (SM3 parity {parity})")
+
+    def prepare_graphs(self) -> bool:
+        """capture every parity's graph that the eager warm-up has not produced yet, so timed steps are replays
+        only (benchmarks call this after their warm-up steps). False if graphs are not in use or not warm yet."""
+        g = getattr(self, "_graph", None)
+        if not (self.params.use_hip_graphs and self._graphs_ok()) or g is None or g["warm"] < 2:
+            return False
+        for parity in (0, 1):
+            if parity not in g["graphs"]:
+                self._capture(parity, learning_rate(self.params, self.global_step))
+        return True
 
     # ---------------------------------------------------------------------------------------------------------------
     def _multi_loss_step(self, batch):
