@@ -237,8 +237,9 @@ __global__ __launch_bounds__(NTH) void moe_bwd_kernel(const bf16_t* __restrict__
                                                       const float* __restrict__ P, bf16_t* __restrict__ DU,
                                                       bf16_t* __restrict__ DLg, long long T, int N, int E) {
   __shared__ float dp_s[512];
+  __shared__ float dpp[NTH * 8];   // [row group][E] partial dp sums, added in row-group order (no LDS atomics)
   __shared__ float red[NW];
-  const int tid = threadIdx.x, lpr = E >> 3, c = tid & (lpr - 1);
+  const int tid = threadIdx.x, lpr = E >> 3, c = tid & (lpr - 1), rg = tid / lpr, nrg = NTH / lpr;
   for (long long t = blockIdx.x; t < T; t += gridDim.x) {
     for (int e = tid; e < E; e += NTH) dp_s[e] = 0.f;
     float pc[8], dp[8];
@@ -255,7 +256,13 @@ __global__ __launch_bounds__(NTH) void moe_bwd_kernel(const bf16_t* __restrict__
       *reinterpret_cast<uint4*>(DU + o) = pack8(g);
     }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) atomicAdd(&dp_s[c * 8 + j], dp[j]);
+    for (int j = 0; j < 8; ++j) dpp[rg * E + c * 8 + j] = dp[j];
+    __syncthreads();
+    for (int e = tid; e < E; e += NTH) {
+      float v = 0.f;
+      for (int r = 0; r < nrg; ++r) v += dpp[r * E + e];
+      dp_s[e] = v;
+    }
     __syncthreads();
     float s = 0.f;
     for (int e = tid; e < E; e += NTH) s += P[t * E + e] * dp_s[e];

@@ -65,9 +65,10 @@ __global__ __launch_bounds__(NTH) void ew_kernel(int op_rt, int act_rt, const bf
   }
 }
 
-// sum of x*dy over all elements into out[0] (rezero gradient: d g = sum(x * dy))
+// sum of x*dy over all elements (rezero gradient: d g = sum(x * dy)): one partial per block into part[blockIdx.x],
+// then dot_fold_kernel adds the partials to out[0] in block order (bitwise reproducible, no float atomics)
 __global__ __launch_bounds__(NTH) void dot_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ DY,
-                                                  float* __restrict__ out, long long nvec) {
+                                                  float* __restrict__ part, long long nvec) {
   __shared__ float red[4];
   float acc = 0.f;
   for (long long v = (long long)blockIdx.x * NTH + threadIdx.x; v < nvec; v += (long long)gridDim.x * NTH) {
@@ -78,7 +79,16 @@ __global__ __launch_bounds__(NTH) void dot_kernel(const bf16_t* __restrict__ X, 
     for (int j = 0; j < 8; ++j) acc += x[j] * d[j];
   }
   acc = block_sum<4>(acc, red);
-  if (threadIdx.x == 0) atomicAdd(out, acc);
+  if (threadIdx.x == 0) part[blockIdx.x] = acc;
+}
+
+// out[0] += sum of part[0..n) in a fixed order (one block: strided per-thread sums, then the block tree)
+__global__ __launch_bounds__(NTH) void dot_fold_kernel(const float* __restrict__ part, int n, float* __restrict__ out) {
+  __shared__ float red[4];
+  float acc = 0.f;
+  for (int i = threadIdx.x; i < n; i += NTH) acc += part[i];
+  acc = block_sum<4>(acc, red);
+  if (threadIdx.x == 0) out[0] += acc;
 }
 
 // out[t, :] = E[idx[t], :]   (E bf16 [V, F], F % 8 == 0)
@@ -105,6 +115,37 @@ __global__ __launch_bounds__(NTH) void scatter_add_kernel(const int* __restrict_
     int r = idx[t];
     r = r < 0 ? 0 : (r >= V ? V - 1 : r);
     atomicAdd(dE + (long long)r * F + c, bf2f(DY[e]));
+  }
+}
+
+// Deterministic embedding gradient: the token ids are sorted (stable) on the host side's stream, so the rows
+// that add into one table row form a segment of the sorted order. One block per sorted position; the block that
+// starts a segment sums the segment's dy rows in sorted order (8 columns per lane, 16-byte loads) and adds the sum
+// to its table row -- every row is owned by one block, so the result is bitwise reproducible (no float atomics).
+__global__ __launch_bounds__(NTH) void scatter_sorted_kernel(const int* __restrict__ sidx,
+                                                             const long long* __restrict__ perm,
+                                                             const bf16_t* __restrict__ DY, float* __restrict__ dE,
+                                                             long long T, int F) {
+  const long long i = blockIdx.x;
+  const int r = sidx[i];
+  if (i > 0 && sidx[i - 1] == r) return;
+  long long j = i + 1;
+  while (j < T && sidx[j] == r) ++j;
+  float* row = dE + (long long)r * F;
+  for (int c0 = threadIdx.x * 8; c0 < F; c0 += NTH * 8) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (long long k = i; k < j; ++k) {
+      float d[8];
+      unpack8(*reinterpret_cast<const uint4*>(DY + perm[k] * F + c0), d);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += d[e];
+    }
+    float4* o = reinterpret_cast<float4*>(row + c0);
+    float4 a = o[0], b = o[1];
+    a.x += acc[0]; a.y += acc[1]; a.z += acc[2]; a.w += acc[3];
+    b.x += acc[4]; b.y += acc[5]; b.z += acc[6]; b.w += acc[7];
+    o[0] = a;
+    o[1] = b;
   }
 }
 
@@ -189,9 +230,14 @@ OBST_API int obst_elementwise(const ObstEwDesc* d, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
-OBST_API int obst_dot(const void* X, const void* DY, float* out, long long n, hipStream_t st) {
+// part: obst_dot_parts(n) floats of workspace
+OBST_API int obst_dot_parts(long long n) { return grid_for(n / 8); }
+
+OBST_API int obst_dot(const void* X, const void* DY, float* out, float* part, long long n, hipStream_t st) {
   if (n % 8) return -1;
-  hipLaunchKernelGGL(dot_kernel, dim3(grid_for(n / 8)), dim3(NTH), 0, st, (const bf16_t*)X, (const bf16_t*)DY, out, n / 8);
+  const int g = grid_for(n / 8);
+  hipLaunchKernelGGL(dot_kernel, dim3(g), dim3(NTH), 0, st, (const bf16_t*)X, (const bf16_t*)DY, part, n / 8);
+  hipLaunchKernelGGL(dot_fold_kernel, dim3(1), dim3(NTH), 0, st, part, g, out);
   return (int)hipGetLastError();
 }
 
@@ -204,6 +250,16 @@ OBST_API int obst_gather(const int* idx, const void* E, void* out, long long T, 
 
 OBST_API int obst_scatter_add(const int* idx, const void* DY, float* dE, long long T, int F, int V, hipStream_t st) {
   hipLaunchKernelGGL(scatter_add_kernel, dim3(grid_for(T * F)), dim3(NTH), 0, st, idx, (const bf16_t*)DY, dE, T, F, V);
+  return (int)hipGetLastError();
+}
+
+// sidx: token ids sorted ascending (already clamped to [0, V)); perm: their positions (int64, stable order)
+OBST_API int obst_scatter_add_sorted(const int* sidx, const long long* perm, const void* DY, float* dE, long long T,
+                                     int F, hipStream_t st) {
+  if (F % 8 || T <= 0) return -1;
+  if ((((uintptr_t)DY) | ((uintptr_t)dE)) & 15) return -2;
+  hipLaunchKernelGGL(scatter_sorted_kernel, dim3((unsigned)T), dim3(NTH), 0, st, sidx, perm, (const bf16_t*)DY, dE,
+                     T, F);
   return (int)hipGetLastError();
 }
 

@@ -4,7 +4,9 @@
 // rows are (token, head) pairs and the [heads, F] scale/shift is indexed by row % groups).
 // One wave per row, the row held in registers (16-byte bf16 vector loads, Guideline 13), two-pass statistics,
 // fp32 math. Backward: dx = rstd * (dxh - mean(dxh) - xh * mean(dxh * xh)); scale/shift gradients are summed per
-// block in registers and added to the fp32 gradient buffer with one atomic per element per block.
+// lane group in registers, stored as per-block (groups == 1) or per-lane-group partial slabs, and folded into the
+// fp32 gradient buffer by norm_fold_kernel in a fixed order -- no float atomics, so the gradients (and with them the
+// whole training step) are bitwise reproducible run to run and between eager and hipGraph replay.
 // A split "row statistics" path (partial sums -> all-reduce over the TP group -> apply) serves the non-group
 // norm when `heads` is split across ranks (collective X05).
 #include "common.h"
@@ -162,7 +164,7 @@ __global__ __launch_bounds__(NTH) void norm_bwd_kernel(const bf16_t* __restrict_
                                                        float* __restrict__ dshift, long long rows, int F, int groups,
                                                        int Ffull, float* __restrict__ partial_out,
                                                        const float* __restrict__ ext_dsum,
-                                                       const bf16_t* __restrict__ R) {
+                                                       const bf16_t* __restrict__ R, float* __restrict__ ws) {
   constexpr int RPW = 64 / LPR;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* red_s = reinterpret_cast<float*>(smem);           // [4 waves][F] dscale partials, then dshift
@@ -241,24 +243,23 @@ __global__ __launch_bounds__(NTH) void norm_bwd_kernel(const bf16_t* __restrict_
     }
   }
   if (want_param && groups > 1) {
-    // one atomic per element per lane group into its group of the [groups, F] parameters
-    if (first < rows) {
-      const long long poff = (long long)(first % groups) * F;
+    // lane group `first` (its rows are first, first + nw, ... -- all of group first % groups) stores its partial
+    // sums as row `first` of the [nw][2F] slab (lane groups without rows store zeros)
+    float* wr = ws + first * 2 * F;
 #pragma unroll
-      for (int c = 0; c < NCH; ++c)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int col = c * LPR * 8 + sl * 8 + j;
-          if (col < F) {
-            if (dscale) atomicAdd(dscale + poff + col, gs[c][j]);
-            if (dshift) atomicAdd(dshift + poff + col, gb[c][j]);
-          }
-        }
+    for (int c = 0; c < NCH; ++c) {
+      const int col = c * LPR * 8 + sl * 8;
+      if (col < F) {
+        *reinterpret_cast<float4*>(wr + col) = make_float4(gs[c][0], gs[c][1], gs[c][2], gs[c][3]);
+        *reinterpret_cast<float4*>(wr + col + 4) = make_float4(gs[c][4], gs[c][5], gs[c][6], gs[c][7]);
+        *reinterpret_cast<float4*>(wr + F + col) = make_float4(gb[c][0], gb[c][1], gb[c][2], gb[c][3]);
+        *reinterpret_cast<float4*>(wr + F + col + 4) = make_float4(gb[c][4], gb[c][5], gb[c][6], gb[c][7]);
+      }
     }
   }
   if (want_param && groups == 1) {
     // fold the row-groups of the wave, then per chunk reduce the 4 waves through LDS ([2][4][LPR*8] floats) and
-    // issue one atomic per element per block
+    // store the block's partial sums as row blockIdx.x of the [grid][2F] slab
     constexpr int CW = LPR * 8;
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
@@ -273,12 +274,45 @@ __global__ __launch_bounds__(NTH) void norm_bwd_kernel(const bf16_t* __restrict_
         if (col < F) {
           const float a = red_s[k] + red_s[CW + k] + red_s[2 * CW + k] + red_s[3 * CW + k];
           const float b = red_s[4 * CW + k] + red_s[5 * CW + k] + red_s[6 * CW + k] + red_s[7 * CW + k];
-          if (dscale) atomicAdd(dscale + col, a);
-          if (dshift) atomicAdd(dshift + col, b);
+          ws[(long long)blockIdx.x * 2 * F + col] = a;
+          ws[(long long)blockIdx.x * 2 * F + F + col] = b;
         }
       }
       __syncthreads();
     }
+  }
+}
+
+// deterministic fold of the parameter-gradient slab: out[g][f] += sum over partial rows p = g, g + period, ... (in
+// order) of ws[p][which * F + f] for the scale (which 0) and shift (which 1) halves. Block = 32 output columns x 8
+// segments of the partial rows; the 8 segment sums are added in segment order.
+__global__ __launch_bounds__(NTH) void norm_fold_kernel(const float* __restrict__ ws, long long nparts, int period,
+                                                        int F, int groups, float* __restrict__ dscale,
+                                                        float* __restrict__ dshift) {
+  __shared__ float red[8][32];
+  const int c = threadIdx.x & 31, seg = threadIdx.x >> 5;
+  const long long o = (long long)blockIdx.x * 32 + c;
+  const long long nout = 2LL * groups * F;
+  float acc = 0.f;
+  int which = 0, g = 0, f = 0;
+  if (o < nout) {
+    which = (int)(o / ((long long)groups * F));
+    const int rem = (int)(o % ((long long)groups * F));
+    g = rem / F;
+    f = rem % F;
+    const long long K = nparts > g ? (nparts - g + period - 1) / period : 0;   // partial rows of this group
+    const long long k0 = K * seg / 8, k1 = K * (seg + 1) / 8;
+    const float* src = ws + (long long)which * F + f;
+    for (long long k = k0; k < k1; ++k) acc += src[(g + k * period) * 2 * F];
+  }
+  red[seg][c] = acc;
+  __syncthreads();
+  if (seg == 0 && o < nout) {
+    float s = red[0][c];
+#pragma unroll
+    for (int i = 1; i < 8; ++i) s += red[i][c];
+    float* dst = which ? dshift : dscale;
+    if (dst) dst[(long long)g * F + f] += s;
   }
 }
 
@@ -295,6 +329,7 @@ struct ObstNormDesc {
   float* partial; const float* ext;   // TP path
   long long rows; int F; int groups; int Ffull; float eps;
   const void* R;                      // backward: gradient added to DX (residual input of the block) or null
+  float* ws;                          // backward with parameter gradients: obst_norm_bwd_ws(desc) floats
 };
 
 #define NORM_DISPATCH_L(KERNEL, LPR, GRID, LDSB, ...)                                               \
@@ -334,11 +369,8 @@ OBST_API int obst_norm_partial(const ObstNormDesc* d, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
-OBST_API int obst_norm_bwd(const ObstNormDesc* d, hipStream_t st) {
-  if (d->F % 8 || d->rows <= 0) return -1;
-  const size_t lds = (d->groups == 1 && (d->dscale || d->dshift) && !d->partial)
-                         ? (size_t)8 * lanes_per_row(d->F) * 8 * 4 : 0;   // <= 16 KiB
-  // more rows per block amortises the parameter-gradient atomics; 2048 blocks keep ~8 waves per SIMD in flight
+static int norm_bwd_grid(const ObstNormDesc* d) {
+  // more rows per block shrinks the parameter-gradient slab; 2048 blocks keep ~8 waves per SIMD in flight
   long long g = (d->rows + 15) / 16;
   int grid = (int)(g < 2048 ? (g < 1 ? 1 : g) : 2048);
   if (d->groups > 1) {   // rows per grid step (4 waves x 64/LPR rows per block) must be a multiple of groups
@@ -347,8 +379,34 @@ OBST_API int obst_norm_bwd(const ObstNormDesc* d, hipStream_t st) {
     const int q = d->groups / a;                 // blocks per group period
     grid = grid < q ? q : grid / q * q;
   }
+  return grid;
+}
+
+static bool norm_bwd_params(const ObstNormDesc* d) { return (d->dscale || d->dshift) && !d->partial; }
+
+// floats of the parameter-gradient slab obst_norm_bwd needs in desc->ws (0: no parameter gradients)
+OBST_API long long obst_norm_bwd_ws(const ObstNormDesc* d) {
+  if (!norm_bwd_params(d) || d->F <= 0 || d->rows <= 0) return 0;
+  const long long grid = norm_bwd_grid(d);
+  const long long parts = d->groups > 1 ? grid * 4 * (64 / lanes_per_row(d->F)) : grid;
+  return parts * 2 * d->F;
+}
+
+OBST_API int obst_norm_bwd(const ObstNormDesc* d, hipStream_t st) {
+  if (d->F % 8 || d->rows <= 0) return -1;
+  const bool params = norm_bwd_params(d);
+  if (params && !d->ws) return -3;
+  const size_t lds = (d->groups == 1 && params) ? (size_t)8 * lanes_per_row(d->F) * 8 * 4 : 0;   // <= 16 KiB
+  const int grid = norm_bwd_grid(d);
   NORM_DISPATCH(norm_bwd_kernel, dim3(grid), lds, (const bf16_t*)d->X, (const bf16_t*)d->DY, d->scale, d->stats,
                 (bf16_t*)d->DX, d->dscale, d->dshift, d->rows, d->F, d->groups, d->Ffull, d->partial, d->ext,
-                (const bf16_t*)d->R);
+                (const bf16_t*)d->R, d->ws);
+  if (params) {
+    const long long parts = d->groups > 1 ? (long long)grid * 4 * (64 / lanes_per_row(d->F)) : grid;
+    const long long nout = 2LL * d->groups * d->F;
+    // a lane group's rows are p, p + nw, ... so partial row p belongs to group p % groups (nw % groups == 0)
+    hipLaunchKernelGGL(norm_fold_kernel, dim3((unsigned)((nout + 31) / 32)), dim3(NTH), 0, st, d->ws, parts,
+                       d->groups > 1 ? d->groups : 1, d->F, d->groups, d->dscale, d->dshift);
+  }
   return (int)hipGetLastError();
 }

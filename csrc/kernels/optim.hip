@@ -49,6 +49,7 @@ struct ApplyArgs {
   int final_seg, emit_stats, emit_factored;
   float lr, wd, rezero_mult, grad_scale, beta1, beta2, step_count;
   const float* dyn;           // device [lr, step_count] (graph replay: the host values change every step) or null
+  float* part; int part_base; // emit_stats: block b stores (sum x^2, sum x) at part[(part_base + b) * 4 + 0/1]
 };
 
 __device__ __forceinline__ float lr_of(const ApplyArgs& a) { return a.dyn ? a.dyn[0] : a.lr; }
@@ -345,7 +346,10 @@ __global__ __launch_bounds__(NTA) void opt_apply_kernel(ApplyArgs a) {
     __shared__ float red[8];
     s2 = block_sum<8>(s2, red);
     s1 = block_sum<8>(s1, red);
-    if (threadIdx.x == 0) { atomicAdd(a.stats + ck.t * 8 + 0, s2); atomicAdd(a.stats + ck.t * 8 + 1, s1); }
+    if (threadIdx.x == 0) {
+      a.part[(a.part_base + blockIdx.x) * 4 + 0] = s2;
+      a.part[(a.part_base + blockIdx.x) * 4 + 1] = s1;
+    }
   }
 }
 
@@ -676,13 +680,17 @@ __global__ __launch_bounds__(RW_NT) void opt_rows_kernel(ApplyArgs a, const RChu
     __shared__ float red[4];
     s2 = block_sum<4>(s2, red);
     s1 = block_sum<4>(s1, red);
-    if (threadIdx.x == 0) { atomicAdd(a.stats + ck.t * 8 + 0, s2); atomicAdd(a.stats + ck.t * 8 + 1, s1); }
+    if (threadIdx.x == 0) {
+      a.part[(a.part_base + blockIdx.x) * 4 + 0] = s2;
+      a.part[(a.part_base + blockIdx.x) * 4 + 1] = s1;
+    }
   }
 }
 
-// pass 0: sum g^2, sum g of the (scaled) raw gradient, sum w^2, sum w of the weights (float4 when aligned)
+// pass 0: sum g^2, sum g of the (scaled) raw gradient, sum w^2, sum w of the weights (float4 when aligned), one
+// partial per chunk into part[chunk][4]; opt_fold_kernel sums each tensor's chunks in chunk order (no atomics)
 __global__ __launch_bounds__(NTH) void opt_stats_kernel(const OptTensor* tensors, const Chunk* chunks,
-                                                        const float* grad, const float* master, float* stats,
+                                                        const float* grad, const float* master, float* part,
                                                         float grad_scale) {
   const Chunk ck = chunks[blockIdx.x];
   const OptTensor T = tensors[ck.t];
@@ -705,9 +713,26 @@ __global__ __launch_bounds__(NTH) void opt_stats_kernel(const OptTensor* tensors
   }
   __shared__ float red[4];
   a0 = block_sum<4>(a0, red); a1 = block_sum<4>(a1, red); a2 = block_sum<4>(a2, red); a3 = block_sum<4>(a3, red);
-  if (threadIdx.x == 0) {
-    float* s = stats + ck.t * 8;
-    atomicAdd(s + 0, a0); atomicAdd(s + 1, a1); atomicAdd(s + 2, a2); atomicAdd(s + 3, a3);
+  if (threadIdx.x == 0)
+    *reinterpret_cast<float4*>(part + (long long)blockIdx.x * 4) = make_float4(a0, a1, a2, a3);
+}
+
+// stats[t][j] = sum over the tensor's partial rows part[first .. first + count)[j] (j < ncols), in row order: one
+// wave per tensor, lane-strided sums combined by the (deterministic) butterfly
+__global__ __launch_bounds__(NTH) void opt_fold_kernel(const int* __restrict__ ranges, int ntensors,
+                                                       const float* __restrict__ part, float* __restrict__ stats,
+                                                       int ncols) {
+  const int t = blockIdx.x * (NTH / 64) + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (t >= ntensors) return;
+  const int first = ranges[2 * t], count = ranges[2 * t + 1];
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int i = lane; i < count; i += 64) {
+    const float4 v = *reinterpret_cast<const float4*>(part + (long long)(first + i) * 4);
+    acc[0] += v.x; acc[1] += v.y; acc[2] += v.z; acc[3] += v.w;
+  }
+  for (int j = 0; j < ncols; ++j) {
+    const float v = wave_sum(acc[j]);
+    if (lane == 0) stats[t * 8 + j] = v;
   }
 }
 
@@ -789,6 +814,8 @@ struct ObstOptDesc {
   float lr, wd, rezero_mult, grad_scale, beta1, beta2, step_count;
   int tp_size;
   const float* dyn;        // device [lr, step_count] or null (then lr / step_count above)
+  float* part;             // per-block partial statistics ([blocks][4] floats), folded by obst_opt_fold
+  int part_base;           // emit_stats of obst_opt_apply: first partial row of this launch's blocks
 };
 
 static_assert(sizeof(OptTensor) == 88, "OptTensor layout is mirrored in python (optim/fused.py)");
@@ -796,8 +823,17 @@ static_assert(sizeof(Chunk) == 24, "Chunk layout is mirrored in python (optim/fu
 static_assert(sizeof(RChunk) == 24, "RChunk layout is mirrored in python (optim/fused.py)");
 
 OBST_API int obst_opt_stats(const ObstOptDesc* d, hipStream_t s) {
+  if (!d->part) return -1;
   hipLaunchKernelGGL(opt_stats_kernel, dim3(d->nchunks), dim3(NTH), 0, s, (const OptTensor*)d->tensors,
-                     (const Chunk*)d->chunks, d->grad, d->master, d->stats, d->grad_scale);
+                     (const Chunk*)d->chunks, d->grad, d->master, d->part, d->grad_scale);
+  return (int)hipGetLastError();
+}
+
+// ranges: int32 [ntensors][2] = (first partial row, count) of each tensor
+OBST_API int obst_opt_fold(const ObstOptDesc* d, const int* ranges, int ncols, hipStream_t s) {
+  if (!d->part || ncols < 1 || ncols > 4) return -1;
+  hipLaunchKernelGGL(opt_fold_kernel, dim3((unsigned)((d->ntensors + 3) / 4)), dim3(NTH), 0, s, ranges,
+                     d->ntensors, d->part, d->stats, ncols);
   return (int)hipGetLastError();
 }
 
@@ -829,11 +865,13 @@ static ApplyArgs apply_args(const ObstOptDesc* d) {
   a.nst = d->nst; a.final_seg = d->final_seg; a.emit_stats = d->emit_stats; a.emit_factored = d->emit_factored;
   a.lr = d->lr; a.wd = d->wd; a.rezero_mult = d->rezero_mult; a.grad_scale = d->grad_scale;
   a.beta1 = d->beta1; a.beta2 = d->beta2; a.step_count = d->step_count; a.dyn = d->dyn;
+  a.part = d->part; a.part_base = d->part_base;
   return a;
 }
 
 OBST_API int obst_opt_apply(const ObstOptDesc* d, hipStream_t s) {
   if (d->nst > MAXST) return -1;
+  if (d->emit_stats && !d->part) return -3;
   if (d->nchunks <= 0) return 0;
   hipLaunchKernelGGL(opt_apply_kernel, dim3(d->nchunks), dim3(NTA), 0, s, apply_args(d));
   return (int)hipGetLastError();
@@ -842,6 +880,7 @@ OBST_API int obst_opt_apply(const ObstOptDesc* d, hipStream_t s) {
 // row-tiled apply (no Adafactor stages, no factored-stat emission); rchunks: RChunk[nrchunks]
 OBST_API int obst_opt_apply_rows(const ObstOptDesc* d, const void* rchunks, int nrchunks, hipStream_t s) {
   if (d->nst > MAXST || d->emit_factored) return -1;
+  if (d->emit_stats && !d->part) return -3;
   for (int i = 0; i < d->nst; ++i)
     if (d->stages[4 * i] == OP_ADAFACTOR || d->stages[4 * i] == OP_ADAFACTOR_CLIP) return -2;
   if (nrchunks <= 0) return 0;

@@ -56,7 +56,7 @@ class AttnDesc(ctypes.Structure):
 class NormDesc(ctypes.Structure):
     _fields_ = [("X", c_p), ("scale", c_p), ("shift", c_p), ("Y", c_p), ("stats", c_p),
                 ("DY", c_p), ("DX", c_p), ("dscale", c_p), ("dshift", c_p), ("partial", c_p), ("ext", c_p),
-                ("rows", c_ll), ("F", c_i), ("groups", c_i), ("Ffull", c_i), ("eps", c_f), ("R", c_p)]
+                ("rows", c_ll), ("F", c_i), ("groups", c_i), ("Ffull", c_i), ("eps", c_f), ("R", c_p), ("ws", c_p)]
 
 
 class EwDesc(ctypes.Structure):
@@ -71,7 +71,7 @@ class OptDesc(ctypes.Structure):
                 ("sm3_old", c_p), ("sm3_new", c_p), ("af_state", c_p), ("af_rows_sum", c_p), ("af_cols_sum", c_p),
                 ("stages", c_i * 32), ("nst", c_i), ("final_seg", c_i), ("emit_stats", c_i), ("emit_factored", c_i),
                 ("lr", c_f), ("wd", c_f), ("rezero_mult", c_f), ("grad_scale", c_f), ("beta1", c_f), ("beta2", c_f),
-                ("step_count", c_f), ("tp_size", c_i), ("dyn", c_p)]
+                ("step_count", c_f), ("tp_size", c_i), ("dyn", c_p), ("part", c_p), ("part_base", c_i)]
 
 
 _SIGS = {
@@ -81,8 +81,11 @@ _SIGS = {
     "obst_norm_fwd": [ctypes.POINTER(NormDesc), c_p],
     "obst_norm_bwd": [ctypes.POINTER(NormDesc), c_p],
     "obst_norm_partial": [ctypes.POINTER(NormDesc), c_p],
+    "obst_norm_bwd_ws": [ctypes.POINTER(NormDesc)],
     "obst_elementwise": [ctypes.POINTER(EwDesc), c_p],
-    "obst_dot": [c_p, c_p, c_p, c_ll, c_p],
+    "obst_dot": [c_p, c_p, c_p, c_p, c_ll, c_p],
+    "obst_dot_parts": [c_ll],
+    "obst_scatter_add_sorted": [c_p, c_p, c_p, c_p, c_ll, c_i, c_p],
     "obst_gather": [c_p, c_p, c_p, c_ll, c_i, c_i, c_p],
     "obst_scatter_add": [c_p, c_p, c_p, c_ll, c_i, c_i, c_p],
     "obst_cumsum": [c_p, c_p, c_ll, c_i, c_ll, c_i, c_i, c_i, c_p],
@@ -94,6 +97,7 @@ _SIGS = {
     "obst_opt_stats": [ctypes.POINTER(OptDesc), c_p],
     "obst_opt_scalar": [ctypes.POINTER(OptDesc), c_p],
     "obst_opt_apply": [ctypes.POINTER(OptDesc), c_p],
+    "obst_opt_fold": [ctypes.POINTER(OptDesc), c_p, c_i, c_p],
     "obst_opt_apply_rows": [ctypes.POINTER(OptDesc), c_p, c_i, c_p],
     "obst_blaslt_enabled": [],
     "obst_blaslt_set": [c_i],
@@ -112,6 +116,7 @@ _SIGS = {
     "obst_skinny_gemm": [c_p, c_i, c_p, c_i, c_p, c_i, c_i, c_i, c_i, c_p, c_p],
     "obst_decode_attn": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_f, c_i, c_p, c_p],
 }
+_RESTYPES = {"obst_norm_bwd_ws": c_ll}
 
 
 def lib():
@@ -129,7 +134,7 @@ def lib():
             for name, args in _SIGS.items():
                 fn = getattr(handle, name)
                 fn.argtypes = args
-                fn.restype = c_i
+                fn.restype = _RESTYPES.get(name, c_i)
             _lib = handle
     return _lib
 

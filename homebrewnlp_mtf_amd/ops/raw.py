@@ -375,6 +375,9 @@ def norm_bwd(x, dy, scale, stats, dx, dscale, dshift, rows: int, F: int, groups:
             _need(R, rows * F - 1, "R")
         d = L.NormDesc(x.data_ptr(), L.ptr(scale), 0, 0, stats.data_ptr(), dy.data_ptr(), L.ptr(dx), L.ptr(dscale),
                        L.ptr(dshift), L.ptr(partial), L.ptr(ext_dsum), rows, F, groups, Ffull, EPS, L.ptr(R))
+        nws = int(L.lib().obst_norm_bwd_ws(d))
+        ws = torch.empty(max(nws, 1), dtype=torch.float32, device=x.device) if nws else None
+        d.ws = L.ptr(ws)     # parameter-gradient partial slab, folded in a fixed order (no float atomics)
         L.check(L.lib().obst_norm_bwd(d, L.stream_ptr()), "norm_bwd")
         return
     xv = _f(x.reshape(rows, F))
@@ -479,7 +482,9 @@ def dot(x, dy, out):
         n = x.numel()
         if n % 8:
             raise L.KernelError("dot size must be a multiple of 8")
-        L.check(L.lib().obst_dot(x.data_ptr(), dy.data_ptr(), out.data_ptr(), n, L.stream_ptr()), "dot")
+        part = torch.empty(int(L.lib().obst_dot_parts(n)), dtype=torch.float32, device=x.device)
+        L.check(L.lib().obst_dot(x.data_ptr(), dy.data_ptr(), out.data_ptr(), part.data_ptr(), n, L.stream_ptr()),
+                "dot")
         return
     out.view(-1)[0] += (_f(x) * _f(dy)).sum()
 
@@ -554,6 +559,12 @@ def scatter_add(idx, dy, dtable, T: int, F: int, V: int):
         _need(idx, T - 1, "idx")
         _need(dy, T * F - 1, "dy")
         _need(dtable, V * F - 1, "dtable")
+        if F % 8 == 0 and dy.data_ptr() % 16 == 0 and dtable.data_ptr() % 16 == 0:
+            # deterministic: stable sort of the (clamped) ids, then one owner block per table row
+            sidx, perm = torch.sort(idx.reshape(-1)[:T].clamp(0, V - 1).to(torch.int32), stable=True)
+            L.check(L.lib().obst_scatter_add_sorted(sidx.data_ptr(), perm.data_ptr(), dy.data_ptr(),
+                                                    dtable.data_ptr(), T, F, L.stream_ptr()), "scatter_add_sorted")
+            return
         L.check(L.lib().obst_scatter_add(idx.data_ptr(), dy.data_ptr(), dtable.data_ptr(), T, F, V, L.stream_ptr()),
                 "scatter_add")
         return

@@ -175,6 +175,24 @@ class FusedOptimizer:
                 for row0 in range(0, R, per):
                     rchunks.append(struct.pack("<6i", ti, row0, min(per, R - row0), col0, ncols, vec))
         self.nrchunks, self.nschunks = len(rchunks), len(schunks)
+        # per-tensor (first, count) partial rows for the deterministic statistics fold (optim.hip opt_fold_kernel):
+        # over the chunk table, and over [row-tiled chunks..., generic chunks...] for the row-tiled apply
+        tid = lambda c: struct.unpack_from("<i", c)[0]  # noqa: E731
+        def ranges(tables):
+            rng = [[0, 0] for _ in names]
+            base = 0
+            for table in tables:
+                for i, c in enumerate(table):
+                    t = tid(c)
+                    if rng[t][1] == 0:
+                        rng[t][0] = base + i
+                    rng[t][1] += 1
+                base += len(table)
+            return torch.tensor(rng or [[0, 0]], dtype=torch.int32, device=dev).view(-1)
+        self.rng_chunks = ranges([chunks])
+        self.rng_rows = ranges([rchunks, schunks]) if self.use_rows else self.rng_chunks
+        self.part = torch.zeros(max(self.nchunks, self.nrchunks + self.nschunks, 1) * 4, dtype=torch.float32,
+                                device=dev)
         self.t_tensors = torch.tensor(bytearray(b"".join(packed)), dtype=torch.uint8, device=dev)
         self.t_chunks = torch.tensor(bytearray(b"".join(chunks)), dtype=torch.uint8, device=dev)
         self.t_rchunks = torch.tensor(bytearray(b"".join(rchunks) or b"\0" * 24), dtype=torch.uint8, device=dev)
@@ -220,6 +238,7 @@ class FusedOptimizer:
         d.beta1, d.beta2, d.step_count = p.opt_beta1, p.opt_beta2, float(step_count)
         d.tp_size = self.tp
         d.dyn = self.dyn.data_ptr()
+        d.part, d.part_base = self.part.data_ptr(), 0
         return d
 
     def set_dyn(self, lr: float, step_count: int):
@@ -257,8 +276,8 @@ class FusedOptimizer:
         if not self.external_dyn:
             self.set_dyn(lr, step_count)
         d = self._desc(lr, step_count, grad_scale)
-        self.stats.zero_()
         L.check(lib.obst_opt_stats(d, sp), "opt_stats")
+        L.check(lib.obst_opt_fold(d, self.rng_chunks.data_ptr(), 4, sp), "opt_fold")
         self._reduce_stats()
         if self.wc:
             self._scalar(d, ("weight_centralisation", ()))
@@ -282,21 +301,21 @@ class FusedOptimizer:
                 self._scalar(d, seg.opener)
             last = k == len(segs) - 1
             d.uin = 0 if src is None else src.data_ptr()
-            if seg.emit_stats:
-                self.stats.view(-1, 8)[:, 0:2].zero_()
             if seg.emit_factored:
                 self.af_sums.zero_()
             d.uout = 0 if last else bufs[bi].data_ptr()
             self._set_stages(d, seg.stages)
             d.final_seg, d.emit_stats, d.emit_factored = int(last), int(seg.emit_stats), int(seg.emit_factored)
             if self.use_rows:
+                d.part_base = 0
                 L.check(lib.obst_opt_apply_rows(d, self.t_rchunks.data_ptr(), self.nrchunks, sp), "opt_apply_rows")
-                d.chunks, d.nchunks = self.t_schunks.data_ptr(), self.nschunks
+                d.chunks, d.nchunks, d.part_base = self.t_schunks.data_ptr(), self.nschunks, self.nrchunks
                 L.check(lib.obst_opt_apply(d, sp), "opt_apply")
-                d.chunks, d.nchunks = self.t_chunks.data_ptr(), self.nchunks
+                d.chunks, d.nchunks, d.part_base = self.t_chunks.data_ptr(), self.nchunks, 0
             else:
                 L.check(lib.obst_opt_apply(d, sp), "opt_apply")
             if seg.emit_stats:
+                L.check(lib.obst_opt_fold(d, self.rng_rows.data_ptr(), 2, sp), "opt_fold")
                 self._reduce_stats()
             if not last:
                 src, bi = bufs[bi], 1 - bi
