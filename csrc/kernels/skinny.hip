@@ -1,87 +1,93 @@
-// Skinny-M GEMM for KV-cache decode steps: C[M][N] = A[M][K] . W[K][N], M <= 32 tokens, bf16 in / bf16 out.
+// Skinny-M GEMM for KV-cache decode steps: C[M][N] = A[M][K] . W[K][N] for M <= 32 tokens, bf16 in / bf16 out,
+// on v_mfma_f32_16x16x32_bf16 with the weight read ONCE for all M rows.
 //
-// hipBLASLt picks MT16x32 tiles for M = 32, which launch ~128 workgroups for a 2048-wide projection and stream the
-// weight at ~435 GB/s (profiles/r1h_decode_kv.md). The op is weight-bandwidth bound (M FMAs per weight element), so
-// this kernel is laid out for HBM streaming: every weight element is read exactly once per 16-row M tile with 16-byte
-// loads, the K range is split over blocks so a 2048x2048 weight launches 256+ blocks, and the fp32 partials
-// (KS x M x N, 1/8 of the weight bytes at KS = 4) are summed by a second pass that writes bf16.
-//
-// Block = 256 threads: tx = t % 8 owns 8 contiguous columns (one uint4 of a weight row), ky = t / 8 (32 k-lanes)
-// walks the block's K range with stride 32. A's [16][KR] tile is staged in LDS as fp32 (reads are broadcasts).
-// Reduction over the 32 k-lanes: xor-shuffles over the 8 k-lanes inside a wave, then LDS across the 4 waves.
+// The op is weight-bandwidth bound (M = 32 FMAs per weight element). The weight comes in as the framework's cached
+// K-contiguous copy Wt[N][K] (ParamStore.transposed), so both MFMA operands load straight from global memory into
+// registers with 16-byte loads and no LDS staging (cdna_hip_programming.md §5, 'GEMV / M <= 16 decode weights':
+// operand streamed once, loads straight to VGPRs, deep unroll):
+//   MFMA A = Wt tile: lane l holds Wt[n0 + (l & 15)][k + 8 (l >> 4) .. +8]   (16 rows x 64 contiguous bytes)
+//   MFMA B = A^T    : lane l holds A[t0 + (l & 15)][k + 8 (l >> 4) .. +8]    (tokens t0 = 0 and 16: two MFMAs)
+//   D[n][t]         : lane l holds rows n0 + 4 (l >> 4) + i, column t0 + (l & 15) -> C[t][n .. n+3] (8-byte store)
+// Block = 4 waves on one 16-column tile of C; wave w takes the 32-deep k-steps s = w, w + 4, ... of the block's K
+// range (4 steps per unrolled iteration: 4 weight + 8 activation loads in flight per lane), the 4 wave sums are
+// added through LDS in wave order. KSPLIT > 1 splits K over blocks (grid.y) into fp32 partial slabs that a second
+// kernel adds in slab order: the result is deterministic either way.
 #include "common.h"
 
 namespace {
 
-constexpr int SK_MT = 16;    // M rows per tile
-constexpr int SK_KR = 512;   // K rows per block
-constexpr int SK_NB = 64;    // columns per block
+constexpr int SK_NT = 16;     // C columns (weight rows of Wt) per block
+constexpr int SK_W = 4;       // waves per block
+constexpr int SK_U = 4;       // k-steps (of 32) per unrolled iteration
 
-__global__ __launch_bounds__(256) void skinny_partial_kernel(const bf16_t* __restrict__ A, int lda,
-                                                             const bf16_t* __restrict__ W, int ldw,
-                                                             float* __restrict__ ws, int M, int N, int K) {
-  __shared__ float xs[SK_MT][SK_KR];
-  __shared__ float red[4][8][SK_MT * 8 + 1];
-  const int t = threadIdx.x, tx = t & 7, ky = t >> 3, lane = t & 63, w = t >> 6;
-  const int n0 = blockIdx.x * SK_NB + tx * 8;
-  const int kb = blockIdx.y * SK_KR;
-  const int m0 = blockIdx.z * SK_MT;
-  const int kr = min(SK_KR, K - kb);
-  for (int i = t; i < SK_MT * SK_KR; i += 256) {
-    const int m = i / SK_KR, k = i % SK_KR;
-    xs[m][k] = (m0 + m < M && k < kr) ? bf2f(A[(long long)(m0 + m) * lda + kb + k]) : 0.f;
-  }
-  __syncthreads();
-  float acc[SK_MT][8];
+__device__ __forceinline__ bf16x8_t ld8(const bf16_t* p) {
+  return __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(p));
+}
+
+__global__ __launch_bounds__(SK_W * 64) void skinny_mfma_kernel(const bf16_t* __restrict__ A, int lda,
+                                                                const bf16_t* __restrict__ Wt, int ldw,
+                                                                bf16_t* __restrict__ C, int ldc,
+                                                                float* __restrict__ ws, int M, int N, int K,
+                                                                int kchunk) {
+  if (__builtin_amdgcn_wavefrontsize() != 64) __builtin_trap();   // fragment maps below are wave64 maps
+  __shared__ float red[SK_W][64][8];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r = lane & 15, q = lane >> 4;
+  const int n0 = blockIdx.x * SK_NT;
+  const int kb = blockIdx.y * kchunk, ke = min(K, kb + kchunk);
+  const bf16_t* wrow = Wt + (long long)(n0 + r) * ldw + 8 * q;
+  const bool t0ok = r < M, t1ok = r + 16 < M;
+  const bf16_t* a0 = A + (long long)(t0ok ? r : 0) * lda + 8 * q;
+  const bf16_t* a1 = A + (long long)(t1ok ? r + 16 : 0) * lda + 8 * q;
+  const bf16x8_t zero = __builtin_bit_cast(bf16x8_t, make_uint4(0, 0, 0, 0));
+  f32x4_t acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  const int nsteps = (ke - kb) / 32;
+  int s = w;
+  for (; s + (SK_U - 1) * SK_W < nsteps; s += SK_U * SK_W) {
+    bf16x8_t wf[SK_U], x0[SK_U], x1[SK_U];
 #pragma unroll
-  for (int m = 0; m < SK_MT; ++m)
+    for (int u = 0; u < SK_U; ++u) {
+      const int k = kb + (s + u * SK_W) * 32;
+      wf[u] = ld8(wrow + k);
+      x0[u] = t0ok ? ld8(a0 + k) : zero;
+      x1[u] = t1ok ? ld8(a1 + k) : zero;
+    }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[m][j] = 0.f;
-  const bool colok = n0 < N;
-#pragma unroll 4
-  for (int k = ky; k < kr; k += 32) {
-    uint4 u = make_uint4(0, 0, 0, 0);
-    if (colok) u = *reinterpret_cast<const uint4*>(W + (long long)(kb + k) * ldw + n0);
-    const uint32_t p[4] = {u.x, u.y, u.z, u.w};
-    float wv[8];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) { wv[2 * j] = bf2f(p[j] & 0xffff); wv[2 * j + 1] = bf2f(p[j] >> 16); }
-#pragma unroll
-    for (int m = 0; m < SK_MT; ++m) {
-      const float xv = xs[m][k];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc[m][j] = fmaf(xv, wv[j], acc[m][j]);
+    for (int u = 0; u < SK_U; ++u) {
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[u], x0[u], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[u], x1[u], acc1, 0, 0, 0);
     }
   }
-  // lanes with the same tx inside a wave differ in bits 3..5 of the lane id
-#pragma unroll
-  for (int m = 0; m < SK_MT; ++m)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float v = acc[m][j];
-      v += __shfl_xor(v, 8);
-      v += __shfl_xor(v, 16);
-      v += __shfl_xor(v, 32);
-      acc[m][j] = v;
-    }
-  if (lane < 8) {
-#pragma unroll
-    for (int m = 0; m < SK_MT; ++m)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) red[w][lane][m * 8 + j] = acc[m][j];
+  for (; s < nsteps; s += SK_W) {
+    const int k = kb + s * 32;
+    const bf16x8_t wf = ld8(wrow + k);
+    const bf16x8_t x0 = t0ok ? ld8(a0 + k) : zero, x1 = t1ok ? ld8(a1 + k) : zero;
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, x0, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, x1, acc1, 0, 0, 0);
   }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) { red[w][lane][i] = acc0[i]; red[w][lane][4 + i] = acc1[i]; }
   __syncthreads();
-  // 256 threads write the block's [16][64] partial: thread -> (m, column)
-  for (int i = t; i < SK_MT * SK_NB; i += 256) {
-    const int m = i / SK_NB, c = i % SK_NB, g = c / 8, j = c % 8;
-    const int n = blockIdx.x * SK_NB + c;
-    if (m0 + m < M && n < N) {
-      const float v = red[0][g][m * 8 + j] + red[1][g][m * 8 + j] + red[2][g][m * 8 + j] + red[3][g][m * 8 + j];
-      ws[((long long)blockIdx.y * M + m0 + m) * N + n] = v;
+  if (w != 0) return;
+  float v[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = red[0][lane][i] + red[1][lane][i] + red[2][lane][i] + red[3][lane][i];
+  const int n = n0 + 4 * q;                 // this lane's 4 consecutive columns
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int t = r + 16 * h;
+    if (t >= M) continue;
+    const float* vv = v + 4 * h;
+    if (ws) {
+      *reinterpret_cast<float4*>(ws + ((long long)blockIdx.y * M + t) * N + n) = make_float4(vv[0], vv[1], vv[2], vv[3]);
+    } else {
+      const uint2 o = make_uint2(pack_bf16x2(vv[0], vv[1]), pack_bf16x2(vv[2], vv[3]));
+      *reinterpret_cast<uint2*>(C + (long long)t * ldc + n) = o;
     }
   }
 }
 
+// C[t][n] = sum over slabs s (in order) of ws[s][t][n]
 __global__ __launch_bounds__(256) void skinny_combine_kernel(const float* __restrict__ ws, bf16_t* __restrict__ C,
                                                              int ldc, int M, int N, int KS) {
   const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
@@ -92,18 +98,39 @@ __global__ __launch_bounds__(256) void skinny_combine_kernel(const float* __rest
   C[(long long)m * ldc + n] = f2bf(s);
 }
 
+int ksplit_for(int M, int N, int K) {
+  // enough blocks to put a block on most CUs (256), each block still streaming >= 256 k per wave-step range
+  const int tiles = N / SK_NT;
+  int ks = 1;
+  while (tiles * ks < 256 && K / (ks * 2) >= 1024 && ks < 8) ks *= 2;
+  return ks;
+}
+
 }  // namespace
 
-// ws: fp32 [ceil(K / 512)][M][N]
-OBST_API int obst_skinny_gemm(const void* A, int lda, const void* W, int ldw, void* C, int ldc, int M, int N, int K,
+// floats of fp32 workspace obst_skinny_gemm needs (0: single pass)
+OBST_API long long obst_skinny_ws(int M, int N, int K) {
+  const int ks = ksplit_for(M, N, K);
+  return ks > 1 ? (long long)ks * M * N : 0;
+}
+
+// A [M][K] (lda), Wt [N][K] (ldw: the K-contiguous weight copy), C [M][N] (ldc); M <= 32, N % 16 == 0, K % 32 == 0,
+// 16-byte aligned A / Wt rows; ws: obst_skinny_ws(M, N, K) floats (or null when that is 0)
+OBST_API int obst_skinny_gemm(const void* A, int lda, const void* Wt, int ldw, void* C, int ldc, int M, int N, int K,
                               float* ws, hipStream_t st) {
-  if (M <= 0 || M > 2 * SK_MT || N <= 0 || K <= 0 || N % 8 || ldw % 8 || lda < K || ldw < N || ldc < N) return -1;
-  if (((uintptr_t)W) & 15) return -2;
-  const int KS = (K + SK_KR - 1) / SK_KR;
-  hipLaunchKernelGGL(skinny_partial_kernel, dim3((N + SK_NB - 1) / SK_NB, KS, (M + SK_MT - 1) / SK_MT), dim3(256), 0,
-                     st, (const bf16_t*)A, lda, (const bf16_t*)W, ldw, ws, M, N, K);
-  const long long total = (long long)M * N;
-  hipLaunchKernelGGL(skinny_combine_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, ws, (bf16_t*)C,
-                     ldc, M, N, KS);
+  if (M <= 0 || M > 32 || N <= 0 || K <= 0 || N % SK_NT || K % 32 || lda % 8 || ldw % 8 || ldc % 4 || lda < K ||
+      ldw < K || ldc < N)
+    return -1;
+  if ((((uintptr_t)A) | ((uintptr_t)Wt)) & 15 || ((uintptr_t)C) & 7) return -2;
+  const int ks = ksplit_for(M, N, K);
+  if (ks > 1 && !ws) return -3;
+  const int kchunk = (K / 32 + ks - 1) / ks * 32;
+  hipLaunchKernelGGL(skinny_mfma_kernel, dim3(N / SK_NT, ks), dim3(SK_W * 64), 0, st, (const bf16_t*)A, lda,
+                     (const bf16_t*)Wt, ldw, (bf16_t*)C, ldc, ks > 1 ? ws : nullptr, M, N, K, kchunk);
+  if (ks > 1) {
+    const long long total = (long long)M * N;
+    hipLaunchKernelGGL(skinny_combine_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, ws,
+                       (bf16_t*)C, ldc, M, N, ks);
+  }
   return (int)hipGetLastError();
 }

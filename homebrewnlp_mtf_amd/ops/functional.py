@@ -97,7 +97,8 @@ _KCONTIG = __import__("os").environ.get("OBST_TRANSPOSED_OPERANDS", "1") != "0"
 # hipBLASLt forward GEMMs also read the cached [N][K] weight copy: on the GPT-Neo-1.3B step the same product runs
 # 1444 TF/s with the weight K-contiguous against 1256 TF/s on the stored [K][N] layout (tools/gemm_census.py,
 # profiles/r2_gemm_census.md); refreshing every copy costs one transpose pass over the bf16 weights per step (~1 ms).
-# Only token-rich products (training, prefill): a decode step streams each weight once either way.
+# Decode-step products (M = 32 tokens) gain too: 6.1-12.4 us against 7.1-21.5 us per projection
+# (tools/bench_skinny.py, profiles/r2_skinny_gemm.txt).
 _FWD_WT = __import__("os").environ.get("OBST_FWD_WT", "1") != "0"
 
 
@@ -106,7 +107,7 @@ def _wT(w, plan: LinearPlan, act=None, has_r: bool = False):
     if not _KCONTIG or store is None or not raw.on_gpu(w) or w.dtype != torch.bfloat16:
         return None
     if raw.lt_enabled() and (act is None or (act == "gelu" and not has_r)):   # runs on hipBLASLt (blaslt.cpp)
-        if not (_FWD_WT and plan.M >= 4096):
+        if not _FWD_WT:
             return None
     if plan.K % 8 or plan.N % 8:
         return None

@@ -137,8 +137,27 @@ class Operand(typing.NamedTuple):
     s2: int = 0
 
 
-# opt-in: the first version measures 2x slower than hipBLASLt in the graphed decode step (3.8k vs 7.2k tokens/s)
+# OBST_SKINNY_GEMM=1: decode-step projections (M <= 32 tokens) on the MFMA weight-streaming kernel
+# (csrc/kernels/skinny.hip) instead of hipBLASLt. Both read the cached K-contiguous weight copy; graph-replayed per
+# call the kernel takes 6.0-15.4 us where hipBLASLt takes 5.3-12.4 us on the GPT-Neo-1.3B projections (70 vs 32 us
+# on the 50304-wide logits, profiles/r2_skinny_gemm.txt), so it stays opt-in.
 _SKINNY = __import__("os").environ.get("OBST_SKINNY_GEMM", "0") == "1"
+_SKINNY_WS: typing.Dict[typing.Any, torch.Tensor] = {}
+
+
+def skinny_ok(M: int, N: int, K: int) -> bool:
+    return _SKINNY and 0 < M <= 32 and N % 16 == 0 and K % 32 == 0
+
+
+def _skinny_ws(device, n: int) -> typing.Optional[torch.Tensor]:
+    """per-device fp32 workspace of the split-K skinny GEMM, grown on demand and reused"""
+    if n <= 0:
+        return None
+    ws = _SKINNY_WS.get(device)
+    if ws is None or ws.numel() < n:
+        ws = torch.empty(max(n, 1 << 20), dtype=torch.float32, device=device)
+        _SKINNY_WS[device] = ws
+    return ws
 
 
 def gemm(a: Operand, b: Operand, c: Operand, M: int, N: int, K: int, batch: typing.Tuple[int, int] = (1, 1),
@@ -154,17 +173,18 @@ def gemm(a: Operand, b: Operand, c: Operand, M: int, N: int, K: int, batch: typi
     if c.t.device.type == "meta":
         return c.t
     b1, b2 = batch
-    if (_SKINNY and on_gpu(c.t) and M <= 32 and act is None and R is None and Zout is None and Zin is None and tri == 0
-            and b1 * b2 == 1 and alpha == 1.0 and a.trans == 0 and b.trans == 1 and c.t.dtype == torch.bfloat16
-            and a.t.dtype == torch.bfloat16 and b.t.dtype == torch.bfloat16 and N % 8 == 0 and b.ld % 8 == 0
-            and a.ld >= K and b.ld >= N and c.ld >= N and b.t.data_ptr() % 16 == 0):
-        # decode-step projections (M = batch tokens): split-K weight-streaming kernel (csrc/kernels/skinny.hip)
+    if (on_gpu(c.t) and skinny_ok(M, N, K) and act is None and R is None and Zout is None and Zin is None
+            and tri == 0 and b1 * b2 == 1 and alpha == 1.0 and a.trans == 0 and b.trans == 0
+            and c.t.dtype == torch.bfloat16 and a.t.dtype == torch.bfloat16 and b.t.dtype == torch.bfloat16
+            and a.ld % 8 == 0 and b.ld % 8 == 0 and c.ld % 4 == 0 and a.ld >= K and b.ld >= K and c.ld >= N
+            and a.t.data_ptr() % 16 == 0 and b.t.data_ptr() % 16 == 0 and c.t.data_ptr() % 8 == 0):
+        # decode-step projection (M = batch tokens) against the K-contiguous weight: MFMA weight-streaming kernel
         _need(a.t, (M - 1) * a.ld + K - 1, "A")
-        _need(b.t, (K - 1) * b.ld + N - 1, "B")
+        _need(b.t, (N - 1) * b.ld + K - 1, "B")
         _need(c.t, (M - 1) * c.ld + N - 1, "C")
-        ws = torch.empty(-(-K // 512) * M * N, dtype=torch.float32, device=c.t.device)
+        ws = _skinny_ws(c.t.device, int(L.lib().obst_skinny_ws(M, N, K)))
         L.check(L.lib().obst_skinny_gemm(a.t.data_ptr(), a.ld, b.t.data_ptr(), b.ld, c.t.data_ptr(), c.ld, M, N, K,
-                                         ws.data_ptr(), L.stream_ptr()), "skinny_gemm")
+                                         L.ptr(ws), L.stream_ptr()), "skinny_gemm")
         return c.t
     if (on_gpu(c.t) and act is not None and tri == 0 and lt_enabled() == 1 and c.t.dtype == torch.bfloat16
             and b1 * b2 == 1 and c.ld == N and (M * N) % 8 == 0 and c.t.is_contiguous() and c.t.numel() == M * N):

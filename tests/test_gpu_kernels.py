@@ -351,16 +351,23 @@ def test_token_mixer_big_tiles(cuda, causal):
     _close(wg.grad, wf.grad, 1e-1, 3e-2, "mixer dw")
 
 
-@pytest.mark.parametrize("M,K,N", [(1, 2048, 2048), (7, 100, 64), (16, 2048, 8192), (32, 8192, 2048),
-                                   (32, 2048, 6144), (20, 1000, 1032)])
+@pytest.mark.parametrize("M,K,N", [(1, 2048, 2048), (7, 96, 64), (16, 2048, 8192), (32, 8192, 2048),
+                                   (32, 2048, 6144), (20, 1024, 1040), (32, 2048, 50304), (17, 4096, 2048)])
 def test_skinny_gemm_matches_fp32(cuda, M, K, N, monkeypatch):
-    """decode-step GEMM (M <= 32 tokens) on csrc/kernels/skinny.hip vs a PyTorch fp32 reference"""
+    """decode-step GEMM (M <= 32 tokens) on the MFMA kernel of csrc/kernels/skinny.hip (weight as the K-contiguous
+    [N][K] copy, split-K slabs for the narrow shapes) vs a PyTorch fp32 reference; a second call gives the same bits"""
     monkeypatch.setattr(raw, "_SKINNY", True)
+    assert raw.skinny_ok(M, N, K)
     g = torch.Generator().manual_seed(M * 7 + K)
     a = torch.randn(M, K, generator=g).bfloat16()
     w = (torch.randn(K, N, generator=g) / math.sqrt(K)).bfloat16()
+    wt = w.t().contiguous()
     c = torch.full((M * N,), float("nan"), dtype=torch.bfloat16, device=cuda)
-    raw.gemm(raw.Operand(a.to(cuda).flatten(), 0, K), raw.Operand(w.to(cuda).flatten(), 1, N),
-             raw.Operand(c, 0, N), M, N, K)
+    op = lambda: raw.gemm(raw.Operand(a.to(cuda).flatten(), 0, K), raw.Operand(wt.to(cuda).flatten(), 0, K),  # noqa
+                          raw.Operand(c, 0, N), M, N, K)
+    op()
+    first = c.clone()
+    op()
+    assert torch.equal(first, c)
     ref = a.float() @ w.float()
     _close(c.view(M, N).float().cpu(), ref, 2e-2, 2e-2, f"skinny {M}x{K}x{N}")

@@ -1,4 +1,5 @@
-"""Skinny-M (decode-step) GEMM: csrc/kernels/skinny.hip vs hipBLASLt, per-call time over the GPT-Neo-1.3B shapes.
+"""Skinny-M (decode-step) GEMM: csrc/kernels/skinny.hip vs hipBLASLt (both weight layouts), graph-replayed per-call
+time over the GPT-Neo-1.3B decode shapes (weights L2/MALL-warm: replayed back to back).
     python tools/bench_skinny.py"""
 import os
 import sys
@@ -9,12 +10,13 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from homebrewnlp_mtf_amd.ops import raw  # noqa: E402
 
 
-def run(M, K, N, skinny, iters=200):
+def run(M, K, N, skinny, kcontig, iters=200):
     raw._SKINNY = skinny
     a = torch.randn(M * K, device="cuda").bfloat16()
     w = torch.randn(K * N, device="cuda").bfloat16()
+    bop = raw.Operand(w, 0, K) if kcontig else raw.Operand(w, 1, N)   # [N][K] copy or the stored [K][N]
     c = torch.empty(M * N, device="cuda", dtype=torch.bfloat16)
-    f = lambda: raw.gemm(raw.Operand(a, 0, K), raw.Operand(w, 1, N), raw.Operand(c, 0, N), M, N, K)  # noqa: E731
+    f = lambda: raw.gemm(raw.Operand(a, 0, K), bop, raw.Operand(c, 0, N), M, N, K)  # noqa: E731
     for _ in range(10):
         f()
     g = torch.cuda.CUDAGraph()
@@ -33,7 +35,10 @@ def run(M, K, N, skinny, iters=200):
     return us, K * N * 2 / us / 1e3
 
 
-for M, K, N in [(32, 2048, 2048), (32, 2048, 6144), (32, 2048, 8192), (32, 8192, 2048), (16, 2048, 2048)]:
-    ul, bl = run(M, K, N, False)
-    us, bs = run(M, K, N, True)
-    print(f"M{M} K{K} N{N}: hipBLASLt {ul:7.1f} us ({bl:5.0f} GB/s)  skinny {us:7.1f} us ({bs:5.0f} GB/s)", flush=True)
+for M, K, N in [(32, 2048, 2048), (32, 4096, 2048), (32, 2048, 4096), (32, 2048, 6144), (32, 2048, 8192),
+                (32, 8192, 2048), (16, 2048, 2048), (32, 2048, 50304)]:
+    ul, bl = run(M, K, N, False, False)
+    ut, bt = run(M, K, N, False, True)
+    us, bs = run(M, K, N, True, True)
+    print(f"M{M} K{K} N{N}: hipBLASLt [K][N] {ul:7.1f} us ({bl:5.0f} GB/s)  hipBLASLt [N][K] {ut:7.1f} us "
+          f"({bt:5.0f} GB/s)  MFMA skinny {us:7.1f} us ({bs:5.0f} GB/s)", flush=True)
