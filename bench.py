@@ -57,11 +57,18 @@ def main():
         if world == 1 and args.gpus > 1:
             raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one process per GPU)")
         raise SystemExit(f"WORLD_SIZE={world} != --gpus {args.gpus}")
-    torch.cuda.set_device(local_rank)
-    device = torch.device("cuda", local_rank)
+    # OBST_DIST_BACKEND=gloo rehearses the N-rank code path with several ranks sharing the visible GPUs (RCCL needs
+    # one GPU per rank); the measured numbers always use the default, RCCL ("nccl") with one process per GPU
+    backend = os.environ.get("OBST_DIST_BACKEND", "nccl")
+    local_dev = local_rank % max(torch.cuda.device_count(), 1) if backend != "nccl" else local_rank
+    torch.cuda.set_device(local_dev)
+    device = torch.device("cuda", local_dev)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=device)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(backend)
     mesh = pstate.Mesh(dp=world, tp=1, rank=rank).build_groups()
 
     overrides = {}
@@ -90,7 +97,10 @@ def main():
 
     def barrier():
         if world > 1:
-            dist.barrier(device_ids=[local_rank])
+            if backend == "nccl":
+                dist.barrier(device_ids=[local_dev])
+            else:
+                dist.barrier()
 
     t_w = time.time()
     for i in range(args.warmup):

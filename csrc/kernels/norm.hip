@@ -177,11 +177,12 @@ __global__ __launch_bounds__(NTH) void norm_bwd_kernel(const bf16_t* __restrict_
     for (int j = 0; j < 8; ++j) gs[c][j] = gb[c][j] = 0.f;
   const long long nw = (long long)gridDim.x * 4 * RPW;
   const long long first = ((long long)blockIdx.x * 4 + w) * RPW + sub;
-  uint4 nx[NCH], nd[NCH];   // next row in flight while this one is processed
+  uint4 nx[NCH], nd[NCH], nr[NCH];   // next row (x, dy and the residual gradient) in flight while this one is processed
   {
     const long long row = ((long long)blockIdx.x * 4 + w) * RPW + sub;
     load_raw<NCH, LPR>(X + row * F, F, sl, row < rows, nx);
     load_raw<NCH, LPR>(DY + row * F, F, sl, row < rows, nd);
+    if (R) load_raw<NCH, LPR>(R + row * F, F, sl, row < rows, nr);
   }
   for (long long r0 = ((long long)blockIdx.x * 4 + w) * RPW; r0 < rows; r0 += nw) {
     const long long row = r0 + sub;
@@ -189,6 +190,12 @@ __global__ __launch_bounds__(NTH) void norm_bwd_kernel(const bf16_t* __restrict_
     float x[NCH][8], dy[NCH][8];
     unpack_row<NCH>(nx, x);
     unpack_row<NCH>(nd, dy);
+    uint4 cr[NCH];
+    if (R) {
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) cr[c] = nr[c];
+      load_raw<NCH, LPR>(R + (row + nw) * F, F, sl, row + nw < rows, nr);
+    }
     load_raw<NCH, LPR>(X + (row + nw) * F, F, sl, row + nw < rows, nx);
     load_raw<NCH, LPR>(DY + (row + nw) * F, F, sl, row + nw < rows, nd);
     const float mean = ok ? stats[2 * row] : 0.f, rstd = ok ? stats[2 * row + 1] : 0.f;
@@ -229,7 +236,7 @@ __global__ __launch_bounds__(NTH) void norm_bwd_kernel(const bf16_t* __restrict_
       if (col >= F) continue;
       float r[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
       if (R) {   // the block's residual-input gradient, summed here instead of in a separate elementwise pass
-        const uint4 u = *reinterpret_cast<const uint4*>(R + row * F + col);
+        const uint4 u = cr[c];
         const uint32_t w[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
         for (int j = 0; j < 4; ++j) { r[2 * j] = bf2f(w[j] & 0xffff); r[2 * j + 1] = bf2f(w[j] >> 16); }
@@ -302,8 +309,17 @@ __global__ __launch_bounds__(NTH) void norm_fold_kernel(const float* __restrict_
     f = rem % F;
     const long long K = nparts > g ? (nparts - g + period - 1) / period : 0;   // partial rows of this group
     const long long k0 = K * seg / 8, k1 = K * (seg + 1) / 8;
-    const float* src = ws + (long long)which * F + f;
-    for (long long k = k0; k < k1; ++k) acc += src[(g + k * period) * 2 * F];
+    const float* src = ws + (long long)which * F + f + (long long)g * 2 * F;
+    const long long step = (long long)period * 2 * F;
+    long long k = k0;
+    for (; k + 4 <= k1; k += 4) {   // four loads in flight, added in k order
+      const float v0 = src[k * step], v1 = src[(k + 1) * step], v2 = src[(k + 2) * step], v3 = src[(k + 3) * step];
+      acc += v0;
+      acc += v1;
+      acc += v2;
+      acc += v3;
+    }
+    for (; k < k1; ++k) acc += src[k * step];
   }
   red[seg][c] = acc;
   __syncthreads();
@@ -370,9 +386,10 @@ OBST_API int obst_norm_partial(const ObstNormDesc* d, hipStream_t st) {
 }
 
 static int norm_bwd_grid(const ObstNormDesc* d) {
-  // more rows per block shrinks the parameter-gradient slab; 2048 blocks keep ~8 waves per SIMD in flight
+  // one resident wave of blocks (~170 VGPRs: 2 blocks of 4 waves per CU) grid-strides over the rows; more blocks
+  // only grow the parameter-gradient slab that norm_fold_kernel reads back (2048 blocks: 103 us per fold)
   long long g = (d->rows + 15) / 16;
-  int grid = (int)(g < 2048 ? (g < 1 ? 1 : g) : 2048);
+  int grid = (int)(g < 512 ? (g < 1 ? 1 : g) : 512);
   if (d->groups > 1) {   // rows per grid step (4 waves x 64/LPR rows per block) must be a multiple of groups
     int a = d->groups, b = 4 * (64 / lanes_per_row(d->F));
     while (b) { const int t = a % b; a = b; b = t; }
