@@ -255,6 +255,9 @@ class ParamStore:
 
     def zero_grad(self):
         self.grad.zero_()
+        # variables whose gradient has received no contribution yet this step: their first weight-gradient GEMM
+        # may overwrite (beta = 0) instead of accumulating (ops/functional.py::_acc_grad_beta)
+        self.fresh = set(self.order)
 
     def fold_leaf_grads(self):
         """Paths that use plain torch autograd (exotic layer variants) leave gradients on the leaves' ``.grad``;

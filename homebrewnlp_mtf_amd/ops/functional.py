@@ -1,7 +1,8 @@
 """Autograd ops of the model, written once against ``ops.raw`` (HIP on GPU, torch oracle on CPU).
 
 Weight gradients never go through autograd: every op adds its fp32 weight gradient straight into the flat gradient
-buffer (``weight.main_grad``, see ``models/variables.py``) with a beta=1 GEMM epilogue and returns ``None`` -- this
+buffer (``weight.main_grad``, see ``models/variables.py``) with a beta=1 GEMM epilogue (beta=0 for the first
+contribution of a step) and returns ``None`` -- this
 is the MI355X-native replacement of the reference's per-variable gradient einsums (src/optimizer/__init__.py:128-174)
 and lets the DP all-reduce start on contiguous buckets while backward is still running.
 
@@ -36,8 +37,25 @@ def _acc_grad(w: torch.Tensor) -> typing.Tuple[torch.Tensor, bool]:
     """(fp32 buffer to accumulate the weight gradient into, whether it is the flat main_grad)"""
     mg = getattr(w, "main_grad", None)
     if mg is not None:
+        fresh = getattr(getattr(w, "store", None), "fresh", None)
+        if fresh is not None:
+            fresh.discard(w.var_name)
         return mg, True
     return torch.zeros(w.shape, dtype=torch.float32, device=w.device), False
+
+
+def _acc_grad_beta(w: torch.Tensor) -> typing.Tuple[torch.Tensor, bool, float]:
+    """like ``_acc_grad`` plus the GEMM beta: 0 (overwrite) for the first contribution of the step to a flat-buffer
+    gradient, 1 (accumulate) after that. hipBLASLt's fp32 weight-gradient GEMM runs up to 13 % faster without the
+    C read-back (tools/bench_wgrad.py, profiles/r2_wgrad_layouts.txt)."""
+    mg = getattr(w, "main_grad", None)
+    if mg is None:
+        return torch.zeros(w.shape, dtype=torch.float32, device=w.device), False, 0.0
+    fresh = getattr(getattr(w, "store", None), "fresh", None)
+    first = fresh is not None and w.var_name in fresh
+    if fresh is not None:
+        fresh.discard(w.var_name)
+    return mg, True, 0.0 if first else 1.0
 
 
 def _param32(t: typing.Optional[torch.Tensor]) -> typing.Optional[torch.Tensor]:
@@ -139,30 +157,39 @@ def _dgrad_gemm(dy2, w, dx2, plan: LinearPlan, act=None, Zin=None, R=None):
              M, K, N, batch=(H, 1), act=act, act_bwd=Zin is not None, Zin=Zin, R=R)
 
 
-def _wgrad_gemm(x2, dy2, gw, plan: LinearPlan, xT=None, dyT=None):
-    """gw[H][K][N] += x[M][H][K]ᵀ · dy[M][H][N]; with token-contiguous transposes (xT [H*K][M], dyT [H*N][M]) both
-    operands are K-contiguous"""
+def _wgrad_gemm(x2, dy2, gw, plan: LinearPlan, xT=None, dyT=None, beta: float = 1.0):
+    """gw[H][K][N] (+)= x[M][H][K]ᵀ · dy[M][H][N] (beta 0: overwrite, 1: accumulate); with token-contiguous
+    transposes (xT [H*K][M], dyT [H*N][M]) the operands are K-contiguous"""
     M, H, K, N = plan.M, plan.H, plan.K, plan.N
     if xT is None:
         xT = tokens_transposed(x2, M, H * K)
-    if (xT is None and dyT is None and raw.on_gpu(x2) and raw.lt_enabled() and H == 1 and N >= 2 * K
-            and N >= 4096 and M % 8 == 0 and K % 8 == 0):
+    lt_big = (xT is None and dyT is None and raw.on_gpu(x2) and raw.lt_enabled() and H == 1 and M % 8 == 0
+              and K % 8 == 0 and N % 8 == 0)
+    if lt_big and N >= 2 * K and N >= 4096:
         # hipBLASLt reads a token-contiguous x ~20 % faster than the token-strided one (tools/bench_wgrad.py); the
         # saving grows with N while the transpose costs ~K: worth it for the d -> 2d projections
         xT = torch.empty(K * M, dtype=x2.dtype, device=x2.device)
         raw.transpose(x2, xT, M, K, K, M)
+    elif lt_big and K >= 2 * N and K >= 4096:
+        # the 2d -> d projections: token-contiguous dy (the narrow operand, cheap to transpose) -- T 131072,
+        # 4096 -> 2048: 1562 us (+ 220 us transpose) against 2041 us token-strided (profiles/r2_wgrad_layouts.txt)
+        dyT = torch.empty(N * M, dtype=dy2.dtype, device=dy2.device)
+        raw.transpose(dy2, dyT, M, N, N, M)
+        raw.gemm(raw.Operand(x2, 1, K, K * M), raw.Operand(dyT, 0, M, N * M), raw.Operand(gw, 0, N, K * N),
+                 K, N, M, beta=beta)
+        return
     if xT is not None and dyT is None:
         dyT = tokens_transposed(dy2, M, H * N)
     if xT is not None and dyT is not None:
         raw.gemm(raw.Operand(xT, 0, M, K * M), raw.Operand(dyT, 0, M, N * M), raw.Operand(gw, 0, N, K * N),
-                 K, N, M, batch=(H, 1), beta=1.0)
+                 K, N, M, batch=(H, 1), beta=beta)
         return
     if xT is not None:      # shared token-contiguous x (hipBLASLt: NT runs ~25 % faster than TT at T = 32k)
         raw.gemm(raw.Operand(xT, 0, M, K * M), raw.Operand(dy2, 1, H * N, N), raw.Operand(gw, 0, N, K * N),
-                 K, N, M, batch=(H, 1), beta=1.0)
+                 K, N, M, batch=(H, 1), beta=beta)
         return
     raw.gemm(raw.Operand(x2, 1, H * K, K), raw.Operand(dy2, 1, H * N, N), raw.Operand(gw, 0, N, K * N),
-             K, N, M, batch=(H, 1), beta=1.0)
+             K, N, M, batch=(H, 1), beta=beta)
 
 
 class _Linear(torch.autograd.Function):
@@ -203,8 +230,8 @@ class _Linear(torch.autograd.Function):
             if plan.x_perm is not None:
                 inv = [plan.x_perm.index(i) for i in range(len(plan.x_perm))]
                 dx = dx.permute(inv)
-        gw, is_main = _acc_grad(w)
-        _wgrad_gemm(xc, dy, gw, plan)
+        gw, is_main, beta = _acc_grad_beta(w)
+        _wgrad_gemm(xc, dy, gw, plan, beta=beta)
         _done(w)
         return dx, (None if is_main else gw.to(w.dtype)), None, None
 
@@ -272,13 +299,13 @@ class _FFN(torch.autograd.Function):
         # dZ = (dY W2^T) * act'(Z) in ONE gemm epilogue
         dz = _empty(p1.canon_o_shape, dy)
         _dgrad_gemm(dy, w2, dz, p2, act=act, Zin=z if act else None)
-        g2, m2 = _acc_grad(w2)
-        _wgrad_gemm(a, dy, g2, p2)
+        g2, m2, b2 = _acc_grad_beta(w2)
+        _wgrad_gemm(a, dy, g2, p2, beta=b2)
         _done(w2)
         dx = _empty(xc.shape, xc)
         _dgrad_gemm(dz, w1, dx, p1)
-        g1, m1 = _acc_grad(w1)
-        _wgrad_gemm(xc, dz, g1, p1)
+        g1, m1, b1 = _acc_grad_beta(w1)
+        _wgrad_gemm(xc, dz, g1, p1, beta=b1)
         _done(w1)
         dres = dy if ctx.has_res else None
         if dres is not None and ctx.carrier is not None:   # handed to the block's opening norm (ResidualGrad)
@@ -356,8 +383,8 @@ class _DotAttention(torch.autograd.Function):
             last = j == 2
             _dgrad_gemm(dkqv[j], ws[j], dbase, p_out, act=act if last else None,
                         Zin=z if (last and act) else None, R=dbase if j > 0 else None)
-            g, m = _acc_grad(ws[j])
-            _wgrad_gemm(base, dkqv[j], g, p_out, xT=baseT,
+            g, m, bj = _acc_grad_beta(ws[j])
+            _wgrad_gemm(base, dkqv[j], g, p_out, xT=baseT, beta=bj,
                         dyT=None if dkqvT is None else dkqvT[j * No * Mo:(j + 1) * No * Mo])
             _done(ws[j])
             outs.append(None if m else g.to(ws[j].dtype))
@@ -367,8 +394,8 @@ class _DotAttention(torch.autograd.Function):
             pstate.tp_all_reduce(dbase)
         dx = _empty(xc.shape, xc)
         _dgrad_gemm(dbase, w_in, dx, p_in)
-        g, m = _acc_grad(w_in)
-        _wgrad_gemm(xc, dbase, g, p_in)
+        g, m, bi = _acc_grad_beta(w_in)
+        _wgrad_gemm(xc, dbase, g, p_in, beta=bi)
         _done(w_in)
         dres = dout if has_res else None
         if dres is not None and ctx.carrier is not None:   # handed to the block's opening norm (ResidualGrad)

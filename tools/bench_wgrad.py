@@ -10,10 +10,10 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from homebrewnlp_mtf_amd.ops import raw  # noqa: E402
 
-T = 32768
+T = int(os.environ.get("T", 32768))
 
 
-def timeit(fn, n=5):
+def timeit(fn, n=10):
     fn()
     torch.cuda.synchronize()
     t = time.perf_counter()
@@ -35,11 +35,11 @@ def main():
                            ("NT (x transposed)", raw.Operand(XT, 0, T), raw.Operand(dY, 1, O)),
                            ("TN (dy transposed)", raw.Operand(X, 1, I), raw.Operand(dYT, 0, T)),
                            ("NN-K (both transposed)", raw.Operand(XT, 0, T), raw.Operand(dYT, 0, T))):
-            for dt in (torch.float32, torch.bfloat16):
+            for dt, beta in ((torch.float32, 1.0), (torch.float32, 0.0), (torch.bfloat16, 0.0)):
                 C = torch.zeros(I * O, device=dev, dtype=dt)
-                beta = 1.0 if dt == torch.float32 else 0.0
                 t = timeit(lambda: raw.gemm(a, b, raw.Operand(C, 0, O), I, O, T, beta=beta))
-                print(f"in {I} out {O} {name:24s} {str(dt)[6:]:9s}: {t * 1e6:7.1f} us {f / t:7.1f} TF/s")
+                print(f"in {I} out {O} {name:24s} {str(dt)[6:]:9s} beta {beta:.0f}: {t * 1e6:7.1f} us "
+                      f"{f / t:7.1f} TF/s", flush=True)
         tt = timeit(lambda: raw.transpose(X, XT, T, I, I, T))
         print(f"transpose [{T}][{I}]: {tt * 1e6:.1f} us")
 
