@@ -130,8 +130,11 @@ def main():
     if rank == 0:
         log(f"loss={float(m['loss']):.4f} acc={float(m['accuracy']):.4f} step={ms:.1f}ms "
             f"tokens/s={tps:.0f} MFU={mfu * 100:.1f}% ({fpt / 1e9:.2f} GFLOP/token)")
+        model = os.path.basename(args.config).replace(".json", "")
+        metric = ("tokens/sec (whole node), GPT-Neo-1.3B seq2048 bf16" if model == "gpt_neo_1.3b" else
+                  f"tokens/sec (whole node), {model} seq{S} bf16")
         print(json.dumps({
-            "metric": "tokens/sec (whole node), GPT-Neo-1.3B seq2048 bf16",
+            "metric": metric,
             "value": round(tps, 1), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "bf16", "data": "synthetic (uniform random tokens), random-init weights",

@@ -65,7 +65,7 @@ __device__ __forceinline__ int lds_off16(int row, int chunk) {
 // waits with vm_wait<0>() before the publishing barrier -- the builtin made the compiler put vmcnt(0) in front of
 // every LDS read, so the next tile's DMA could never overlap the current tile's MFMAs): the per-lane SOURCE chunk is
 // pre-swizzled so the image matches lds_off(). Rows >= nvalid are clamped to the last valid row (masked later).
-template <int D, int ROWS>
+template <int D, int ROWS, int NW = 4>
 __device__ __forceinline__ void stage_rows(char* lds, const bf16_t* g, long long ld, int nvalid, int tid) {
   constexpr int CPR = Geo<D>::CPR;
   constexpr int PIECES = ROWS * CPR * 16 / 1024;   // 1 KiB pieces in the image
@@ -73,9 +73,9 @@ __device__ __forceinline__ void stage_rows(char* lds, const bf16_t* g, long long
   const int wave = tid >> 6, lane = tid & 63;
   const int last = nvalid - 1;
 #pragma unroll
-  for (int i = 0; i < (PIECES + 3) / 4; ++i) {
-    const int j = wave + 4 * i;
-    if (PIECES % 4 == 0 || j < PIECES) {
+  for (int i = 0; i < (PIECES + NW - 1) / NW; ++i) {
+    const int j = wave + NW * i;
+    if (PIECES % NW == 0 || j < PIECES) {
       const int row = j * RPP + lane / CPR;
       const int p = lane % CPR;
       const int c = p ^ swz16<D>(row);
@@ -87,7 +87,7 @@ __device__ __forceinline__ void stage_rows(char* lds, const bf16_t* g, long long
 
 // 4-byte values (lse / delta rows) for `n` <= 64 consecutive queries: one 256-B piece from wave 0
 __device__ __forceinline__ void stage_f32(char* lds, const float* g, int n, int nvalid, int tid) {
-  if (tid < 64) {   // wave 0, all lanes (n <= 64: lanes past n re-read the last value)
+  if (tid >= 0 && tid < 64) {   // one wave, all lanes (n <= 64: lanes past n re-read the last value)
     const int q = min(min(tid, n - 1), nvalid - 1);
     glds4_asm(g + q, lds);
   }
@@ -147,7 +147,8 @@ struct AttnArgs {
   bf16_t *Oout, *dQ, *dK, *dV;
   float *LSE, *delta;
   int B, S, H;
-  long long ld;   // token stride (elements), usually H*D
+  long long ld;   // token stride (elements) of Q, K, V and dQ, dK, dV: H*D, or 3*H*D for the interleaved k|q|v layout
+  long long ld_o; // token stride of O and dO (H*D)
   float scale;
   int causal;
   int prio;       // s_setprio(1) around the MFMA clusters: bit 0 dK/dV kernel (default on: -2 %), bit 1 dQ (+1 %: off)
@@ -306,7 +307,7 @@ __global__ __launch_bounds__(NTH, 2) void attn_fwd_kernel(AttnArgs a) {
     __syncthreads();
   }
   // epilogue: lane holds O[q = qw + qt*16 + i][d = dt*16 + 4g + v]
-  bf16_t* Ob = a.Oout + (long long)b * a.S * a.ld + h * D;
+  bf16_t* Ob = a.Oout + (long long)b * a.S * a.ld_o + h * D;
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
     const int q = qw + qt * 16 + i;
@@ -315,7 +316,7 @@ __global__ __launch_bounds__(NTH, 2) void attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
     for (int dt = 0; dt < G::DT; ++dt) {
       const int d = dt * 16 + 4 * g;
-      *reinterpret_cast<uint2*>(Ob + (long long)q * a.ld + d) =
+      *reinterpret_cast<uint2*>(Ob + (long long)q * a.ld_o + d) =
           make_uint2(pack_bf16x2(o[dt][qt][0] * inv, o[dt][qt][1] * inv), pack_bf16x2(o[dt][qt][2] * inv, o[dt][qt][3] * inv));
     }
     if (g == 0) a.LSE[((long long)b * a.H + h) * a.S + q] = (m[qt] + __log2f(l[qt])) / LOG2E;
@@ -333,8 +334,8 @@ __global__ __launch_bounds__(NTH) void attn_delta_kernel(AttnArgs a) {
   const int h = row % a.H;
   const long long bq = row / a.H;
   const int q = bq % a.S, b = bq / a.S;
-  const bf16_t* o = a.O + bq * a.ld + h * D;
-  const bf16_t* d = a.dO + bq * a.ld + h * D;
+  const bf16_t* o = a.O + bq * a.ld_o + h * D;
+  const bf16_t* d = a.dO + bq * a.ld_o + h * D;
   float acc = 0.f;
   for (int j = lane * 2; j < D; j += 128) {
     uint32_t ov = *reinterpret_cast<const uint32_t*>(o + j);
@@ -411,24 +412,36 @@ __device__ __forceinline__ void dq_tile(const char* sK, const char* sV, const bf
 }
 
 // ----------------------------------------------------------------------------------------------------------------
-// dQ: block = 128 queries; recompute Sᵀ, Pᵀ, dPᵀ = V·dOᵀ, dSᵀ, dQᵀ += Kᵀ·dSᵀ. K/V tiles double-buffered (LDS-DMA).
-template <int D>
-__global__ __launch_bounds__(NTH, 2) void attn_bwd_dq_kernel(AttnArgs a) {
+// dQ: block = NW x 32 queries; recompute Sᵀ, Pᵀ, dPᵀ = V·dOᵀ, dSᵀ, dQᵀ += Kᵀ·dSᵀ. K/V tiles in an NS-deep LDS ring
+// filled by LDS-DMA NS - 1 tiles ahead (NW = 8, NS = 3: one block per CU, every wave's DMA share of a tile is 4
+// pieces, a tile has two tiles' time to land instead of one).
+template <int D, int NW = 4, int NS = 2>
+__global__ __launch_bounds__(NW * 64, 2) void attn_bwd_dq_kernel(AttnArgs a) {
   using G = Geo<D>;
   constexpr int TILE = 64 * G::ROWB;
+  constexpr int QB = 32 * NW;                          // queries per block
+  constexpr int PPW = 2 * (TILE / 1024) / NW;          // LDS-DMA pieces per wave per stage (K + V)
+  static_assert(NS == 2 || (2 * (TILE / 1024)) % NW == 0, "counted waits need an even piece split");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, i = lane & 15;
-  const int nx = (a.S + 127) / 128;
+  const int nx = (a.S + QB - 1) / QB;
   int bx, bh;
   attn_block(nx, bx, bh);
   const int b = bh / a.H, h = bh % a.H;
-  const int qblk = (a.causal ? (nx - 1 - bx) : bx) * 128;  // heaviest first
+  const int qblk = (a.causal ? (nx - 1 - bx) : bx) * QB;  // heaviest first
   const int qw = qblk + w * 32;
   const long long base = (long long)b * a.S * a.ld + h * D;
-  const int kend = a.causal ? min(a.S, qblk + 128) : a.S;
+  const long long base_o = (long long)b * a.S * a.ld_o + h * D;
+  const int kend = a.causal ? min(a.S, qblk + QB) : a.S;
   const int nkb = (kend + 63) / 64;
-  stage_rows<D, 64>(smem, a.K + base, a.ld, a.S, tid);
-  stage_rows<D, 64>(smem + TILE, a.V + base, a.ld, a.S, tid);
+#pragma unroll
+  for (int st = 0; st < NS - 1; ++st) {
+    if (st < nkb) {
+      stage_rows<D, 64, NW>(smem + st * 2 * TILE, a.K + base + (long long)st * 64 * a.ld, a.ld, a.S - st * 64, tid);
+      stage_rows<D, 64, NW>(smem + st * 2 * TILE + TILE, a.V + base + (long long)st * 64 * a.ld, a.ld, a.S - st * 64,
+                            tid);
+    }
+  }
 
   bf16x8_t qf[2][G::DS], df[2][G::DS];
   float lse2[2], dlt[2];
@@ -439,7 +452,7 @@ __global__ __launch_bounds__(NTH, 2) void attn_bwd_dq_kernel(AttnArgs a) {
 #pragma unroll
     for (int ds = 0; ds < G::DS; ++ds) {
       qf[qt][ds] = load_frag_g(a.Q + base + (long long)q * a.ld + ds * 32 + 8 * g, ok);
-      df[qt][ds] = load_frag_g(a.dO + base + (long long)q * a.ld + ds * 32 + 8 * g, ok);
+      df[qt][ds] = load_frag_g(a.dO + base_o + (long long)q * a.ld_o + ds * 32 + 8 * g, ok);
     }
     const long long si = ((long long)b * a.H + h) * a.S + (ok ? q : 0);
     lse2[qt] = a.LSE[si] * LOG2E;
@@ -448,7 +461,7 @@ __global__ __launch_bounds__(NTH, 2) void attn_bwd_dq_kernel(AttnArgs a) {
     float part = 0.f;
 #pragma unroll
     for (int ds = 0; ds < G::DS; ++ds) {
-      const bf16x8_t of = load_frag_g(a.O + base + (long long)q * a.ld + ds * 32 + 8 * g, ok);
+      const bf16x8_t of = load_frag_g(a.O + base_o + (long long)q * a.ld_o + ds * 32 + 8 * g, ok);
 #pragma unroll
       for (int j = 0; j < 8; ++j) part += (float)of[j] * (float)df[qt][ds][j];
     }
@@ -465,19 +478,23 @@ __global__ __launch_bounds__(NTH, 2) void attn_bwd_dq_kernel(AttnArgs a) {
   __syncthreads();
   for (int kb = 0; kb < nkb; ++kb) {
     const int k0 = kb * 64;
-    const char* sK = smem + (kb & 1) * 2 * TILE;
+    const char* sK = smem + (kb % NS) * 2 * TILE;
     const char* sV = sK + TILE;
-    if (kb + 1 < nkb) {
-      char* nxt = smem + ((kb + 1) & 1) * 2 * TILE;
-      stage_rows<D, 64>(nxt, a.K + base + (long long)(k0 + 64) * a.ld, a.ld, a.S - k0 - 64, tid);
-      stage_rows<D, 64>(nxt + TILE, a.V + base + (long long)(k0 + 64) * a.ld, a.ld, a.S - k0 - 64, tid);
+    const int kn = kb + NS - 1;   // tile issued now; its slot was last read in iteration kb - 1 (behind a barrier)
+    if (kn < nkb) {
+      char* nxt = smem + (kn % NS) * 2 * TILE;
+      stage_rows<D, 64, NW>(nxt, a.K + base + (long long)kn * 64 * a.ld, a.ld, a.S - kn * 64, tid);
+      stage_rows<D, 64, NW>(nxt + TILE, a.V + base + (long long)kn * 64 * a.ld, a.ld, a.S - kn * 64, tid);
     }
     if (!(a.causal && k0 > qw + 31)) {
       const bool need_mask = (a.causal && k0 + 63 > qw) || k0 + 64 > a.S;
       if (need_mask) dq_tile<D, true>(sK, sV, qf, df, lse2, dlt, acc, k0, qw, a.S, a.causal, c2, lane, a.prio & 2);
       else dq_tile<D, false>(sK, sV, qf, df, lse2, dlt, acc, k0, qw, a.S, a.causal, c2, lane, a.prio & 2);
     }
-    vm_wait<0>();   // staged tiles (asm LDS-DMA: the compiler does not track them) have landed
+    // tile kb + 1 must have landed; with NS = 3 tile kb + 2 may stay in flight across the barrier (counted wait:
+    // the only vector-memory ops of this loop are the DMA pieces, PPW per wave per tile)
+    if (NS == 3 && kb + 2 < nkb) vm_wait<PPW>();
+    else vm_wait<0>();
     __syncthreads();
   }
 #pragma unroll
@@ -555,33 +572,44 @@ __device__ __forceinline__ void dkv_chunk(const char* sQ, const char* sD, const 
 }
 
 // ----------------------------------------------------------------------------------------------------------------
-// dK/dV: block = 64 keys; wave w owns keys k0 + 16w + [0,16). Loop over 64-query chunks (Q, dO, lse, delta)
-// double-buffered in LDS via LDS-DMA.
-template <int D>
-__global__ __launch_bounds__(NTH, 2) void attn_bwd_dkv_kernel(AttnArgs a) {
+// dK/dV: block = NW x 16 keys; wave w owns keys k0 + 16w + [0,16). Loop over 64-query chunks (Q, dO, lse, delta) in
+// an NS-deep LDS ring filled by LDS-DMA NS - 1 chunks ahead.
+template <int D, int NW = 4, int NS = 2>
+__global__ __launch_bounds__(NW * 64, 2) void attn_bwd_dkv_kernel(AttnArgs a) {
   using G = Geo<D>;
   constexpr int QC = 64;
   constexpr int TILE = QC * G::ROWB;
   constexpr int STAGE = 2 * TILE + 2 * 256;   // Q, dO, lse[64], delta[64]
+  constexpr int KB = 16 * NW;                 // keys per block
+  constexpr int PPW = 2 * (TILE / 1024) / NW; // Q + dO pieces per wave per stage (+1 on waves 0 / 1: lse / delta)
+  static_assert(NS == 2 || (2 * (TILE / 1024)) % NW == 0, "counted waits need an even piece split");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, i = lane & 15;
   int bx, bh;
-  attn_block((a.S + 63) / 64, bx, bh);
+  attn_block((a.S + KB - 1) / KB, bx, bh);
   const int b = bh / a.H, h = bh % a.H;
-  const int kblk = bx * 64;
+  const int kblk = bx * KB;
   const int kw = kblk + w * 16;
   const long long base = (long long)b * a.S * a.ld + h * D;
+  const long long base_o = (long long)b * a.S * a.ld_o + h * D;
   const long long sbase = ((long long)b * a.H + h) * a.S;
   const int qstart = a.causal ? (kblk / QC) * QC : 0;
   const int nqc = (a.S - qstart + QC - 1) / QC;
 
   auto stage = [&](char* st, int q0) {
-    stage_rows<D, QC>(st, a.Q + base + (long long)q0 * a.ld, a.ld, a.S - q0, tid);
-    stage_rows<D, QC>(st + TILE, a.dO + base + (long long)q0 * a.ld, a.ld, a.S - q0, tid);
-    stage_f32(st + 2 * TILE, a.LSE + sbase + q0, QC, a.S - q0, tid);
-    stage_f32(st + 2 * TILE + 256, a.delta + sbase + q0, QC, a.S - q0, tid);
+    stage_rows<D, QC, NW>(st, a.Q + base + (long long)q0 * a.ld, a.ld, a.S - q0, tid);
+    stage_rows<D, QC, NW>(st + TILE, a.dO + base_o + (long long)q0 * a.ld_o, a.ld_o, a.S - q0, tid);
+    if (NW == 4) {   // wave 0 stages both
+      stage_f32(st + 2 * TILE, a.LSE + sbase + q0, QC, a.S - q0, tid);
+      stage_f32(st + 2 * TILE + 256, a.delta + sbase + q0, QC, a.S - q0, tid);
+    } else {         // wave 0: lse, wave 1: delta (one extra piece each)
+      stage_f32(st + 2 * TILE, a.LSE + sbase + q0, QC, a.S - q0, tid);
+      stage_f32(st + 2 * TILE + 256, a.delta + sbase + q0, QC, a.S - q0, tid - 64);
+    }
   };
-  if (nqc > 0) stage(smem, qstart);
+#pragma unroll
+  for (int c = 0; c < NS - 1; ++c)
+    if (c < nqc) stage(smem + c * STAGE, qstart + c * QC);
 
   bf16x8_t kf[G::DS], vf[G::DS];
   {
@@ -602,17 +630,24 @@ __global__ __launch_bounds__(NTH, 2) void attn_bwd_dkv_kernel(AttnArgs a) {
   __syncthreads();
   for (int c = 0; c < nqc; ++c) {
     const int q0 = qstart + c * QC;
-    const char* sQ = smem + (c & 1) * STAGE;
+    const char* sQ = smem + (c % NS) * STAGE;
     const char* sD = sQ + TILE;
     const float* sL = reinterpret_cast<const float*>(sQ + 2 * TILE);
     const float* sDl = sL + 64;
-    if (c + 1 < nqc) stage(smem + ((c + 1) & 1) * STAGE, q0 + QC);
+    const int cn = c + NS - 1;
+    if (cn < nqc) stage(smem + (cn % NS) * STAGE, qstart + cn * QC);
     if (!(a.causal && q0 + QC - 1 < kw)) {  // every query of this chunk precedes this wave's keys
       const bool need_mask = (a.causal && q0 < kw + 15) || q0 + QC > a.S || kw + 16 > a.S;
       if (need_mask) dkv_chunk<D, true>(sQ, sD, sL, sDl, kf, vf, dk, dv, q0, key, a.S, a.causal, c2, lane, a.prio & 1);
       else dkv_chunk<D, false>(sQ, sD, sL, sDl, kf, vf, dk, dv, q0, key, a.S, a.causal, c2, lane, a.prio & 1);
     }
-    vm_wait<0>();   // staged tiles (asm LDS-DMA: the compiler does not track them) have landed
+    // chunk c + 1 must have landed; with NS = 3 chunk c + 2 may stay in flight across the barrier
+    if (NS == 3 && c + 2 < nqc) {
+      if (w < 2) vm_wait<PPW + 1>();
+      else vm_wait<PPW>();
+    } else {
+      vm_wait<0>();
+    }
     __syncthreads();
   }
   if (key < a.S) {
@@ -835,7 +870,7 @@ __global__ __launch_bounds__(NTH, 2) void attn_fwd32_kernel(AttnArgs a) {
   l = xh_sum(l);
   if (q < a.S) {
     const float inv = 1.f / l;
-    bf16_t* orow = a.Oout + base + (long long)q * a.ld;
+    bf16_t* orow = a.Oout + (long long)b * a.S * a.ld_o + hd * D + (long long)q * a.ld_o;
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
@@ -1024,7 +1059,10 @@ static int attn_impl() {   // OBST_ATTN_IMPL=1 forces the 16x16x32 kernels (A/B 
   return v;
 }
 
-static int attn_bwd_impl() {   // OBST_ATTN_BWD=2 selects the 32x32x16 dK/dV kernel (slower so far: A/B only)
+// OBST_ATTN_BWD=2 selects the 32x32x16 dK/dV kernel; 3 (4 / 5: dQ / dK-dV only) the 8-wave blocks with 3-deep LDS
+// rings. A/B only: at B64 S2048 H16 D128 causal the default pair takes 5.23 ms, 3 / 4 / 5 take 5.86 / 5.68 / 5.61 ms
+// (the longer blocks lose more to the causal-diagonal imbalance than the deeper ring gains; r2 bench_attn_ab)
+static int attn_bwd_impl() {
   static int v = [] { const char* e = getenv("OBST_ATTN_BWD"); return e ? atoi(e) : 1; }();
   return v;
 }
@@ -1043,8 +1081,24 @@ int launch_fwd(const AttnArgs& a, hipStream_t st) {
 template <int D>
 int launch_bwd(const AttnArgs& a, hipStream_t st) {
   // dQ first: it also produces delta = rowsum(dO * O), which the dK/dV kernel reads
+  const int impl = attn_bwd_impl();
+  if (D == 128 && impl >= 3) {   // 8-wave blocks, 3-deep LDS rings (one block per CU): 3 both, 4 dQ only, 5 dK/dV only
+    if (impl != 5)
+      hipLaunchKernelGGL((attn_bwd_dq_kernel<D, 8, 3>), dim3((a.S + 255) / 256 * a.B * a.H), dim3(512),
+                         3 * 2 * 64 * Geo<D>::ROWB, st, a);
+    else
+      hipLaunchKernelGGL(attn_bwd_dq_kernel<D>, dim3((a.S + 127) / 128 * a.B * a.H), dim3(NTH),
+                         4 * 64 * Geo<D>::ROWB, st, a);
+    if (impl != 4)
+      hipLaunchKernelGGL((attn_bwd_dkv_kernel<D, 8, 3>), dim3((a.S + 127) / 128 * a.B * a.H), dim3(512),
+                         3 * (2 * 64 * Geo<D>::ROWB + 512), st, a);
+    else
+      hipLaunchKernelGGL(attn_bwd_dkv_kernel<D>, dim3((a.S + 63) / 64 * a.B * a.H), dim3(NTH),
+                         2 * (2 * 64 * Geo<D>::ROWB + 512), st, a);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(attn_bwd_dq_kernel<D>, dim3((a.S + 127) / 128 * a.B * a.H), dim3(NTH), 4 * 64 * Geo<D>::ROWB, st, a);
-  if (D == 128 && attn_bwd_impl() == 2)
+  if (D == 128 && attn_bwd_impl() == 2 && a.ld == a.ld_o)   // its Q / dO staging shares one row-offset table
     hipLaunchKernelGGL(attn_bwd_dkv32_kernel, dim3((a.S + 127) / 128 * a.B * a.H), dim3(NTH), 2 * (2 * 64 * 256 + 512),
                        st, a);
   else
@@ -1063,6 +1117,7 @@ struct ObstAttnDesc {
   long long ld;
   float scale;
   int causal;
+  long long ld_o;   // 0: same as ld
 };
 
 static bool fill(AttnArgs& a, const ObstAttnDesc* d) {
@@ -1071,9 +1126,11 @@ static bool fill(AttnArgs& a, const ObstAttnDesc* d) {
   a.Oout = (bf16_t*)d->Oout; a.dQ = (bf16_t*)d->dQ; a.dK = (bf16_t*)d->dK; a.dV = (bf16_t*)d->dV;
   a.LSE = d->LSE; a.delta = d->delta;
   a.B = d->B; a.S = d->S; a.H = d->H; a.ld = d->ld; a.scale = d->scale; a.causal = d->causal;
+  a.ld_o = d->ld_o ? d->ld_o : d->ld;
   static const int prio = [] { const char* e = getenv("OBST_ATTN_PRIO"); return e ? atoi(e) : 1; }();
   a.prio = prio;
-  return d->B > 0 && d->S > 0 && d->H > 0 && d->ld % 8 == 0 && d->ld >= (long long)d->H * d->D;
+  return d->B > 0 && d->S > 0 && d->H > 0 && d->ld % 8 == 0 && d->ld >= (long long)d->H * d->D &&
+         a.ld_o % 8 == 0 && a.ld_o >= (long long)d->H * d->D;
 }
 
 OBST_API int obst_attn_fwd(const ObstAttnDesc* d, hipStream_t st) {

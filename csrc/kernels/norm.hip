@@ -73,64 +73,78 @@ __device__ __forceinline__ void load_row(const bf16_t* x, int F, int sl, bool ok
   }
 }
 
+// The host sizes the grid so that the rows of one lane group (row, row + nw, ...) all belong to one parameter group
+// (nw % groups == 0): scale / shift are loaded into registers once, not re-fetched per row (with 256-wide group rows
+// the per-row parameter loads were 4x the row's own bytes)
 template <int NCH, int LPR>
 __global__ __launch_bounds__(NTH) void norm_fwd_kernel(const bf16_t* __restrict__ X, const float* __restrict__ scale,
                                                        const float* __restrict__ shift, bf16_t* __restrict__ Y,
                                                        float* __restrict__ rstd_out, long long rows, int F,
                                                        int groups, float eps, const float* __restrict__ ext_stats) {
   constexpr int RPW = 64 / LPR;
+  constexpr int U = 1;   // (2-4 rows in flight per lane group measured 2 % slower than 1)
   const int lane = threadIdx.x & 63, sub = lane / LPR, sl = lane % LPR;
   const long long nw = (long long)gridDim.x * 4 * RPW;
   long long r0 = ((long long)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
-  uint4 nxt[NCH];   // the next row's data is in flight while this row is reduced and written
-  load_raw<NCH, LPR>(X + (r0 + sub) * F, F, sl, r0 + sub < rows, nxt);
-  for (; r0 < rows; r0 += nw) {
-    const long long row = r0 + sub;
-    const bool ok = row < rows;
-    float v[NCH][8];
-    unpack_row<NCH>(nxt, v);
-    load_raw<NCH, LPR>(X + (row + nw) * F, F, sl, row + nw < rows, nxt);
-    float mean, rstd;
-    if (ext_stats) {  // [rows, 2] = (mean, rstd) computed over the full (TP-gathered) feature set
-      mean = ok ? ext_stats[2 * row] : 0.f;
-      rstd = ok ? ext_stats[2 * row + 1] : 0.f;
-    } else {
-      float s = 0.f;
-#pragma unroll
-      for (int c = 0; c < NCH; ++c)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) s += v[c][j];
-      mean = row_sum<LPR>(s) / F;
-      float q = 0.f;
-#pragma unroll
-      for (int c = 0; c < NCH; ++c)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int col = c * LPR * 8 + sl * 8 + j;
-          const float d = col < F ? v[c][j] - mean : 0.f;
-          q += d * d;
-        }
-      rstd = rsqrtf(row_sum<LPR>(q) / F + eps);
-    }
-    if (!ok) continue;
-    if (rstd_out && sl == 0) { rstd_out[2 * row] = mean; rstd_out[2 * row + 1] = rstd; }
-    const long long poff = (long long)(row % groups) * F;
+  float sc[NCH][8], sh[NCH][8];
+  {
+    const long long poff = (long long)((r0 + sub) % groups) * F;
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       const int col = c * LPR * 8 + sl * 8;
-      if (col >= F) continue;
-      float sc[8], sh[8];
-      if (scale) load8f(scale + poff + col, sc);
-      if (shift) load8f(shift + poff + col, sh);
-      uint32_t o[4];
+      if (scale && col < F) load8f(scale + poff + col, sc[c]);
+      if (shift && col < F) load8f(shift + poff + col, sh[c]);
+    }
+  }
+  uint4 nxt[U][NCH];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float y0 = (v[c][2 * j] - mean) * rstd, y1 = (v[c][2 * j + 1] - mean) * rstd;
-        if (scale) { y0 *= sc[2 * j]; y1 *= sc[2 * j + 1]; }
-        if (shift) { y0 += sh[2 * j]; y1 += sh[2 * j + 1]; }
-        o[j] = pack_bf16x2(y0, y1);
+  for (int u = 0; u < U; ++u) load_raw<NCH, LPR>(X + (r0 + u * nw + sub) * F, F, sl, r0 + u * nw + sub < rows, nxt[u]);
+  for (; r0 < rows; r0 += U * nw) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long row = r0 + u * nw + sub;
+      const bool ok = row < rows;
+      float v[NCH][8];
+      unpack_row<NCH>(nxt[u], v);
+      load_raw<NCH, LPR>(X + (row + U * nw) * F, F, sl, row + U * nw < rows, nxt[u]);
+      float mean, rstd;
+      if (ext_stats) {  // [rows, 2] = (mean, rstd) computed over the full (TP-gathered) feature set
+        mean = ok ? ext_stats[2 * row] : 0.f;
+        rstd = ok ? ext_stats[2 * row + 1] : 0.f;
+      } else {
+        float s = 0.f;
+#pragma unroll
+        for (int c = 0; c < NCH; ++c)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) s += v[c][j];
+        mean = row_sum<LPR>(s) / F;
+        float q = 0.f;
+#pragma unroll
+        for (int c = 0; c < NCH; ++c)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int col = c * LPR * 8 + sl * 8 + j;
+            const float d = col < F ? v[c][j] - mean : 0.f;
+            q += d * d;
+          }
+        rstd = rsqrtf(row_sum<LPR>(q) / F + eps);
       }
-      *reinterpret_cast<uint4*>(Y + row * F + col) = make_uint4(o[0], o[1], o[2], o[3]);
+      if (!ok) continue;
+      if (rstd_out && sl == 0) *reinterpret_cast<float2*>(rstd_out + 2 * row) = make_float2(mean, rstd);
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        const int col = c * LPR * 8 + sl * 8;
+        if (col >= F) continue;
+        uint32_t o[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float y0 = (v[c][2 * j] - mean) * rstd, y1 = (v[c][2 * j + 1] - mean) * rstd;
+          if (scale) { y0 *= sc[c][2 * j]; y1 *= sc[c][2 * j + 1]; }
+          if (shift) { y0 += sh[c][2 * j]; y1 += sh[c][2 * j + 1]; }
+          o[j] = pack_bf16x2(y0, y1);
+        }
+        *reinterpret_cast<uint4*>(Y + row * F + col) = make_uint4(o[0], o[1], o[2], o[3]);
+      }
     }
   }
 }
@@ -168,6 +182,14 @@ __global__ __launch_bounds__(NTH) void norm_bwd_kernel(const bf16_t* __restrict_
   constexpr int RPW = 64 / LPR;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* red_s = reinterpret_cast<float*>(smem);           // [4 waves][F] dscale partials, then dshift
+  // wide rows, one parameter group: scale staged once in LDS behind the reduction scratch (row reads by ds_read)
+  float* sc_s = red_s + 8 * LPR * 8;
+  const bool sc_lds = NCH > 2 && scale != nullptr && groups == 1;
+  if (sc_lds) {
+    for (int i = threadIdx.x * 4; i < F; i += NTH * 4)
+      *reinterpret_cast<float4*>(sc_s + i) = *reinterpret_cast<const float4*>(scale + i);
+    __syncthreads();
+  }
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, sub = lane / LPR, sl = lane % LPR;
   const bool want_param = (dscale || dshift) && partial_out == nullptr;
   float gs[NCH][8], gb[NCH][8];
@@ -177,35 +199,67 @@ __global__ __launch_bounds__(NTH) void norm_bwd_kernel(const bf16_t* __restrict_
     for (int j = 0; j < 8; ++j) gs[c][j] = gb[c][j] = 0.f;
   const long long nw = (long long)gridDim.x * 4 * RPW;
   const long long first = ((long long)blockIdx.x * 4 + w) * RPW + sub;
-  uint4 nx[NCH], nd[NCH], nr[NCH];   // next row (x, dy and the residual gradient) in flight while this one is processed
-  {
-    const long long row = ((long long)blockIdx.x * 4 + w) * RPW + sub;
-    load_raw<NCH, LPR>(X + row * F, F, sl, row < rows, nx);
-    load_raw<NCH, LPR>(DY + row * F, F, sl, row < rows, nd);
-    if (R) load_raw<NCH, LPR>(R + row * F, F, sl, row < rows, nr);
+  constexpr int U = NCH == 1 ? 4 : NCH == 2 ? 2 : 1;   // rows per lane group in flight
+  // next rows (x, dy, the residual gradient and the row statistics) in flight while this one is processed
+  uint4 nx[U][NCH], nd[U][NCH], nr[U][NCH];
+  float2 nst[U];
+  const long long rbase = ((long long)blockIdx.x * 4 + w) * RPW + sub;
+  // narrow rows: the lane group's scale is loaded once (all its rows are of group rbase % groups)
+  constexpr bool HOIST = NCH <= 2;
+  float hsc[HOIST ? NCH : 1][8];
+  if (HOIST && scale) {
+#pragma unroll
+    for (int c = 0; c < (HOIST ? NCH : 1); ++c) {
+      const int col0 = c * LPR * 8 + sl * 8;
+      if (col0 < F) load8f(scale + (long long)(rbase % groups) * F + col0, hsc[c]);
+    }
   }
-  for (long long r0 = ((long long)blockIdx.x * 4 + w) * RPW; r0 < rows; r0 += nw) {
-    const long long row = r0 + sub;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const long long row = rbase + u * nw;
+    load_raw<NCH, LPR>(X + row * F, F, sl, row < rows, nx[u]);
+    load_raw<NCH, LPR>(DY + row * F, F, sl, row < rows, nd[u]);
+    if (R) load_raw<NCH, LPR>(R + row * F, F, sl, row < rows, nr[u]);
+    nst[u] = row < rows ? *reinterpret_cast<const float2*>(stats + 2 * row) : make_float2(0.f, 0.f);
+  }
+  for (long long r0 = rbase - sub; r0 < rows; r0 += U * nw) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+    const long long row = r0 + u * nw + sub;
     const bool ok = row < rows;
+    const long long nrow = row + U * nw;
     float x[NCH][8], dy[NCH][8];
-    unpack_row<NCH>(nx, x);
-    unpack_row<NCH>(nd, dy);
+    unpack_row<NCH>(nx[u], x);
+    unpack_row<NCH>(nd[u], dy);
     uint4 cr[NCH];
     if (R) {
 #pragma unroll
-      for (int c = 0; c < NCH; ++c) cr[c] = nr[c];
-      load_raw<NCH, LPR>(R + (row + nw) * F, F, sl, row + nw < rows, nr);
+      for (int c = 0; c < NCH; ++c) cr[c] = nr[u][c];
+      load_raw<NCH, LPR>(R + nrow * F, F, sl, nrow < rows, nr[u]);
     }
-    load_raw<NCH, LPR>(X + (row + nw) * F, F, sl, row + nw < rows, nx);
-    load_raw<NCH, LPR>(DY + (row + nw) * F, F, sl, row + nw < rows, nd);
-    const float mean = ok ? stats[2 * row] : 0.f, rstd = ok ? stats[2 * row + 1] : 0.f;
+    load_raw<NCH, LPR>(X + nrow * F, F, sl, nrow < rows, nx[u]);
+    load_raw<NCH, LPR>(DY + nrow * F, F, sl, nrow < rows, nd[u]);
+    const float mean = ok ? nst[u].x : 0.f, rstd = ok ? nst[u].y : 0.f;
+    nst[u] = nrow < rows ? *reinterpret_cast<const float2*>(stats + 2 * nrow) : make_float2(0.f, 0.f);
     const long long poff = (long long)(row % groups) * F;
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       float gsc[8];
       const int col0 = c * LPR * 8 + sl * 8;
-      if (scale && ok && col0 < F) load8f(scale + poff + col0, gsc);
+      if (HOIST) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) gsc[j] = hsc[HOIST ? c : 0][j];
+      } else if (sc_lds) {
+        if (col0 < F) {
+          const float4 a4 = *reinterpret_cast<const float4*>(sc_s + col0);
+          const float4 b4 = *reinterpret_cast<const float4*>(sc_s + col0 + 4);
+          gsc[0] = a4.x; gsc[1] = a4.y; gsc[2] = a4.z; gsc[3] = a4.w;
+          gsc[4] = b4.x; gsc[5] = b4.y; gsc[6] = b4.z; gsc[7] = b4.w;
+        }
+      } else if (scale && ok && col0 < F) {
+        load8f(scale + poff + col0, gsc);
+      }
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int col = col0 + j;
@@ -236,10 +290,10 @@ __global__ __launch_bounds__(NTH) void norm_bwd_kernel(const bf16_t* __restrict_
       if (col >= F) continue;
       float r[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
       if (R) {   // the block's residual-input gradient, summed here instead of in a separate elementwise pass
-        const uint4 u = cr[c];
-        const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+        const uint4 uu = cr[c];
+        const uint32_t wv[4] = {uu.x, uu.y, uu.z, uu.w};
 #pragma unroll
-        for (int j = 0; j < 4; ++j) { r[2 * j] = bf2f(w[j] & 0xffff); r[2 * j + 1] = bf2f(w[j] >> 16); }
+        for (int j = 0; j < 4; ++j) { r[2 * j] = bf2f(wv[j] & 0xffff); r[2 * j + 1] = bf2f(wv[j] >> 16); }
       }
       uint32_t o[4];
 #pragma unroll
@@ -247,6 +301,7 @@ __global__ __launch_bounds__(NTH) void norm_bwd_kernel(const bf16_t* __restrict_
         o[j] = pack_bf16x2(rstd * (dy[c][2 * j] - m1 - x[c][2 * j] * m2) + r[2 * j],
                            rstd * (dy[c][2 * j + 1] - m1 - x[c][2 * j + 1] * m2) + r[2 * j + 1]);
       *reinterpret_cast<uint4*>(DX + row * F + col) = make_uint4(o[0], o[1], o[2], o[3]);
+    }
     }
   }
   if (want_param && groups > 1) {
@@ -371,9 +426,19 @@ static int lanes_per_row(int F) { return F <= 64 ? 8 : F <= 128 ? 16 : F <= 256 
     }                                                                                               \
   } while (0)
 
+static int group_aligned(int grid, int groups, int F) {
+  // rows per grid step (4 waves x 64/LPR rows per block) must be a multiple of groups
+  if (groups <= 1) return grid;
+  int a = groups, b = 4 * (64 / lanes_per_row(F));
+  while (b) { const int t = a % b; a = b; b = t; }
+  const int q = groups / a;                 // blocks per group period
+  return grid < q ? q : grid / q * q;
+}
+
 OBST_API int obst_norm_fwd(const ObstNormDesc* d, hipStream_t st) {
   if (d->F % 8 || d->rows <= 0) return -1;
-  NORM_DISPATCH(norm_fwd_kernel, dim3(grid_for(d->rows)), 0, (const bf16_t*)d->X, d->scale, d->shift, (bf16_t*)d->Y,
+  NORM_DISPATCH(norm_fwd_kernel, dim3(group_aligned(grid_for(d->rows), d->groups, d->F)), 0, (const bf16_t*)d->X,
+                d->scale, d->shift, (bf16_t*)d->Y,
                 d->stats, d->rows, d->F, d->groups, d->eps, d->ext);
   return (int)hipGetLastError();
 }
@@ -413,7 +478,9 @@ OBST_API int obst_norm_bwd(const ObstNormDesc* d, hipStream_t st) {
   if (d->F % 8 || d->rows <= 0) return -1;
   const bool params = norm_bwd_params(d);
   if (params && !d->ws) return -3;
-  const size_t lds = (d->groups == 1 && params) ? (size_t)8 * lanes_per_row(d->F) * 8 * 4 : 0;   // <= 16 KiB
+  // reduction scratch [8][LPR*8] floats (<= 16 KiB), plus the staged scale ([F] floats) for wide rows
+  const int nch = (d->F + lanes_per_row(d->F) * 8 - 1) / (lanes_per_row(d->F) * 8);
+  const size_t lds = (size_t)8 * lanes_per_row(d->F) * 8 * 4 + (nch > 2 && d->scale && d->groups == 1 ? d->F * 4 : 0);
   const int grid = norm_bwd_grid(d);
   NORM_DISPATCH(norm_bwd_kernel, dim3(grid), lds, (const bf16_t*)d->X, (const bf16_t*)d->DY, d->scale, d->stats,
                 (bf16_t*)d->DX, d->dscale, d->dshift, d->rows, d->F, d->groups, d->Ffull, d->partial, d->ext,

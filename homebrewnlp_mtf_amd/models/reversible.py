@@ -82,16 +82,28 @@ class _RevStack(torch.autograd.Function):
         sd = _stream_dtype(dt)
         g1 = torch.zeros_like(y1) if g1 is None else g1.to(sd)
         g2 = torch.zeros_like(y2) if g2 is None else g2.to(sd)
+        y1b = g2b = None    # bf16 copies of y1 / g2, written by the previous block's fused fp32 mixes
         for f in reversed(ctx.blocks):
             if mode == "revnet":
                 # y1 = x2, y2 = x1 + F(x2)
+                bf = dt == torch.bfloat16
+                if bf:
+                    y1b = raw.to_bf16(y1) if y1b is None else y1b
+                    g2b = raw.to_bf16(g2) if g2b is None else g2b
                 with torch.enable_grad():
-                    x2 = (raw.to_bf16(y1) if dt == torch.bfloat16 else y1.to(dt)).detach().requires_grad_(True)
+                    x2 = (y1b if bf else y1.to(dt)).detach().requires_grad_(True)
                     fx = f(x2)
-                torch.autograd.backward(fx, raw.to_bf16(g2) if dt == torch.bfloat16 else g2.to(dt))
-                if dt == torch.bfloat16:
-                    x1 = raw.mix_f32(y2, fx.detach(), 1.0, -1.0)
-                    dx2 = g1 if x2.grad is None else raw.mix_f32(g1, x2.grad, 1.0, 1.0)
+                torch.autograd.backward(fx, g2b if bf else g2.to(dt))
+                if bf:
+                    # x1 = y2 - F(x2) and dx2 = g1 + dF/dx2, each with its bf16 copy for the next (earlier) block
+                    nb1 = torch.empty_like(y1b)
+                    x1 = raw.mix_f32(y2, fx.detach(), 1.0, -1.0, yb=nb1)
+                    if x2.grad is None:
+                        dx2, nb2 = g1, None
+                    else:
+                        nb2 = torch.empty_like(y1b)
+                        dx2 = raw.mix_f32(g1, x2.grad, 1.0, 1.0, yb=nb2)
+                    y1b, g2b = nb1, nb2
                 else:
                     x1 = y2 - fx.detach().to(sd)
                     dx2 = g1 if x2.grad is None else g1 + x2.grad.to(sd)

@@ -253,6 +253,17 @@ class ParamStore:
             self._t_version[name] = ver
         return out
 
+    def derived(self, name: str, tag: str, fn: typing.Callable[[], torch.Tensor]) -> torch.Tensor:
+        """a tensor computed from variable `name`'s compute copy (e.g. the masked token-mixer weight), cached until
+        the next ``bump``: a depth-shared weight is derived once per step instead of once per use"""
+        cache = self.__dict__.setdefault("_derived", {})
+        ver = getattr(self, "version", 0)
+        hit = cache.get((name, tag))
+        if hit is None or hit[0] != ver:
+            hit = (ver, fn())
+            cache[(name, tag)] = hit
+        return hit[1]
+
     def zero_grad(self):
         self.grad.zero_()
         # variables whose gradient has received no contribution yet this step: their first weight-gradient GEMM

@@ -325,6 +325,13 @@ def ffn(x, w1, w2, xdims, w1dims, mdims, w2dims, odims, act, residual=None, carr
 # fused dot-product attention block (reference spatial.py:42-81 with 'dot_product', 'context'/'embedded' keys):
 #   base = act(x W_in);  k, q, v = base W_k, base W_q, base W_v;  out = softmax(q k^T * scale, causal) v (+ residual)
 class _DotAttention(torch.autograd.Function):
+    """k, q and v live interleaved in ONE token-major buffer kqv[T][3N] (row = k | q | v of a token; the attention
+    kernels take the 3N row stride), so with the three weights adjacent in the flat buffer (the registration order)
+      forward : kqv = base · [W_k W_q W_v]           -- one GEMM, N = 3N, on the stacked K-contiguous weight copies
+      dgrad   : dbase = dkqv · [W_k W_q W_v]ᵀ         -- one GEMM, K = 3N, no residual-input chaining
+      wgrad   : dW_j = baseᵀ · dkqv[:, jN:(j+1)N]     -- three GEMMs on column slices (3N row stride)
+    (GPT-Neo-1.3B: the three dgrads took 4.96 ms per layer as one plain + two residual-chained products)."""
+
     @staticmethod
     def forward(ctx, x, w_in, w_k, w_q, w_v, p_in: LinearPlan, p_out: LinearPlan, act, scale, causal, residual,
                 geo, carrier=None):
@@ -335,57 +342,49 @@ class _DotAttention(torch.autograd.Function):
         _fwd_gemm(xc, w_in, base, p_in, act=act, Zout=z)
         if p_in.row_parallel and pstate.tp_size() > 1:
             pstate.tp_all_reduce(base)
-        T = p_out.M
-        Nq = p_out.N
-        # q, k, v in one launch when the three weights are adjacent in the flat buffer
-        kqv = _empty([3] + p_out.canon_o_shape, xc)
-        _qkv_fwd(base, (w_k, w_q, w_v), kqv, p_out)
-        k, q, v = kqv[0], kqv[1], kqv[2]
+        T, K, N = p_out.M, p_out.K, p_out.N
+        kqv = _empty([T, 3 * N], xc)
+        _kqv_fwd(base, (w_k, w_q, w_v), kqv, p_out)
+        k, q, v = kqv[:, 0:N], kqv[:, N:2 * N], kqv[:, 2 * N:]
         o = _empty(p_out.canon_o_shape, xc)
         lse = torch.empty(B * H * S, dtype=torch.float32, device=xc.device)
-        ld = H * D
-        raw.attn_fwd(q, k, v, o, lse, B, S, H, D, ld, scale, causal)
+        raw.attn_fwd(q, k, v, o, lse, B, S, H, D, 3 * N, scale, causal, ld_o=H * D)
         if residual is not None:
             out = torch.empty_like(o)
             raw.elementwise("add", o, out, z=residual.contiguous())
         else:
             out = o
         ctx.save_for_backward(xc, w_in, w_k, w_q, w_v, z, base, kqv, o, lse)
-        ctx.cfg = (p_in, p_out, act, scale, causal, geo, residual is not None, T, Nq)
+        ctx.cfg = (p_in, p_out, act, scale, causal, geo, residual is not None)
         ctx.carrier = carrier
         return out
 
     @staticmethod
     def backward(ctx, dout):
         xc, w_in, w_k, w_q, w_v, z, base, kqv, o, lse = ctx.saved_tensors
-        p_in, p_out, act, scale, causal, (B, S, H, D), has_res, T, Nq = ctx.cfg
+        p_in, p_out, act, scale, causal, (B, S, H, D), has_res = ctx.cfg
         dout = dout.contiguous()
-        k, q, v = kqv[0], kqv[1], kqv[2]
+        T, K, N = p_out.M, p_out.K, p_out.N
+        k, q, v = kqv[:, 0:N], kqv[:, N:2 * N], kqv[:, 2 * N:]
         dkqv = torch.empty_like(kqv)
         delta = torch.empty(B * H * S, dtype=torch.float32, device=xc.device)
-        raw.attn_bwd(q, k, v, o, dout, lse, delta, dkqv[1], dkqv[0], dkqv[2], B, S, H, D, H * D, scale, causal)
-        # weight grads of k/q/v and dbase = sum_j dj W_j^T (chained through the residual input, last one fuses act')
-        dbase = _empty(p_in.canon_o_shape, xc)
+        raw.attn_bwd(q, k, v, o, dout, lse, delta, dkqv[:, N:2 * N], dkqv[:, 0:N], dkqv[:, 2 * N:], B, S, H, D,
+                     3 * N, scale, causal, ld_o=H * D)
         ws = (w_k, w_q, w_v)
-        outs = []
-        Mo, Ko, No = p_out.M, p_out.H * p_out.K, p_out.H * p_out.N
-        baseT = tokens_transposed(base, Mo, Ko)
-        if baseT is None and raw.on_gpu(base) and raw.lt_enabled() and Mo % 8 == 0 and Ko % 8 == 0:
+        dbase = _empty(p_in.canon_o_shape, xc)
+        _kqv_dgrad(dkqv, ws, dbase, p_out, act, z)
+        baseT = None
+        if raw.on_gpu(base) and raw.lt_enabled() and T % 8 == 0 and K % 8 == 0:
             # one transpose of base serves the three q/k/v weight gradients (tools/bench_wgrad.py: -118 us each
             # against the token-strided layout, for one 122 us transpose)
-            baseT = torch.empty(Ko * Mo, dtype=base.dtype, device=base.device)
-            raw.transpose(base, baseT, Mo, Ko, Ko, Mo)
-        dkqvT = None
-        if baseT is not None and Mo % 8 == 0 and No % 8 == 0 and not raw.lt_enabled():
-            dkqvT = torch.empty(3 * No * Mo, dtype=dkqv.dtype, device=dkqv.device)
-            raw.transpose(dkqv, dkqvT, Mo, No, No, Mo, 3, Mo * No, Mo * No)
+            baseT = torch.empty(K * T, dtype=base.dtype, device=base.device)
+            raw.transpose(base, baseT, T, K, K, T)
+        outs = []
         for j in range(3):
-            last = j == 2
-            _dgrad_gemm(dkqv[j], ws[j], dbase, p_out, act=act if last else None,
-                        Zin=z if (last and act) else None, R=dbase if j > 0 else None)
             g, m, bj = _acc_grad_beta(ws[j])
-            _wgrad_gemm(base, dkqv[j], g, p_out, xT=baseT, beta=bj,
-                        dyT=None if dkqvT is None else dkqvT[j * No * Mo:(j + 1) * No * Mo])
+            dyj = dkqv[:, j * N:(j + 1) * N]
+            a_op = raw.Operand(baseT, 0, T, K * T) if baseT is not None else raw.Operand(base, 1, K, K * T)
+            raw.gemm(a_op, raw.Operand(dyj, 1, 3 * N), raw.Operand(g, 0, N, K * N), K, N, T, beta=bj)
             _done(ws[j])
             outs.append(None if m else g.to(ws[j].dtype))
         if p_out.col_parallel and pstate.tp_size() > 1:
@@ -404,32 +403,53 @@ class _DotAttention(torch.autograd.Function):
                 dres, None, None)
 
 
-def _qkv_fwd(base, ws, out, p: LinearPlan):
-    """k, q, v = base @ W_j. One batched launch if the three weights are equally spaced in memory."""
+def _stacked(ws) -> bool:
+    """the three weights are equal-sized blocks adjacent in the flat buffer, in order (registration order)"""
+    w0 = ws[0]
+    n = w0.numel()
+    es = w0.element_size()
+    return (all(w.is_contiguous() and w.numel() == n for w in ws) and ws[1].data_ptr() - w0.data_ptr() == n * es
+            and ws[2].data_ptr() - ws[1].data_ptr() == n * es)
+
+
+def _kqv_fwd(base, ws, kqv, p: LinearPlan):
+    """kqv[T][3N] = base · [W_k W_q W_v]"""
     M, H, K, N = p.M, p.H, p.K, p.N
-    stride = ws[1].data_ptr() - ws[0].data_ptr()
-    es = ws[0].element_size()
-    same = (H == 1 and stride > 0 and stride % es == 0 and ws[2].data_ptr() - ws[1].data_ptr() == stride
-            and all(w.is_contiguous() for w in ws))
-    if same:
-        wt = _wT(ws[0], p)
-        if wt is not None and raw.lt_enabled():
-            # hipBLASLt on the K-contiguous copies: three plain products (1478 TF/s each on GPT-Neo-1.3B against
-            # 1307 TF/s for the batched product on the [K][N] weights; hipBLASLt faults on a batched [N][K] B with
-            # a shared A, so that combination is never issued -- blaslt.cpp declines it)
-            for j in range(3):
-                _fwd_gemm(base, ws[j], out[j], p)
-            return
-        if wt is not None:
-            for j in (1, 2):
-                _wT(ws[j], p)           # refresh the neighbours' transposed copies too
-            bop = raw.Operand(wt, 0, K, stride // es)
-        else:
-            bop = raw.Operand(ws[0], 1, N, stride // es)
-        raw.gemm(raw.Operand(base, 0, K, 0), bop, raw.Operand(out, 0, N, M * N), M, N, K, batch=(3, 1))
-    else:
-        for j in range(3):
-            _fwd_gemm(base, ws[j], out[j], p)
+    if H != 1:
+        raise NotImplementedError("interleaved k|q|v projection needs plain [K][N] weights")
+    wt = _wT(ws[0], p) if _stacked(ws) else None
+    if wt is not None:
+        for j in (1, 2):
+            _wT(ws[j], p)           # refresh the neighbours' transposed copies (adjacent to wt: a [3N][K] stack)
+        raw.gemm(raw.Operand(base, 0, K), raw.Operand(wt, 0, K), raw.Operand(kqv, 0, 3 * N), M, 3 * N, K)
+        return
+    if _stacked(ws):   # one batched launch: C block j at column offset j*N of the 3N-wide rows
+        raw.gemm(raw.Operand(base, 0, K, 0), raw.Operand(ws[0], 1, N, K * N), raw.Operand(kqv, 0, 3 * N, N),
+                 M, N, K, batch=(3, 1))
+        return
+    for j in range(3):
+        raw.gemm(raw.Operand(base, 0, K), raw.Operand(ws[j], 1, N), raw.Operand(kqv[:, j * N:], 0, 3 * N), M, N, K)
+
+
+def _kqv_dgrad(dkqv, ws, dbase, p: LinearPlan, act, z):
+    """dbase = act'(z) * (dkqv · [W_k W_q W_v]ᵀ): on the GPU ONE GEMM over K = 3N whose B operand is the weights
+    concatenated along N ([K][3N], derived once per step); elsewhere three products chained through the residual
+    input"""
+    M, K, N = p.M, p.K, p.N
+    w0 = ws[0]
+    store = getattr(w0, "store", None)
+    if raw.on_gpu(dkqv) and store is not None and _stacked(ws):
+        cat = store.derived(w0.var_name, f"kqv_cat@{w0.data_ptr()}",
+                            lambda: torch.as_strided(w0.detach(), (3, K, N), (K * N, N, 1)).permute(1, 0, 2)
+                            .contiguous().view(K, 3 * N))
+        raw.gemm(raw.Operand(dkqv, 0, 3 * N), raw.Operand(cat, 0, 3 * N), raw.Operand(dbase, 0, K), M, K, 3 * N,
+                 act=act, act_bwd=act is not None, Zin=z if act else None)
+        return
+    for j in range(3):
+        last = j == 2
+        raw.gemm(raw.Operand(dkqv[:, j * N:], 0, 3 * N), raw.Operand(ws[j], 0, N), raw.Operand(dbase, 0, K),
+                 M, K, N, act=act if last else None, act_bwd=last and act is not None,
+                 Zin=z if (last and act) else None, R=dbase if j > 0 else None)
 
 
 def dot_attention(x, w_in, w_k, w_q, w_v, xdims, w_in_dims, base_dims, w_out_dims, act, scale, causal, geo,
@@ -449,7 +469,12 @@ class _TokenMixer(torch.autograd.Function):
     def forward(ctx, x, w, causal: bool):
         B, S, H, Fd = x.shape
         xc = x.contiguous()
-        wm = torch.tril(w) if causal else w.contiguous()
+        store = getattr(w, "store", None)
+        if causal and store is not None and w.device.type == "cuda":
+            # the masked weight of a depth-shared mixer is built once per step (ParamStore.derived)
+            wm = store.derived(w.var_name, f"tril@{w.data_ptr()}", lambda: torch.tril(w.detach()))
+        else:
+            wm = torch.tril(w) if causal else w.contiguous()
         y = torch.empty_like(xc)
         hf = H * Fd
         raw.gemm(raw.Operand(wm, 0, S, 0, S * S), raw.Operand(xc, 1, hf, S * hf, Fd), raw.Operand(y, 0, hf, S * hf, Fd),

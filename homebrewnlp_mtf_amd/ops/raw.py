@@ -262,19 +262,21 @@ def _bshd(t: torch.Tensor, B, S, H, D, ld):
     return torch.as_strided(t, (B, S, H, D), (S * ld, ld, D, 1), t.storage_offset())
 
 
-def attn_fwd(q, k, v, o, lse, B, S, H, D, ld, scale: float, causal: bool):
+def attn_fwd(q, k, v, o, lse, B, S, H, D, ld, scale: float, causal: bool, ld_o: int = 0):
+    """ld: token stride of q / k / v (H*D, or 3*H*D for an interleaved k|q|v buffer); ld_o: that of o (0: ld)"""
     if q.device.type == "meta":
         return None
+    ld_o = ld_o or ld
     if on_gpu(q):
         if D not in (32, 64, 128):
             raise L.KernelError(f"attention head dim {D} not supported by the HIP kernel (32/64/128)")
-        for nm, t in (("q", q), ("k", k), ("v", v), ("o", o)):
+        for nm, t, l in (("q", q, ld), ("k", k, ld), ("v", v, ld), ("o", o, ld_o)):
             if t.dtype != torch.bfloat16:
                 raise L.KernelError(f"attention {nm} must be bf16")
-            _need(t, (B * S - 1) * ld + (H - 1) * D + D - 1, nm)
+            _need(t, (B * S - 1) * l + (H - 1) * D + D - 1, nm)
         _need(lse, B * H * S - 1, "lse")
         d = L.AttnDesc(q.data_ptr(), k.data_ptr(), v.data_ptr(), 0, 0, o.data_ptr(), 0, 0, 0, lse.data_ptr(), 0,
-                       B, S, H, D, ld, float(scale), int(causal))
+                       B, S, H, D, ld, float(scale), int(causal), ld_o)
         L.check(L.lib().obst_attn_fwd(d, L.stream_ptr()), "attn_fwd")
         return
     qv, kv, vv = (_f(_bshd(t, B, S, H, D, ld)) for t in (q, k, v))
@@ -283,28 +285,32 @@ def attn_fwd(q, k, v, o, lse, B, S, H, D, ld, scale: float, causal: bool):
         s = s.masked_fill(torch.ones(S, S, dtype=torch.bool, device=s.device).triu(1), float("-inf"))
     m = s.logsumexp(-1)
     p = torch.exp(s - m.unsqueeze(-1))
-    _bshd(o, B, S, H, D, ld).copy_(torch.einsum("bhqk,bkhd->bqhd", p, vv))
+    _bshd(o, B, S, H, D, ld_o).copy_(torch.einsum("bhqk,bkhd->bqhd", p, vv))
     lse.view(B, H, S).copy_(m)
 
 
-def attn_bwd(q, k, v, o, do, lse, delta, dq, dk, dv, B, S, H, D, ld, scale: float, causal: bool):
+def attn_bwd(q, k, v, o, do, lse, delta, dq, dk, dv, B, S, H, D, ld, scale: float, causal: bool, ld_o: int = 0):
+    """ld: token stride of q / k / v and dq / dk / dv; ld_o: that of o and do (0: ld)"""
     if q.device.type == "meta":
         return None
+    ld_o = ld_o or ld
     if on_gpu(q):
         if D not in (32, 64, 128):
             raise L.KernelError(f"attention head dim {D} not supported by the HIP kernel (32/64/128)")
-        for nm, t in (("q", q), ("k", k), ("v", v), ("o", o), ("do", do), ("dq", dq), ("dk", dk), ("dv", dv)):
+        for nm, t, l in (("q", q, ld), ("k", k, ld), ("v", v, ld), ("o", o, ld_o), ("do", do, ld_o), ("dq", dq, ld),
+                         ("dk", dk, ld), ("dv", dv, ld)):
             if t.dtype != torch.bfloat16:
                 raise L.KernelError(f"attention {nm} must be bf16")
-            _need(t, (B * S - 1) * ld + (H - 1) * D + D - 1, nm)
+            _need(t, (B * S - 1) * l + (H - 1) * D + D - 1, nm)
         _need(lse, B * H * S - 1, "lse")
         _need(delta, B * H * S - 1, "delta")
         d = L.AttnDesc(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), do.data_ptr(), 0, dq.data_ptr(),
                        dk.data_ptr(), dv.data_ptr(), lse.data_ptr(), delta.data_ptr(), B, S, H, D, ld, float(scale),
-                       int(causal))
+                       int(causal), ld_o)
         L.check(L.lib().obst_attn_bwd(d, L.stream_ptr()), "attn_bwd")
         return
-    qv, kv, vv, ov, dov = (_f(_bshd(t, B, S, H, D, ld)) for t in (q, k, v, o, do))
+    qv, kv, vv = (_f(_bshd(t, B, S, H, D, ld)) for t in (q, k, v))
+    ov, dov = (_f(_bshd(t, B, S, H, D, ld_o)) for t in (o, do))
     s = torch.einsum("bqhd,bkhd->bhqk", qv, kv) * scale
     if causal:
         s = s.masked_fill(torch.ones(S, S, dtype=torch.bool, device=s.device).triu(1), float("-inf"))
