@@ -616,7 +616,54 @@ __device__ __forceinline__ void rows_body(const ApplyArgs& a, const OptTensor& T
     }
     float rmax = 0.f;
     const long long rbase = T.off + (long long)row * C + ck.col0;
-    for (int c = tid * V; c < ck.ncols; c += RW_NT * V) {
+    int c0 = tid * V;
+    if (PROG == 1 && V == 4 && sm3_on && a.final_seg && !a.uin && !a.emit_stats) {
+      // the shipped chain on float4 rows, two column groups per pass with every load of both issued before any
+      // store: the generic loop below issues one group's loads only after the previous group's stores (the
+      // compiler cannot prove master / mom / compute apart), one round trip per 1024 columns
+      const Stage M = a.st[2];
+      const float lr = lr_of(a), cl = F[0];
+      for (; c0 + RW_NT * V < ck.ncols; c0 += 2 * RW_NT * V) {
+        const int cc[2] = {c0, c0 + RW_NT * V};
+        float4 gv[2], wv[2], mv[2], av[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const long long gi = rbase + cc[u];
+          gv[u] = *reinterpret_cast<const float4*>(a.grad + gi);
+          wv[u] = *reinterpret_cast<const float4*>(a.master + gi);
+          mv[u] = *reinterpret_cast<const float4*>(a.mom + gi);
+          av[u] = *reinterpret_cast<const float4*>(acc_last + cc[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const long long gi = rbase + cc[u];
+          float g[4] = {gv[u].x, gv[u].y, gv[u].z, gv[u].w}, w[4] = {wv[u].x, wv[u].y, wv[u].z, wv[u].w};
+          float m[4] = {mv[u].x, mv[u].y, mv[u].z, mv[u].w}, al[4] = {av[u].x, av[u].y, av[u].z, av[u].w};
+          float tm[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            tm[j] = tmax[cc[u] + j];
+            g[j] *= a.grad_scale;   // same operation order as the generic path: bit-identical updates
+            g[j] *= cl;
+            const float nu = fminf(lead, al[j]) + g[j] * g[j];
+            tm[j] = fmaxf(tm[j], nu);
+            rmax = fmaxf(rmax, nu);
+            g[j] *= opt_rsqrt(nu);
+            m[j] = M.a * m[j] + g[j] * M.b;
+            g[j] = (M.c != 0.f ? g[j] + M.a * m[j] : m[j]) * lr;
+            if (T.flags & 2) g[j] *= a.rezero_mult;
+            if ((T.flags & 1) && a.wd > 0.f) g[j] += w[j] * lr * a.wd;
+            w[j] -= g[j];
+            tmax[cc[u] + j] = tm[j];
+          }
+          *reinterpret_cast<float4*>(a.mom + gi) = make_float4(m[0], m[1], m[2], m[3]);
+          *reinterpret_cast<float4*>(a.master + gi) = make_float4(w[0], w[1], w[2], w[3]);
+          if (a.compute)
+            *reinterpret_cast<uint2*>(a.compute + gi) = make_uint2(pack_bf16x2(w[0], w[1]), pack_bf16x2(w[2], w[3]));
+        }
+      }
+    }
+    for (int c = c0; c < ck.ncols; c += RW_NT * V) {
       const long long gi = rbase + c;
       float g[V], w[V];
       if (V == 4) {
