@@ -213,7 +213,7 @@ Plan make_plan(State& S, const Key& k, const Runner& run_in) {
 // has kernels for them (hipBLASLt's GELU is the tanh form, the reference's: src/model/activation.py). Otherwise the
 // Python layer (ops/raw.py) splits an activation GEMM into a plain hipBLASLt GEMM plus the elementwise kernel.
 int obst_blaslt_gemm(const ObstGemmDesc* d, hipStream_t stream) {
-  if (!enabled() || d->tri != 0) return 1;
+  if (!enabled() || d->tri != 0 || d->kin != 0) return 1;
   int epi = 0;
   if (d->act == 0) {
     if (d->mode != 0 || d->Zout || d->Zin) return 1;

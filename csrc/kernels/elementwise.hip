@@ -224,7 +224,10 @@ OBST_API int obst_elementwise(const ObstEwDesc* d, hipStream_t st) {
   auto k = ew_kernel<-1, -1>;
   if (d->act == ACT_GELU && d->op == 0) k = ew_kernel<0, ACT_GELU>;
   else if (d->act == ACT_GELU && d->op == 1) k = ew_kernel<1, ACT_GELU>;
+  else if (d->act == ACT_RELU && d->op == 0) k = ew_kernel<0, ACT_RELU>;   // bottleneck linears (ctx32_mixer)
+  else if (d->act == ACT_RELU && d->op == 1) k = ew_kernel<1, ACT_RELU>;
   else if (d->op == 2) k = ew_kernel<2, 0>;
+  else if (d->op == 5) k = ew_kernel<5, 0>;                                  // axpby (MomentumNet / RevNet)
   hipLaunchKernelGGL(k, dim3(grid_for(nvec)), dim3(NTH), 0, st, d->op, d->act, (const bf16_t*)d->X,
                      (const bf16_t*)d->Z, (bf16_t*)d->Y, nvec, d->sptr, d->alpha, d->beta, d->seed, d->keep);
   return (int)hipGetLastError();

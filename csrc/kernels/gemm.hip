@@ -39,6 +39,8 @@ struct GemmArgs {
                           // 3 only C[m][n] with n <= m is produced (strictly-upper outputs get no contribution)
   int ksplit;             // phase kernel only: K split over blockIdx.y; partial tiles go to `ws` [split][M][N]
   float* ws;              // split-K workspace (fp32), summed into C by splitk_reduce_kernel
+  int kin;                // phase kernel only: split contraction index, see ObstGemmDesc (0: plain K)
+  long long a_sk, b_sk;
 };
 
 __device__ __forceinline__ int kswz(int k) { return ((k & 3) << 1) | (((k >> 3) & 1) << 3); }
@@ -448,7 +450,7 @@ __device__ __forceinline__ void bar() {
 }
 
 template <int T, bool IS_A>
-__device__ __forceinline__ void stage_piece(char* img, const bf16_t* X, long long ld, int base0, int R, int k0,
+__device__ __forceinline__ void stage_piece(char* img, const bf16_t* X, long long ld, int base0, int R, long long k0,
                                             int q, int wave, int lane) {
 #pragma unroll
   for (int rd = 0; rd < 2; ++rd) {
@@ -493,14 +495,26 @@ __global__ __launch_bounds__(NT2, 1) void gemm_ph_kernel(GemmArgs p) {
   if (p.tri == 1) kspan = min(p.K, (m0 + BM2 + BK - 1) / BK * BK);             // A[m][k] = 0 for k > m
   if (p.tri == 2) { kbeg = min(m0 / BK * BK, p.K - BK); kspan = p.K - kbeg; }   // A[m][k] = 0 for k < m
   if (p.tri == 3 && OUT_F32 && p.beta == 1.f && n0 > m0 + BM2 - 1) return;     // no output in this tile
-  const bf16_t* A = p.A + b1 * p.a_s1 + b2 * p.a_s2 + (A_T == 0 ? (long long)kbeg : (long long)kbeg * p.lda);
-  const bf16_t* B = p.B + b1 * p.b_s1 + b2 * p.b_s2 + (B_T == 0 ? (long long)kbeg : (long long)kbeg * p.ldb);
+  const bool ksp = p.kin > 0;   // split contraction index: tile offsets are mapped per tile (K-contiguous operands)
+  const bf16_t* A = p.A + b1 * p.a_s1 + b2 * p.a_s2 +
+                    (ksp ? 0LL : (A_T == 0 ? (long long)kbeg : (long long)kbeg * p.lda));
+  const bf16_t* B = p.B + b1 * p.b_s1 + b2 * p.b_s2 +
+                    (ksp ? 0LL : (B_T == 0 ? (long long)kbeg : (long long)kbeg * p.ldb));
   const int nk = kspan / BK;
+  auto ktile = [&](int t, long long sk) -> long long {   // element offset of k-tile t (kin % BK == 0)
+    if (!ksp) return (long long)t * BK;
+    const int k = kbeg + t * BK;
+    return (long long)(k / p.kin) * sk + (k % p.kin);
+  };
 
   // piece slots: (parity * 4 + {A0, A1, B0, B1}) * 16 KiB
   auto slot = [&](int t, int pc) -> char* { return smem + ((t & 1) * 4 + pc) * PIECE; };
-  auto stageA = [&](int t, int q) { stage_piece<A_T, true>(slot(t, q), A, p.lda, m0, p.M, t * BK, q, wave, lane); };
-  auto stageB = [&](int t, int q) { stage_piece<B_T, false>(slot(t, 2 + q), B, p.ldb, n0, p.N, t * BK, q, wave, lane); };
+  auto stageA = [&](int t, int q) {
+    stage_piece<A_T, true>(slot(t, q), A, p.lda, m0, p.M, ktile(t, p.a_sk), q, wave, lane);
+  };
+  auto stageB = [&](int t, int q) {
+    stage_piece<B_T, false>(slot(t, 2 + q), B, p.ldb, n0, p.N, ktile(t, p.b_sk), q, wave, lane);
+  };
 
   f32x4_t acc[8][4];
 #pragma unroll
@@ -698,6 +712,17 @@ OBST_API int obst_gemm(const ObstGemmDesc* d, hipStream_t stream) {
   a.M = d->M; a.N = d->N; a.K = d->K; a.nb2 = d->batch2;
   a.tiles_m = (d->M + BM - 1) / BM; a.tiles_n = (d->N + BN - 1) / BN;
   a.alpha = d->alpha; a.beta = d->beta; a.act = d->act; a.mode = d->mode; a.tri = d->tri;
+  a.kin = d->kin; a.a_sk = d->a_sk; a.b_sk = d->b_sk;
+  if (d->kin) {   // split contraction index: phase kernel, K-contiguous operands, whole 64-deep tiles per inner block
+    if (d->kin < 0 || d->kin % 64 || d->K % d->kin || d->a_t || d->b_t || (d->tri == 1 || d->tri == 2) ||
+        d->a_sk % 8 || d->b_sk % 8 || d->M < 256 || d->N < 256)
+      return -9;
+    a.ksplit = 1;
+    a.ws = nullptr;
+    const int batch = d->batch1 * d->batch2;
+    hipError_t e = d->out_f32 ? launch_ph<0, 0, true>(a, batch, stream) : launch_ph<0, 0, false>(a, batch, stream);
+    return e == hipSuccess ? 0 : (int)e;
+  }
   if (d->tri < 0 || d->tri > 3 || ((d->tri == 1 || d->tri == 2) && d->M != d->K) || (d->tri == 3 && d->M != d->N))
     return -8;
   const int batch = d->batch1 * d->batch2;

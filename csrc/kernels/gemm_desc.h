@@ -9,6 +9,10 @@ struct ObstGemmDesc {
   int a_t, b_t, out_f32, act, mode;
   float alpha, beta;
   int tri;
+  // split contraction index (MFMA phase kernel, K-contiguous operands only): k -> (k / kin) * sk + k % kin, i.e.
+  // K = (outer, inner) with inner blocks of kin contiguous elements and an outer stride a_sk / b_sk (0: plain K)
+  int kin;
+  long long a_sk, b_sk;
 };
 
 // plain GEMMs through hipBLASLt: 0 done, 1 not eligible (run the MFMA kernels), < 0 hipBLASLt error

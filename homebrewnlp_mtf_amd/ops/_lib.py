@@ -44,7 +44,7 @@ class GemmDesc(ctypes.Structure):
                 ("a_s1", c_ll), ("a_s2", c_ll), ("b_s1", c_ll), ("b_s2", c_ll), ("c_s1", c_ll), ("c_s2", c_ll),
                 ("M", c_i), ("N", c_i), ("K", c_i), ("batch1", c_i), ("batch2", c_i),
                 ("a_t", c_i), ("b_t", c_i), ("out_f32", c_i), ("act", c_i), ("mode", c_i),
-                ("alpha", c_f), ("beta", c_f), ("tri", c_i)]
+                ("alpha", c_f), ("beta", c_f), ("tri", c_i), ("kin", c_i), ("a_sk", c_ll), ("b_sk", c_ll)]
 
 
 class AttnDesc(ctypes.Structure):

@@ -495,12 +495,17 @@ class _TokenMixer(torch.autograd.Function):
             raw.gemm(raw.Operand(wm, 1, S, 0, S * S), raw.Operand(dy, 1, hf, S * hf, Fd),
                      raw.Operand(dx, 0, hf, S * hf, Fd), S, Fd, S, batch=(B, H), tri=2 if ctx.causal else 0)
         g, m = _acc_grad(w)
-        # dW[h] = dy_h · x_hᵀ over (batch, features): both operands as [H][S][B*F] (K-contiguous)
-        dyp = dy.permute(2, 1, 0, 3).reshape(H, S, B * Fd).contiguous()
-        xp = xc.permute(2, 1, 0, 3).reshape(H, S, B * Fd).contiguous()
+        # dW[h] = dy_h · x_hᵀ over (batch, features), both read in place from [B, S, H, F]: the contraction index
+        # (b, f) is split (kin = F contiguous features, outer stride S*H*F), so no [H][S][B*F] copies are made
         kk = B * Fd
-        raw.gemm(raw.Operand(dyp, 0, kk, 0, S * kk), raw.Operand(xp, 0, kk, 0, S * kk), raw.Operand(g, 0, S, 0, S * S),
-                 S, S, kk, batch=(1, H), beta=1.0, tri=3 if ctx.causal else 0)
+        if raw.on_gpu(dy) and Fd % 64 == 0 and S >= 256:
+            raw.gemm(raw.Operand(dy, 0, hf, 0, Fd), raw.Operand(xc, 0, hf, 0, Fd), raw.Operand(g, 0, S, 0, S * S),
+                     S, S, kk, batch=(1, H), beta=1.0, tri=3 if ctx.causal else 0, kin=Fd, a_sk=S * hf, b_sk=S * hf)
+        else:
+            dyp = dy.permute(2, 1, 0, 3).reshape(H, S, B * Fd).contiguous()
+            xp = xc.permute(2, 1, 0, 3).reshape(H, S, B * Fd).contiguous()
+            raw.gemm(raw.Operand(dyp, 0, kk, 0, S * kk), raw.Operand(xp, 0, kk, 0, S * kk),
+                     raw.Operand(g, 0, S, 0, S * S), S, S, kk, batch=(1, H), beta=1.0, tri=3 if ctx.causal else 0)
         _done(w)
         return dx, (None if m else g.to(w.dtype)), None
 

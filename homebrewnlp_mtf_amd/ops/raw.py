@@ -163,17 +163,21 @@ def _skinny_ws(device, n: int) -> typing.Optional[torch.Tensor]:
 def gemm(a: Operand, b: Operand, c: Operand, M: int, N: int, K: int, batch: typing.Tuple[int, int] = (1, 1),
          alpha: float = 1.0, beta: float = 0.0, act: typing.Optional[str] = None, act_bwd: bool = False,
          R: typing.Optional[torch.Tensor] = None, Zout: typing.Optional[torch.Tensor] = None,
-         Zin: typing.Optional[torch.Tensor] = None, tri: int = 0):
+         Zin: typing.Optional[torch.Tensor] = None, tri: int = 0, kin: int = 0, a_sk: int = 0, b_sk: int = 0):
     """C = epilogue(alpha * A·B). R, Zout, Zin share C's leading dims / batch strides.
     tri: 1/2 = A is lower/upper triangular (zero tiles are skipped, A must hold the zeros), 3 = only the lower
     triangle (n <= m) of C receives the product (M == N).
+    kin > 0 (K-contiguous A and B only): the contraction index is split, k -> (k // kin) * sk + k % kin with the
+    outer strides a_sk / b_sk -- a product over (batch, feature) pairs of a [B, S, H, F] tensor reads it in place.
 
     epilogue (act_bwd False): v = alpha*acc (+ beta*C if C is fp32) (+ R); Zout <- v; C <- act(v)
     epilogue (act_bwd True) : C <- (alpha*acc + R) * act'(Zin)"""
     if c.t.device.type == "meta":
         return c.t
     b1, b2 = batch
-    if (on_gpu(c.t) and skinny_ok(M, N, K) and act is None and R is None and Zout is None and Zin is None
+    if kin and (a.trans or b.trans or K % kin):
+        raise L.KernelError("split contraction index needs K-contiguous operands and K % kin == 0")
+    if (not kin and on_gpu(c.t) and skinny_ok(M, N, K) and act is None and R is None and Zout is None and Zin is None
             and tri == 0 and b1 * b2 == 1 and alpha == 1.0 and a.trans == 0 and b.trans == 0
             and c.t.dtype == torch.bfloat16 and a.t.dtype == torch.bfloat16 and b.t.dtype == torch.bfloat16
             and a.ld % 8 == 0 and b.ld % 8 == 0 and c.ld % 4 == 0 and a.ld >= K and b.ld >= K and c.ld >= N
@@ -186,7 +190,7 @@ def gemm(a: Operand, b: Operand, c: Operand, M: int, N: int, K: int, batch: typi
         L.check(L.lib().obst_skinny_gemm(a.t.data_ptr(), a.ld, b.t.data_ptr(), b.ld, c.t.data_ptr(), c.ld, M, N, K,
                                          L.ptr(ws), L.stream_ptr()), "skinny_gemm")
         return c.t
-    if (on_gpu(c.t) and act is not None and tri == 0 and lt_enabled() == 1 and c.t.dtype == torch.bfloat16
+    if (not kin and on_gpu(c.t) and act is not None and tri == 0 and lt_enabled() == 1 and c.t.dtype == torch.bfloat16
             and b1 * b2 == 1 and c.ld == N and (M * N) % 8 == 0 and c.t.is_contiguous() and c.t.numel() == M * N):
         # activation GEMM on hipBLASLt: plain product, then the elementwise kernel (pre-activation kept in Zout)
         if not act_bwd:
@@ -197,7 +201,7 @@ def gemm(a: Operand, b: Operand, c: Operand, M: int, N: int, K: int, batch: typi
             gemm(a, b, c, M, N, K, alpha=alpha, R=R)
             elementwise("act_bwd", Zin, c.t, z=c.t, act=act)    # in place: C = C * act'(Zin)
         return c.t
-    if (on_gpu(c.t) and R is not None and act is None and tri == 0 and lt_enabled() == 1 and _RSPLIT
+    if (not kin and on_gpu(c.t) and R is not None and act is None and tri == 0 and lt_enabled() == 1 and _RSPLIT
             and c.t.dtype == torch.bfloat16 and b1 * b2 == 1 and c.ld == N and (M * N) % 8 == 0
             and c.t.is_contiguous() and c.t.numel() == M * N and R.is_contiguous() and R.numel() == M * N):
         # residual input: hipBLASLt's out-of-place beta*C path runs 2-3x slower than the plain product on some
@@ -215,22 +219,32 @@ def gemm(a: Operand, b: Operand, c: Operand, M: int, N: int, K: int, batch: typi
         if (R is not None or Zout is not None or Zin is not None) and out_f32 and (Zout is not None or act_bwd):
             raise L.KernelError("pre-activation output / activation-backward epilogue need a bf16 output")
         bo = (b1 - 1) * a.s1 + (b2 - 1) * a.s2
-        _need(a.t, bo + ((M - 1) * a.ld + K - 1 if a.trans == 0 else (K - 1) * a.ld + M - 1), "A")
+        kext_a = (K // kin - 1) * a_sk + kin - 1 if kin else K - 1
+        kext_b = (K // kin - 1) * b_sk + kin - 1 if kin else K - 1
+        _need(a.t, bo + ((M - 1) * a.ld + kext_a if a.trans == 0 else (K - 1) * a.ld + M - 1), "A")
         bo = (b1 - 1) * b.s1 + (b2 - 1) * b.s2
-        _need(b.t, bo + ((N - 1) * b.ld + K - 1 if b.trans == 0 else (K - 1) * b.ld + N - 1), "B")
+        _need(b.t, bo + ((N - 1) * b.ld + kext_b if b.trans == 0 else (K - 1) * b.ld + N - 1), "B")
         cmax = (b1 - 1) * c.s1 + (b2 - 1) * c.s2 + (M - 1) * c.ld + N - 1
         for nm, t in (("C", c.t), ("R", R), ("Zout", Zout), ("Zin", Zin)):
             _need(t, cmax, nm)
         d = L.GemmDesc(a.t.data_ptr(), b.t.data_ptr(), c.t.data_ptr(), L.ptr(R), L.ptr(Zout), L.ptr(Zin),
                        a.ld, b.ld, c.ld, a.s1, a.s2, b.s1, b.s2, c.s1, c.s2, M, N, K, b1, b2,
-                       a.trans, b.trans, int(out_f32), ACTS[act], int(act_bwd), float(alpha), float(beta), int(tri))
+                       a.trans, b.trans, int(out_f32), ACTS[act], int(act_bwd), float(alpha), float(beta), int(tri),
+                       int(kin), int(a_sk), int(b_sk))
         L.check(L.lib().obst_gemm(d, L.stream_ptr()), "gemm")
         return c.t
     # ---- torch oracle
-    av = torch.as_strided(a.t, (b1, b2, M, K), (a.s1, a.s2, a.ld, 1) if a.trans == 0 else (a.s1, a.s2, 1, a.ld),
-                          a.t.storage_offset())
-    bv = torch.as_strided(b.t, (b1, b2, K, N), (b.s1, b.s2, 1, b.ld) if b.trans == 0 else (b.s1, b.s2, b.ld, 1),
-                          b.t.storage_offset())
+    if kin:
+        ko = K // kin
+        av = torch.as_strided(a.t, (b1, b2, M, ko, kin), (a.s1, a.s2, a.ld, a_sk, 1),
+                              a.t.storage_offset()).reshape(b1, b2, M, K)
+        bv = torch.as_strided(b.t, (b1, b2, N, ko, kin), (b.s1, b.s2, b.ld, b_sk, 1),
+                              b.t.storage_offset()).reshape(b1, b2, N, K).transpose(2, 3)
+    else:
+        av = torch.as_strided(a.t, (b1, b2, M, K), (a.s1, a.s2, a.ld, 1) if a.trans == 0 else (a.s1, a.s2, 1, a.ld),
+                              a.t.storage_offset())
+        bv = torch.as_strided(b.t, (b1, b2, K, N), (b.s1, b.s2, 1, b.ld) if b.trans == 0 else (b.s1, b.s2, b.ld, 1),
+                              b.t.storage_offset())
     shape, strides = (b1, b2, M, N), (c.s1, c.s2, c.ld, 1)
 
     def view(t):

@@ -371,3 +371,18 @@ def test_skinny_gemm_matches_fp32(cuda, M, K, N, monkeypatch):
     assert torch.equal(first, c)
     ref = a.float() @ w.float()
     _close(c.view(M, N).float().cpu(), ref, 2e-2, 2e-2, f"skinny {M}x{K}x{N}")
+
+
+@pytest.mark.parametrize("out_f32", [False, True])
+def test_gemm_split_contraction_index(cuda, out_f32):
+    """C[h] = A_h · B_hᵀ with the contraction over (b, f) pairs of [B, S, H, F] tensors read in place (kin = F)"""
+    torch.manual_seed(11)
+    Bb, S, H, Fd = 4, 512, 2, 128
+    a = (torch.randn(Bb, S, H, Fd) * 0.5).to(BF)
+    b = (torch.randn(Bb, S, H, Fd) * 0.5).to(BF)
+    hf = H * Fd
+    c = torch.zeros(H * S * S, device=cuda, dtype=torch.float32 if out_f32 else BF)
+    raw.gemm(raw.Operand(a.to(cuda).flatten(), 0, hf, 0, Fd), raw.Operand(b.to(cuda).flatten(), 0, hf, 0, Fd),
+             raw.Operand(c, 0, S, 0, S * S), S, S, Bb * Fd, batch=(1, H), kin=Fd, a_sk=S * hf, b_sk=S * hf)
+    ref = torch.einsum("bshf,bthf->hst", a.float(), b.float())
+    _close(c.view(H, S, S).float().cpu(), ref, 3e-2, 2e-2, "split-index gemm")
