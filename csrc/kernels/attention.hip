@@ -69,15 +69,16 @@ template <int D, int ROWS, int NW = 4>
 __device__ __forceinline__ void stage_rows(char* lds, const bf16_t* g, long long ld, int nvalid, int tid) {
   constexpr int CPR = Geo<D>::CPR;
   constexpr int PIECES = ROWS * CPR * 16 / 1024;   // 1 KiB pieces in the image
-  constexpr int RPP = 64 / CPR;                    // rows per piece
+  static_assert(ROWS * CPR % 64 == 0, "the image must be whole 1 KiB pieces");
   const int wave = tid >> 6, lane = tid & 63;
   const int last = nvalid - 1;
 #pragma unroll
   for (int i = 0; i < (PIECES + NW - 1) / NW; ++i) {
     const int j = wave + NW * i;
     if (PIECES % NW == 0 || j < PIECES) {
-      const int row = j * RPP + lane / CPR;
-      const int p = lane % CPR;
+      // chunk j*64 + lane of the row-major image (D = 96: 12 chunks per row, so a piece straddles rows)
+      const int row = (j * 64 + lane) / CPR;
+      const int p = (j * 64 + lane) % CPR;
       const int c = p ^ swz16<D>(row);
       const int srow = row < last ? row : last;
       glds16_asm(g + srow * ld + c * 8, lds + j * 1024);
@@ -1139,6 +1140,7 @@ OBST_API int obst_attn_fwd(const ObstAttnDesc* d, hipStream_t st) {
   switch (d->D) {
     case 32: return launch_fwd<32>(a, st);
     case 64: return launch_fwd<64>(a, st);
+    case 96: return launch_fwd<96>(a, st);
     case 128: return launch_fwd<128>(a, st);
     default: return -2;
   }
@@ -1150,6 +1152,7 @@ OBST_API int obst_attn_bwd(const ObstAttnDesc* d, hipStream_t st) {
   switch (d->D) {
     case 32: return launch_bwd<32>(a, st);
     case 64: return launch_bwd<64>(a, st);
+    case 96: return launch_bwd<96>(a, st);
     case 128: return launch_bwd<128>(a, st);
     default: return -2;
   }

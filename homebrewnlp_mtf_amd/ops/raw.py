@@ -282,8 +282,8 @@ def attn_fwd(q, k, v, o, lse, B, S, H, D, ld, scale: float, causal: bool, ld_o: 
         return None
     ld_o = ld_o or ld
     if on_gpu(q):
-        if D not in (32, 64, 128):
-            raise L.KernelError(f"attention head dim {D} not supported by the HIP kernel (32/64/128)")
+        if D not in (32, 64, 96, 128):
+            raise L.KernelError(f"attention head dim {D} not supported by the HIP kernel (32/64/96/128)")
         for nm, t, l in (("q", q, ld), ("k", k, ld), ("v", v, ld), ("o", o, ld_o)):
             if t.dtype != torch.bfloat16:
                 raise L.KernelError(f"attention {nm} must be bf16")
@@ -309,8 +309,8 @@ def attn_bwd(q, k, v, o, do, lse, delta, dq, dk, dv, B, S, H, D, ld, scale: floa
         return None
     ld_o = ld_o or ld
     if on_gpu(q):
-        if D not in (32, 64, 128):
-            raise L.KernelError(f"attention head dim {D} not supported by the HIP kernel (32/64/128)")
+        if D not in (32, 64, 96, 128):
+            raise L.KernelError(f"attention head dim {D} not supported by the HIP kernel (32/64/96/128)")
         for nm, t, l in (("q", q, ld), ("k", k, ld), ("v", v, ld), ("o", o, ld_o), ("do", do, ld_o), ("dq", dq, ld),
                          ("dk", dk, ld), ("dv", dv, ld)):
             if t.dtype != torch.bfloat16:

@@ -166,7 +166,7 @@ def test_gemm_oob_rejected(cuda):
 
 
 # ----------------------------------------------------------------------------------------------------------------
-@pytest.mark.parametrize("D", [32, 64, 128])
+@pytest.mark.parametrize("D", [32, 64, 96, 128])
 @pytest.mark.parametrize("S,causal", [(128, True), (200, True), (256, False), (64, True), (576, True), (1000, False)])
 def test_attention_fwd_bwd(cuda, D, S, causal):
     torch.manual_seed(D + S)

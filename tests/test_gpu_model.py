@@ -28,9 +28,11 @@ def _pair(cfg, cuda):
     return m_cpu, m_gpu
 
 
-@pytest.mark.parametrize("variant", ["gpt", "revnet", "mixer"])
+@pytest.mark.parametrize("variant", ["gpt", "gpt_d96", "revnet", "mixer"])
 def test_model_forward_backward(cuda, variant):
     cfg = dict(GPT)
+    if variant == "gpt_d96":     # GPT-Neo 20B-scale head dim
+        cfg.update(features_per_head=96)
     if variant == "revnet":
         cfg.update(memory_reduction_strategy="revnet",
                    block_config=[{"layer": ["norm-shift-scale", "attention-dot_product-context"]},
@@ -61,7 +63,7 @@ def test_model_forward_backward(cuda, variant):
         denom = a.norm().item() + 1e-6
         rel = (a - b).norm().item() / denom
         # reversible bodies reconstruct activations in bf16 (as the reference does): drift grows towards the input
-        tol = 0.08 if variant == "gpt" else 0.2
+        tol = 0.08 if variant.startswith("gpt") else 0.2
         assert rel < tol, f"{variant}: gradient of {name} off by {rel:.3f} (|g|={denom:.3g})"
 
 
