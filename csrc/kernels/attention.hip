@@ -512,21 +512,26 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_bwd_dq_kernel(AttnArgs a) {
   }
 }
 
-// one 64-query chunk of the dK/dV kernel for a wave's 16 keys (key on the lane: S = Q·Kᵀ, P and dS feed dVᵀ and
-// dKᵀ as B operands straight from the accumulators). dP starts from -delta[q] (read from LDS as one f32x4 per tile).
-template <int D, bool MASK>
+// one 64-query chunk of the dK/dV kernel for a wave's KG groups of 16 keys (key on the lane: S = Q·Kᵀ, P and dS feed
+// dVᵀ and dKᵀ as B operands straight from the accumulators). dP starts from -delta[q] (read from LDS as one f32x4 per
+// tile). Every Q / dO fragment read from LDS feeds KG MFMAs: with KG = 2 the LDS bytes per MFMA halve (at KG = 1 the
+// 104 LDS reads of a chunk take ~2300 LDS cycles per CU against ~2050 MFMA cycles per SIMD: LDS-bound).
+template <int D, bool MASK, int KG>
 __device__ __forceinline__ void dkv_chunk(const char* sQ, const char* sD, const float* sL, const float* sDl,
-                                          const bf16x8_t (&kf)[Geo<D>::DS], const bf16x8_t (&vf)[Geo<D>::DS],
-                                          f32x4_t (&dk)[Geo<D>::DT], f32x4_t (&dv)[Geo<D>::DT], int q0, int key, int S,
-                                          int causal, float c2, int lane, int prio) {
+                                          const bf16x8_t (&kf)[KG][Geo<D>::DS], const bf16x8_t (&vf)[KG][Geo<D>::DS],
+                                          f32x4_t (&dk)[KG][Geo<D>::DT], f32x4_t (&dv)[KG][Geo<D>::DT], int q0,
+                                          int key, int S, int causal, float c2, int lane, int prio) {
   using G = Geo<D>;
   const int g = lane >> 4;
-  f32x4_t sc[4], dp[4];
+  f32x4_t sc[KG][4], dp[KG][4];
 #pragma unroll
   for (int qt = 0; qt < 4; ++qt) {
     const float4 dl = *reinterpret_cast<const float4*>(sDl + qt * 16 + 4 * g);
-    sc[qt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    dp[qt] = f32x4_t{-dl.x, -dl.y, -dl.z, -dl.w};
+#pragma unroll
+    for (int j = 0; j < KG; ++j) {
+      sc[j][qt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      dp[j][qt] = f32x4_t{-dl.x, -dl.y, -dl.z, -dl.w};
+    }
   }
   if (prio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -535,53 +540,66 @@ __device__ __forceinline__ void dkv_chunk(const char* sQ, const char* sD, const 
     for (int qt = 0; qt < 4; ++qt) {
       bf16x8_t qa = row_frag<D>(sQ, qt * 16, ds, lane);
       bf16x8_t da = row_frag<D>(sD, qt * 16, ds, lane);
-      sc[qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa, kf[ds], sc[qt], 0, 0, 0);
-      dp[qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, vf[ds], dp[qt], 0, 0, 0);
+#pragma unroll
+      for (int j = 0; j < KG; ++j) {
+        sc[j][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa, kf[j][ds], sc[j][qt], 0, 0, 0);
+        dp[j][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, vf[j][ds], dp[j][qt], 0, 0, 0);
+      }
     }
   }
   if (prio) __builtin_amdgcn_s_setprio(0);
-  // sc[qt][v] = S[q = q0 + qt*16 + 4g + v][key]
+  // sc[j][qt][v] = S[q = q0 + qt*16 + 4g + v][key + 16 j]
 #pragma unroll
   for (int qt = 0; qt < 4; ++qt) {
     const float4 lv = *reinterpret_cast<const float4*>(sL + qt * 16 + 4 * g);
     const float nl[4] = {-lv.x * LOG2E, -lv.y * LOG2E, -lv.z * LOG2E, -lv.w * LOG2E};
 #pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      float pv = fexp2(__builtin_fmaf(sc[qt][v], c2, nl[v]));
-      if (MASK) {
-        const int q = q0 + qt * 16 + 4 * g + v;
-        pv = (q >= S || key >= S || (causal && key > q)) ? 0.f : pv;
+    for (int j = 0; j < KG; ++j)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        float pv = fexp2(__builtin_fmaf(sc[j][qt][v], c2, nl[v]));
+        if (MASK) {
+          const int q = q0 + qt * 16 + 4 * g + v, kj = key + 16 * j;
+          pv = (q >= S || kj >= S || (causal && kj > q)) ? 0.f : pv;
+        }
+        sc[j][qt][v] = pv;
+        dp[j][qt][v] = pv * dp[j][qt][v];
       }
-      sc[qt][v] = pv;
-      dp[qt][v] = pv * dp[qt][v];
-    }
   }
   if (prio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
   for (int st = 0; st < 2; ++st) {
-    const bf16x8_t pb = pack_p(sc[2 * st], sc[2 * st + 1]);
-    const bf16x8_t sb = pack_p(dp[2 * st], dp[2 * st + 1]);
+    bf16x8_t pb[KG], sb[KG];
+#pragma unroll
+    for (int j = 0; j < KG; ++j) {
+      pb[j] = pack_p(sc[j][2 * st], sc[j][2 * st + 1]);
+      sb[j] = pack_p(dp[j][2 * st], dp[j][2 * st + 1]);
+    }
 #pragma unroll
     for (int dt = 0; dt < G::DT; ++dt) {
       bf16x8_t dot = tr_frag<D>(sD, st * 32, dt * 16, lane);
       bf16x8_t qtr = tr_frag<D>(sQ, st * 32, dt * 16, lane);
-      dv[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dot, pb, dv[dt], 0, 0, 0);
-      dk[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qtr, sb, dk[dt], 0, 0, 0);
+#pragma unroll
+      for (int j = 0; j < KG; ++j) {
+        dv[j][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dot, pb[j], dv[j][dt], 0, 0, 0);
+        dk[j][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qtr, sb[j], dk[j][dt], 0, 0, 0);
+      }
     }
   }
   if (prio) __builtin_amdgcn_s_setprio(0);
 }
 
 // ----------------------------------------------------------------------------------------------------------------
-// dK/dV: block = NW x 16 keys; wave w owns keys k0 + 16w + [0,16). Loop over 64-query chunks (Q, dO, lse, delta) in
-// an NS-deep LDS ring filled by LDS-DMA NS - 1 chunks ahead.
-template <int D, int NW = 4, int NS = 2>
-__global__ __launch_bounds__(NW * 64, 2) void attn_bwd_dkv_kernel(AttnArgs a) {
+// dK/dV: block = NW x KG x 16 keys; wave w owns keys k0 + 16 KG w + [0, 16 KG). Loop over 64-query chunks (Q, dO, lse,
+// delta) in an NS-deep LDS ring filled by LDS-DMA NS - 1 chunks ahead. KG = 2 holds ~300 registers: one wave per SIMD.
+template <int D, int NW = 4, int NS = 2, int KG = 1>
+__global__ __launch_bounds__(NW * 64, KG == 1 ? 2 : 1) void attn_bwd_dkv_kernel(AttnArgs a) {
   using G = Geo<D>;
   constexpr int QC = 64;
   constexpr int TILE = QC * G::ROWB;
   constexpr int STAGE = 2 * TILE + 2 * 256;   // Q, dO, lse[64], delta[64]
-  constexpr int KB = 16 * NW;                 // keys per block
+  constexpr int KW = 16 * KG;                 // keys per wave
+  constexpr int KB = KW * NW;                 // keys per block
   constexpr int PPW = 2 * (TILE / 1024) / NW; // Q + dO pieces per wave per stage (+1 on waves 0 / 1: lse / delta)
   static_assert(NS == 2 || (2 * (TILE / 1024)) % NW == 0, "counted waits need an even piece split");
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -590,7 +608,7 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_bwd_dkv_kernel(AttnArgs a) {
   attn_block((a.S + KB - 1) / KB, bx, bh);
   const int b = bh / a.H, h = bh % a.H;
   const int kblk = bx * KB;
-  const int kw = kblk + w * 16;
+  const int kw = kblk + w * KW;
   const long long base = (long long)b * a.S * a.ld + h * D;
   const long long base_o = (long long)b * a.S * a.ld_o + h * D;
   const long long sbase = ((long long)b * a.H + h) * a.S;
@@ -612,19 +630,22 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_bwd_dkv_kernel(AttnArgs a) {
   for (int c = 0; c < NS - 1; ++c)
     if (c < nqc) stage(smem + c * STAGE, qstart + c * QC);
 
-  bf16x8_t kf[G::DS], vf[G::DS];
-  {
-    const int key = kw + i;
+  bf16x8_t kf[KG][G::DS], vf[KG][G::DS];
+#pragma unroll
+  for (int j = 0; j < KG; ++j) {
+    const int key = kw + 16 * j + i;
     const bool ok = key < a.S;
 #pragma unroll
     for (int ds = 0; ds < G::DS; ++ds) {
-      kf[ds] = load_frag_g(a.K + base + (long long)key * a.ld + ds * 32 + 8 * g, ok);
-      vf[ds] = load_frag_g(a.V + base + (long long)key * a.ld + ds * 32 + 8 * g, ok);
+      kf[j][ds] = load_frag_g(a.K + base + (long long)key * a.ld + ds * 32 + 8 * g, ok);
+      vf[j][ds] = load_frag_g(a.V + base + (long long)key * a.ld + ds * 32 + 8 * g, ok);
     }
   }
-  f32x4_t dk[G::DT], dv[G::DT];
+  f32x4_t dk[KG][G::DT], dv[KG][G::DT];
 #pragma unroll
-  for (int dt = 0; dt < G::DT; ++dt) dk[dt] = dv[dt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  for (int j = 0; j < KG; ++j)
+#pragma unroll
+    for (int dt = 0; dt < G::DT; ++dt) dk[j][dt] = dv[j][dt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   const float c2 = a.scale * LOG2E;
   const int key = kw + i;
   vm_wait<0>();   // staged tiles (asm LDS-DMA: the compiler does not track them) have landed
@@ -638,28 +659,35 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_bwd_dkv_kernel(AttnArgs a) {
     const int cn = c + NS - 1;
     if (cn < nqc) stage(smem + (cn % NS) * STAGE, qstart + cn * QC);
     if (!(a.causal && q0 + QC - 1 < kw)) {  // every query of this chunk precedes this wave's keys
-      const bool need_mask = (a.causal && q0 < kw + 15) || q0 + QC > a.S || kw + 16 > a.S;
-      if (need_mask) dkv_chunk<D, true>(sQ, sD, sL, sDl, kf, vf, dk, dv, q0, key, a.S, a.causal, c2, lane, a.prio & 1);
-      else dkv_chunk<D, false>(sQ, sD, sL, sDl, kf, vf, dk, dv, q0, key, a.S, a.causal, c2, lane, a.prio & 1);
+      const bool need_mask = (a.causal && q0 < kw + KW - 1) || q0 + QC > a.S || kw + KW > a.S;
+      if (need_mask)
+        dkv_chunk<D, true, KG>(sQ, sD, sL, sDl, kf, vf, dk, dv, q0, key, a.S, a.causal, c2, lane, a.prio & 1);
+      else
+        dkv_chunk<D, false, KG>(sQ, sD, sL, sDl, kf, vf, dk, dv, q0, key, a.S, a.causal, c2, lane, a.prio & 1);
     }
     // chunk c + 1 must have landed; with NS = 3 chunk c + 2 may stay in flight across the barrier
-    if (NS == 3 && c + 2 < nqc) {
-      if (w < 2) vm_wait<PPW + 1>();
+    if (NS == 3 && c + 2 < nqc) {   // lse / delta pieces: NW = 4 wave 0 issues both, NW = 8 waves 0 and 1 one each
+      if (NW == 4 && w == 0) vm_wait<PPW + 2>();
+      else if (NW != 4 && w < 2) vm_wait<PPW + 1>();
       else vm_wait<PPW>();
     } else {
       vm_wait<0>();
     }
     __syncthreads();
   }
-  if (key < a.S) {
 #pragma unroll
-    for (int dt = 0; dt < G::DT; ++dt) {
-      const int d = dt * 16 + 4 * g;
-      const float sc = a.scale;
-      *reinterpret_cast<uint2*>(a.dK + base + (long long)key * a.ld + d) =
-          make_uint2(pack_bf16x2(dk[dt][0] * sc, dk[dt][1] * sc), pack_bf16x2(dk[dt][2] * sc, dk[dt][3] * sc));
-      *reinterpret_cast<uint2*>(a.dV + base + (long long)key * a.ld + d) =
-          make_uint2(pack_bf16x2(dv[dt][0], dv[dt][1]), pack_bf16x2(dv[dt][2], dv[dt][3]));
+  for (int j = 0; j < KG; ++j) {
+    const int kj = key + 16 * j;
+    if (kj < a.S) {
+#pragma unroll
+      for (int dt = 0; dt < G::DT; ++dt) {
+        const int d = dt * 16 + 4 * g;
+        const float sc = a.scale;
+        *reinterpret_cast<uint2*>(a.dK + base + (long long)kj * a.ld + d) =
+            make_uint2(pack_bf16x2(dk[j][dt][0] * sc, dk[j][dt][1] * sc), pack_bf16x2(dk[j][dt][2] * sc, dk[j][dt][3] * sc));
+        *reinterpret_cast<uint2*>(a.dV + base + (long long)kj * a.ld + d) =
+            make_uint2(pack_bf16x2(dv[j][dt][0], dv[j][dt][1]), pack_bf16x2(dv[j][dt][2], dv[j][dt][3]));
+      }
     }
   }
 }
@@ -1063,6 +1091,14 @@ static int attn_impl() {   // OBST_ATTN_IMPL=1 forces the 16x16x32 kernels (A/B 
 // OBST_ATTN_BWD=2 selects the 32x32x16 dK/dV kernel; 3 (4 / 5: dQ / dK-dV only) the 8-wave blocks with 3-deep LDS
 // rings. A/B only: at B64 S2048 H16 D128 causal the default pair takes 5.23 ms, 3 / 4 / 5 take 5.86 / 5.68 / 5.61 ms
 // (the longer blocks lose more to the causal-diagonal imbalance than the deeper ring gains; r2 bench_attn_ab)
+// OBST_ATTN_DKV_KG=2: two 16-key groups per dK/dV wave (half the LDS bytes per MFMA, ~490 registers: one wave per
+// SIMD). A/B only: B64 S2048 H16 D128 causal backward 5.24 -> 6.27 ms (3-deep ring: 6.33) -- without the partner
+// wave the softmax VALU and the LDS waits no longer hide under another wave's MFMAs (r2 tools/gpu_attn_kg.sh)
+static int attn_dkv_kg() {
+  static int v = [] { const char* e = getenv("OBST_ATTN_DKV_KG"); return e ? atoi(e) : 1; }();
+  return v;
+}
+
 static int attn_bwd_impl() {
   static int v = [] { const char* e = getenv("OBST_ATTN_BWD"); return e ? atoi(e) : 1; }();
   return v;
@@ -1102,6 +1138,9 @@ int launch_bwd(const AttnArgs& a, hipStream_t st) {
   if (D == 128 && attn_bwd_impl() == 2 && a.ld == a.ld_o)   // its Q / dO staging shares one row-offset table
     hipLaunchKernelGGL(attn_bwd_dkv32_kernel, dim3((a.S + 127) / 128 * a.B * a.H), dim3(NTH), 2 * (2 * 64 * 256 + 512),
                        st, a);
+  else if (attn_dkv_kg() == 2)
+    hipLaunchKernelGGL((attn_bwd_dkv_kernel<D, 4, 2, 2>), dim3((a.S + 127) / 128 * a.B * a.H), dim3(NTH),
+                       2 * (2 * 64 * Geo<D>::ROWB + 512), st, a);
   else
     hipLaunchKernelGGL(attn_bwd_dkv_kernel<D>, dim3((a.S + 63) / 64 * a.B * a.H), dim3(NTH),
                        2 * (2 * 64 * Geo<D>::ROWB + 512), st, a);
