@@ -153,7 +153,21 @@ struct AttnArgs {
   float scale;
   int causal;
   int prio;       // s_setprio(1) around the MFMA clusters: bit 0 dK/dV kernel (default on: -2 %), bit 1 dQ (+1 %: off)
+  const bf16_t* Res;   // forward, optional: Sum = bf16(O) + Res, the block's residual add (O's layout, row stride ld_o)
+  bf16_t* Sum;
 };
+
+// the forward epilogue's 4-element store of O (and, with a residual, of O + residual from the rounded O values)
+__device__ __forceinline__ void store_o4(const AttnArgs& a, long long off, float v0, float v1, float v2, float v3) {
+  const uint2 ov = make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
+  *reinterpret_cast<uint2*>(a.Oout + off) = ov;
+  if (a.Sum) {
+    const uint2 r = *reinterpret_cast<const uint2*>(a.Res + off);
+    *reinterpret_cast<uint2*>(a.Sum + off) =
+        make_uint2(pack_bf16x2(bf2f(ov.x & 0xffff) + bf2f(r.x & 0xffff), bf2f(ov.x >> 16) + bf2f(r.x >> 16)),
+                   pack_bf16x2(bf2f(ov.y & 0xffff) + bf2f(r.y & 0xffff), bf2f(ov.y >> 16) + bf2f(r.y >> 16)));
+  }
+}
 
 // ----------------------------------------------------------------------------------------------------------------
 // raw v_exp_f32 (2^x): no denormal range fix-up (exp2f adds a compare + 2 ldexp per call); -inf -> 0
@@ -308,7 +322,7 @@ __global__ __launch_bounds__(NTH, 2) void attn_fwd_kernel(AttnArgs a) {
     __syncthreads();
   }
   // epilogue: lane holds O[q = qw + qt*16 + i][d = dt*16 + 4g + v]
-  bf16_t* Ob = a.Oout + (long long)b * a.S * a.ld_o + h * D;
+  const long long ob = (long long)b * a.S * a.ld_o + h * D;
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
     const int q = qw + qt * 16 + i;
@@ -317,8 +331,8 @@ __global__ __launch_bounds__(NTH, 2) void attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
     for (int dt = 0; dt < G::DT; ++dt) {
       const int d = dt * 16 + 4 * g;
-      *reinterpret_cast<uint2*>(Ob + (long long)q * a.ld_o + d) =
-          make_uint2(pack_bf16x2(o[dt][qt][0] * inv, o[dt][qt][1] * inv), pack_bf16x2(o[dt][qt][2] * inv, o[dt][qt][3] * inv));
+      store_o4(a, ob + (long long)q * a.ld_o + d, o[dt][qt][0] * inv, o[dt][qt][1] * inv, o[dt][qt][2] * inv,
+               o[dt][qt][3] * inv);
     }
     if (g == 0) a.LSE[((long long)b * a.H + h) * a.S + q] = (m[qt] + __log2f(l[qt])) / LOG2E;
   }
@@ -899,15 +913,14 @@ __global__ __launch_bounds__(NTH, 2) void attn_fwd32_kernel(AttnArgs a) {
   l = xh_sum(l);
   if (q < a.S) {
     const float inv = 1.f / l;
-    bf16_t* orow = a.Oout + (long long)b * a.S * a.ld_o + hd * D + (long long)q * a.ld_o;
+    const long long orow = (long long)b * a.S * a.ld_o + hd * D + (long long)q * a.ld_o;
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
         const int d = dt * 32 + 8 * g4 + 4 * h;
-        *reinterpret_cast<uint2*>(orow + d) =
-            make_uint2(pack_bf16x2(o[dt][4 * g4] * inv, o[dt][4 * g4 + 1] * inv),
-                       pack_bf16x2(o[dt][4 * g4 + 2] * inv, o[dt][4 * g4 + 3] * inv));
+        store_o4(a, orow + d, o[dt][4 * g4] * inv, o[dt][4 * g4 + 1] * inv, o[dt][4 * g4 + 2] * inv,
+                 o[dt][4 * g4 + 3] * inv);
       }
     if (h == 0) a.LSE[((long long)b * a.H + hd) * a.S + q] = (m + __log2f(l)) / LOG2E;
   }
@@ -1158,6 +1171,8 @@ struct ObstAttnDesc {
   float scale;
   int causal;
   long long ld_o;   // 0: same as ld
+  const void* Res;  // forward: optional residual input, Sum = bf16(O) + Res (O's layout)
+  void* Sum;
 };
 
 static bool fill(AttnArgs& a, const ObstAttnDesc* d) {
@@ -1167,6 +1182,8 @@ static bool fill(AttnArgs& a, const ObstAttnDesc* d) {
   a.LSE = d->LSE; a.delta = d->delta;
   a.B = d->B; a.S = d->S; a.H = d->H; a.ld = d->ld; a.scale = d->scale; a.causal = d->causal;
   a.ld_o = d->ld_o ? d->ld_o : d->ld;
+  a.Res = (const bf16_t*)d->Res; a.Sum = (bf16_t*)d->Sum;
+  if ((a.Res == nullptr) != (a.Sum == nullptr)) return false;
   static const int prio = [] { const char* e = getenv("OBST_ATTN_PRIO"); return e ? atoi(e) : 1; }();
   a.prio = prio;
   return d->B > 0 && d->S > 0 && d->H > 0 && d->ld % 8 == 0 && d->ld >= (long long)d->H * d->D &&

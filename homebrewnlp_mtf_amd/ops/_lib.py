@@ -51,7 +51,7 @@ class AttnDesc(ctypes.Structure):
     _fields_ = [("Q", c_p), ("K", c_p), ("V", c_p), ("O", c_p), ("dO", c_p),
                 ("Oout", c_p), ("dQ", c_p), ("dK", c_p), ("dV", c_p), ("LSE", c_p), ("delta", c_p),
                 ("B", c_i), ("S", c_i), ("H", c_i), ("D", c_i), ("ld", c_ll), ("scale", c_f), ("causal", c_i),
-                ("ld_o", c_ll)]
+                ("ld_o", c_ll), ("Res", c_p), ("Sum", c_p)]
 
 
 class NormDesc(ctypes.Structure):

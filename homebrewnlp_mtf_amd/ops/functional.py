@@ -118,6 +118,8 @@ _KCONTIG = __import__("os").environ.get("OBST_TRANSPOSED_OPERANDS", "1") != "0"
 # Decode-step products (M = 32 tokens) gain too: 6.1-12.4 us against 7.1-21.5 us per projection
 # (tools/bench_skinny.py, profiles/r2_skinny_gemm.txt).
 _FWD_WT = __import__("os").environ.get("OBST_FWD_WT", "1") != "0"
+# OBST_ATTN_FUSED_RESIDUAL=0: the attention block's residual add as a separate elementwise pass (A/B)
+_ATTN_RES = __import__("os").environ.get("OBST_ATTN_FUSED_RESIDUAL", "1") == "1"
 
 
 def _wT(w, plan: LinearPlan, act=None, has_r: bool = False):
@@ -348,12 +350,16 @@ class _DotAttention(torch.autograd.Function):
         k, q, v = kqv[:, 0:N], kqv[:, N:2 * N], kqv[:, 2 * N:]
         o = _empty(p_out.canon_o_shape, xc)
         lse = torch.empty(B * H * S, dtype=torch.float32, device=xc.device)
-        raw.attn_fwd(q, k, v, o, lse, B, S, H, D, 3 * N, scale, causal, ld_o=H * D)
-        if residual is not None:
+        if residual is not None and _ATTN_RES:   # the residual add rides in the attention epilogue (o kept: backward)
             out = torch.empty_like(o)
-            raw.elementwise("add", o, out, z=residual.contiguous())
+            raw.attn_fwd(q, k, v, o, lse, B, S, H, D, 3 * N, scale, causal, ld_o=H * D,
+                         residual=residual.contiguous(), out=out)
         else:
+            raw.attn_fwd(q, k, v, o, lse, B, S, H, D, 3 * N, scale, causal, ld_o=H * D)
             out = o
+            if residual is not None:
+                out = torch.empty_like(o)
+                raw.elementwise("add", o, out, z=residual.contiguous())
         ctx.save_for_backward(xc, w_in, w_k, w_q, w_v, z, base, kqv, o, lse)
         ctx.cfg = (p_in, p_out, act, scale, causal, geo, residual is not None)
         ctx.carrier = carrier

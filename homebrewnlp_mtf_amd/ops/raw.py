@@ -276,21 +276,28 @@ def _bshd(t: torch.Tensor, B, S, H, D, ld):
     return torch.as_strided(t, (B, S, H, D), (S * ld, ld, D, 1), t.storage_offset())
 
 
-def attn_fwd(q, k, v, o, lse, B, S, H, D, ld, scale: float, causal: bool, ld_o: int = 0):
-    """ld: token stride of q / k / v (H*D, or 3*H*D for an interleaved k|q|v buffer); ld_o: that of o (0: ld)"""
+def attn_fwd(q, k, v, o, lse, B, S, H, D, ld, scale: float, causal: bool, ld_o: int = 0, residual=None, out=None):
+    """ld: token stride of q / k / v (H*D, or 3*H*D for an interleaved k|q|v buffer); ld_o: that of o (0: ld).
+    residual / out (optional, o's layout): the epilogue also writes out = bf16(o) + residual (the block's residual
+    add, fused: o is still written -- the backward reads it)"""
     if q.device.type == "meta":
         return None
     ld_o = ld_o or ld
+    if (residual is None) != (out is None):
+        raise L.KernelError("attention residual and out come together")
     if on_gpu(q):
         if D not in (32, 64, 96, 128):
             raise L.KernelError(f"attention head dim {D} not supported by the HIP kernel (32/64/96/128)")
-        for nm, t, l in (("q", q, ld), ("k", k, ld), ("v", v, ld), ("o", o, ld_o)):
+        ts = (("q", q, ld), ("k", k, ld), ("v", v, ld), ("o", o, ld_o))
+        if out is not None:
+            ts += (("residual", residual, ld_o), ("out", out, ld_o))
+        for nm, t, l in ts:
             if t.dtype != torch.bfloat16:
                 raise L.KernelError(f"attention {nm} must be bf16")
             _need(t, (B * S - 1) * l + (H - 1) * D + D - 1, nm)
         _need(lse, B * H * S - 1, "lse")
         d = L.AttnDesc(q.data_ptr(), k.data_ptr(), v.data_ptr(), 0, 0, o.data_ptr(), 0, 0, 0, lse.data_ptr(), 0,
-                       B, S, H, D, ld, float(scale), int(causal), ld_o)
+                       B, S, H, D, ld, float(scale), int(causal), ld_o, L.ptr(residual), L.ptr(out))
         L.check(L.lib().obst_attn_fwd(d, L.stream_ptr()), "attn_fwd")
         return
     qv, kv, vv = (_f(_bshd(t, B, S, H, D, ld)) for t in (q, k, v))
@@ -301,6 +308,8 @@ def attn_fwd(q, k, v, o, lse, B, S, H, D, ld, scale: float, causal: bool, ld_o: 
     p = torch.exp(s - m.unsqueeze(-1))
     _bshd(o, B, S, H, D, ld_o).copy_(torch.einsum("bhqk,bkhd->bqhd", p, vv))
     lse.view(B, H, S).copy_(m)
+    if out is not None:
+        _bshd(out, B, S, H, D, ld_o).copy_(_f(_bshd(o, B, S, H, D, ld_o)) + _f(_bshd(residual, B, S, H, D, ld_o)))
 
 
 def attn_bwd(q, k, v, o, do, lse, delta, dq, dk, dv, B, S, H, D, ld, scale: float, causal: bool, ld_o: int = 0):

@@ -189,6 +189,24 @@ def test_attention_fwd_bwd(cuda, D, S, causal):
         _close(g, c, 3e-2, 3e-2, f"attention D={D} S={S} causal={causal} {name}")
 
 
+@pytest.mark.parametrize("D", [64, 128])
+def test_attention_fused_residual(cuda, D):
+    """out = bf16(o) + residual written by the forward epilogue == the unfused o, then the elementwise add"""
+    torch.manual_seed(3)
+    B, S, H = 2, 320, 3
+    ld = H * D
+    q, k, v, r = [(torch.randn(B * S * ld) * 0.8).to(BF).to(cuda) for _ in range(4)]
+    o1, o2, out = [torch.zeros(B * S * ld, dtype=BF, device=cuda) for _ in range(3)]
+    l1, l2 = [torch.zeros(B * H * S, device=cuda) for _ in range(2)]
+    raw.attn_fwd(q, k, v, o1, l1, B, S, H, D, ld, D ** -0.5, True)
+    raw.attn_fwd(q, k, v, o2, l2, B, S, H, D, ld, D ** -0.5, True, residual=r, out=out)
+    ref = torch.empty_like(o1)
+    raw.elementwise("add", o1, ref, z=r)
+    torch.cuda.synchronize()
+    assert torch.equal(o1, o2) and torch.equal(l1, l2)
+    assert torch.equal(out, ref)
+
+
 # ----------------------------------------------------------------------------------------------------------------
 @pytest.mark.parametrize("F_,groups,nrows", [(2048, 1, 96), (128, 16, 96), (64, 1, 96), (1000, 1, 96),
                                            (128, 1, 5000), (256, 8, 4000), (32, 4, 3001)])
