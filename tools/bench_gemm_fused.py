@@ -35,12 +35,15 @@ def main():
         ops = (raw.Operand(A, 0, K), raw.Operand(Bw, 0, K), raw.Operand(C, 0, N))
         f = 2 * M * N * K / 1e12
         row = []
-        for lt in (1, 0):
+        for lt in (2, 1, 0):     # 2: hipBLASLt's own GELU_AUX / DGELU epilogues (tanh-form gelu, as the reference)
             raw.lt_set(bool(lt))
+            if lt == 2:
+                raw.L.lib().obst_blaslt_set(2)
+                raw._LT = 2
             tp = timeit(lambda: raw.gemm(*ops, M, N, K))
             ta = timeit(lambda: raw.gemm(*ops, M, N, K, act="gelu", Zout=Z))
             tb = timeit(lambda: raw.gemm(*ops, M, N, K, act="gelu", act_bwd=True, Zin=Z))
-            row.append(f"{'hipBLASLt' if lt else 'MFMA'}: plain {tp * 1e3:.3f} ms ({f / tp:.0f} TF/s) "
+            row.append(f"{['MFMA', 'hipBLASLt', 'hipBLASLt-epilogue'][lt]}: plain {tp * 1e3:.3f} ms ({f / tp:.0f} TF/s) "
                        f"gelu+Zout {ta * 1e3:.3f} ms gelu-bwd {tb * 1e3:.3f} ms")
         raw.lt_set(True)
         print(f"M {M} N {N} K {K} | " + " | ".join(row), flush=True)

@@ -42,6 +42,11 @@ def main():
     us = timed(lambda: raw.norm_bwd(x, dy, sc, st, dx, dsc, dsh, rows, F, groups, R=r))
     nb = rows * F * 2 * 4
     print(f"norm_bwd (+R, param grads) rows {rows} F {F}: {us:7.1f} us  {nb / us / 1e3:6.0f} GB/s", flush=True)
+    us = timed(lambda: raw.norm_bwd(x, dy, sc, st, dx, None, None, rows, F, groups, R=r))
+    print(f"norm_bwd (+R, no param grads) rows {rows} F {F}: {us:7.1f} us  {nb / us / 1e3:6.0f} GB/s", flush=True)
+    us = timed(lambda: raw.norm_bwd(x, dy, sc, st, dx, None, None, rows, F, groups))
+    nb = rows * F * 2 * 3
+    print(f"norm_bwd (no R, no param grads) rows {rows} F {F}: {us:7.1f} us  {nb / us / 1e3:6.0f} GB/s", flush=True)
 
 
 if __name__ == "__main__":
