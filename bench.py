@@ -31,6 +31,7 @@ from homebrewnlp_mtf_amd.run.trainer import Trainer  # noqa: E402
 from homebrewnlp_mtf_amd.utils.log import log  # noqa: E402
 
 PEAK_BF16_DENSE = 2.5e15  # MI355X dense bf16 MFMA peak (spec, no sparsity)
+TORCH_EAGER_1GPU = 80262.0  # tools/torch_baseline.py --batch 32 on one MI355X (profiles/r2_torch_baseline.md)
 
 
 def main():
@@ -139,6 +140,9 @@ def main():
             "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "bf16", "data": "synthetic (uniform random tokens), random-init weights",
             "mfu": round(mfu, 4), "final_loss": round(float(m["loss"]), 4),
+            # informational: the plain PyTorch-ROCm eager run of the same model on one MI355X (80,262 tokens/s at
+            # batch 32; profiles/r2_torch_baseline.md) -- BASELINE.md publishes no number, so vs_baseline stays null
+            "vs_torch_eager_per_gpu": (round(tps / world / TORCH_EAGER_1GPU, 3) if model == "gpt_neo_1.3b" else None),
             "config": {"model": os.path.basename(args.config).replace(".json", "") +
                                 (f"-depth{args.depth}(debug)" if args.depth else ""),
                        "global_batch": params.train_batch_size, "seq_len": S, "parallelism": f"dp{world}",
