@@ -476,20 +476,29 @@ __global__ __launch_bounds__(NT2, 1) void gemm_ph_kernel(GemmArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 2, wc = wave & 3;
-  int bid = blockIdx.x;
+  // XCD-aware remap over the WHOLE grid (tiles x batches): the hardware deals workgroups to the 8 XCDs round-robin
+  // in linear order, so with few tiles per batch (token mixer: 8 M-tiles x 256 (b, h) batches) a per-row remap
+  // pinned tile index x to XCD x for every batch -- with triangular operands one XCD got all the longest tiles
+  // (8 K-tiles) and another all the shortest (1). Remapped linearly, each XCD owns a contiguous run of whole
+  // batches, i.e. every tile shape in equal measure.
+  int bid, ybat;
   {
-    const int nwg = gridDim.x, xcd = bid & 7, qq = nwg >> 3, r = nwg & 7;
-    const int base = xcd < r ? xcd * (qq + 1) : r * (qq + 1) + (xcd - r) * qq;
-    bid = base + (bid >> 3);
+    const int nx = gridDim.x;
+    const long long nwg = (long long)nx * gridDim.y, lin = (long long)blockIdx.y * nx + blockIdx.x;
+    const long long xcd = lin & 7, qq = nwg >> 3, r = nwg & 7;
+    const long long lg = (xcd < r ? xcd * (qq + 1) : r * (qq + 1) + (xcd - r) * qq) + (lin >> 3);
+    bid = (int)(lg % nx);
+    ybat = (int)(lg / nx);
   }
   const int GROUP = 4;
   const int per_group = GROUP * p.tiles_n;
   const int first_m = (bid / per_group) * GROUP;
   const int gsz = min(p.tiles_m - first_m, GROUP);
-  const int tm = first_m + (bid % per_group) % gsz;
+  int tm = first_m + (bid % per_group) % gsz;
   const int tn = (bid % per_group) / gsz;
+  if (p.tri == 1) tm = p.tiles_m - 1 - tm;   // lower-triangular A: the longest K spans (largest m) dispatch first
   const int m0 = tm * BM2, n0 = tn * BN2;
-  const int split = blockIdx.y % p.ksplit, bidx = blockIdx.y / p.ksplit;
+  const int split = ybat % p.ksplit, bidx = ybat / p.ksplit;
   const int b1 = bidx / p.nb2, b2 = bidx % p.nb2;
   int kspan = p.K / p.ksplit, kbeg = split * kspan;
   if (p.tri == 1) kspan = min(p.K, (m0 + BM2 + BK - 1) / BK * BK);             // A[m][k] = 0 for k > m
