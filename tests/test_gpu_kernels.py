@@ -328,6 +328,43 @@ def test_gemm_big_tile(cuda, a_t, b_t, K):
     _close(Cf.view(M, N), ref + 1, 2e-2, 2e-2, f"gemm256 f32 {a_t}{b_t} K{K}")
 
 
+@pytest.mark.parametrize("out_f32", [False, True])
+@pytest.mark.parametrize("a_t,b_t", [(0, 0), (0, 1), (1, 0), (1, 1)])
+def test_gemm_persistent(cuda, a_t, b_t, out_f32):
+    """(hipBLASLt off) the persistent phase kernel (whole 256x256 tiles, >= 512 of them): 6 tiles per batch x 90 batches = 540 tiles
+    (uneven per XCD, a partial last round per CU), 5 K-tiles; then tri = 3 (lower-triangle outputs) on square
+    tiles. Repeats are bitwise identical."""
+    torch.manual_seed(7 + a_t + 2 * b_t + 4 * out_f32)
+    old = raw.lt_set(False)
+    try:
+        _persistent_cases(cuda, a_t, b_t, out_f32)
+    finally:
+        raw.lt_set(old)
+
+
+def _persistent_cases(cuda, a_t, b_t, out_f32):
+    for M, N, K, nb, tri in ((768, 512, 320, 90, 0), (512, 512, 320, 140, 3)):
+        A = (torch.randn(nb * M * K) * 0.5).to(BF)
+        B = (torch.randn(nb * N * K) * 0.5).to(BF)
+        lda = K if a_t == 0 else M
+        ldb = K if b_t == 0 else N
+        av = A.view(nb, M, K) if a_t == 0 else A.view(nb, K, M).transpose(1, 2)
+        bv = B.view(nb, N, K).transpose(1, 2) if b_t == 0 else B.view(nb, K, N)
+        ref = av.float() @ bv.float()
+        if tri == 3:
+            ref = ref * torch.ones(M, N).tril()
+        Ad, Bd = A.to(cuda), B.to(cuda)
+        outs = []
+        for _ in range(2):
+            C = torch.zeros(nb * M * N, dtype=torch.float32 if out_f32 else BF, device=cuda)
+            raw.gemm(raw.Operand(Ad, a_t, lda, M * K), raw.Operand(Bd, b_t, ldb, N * K), raw.Operand(C, 0, N, M * N),
+                     M, N, K, batch=(nb, 1), tri=tri)
+            outs.append(C)
+        torch.cuda.synchronize()
+        _close(outs[0].view(nb, M, N), ref, 4e-2, 2e-2, f"persistent gemm {a_t}{b_t} f32={out_f32} tri={tri}")
+        assert torch.equal(outs[0], outs[1]), "run-to-run difference"
+
+
 @pytest.mark.parametrize("a_t,b_t", [(0, 0), (1, 1)])
 def test_gemm_splitk_wgrad(cuda, a_t, b_t):
     """few output tiles + long K + fp32 accumulate: the phase kernel splits K into a workspace and reduces"""
