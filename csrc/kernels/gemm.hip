@@ -17,34 +17,11 @@
 // grouped 8 tiles along M so blocks that share an XCD share A panels in its L2.
 #include "common.h"
 #include "gemm_desc.h"
+#include "gemm_kern.h"
 #include <stdlib.h>
 
 namespace {
 
-constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
-constexpr int TILE_BYTES = 128 * 64 * 2;  // one operand tile, either image
-
-struct GemmArgs {
-  const bf16_t* A; const bf16_t* B; void* C;
-  const void* R;          // residual added before the activation (same dtype/layout as C) or null
-  bf16_t* Zout;           // pre-activation output (bf16, layout of C) or null
-  const bf16_t* Zin;      // saved pre-activation for the activation-backward epilogue (layout of C)
-  long long lda, ldb, ldc;
-  long long a_s1, a_s2, b_s1, b_s2, c_s1, c_s2;
-  int M, N, K, nb2;
-  int tiles_m, tiles_n;
-  float alpha, beta;      // beta: fp32 output only, C = alpha*acc + beta*C_old (gradient accumulation)
-  int act, mode;          // mode 0: out = act(alpha*acc + R); mode 1: out = (alpha*acc + R) * act'(Zin)
-  int tri;                // 0 dense; 1 A lower-triangular (A[m][k] = 0 for k > m); 2 A upper-triangular (k < m);
-                          // 3 only C[m][n] with n <= m is produced (strictly-upper outputs get no contribution)
-  int ksplit;             // phase kernel only: K split over blockIdx.y; partial tiles go to `ws` [split][M][N]
-  float* ws;              // split-K workspace (fp32), summed into C by splitk_reduce_kernel
-  int kin;                // phase kernel only: split contraction index, see ObstGemmDesc (0: plain K)
-  long long a_sk, b_sk;
-  int nbatch;             // persistent phase kernel: batches (the grid is one block per CU)
-};
-
-__device__ __forceinline__ int kswz(int k) { return ((k & 3) << 1) | (((k >> 3) & 1) << 3); }
 
 // --- staging: global -> registers -------------------------------------------------------------------------------
 template <int T>
@@ -83,28 +60,6 @@ __device__ __forceinline__ void store_tile(char* lds, const uint4 (&reg)[4], int
       off = k * 256 + ((c ^ kswz(k)) << 4);
     }
     *reinterpret_cast<uint4*>(lds + off) = reg[i];
-  }
-}
-
-// --- LDS -> MFMA fragment (8 consecutive k of one row/col) -------------------------------------------------------
-template <int T>
-__device__ __forceinline__ bf16x8_t read_frag(const char* lds, int rbase, int kk, int lane) {
-  if (T == 0) {
-    const int r = rbase + (lane & 15);
-    const int c = kk * 4 + (lane >> 4);
-    return *reinterpret_cast<const bf16x8_t*>(lds + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
-  } else {
-    const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, pp = i16 & 3;
-    const int col = rbase + 4 * pp;
-    const int c = col >> 3;
-    const int k0 = kk * 32 + 8 * g + q;
-    const int k1 = k0 + 4;
-    const int off0 = k0 * 256 + ((c ^ kswz(k0)) << 4) + ((pp & 1) << 3);
-    const int off1 = k1 * 256 + ((c ^ kswz(k1)) << 4) + ((pp & 1) << 3);
-    s16x4_t v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4_t, lds + off0));
-    s16x4_t v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4_t, lds + off1));
-    s16x8_t v = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-    return __builtin_bit_cast(bf16x8_t, v);
   }
 }
 
@@ -254,60 +209,10 @@ hipError_t launch(const GemmArgs& a, int batch, hipStream_t stream) {
 
 
 // ================================================================================================================
-// 256x256x64 tile, 8 waves (2 M x 4 N, 128x64 per wave), staged by direct global->LDS DMA
+// 256x256x64 tiles, 8 waves (2 M x 4 N, 128x64 per wave), staged by direct global->LDS DMA
 // (global_load_lds_dwordx4: each wave-instruction writes 1 KiB of LDS lane-linearly). The XOR swizzle of the LDS
 // image is applied to the per-lane SOURCE address (cdna guide §5.4 rule 21), the ds_read side applies the same
-// XOR. Two LDS stages (2 x 64 KiB), one barrier per K-step; 1 block per CU. Requires K % 64 == 0; rows/columns
-// beyond M/N are clamped to valid memory (their results are never stored).
-constexpr int BM2 = 256, BN2 = 256, NT2 = 512;
-constexpr int IMG2 = 256 * 64 * 2;  // 32 KiB per operand image
-
-__device__ __forceinline__ void glds16(const bf16_t* src, char* lds_base) {
-  __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
-                                   (void __attribute__((address_space(3)))*)lds_base, 16, 0, 0);
-}
-
-template <int T>
-__device__ __forceinline__ void stage256(char* img, const bf16_t* X, long long ld, int r0, int R, int k0, int wave,
-                                         int lane) {
-#pragma unroll
-  for (int rd = 0; rd < 4; ++rd) {
-    const int j = wave * 4 + rd;           // 1 KiB piece of the 32 KiB image
-    const bf16_t* src;
-    if (T == 0) {                          // [256 rows][64 k], 128-B rows, 8 rows per piece
-      const int rr = j * 8 + (lane >> 3), p = lane & 7;
-      const int c = p ^ ((rr >> 1) & 7);
-      const int row = min(r0 + rr, R - 1);
-      src = X + (long long)row * ld + k0 + c * 8;
-    } else {                               // [64 k][256 rows], 512-B rows, 2 k-rows per piece
-      const int kr = j * 2 + (lane >> 5), p = lane & 31;
-      const int c = p ^ kswz(kr);
-      const int col = min(r0 + c * 8, R - 8);
-      src = X + (long long)(k0 + kr) * ld + col;
-    }
-    glds16(src, img + j * 1024);
-  }
-}
-
-template <int T>
-__device__ __forceinline__ bf16x8_t read_frag256(const char* lds, int rbase, int kk, int lane) {
-  if (T == 0) {
-    const int r = rbase + (lane & 15);
-    const int c = kk * 4 + (lane >> 4);
-    return *reinterpret_cast<const bf16x8_t*>(lds + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
-  } else {
-    const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, pp = i16 & 3;
-    const int c = (rbase + 4 * pp) >> 3;
-    const int k0 = kk * 32 + 8 * g + q;
-    const int k1 = k0 + 4;
-    const int off0 = k0 * 512 + ((c ^ kswz(k0)) << 4) + ((pp & 1) << 3);
-    const int off1 = k1 * 512 + ((c ^ kswz(k1)) << 4) + ((pp & 1) << 3);
-    s16x4_t v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4_t, lds + off0));
-    s16x4_t v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4_t, lds + off1));
-    s16x8_t v = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-    return __builtin_bit_cast(bf16x8_t, v);
-  }
-}
+// XOR. Requires K % 64 == 0; rows/columns beyond M/N are clamped to valid memory (their results are never stored).
 
 template <bool OUT_F32>
 __device__ __forceinline__ void epilogue_store(const GemmArgs& p, long long idx, float (&v)[4]) {
@@ -349,83 +254,6 @@ __device__ __forceinline__ void epilogue_store(const GemmArgs& p, long long idx,
   }
 }
 
-template <int A_T, int B_T, bool OUT_F32>
-__global__ __launch_bounds__(NT2, 1) void gemm256_kernel(GemmArgs p) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 2, wn = wave & 3;
-  int bid = blockIdx.x;
-  {
-    const int nwg = gridDim.x, xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-    const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
-    bid = base + (bid >> 3);
-  }
-  const int GROUP = 4;
-  const int per_group = GROUP * p.tiles_n;
-  const int first_m = (bid / per_group) * GROUP;
-  const int gsz = min(p.tiles_m - first_m, GROUP);
-  const int tm = first_m + (bid % per_group) % gsz;
-  const int tn = (bid % per_group) / gsz;
-  const int m0 = tm * BM2, n0 = tn * BN2;
-  const int b1 = blockIdx.y / p.nb2, b2 = blockIdx.y % p.nb2;
-  const bf16_t* A = p.A + b1 * p.a_s1 + b2 * p.a_s2;
-  const bf16_t* B = p.B + b1 * p.b_s1 + b2 * p.b_s2;
-
-  f32x4_t acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-
-  const int nk = p.K / BK;
-  stage256<A_T>(smem, A, p.lda, m0, p.M, 0, wave, lane);
-  stage256<B_T>(smem + IMG2, B, p.ldb, n0, p.N, 0, wave, lane);
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int s = kt & 1;
-    if (kt + 1 < nk) {
-      char* nxt = smem + (s ^ 1) * 2 * IMG2;
-      stage256<A_T>(nxt, A, p.lda, m0, p.M, (kt + 1) * BK, wave, lane);
-      stage256<B_T>(nxt + IMG2, B, p.ldb, n0, p.N, (kt + 1) * BK, wave, lane);
-    }
-    const char* ca = smem + s * 2 * IMG2;
-    const char* cb = ca + IMG2;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      bf16x8_t bfr[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) bfr[j] = read_frag256<B_T>(cb, wn * 64 + j * 16, kk, lane);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const bf16x8_t af = read_frag256<A_T>(ca, wm * 128 + i * 16, kk, lane);
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af, acc[i][j], 0, 0, 0);
-      }
-    }
-    __syncthreads();
-  }
-  const long long coff = b1 * p.c_s1 + b2 * p.c_s2;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int m = m0 + wm * 128 + i * 16 + (lane & 15);
-    if (m >= p.M) continue;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
-      if (n >= p.N) continue;
-      float v[4];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) v[t] = p.alpha * acc[i][j][t];
-      if (p.tri == 3) {
-#pragma unroll
-        for (int t = 0; t < 4; ++t) if (n + t > m) v[t] = 0.f;
-      }
-      epilogue_store<OUT_F32>(p, coff + (long long)m * p.ldc + n, v);
-    }
-  }
-}
-
 // ---------------------------------------------------------------------------------------------------------------
 // Phase-pipelined 256x256 kernel (cdna_hip_programming.md §5 "256² 8-phase template", re-derived here).
 // 8 waves = 2 (M) x 4 (N) groups; C is cut into quadrants (qm, qn) of 128 x 128, and wave (wr, wc) owns the
@@ -442,36 +270,6 @@ __global__ __launch_bounds__(NT2, 1) void gemm256_kernel(GemmArgs p) {
 // MFMAs (setprio 1), barrier. Derived hazard rules (intervals between barriers, stagger included):
 //   RAW: a piece read in phase Q was waited for in phase <= Q-1 by every thread (vmcnt counts above);
 //   WAR: a piece's slot is restaged >= 2 phases after its last read phase (A0: +2, B0: +3, B1: +3, A1: +3).
-constexpr int PIECE = 16384;
-
-__device__ __forceinline__ void bar() {
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
-
-template <int T, bool IS_A>
-__device__ __forceinline__ void stage_piece(char* img, const bf16_t* X, long long ld, int base0, int R, long long k0,
-                                            int q, int wave, int lane) {
-#pragma unroll
-  for (int rd = 0; rd < 2; ++rd) {
-    const int jj = rd * 8 + wave;            // 1 KiB sub-piece
-    const bf16_t* src;
-    if (T == 0) {                            // [128 rows][64 k], 128-B rows
-      const int lr = jj * 8 + (lane >> 3), pc = lane & 7;
-      const int c = pc ^ ((lr >> 1) & 7);
-      const int row = min(base0 + q * 128 + lr, R - 1);
-      src = X + (long long)row * ld + k0 + c * 8;
-    } else {                                 // [64 k][128 cols], 256-B rows
-      const int kr = jj * 4 + (lane >> 4), pc = lane & 15;
-      const int lc = (pc ^ kswz(kr)) * 8;
-      const int col = min(base0 + q * 128 + lc, R - 8);
-      src = X + (long long)(k0 + kr) * ld + col;
-    }
-    glds16(src, img + jj * 1024);
-  }
-}
-
 template <int A_T, int B_T, bool OUT_F32>
 __global__ __launch_bounds__(NT2, 1) void gemm_ph_kernel(GemmArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -621,194 +419,6 @@ __global__ __launch_bounds__(NT2, 1) void gemm_ph_kernel(GemmArgs p) {
   }
 }
 
-// ---------------------------------------------------------------------------------------------------------------
-// Persistent phase kernel: the same 256x256 8-wave phase pipeline, but one block per CU walks a run of tiles, and a
-// tile's epilogue stores overlap the NEXT tile's prologue loads (issued first) instead of leaving the CU idle
-// through the HBM latency of every new tile -- on the token mixer's short triangular tiles (4-32 K-tiles of 64) a
-// dense-to-triangular time ratio of 0.76 for 0.56 of the work put that fixed cost at several K-tiles per tile.
-// Plain epilogue (alpha, tri 3 mask) on whole tiles only (M % 256 == N % 256 == 0), so every thread issues exactly 32
-// stores per tile and the counted vmcnt waits of the next tile's first K-tile can step over them (vmcnt counts
-// loads and stores in issue order on gfx9). XCD k owns a contiguous run of tiles (logical tile order as in
-// gemm_ph_kernel: batches x M-groups, lower-triangular tiles longest first), dealt to its 32 CUs in rounds.
-template <int A_T, int B_T, bool OUT_F32>
-__global__ __launch_bounds__(NT2, 1) void gemm_pp_kernel(GemmArgs p) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = wave >> 2, wc = wave & 3;
-  const int ntile = p.tiles_m * p.tiles_n;
-  const long long total = (long long)ntile * p.nbatch;
-  const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3, nslot = gridDim.x >> 3;
-  const long long Q = total >> 3, Rm = total & 7;
-  const long long base = xcd < Rm ? xcd * (Q + 1) : Rm * (Q + 1) + (xcd - Rm) * Q;
-  const long long len = Q + (xcd < Rm ? 1 : 0);
-
-  struct Tile {
-    const bf16_t* A;
-    const bf16_t* B;
-    long long coff;
-    int m0, n0, nk;
-  };
-  auto decode = [&](long long L) {
-    Tile T;
-    const int bid = (int)(L % ntile), ybat = (int)(L / ntile);
-    const int GROUP = 4;
-    const int per_group = GROUP * p.tiles_n;
-    const int first_m = (bid / per_group) * GROUP;
-    const int gsz = min(p.tiles_m - first_m, GROUP);
-    int tm = first_m + (bid % per_group) % gsz;
-    const int tn = (bid % per_group) / gsz;
-    if (p.tri == 1) tm = p.tiles_m - 1 - tm;
-    T.m0 = tm * BM2;
-    T.n0 = tn * BN2;
-    const int b1 = ybat / p.nb2, b2 = ybat % p.nb2;
-    int kspan = p.K, kbeg = 0;
-    if (p.tri == 1) kspan = min(p.K, (T.m0 + BM2 + BK - 1) / BK * BK);
-    if (p.tri == 2) { kbeg = min(T.m0 / BK * BK, p.K - BK); kspan = p.K - kbeg; }
-    T.A = p.A + b1 * p.a_s1 + b2 * p.a_s2 + (A_T == 0 ? (long long)kbeg : (long long)kbeg * p.lda);
-    T.B = p.B + b1 * p.b_s1 + b2 * p.b_s2 + (B_T == 0 ? (long long)kbeg : (long long)kbeg * p.ldb);
-    T.nk = kspan / BK;
-    T.coff = b1 * p.c_s1 + b2 * p.c_s2;
-    return T;
-  };
-  auto slot_p = [&](int t, int pc) -> char* { return smem + ((t & 1) * 4 + pc) * PIECE; };
-  auto stageA = [&](const Tile& T, int t, int q) {
-    stage_piece<A_T, true>(slot_p(t, q), T.A, p.lda, T.m0, p.M, (long long)t * BK, q, wave, lane);
-  };
-  auto stageB = [&](const Tile& T, int t, int q) {
-    stage_piece<B_T, false>(slot_p(t, 2 + q), T.B, p.ldb, T.n0, p.N, (long long)t * BK, q, wave, lane);
-  };
-  auto prologue = [&](const Tile& T) {   // the pieces phases -6..-1 would have staged
-    stageA(T, 0, 0); stageB(T, 0, 0); stageB(T, 0, 1); stageA(T, 0, 1);
-    if (T.nk > 1) { stageA(T, 1, 0); stageB(T, 1, 0); }
-  };
-
-  // round r of this XCD's run covers logical tiles base + r*nslot + [0, nslot); block `slot` takes the one at
-  // offset (slot + r) % nslot, so with few tiles per batch (the token mixer's 8 M-tiles) a CU does not get the same
-  // tile row -- the same K span under triangular operands -- in every round
-  int rnd = 0;
-  long long k = slot;
-  if (k >= len) return;
-  Tile cur = decode(base + k);
-  prologue(cur);
-  bool pend = false;   // the previous tile's 32 epilogue stores are still counted in vmcnt
-  f32x4_t acc[8][4];
-  bf16x8_t af[4][2], bq0[2][2], bq1[2][2];
-  while (true) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    const int nk = cur.nk;
-    if (nk <= 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else if (pend) asm volatile("s_waitcnt vmcnt(40)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    if (wr == 1) bar();
-    bar();
-    for (int t = 0; t < nk; ++t) {
-      const bool tail = t + 2 >= nk;
-      const bool first = t == 0 && pend;
-#pragma unroll
-      for (int ph = 0; ph < 4; ++ph) {
-        const int qm = (ph == 0 || ph == 1) ? 0 : 1;
-        const int qn = (ph == 0 || ph == 3) ? 0 : 1;
-        if (ph == 0) {
-          const char* ib = slot_p(t, 2);
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int kk = 0; kk < 2; ++kk) bq0[j][kk] = read_frag<B_T>(ib, wc * 32 + j * 16, kk, lane);
-        }
-        if (ph == 0 || ph == 2) {
-          const char* ia = slot_p(t, qm);
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int kk = 0; kk < 2; ++kk) af[i][kk] = read_frag<A_T>(ia, wr * 64 + i * 16, kk, lane);
-        }
-        if (ph == 1) {
-          const char* ib = slot_p(t, 3);
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int kk = 0; kk < 2; ++kk) bq1[j][kk] = read_frag<B_T>(ib, wc * 32 + j * 16, kk, lane);
-        }
-        if (ph == 0 && t + 1 < nk) stageB(cur, t + 1, 1);
-        if (ph == 1 && t + 1 < nk) stageA(cur, t + 1, 1);
-        if (ph == 2 && t + 2 < nk) stageA(cur, t + 2, 0);
-        if (ph == 3 && t + 2 < nk) stageB(cur, t + 2, 0);
-        // t = 0 reads only prologue pieces, which are older than the previous tile's stores: step over them
-        if (tail) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        else if (first) asm volatile("s_waitcnt vmcnt(40)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        bar();
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int kk = 0; kk < 2; ++kk) {
-              const bf16x8_t bb = qn == 0 ? bq0[j][kk] : bq1[j][kk];
-              acc[qm * 4 + i][qn * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bb, af[i][kk],
-                                                                                    acc[qm * 4 + i][qn * 2 + j], 0, 0, 0);
-            }
-        __builtin_amdgcn_s_setprio(0);
-        bar();
-      }
-    }
-    if (wr == 0) bar();
-    // every LDS slot is free: the next tile's prologue goes out before this tile's stores
-    const Tile done = cur;
-    ++rnd;
-    k = (long long)rnd * nslot + (slot + rnd) % nslot;
-    const bool more = k < len;
-    if (more) {
-      cur = decode(base + k);
-      prologue(cur);
-    }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int m = done.m0 + (i >> 2) * 128 + wr * 64 + (i & 3) * 16 + (lane & 15);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int n = done.n0 + (j >> 1) * 128 + wc * 32 + (j & 1) * 16 + 4 * (lane >> 4);
-        float v[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = p.alpha * acc[i][j][u];
-        if (p.tri == 3) {
-#pragma unroll
-          for (int u = 0; u < 4; ++u) if (n + u > m) v[u] = 0.f;
-        }
-        const long long idx = done.coff + (long long)m * p.ldc + n;
-        if (OUT_F32)
-          *reinterpret_cast<float4*>(reinterpret_cast<float*>(p.C) + idx) = make_float4(v[0], v[1], v[2], v[3]);
-        else
-          *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.C) + idx) =
-              make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
-      }
-    }
-    if (!more) break;
-    pend = true;
-  }
-}
-
-template <int A_T, int B_T, bool F32>
-hipError_t launch_pp(GemmArgs a, int batch, hipStream_t stream) {
-  a.tiles_m = a.M / BM2;
-  a.tiles_n = a.N / BN2;
-  a.nbatch = batch;
-  const size_t lds = 8 * PIECE;
-  auto k = gemm_pp_kernel<A_T, B_T, F32>;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    attr = true;
-  }
-  hipLaunchKernelGGL(k, dim3(256), dim3(NT2), lds, stream, a);   // one block per CU, 32 per XCD
-  return hipGetLastError();
-}
-
 // C[m][n] = beta * C[m][n] + sum_s ws[s][m][n]   (float4 per lane)
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(float* __restrict__ C, const float* __restrict__ ws,
                                                              long long mn, long long ldc, int N, int ks, float beta) {
@@ -861,29 +471,14 @@ hipError_t launch_ph(GemmArgs a, int batch, hipStream_t stream) {
   return hipGetLastError();
 }
 
-template <int A_T, int B_T, bool F32>
-hipError_t launch256(GemmArgs a, int batch, hipStream_t stream) {
-  a.tiles_m = (a.M + BM2 - 1) / BM2;
-  a.tiles_n = (a.N + BN2 - 1) / BN2;
-  dim3 grid(a.tiles_m * a.tiles_n, batch);
-  const size_t lds = 4 * IMG2;
-  auto k = gemm256_kernel<A_T, B_T, F32>;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    attr = true;
-  }
-  hipLaunchKernelGGL(k, grid, dim3(NT2), lds, stream, a);
-  return hipGetLastError();
-}
-
 }  // namespace
 
-static int getenv_big() {
+static int getenv_big() {   // OBST_GEMM_BIG=0: only the 128x128 kernel (A/B, debugging)
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("OBST_GEMM_BIG");
     v = e ? (e[0] - '0') : 2;
+    if (v == 1) v = 2;       // the former two-stage 256x256 kernel (superseded by the phase kernels, removed)
   }
   return v;
 }
@@ -958,20 +553,13 @@ OBST_API int obst_gemm(const ObstGemmDesc* d, hipStream_t stream) {
   }
   if (big && impl >= 2 && pp_env && a.ksplit == 1 && d->M % 256 == 0 && d->N % 256 == 0 && !d->R && !d->Zout &&
       !d->Zin && d->act == 0 && d->mode == 0 && (!d->out_f32 || d->beta == 0.f) && big_tiles >= 512) {
-#define OBST_GEMMPP_CASE(AT, BT, F)                                                              \
-    if (d->a_t == AT && d->b_t == BT && (d->out_f32 != 0) == F) {                                \
-      e = launch_pp<AT, BT, F>(a, batch, stream);                                                  \
-      return e == hipSuccess ? 0 : (int)e;                                                         \
-    }
-    OBST_GEMMPP_CASE(0, 0, false) OBST_GEMMPP_CASE(0, 1, false) OBST_GEMMPP_CASE(1, 0, false)
-    OBST_GEMMPP_CASE(1, 1, false) OBST_GEMMPP_CASE(0, 0, true) OBST_GEMMPP_CASE(0, 1, true)
-    OBST_GEMMPP_CASE(1, 0, true) OBST_GEMMPP_CASE(1, 1, true)
-#undef OBST_GEMMPP_CASE
+    e = gemm_pp_launch(&a, d->a_t, d->b_t, d->out_f32, batch, stream);
+    return e == hipSuccess ? 0 : (int)e;
   }
   if (big) {
 #define OBST_GEMM256_CASE(AT, BT, F)                                                             \
     if (d->a_t == AT && d->b_t == BT && (d->out_f32 != 0) == F) {                                \
-      e = impl >= 2 ? launch_ph<AT, BT, F>(a, batch, stream) : launch256<AT, BT, F>(a, batch, stream); \
+      e = launch_ph<AT, BT, F>(a, batch, stream);                                              \
       return e == hipSuccess ? 0 : (int)e;                                                         \
     }
     OBST_GEMM256_CASE(0, 0, false) OBST_GEMM256_CASE(0, 1, false) OBST_GEMM256_CASE(1, 0, false)

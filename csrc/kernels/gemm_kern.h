@@ -1,0 +1,102 @@
+// Shared by the MFMA GEMM translation units (gemm.hip: 128x128 and phase kernels and the dispatcher;
+// gemm_pp.hip: the persistent phase kernel, split out so the two heavy template sets compile in parallel).
+#pragma once
+#include "common.h"
+
+namespace gemmk {   // external linkage: gemm.hip hands a filled GemmArgs to gemm_pp.hip
+struct GemmArgs {
+  const bf16_t* A; const bf16_t* B; void* C;
+  const void* R;          // residual added before the activation (same dtype/layout as C) or null
+  bf16_t* Zout;           // pre-activation output (bf16, layout of C) or null
+  const bf16_t* Zin;      // saved pre-activation for the activation-backward epilogue (layout of C)
+  long long lda, ldb, ldc;
+  long long a_s1, a_s2, b_s1, b_s2, c_s1, c_s2;
+  int M, N, K, nb2;
+  int tiles_m, tiles_n;
+  float alpha, beta;      // beta: fp32 output only, C = alpha*acc + beta*C_old (gradient accumulation)
+  int act, mode;          // mode 0: out = act(alpha*acc + R); mode 1: out = (alpha*acc + R) * act'(Zin)
+  int tri;                // 0 dense; 1 A lower-triangular (A[m][k] = 0 for k > m); 2 A upper-triangular (k < m);
+                          // 3 only C[m][n] with n <= m is produced (strictly-upper outputs get no contribution)
+  int ksplit;             // phase kernel only: K split over blockIdx.y; partial tiles go to `ws` [split][M][N]
+  float* ws;              // split-K workspace (fp32), summed into C by splitk_reduce_kernel
+  int kin;                // phase kernel only: split contraction index, see ObstGemmDesc (0: plain K)
+  long long a_sk, b_sk;
+  int nbatch;             // persistent phase kernel: batches (the grid is one block per CU)
+};
+}  // namespace gemmk
+
+namespace {
+
+constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
+constexpr int TILE_BYTES = 128 * 64 * 2;  // one operand tile, either image
+
+using gemmk::GemmArgs;
+
+__device__ __forceinline__ int kswz(int k) { return ((k & 3) << 1) | (((k >> 3) & 1) << 3); }
+
+// --- LDS -> MFMA fragment (8 consecutive k of one row/col) -------------------------------------------------------
+template <int T>
+__device__ __forceinline__ bf16x8_t read_frag(const char* lds, int rbase, int kk, int lane) {
+  if (T == 0) {
+    const int r = rbase + (lane & 15);
+    const int c = kk * 4 + (lane >> 4);
+    return *reinterpret_cast<const bf16x8_t*>(lds + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
+  } else {
+    const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, pp = i16 & 3;
+    const int col = rbase + 4 * pp;
+    const int c = col >> 3;
+    const int k0 = kk * 32 + 8 * g + q;
+    const int k1 = k0 + 4;
+    const int off0 = k0 * 256 + ((c ^ kswz(k0)) << 4) + ((pp & 1) << 3);
+    const int off1 = k1 * 256 + ((c ^ kswz(k1)) << 4) + ((pp & 1) << 3);
+    s16x4_t v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4_t, lds + off0));
+    s16x4_t v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4_t, lds + off1));
+    s16x8_t v = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+    return __builtin_bit_cast(bf16x8_t, v);
+  }
+}
+
+
+constexpr int BM2 = 256, BN2 = 256, NT2 = 512;
+
+__device__ __forceinline__ void glds16(const bf16_t* src, char* lds_base) {
+  __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
+                                   (void __attribute__((address_space(3)))*)lds_base, 16, 0, 0);
+}
+
+
+constexpr int PIECE = 16384;
+
+__device__ __forceinline__ void bar() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int T, bool IS_A>
+__device__ __forceinline__ void stage_piece(char* img, const bf16_t* X, long long ld, int base0, int R, long long k0,
+                                            int q, int wave, int lane) {
+#pragma unroll
+  for (int rd = 0; rd < 2; ++rd) {
+    const int jj = rd * 8 + wave;            // 1 KiB sub-piece
+    const bf16_t* src;
+    if (T == 0) {                            // [128 rows][64 k], 128-B rows
+      const int lr = jj * 8 + (lane >> 3), pc = lane & 7;
+      const int c = pc ^ ((lr >> 1) & 7);
+      const int row = min(base0 + q * 128 + lr, R - 1);
+      src = X + (long long)row * ld + k0 + c * 8;
+    } else {                                 // [64 k][128 cols], 256-B rows
+      const int kr = jj * 4 + (lane >> 4), pc = lane & 15;
+      const int lc = (pc ^ kswz(kr)) * 8;
+      const int col = min(base0 + q * 128 + lc, R - 8);
+      src = X + (long long)(k0 + kr) * ld + col;
+    }
+    glds16(src, img + jj * 1024);
+  }
+}
+
+
+}  // namespace
+
+// the persistent phase kernel (gemm_pp.hip) for a GemmArgs filled by obst_gemm: plain products on whole tiles
+hipError_t gemm_pp_launch(const gemmk::GemmArgs* a, int a_t, int b_t, int out_f32, int batch, hipStream_t stream);
