@@ -136,14 +136,17 @@ class Sampler:
             return self.sample(x, pos, temp, end)
         try:
             rows = torch.arange(B, device=self.device)
-            while True:
+            # every active row advances one position per step, so the loop runs max(end - pos) steps: one host sync
+            # here instead of an any(pos < end) read-back after every token
+            steps = int((end - pos).clamp(min=0).max())
+            for it in range(steps):
                 active = pos < end
                 P, V = logits.shape[2], logits.shape[3]
                 pred = torch.empty(B * P, dtype=torch.int32, device=self.device)
                 R.sample(logits.reshape(B * P, V).contiguous(), temp, pred, self.seeds.next(), x=x, pos=pos, end=end,
                          patch=P)
                 pos = torch.where(active, pos + 1, pos)
-                if not bool((pos < end).any()):
+                if it == steps - 1:
                     break
                 cur = (pos - 1).clamp(max=S - 1)           # the token just written; inactive rows rewrite theirs
                 logits = m.decode(x[rows, cur].unsqueeze(1), cur)
