@@ -326,6 +326,60 @@ __global__ __launch_bounds__(NTH) void sample_kernel(const float* __restrict__ L
   }
 }
 
+// Split variant for decode-sized batches (rows << CUs): NB blocks per row each reduce a contiguous slice of the
+// vocabulary to one (value, index) pair in `ws`; sample_final_kernel picks each row's winner (ties -> smallest
+// index, so the split changes nothing but the parallelism: 32 rows x 50304 logits took 55 us on 32 blocks).
+__global__ __launch_bounds__(NTH) void sample_part_kernel(const float* __restrict__ L, long long rows, int V, int Pt,
+                                                          int NB, const float* __restrict__ temp,
+                                                          unsigned long long seed, float2* __restrict__ ws) {
+  __shared__ float rm[NW];
+  __shared__ int ri[NW];
+  const long long r = blockIdx.x / NB;
+  const int part = blockIdx.x % NB;
+  if (r >= rows) return;
+  const int chunk = (V + NB - 1) / NB;
+  const int v0 = part * chunk, v1 = min(V, v0 + chunk);
+  const float T = temp[r / Pt];
+  float m = -INFINITY;
+  int mi = V;
+  for (int v = v0 + threadIdx.x; v < v1; v += NTH) {
+    float l = L[r * V + v];
+    if (T != 0.f) l -= T * logf(-logf(hash_uniform((unsigned long long)(r * V + v), seed)));
+    if (l > m) { m = l; mi = v; }
+  }
+  wave_argmax(m, mi);
+  if ((threadIdx.x & 63) == 0) { rm[threadIdx.x >> 6] = m; ri[threadIdx.x >> 6] = mi; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < NW; ++w)
+      if (rm[w] > m || (rm[w] == m && ri[w] < mi)) { m = rm[w]; mi = ri[w]; }
+    ws[r * NB + part] = make_float2(m, __int_as_float(mi));
+  }
+}
+
+__global__ __launch_bounds__(NTH) void sample_final_kernel(long long rows, int V, int Pt, int NB,
+                                                           const float2* __restrict__ ws,
+                                                           const long long* __restrict__ pos,
+                                                           const long long* __restrict__ end, int* __restrict__ X,
+                                                           int S, int* __restrict__ pred) {
+  const long long r = (long long)blockIdx.x * NTH + threadIdx.x;
+  if (r >= rows) return;
+  float m = -INFINITY;
+  int mi = V;
+  for (int k = 0; k < NB; ++k) {   // parts in vocabulary order: a tie keeps the earlier (smaller) index
+    const float2 e = ws[r * NB + k];
+    const int ei = __float_as_int(e.y);
+    if (e.x > m || (e.x == m && ei < mi)) { m = e.x; mi = ei; }
+  }
+  if (mi >= V) mi = 0;
+  if (pred) pred[r] = mi;
+  const long long b = r / Pt;
+  if (X && pos[b] < end[b]) {
+    const long long w = pos[b] < S - 1 ? pos[b] : S - 1;
+    X[(b * S + w) * Pt + r % Pt] = mi;
+  }
+}
+
 // ---------------------------------------------------------------------------------------------------------------
 // K24 frame unpack: V [rows][C] (uint8 or int32) -> Y [rows][C * folds] bf16,
 // Y[r][i * C + c] = ((V[r][c] / base^i) % base) / 255   (folds == 1: V / 255)
@@ -666,9 +720,27 @@ OBST_API int obst_sum_axis(const void* X, void* Y, long long outer, int H, long 
   return (int)hipGetLastError();
 }
 
+// blocks per row of the split sampler (1: the single-kernel path): enough blocks to cover the CUs when rows are few
+OBST_API int obst_sample_parts(long long rows, int V) {
+  if (rows <= 0 || rows >= 256 || V < 4 * 1024) return 1;
+  const long long want = (512 + rows - 1) / rows;
+  const long long cap = V / 2048;
+  return (int)(want < cap ? (want < 16 ? want : 16) : (cap < 16 ? cap : 16));
+}
+
+// ws: obst_sample_parts(rows, V) * rows float2 pairs when that is > 1 (else unused)
 OBST_API int obst_sample(const float* L, long long rows, int V, int Pt, const float* temp, const long long* pos,
-                         const long long* end, int* X, int S, int* pred, unsigned long long seed, hipStream_t st) {
+                         const long long* end, int* X, int S, int* pred, unsigned long long seed, void* ws,
+                         hipStream_t st) {
   if (rows <= 0 || V <= 0 || Pt <= 0 || (X && (!pos || !end || S <= 0))) return -1;
+  const int nb = obst_sample_parts(rows, V);
+  if (nb > 1 && ws) {
+    hipLaunchKernelGGL(sample_part_kernel, dim3((unsigned)(rows * nb)), dim3(NTH), 0, st, L, rows, V, Pt, nb, temp,
+                       seed, (float2*)ws);
+    hipLaunchKernelGGL(sample_final_kernel, dim3((unsigned)((rows + NTH - 1) / NTH)), dim3(NTH), 0, st, rows, V, Pt,
+                       nb, (const float2*)ws, pos, end, X, S, pred);
+    return (int)hipGetLastError();
+  }
   const int g = (int)(rows < 16384 ? rows : 16384);
   hipLaunchKernelGGL(sample_kernel, dim3(g), dim3(NTH), 0, st, L, rows, V, Pt, temp, pos, end, X, S, pred, seed);
   return (int)hipGetLastError();

@@ -869,6 +869,19 @@ def gumbel_scores(logits, temp, seed: int):
     return logits.float() - temp.view(rows, 1).float() * noise
 
 
+_SAMPLE_WS: typing.Dict[str, torch.Tensor] = {}
+
+
+def _sample_ws(device, n: int) -> torch.Tensor:
+    """per-device (value, index) partials of the split sampler, grown as needed and reused across steps"""
+    key = str(device)
+    t = _SAMPLE_WS.get(key)
+    if t is None or t.numel() < n:
+        t = torch.empty(n, dtype=torch.float32, device=device)
+        _SAMPLE_WS[key] = t
+    return t
+
+
 def sample(logits, temp, pred, seed: int, x=None, pos=None, end=None, patch: int = 1):
     """pred[r] = argmax_v(logits[r][v] - temp[r // patch] log(-log u)); with x [B][S][patch] (int32) the winner is
     also written to x[b][min(pos_b, S-1)][r % patch] for rows whose pos_b < end_b"""
@@ -885,9 +898,11 @@ def sample(logits, temp, pred, seed: int, x=None, pos=None, end=None, patch: int
                     or end.dtype != torch.int64 or pos.numel() < B or end.numel() < B):
                 raise L.KernelError("sample: int32 token buffer, int64 pos / end")
             S = x.numel() // (B * patch)
+        nb = int(L.lib().obst_sample_parts(rows, V))
+        ws = _sample_ws(logits.device, rows * nb * 2) if nb > 1 else None
         L.check(L.lib().obst_sample(logits.data_ptr(), rows, V, patch, temp.data_ptr(), L.ptr(pos), L.ptr(end),
-                                    L.ptr(x), S, pred.data_ptr(), int(seed) & (2 ** 64 - 1), L.stream_ptr()),
-                "sample")
+                                    L.ptr(x), S, pred.data_ptr(), int(seed) & (2 ** 64 - 1), L.ptr(ws),
+                                    L.stream_ptr()), "sample")
         return pred
     t = temp.reshape(-1)[:B].repeat_interleave(patch)
     scores = gumbel_scores(logits, t, seed)

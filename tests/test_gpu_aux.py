@@ -116,9 +116,11 @@ def test_sum_axis_and_swap(cuda):
     assert torch.equal(X.swap_axes(x2.to(cuda), 1, 2).cpu(), x2.transpose(1, 2).contiguous())
 
 
-def test_sample_kernel_matches_oracle(cuda):
+@pytest.mark.parametrize("V", [1000, 50304])
+def test_sample_kernel_matches_oracle(cuda, V):
+    """V = 50304 with 12 rows takes the split sampler (16 blocks per row + the final reduce)"""
     torch.manual_seed(4)
-    B, P, V, S = 6, 2, 1000, 16
+    B, P, S = 6, 2, 16
     logits = torch.randn(B * P, V) * 3
     temp = torch.tensor([0.0, 0.5, 1.0, 2.0, 1.0, 0.7])
     pos = torch.tensor([3, 5, 16, 0, 15, 9])
