@@ -363,7 +363,7 @@ __global__ __launch_bounds__(NTH) void attn_delta_kernel(AttnArgs a) {
 
 // one 64-key tile of the dQ kernel for a wave's 32 queries (two 32-key halves: P needs only the stored LSE, so no
 // state crosses the halves). dP starts from -delta (the accumulator init), so dS = P * dP.
-template <int D, bool MASK>
+template <int D, bool MASK, int HALVES = 2>
 __device__ __forceinline__ void dq_tile(const char* sK, const char* sV, const bf16x8_t (&qf)[2][Geo<D>::DS],
                                         const bf16x8_t (&df)[2][Geo<D>::DS], const float (&lse2)[2],
                                         const float (&dlt)[2], f32x4_t (&acc)[Geo<D>::DT][2], int k0, int qw, int S,
@@ -371,7 +371,7 @@ __device__ __forceinline__ void dq_tile(const char* sK, const char* sV, const bf
   using G = Geo<D>;
   const int g = lane >> 4, i = lane & 15;
 #pragma unroll
-  for (int st = 0; st < 2; ++st) {
+  for (int st = 0; st < HALVES; ++st) {
     f32x4_t sc[2][2], dp[2][2];
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt)
@@ -430,10 +430,10 @@ __device__ __forceinline__ void dq_tile(const char* sK, const char* sV, const bf
 // dQ: block = NW x 32 queries; recompute Sᵀ, Pᵀ, dPᵀ = V·dOᵀ, dSᵀ, dQᵀ += Kᵀ·dSᵀ. K/V tiles in an NS-deep LDS ring
 // filled by LDS-DMA NS - 1 tiles ahead (NW = 8, NS = 3: one block per CU, every wave's DMA share of a tile is 4
 // pieces, a tile has two tiles' time to land instead of one).
-template <int D, int NW = 4, int NS = 2>
+template <int D, int NW = 4, int NS = 2, int KT = 64>
 __global__ __launch_bounds__(NW * 64, 2) void attn_bwd_dq_kernel(AttnArgs a) {
   using G = Geo<D>;
-  constexpr int TILE = 64 * G::ROWB;
+  constexpr int TILE = KT * G::ROWB;                   // KT keys per K / V tile (64, or 32 in a 4-deep ring)
   constexpr int QB = 32 * NW;                          // queries per block
   constexpr int PPW = 2 * (TILE / 1024) / NW;          // LDS-DMA pieces per wave per stage (K + V)
   static_assert(NS == 2 || (2 * (TILE / 1024)) % NW == 0, "counted waits need an even piece split");
@@ -448,12 +448,12 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_bwd_dq_kernel(AttnArgs a) {
   const long long base = (long long)b * a.S * a.ld + h * D;
   const long long base_o = (long long)b * a.S * a.ld_o + h * D;
   const int kend = a.causal ? min(a.S, qblk + QB) : a.S;
-  const int nkb = (kend + 63) / 64;
+  const int nkb = (kend + KT - 1) / KT;
 #pragma unroll
   for (int st = 0; st < NS - 1; ++st) {
     if (st < nkb) {
-      stage_rows<D, 64, NW>(smem + st * 2 * TILE, a.K + base + (long long)st * 64 * a.ld, a.ld, a.S - st * 64, tid);
-      stage_rows<D, 64, NW>(smem + st * 2 * TILE + TILE, a.V + base + (long long)st * 64 * a.ld, a.ld, a.S - st * 64,
+      stage_rows<D, KT, NW>(smem + st * 2 * TILE, a.K + base + (long long)st * KT * a.ld, a.ld, a.S - st * KT, tid);
+      stage_rows<D, KT, NW>(smem + st * 2 * TILE + TILE, a.V + base + (long long)st * KT * a.ld, a.ld, a.S - st * KT,
                             tid);
     }
   }
@@ -492,23 +492,27 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_bwd_dq_kernel(AttnArgs a) {
   vm_wait<0>();   // staged tiles (asm LDS-DMA: the compiler does not track them) have landed
   __syncthreads();
   for (int kb = 0; kb < nkb; ++kb) {
-    const int k0 = kb * 64;
+    const int k0 = kb * KT;
     const char* sK = smem + (kb % NS) * 2 * TILE;
     const char* sV = sK + TILE;
     const int kn = kb + NS - 1;   // tile issued now; its slot was last read in iteration kb - 1 (behind a barrier)
     if (kn < nkb) {
       char* nxt = smem + (kn % NS) * 2 * TILE;
-      stage_rows<D, 64, NW>(nxt, a.K + base + (long long)kn * 64 * a.ld, a.ld, a.S - kn * 64, tid);
-      stage_rows<D, 64, NW>(nxt + TILE, a.V + base + (long long)kn * 64 * a.ld, a.ld, a.S - kn * 64, tid);
+      stage_rows<D, KT, NW>(nxt, a.K + base + (long long)kn * KT * a.ld, a.ld, a.S - kn * KT, tid);
+      stage_rows<D, KT, NW>(nxt + TILE, a.V + base + (long long)kn * KT * a.ld, a.ld, a.S - kn * KT, tid);
     }
     if (!(a.causal && k0 > qw + 31)) {
-      const bool need_mask = (a.causal && k0 + 63 > qw) || k0 + 64 > a.S;
-      if (need_mask) dq_tile<D, true>(sK, sV, qf, df, lse2, dlt, acc, k0, qw, a.S, a.causal, c2, lane, a.prio & 2);
-      else dq_tile<D, false>(sK, sV, qf, df, lse2, dlt, acc, k0, qw, a.S, a.causal, c2, lane, a.prio & 2);
+      const bool need_mask = (a.causal && k0 + KT - 1 > qw) || k0 + KT > a.S;
+      if (need_mask)
+        dq_tile<D, true, KT / 32>(sK, sV, qf, df, lse2, dlt, acc, k0, qw, a.S, a.causal, c2, lane, a.prio & 2);
+      else
+        dq_tile<D, false, KT / 32>(sK, sV, qf, df, lse2, dlt, acc, k0, qw, a.S, a.causal, c2, lane, a.prio & 2);
     }
-    // tile kb + 1 must have landed; with NS = 3 tile kb + 2 may stay in flight across the barrier (counted wait:
-    // the only vector-memory ops of this loop are the DMA pieces, PPW per wave per tile)
-    if (NS == 3 && kb + 2 < nkb) vm_wait<PPW>();
+    // tile kb + 1 must have landed; tiles kb + 2 .. kb + NS - 2 may stay in flight across the barrier (counted
+    // wait: the only vector-memory ops of this loop are the DMA pieces, PPW per wave per tile)
+    const int ahead = min(NS - 2, nkb - 2 - kb);
+    if (NS >= 4 && ahead >= 2) vm_wait<2 * PPW>();
+    else if (NS >= 3 && ahead >= 1) vm_wait<PPW>();
     else vm_wait<0>();
     __syncthreads();
   }
@@ -530,16 +534,16 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_bwd_dq_kernel(AttnArgs a) {
 // dVᵀ and dKᵀ as B operands straight from the accumulators). dP starts from -delta[q] (read from LDS as one f32x4 per
 // tile). Every Q / dO fragment read from LDS feeds KG MFMAs: with KG = 2 the LDS bytes per MFMA halve (at KG = 1 the
 // 104 LDS reads of a chunk take ~2300 LDS cycles per CU against ~2050 MFMA cycles per SIMD: LDS-bound).
-template <int D, bool MASK, int KG>
+template <int D, bool MASK, int KG, int NQT = 4>
 __device__ __forceinline__ void dkv_chunk(const char* sQ, const char* sD, const float* sL, const float* sDl,
                                           const bf16x8_t (&kf)[KG][Geo<D>::DS], const bf16x8_t (&vf)[KG][Geo<D>::DS],
                                           f32x4_t (&dk)[KG][Geo<D>::DT], f32x4_t (&dv)[KG][Geo<D>::DT], int q0,
                                           int key, int S, int causal, float c2, int lane, int prio) {
   using G = Geo<D>;
   const int g = lane >> 4;
-  f32x4_t sc[KG][4], dp[KG][4];
+  f32x4_t sc[KG][NQT], dp[KG][NQT];
 #pragma unroll
-  for (int qt = 0; qt < 4; ++qt) {
+  for (int qt = 0; qt < NQT; ++qt) {
     const float4 dl = *reinterpret_cast<const float4*>(sDl + qt * 16 + 4 * g);
 #pragma unroll
     for (int j = 0; j < KG; ++j) {
@@ -551,7 +555,7 @@ __device__ __forceinline__ void dkv_chunk(const char* sQ, const char* sD, const 
 #pragma unroll
   for (int ds = 0; ds < G::DS; ++ds) {
 #pragma unroll
-    for (int qt = 0; qt < 4; ++qt) {
+    for (int qt = 0; qt < NQT; ++qt) {
       bf16x8_t qa = row_frag<D>(sQ, qt * 16, ds, lane);
       bf16x8_t da = row_frag<D>(sD, qt * 16, ds, lane);
 #pragma unroll
@@ -564,7 +568,7 @@ __device__ __forceinline__ void dkv_chunk(const char* sQ, const char* sD, const 
   if (prio) __builtin_amdgcn_s_setprio(0);
   // sc[j][qt][v] = S[q = q0 + qt*16 + 4g + v][key + 16 j]
 #pragma unroll
-  for (int qt = 0; qt < 4; ++qt) {
+  for (int qt = 0; qt < NQT; ++qt) {
     const float4 lv = *reinterpret_cast<const float4*>(sL + qt * 16 + 4 * g);
     const float nl[4] = {-lv.x * LOG2E, -lv.y * LOG2E, -lv.z * LOG2E, -lv.w * LOG2E};
 #pragma unroll
@@ -582,7 +586,7 @@ __device__ __forceinline__ void dkv_chunk(const char* sQ, const char* sD, const 
   }
   if (prio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-  for (int st = 0; st < 2; ++st) {
+  for (int st = 0; st < NQT / 2; ++st) {
     bf16x8_t pb[KG], sb[KG];
 #pragma unroll
     for (int j = 0; j < KG; ++j) {
@@ -606,10 +610,9 @@ __device__ __forceinline__ void dkv_chunk(const char* sQ, const char* sD, const 
 // ----------------------------------------------------------------------------------------------------------------
 // dK/dV: block = NW x KG x 16 keys; wave w owns keys k0 + 16 KG w + [0, 16 KG). Loop over 64-query chunks (Q, dO, lse,
 // delta) in an NS-deep LDS ring filled by LDS-DMA NS - 1 chunks ahead. KG = 2 holds ~300 registers: one wave per SIMD.
-template <int D, int NW = 4, int NS = 2, int KG = 1>
+template <int D, int NW = 4, int NS = 2, int KG = 1, int QC = 64>
 __global__ __launch_bounds__(NW * 64, KG == 1 ? 2 : 1) void attn_bwd_dkv_kernel(AttnArgs a) {
   using G = Geo<D>;
-  constexpr int QC = 64;
   constexpr int TILE = QC * G::ROWB;
   constexpr int STAGE = 2 * TILE + 2 * 256;   // Q, dO, lse[64], delta[64]
   constexpr int KW = 16 * KG;                 // keys per wave
@@ -675,14 +678,20 @@ __global__ __launch_bounds__(NW * 64, KG == 1 ? 2 : 1) void attn_bwd_dkv_kernel(
     if (!(a.causal && q0 + QC - 1 < kw)) {  // every query of this chunk precedes this wave's keys
       const bool need_mask = (a.causal && q0 < kw + KW - 1) || q0 + QC > a.S || kw + KW > a.S;
       if (need_mask)
-        dkv_chunk<D, true, KG>(sQ, sD, sL, sDl, kf, vf, dk, dv, q0, key, a.S, a.causal, c2, lane, a.prio & 1);
+        dkv_chunk<D, true, KG, QC / 16>(sQ, sD, sL, sDl, kf, vf, dk, dv, q0, key, a.S, a.causal, c2, lane, a.prio & 1);
       else
-        dkv_chunk<D, false, KG>(sQ, sD, sL, sDl, kf, vf, dk, dv, q0, key, a.S, a.causal, c2, lane, a.prio & 1);
+        dkv_chunk<D, false, KG, QC / 16>(sQ, sD, sL, sDl, kf, vf, dk, dv, q0, key, a.S, a.causal, c2, lane, a.prio & 1);
     }
-    // chunk c + 1 must have landed; with NS = 3 chunk c + 2 may stay in flight across the barrier
-    if (NS == 3 && c + 2 < nqc) {   // lse / delta pieces: NW = 4 wave 0 issues both, NW = 8 waves 0 and 1 one each
-      if (NW == 4 && w == 0) vm_wait<PPW + 2>();
-      else if (NW != 4 && w < 2) vm_wait<PPW + 1>();
+    // chunk c + 1 must have landed; chunks c + 2 .. c + NS - 2 may stay in flight across the barrier. Per chunk a
+    // wave issues PPW pieces, plus the lse / delta pieces: NW = 4 wave 0 issues both, NW = 8 waves 0 and 1 one each
+    const int ahead = min(NS - 2, nqc - 2 - c);
+    constexpr int X0 = NW == 4 ? 2 : 1;
+    const bool extra = NW == 4 ? w == 0 : w < 2;
+    if (NS >= 4 && ahead >= 2) {
+      if (extra) vm_wait<2 * (PPW + X0)>();
+      else vm_wait<2 * PPW>();
+    } else if (NS >= 3 && ahead >= 1) {
+      if (extra) vm_wait<PPW + X0>();
       else vm_wait<PPW>();
     } else {
       vm_wait<0>();
@@ -1112,6 +1121,20 @@ static int attn_dkv_kg() {
   return v;
 }
 
+static int attn_dq_ring() {   // OBST_ATTN_DQ_RING=4: dQ kernel over 32-key tiles, 4-deep LDS-DMA ring
+  static int v = [] { const char* e = getenv("OBST_ATTN_DQ_RING"); return e ? atoi(e) : 4; }();
+  return v;
+}
+
+// OBST_ATTN_DKV_RING=4: dK/dV kernel over 32-query chunks in a 4-deep LDS-DMA ring. A/B only: B64 S2048 H16 D128
+// causal backward 4.98 -> 5.59 ms (the dK/dV loop is bound by its LDS reads, not by the DMA latency the deeper ring
+// hides; half-size chunks double its barriers and lse/delta reads). The dQ kernel's ring of 32-key tiles (default
+// since r2) took the backward 5.21 -> 4.99 ms.
+static int attn_dkv_ring() {
+  static int v = [] { const char* e = getenv("OBST_ATTN_DKV_RING"); return e ? atoi(e) : 2; }();
+  return v;
+}
+
 static int attn_bwd_impl() {
   static int v = [] { const char* e = getenv("OBST_ATTN_BWD"); return e ? atoi(e) : 1; }();
   return v;
@@ -1147,10 +1170,18 @@ int launch_bwd(const AttnArgs& a, hipStream_t st) {
                          2 * (2 * 64 * Geo<D>::ROWB + 512), st, a);
     return (int)hipGetLastError();
   }
-  hipLaunchKernelGGL(attn_bwd_dq_kernel<D>, dim3((a.S + 127) / 128 * a.B * a.H), dim3(NTH), 4 * 64 * Geo<D>::ROWB, st, a);
+  if (attn_dq_ring() == 4)   // 32-key K/V tiles in a 4-deep ring (same 64 KiB of LDS)
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<D, 4, 4, 32>), dim3((a.S + 127) / 128 * a.B * a.H), dim3(NTH),
+                       4 * 2 * 32 * Geo<D>::ROWB, st, a);
+  else
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<D>, dim3((a.S + 127) / 128 * a.B * a.H), dim3(NTH), 4 * 64 * Geo<D>::ROWB,
+                       st, a);
   if (D == 128 && attn_bwd_impl() == 2 && a.ld == a.ld_o)   // its Q / dO staging shares one row-offset table
     hipLaunchKernelGGL(attn_bwd_dkv32_kernel, dim3((a.S + 127) / 128 * a.B * a.H), dim3(NTH), 2 * (2 * 64 * 256 + 512),
                        st, a);
+  else if (attn_dkv_ring() == 4)   // 32-query chunks in a 4-deep ring (the same 66 KiB of LDS)
+    hipLaunchKernelGGL((attn_bwd_dkv_kernel<D, 4, 4, 1, 32>), dim3((a.S + 63) / 64 * a.B * a.H), dim3(NTH),
+                       4 * (2 * 32 * Geo<D>::ROWB + 512), st, a);
   else if (attn_dkv_kg() == 2)
     hipLaunchKernelGGL((attn_bwd_dkv_kernel<D, 4, 2, 2>), dim3((a.S + 127) / 128 * a.B * a.H), dim3(NTH),
                        2 * (2 * 64 * Geo<D>::ROWB + 512), st, a);
