@@ -770,16 +770,16 @@ __device__ __forceinline__ bf16x8_t tr_pair(const char* lds, int o0, int o1) {
 }
 
 // one 64-key tile for a wave's 32 queries (query n = lane&31 is `q`); l is this lane's partial row sum
-template <bool MASK>
+template <bool MASK, int NKT = 2>
 __device__ __forceinline__ void fwd32_tile(const char* sK, const char* sV, const bf16x8_t (&qf)[8],
                                            f32x16_t (&o)[4], float& m, float& l, int k0, int q, int S, int causal,
                                            float c2, int lane) {
   const int h = lane >> 5;
   Frag32 fo;
   frag32_offsets(fo, lane);
-  f32x16_t s[2];
+  f32x16_t s[NKT];
 #pragma unroll
-  for (int kt = 0; kt < 2; ++kt) {
+  for (int kt = 0; kt < NKT; ++kt) {
     s[kt] = f32x16_t{};
 #pragma unroll
     for (int ks = 0; ks < 8; ++ks) {
@@ -789,7 +789,7 @@ __device__ __forceinline__ void fwd32_tile(const char* sK, const char* sV, const
   }
   float mx = -INFINITY;
 #pragma unroll
-  for (int kt = 0; kt < 2; ++kt)
+  for (int kt = 0; kt < NKT; ++kt)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       if (MASK) {
@@ -812,7 +812,7 @@ __device__ __forceinline__ void fwd32_tile(const char* sK, const char* sV, const
   const float nm = -m;
   float rs = 0.f;
 #pragma unroll
-  for (int kt = 0; kt < 2; ++kt)
+  for (int kt = 0; kt < NKT; ++kt)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const float p = fexp2(__builtin_fmaf(s[kt][r], c2, nm));
@@ -821,7 +821,7 @@ __device__ __forceinline__ void fwd32_tile(const char* sK, const char* sV, const
     }
   l += rs;
 #pragma unroll
-  for (int kt = 0; kt < 2; ++kt)
+  for (int kt = 0; kt < NKT; ++kt)
 #pragma unroll
     for (int st = 0; st < 2; ++st) {
       const bf16x8_t pf = pack8(s[kt], 8 * st);
@@ -835,18 +835,20 @@ __device__ __forceinline__ void fwd32_tile(const char* sK, const char* sV, const
 
 // LDS-DMA of a full 64-row tile: wave-uniform global base + 32-bit per-lane byte offsets computed once (soff), so
 // the loads take the saddr + voffset form and the LDS base (M0) is scalar
-__device__ __forceinline__ void stage_full64(char* lds, const bf16_t* g, const unsigned (&soff)[4], int w) {
+template <int NP>   // NP pieces per wave: 4 for a 64-row tile, 2 for 32 rows
+__device__ __forceinline__ void stage_full64(char* lds, const bf16_t* g, const unsigned (&soff)[NP], int w) {
   const char* gb = reinterpret_cast<const char*>(g);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) glds16_asm(gb + soff[i], lds + (w + 4 * i) * 1024);
+  for (int i = 0; i < NP; ++i) glds16_asm(gb + soff[i], lds + (w + 4 * i) * 1024);
 }
 
 // stage_rows with the asm DMA (ragged last tile: rows >= nvalid clamped to the last valid row)
+template <int NP>
 __device__ __forceinline__ void stage_rows64_asm(char* lds, const bf16_t* g, long long ld, int nvalid, int w,
                                                  int lane) {
   const int last = nvalid - 1;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < NP; ++i) {
     const int j = w + 4 * i;
     const int row = j * 4 + (lane >> 4);
     const int c = (lane & 15) ^ swz<128>(row);
@@ -857,9 +859,13 @@ __device__ __forceinline__ void stage_rows64_asm(char* lds, const bf16_t* g, lon
 
 // block = 128 queries of one (b, h), wave w owns 32; K/V 64-key tiles double-buffered by LDS-DMA, one barrier/tile;
 // the tile loop is unrolled by two so both buffers' fragment addresses are immediates
+// KT = 32: 32-key tiles in a 4-deep ring (the same 64 KiB), the next three tiles in flight instead of one
+template <int KT = 64>
 __global__ __launch_bounds__(NTH, 2) void attn_fwd32_kernel(AttnArgs a) {
   constexpr int D = 128;
-  constexpr int TILE = 64 * 256;
+  constexpr int TILE = KT * 256;
+  constexpr int NS = KT == 64 ? 2 : 4;
+  constexpr int NP = KT / 16;         // LDS-DMA pieces per wave per K (or V) tile
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, n = lane & 31;
   const int nx = (a.S + 127) / 128;
@@ -873,25 +879,27 @@ __global__ __launch_bounds__(NTH, 2) void attn_fwd32_kernel(AttnArgs a) {
   const bf16_t* Kb = a.K + base;
   const bf16_t* Vb = a.V + base;
   const int kend = a.causal ? min(a.S, qblk + 128) : a.S;
-  const int nkb = (kend + 63) / 64;
+  const int nkb = (kend + KT - 1) / KT;
   const int wu = __builtin_amdgcn_readfirstlane(w);
-  unsigned soff[4];
+  unsigned soff[NP];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < NP; ++i) {
     const int row = (wu + 4 * i) * 4 + (lane >> 4);
     soff[i] = (unsigned)(row * (int)a.ld + (((lane & 15) ^ swz<128>(row)) << 3)) * 2u;
   }
   auto stage = [&](char* buf, int k0) {
     k0 = __builtin_amdgcn_readfirstlane(k0);
-    if (k0 + 64 <= a.S) {
-      stage_full64(buf, Kb + (long long)k0 * a.ld, soff, wu);
-      stage_full64(buf + TILE, Vb + (long long)k0 * a.ld, soff, wu);
+    if (k0 + KT <= a.S) {
+      stage_full64<NP>(buf, Kb + (long long)k0 * a.ld, soff, wu);
+      stage_full64<NP>(buf + TILE, Vb + (long long)k0 * a.ld, soff, wu);
     } else {
-      stage_rows64_asm(buf, Kb + (long long)k0 * a.ld, a.ld, a.S - k0, wu, lane);
-      stage_rows64_asm(buf + TILE, Vb + (long long)k0 * a.ld, a.ld, a.S - k0, wu, lane);
+      stage_rows64_asm<NP>(buf, Kb + (long long)k0 * a.ld, a.ld, a.S - k0, wu, lane);
+      stage_rows64_asm<NP>(buf + TILE, Vb + (long long)k0 * a.ld, a.ld, a.S - k0, wu, lane);
     }
   };
-  stage(smem, 0);
+#pragma unroll
+  for (int t = 0; t < NS - 1; ++t)
+    if (t < nkb) stage(smem + t * 2 * TILE, t * KT);
   bf16x8_t qf[8];
 #pragma unroll
   for (int ks = 0; ks < 8; ++ks) qf[ks] = load_frag_g(a.Q + base + (long long)q * a.ld + ks * 16 + 8 * h, q < a.S);
@@ -907,16 +915,21 @@ __global__ __launch_bounds__(NTH, 2) void attn_fwd32_kernel(AttnArgs a) {
   vm_wait<0>();
   __syncthreads();
   for (int kb = 0; kb < nkb; ++kb) {
-    const int k0 = kb * 64;
-    const char* sK = smem + (kb & 1) * 2 * TILE;
+    const int k0 = kb * KT;
+    const char* sK = smem + (kb % NS) * 2 * TILE;
     const char* sV = sK + TILE;
-    if (kb + 1 < nkb) stage(smem + ((kb + 1) & 1) * 2 * TILE, k0 + 64);
+    const int kn = kb + NS - 1;   // its slot was last read in iteration kb - 1 (behind the barrier)
+    if (kn < nkb) stage(smem + (kn % NS) * 2 * TILE, kn * KT);
     if (!(a.causal && k0 > qw + 31)) {
-      const bool need_mask = (a.causal && k0 + 63 > qw) || k0 + 64 > a.S;
-      if (need_mask) fwd32_tile<true>(sK, sV, qf, o, m, l, k0, q, a.S, a.causal, c2, lane);
-      else fwd32_tile<false>(sK, sV, qf, o, m, l, k0, q, a.S, a.causal, c2, lane);
+      const bool need_mask = (a.causal && k0 + KT - 1 > qw) || k0 + KT > a.S;
+      if (need_mask) fwd32_tile<true, KT / 32>(sK, sV, qf, o, m, l, k0, q, a.S, a.causal, c2, lane);
+      else fwd32_tile<false, KT / 32>(sK, sV, qf, o, m, l, k0, q, a.S, a.causal, c2, lane);
     }
-    vm_wait<0>();        // the next tile's DMA (issued before this tile's compute) has landed
+    // tile kb + 1 has landed; tiles kb + 2 .. kb + NS - 2 may stay in flight (2 NP pieces per wave per tile)
+    const int ahead = min(NS - 2, nkb - 2 - kb);
+    if (NS >= 4 && ahead >= 2) vm_wait<4 * NP>();
+    else if (NS >= 3 && ahead >= 1) vm_wait<2 * NP>();
+    else vm_wait<0>();
     __syncthreads();
   }
   l = xh_sum(l);
@@ -1040,8 +1053,8 @@ __global__ __launch_bounds__(NTH, 1) void attn_bwd_dkv32_kernel(AttnArgs a) {
       stage_full64(buf, Qb + (long long)q0 * a.ld, soff, wu);
       stage_full64(buf + TILE, Db + (long long)q0 * a.ld, soff, wu);
     } else {
-      stage_rows64_asm(buf, Qb + (long long)q0 * a.ld, a.ld, a.S - q0, wu, lane);
-      stage_rows64_asm(buf + TILE, Db + (long long)q0 * a.ld, a.ld, a.S - q0, wu, lane);
+      stage_rows64_asm<4>(buf, Qb + (long long)q0 * a.ld, a.ld, a.S - q0, wu, lane);
+      stage_rows64_asm<4>(buf + TILE, Db + (long long)q0 * a.ld, a.ld, a.S - q0, wu, lane);
     }
     if (wu < 2) {   // wave 0: lse, wave 1: delta (64 x 4 B, lane-linear)
       const float* src = (wu == 0 ? a.LSE : a.delta) + sbase;
@@ -1121,6 +1134,14 @@ static int attn_dkv_kg() {
   return v;
 }
 
+// OBST_ATTN_FWD_RING=4: forward over 32-key tiles in a 4-deep LDS-DMA ring. A/B only: B64 S2048 H16 D128 causal
+// 1.37 -> 1.47 ms (unlike the dQ kernel, the forward's 64-key tiles already cover the DMA latency; halving them
+// doubles the barriers and the row max / rescale work per key)
+static int attn_fwd_ring() {
+  static int v = [] { const char* e = getenv("OBST_ATTN_FWD_RING"); return e ? atoi(e) : 2; }();
+  return v;
+}
+
 static int attn_dq_ring() {   // OBST_ATTN_DQ_RING=4: dQ kernel over 32-key tiles, 4-deep LDS-DMA ring
   static int v = [] { const char* e = getenv("OBST_ATTN_DQ_RING"); return e ? atoi(e) : 4; }();
   return v;
@@ -1144,7 +1165,8 @@ template <int D>
 int launch_fwd(const AttnArgs& a, hipStream_t st) {
   dim3 grid((a.S + 127) / 128 * a.B * a.H);
   if (D == 128 && attn_impl() == 2) {
-    hipLaunchKernelGGL(attn_fwd32_kernel, grid, dim3(NTH), 4 * 64 * 256, st, a);
+    if (attn_fwd_ring() == 4) hipLaunchKernelGGL(attn_fwd32_kernel<32>, grid, dim3(NTH), 4 * 2 * 32 * 256, st, a);
+    else hipLaunchKernelGGL(attn_fwd32_kernel<64>, grid, dim3(NTH), 2 * 2 * 64 * 256, st, a);
     return (int)hipGetLastError();
   }
   hipLaunchKernelGGL(attn_fwd_kernel<D>, grid, dim3(NTH), 4 * 64 * Geo<D>::ROWB, st, a);
