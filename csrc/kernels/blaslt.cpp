@@ -293,7 +293,79 @@ int obst_blaslt_gemm(const ObstGemmDesc* d, hipStream_t stream) {
   return st == HIPBLAS_STATUS_SUCCESS ? 0 : -(int)st - 200;
 }
 
+// Split-K weight gradients. The fp32 weight-gradient products of the step contract over all T = 131072 tokens into
+// few output tiles (M x N = 4096 x 2048: 128 256x256 tiles for 256 CUs); split into s K-slabs they run as one strided
+// batch of s x 128 tiles into a fixed workspace [s][M][N], folded (beta * C + slabs in index order: deterministic)
+// by obst_splitk_fold. s x tiles <= 256 bounds the workspace at 256 x 256 x 256 fp32 = 64 MiB, allocated once at the
+// first eligible call (eager: a captured graph never sees it move). OBST_LT_SPLITK=0 turns it off.
+extern "C" int obst_splitk_fold(const float* W, float* C, int M, int N, long long ldc, int s, float beta,
+                                hipStream_t st);
+namespace {
+constexpr size_t SK_WS_BYTES = 64ull << 20;
+void* g_sk_ws = nullptr;
+
+int g_splitk = -1;
+
+int splitk_on() {
+  if (g_splitk < 0) {
+    const char* e = getenv("OBST_LT_SPLITK");
+    g_splitk = e ? atoi(e) : 1;
+  }
+  return g_splitk;
+}
+
+int splitk_factor(const ObstGemmDesc* d) {
+  if (!splitk_on() || d->batch1 * d->batch2 != 1 || !d->out_f32 || d->R || d->act || d->mode || d->tri || d->kin)
+    return 1;
+  if (d->K < 16384 || d->N % 4 || d->ldc % 4) return 1;
+  const long long tiles = (long long)((d->M + 255) / 256) * ((d->N + 255) / 256);
+  if (tiles > 160) return 1;
+  int s = (int)(256 / tiles);
+  s = s > 4 ? 4 : s;
+  while (s > 1 && d->K % (s * 256)) --s;
+  if (s < 2 || (size_t)s * d->M * d->N * 4 > SK_WS_BYTES) return 1;
+  return s;
+}
+}  // namespace
+
+int obst_blaslt_gemm_split(const ObstGemmDesc* d, hipStream_t stream) {
+  const int s = splitk_factor(d);
+  if (s < 2 || !enabled()) return obst_blaslt_gemm(d, stream);
+  if (!g_sk_ws) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone)
+      return obst_blaslt_gemm(d, stream);       // never allocate under capture
+    if (hipMalloc(&g_sk_ws, SK_WS_BYTES) != hipSuccess) {
+      (void)hipGetLastError();
+      g_sk_ws = nullptr;
+      return obst_blaslt_gemm(d, stream);
+    }
+  }
+  const long long kc = d->K / s;
+  ObstGemmDesc b = *d;
+  b.C = g_sk_ws;
+  b.ldc = d->N;
+  b.K = (int)kc;
+  b.batch1 = s;
+  b.batch2 = 1;
+  b.a_s1 = d->a_t == 0 ? kc : kc * d->lda;      // A [M][K] / [K][M]: slab j starts j*kc along K
+  b.b_s1 = d->b_t == 0 ? kc : kc * d->ldb;      // B [N][K] / [K][N]
+  b.c_s1 = (long long)d->M * d->N;
+  b.a_s2 = b.b_s2 = b.c_s2 = 0;
+  b.beta = 0.f;
+  const int r = obst_blaslt_gemm(&b, stream);
+  if (r != 0) return r == 1 ? obst_blaslt_gemm(d, stream) : r;
+  return obst_splitk_fold((const float*)g_sk_ws, (float*)d->C, d->M, d->N, d->ldc, s, d->beta, stream) == 0 ? 0 : -300;
+}
+
 OBST_API int obst_blaslt_enabled() { return enabled(); }
+
+// runtime switch of the split-K weight-gradient path (tests); returns the previous setting
+OBST_API int obst_blaslt_splitk_set(int on) {
+  const int old = splitk_on();
+  g_splitk = on;
+  return old;
+}
 
 // counters for tests / diagnostics: out[0] = hipBLASLt dispatches, out[1] = eligible calls it declined
 OBST_API int obst_blaslt_stats(long long* out) {

@@ -277,3 +277,34 @@ OBST_API int obst_cast_f32_bf16(const float* X, void* Y, long long n, hipStream_
   hipLaunchKernelGGL(cast_f32_bf16_kernel, dim3(grid_for((n + 3) / 4)), dim3(NTH), 0, st, X, (bf16_t*)Y, n);
   return (int)hipGetLastError();
 }
+
+namespace {
+// split-K fold of the weight-gradient GEMM (blaslt.cpp): C[m][n] = beta * C[m][n] + sum_j W[j][m][n], slabs summed in
+// index order (deterministic); 4 fp32 per lane, N % 4 == 0
+__global__ __launch_bounds__(NTH) void splitk_fold_kernel(const float* __restrict__ W, float* __restrict__ C, int M,
+                                                          int N, long long ldc, int s, float beta) {
+  const long long n4 = (long long)M * (N / 4), slab = (long long)M * N;
+  for (long long v = (long long)blockIdx.x * NTH + threadIdx.x; v < n4; v += (long long)gridDim.x * NTH) {
+    const long long e = v * 4, m = e / N, n = e % N;
+    float4 acc = reinterpret_cast<const float4*>(W)[v];
+    for (int j = 1; j < s; ++j) {
+      const float4 w = reinterpret_cast<const float4*>(W + j * slab)[v];
+      acc.x += w.x; acc.y += w.y; acc.z += w.z; acc.w += w.w;
+    }
+    float4* c = reinterpret_cast<float4*>(C + m * ldc + n);
+    if (beta != 0.f) {
+      const float4 o = *c;
+      acc.x += beta * o.x; acc.y += beta * o.y; acc.z += beta * o.z; acc.w += beta * o.w;
+    }
+    *c = acc;
+  }
+}
+}  // namespace
+
+OBST_API int obst_splitk_fold(const float* W, float* C, int M, int N, long long ldc, int s, float beta, hipStream_t st) {
+  if (N % 4 || ldc % 4 || s < 1) return -1;
+  if ((((uintptr_t)W) | ((uintptr_t)C)) & 15) return -2;
+  hipLaunchKernelGGL(splitk_fold_kernel, dim3(grid_for((long long)M * N / 4)), dim3(NTH), 0, st, W, C, M, N, ldc, s,
+                     beta);
+  return (int)hipGetLastError();
+}

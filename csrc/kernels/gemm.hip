@@ -494,7 +494,7 @@ OBST_API int obst_gemm(const ObstGemmDesc* d, hipStream_t stream) {
   if (((uintptr_t)d->A | (uintptr_t)d->B) & 15) return -5;
   if (((uintptr_t)d->C) & 15) return -6;
   {
-    const int r = obst_blaslt_gemm(d, stream);
+    const int r = obst_blaslt_gemm_split(d, stream);
     if (r <= 0) return r;
   }
   GemmArgs a;

@@ -17,3 +17,5 @@ struct ObstGemmDesc {
 
 // plain GEMMs through hipBLASLt: 0 done, 1 not eligible (run the MFMA kernels), < 0 hipBLASLt error
 int obst_blaslt_gemm(const ObstGemmDesc* d, hipStream_t stream);
+// the same, with the fp32 weight-gradient products of few output tiles split over K (blaslt.cpp)
+int obst_blaslt_gemm_split(const ObstGemmDesc* d, hipStream_t stream);

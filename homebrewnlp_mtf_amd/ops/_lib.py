@@ -102,6 +102,7 @@ _SIGS = {
     "obst_opt_apply_rows": [ctypes.POINTER(OptDesc), c_p, c_i, c_p],
     "obst_blaslt_enabled": [],
     "obst_blaslt_set": [c_i],
+    "obst_blaslt_splitk_set": [c_i],
     "obst_blaslt_stats": [c_p],
     "obst_glu": [c_p, c_p, c_p, c_p, c_p, c_ll, c_p],
     "obst_pkm_top1": [c_p, c_p, c_p, c_p, c_p, c_ll, c_i, c_i, c_p],

@@ -59,6 +59,12 @@ def lt_set(on: bool) -> bool:
     return old
 
 
+def lt_splitk_set(on: bool) -> bool:
+    """switch the split-K fp32 weight-gradient path of the hipBLASLt dispatch (few output tiles, K >= 16384: one
+    strided batch over K-slabs + a deterministic fold; OBST_LT_SPLITK) at run time; returns the previous setting"""
+    return bool(L.lib().obst_blaslt_splitk_set(int(on)))
+
+
 def _room(t: torch.Tensor) -> int:
     """elements addressable from t.data_ptr() to the end of its storage"""
     return t.untyped_storage().nbytes() // t.element_size() - t.storage_offset()

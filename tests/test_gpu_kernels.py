@@ -384,6 +384,40 @@ def test_gemm_splitk_wgrad(cuda, a_t, b_t):
     _close(Cf.view(M, N), ref, 5e-2, 1e-2, f"splitk {a_t}{b_t}")
 
 
+@pytest.mark.parametrize("a_t,b_t", [(0, 1), (1, 0), (0, 0)])
+@pytest.mark.parametrize("beta", [0.0, 1.0])
+def test_blaslt_splitk_wgrad(cuda, a_t, b_t, beta):
+    """hipBLASLt split-K weight gradient (K-slabs as one strided batch + deterministic fold) into a strided fp32 C
+    against the fp32 product; bitwise run-to-run"""
+    if not raw.lt_enabled():
+        pytest.skip("hipBLASLt path off")
+    torch.manual_seed(6)
+    M, N, K, ldc = 512, 768, 32768, 1024
+    A = (torch.randn(M * K) * 0.5).to(BF)
+    B = (torch.randn(N * K) * 0.5).to(BF)
+    lda = K if a_t == 0 else M
+    ldb = K if b_t == 0 else N
+    av = A.view(M, K) if a_t == 0 else A.view(K, M).t()
+    bv = B.view(N, K).t() if b_t == 0 else B.view(K, N)
+    C0 = torch.randn(M, ldc)
+    ref = av.float() @ bv.float() + beta * C0[:, :N]
+    Ag, Bg = A.to(cuda), B.to(cuda)
+    old = raw.lt_splitk_set(True)
+    try:
+        outs = []
+        for _ in range(2):
+            Cf = C0.to(cuda).reshape(-1).contiguous()
+            raw.gemm(raw.Operand(Ag, a_t, lda), raw.Operand(Bg, b_t, ldb), raw.Operand(Cf, 0, ldc), M, N, K,
+                     beta=beta)
+            outs.append(Cf.view(M, ldc))
+        torch.cuda.synchronize()
+    finally:
+        raw.lt_splitk_set(old)
+    _close(outs[0][:, :N], ref, 5e-2, 1e-2, f"lt splitk {a_t}{b_t}")
+    assert torch.equal(outs[0], outs[1])
+    assert torch.equal(outs[0][:, N:].cpu(), C0[:, N:]), "columns past N must stay untouched"
+
+
 @pytest.mark.parametrize("causal", [True, False])
 def test_token_mixer_big_tiles(cuda, causal):
     """K03 through the 256x256 phase kernel (>= 512 tiles) incl. the triangular tile skipping (tri = 1/2/3)"""
