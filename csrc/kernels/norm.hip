@@ -46,6 +46,24 @@ __device__ __forceinline__ void load_raw(const bf16_t* x, int F, int sl, bool ok
   }
 }
 
+// unconditional 16-byte loads of a row whose pointer the caller has clamped to a valid row; lanes past F re-read
+// column 0 (their values are never used). No branch around the loads, so the compiler need not wait for each one
+// before the join (a conditional load compiled to load + vmcnt(0) per chunk)
+template <int NCH, int LPR>
+__device__ __forceinline__ void load_rawc(const bf16_t* x, int F, int sl, uint4 (&u)[NCH]) {
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = c * LPR * 8 + sl * 8;
+    u[c] = *reinterpret_cast<const uint4*>(x + (col < F ? col : 0));
+  }
+}
+
+__device__ __forceinline__ void unpack8(const uint4& u, float (&v)[8]) {
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { v[2 * j] = bf2f(w[j] & 0xffff); v[2 * j + 1] = bf2f(w[j] >> 16); }
+}
+
 template <int NCH>
 __device__ __forceinline__ void unpack_row(const uint4 (&u)[NCH], float (&v)[NCH][8]) {
 #pragma unroll
@@ -167,12 +185,34 @@ __global__ __launch_bounds__(NTH) void norm_partial_kernel(const bf16_t* __restr
   if (lane == 0) { out[2 * row] = s; out[2 * row + 1] = q; }
 }
 
+// the scale values of chunk c for a backward row: hoisted registers (narrow rows), the LDS copy (wide rows, one
+// group) or global memory
+template <int NCH, int LPR, bool HOIST>
+__device__ __forceinline__ void scale8(int c, int sl, int F, bool ok, long long poff, const float* __restrict__ scale,
+                                       bool sc_lds, const float* sc_s, const float (&hsc)[HOIST ? NCH : 1][8],
+                                       float (&gsc)[8]) {
+  const int col0 = c * LPR * 8 + sl * 8;
+  if (HOIST) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) gsc[j] = hsc[HOIST ? c : 0][j];
+  } else if (sc_lds) {
+    if (col0 < F) {
+      const float4 a4 = *reinterpret_cast<const float4*>(sc_s + col0);
+      const float4 b4 = *reinterpret_cast<const float4*>(sc_s + col0 + 4);
+      gsc[0] = a4.x; gsc[1] = a4.y; gsc[2] = a4.z; gsc[3] = a4.w;
+      gsc[4] = b4.x; gsc[5] = b4.y; gsc[6] = b4.z; gsc[7] = b4.w;
+    }
+  } else if (scale && ok && col0 < F) {
+    load8f(scale + poff + col0, gsc);
+  }
+}
+
 // backward. stats = (mean, rstd) per row. If `partial_out` is set, only writes per-row partial
 // (sum dxh, sum dxh*xh) for the TP all-reduce and returns (phase 1); with `ext_dsum` (phase 2) uses them.
 // Parameter gradients: per-lane register sums; the host sizes the grid so that (rows per grid step) % groups == 0,
 // so every lane only ever sees rows of one group (row % groups is fixed along the grid-stride loop).
 template <int NCH, int LPR>
-__global__ __launch_bounds__(NTH) void norm_bwd_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ DY,
+__global__ __launch_bounds__(NTH, 2) void norm_bwd_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ DY,
                                                        const float* __restrict__ scale, const float* __restrict__ stats,
                                                        bf16_t* __restrict__ DX, float* __restrict__ dscale,
                                                        float* __restrict__ dshift, long long rows, int F, int groups,
@@ -216,62 +256,51 @@ __global__ __launch_bounds__(NTH) void norm_bwd_kernel(const bf16_t* __restrict_
   }
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    const long long row = rbase + u * nw;
-    load_raw<NCH, LPR>(X + row * F, F, sl, row < rows, nx[u]);
-    load_raw<NCH, LPR>(DY + row * F, F, sl, row < rows, nd[u]);
-    if (R) load_raw<NCH, LPR>(R + row * F, F, sl, row < rows, nr[u]);
-    nst[u] = row < rows ? *reinterpret_cast<const float2*>(stats + 2 * row) : make_float2(0.f, 0.f);
+    const long long row = rbase + u * nw, rc = row < rows ? row : rows - 1;
+    load_rawc<NCH, LPR>(X + rc * F, F, sl, nx[u]);
+    load_rawc<NCH, LPR>(DY + rc * F, F, sl, nd[u]);
+    if (R) load_rawc<NCH, LPR>(R + rc * F, F, sl, nr[u]);
+    nst[u] = *reinterpret_cast<const float2*>(stats + 2 * rc);
   }
   for (long long r0 = rbase - sub; r0 < rows; r0 += U * nw) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
     const long long row = r0 + u * nw + sub;
     const bool ok = row < rows;
-    const long long nrow = row + U * nw;
-    float x[NCH][8], dy[NCH][8];
-    unpack_row<NCH>(nx[u], x);
-    unpack_row<NCH>(nd[u], dy);
-    uint4 cr[NCH];
-    if (R) {
+    const long long nrow = row + U * nw, nrc = nrow < rows ? nrow : rows - 1;
+    // this row stays packed (bf16) and is unpacked once per pass: the float copies of x and dy held across both
+    // passes pushed the kernel to 255 VGPRs, and the register reuse then forced a vmcnt(0) behind every next-row load
+    uint4 cx[NCH], cd[NCH], cr[NCH];
 #pragma unroll
-      for (int c = 0; c < NCH; ++c) cr[c] = nr[u][c];
-      load_raw<NCH, LPR>(R + nrow * F, F, sl, nrow < rows, nr[u]);
+    for (int c = 0; c < NCH; ++c) {
+      cx[c] = nx[u][c];
+      cd[c] = nd[u][c];
+      if (R) cr[c] = nr[u][c];
     }
-    load_raw<NCH, LPR>(X + nrow * F, F, sl, nrow < rows, nx[u]);
-    load_raw<NCH, LPR>(DY + nrow * F, F, sl, nrow < rows, nd[u]);
+    if (R) load_rawc<NCH, LPR>(R + nrc * F, F, sl, nr[u]);
+    load_rawc<NCH, LPR>(X + nrc * F, F, sl, nx[u]);
+    load_rawc<NCH, LPR>(DY + nrc * F, F, sl, nd[u]);
     const float mean = ok ? nst[u].x : 0.f, rstd = ok ? nst[u].y : 0.f;
-    nst[u] = nrow < rows ? *reinterpret_cast<const float2*>(stats + 2 * nrow) : make_float2(0.f, 0.f);
+    nst[u] = *reinterpret_cast<const float2*>(stats + 2 * nrc);
     const long long poff = (long long)(row % groups) * F;
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
-      float gsc[8];
+      float gsc[8], x[8], dy[8];
+      scale8<NCH, LPR, HOIST>(c, sl, F, ok, poff, scale, sc_lds, sc_s, hsc, gsc);
+      unpack8(cx[c], x);
+      unpack8(cd[c], dy);
       const int col0 = c * LPR * 8 + sl * 8;
-      if (HOIST) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) gsc[j] = hsc[HOIST ? c : 0][j];
-      } else if (sc_lds) {
-        if (col0 < F) {
-          const float4 a4 = *reinterpret_cast<const float4*>(sc_s + col0);
-          const float4 b4 = *reinterpret_cast<const float4*>(sc_s + col0 + 4);
-          gsc[0] = a4.x; gsc[1] = a4.y; gsc[2] = a4.z; gsc[3] = a4.w;
-          gsc[4] = b4.x; gsc[5] = b4.y; gsc[6] = b4.z; gsc[7] = b4.w;
-        }
-      } else if (scale && ok && col0 < F) {
-        load8f(scale + poff + col0, gsc);
-      }
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int col = col0 + j;
         if (ok && col < F) {
-          const float xh = (x[c][j] - mean) * rstd;
+          const float xh = (x[j] - mean) * rstd;
           const float g = scale ? gsc[j] : 1.f;
-          const float dxh = dy[c][j] * g;
+          const float dxh = dy[j] * g;
           s1 += dxh;
           s2 += dxh * xh;
-          if (want_param) { gs[c][j] += dy[c][j] * xh; gb[c][j] += dy[c][j]; }
-          x[c][j] = xh;
-          dy[c][j] = dxh;
+          if (want_param) { gs[c][j] += dy[j] * xh; gb[c][j] += dy[j]; }
         }
       }
     }
@@ -288,18 +317,21 @@ __global__ __launch_bounds__(NTH) void norm_bwd_kernel(const bf16_t* __restrict_
     for (int c = 0; c < NCH; ++c) {
       const int col = c * LPR * 8 + sl * 8;
       if (col >= F) continue;
+      float gsc[8], x[8], dy[8];
+      scale8<NCH, LPR, HOIST>(c, sl, F, ok, poff, scale, sc_lds, sc_s, hsc, gsc);
+      unpack8(cx[c], x);
+      unpack8(cd[c], dy);
       float r[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      if (R) {   // the block's residual-input gradient, summed here instead of in a separate elementwise pass
-        const uint4 uu = cr[c];
-        const uint32_t wv[4] = {uu.x, uu.y, uu.z, uu.w};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) { r[2 * j] = bf2f(wv[j] & 0xffff); r[2 * j + 1] = bf2f(wv[j] >> 16); }
-      }
+      if (R) unpack8(cr[c], r);   // the block's residual-input gradient, summed here instead of in a separate pass
       uint32_t o[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        o[j] = pack_bf16x2(rstd * (dy[c][2 * j] - m1 - x[c][2 * j] * m2) + r[2 * j],
-                           rstd * (dy[c][2 * j + 1] - m1 - x[c][2 * j + 1] * m2) + r[2 * j + 1]);
+      for (int j = 0; j < 4; ++j) {
+        const int j0 = 2 * j, j1 = 2 * j + 1;
+        const float g0 = scale ? gsc[j0] : 1.f, g1 = scale ? gsc[j1] : 1.f;
+        const float xh0 = (x[j0] - mean) * rstd, xh1 = (x[j1] - mean) * rstd;
+        const float d0 = dy[j0] * g0, d1 = dy[j1] * g1;
+        o[j] = pack_bf16x2(rstd * (d0 - m1 - xh0 * m2) + r[j0], rstd * (d1 - m1 - xh1 * m2) + r[j1]);
+      }
       *reinterpret_cast<uint4*>(DX + row * F + col) = make_uint4(o[0], o[1], o[2], o[3]);
     }
     }
