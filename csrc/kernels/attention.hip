@@ -857,6 +857,11 @@ __device__ __forceinline__ void stage_rows64_asm(char* lds, const bf16_t* g, lon
   }
 }
 
+// forward epilogue through LDS (whole-row 16-byte stores); 0: per-lane 8-byte stores at row stride (A/B)
+#ifndef FWD_EPI_LDS
+#define FWD_EPI_LDS 1
+#endif
+
 // block = 128 queries of one (b, h), wave w owns 32; K/V 64-key tiles double-buffered by LDS-DMA, one barrier/tile;
 // the tile loop is unrolled by two so both buffers' fragment addresses are immediates
 // KT = 32: 32-key tiles in a 4-deep ring (the same 64 KiB), the next three tiles in flight instead of one
@@ -933,8 +938,47 @@ __global__ __launch_bounds__(NTH, 2) void attn_fwd32_kernel(AttnArgs a) {
     __syncthreads();
   }
   l = xh_sum(l);
-  if (q < a.S) {
-    const float inv = 1.f / l;
+  const float inv = 1.f / l;
+  if (q < a.S && h == 0) a.LSE[((long long)b * a.H + hd) * a.S + q] = (m + __log2f(l)) / LOG2E;
+  if (FWD_EPI_LDS) {
+    // O through LDS, stored as whole rows: the lane's 64 values are 16 pieces of 8 bytes at row stride (each store
+    // instruction touched 32 rows); staged in the wave's 8 KiB of the (now idle) K/V ring and read back as 16-byte
+    // chunks, 16 lanes per 256-byte row, every store instruction writes 4 whole rows (and the residual add reads them
+    // the same way). Image: row n, 16-byte chunk c at (c ^ (n & 7)), 8-byte half h at h ^ ((n >> 3) & 1) -- the 16
+    // lanes of a ds_write_b64 group (rows n..n+15, one c, one h) hit 16 distinct 8-byte slots of 128 bytes.
+    char* so = smem + w * 32 * 256;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int c = dt * 4 + g4;
+        const uint2 v = make_uint2(pack_bf16x2(o[dt][4 * g4] * inv, o[dt][4 * g4 + 1] * inv),
+                                   pack_bf16x2(o[dt][4 * g4 + 2] * inv, o[dt][4 * g4 + 3] * inv));
+        *reinterpret_cast<uint2*>(so + n * 256 + ((c ^ (n & 7)) << 4) + ((h ^ ((n >> 3) & 1)) << 3)) = v;
+      }
+    __syncthreads();
+    const int c = lane & 15;
+    const long long obase = (long long)b * a.S * a.ld_o + hd * D + c * 8;
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+      const int rr = it * 4 + (lane >> 4), qr = qw + rr;
+      uint4 v = *reinterpret_cast<const uint4*>(so + rr * 256 + ((c ^ (rr & 7)) << 4));
+      if ((rr >> 3) & 1) v = make_uint4(v.z, v.w, v.x, v.y);
+      if (qr < a.S) {
+        const long long off = obase + (long long)qr * a.ld_o;
+        *reinterpret_cast<uint4*>(a.Oout + off) = v;
+        if (a.Sum) {
+          const uint4 r = *reinterpret_cast<const uint4*>(a.Res + off);
+          const uint32_t ov[4] = {v.x, v.y, v.z, v.w}, rv[4] = {r.x, r.y, r.z, r.w};
+          uint32_t sv[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            sv[j] = pack_bf16x2(bf2f(ov[j] & 0xffff) + bf2f(rv[j] & 0xffff), bf2f(ov[j] >> 16) + bf2f(rv[j] >> 16));
+          *reinterpret_cast<uint4*>(a.Sum + off) = make_uint4(sv[0], sv[1], sv[2], sv[3]);
+        }
+      }
+    }
+  } else if (q < a.S) {
     const long long orow = (long long)b * a.S * a.ld_o + hd * D + (long long)q * a.ld_o;
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt)
@@ -944,7 +988,6 @@ __global__ __launch_bounds__(NTH, 2) void attn_fwd32_kernel(AttnArgs a) {
         store_o4(a, orow + d, o[dt][4 * g4] * inv, o[dt][4 * g4 + 1] * inv, o[dt][4 * g4 + 2] * inv,
                  o[dt][4 * g4 + 3] * inv);
       }
-    if (h == 0) a.LSE[((long long)b * a.H + hd) * a.S + q] = (m + __log2f(l)) / LOG2E;
   }
 }
 
