@@ -169,6 +169,22 @@ __device__ __forceinline__ void store_o4(const AttnArgs& a, long long off, float
   }
 }
 
+// Epilogue staging of a wave's [rows][128] bf16 output tile held in 16x16 accumulator layout (lane i = row within a
+// 16-row group, g = lane >> 4: d = dt*16 + 4g + [0, 4)), so the global stores go out as whole 256-byte rows, 16-byte
+// per lane, instead of 8-byte pieces at row stride. Image: row r, 16-byte chunk c at (c ^ (r & 7)), 8-byte half at
+// hf ^ ((r >> 3) & 1): the 16 lanes of a ds_write_b64 group (16 rows, one chunk, one half) hit 16 distinct slots.
+__device__ __forceinline__ void epi_put(char* so, int row, int dt, int g, const f32x4_t& v, float sc) {
+  const int c = 2 * dt + (g >> 1), hf = g & 1;
+  *reinterpret_cast<uint2*>(so + row * 256 + ((c ^ (row & 7)) << 4) + ((hf ^ ((row >> 3) & 1)) << 3)) =
+      make_uint2(pack_bf16x2(v[0] * sc, v[1] * sc), pack_bf16x2(v[2] * sc, v[3] * sc));
+}
+
+// 16-byte chunk c (elements 8c..8c+7) of row rr of the staged image, in logical order
+__device__ __forceinline__ uint4 epi_get(const char* so, int rr, int c) {
+  const uint4 v = *reinterpret_cast<const uint4*>(so + rr * 256 + ((c ^ (rr & 7)) << 4));
+  return ((rr >> 3) & 1) ? make_uint4(v.z, v.w, v.x, v.y) : v;
+}
+
 // ----------------------------------------------------------------------------------------------------------------
 // raw v_exp_f32 (2^x): no denormal range fix-up (exp2f adds a compare + 2 ldexp per call); -inf -> 0
 __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
@@ -516,6 +532,21 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_bwd_dq_kernel(AttnArgs a) {
     else vm_wait<0>();
     __syncthreads();
   }
+  if constexpr (D == 128 && NW * 32 * 256 <= NS * 2 * TILE) {   // dQ through LDS as whole rows (epi_put)
+    char* so = smem + w * 32 * 256;
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+      for (int dt = 0; dt < G::DT; ++dt) epi_put(so, qt * 16 + i, dt, g, acc[dt][qt], a.scale);
+    __syncthreads();
+    const int c = lane & 15;
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+      const int rr = it * 4 + (lane >> 4), q = qw + rr;
+      const uint4 v = epi_get(so, rr, c);
+      if (q < a.S) *reinterpret_cast<uint4*>(a.dQ + base + (long long)q * a.ld + c * 8) = v;
+    }
+  } else {
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
     const int q = qw + qt * 16 + i;
@@ -527,6 +558,7 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_bwd_dq_kernel(AttnArgs a) {
       *reinterpret_cast<uint2*>(a.dQ + base + (long long)q * a.ld + d) =
           make_uint2(pack_bf16x2(acc[dt][qt][0] * sc, acc[dt][qt][1] * sc), pack_bf16x2(acc[dt][qt][2] * sc, acc[dt][qt][3] * sc));
     }
+  }
   }
 }
 
@@ -697,6 +729,29 @@ __global__ __launch_bounds__(NW * 64, KG == 1 ? 2 : 1) void attn_bwd_dkv_kernel(
       vm_wait<0>();
     }
     __syncthreads();
+  }
+  if constexpr (D == 128 && NW * 2 * KW * 256 <= NS * STAGE) {   // dK, dV through LDS as whole rows (epi_put)
+    char* sk = smem + w * 2 * KW * 256;
+    char* sv = sk + KW * 256;
+#pragma unroll
+    for (int j = 0; j < KG; ++j)
+#pragma unroll
+      for (int dt = 0; dt < G::DT; ++dt) {
+        epi_put(sk, 16 * j + i, dt, g, dk[j][dt], a.scale);
+        epi_put(sv, 16 * j + i, dt, g, dv[j][dt], 1.f);
+      }
+    __syncthreads();
+    const int c = lane & 15;
+#pragma unroll
+    for (int it = 0; it < KW / 4; ++it) {
+      const int rr = it * 4 + (lane >> 4), kj = kw + rr;
+      const uint4 vk = epi_get(sk, rr, c), vv = epi_get(sv, rr, c);
+      if (kj < a.S) {
+        *reinterpret_cast<uint4*>(a.dK + base + (long long)kj * a.ld + c * 8) = vk;
+        *reinterpret_cast<uint4*>(a.dV + base + (long long)kj * a.ld + c * 8) = vv;
+      }
+    }
+    return;
   }
 #pragma unroll
   for (int j = 0; j < KG; ++j) {
