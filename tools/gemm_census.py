@@ -45,12 +45,30 @@ def _wrapped(a, b, c, M, N, K, batch=(1, 1), alpha=1.0, beta=0.0, act=None, act_
     return out
 
 
+_orig_t = raw.transpose
+_trecords = []
+
+
+def _wrapped_t(x, y, rows, cols, ldx, ldy, batch=1, sx=0, sy=0):
+    if not _on[0]:
+        return _orig_t(x, y, rows, cols, ldx, ldy, batch, sx, sy)
+    import traceback
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    out = _orig_t(x, y, rows, cols, ldx, ldy, batch, sx, sy)
+    e1.record()
+    caller = traceback.extract_stack(limit=3)[0]
+    _trecords.append(((rows, cols, batch, f"{os.path.basename(caller.filename)}:{caller.lineno}"), e0, e1))
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="configs/gpt_neo_1.3b.json")
     ap.add_argument("--batch-per-gpu", type=int, default=64)
     args = ap.parse_args()
     raw.gemm = _wrapped
+    raw.transpose = _wrapped_t
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     mesh = pstate.Mesh(dp=1, tp=1, rank=0).build_groups()
@@ -80,6 +98,16 @@ def main():
         M, N, K = sig[0], sig[1], sig[2]
         fl = 2.0 * M * N * K * sig[10] * n
         print("| " + " | ".join(str(s) for s in sig) + f" | {n} | {t:.2f} | {1000 * t / n:.0f} | {fl / t / 1e9:.0f} |")
+    tagg = collections.OrderedDict()
+    for sig, e0, e1 in _trecords:
+        n, t = tagg.get(sig, (0, 0.0))
+        tagg[sig] = (n + 1, t + e0.elapsed_time(e1))
+    print(f"\n{len(_trecords)} transposes, {sum(t for _, t in tagg.values()):.1f} ms")
+    print("| rows | cols | batch | caller | calls | ms | us/call | GB/s |")
+    print("|---|---|---|---|---|---|---|---|")
+    for sig, (n, t) in sorted(tagg.items(), key=lambda kv: -kv[1][1]):
+        gb = 4.0 * sig[0] * sig[1] * sig[2] * n / 1e9
+        print("| " + " | ".join(str(s) for s in sig) + f" | {n} | {t:.2f} | {1000 * t / n:.0f} | {gb / t * 1e3:.0f} |")
 
 
 if __name__ == "__main__":
