@@ -890,21 +890,21 @@ __device__ __forceinline__ void fwd32_tile(const char* sK, const char* sV, const
 
 // LDS-DMA of a full 64-row tile: wave-uniform global base + 32-bit per-lane byte offsets computed once (soff), so
 // the loads take the saddr + voffset form and the LDS base (M0) is scalar
-template <int NP>   // NP pieces per wave: 4 for a 64-row tile, 2 for 32 rows
+template <int NP, int NW = 4>   // NP pieces per wave: 4 for a 64-row tile, 2 for 32 rows (NW = 4 waves)
 __device__ __forceinline__ void stage_full64(char* lds, const bf16_t* g, const unsigned (&soff)[NP], int w) {
   const char* gb = reinterpret_cast<const char*>(g);
 #pragma unroll
-  for (int i = 0; i < NP; ++i) glds16_asm(gb + soff[i], lds + (w + 4 * i) * 1024);
+  for (int i = 0; i < NP; ++i) glds16_asm(gb + soff[i], lds + (w + NW * i) * 1024);
 }
 
 // stage_rows with the asm DMA (ragged last tile: rows >= nvalid clamped to the last valid row)
-template <int NP>
+template <int NP, int NW = 4>
 __device__ __forceinline__ void stage_rows64_asm(char* lds, const bf16_t* g, long long ld, int nvalid, int w,
                                                  int lane) {
   const int last = nvalid - 1;
 #pragma unroll
   for (int i = 0; i < NP; ++i) {
-    const int j = w + 4 * i;
+    const int j = w + NW * i;
     const int row = j * 4 + (lane >> 4);
     const int c = (lane & 15) ^ swz<128>(row);
     const int srow = row < last ? row : last;
@@ -920,41 +920,43 @@ __device__ __forceinline__ void stage_rows64_asm(char* lds, const bf16_t* g, lon
 // block = 128 queries of one (b, h), wave w owns 32; K/V 64-key tiles double-buffered by LDS-DMA, one barrier/tile;
 // the tile loop is unrolled by two so both buffers' fragment addresses are immediates
 // KT = 32: 32-key tiles in a 4-deep ring (the same 64 KiB), the next three tiles in flight instead of one
-template <int KT = 64>
-__global__ __launch_bounds__(NTH, 2) void attn_fwd32_kernel(AttnArgs a) {
+// NW = 8: 256 queries per block, one block per CU -- the K/V tiles each CU streams from L2 halve (A/B knob)
+template <int KT = 64, int NW = 4>
+__global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd32_kernel(AttnArgs a) {
   constexpr int D = 128;
   constexpr int TILE = KT * 256;
   constexpr int NS = KT == 64 ? 2 : 4;
-  constexpr int NP = KT / 16;         // LDS-DMA pieces per wave per K (or V) tile
+  constexpr int NP = KT / 4 / NW;     // LDS-DMA pieces per wave per K (or V) tile
+  constexpr int QB = 32 * NW;         // queries per block
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, n = lane & 31;
-  const int nx = (a.S + 127) / 128;
+  const int nx = (a.S + QB - 1) / QB;
   int bx, bh;
   attn_block(nx, bx, bh);
   const int b = bh / a.H, hd = bh % a.H;
-  const int qblk = (a.causal ? (nx - 1 - bx) : bx) * 128;
+  const int qblk = (a.causal ? (nx - 1 - bx) : bx) * QB;
   const int qw = qblk + w * 32;
   const int q = qw + n;
   const long long base = (long long)b * a.S * a.ld + hd * D;
   const bf16_t* Kb = a.K + base;
   const bf16_t* Vb = a.V + base;
-  const int kend = a.causal ? min(a.S, qblk + 128) : a.S;
+  const int kend = a.causal ? min(a.S, qblk + QB) : a.S;
   const int nkb = (kend + KT - 1) / KT;
   const int wu = __builtin_amdgcn_readfirstlane(w);
   unsigned soff[NP];
 #pragma unroll
   for (int i = 0; i < NP; ++i) {
-    const int row = (wu + 4 * i) * 4 + (lane >> 4);
+    const int row = (wu + NW * i) * 4 + (lane >> 4);
     soff[i] = (unsigned)(row * (int)a.ld + (((lane & 15) ^ swz<128>(row)) << 3)) * 2u;
   }
   auto stage = [&](char* buf, int k0) {
     k0 = __builtin_amdgcn_readfirstlane(k0);
     if (k0 + KT <= a.S) {
-      stage_full64<NP>(buf, Kb + (long long)k0 * a.ld, soff, wu);
-      stage_full64<NP>(buf + TILE, Vb + (long long)k0 * a.ld, soff, wu);
+      stage_full64<NP, NW>(buf, Kb + (long long)k0 * a.ld, soff, wu);
+      stage_full64<NP, NW>(buf + TILE, Vb + (long long)k0 * a.ld, soff, wu);
     } else {
-      stage_rows64_asm<NP>(buf, Kb + (long long)k0 * a.ld, a.ld, a.S - k0, wu, lane);
-      stage_rows64_asm<NP>(buf + TILE, Vb + (long long)k0 * a.ld, a.ld, a.S - k0, wu, lane);
+      stage_rows64_asm<NP, NW>(buf, Kb + (long long)k0 * a.ld, a.ld, a.S - k0, wu, lane);
+      stage_rows64_asm<NP, NW>(buf + TILE, Vb + (long long)k0 * a.ld, a.ld, a.S - k0, wu, lane);
     }
   };
 #pragma unroll
@@ -995,7 +997,7 @@ __global__ __launch_bounds__(NTH, 2) void attn_fwd32_kernel(AttnArgs a) {
   l = xh_sum(l);
   const float inv = 1.f / l;
   if (q < a.S && h == 0) a.LSE[((long long)b * a.H + hd) * a.S + q] = (m + __log2f(l)) / LOG2E;
-  if (FWD_EPI_LDS) {
+  if (FWD_EPI_LDS && NW * 32 * 256 <= NS * 2 * TILE) {
     // O through LDS, stored as whole rows: the lane's 64 values are 16 pieces of 8 bytes at row stride (each store
     // instruction touched 32 rows); staged in the wave's 8 KiB of the (now idle) K/V ring and read back as 16-byte
     // chunks, 16 lanes per 256-byte row, every store instruction writes 4 whole rows (and the residual add reads them
@@ -1240,6 +1242,12 @@ static int attn_fwd_ring() {
   return v;
 }
 
+// OBST_ATTN_FWD_NW=8: forward blocks of 8 waves / 256 queries (one block per CU) instead of 4 waves / 128 queries
+static int attn_fwd_nw() {
+  static int v = [] { const char* e = getenv("OBST_ATTN_FWD_NW"); return e ? atoi(e) : 4; }();
+  return v;
+}
+
 static int attn_dq_ring() {   // OBST_ATTN_DQ_RING=4: dQ kernel over 32-key tiles, 4-deep LDS-DMA ring
   static int v = [] { const char* e = getenv("OBST_ATTN_DQ_RING"); return e ? atoi(e) : 4; }();
   return v;
@@ -1263,8 +1271,14 @@ template <int D>
 int launch_fwd(const AttnArgs& a, hipStream_t st) {
   dim3 grid((a.S + 127) / 128 * a.B * a.H);
   if (D == 128 && attn_impl() == 2) {
-    if (attn_fwd_ring() == 4) hipLaunchKernelGGL(attn_fwd32_kernel<32>, grid, dim3(NTH), 4 * 2 * 32 * 256, st, a);
-    else hipLaunchKernelGGL(attn_fwd32_kernel<64>, grid, dim3(NTH), 2 * 2 * 64 * 256, st, a);
+    if (attn_fwd_nw() == 8) {
+      dim3 g8((a.S + 255) / 256 * a.B * a.H);
+      hipLaunchKernelGGL((attn_fwd32_kernel<64, 8>), g8, dim3(512), 2 * 2 * 64 * 256, st, a);
+    } else if (attn_fwd_ring() == 4) {
+      hipLaunchKernelGGL(attn_fwd32_kernel<32>, grid, dim3(NTH), 4 * 2 * 32 * 256, st, a);
+    } else {
+      hipLaunchKernelGGL(attn_fwd32_kernel<64>, grid, dim3(NTH), 2 * 2 * 64 * 256, st, a);
+    }
     return (int)hipGetLastError();
   }
   hipLaunchKernelGGL(attn_fwd_kernel<D>, grid, dim3(NTH), 4 * 64 * Geo<D>::ROWB, st, a);
