@@ -828,11 +828,12 @@ __device__ __forceinline__ bf16x8_t tr_pair(const char* lds, int o0, int o1) {
 template <bool MASK, int NKT = 2>
 __device__ __forceinline__ void fwd32_tile(const char* sK, const char* sV, const bf16x8_t (&qf)[8],
                                            f32x16_t (&o)[4], float& m, float& l, int k0, int q, int S, int causal,
-                                           float c2, int lane) {
+                                           float c2, int lane, int prio = 0) {
   const int h = lane >> 5;
   Frag32 fo;
   frag32_offsets(fo, lane);
   f32x16_t s[NKT];
+  if (prio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
   for (int kt = 0; kt < NKT; ++kt) {
     s[kt] = f32x16_t{};
@@ -842,6 +843,7 @@ __device__ __forceinline__ void fwd32_tile(const char* sK, const char* sV, const
       s[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], s[kt], 0, 0, 0);
     }
   }
+  if (prio) __builtin_amdgcn_s_setprio(0);
   float mx = -INFINITY;
 #pragma unroll
   for (int kt = 0; kt < NKT; ++kt)
@@ -875,6 +877,7 @@ __device__ __forceinline__ void fwd32_tile(const char* sK, const char* sV, const
       rs += p;
     }
   l += rs;
+  if (prio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
   for (int kt = 0; kt < NKT; ++kt)
 #pragma unroll
@@ -886,6 +889,7 @@ __device__ __forceinline__ void fwd32_tile(const char* sK, const char* sV, const
         o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_pair(sV, fo.v[dt][0] + kb, fo.v[dt][1] + kb), pf, o[dt],
                                                         0, 0, 0);
     }
+  if (prio) __builtin_amdgcn_s_setprio(0);
 }
 
 // LDS-DMA of a full 64-row tile: wave-uniform global base + 32-bit per-lane byte offsets computed once (soff), so
@@ -984,8 +988,8 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd32_kernel(AttnArgs a)
     if (kn < nkb) stage(smem + (kn % NS) * 2 * TILE, kn * KT);
     if (!(a.causal && k0 > qw + 31)) {
       const bool need_mask = (a.causal && k0 + KT - 1 > qw) || k0 + KT > a.S;
-      if (need_mask) fwd32_tile<true, KT / 32>(sK, sV, qf, o, m, l, k0, q, a.S, a.causal, c2, lane);
-      else fwd32_tile<false, KT / 32>(sK, sV, qf, o, m, l, k0, q, a.S, a.causal, c2, lane);
+      if (need_mask) fwd32_tile<true, KT / 32>(sK, sV, qf, o, m, l, k0, q, a.S, a.causal, c2, lane, a.prio & 4);
+      else fwd32_tile<false, KT / 32>(sK, sV, qf, o, m, l, k0, q, a.S, a.causal, c2, lane, a.prio & 4);
     }
     // tile kb + 1 has landed; tiles kb + 2 .. kb + NS - 2 may stay in flight (2 NP pieces per wave per tile)
     const int ahead = min(NS - 2, nkb - 2 - kb);
