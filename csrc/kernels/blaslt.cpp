@@ -64,6 +64,17 @@ int tune() {
   return v;
 }
 
+// OBST_LT_ALGO=k (A/B): take the heuristic's k-th candidate (clamped to the ones returned) for every plan
+int algo_idx() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("OBST_LT_ALGO");
+    v = e ? atoi(e) : 0;
+    if (v < 0) v = 0;
+  }
+  return v;
+}
+
 // runs one candidate algorithm of a plan under construction into a scratch D (for timing)
 struct Runner {
   hipblasLtHandle_t handle = nullptr;
@@ -161,7 +172,8 @@ Plan make_plan(State& S, const Key& k, const Runner& run_in) {
   hipblasLtMatmulHeuristicResult_t res[NCAND];
   int n = 0;
   const hipblasStatus_t st =
-      hipblasLtMatmulAlgoGetHeuristic(S.handle, p.op, p.la, p.lb, p.lc, p.ld, pref, tune() ? NCAND : 1, res, &n);
+      hipblasLtMatmulAlgoGetHeuristic(S.handle, p.op, p.la, p.lb, p.lc, p.ld, pref,
+                                      tune() ? NCAND : (algo_idx() + 1 < NCAND ? algo_idx() + 1 : NCAND), res, &n);
   hipblasLtMatmulPreferenceDestroy(pref);
   int good = 0;
   for (int i = 0; i < n; ++i)
@@ -172,7 +184,7 @@ Plan make_plan(State& S, const Key& k, const Runner& run_in) {
               (int)st, n, k.M, k.N, k.K, k.a_t, k.b_t, k.out_f32, k.has_r, k.epi, k.batch);
     return p;
   }
-  p.algo = res[0].algo;
+  p.algo = res[algo_idx() < good ? algo_idx() : good - 1].algo;
   p.ok = true;
   if (good > 1 && run) {
     // first use of this signature: time the heuristic's candidates on the real operands (D -> scratch, so an
