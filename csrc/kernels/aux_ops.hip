@@ -550,21 +550,31 @@ __global__ __launch_bounds__(NTH) void decode_attn_split_kernel(
   float m = -INFINITY, l = 0.f, acc[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) acc[i] = 0.f;
+  // lanes past D read column 0 of their row (values unused); rows past the split's end re-read its last row
+  const bf16_t* Kr = act ? Kb : Kb - e0;
+  const bf16_t* Vr = act ? Vb : Vb - e0;
   for (long long j0 = jb; j0 < je; j0 += 64) {
     float s[4];
-    uint4 vv[4];
+    uint4 kk[4], vv[4];
+    // all 8 K / V row loads of the step issued before any is used: unconditional loads on clamped rows (a load
+    // under `if (j < je)` compiled to load + vmcnt(0), one row in flight per lane at a time)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const long long j = j0 + w * 16 + u * 4 + g, jc = j < je ? j : je - 1;
+      kk[u] = *reinterpret_cast<const uint4*>(Kr + jc * rs);
+      vv[u] = *reinterpret_cast<const uint4*>(Vr + jc * rs);
+    }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const long long j = j0 + w * 16 + u * 4 + g;
-      uint4 kk = make_uint4(0, 0, 0, 0);
-      vv[u] = kk;
-      if (act && j < je) {
-        const bool cur = j == P;
-        kk = cur ? kn : *reinterpret_cast<const uint4*>(Kb + j * rs);
-        vv[u] = cur ? vn : *reinterpret_cast<const uint4*>(Vb + j * rs);
-      }
+      const bool ok = act && j < je, cur = j == P;   // the new token's row: from registers (appended above)
+      kk[u] = !ok ? make_uint4(0, 0, 0, 0) : (cur ? kn : kk[u]);
+      vv[u] = !ok ? make_uint4(0, 0, 0, 0) : (cur ? vn : vv[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
       float kf[8];
-      unpack8(kk, kf);
+      unpack8(kk[u], kf);
       float d = 0.f;
 #pragma unroll
       for (int i = 0; i < 8; ++i) d += q[i] * kf[i];
