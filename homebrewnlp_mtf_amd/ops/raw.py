@@ -972,6 +972,10 @@ def l1(fo, g, mask, inner: int, loss=None, dfo=None, gptr=None, gscale: float = 
     return None
 
 
+# OBST_DECODE_BLOCKS: target block count of the split-K decode attention (key chunks x B x H); A/B knob
+_DEC_BLOCKS = int(__import__("os").environ.get("OBST_DECODE_BLOCKS", "2048"))
+
+
 def decode_attn(q, kn, vn, k, v, o, pos, B: int, S: int, H: int, D: int, scale: float):
     """KV-cache decode step: k[b][pos_b] = kn[b], v[b][pos_b] = vn[b], then
     o[b][h] = softmax_j(scale q[b][h].k[b][j][h], j <= pos_b) . v[b][j][h]; q, kn, vn, o [B][H][D]; caches [B][S][H][D]"""
@@ -985,7 +989,7 @@ def decode_attn(q, kn, vn, k, v, o, pos, B: int, S: int, H: int, D: int, scale: 
                          ("v", v, B * S * H * D), ("o", o, B * H * D)):
             _need(t, n - 1, nm)
         # key splits so that the grid has >= ~2048 blocks (8 per CU), each split >= 64 keys
-        nsplit = max(1, min(-(-2048 // (B * H)), -(-S // 64))) if D % 8 == 0 else 1
+        nsplit = max(1, min(-(-_DEC_BLOCKS // (B * H)), -(-S // 64))) if D % 8 == 0 else 1
         ws = torch.empty(B * H * nsplit * (D + 2) if nsplit > 1 else 1, dtype=torch.float32, device=q.device)
         L.check(L.lib().obst_decode_attn(q.data_ptr(), kn.data_ptr(), vn.data_ptr(), k.data_ptr(), v.data_ptr(),
                                          o.data_ptr(), pos.data_ptr(), B, S, H, D, float(scale), nsplit,
