@@ -214,46 +214,6 @@ hipError_t launch(const GemmArgs& a, int batch, hipStream_t stream) {
 // image is applied to the per-lane SOURCE address (cdna guide §5.4 rule 21), the ds_read side applies the same
 // XOR. Requires K % 64 == 0; rows/columns beyond M/N are clamped to valid memory (their results are never stored).
 
-template <bool OUT_F32>
-__device__ __forceinline__ void epilogue_store(const GemmArgs& p, long long idx, float (&v)[4]) {
-  if (OUT_F32) {
-    float* C = reinterpret_cast<float*>(p.C) + idx;
-    if (p.beta != 0.f) {
-      float4 o = *reinterpret_cast<const float4*>(C);
-      v[0] += p.beta * o.x; v[1] += p.beta * o.y; v[2] += p.beta * o.z; v[3] += p.beta * o.w;
-    }
-    if (p.R) {
-      float4 r = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(p.R) + idx);
-      v[0] += r.x; v[1] += r.y; v[2] += r.z; v[3] += r.w;
-    }
-    if (p.act) {
-#pragma unroll
-      for (int t = 0; t < 4; ++t) v[t] = act_fwd(p.act, v[t]);
-    }
-    *reinterpret_cast<float4*>(C) = make_float4(v[0], v[1], v[2], v[3]);
-  } else {
-    if (p.R) {
-      uint2 r = *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16_t*>(p.R) + idx);
-      v[0] += bf2f(r.x & 0xffff); v[1] += bf2f(r.x >> 16); v[2] += bf2f(r.y & 0xffff); v[3] += bf2f(r.y >> 16);
-    }
-    if (p.mode == 1) {
-      uint2 z = *reinterpret_cast<const uint2*>(p.Zin + idx);
-      v[0] *= act_grad(p.act, bf2f(z.x & 0xffff)); v[1] *= act_grad(p.act, bf2f(z.x >> 16));
-      v[2] *= act_grad(p.act, bf2f(z.y & 0xffff)); v[3] *= act_grad(p.act, bf2f(z.y >> 16));
-    } else {
-      if (p.Zout) {
-        *reinterpret_cast<uint2*>(p.Zout + idx) = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
-      }
-      if (p.act) {
-#pragma unroll
-        for (int t = 0; t < 4; ++t) v[t] = act_fwd(p.act, v[t]);
-      }
-    }
-    *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.C) + idx) =
-        make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
-  }
-}
-
 // ---------------------------------------------------------------------------------------------------------------
 // Phase-pipelined 256x256 kernel (cdna_hip_programming.md §5 "256² 8-phase template", re-derived here).
 // 8 waves = 2 (M) x 4 (N) groups; C is cut into quadrants (qm, qn) of 128 x 128, and wave (wr, wc) owns the
@@ -473,6 +433,23 @@ hipError_t launch_ph(GemmArgs a, int batch, hipStream_t stream) {
 
 }  // namespace
 
+// OBST_GEMM_4W=0 keeps the plain products on the phase kernels (A/B); runtime switch obst_gemm4w_set
+static int g_4w = -1;
+static long long g_4w_calls = 0;
+static int g4w_enabled() {
+  if (g_4w < 0) {
+    const char* e = getenv("OBST_GEMM_4W");
+    g_4w = e ? atoi(e) : 1;
+  }
+  return g_4w;
+}
+OBST_API int obst_gemm4w_set(int on) {
+  const int old = g4w_enabled();
+  g_4w = on;
+  return old;
+}
+OBST_API long long obst_gemm4w_calls() { return g_4w_calls; }
+
 static int getenv_big() {   // OBST_GEMM_BIG=0: only the 128x128 kernel (A/B, debugging)
   static int v = -1;
   if (v < 0) {
@@ -545,6 +522,19 @@ OBST_API int obst_gemm(const ObstGemmDesc* d, hipStream_t stream) {
   const bool big = impl > 0 && d->K % 64 == 0 && d->M >= 256 && d->N >= 256 &&
                    big_tiles * a.ksplit >= (a.ksplit > 1 ? 256 : 512) &&
                    (d->a_t == 0 || d->M % 8 == 0) && (d->b_t == 0 || d->N % 8 == 0);
+  // one-wave-per-SIMD kernel (gemm4w.hip): every plain product (no triangle, no split contraction index)
+  if (g4w_enabled() && d->tri == 0 && d->K % 64 == 0 && (d->a_t == 0 || d->M % 8 == 0) &&
+      (d->b_t == 0 || d->N % 8 == 0) && d->K / a.ksplit >= 64) {
+    e = gemm4w_launch(&a, d->a_t, d->b_t, d->out_f32, batch, stream);
+    if (e == hipSuccess && d->out_f32 && a.ksplit > 1) {
+      const long long mn = (long long)a.M * a.N;
+      hipLaunchKernelGGL(splitk_reduce_kernel, dim3(2048), dim3(256), 0, stream, reinterpret_cast<float*>(a.C), a.ws,
+                         mn, a.ldc, a.N, a.ksplit, a.beta);
+      e = hipGetLastError();
+    }
+    ++g_4w_calls;
+    return e == hipSuccess ? 0 : (int)e;
+  }
   // persistent phase kernel: plain products on whole 256x256 tiles, at least two tiles per CU (OBST_GEMM_PP=0: off)
   static int pp_env = -1;
   if (pp_env < 0) {

@@ -1,0 +1,4 @@
+// gemm4w kernels for A_T = 1, B_T = 0 (kernel: gemm4w.h)
+#include "gemm4w.h"
+
+OBST_GEMM4W_TU(1, 0)

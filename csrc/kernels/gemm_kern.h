@@ -96,7 +96,50 @@ __device__ __forceinline__ void stage_piece(char* img, const bf16_t* X, long lon
 }
 
 
+// fused epilogue of one lane's 4 consecutive outputs C[m][n..n+3] at element index idx (layout of C)
+template <bool OUT_F32>
+__device__ __forceinline__ void epilogue_store(const GemmArgs& p, long long idx, float (&v)[4]) {
+  if (OUT_F32) {
+    float* C = reinterpret_cast<float*>(p.C) + idx;
+    if (p.beta != 0.f) {
+      float4 o = *reinterpret_cast<const float4*>(C);
+      v[0] += p.beta * o.x; v[1] += p.beta * o.y; v[2] += p.beta * o.z; v[3] += p.beta * o.w;
+    }
+    if (p.R) {
+      float4 r = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(p.R) + idx);
+      v[0] += r.x; v[1] += r.y; v[2] += r.z; v[3] += r.w;
+    }
+    if (p.act) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) v[t] = act_fwd(p.act, v[t]);
+    }
+    *reinterpret_cast<float4*>(C) = make_float4(v[0], v[1], v[2], v[3]);
+  } else {
+    if (p.R) {
+      uint2 r = *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16_t*>(p.R) + idx);
+      v[0] += bf2f(r.x & 0xffff); v[1] += bf2f(r.x >> 16); v[2] += bf2f(r.y & 0xffff); v[3] += bf2f(r.y >> 16);
+    }
+    if (p.mode == 1) {
+      uint2 z = *reinterpret_cast<const uint2*>(p.Zin + idx);
+      v[0] *= act_grad(p.act, bf2f(z.x & 0xffff)); v[1] *= act_grad(p.act, bf2f(z.x >> 16));
+      v[2] *= act_grad(p.act, bf2f(z.y & 0xffff)); v[3] *= act_grad(p.act, bf2f(z.y >> 16));
+    } else {
+      if (p.Zout) {
+        *reinterpret_cast<uint2*>(p.Zout + idx) = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+      }
+      if (p.act) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) v[t] = act_fwd(p.act, v[t]);
+      }
+    }
+    *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.C) + idx) =
+        make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+  }
+}
+
 }  // namespace
 
 // the persistent phase kernel (gemm_pp.hip) for a GemmArgs filled by obst_gemm: plain products on whole tiles
 hipError_t gemm_pp_launch(const gemmk::GemmArgs* a, int a_t, int b_t, int out_f32, int batch, hipStream_t stream);
+// the one-wave-per-SIMD 256x256 kernel (gemm4w.hip) for a GemmArgs filled by obst_gemm (ksplit / ws set)
+hipError_t gemm4w_launch(const gemmk::GemmArgs* a, int a_t, int b_t, int out_f32, int batch, hipStream_t stream);

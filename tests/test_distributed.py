@@ -30,9 +30,9 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _batch():
+def _batch(cfg=CFG):
     g = torch.Generator().manual_seed(7)
-    toks = torch.randint(0, 64, (4, 17, 1), generator=g)
+    toks = torch.randint(0, cfg["vocab_size"], (cfg["train_batch_size"], cfg["sequence_length"] + 1, 1), generator=g)
     return {"token_x": toks[:, :-1].contiguous(), "token_y": toks[:, 1:].contiguous()}
 
 
@@ -40,14 +40,14 @@ def _worker(rank, world, port, cfg, mode, out_dir):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.manual_seed(0)
-    dp, tp = (world, 1) if mode == "dp" else (1, world)
+    dp, tp = (world, 1) if mode == "dp" else (1, world) if mode == "tp" else mode
     mesh = pstate.Mesh(dp=dp, tp=tp, rank=rank).build_groups()
     p = ModelParameter(dict(cfg, mesh={"dp": dp, "tp": tp}))
     tr = Trainer(p, "cpu", mesh)
-    b = _batch()
-    if mode == "dp":
-        n = 4 // world
-        b = {k: v[rank * n:(rank + 1) * n] for k, v in b.items()}
+    b = _batch(cfg)
+    if dp > 1:   # each DP replica (a TP group of contiguous ranks) takes its slice of the global batch
+        n = b["token_x"].shape[0] // dp
+        b = {k: v[mesh.dp_rank * n:(mesh.dp_rank + 1) * n] for k, v in b.items()}
     losses = []
     for _ in range(2):
         m = tr.step(b)
@@ -63,15 +63,26 @@ def _single(cfg):
     pstate.set_mesh(pstate.Mesh())
     torch.manual_seed(0)
     tr = Trainer(ModelParameter(dict(cfg)), "cpu")
-    b = _batch()
+    b = _batch(cfg)
     losses = [float(tr.step(b)["loss"]) for _ in range(2)]
     return tr, losses
 
 
-def _run(mode, cfg=CFG):
+def _run(mode, cfg=CFG, world=2):
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(2, _free_port(), cfg, mode, d), nprocs=2, join=True)
-        return [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True) for r in range(2)]
+        mp.spawn(_worker, args=(world, _free_port(), cfg, mode, d), nprocs=world, join=True)
+        return [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True) for r in range(world)]
+
+
+def _gather_tp(ranks, name, full_shape, tp):
+    """the full tensor `name` from the TP shards held by ranks[0:tp] (one DP replica)"""
+    off, n, tp_dim = ranks[0]["specs"][name]
+    if tp_dim is None:
+        return ranks[0]["master"][off:off + n].view(full_shape)
+    shp = list(full_shape)
+    shp[tp_dim] //= tp
+    parts = [r["master"][r["specs"][name][0]:r["specs"][name][0] + r["specs"][name][1]].view(shp) for r in ranks[:tp]]
+    return torch.cat(parts, tp_dim)
 
 
 def test_dp_matches_single_rank():
@@ -137,3 +148,52 @@ def test_collective_sequence_check():
     for r in res:
         assert r["n_ok"] == 0, "verify() at the end of the step resets the sequence"
         assert "diverged" in r["err"]
+
+
+# ctx32_mixer's own block at toy size: grouped norms, bottleneck_group_linear with mid: extras, the depth-shared
+# learned token mixer with input_as_value, gelu, RevNet, the SM3 chain (configs/ctx32_mixer.json)
+MIXER_CFG = dict(model_mode="gpt", use_video=False, use_language=True, heads=4, features_per_head=8, depth=2,
+                 sequence_length=16, train_batch_size=4, vocab_size=32, group_linear_factor=2,
+                 intermediate_feed_forward_multiplier=1, memory_reduction_strategy="revnet",
+                 calculation_dtype="float32", learning_rate=0.01,
+                 optimizer="adaptive_clip:0.003-sm3-momentum:0.9:1:1-learning_rate",
+                 block_config=[{"layer": ["norm-shift-scale-features-group",
+                                          "bottleneck_group_linear-in:relu-mid:relu-mid:norm-mid:shift-mid:scale-mid:features"]},
+                               {"layer": ["norm-shift-scale-features-group",
+                                          "attention-biased_attention_map-absolute-input_as_value-shared",
+                                          "norm-shift-scale-features-group", "activation-gelu",
+                                          "attention-biased_attention_map-absolute-input_as_value-shared"]}])
+
+
+@pytest.mark.parametrize("cfg", [CFG, MIXER_CFG], ids=["gpt", "ctx32_mixer_block"])
+def test_dp2_tp2_mesh_matches_single_rank(cfg):
+    """the reference's 2-D batch x heads mesh (src/dataclass.py:247-252) as DP=2 x TP=2 over 4 gloo ranks: the
+    losses of both replicas average to the single-rank loss, TP pairs agree, the replicas stay identical and every
+    weight (gathered over its TP shards) matches the single-rank step"""
+    ranks = _run((2, 2), cfg, world=4)
+    ref, ref_losses = _single(cfg)
+    for step in range(2):
+        for r in (0, 2):   # TP partners report the same loss
+            assert abs(ranks[r]["losses"][step] - ranks[r + 1]["losses"][step]) < 1e-6
+        mean = (ranks[0]["losses"][step] + ranks[2]["losses"][step]) / 2
+        assert abs(mean - ref_losses[step]) < 1e-4, f"step {step}: DPxTP loss {mean} vs single {ref_losses[step]}"
+    for r in (0, 1):   # DP replicas hold identical shards
+        assert torch.allclose(ranks[r]["master"], ranks[r + 2]["master"]), "DP replicas diverged"
+    for name in ranks[0]["specs"]:
+        full = ref.store.master_view(name)
+        got = _gather_tp(ranks, name, full.shape, 2)
+        diff = (got - full).abs().max().item()
+        assert diff < 5e-5, f"DPxTP weight {name} differs by {diff}"
+
+
+def test_tp_mixer_block_matches_single_rank():
+    """TP=2 on the ctx32_mixer block (group norms and the token mixer are head-local, the bottleneck's dense in
+    projection all-reduces over heads, SM3's accumulators reduce with MAX over TP)"""
+    ranks = _run("tp", MIXER_CFG)
+    ref, ref_losses = _single(MIXER_CFG)
+    for a, b in zip(ranks[0]["losses"], ref_losses):
+        assert abs(a - b) < 1e-4, f"TP loss {a} vs single {b}"
+    for name in ranks[0]["specs"]:
+        full = ref.store.master_view(name)
+        diff = (_gather_tp(ranks, name, full.shape, 2) - full).abs().max().item()
+        assert diff < 5e-5, f"TP weight {name} differs by {diff}"
