@@ -449,6 +449,9 @@ OBST_API int obst_gemm4w_set(int on) {
   return old;
 }
 OBST_API long long obst_gemm4w_calls() { return g_4w_calls; }
+// diagnostics: device buffer of 5 u64 per block (gemm4w.h) filled by the following gemm4w launches; null: off
+static unsigned long long* g_4w_stamps = nullptr;
+OBST_API void obst_gemm4w_stamps(unsigned long long* dev) { g_4w_stamps = dev; }
 
 static int getenv_big() {   // OBST_GEMM_BIG=0: only the 128x128 kernel (A/B, debugging)
   static int v = -1;
@@ -483,6 +486,7 @@ OBST_API int obst_gemm(const ObstGemmDesc* d, hipStream_t stream) {
   a.tiles_m = (d->M + BM - 1) / BM; a.tiles_n = (d->N + BN - 1) / BN;
   a.alpha = d->alpha; a.beta = d->beta; a.act = d->act; a.mode = d->mode; a.tri = d->tri;
   a.kin = d->kin; a.a_sk = d->a_sk; a.b_sk = d->b_sk;
+  a.stamps = g_4w_stamps;
   if (d->kin) {   // split contraction index: phase kernel, K-contiguous operands, whole 64-deep tiles per inner block
     if (d->kin < 0 || d->kin % 64 || d->K % d->kin || d->a_t || d->b_t || (d->tri == 1 || d->tri == 2) ||
         d->a_sk % 8 || d->b_sk % 8 || d->M < 256 || d->N < 256)

@@ -59,7 +59,7 @@ __device__ __forceinline__ i32x4_t make_rsrc(const void* base) {
 // drains it with a vmcnt(0) before later LDS reads nor reorders it: every consumer waits with an explicit counted
 // vmcnt before the barrier that publishes the stage.
 __device__ __forceinline__ void dma16(const i32x4_t& rs, int voff, unsigned m0) {
-  asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rs),
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rs),
                "s"(__builtin_amdgcn_readfirstlane(m0))
                : "memory", "m0");
 }
@@ -73,6 +73,8 @@ __device__ __forceinline__ void mfma_acc(f32x4_t& c, const bf16x8_t& a, const bf
 #pragma clang diagnostic pop
 
 __device__ __forceinline__ void fence() { __builtin_amdgcn_sched_barrier(0); }
+// makes c an asm-produced AGPR value (no later rematerialisation of what it was computed from)
+__device__ __forceinline__ void agpr_opaque(f32x4_t& c) { asm volatile("" : "+a"(c)); }
 
 // compile-time loop: f(std::integral_constant<int, 0>) ... f(<N-1>) -- the K-loop body is 128 MFMA slots, past
 // what #pragma unroll expands, and every register array must stay statically indexed
@@ -184,10 +186,24 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs p) {
     else if constexpr (r < 9) af[r - 1] = frag<A_T>(ia, wm * 128 + (r - 1) * 16, kk, lane);
     else bf[r - 8] = frag<B_T>(ib, wn * 128 + (r - 8) * 16, kk, lane);
   };
-  asm volatile("s_nop 4" ::: "memory");   // accumulator zeroing (VALU) -> first MFMA reading it
+  // Accumulator zeroing (VALU writes of AGPRs) -> first MFMA reading them needs wait states the compiler cannot
+  // see through the asm MFMAs. The zero constants would otherwise be rematerialised right in front of the loop,
+  // past any pad: an empty "+a" asm per accumulator makes each a materialised value before the pad.
+  static_for<64>([&](auto c) { agpr_opaque(acc[decltype(c)::value >> 3][decltype(c)::value & 7]); });
+  asm volatile("s_nop 4" ::: "memory");
+  fence();
   using K0 = std::integral_constant<int, 0>;
   using K1 = std::integral_constant<int, 1>;
 
+  // diagnostic timestamps (GemmArgs::stamps, null in production): per block [start, first tile landed, loop done,
+  // epilogue done] in shader clocks, the XCC id, [start, end] in 100 MHz real time
+  const bool stamp = p.stamps != nullptr && tid == 0;
+  const long long sbase = ((long long)blockIdx.y * gridDim.x + blockIdx.x) * 8;
+  if (stamp) {
+    p.stamps[sbase] = __builtin_amdgcn_s_memtime();
+    p.stamps[sbase + 4] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11));   // HW_REG_XCC_ID[3:0]
+    p.stamps[sbase + 5] = __builtin_amdgcn_s_memrealtime();
+  }
   // prologue: tiles 0 and 1 into stages 0 and 1, wait for tile 0, read its substep-0 fragments
 #pragma unroll
   for (int q = 0; q < 8; ++q) dma_a(0, 0, q);
@@ -200,6 +216,7 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs p) {
   vm_wait<16>();
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_s_waitcnt(0xc07f);   // nothing (kernel-argument loads) pending in lgkmcnt at the loop entry
+  if (stamp) p.stamps[sbase + 1] = __builtin_amdgcn_s_memtime();
   fence();
   static_for<16>([&](auto rc) { read_sub(0, K0{}, rc, a0, b0); fence(); });   // same order as in the loop
   fence();
@@ -226,25 +243,56 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs p) {
       fence();
     });
   }
-  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");   // last MFMA -> accumulator reads
-  vm_wait<0>();   // the over-range prefetches of the last two iterations must land before the LDS is released
+  fence();
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");   // last MFMA -> accumulator reads: the
+  fence();                                                          // fences keep the reads below the pad
+  vm_wait<0>();   // the over-range prefetches of the last two iterations must land before the LDS is reused
+  if (stamp) p.stamps[sbase + 2] = __builtin_amdgcn_s_memtime();
+  __builtin_amdgcn_s_barrier();   // ... by every wave: the epilogue below overwrites both stages
+  fence();
 
+  // Epilogue through LDS: per wave 4 rounds of 32 rows x 128 columns (fp32, rows padded to 132 floats:
+  // conflict-free 16-byte fragment writes). Each round the wave writes two accumulator rows of fragments, then a
+  // compact runtime loop reads 8 consecutive outputs per lane and applies epilogue_store8 with 16-byte global
+  // accesses (a fully unrolled per-fragment epilogue inlined the activation switch 64 times: ~12k branches,
+  // instruction-cache bound, as long as the K loop itself at K = 2048).
+  constexpr int EP_LD = 132;
+  float* ep = reinterpret_cast<float*>(smem) + wave * (32 * EP_LD);
   const long long coff = b1 * p.c_s1 + b2 * p.c_s2;
-  static_for<64>([&](auto qc) {
-    constexpr int i = decltype(qc)::value >> 3, j = decltype(qc)::value & 7;
-    const int m = m0 + wm * 128 + i * 16 + (lane & 15);
-    const int n = n0 + wn * 128 + j * 16 + 4 * (lane >> 4);
-    float v[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) v[u] = p.alpha * acc[i][j][u];
-    if (m < p.M && n < p.N) {
-      if (OUT_F32 && p.ksplit > 1)
-        *reinterpret_cast<float4*>(p.ws + (long long)split * p.M * p.N + (long long)m * p.N + n) =
-            make_float4(v[0], v[1], v[2], v[3]);
-      else
-        epilogue_store<OUT_F32>(p, coff + (long long)m * p.ldc + n, v);
+  const float alpha = p.alpha;
+  static_for<4>([&](auto rc) {
+    constexpr int r = decltype(rc)::value;
+    static_for<16>([&](auto fc) {
+      constexpr int f = decltype(fc)::value, i = 2 * r + (f >> 3), j = f & 7;
+      const int row = (f >> 3) * 16 + (lane & 15), col = j * 16 + 4 * (lane >> 4);
+      *reinterpret_cast<float4*>(ep + row * EP_LD + col) =
+          make_float4(alpha * acc[i][j][0], alpha * acc[i][j][1], alpha * acc[i][j][2], alpha * acc[i][j][3]);
+    });
+#pragma unroll 1
+    for (int it = 0; it < 8; ++it) {
+      const int row = it * 4 + (lane >> 4), col = (lane & 15) * 8;
+      const float4 x0 = *reinterpret_cast<const float4*>(ep + row * EP_LD + col);
+      const float4 x1 = *reinterpret_cast<const float4*>(ep + row * EP_LD + col + 4);
+      float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+      const int m = m0 + wm * 128 + r * 32 + row, n = n0 + wn * 128 + col;
+      if (m < p.M && n < p.N) {
+        if (OUT_F32 && p.ksplit > 1) {
+          float4* w = reinterpret_cast<float4*>(p.ws + (long long)split * p.M * p.N + (long long)m * p.N + n);
+          w[0] = x0;
+          w[1] = x1;
+        } else {
+          epilogue_store8<OUT_F32>(p, coff + (long long)m * p.ldc + n, v);
+        }
+      }
     }
   });
+  if (p.stamps != nullptr) {
+    __syncthreads();
+    if (stamp) {
+      p.stamps[sbase + 3] = __builtin_amdgcn_s_memtime();
+      p.stamps[sbase + 6] = __builtin_amdgcn_s_memrealtime();
+    }
+  }
 }
 
 template <int A_T, int B_T, bool F32>

@@ -22,6 +22,7 @@ struct GemmArgs {
   int kin;                // phase kernel only: split contraction index, see ObstGemmDesc (0: plain K)
   long long a_sk, b_sk;
   int nbatch;             // persistent phase kernel: batches (the grid is one block per CU)
+  unsigned long long* stamps;   // gemm4w diagnostics: per-block timestamps (null: off)
 };
 }  // namespace gemmk
 
@@ -134,6 +135,56 @@ __device__ __forceinline__ void epilogue_store(const GemmArgs& p, long long idx,
     }
     *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.C) + idx) =
         make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+  }
+}
+
+// the same epilogue for 8 consecutive outputs C[m][n..n+7] (16-byte loads / stores; n % 8 == 0, idx % 8 == 0)
+template <bool OUT_F32>
+__device__ __forceinline__ void epilogue_store8(const GemmArgs& p, long long idx, float (&v)[8]) {
+  if (OUT_F32) {
+    float* C = reinterpret_cast<float*>(p.C) + idx;
+    if (p.beta != 0.f) {
+      const float4 o0 = reinterpret_cast<const float4*>(C)[0], o1 = reinterpret_cast<const float4*>(C)[1];
+      v[0] += p.beta * o0.x; v[1] += p.beta * o0.y; v[2] += p.beta * o0.z; v[3] += p.beta * o0.w;
+      v[4] += p.beta * o1.x; v[5] += p.beta * o1.y; v[6] += p.beta * o1.z; v[7] += p.beta * o1.w;
+    }
+    if (p.R) {
+      const float4* R = reinterpret_cast<const float4*>(reinterpret_cast<const float*>(p.R) + idx);
+      const float4 r0 = R[0], r1 = R[1];
+      v[0] += r0.x; v[1] += r0.y; v[2] += r0.z; v[3] += r0.w; v[4] += r1.x; v[5] += r1.y; v[6] += r1.z; v[7] += r1.w;
+    }
+    if (p.act) {
+#pragma unroll
+      for (int t = 0; t < 8; ++t) v[t] = act_fwd(p.act, v[t]);
+    }
+    reinterpret_cast<float4*>(C)[0] = make_float4(v[0], v[1], v[2], v[3]);
+    reinterpret_cast<float4*>(C)[1] = make_float4(v[4], v[5], v[6], v[7]);
+  } else {
+    if (p.R) {
+      const uint4 r = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(p.R) + idx);
+      const uint32_t rw[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+      for (int t = 0; t < 4; ++t) { v[2 * t] += bf2f(rw[t] & 0xffff); v[2 * t + 1] += bf2f(rw[t] >> 16); }
+    }
+    if (p.mode == 1) {
+      const uint4 z = *reinterpret_cast<const uint4*>(p.Zin + idx);
+      const uint32_t zw[4] = {z.x, z.y, z.z, z.w};
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        v[2 * t] *= act_grad(p.act, bf2f(zw[t] & 0xffff));
+        v[2 * t + 1] *= act_grad(p.act, bf2f(zw[t] >> 16));
+      }
+    } else {
+      if (p.Zout)
+        *reinterpret_cast<uint4*>(p.Zout + idx) = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]),
+                                                             pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7]));
+      if (p.act) {
+#pragma unroll
+        for (int t = 0; t < 8; ++t) v[t] = act_fwd(p.act, v[t]);
+      }
+    }
+    *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(p.C) + idx) =
+        make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7]));
   }
 }
 

@@ -21,6 +21,7 @@ extern "C" int obst_gemm(const ObstGemmDesc* d, hipStream_t stream);
 extern "C" int obst_blaslt_set(int on);
 extern "C" int obst_gemm4w_set(int on);
 extern "C" long long obst_gemm4w_calls();
+extern "C" void obst_gemm4w_stamps(unsigned long long* dev);
 
 #define CK(x)                                                                    \
   do {                                                                           \
@@ -75,9 +76,9 @@ static int run(const Shape& s, const void* A, const void* B, void* C, int mode, 
   return obst_gemm(&d, st);
 }
 
-static void host_check(hipStream_t st) {
+static void host_check(hipStream_t st, int K) {
   // fp32 CPU reference of every layout at a small ragged shape, both output types, all three paths
-  const int M = 520, N = 264, K = 192;
+  const int M = 520, N = 264;
   std::vector<uint16_t> ha((size_t)M * K), hb((size_t)N * K);
   for (size_t i = 0; i < ha.size(); ++i) ha[i] = f2bf((float)((i * 7919 % 2003) / 1001.5 - 1.0));
   for (size_t i = 0; i < hb.size(); ++i) hb[i] = f2bf((float)((i * 104729 % 1999) / 999.5 - 1.0));
@@ -122,7 +123,8 @@ static void host_check(hipStream_t st) {
             maxe = e > maxe ? e : maxe;
             if (e > 0.05 + 0.01 * fabs(ref[i])) ++bad;
           }
-          printf("check a_t=%d b_t=%d f32=%d mode=%d rc=%d: %zu bad, max err %.4g\n", at, bt, f32, mode, r, bad, maxe);
+          printf("check K=%d a_t=%d b_t=%d f32=%d mode=%d rc=%d: %zu bad, max err %.4g\n", K, at, bt, f32, mode, r, bad,
+                 maxe);
         }
       }
   CK(hipFree(dA));
@@ -137,7 +139,8 @@ int main(int argc, char** argv) {
   const char* filt = argc > 3 ? argv[3] : "";
   hipStream_t st;
   CK(hipStreamCreate(&st));
-  if (!getenv("SKIP_CHECK")) host_check(st);
+  if (!getenv("SKIP_CHECK"))
+    for (int K : {64, 192, 576}) host_check(st, K);
   const Shape shapes[] = {
       {131072, 4096, 2048, 0, 0, 0, "fwd d->2d (qkv/ffn-in)"},
       {131072, 2048, 4096, 0, 0, 0, "fwd 2d->d / dgrad"},
@@ -219,6 +222,37 @@ int main(int argc, char** argv) {
         sum[mode] += t;
       }
     const double fl = 2.0 * s.M * s.N * (double)s.K;
+    if (getenv("STAMPS")) {   // per-block phase breakdown of one gemm4w launch (shader clocks / real time)
+      const long long nblk = (long long)((s.M + 255) / 256) * ((s.N + 255) / 256) * 2;   // upper bound incl. split-K
+      unsigned long long* ds;
+      CK(hipMalloc(&ds, nblk * 64));
+      CK(hipMemset(ds, 0, nblk * 64));
+      obst_gemm4w_stamps(ds);
+      run(s, A, B, C1, 2, st);
+      CK(hipStreamSynchronize(st));
+      obst_gemm4w_stamps(nullptr);
+      std::vector<unsigned long long> h(nblk * 8);
+      CK(hipMemcpy(h.data(), ds, nblk * 64, hipMemcpyDeviceToHost));
+      double pro = 0, loop = 0, epi = 0, span_rt = 0;
+      unsigned long long rt_min = ~0ull, rt_max = 0;
+      long long nb = 0;
+      for (long long b = 0; b < nblk; ++b) {
+        const unsigned long long* t = &h[b * 8];
+        if (!t[0] || !t[3]) continue;
+        ++nb;
+        pro += (double)(t[1] - t[0]);
+        loop += (double)(t[2] - t[1]);
+        epi += (double)(t[3] - t[2]);
+        span_rt += (double)(t[6] - t[5]);
+        rt_min = t[5] < rt_min ? t[5] : rt_min;
+        rt_max = t[6] > rt_max ? t[6] : rt_max;
+      }
+      printf("%-58s stamps: %lld blocks, mean clocks prologue %.0f loop %.0f epilogue %.0f; mean block %.2f us, "
+             "launch span %.1f us, sum(block)/(256*span) %.3f\n",
+             name, nb, pro / nb, loop / nb, epi / nb, span_rt / nb / 100.0, (rt_max - rt_min) / 100.0,
+             span_rt / 256.0 / (double)(rt_max - rt_min));
+      CK(hipFree(ds));
+    }
     printf("%-58s TF/s best (mean): hipBLASLt %.0f (%.0f)  phase %.0f (%.0f)  4w %.0f (%.0f)   4w/lt %.3f\n", name,
            fl / best[0] / 1e9, fl / (sum[0] / rounds) / 1e9, fl / best[1] / 1e9, fl / (sum[1] / rounds) / 1e9,
            fl / best[2] / 1e9, fl / (sum[2] / rounds) / 1e9, best[0] / best[2]);
