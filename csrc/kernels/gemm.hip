@@ -528,7 +528,27 @@ OBST_API int obst_gemm(const ObstGemmDesc* d, hipStream_t stream) {
                    (d->a_t == 0 || d->M % 8 == 0) && (d->b_t == 0 || d->N % 8 == 0);
   // one-wave-per-SIMD kernel (gemm4w.hip): every plain product (no triangle, no split contraction index)
   if (g4w_enabled() && d->tri == 0 && d->K % 64 == 0 && (d->a_t == 0 || d->M % 8 == 0) &&
-      (d->b_t == 0 || d->N % 8 == 0) && d->K / a.ksplit >= 64) {
+      (d->b_t == 0 || d->N % 8 == 0)) {
+    // split-K for fp32 products with few output tiles (the weight gradients): the persistent kernel runs
+    // ceil(tiles * ks / 256) rounds of K / ks each; a split costs a deterministic fold over ks fp32 slabs. Pick the
+    // ks of least modelled time (1.25 us per 64-deep K-tile of a tile, ~5 TB/s for the fold), workspace <= 1 GiB.
+    int ks = 1;
+    if (ksplit_env > 0 && big_tiles < 512 && d->out_f32 && !d->R && !d->act && d->mode == 0 && batch == 1) {
+      const double per_k = 1.25 / 64.0;   // us per K element of one tile
+      double best = 1e300;
+      for (int c = 1; c <= 8; c *= 2) {
+        if (d->K % (64 * c) || (c > 1 && d->K / c < 512) || (size_t)c * d->M * d->N * 4 > (1ull << 30)) continue;
+        const double rounds = (double)((big_tiles * c + 255) / 256);
+        const double t = rounds * (d->K / c) * per_k +
+                         (c > 1 ? (double)(c + (d->beta != 0.f ? 2 : 1)) * d->M * d->N * 4.0 / 5e6 : 0.0);
+        if (t < best * 0.98) { best = t; ks = c; }
+      }
+      if (ks > 1) {
+        a.ws = splitk_workspace((size_t)ks * d->M * d->N * sizeof(float));
+        if (!a.ws) ks = 1;
+      }
+    }
+    a.ksplit = ks;
     e = gemm4w_launch(&a, d->a_t, d->b_t, d->out_f32, batch, stream);
     if (e == hipSuccess && d->out_f32 && a.ksplit > 1) {
       const long long mn = (long long)a.M * a.N;

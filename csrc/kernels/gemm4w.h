@@ -34,6 +34,8 @@
 namespace {
 
 typedef __attribute__((ext_vector_type(4))) int i32x4_t;
+typedef __attribute__((ext_vector_type(4))) unsigned v4u32_t;
+typedef __attribute__((ext_vector_type(2))) unsigned v2u32_t;
 
 constexpr int Q_OP = 256 * 64 * 2;   // one operand image of a K-tile: 32 KiB
 constexpr int Q_STAGE = 2 * Q_OP;    // A + B: 64 KiB; two stages
@@ -42,22 +44,29 @@ __device__ __forceinline__ unsigned lds_u32(const void* p) {
   return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
 }
 
-// raw buffer resource over [base, base + 4 GiB): stride 0, no range check beyond num_records = 0xffffffff
-__device__ __forceinline__ i32x4_t make_rsrc(const void* base) {
+// raw buffer resource over [base, base + nbytes): stride 0; loads at offsets >= nbytes return zeros (edge tiles)
+__device__ __forceinline__ i32x4_t make_rsrc(const void* base, long long nbytes) {
   const unsigned long long a = (unsigned long long)base;
   i32x4_t r;
   r[0] = __builtin_amdgcn_readfirstlane((int)(unsigned)a);
   r[1] = __builtin_amdgcn_readfirstlane((int)(unsigned)(a >> 32));
-  r[2] = -1;
+  r[2] = __builtin_amdgcn_readfirstlane(
+      (int)(unsigned)(nbytes <= 0 ? 0ull : nbytes >= 0xffffffffll ? 0xffffffffull : (unsigned long long)nbytes));
   r[3] = 0x00020000;
   return r;
+}
+
+// the same resource as the compiler's buffer type (epilogue loads / stores through the raw_buffer builtins)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_brsrc(const void* base, long long nbytes) {
+  const int n = (int)(unsigned)(nbytes <= 0 ? 0ull : nbytes >= 0xffffffffll ? 0xffffffffull : (unsigned long long)nbytes);
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, n, 0x00020000);
 }
 
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Winline-asm"
 // LDS-DMA of 16 B per lane into the 1 KiB at LDS address m0 (lane-linear). In inline asm so the compiler neither
 // drains it with a vmcnt(0) before later LDS reads nor reorders it: every consumer waits with an explicit counted
-// vmcnt before the barrier that publishes the stage.
+// vmcnt before the barrier that publishes the stage. One wait state between the M0 write and the LDS-DMA.
 __device__ __forceinline__ void dma16(const i32x4_t& rs, int voff, unsigned m0) {
   asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rs),
                "s"(__builtin_amdgcn_readfirstlane(m0))
@@ -66,15 +75,36 @@ __device__ __forceinline__ void dma16(const i32x4_t& rs, int voff, unsigned m0) 
 // C += A.B on one 16x16x32 bf16 tile, accumulator pinned to AGPRs: as a builtin, the register allocator re-assigned
 // the 64 loop-carried accumulators every iteration and copied them back through VGPRs at the back edge (512
 // registers, spills); a tied "+a" operand keeps each one in place. Hazards the compiler cannot see inside the asm
-// are padded by hand where the accumulators are initialised and read back (s_nop before / after the K loop).
+// are padded by hand where the accumulators are initialised and read back (s_nop, fenced).
 __device__ __forceinline__ void mfma_acc(f32x4_t& c, const bf16x8_t& a, const bf16x8_t& b) {
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
+}
+// 16-byte buffer store of v at voff + soff + IMM with two wait states behind it. A store of more than 8 bytes
+// reads its data VGPRs after issue; the compiler pads the VALU overwrite of them only when soffset is a constant
+// (its rule exempts an SGPR soffset), and on gfx950 the unpadded SGPR-soffset stores wrote corrupted data (1 of the
+// 64 fp32 fragments per wave, measured). In asm the pad travels with the store.
+template <int IMM>
+__device__ __forceinline__ void store16_padded(const f32x4_t& v, int voff, const i32x4_t& rs, int soff,
+                                               std::integral_constant<int, IMM>) {
+  asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen offset:%4\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(rs),
+               "s"(soff), "n"(IMM)
+               : "memory");
 }
 #pragma clang diagnostic pop
 
 __device__ __forceinline__ void fence() { __builtin_amdgcn_sched_barrier(0); }
 // makes c an asm-produced AGPR value (no later rematerialisation of what it was computed from)
 __device__ __forceinline__ void agpr_opaque(f32x4_t& c) { asm volatile("" : "+a"(c)); }
+
+// 24 wait states after the last MFMA, then every accumulator redefined by asm (8 per statement, in order)
+__device__ __forceinline__ void pad_redefine(f32x4_t (&acc)[8][8]) {
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" : "+a"(acc[0][0]), "+a"(acc[0][1]), "+a"(acc[0][2]), "+a"(acc[0][3]),
+               "+a"(acc[0][4]), "+a"(acc[0][5]), "+a"(acc[0][6]), "+a"(acc[0][7]));
+#pragma unroll
+  for (int i = 1; i < 8; ++i)
+    asm volatile("" : "+a"(acc[i][0]), "+a"(acc[i][1]), "+a"(acc[i][2]), "+a"(acc[i][3]), "+a"(acc[i][4]),
+                 "+a"(acc[i][5]), "+a"(acc[i][6]), "+a"(acc[i][7]));
+}
 
 // compile-time loop: f(std::integral_constant<int, 0>) ... f(<N-1>) -- the K-loop body is 128 MFMA slots, past
 // what #pragma unroll expands, and every register array must stay statically indexed
@@ -87,93 +117,126 @@ __device__ __forceinline__ void static_for(F&& f) {
   static_for_impl(f, std::make_integer_sequence<int, N>{});
 }
 
-// per-lane source offsets (bytes, relative to the tile's K-tile base) of the 8 LDS-DMA pieces this wave stages
-// for one operand. T = 0: [rows][K] operand, piece P = 8 rows; T = 1: [K][rows] operand, piece P = 4 k-rows x 128
-// columns of half P >> 4. Rows / columns past the operand's edge are clamped (their results are never stored).
+// per-lane source offsets (bytes, relative to a K-tile's base) of the 8 LDS-DMA pieces this wave stages for one
+// operand -- the same for every tile (edges are handled by the resource's num_records). T = 0: [rows][K] operand,
+// piece P = 8 rows of 128 B; T = 1: [K][rows] operand, piece P = 4 k-rows x 128 columns of half P >> 4.
 template <int T>
-__device__ __forceinline__ void piece_offsets(int (&vo)[8], long long ld, int r0, int R, int wave, int lane) {
+__device__ __forceinline__ void piece_offsets(int (&vo)[8], long long ld, int wave, int lane) {
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     const int P = wave * 8 + q;
     if (T == 0) {
       const int row = P * 8 + (lane >> 3);
       const int c = (lane & 7) ^ ((row >> 1) & 7);
-      const int rc = min(r0 + row, R - 1) - r0;
-      vo[q] = (int)(rc * ld * 2) + c * 16;
+      vo[q] = (int)(row * ld * 2) + c * 16;
     } else {
       const int h = P >> 4, kr = (P & 15) * 4 + (lane >> 4);
       const int c = (lane & 15) ^ kswz(kr);
-      const int col = min(r0 + h * 128 + c * 8, R - 8) - r0;
-      vo[q] = (int)(kr * ld * 2) + col * 2;
+      vo[q] = (int)(kr * ld * 2) + (h * 128 + c * 8) * 2;
     }
   }
 }
 
-// fragment j (16 rows/cols starting at rbase within the 256 of the tile) of k-substep kk from an operand image
+// fragment (16 rows/cols starting at rbase within the 256 of the tile) of k-substep kk from an operand image
 template <int T>
 __device__ __forceinline__ bf16x8_t frag(const char* img, int rbase, int kk, int lane) {
   if (T == 0) return read_frag<0>(img, rbase, kk, lane);
   return read_frag<1>(img + (rbase >> 7) * (Q_OP / 2), rbase & 127, kk, lane);
 }
 
+// one output tile of the launch: operand bases at its first K-tile, the bytes left in each operand from there
+// (the resource bound that zero-fills rows / columns past the edge), output origin
+struct Tile4 {
+  const char* a;
+  const char* b;
+  long long arem, brem;
+  long long coff;
+  int m0, n0, split;
+};
+
+template <int A_T, int B_T>
+__device__ __forceinline__ Tile4 decode4(const GemmArgs& p, long long L) {
+  const int ntile = p.tiles_m * p.tiles_n;
+  const int bid = (int)(L % ntile);
+  const long long ybat = L / ntile;
+  const int GROUP = 4;   // tile rows per N sweep: neighbouring CUs of an XCD share A panels and B panels
+  const int per_group = GROUP * p.tiles_n;
+  const int first_m = (bid / per_group) * GROUP;
+  const int gsz = min(p.tiles_m - first_m, GROUP);
+  Tile4 T;
+  const int tm = first_m + (bid % per_group) % gsz;
+  const int tn = (bid % per_group) / gsz;
+  T.m0 = tm * 256;
+  T.n0 = tn * 256;
+  T.split = (int)(ybat % p.ksplit);
+  const long long bidx = ybat / p.ksplit;
+  const long long b1 = bidx / p.nb2, b2 = bidx % p.nb2;
+  const long long kbeg = (long long)T.split * (p.K / p.ksplit);
+  const bf16_t* A = p.A + b1 * p.a_s1 + b2 * p.a_s2;
+  const bf16_t* B = p.B + b1 * p.b_s1 + b2 * p.b_s2;
+  // extent of each operand (elements from its batch base): [M][lda] rows / [K][lda] k-rows
+  const long long aext = A_T == 0 ? (long long)(p.M - 1) * p.lda + p.K : (long long)(p.K - 1) * p.lda + p.M;
+  const long long bext = B_T == 0 ? (long long)(p.N - 1) * p.ldb + p.K : (long long)(p.K - 1) * p.ldb + p.N;
+  const long long aoff = A_T == 0 ? (long long)T.m0 * p.lda + kbeg : kbeg * p.lda + T.m0;
+  const long long boff = B_T == 0 ? (long long)T.n0 * p.ldb + kbeg : kbeg * p.ldb + T.n0;
+  T.a = reinterpret_cast<const char*>(A + aoff);
+  T.b = reinterpret_cast<const char*>(B + boff);
+  T.arem = (aext - aoff) * 2;
+  T.brem = (bext - boff) * 2;
+  T.coff = b1 * p.c_s1 + b2 * p.c_s2;
+  return T;
+}
+
+// Persistent kernel: one block per CU walks its tiles; the LDS-DMA stream runs two K-tiles ahead of the MFMAs
+// ACROSS tile boundaries (positions of a flat (tile, K-tile) sequence), so the next tile's first two K-tiles are
+// in LDS when the current tile's epilogue is done, and its first fragments are read under the current tile's
+// last MFMAs. XCD x owns a contiguous run of logical tiles, dealt to its CUs in rounds.
 template <int A_T, int B_T, bool OUT_F32>
 __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs p) {
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
 
-  // XCD-aware remap over the whole grid (tiles x batches x K-splits), then GROUP = 4 tile rows per N sweep
-  int bid, ybat;
-  {
-    const int nx = gridDim.x;
-    const long long nwg = (long long)nx * gridDim.y, lin = (long long)blockIdx.y * nx + blockIdx.x;
-    const long long xcd = lin & 7, qq = nwg >> 3, r = nwg & 7;
-    const long long lg = (xcd < r ? xcd * (qq + 1) : r * (qq + 1) + (xcd - r) * qq) + (lin >> 3);
-    bid = (int)(lg % nx);
-    ybat = (int)(lg / nx);
-  }
-  const int GROUP = 4;
-  const int per_group = GROUP * p.tiles_n;
-  const int first_m = (bid / per_group) * GROUP;
-  const int gsz = min(p.tiles_m - first_m, GROUP);
-  const int tm = first_m + (bid % per_group) % gsz;
-  const int tn = (bid % per_group) / gsz;
-  const int m0 = tm * 256, n0 = tn * 256;
-  const int split = ybat % p.ksplit, bidx = ybat / p.ksplit;
-  const int b1 = bidx / p.nb2, b2 = bidx % p.nb2;
-  const int kspan = p.K / p.ksplit, kbeg = split * kspan;
-  const int nk = kspan / 64;
-
-  // K-tile bases: element pointer of (tile row/col 0, k = kbeg) and the per-K-tile step in bytes
-  const char* abase = reinterpret_cast<const char*>(
-      p.A + b1 * p.a_s1 + b2 * p.a_s2 + (A_T == 0 ? (long long)m0 * p.lda + kbeg : (long long)kbeg * p.lda + m0));
-  const char* bbase = reinterpret_cast<const char*>(
-      p.B + b1 * p.b_s1 + b2 * p.b_s2 + (B_T == 0 ? (long long)n0 * p.ldb + kbeg : (long long)kbeg * p.ldb + n0));
+  const long long total = (long long)p.tiles_m * p.tiles_n * p.nbatch;
+  const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3, nslot = gridDim.x >> 3;
+  const long long Q = total >> 3, Rm = total & 7;
+  const long long base = xcd < Rm ? xcd * (Q + 1) : Rm * (Q + 1) + (xcd - Rm) * Q;
+  const long long len = Q + (xcd < Rm ? 1 : 0);
+  const int ntiles = (int)(len > slot ? (len - slot + nslot - 1) / nslot : 0);   // tiles of this block
+  if (ntiles == 0) return;
+  auto logical = [&](int r) { return base + slot + (long long)r * nslot; };
+  const int nk = p.K / p.ksplit / 64;
   const long long astep = A_T == 0 ? 128 : 128 * p.lda;
   const long long bstep = B_T == 0 ? 128 : 128 * p.ldb;
 
   int voa[8], vob[8];
-  piece_offsets<A_T>(voa, p.lda, m0, p.M, wave, lane);
-  piece_offsets<B_T>(vob, p.ldb, n0, p.N, wave, lane);
+  piece_offsets<A_T>(voa, p.lda, wave, lane);
+  piece_offsets<B_T>(vob, p.ldb, wave, lane);
   const unsigned lds0 = lds_u32(smem);
   // this wave's 8 pieces of an operand image are contiguous: 8 KiB at (wave * 8 KiB)
   auto stage_a = [&](int s) -> unsigned { return lds0 + s * Q_STAGE + wave * 8192; };
   auto stage_b = [&](int s) -> unsigned { return lds0 + s * Q_STAGE + Q_OP + wave * 8192; };
 
-  auto dma_a = [&](int t, int s, int q) {
-    const int tc = min(t, nk - 1);
-    dma16(make_rsrc(abase + tc * astep), voa[q], stage_a(s) + q * 1024);
+  // DMA cursor: (tile round, K-tile) of the next position to stage; past the last tile it re-stages the last
+  // position into the stage nobody reads any more
+  int d_rnd = 0, d_kt = 0;
+  Tile4 dt = decode4<A_T, B_T>(p, logical(0));
+  i32x4_t ra, rb;
+  auto dma_setup = [&]() {   // resources of the cursor's K-tile
+    ra = make_rsrc(dt.a + d_kt * astep, dt.arem - d_kt * astep);
+    rb = make_rsrc(dt.b + d_kt * bstep, dt.brem - d_kt * bstep);
   };
-  auto dma_b = [&](int t, int s, int q) {
-    const int tc = min(t, nk - 1);
-    dma16(make_rsrc(bbase + tc * bstep), vob[q], stage_b(s) + q * 1024);
+  auto dma_advance = [&]() {
+    if (d_kt + 1 < nk) {
+      ++d_kt;
+    } else if (d_rnd + 1 < ntiles) {
+      ++d_rnd;
+      d_kt = 0;
+      dt = decode4<A_T, B_T>(p, logical(d_rnd));
+    }
   };
 
   f32x4_t acc[8][8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   bf16x8_t a0[8], b0[8], a1[8], b1f[8];
 
   // read order of a substep's 16 fragments: A0, B0, A1..A7, B1..B7 (the order the MFMA stream consumes them)
@@ -186,110 +249,197 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs p) {
     else if constexpr (r < 9) af[r - 1] = frag<A_T>(ia, wm * 128 + (r - 1) * 16, kk, lane);
     else bf[r - 8] = frag<B_T>(ib, wn * 128 + (r - 8) * 16, kk, lane);
   };
-  // Accumulator zeroing (VALU writes of AGPRs) -> first MFMA reading them needs wait states the compiler cannot
-  // see through the asm MFMAs. The zero constants would otherwise be rematerialised right in front of the loop,
-  // past any pad: an empty "+a" asm per accumulator makes each a materialised value before the pad.
-  static_for<64>([&](auto c) { agpr_opaque(acc[decltype(c)::value >> 3][decltype(c)::value & 7]); });
-  asm volatile("s_nop 4" ::: "memory");
-  fence();
   using K0 = std::integral_constant<int, 0>;
   using K1 = std::integral_constant<int, 1>;
 
-  // diagnostic timestamps (GemmArgs::stamps, null in production): per block [start, first tile landed, loop done,
-  // epilogue done] in shader clocks, the XCC id, [start, end] in 100 MHz real time
+  // diagnostic timestamps (GemmArgs::stamps, null in production): per block [start, first tile landed, summed
+  // loop clocks, summed epilogue clocks], the XCC id, [start, end] in 100 MHz real time, tiles
   const bool stamp = p.stamps != nullptr && tid == 0;
-  const long long sbase = ((long long)blockIdx.y * gridDim.x + blockIdx.x) * 8;
+  const long long sbase = (long long)blockIdx.x * 8;
+  unsigned long long loop_clk = 0, epi_clk = 0, tmark = 0;
   if (stamp) {
     p.stamps[sbase] = __builtin_amdgcn_s_memtime();
     p.stamps[sbase + 4] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11));   // HW_REG_XCC_ID[3:0]
     p.stamps[sbase + 5] = __builtin_amdgcn_s_memrealtime();
+    p.stamps[sbase + 7] = ntiles;
   }
-  // prologue: tiles 0 and 1 into stages 0 and 1, wait for tile 0, read its substep-0 fragments
+
+  // prologue: positions 0 and 1 into stages 0 and 1, wait for position 0, read its substep-0 fragments
+  dma_setup();
 #pragma unroll
-  for (int q = 0; q < 8; ++q) dma_a(0, 0, q);
+  for (int q = 0; q < 8; ++q) dma16(ra, voa[q], stage_a(0) + q * 1024);
 #pragma unroll
-  for (int q = 0; q < 8; ++q) dma_b(0, 0, q);
+  for (int q = 0; q < 8; ++q) dma16(rb, vob[q], stage_b(0) + q * 1024);
+  dma_advance();
+  dma_setup();
 #pragma unroll
-  for (int q = 0; q < 8; ++q) dma_a(1, 1, q);
+  for (int q = 0; q < 8; ++q) dma16(ra, voa[q], stage_a(1) + q * 1024);
 #pragma unroll
-  for (int q = 0; q < 8; ++q) dma_b(1, 1, q);
+  for (int q = 0; q < 8; ++q) dma16(rb, vob[q], stage_b(1) + q * 1024);
+  dma_advance();
   vm_wait<16>();
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_s_waitcnt(0xc07f);   // nothing (kernel-argument loads) pending in lgkmcnt at the loop entry
   if (stamp) p.stamps[sbase + 1] = __builtin_amdgcn_s_memtime();
   fence();
   static_for<16>([&](auto rc) { read_sub(0, K0{}, rc, a0, b0); fence(); });   // same order as in the loop
-  fence();
 
-  for (int t = 0; t < nk; ++t) {
-    const int s = t & 1;
-    static_for<128>([&](auto qc) {
-      constexpr int q = decltype(qc)::value;
-      constexpr int sub = q >> 6, j = (q >> 3) & 7, i = q & 7;
-      if constexpr (sub == 0) mfma_acc(acc[i][j], b0[j], a0[i]);
-      else mfma_acc(acc[i][j], b1f[j], a1[i]);
-      if constexpr (q < 16) read_sub(s, K1{}, qc, a1, b1f);               // substep-1 fragments of tile t
-      if constexpr (q == 25) {                                          // stage s fully read by every wave
-        __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0) as a builtin: the compiler's wait model learns the
-        __builtin_amdgcn_s_barrier();          // substep-1 reads are done (asm would leave it waiting for them again)
-      }
-      if constexpr (q >= 26 && q < 64 && (q - 26) % 5 == 0) dma_a(t + 2, s, (q - 26) / 5);
-      if constexpr (q >= 66 && q < 106 && (q - 66) % 5 == 0) dma_b(t + 2, s, (q - 66) / 5);
-      if constexpr (q == 107) {                                         // tile t+1 landed in stage s^1
-        vm_wait<16>();
-        __builtin_amdgcn_s_barrier();
-      }
-      if constexpr (q >= 108 && q < 124) read_sub(s ^ 1, K0{}, std::integral_constant<int, q - 108>{}, a0, b0);   // substep-0 fragments of tile t+1
-      fence();
-    });
-  }
-  fence();
-  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");   // last MFMA -> accumulator reads: the
-  fence();                                                          // fences keep the reads below the pad
-  vm_wait<0>();   // the over-range prefetches of the last two iterations must land before the LDS is reused
-  if (stamp) p.stamps[sbase + 2] = __builtin_amdgcn_s_memtime();
-  __builtin_amdgcn_s_barrier();   // ... by every wave: the epilogue below overwrites both stages
-  fence();
+  int pos = 0;   // flat position of the K-tile being multiplied (its stage is pos & 1)
+  for (int rnd = 0; rnd < ntiles; ++rnd) {
+    const Tile4 ct = decode4<A_T, B_T>(p, logical(rnd));
+    // Accumulator zeroing (VALU writes of AGPRs) -> first MFMA reading them needs wait states the compiler cannot
+    // see through the asm MFMAs; the empty "+a" asms pin the zeros before the pad (no rematerialisation past it)
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    static_for<64>([&](auto c) { agpr_opaque(acc[decltype(c)::value >> 3][decltype(c)::value & 7]); });
+    asm volatile("s_nop 4" ::: "memory");
+    fence();
+    if (stamp) tmark = __builtin_amdgcn_s_memtime();
 
-  // Epilogue through LDS: per wave 4 rounds of 32 rows x 128 columns (fp32, rows padded to 132 floats:
-  // conflict-free 16-byte fragment writes). Each round the wave writes two accumulator rows of fragments, then a
-  // compact runtime loop reads 8 consecutive outputs per lane and applies epilogue_store8 with 16-byte global
-  // accesses (a fully unrolled per-fragment epilogue inlined the activation switch 64 times: ~12k branches,
-  // instruction-cache bound, as long as the K loop itself at K = 2048).
-  constexpr int EP_LD = 132;
-  float* ep = reinterpret_cast<float*>(smem) + wave * (32 * EP_LD);
-  const long long coff = b1 * p.c_s1 + b2 * p.c_s2;
-  const float alpha = p.alpha;
-  static_for<4>([&](auto rc) {
-    constexpr int r = decltype(rc)::value;
-    static_for<16>([&](auto fc) {
-      constexpr int f = decltype(fc)::value, i = 2 * r + (f >> 3), j = f & 7;
-      const int row = (f >> 3) * 16 + (lane & 15), col = j * 16 + 4 * (lane >> 4);
-      *reinterpret_cast<float4*>(ep + row * EP_LD + col) =
-          make_float4(alpha * acc[i][j][0], alpha * acc[i][j][1], alpha * acc[i][j][2], alpha * acc[i][j][3]);
-    });
-#pragma unroll 1
-    for (int it = 0; it < 8; ++it) {
-      const int row = it * 4 + (lane >> 4), col = (lane & 15) * 8;
-      const float4 x0 = *reinterpret_cast<const float4*>(ep + row * EP_LD + col);
-      const float4 x1 = *reinterpret_cast<const float4*>(ep + row * EP_LD + col + 4);
-      float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-      const int m = m0 + wm * 128 + r * 32 + row, n = n0 + wn * 128 + col;
-      if (m < p.M && n < p.N) {
-        if (OUT_F32 && p.ksplit > 1) {
-          float4* w = reinterpret_cast<float4*>(p.ws + (long long)split * p.M * p.N + (long long)m * p.N + n);
-          w[0] = x0;
-          w[1] = x1;
-        } else {
-          epilogue_store8<OUT_F32>(p, coff + (long long)m * p.ldc + n, v);
+    for (int t = 0; t < nk; ++t, ++pos) {
+      const int s = pos & 1;
+      static_for<128>([&](auto qc) {
+        constexpr int q = decltype(qc)::value;
+        constexpr int sub = q >> 6, j = (q >> 3) & 7, i = q & 7;
+        if constexpr (sub == 0) mfma_acc(acc[i][j], b0[j], a0[i]);
+        else mfma_acc(acc[i][j], b1f[j], a1[i]);
+        if constexpr (q < 16) read_sub(s, K1{}, qc, a1, b1f);               // substep-1 fragments of position pos
+        if constexpr (q == 16) dma_setup();                                 // resources of position pos + 2
+        if constexpr (q == 25) {                                            // stage s fully read by every wave
+          __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0) as a builtin: the compiler's wait model learns the
+          __builtin_amdgcn_s_barrier();          // substep-1 reads are done (asm would leave it waiting again)
         }
-      }
+        if constexpr (q >= 26 && q < 64 && (q - 26) % 5 == 0) dma16(ra, voa[(q - 26) / 5], stage_a(s) + (q - 26) / 5 * 1024);
+        if constexpr (q >= 66 && q < 106 && (q - 66) % 5 == 0) dma16(rb, vob[(q - 66) / 5], stage_b(s) + (q - 66) / 5 * 1024);
+        if constexpr (q == 107) {                                           // position pos+1 landed in stage s^1
+          vm_wait<16>();
+          __builtin_amdgcn_s_barrier();
+        }
+        if constexpr (q >= 108 && q < 124)                                  // substep-0 fragments of position pos+1
+          read_sub(s ^ 1, K0{}, std::integral_constant<int, q - 108>{}, a0, b0);
+        fence();
+      });
+      dma_advance();
     }
-  });
+    // last MFMA -> accumulator reads: the pad redefines every accumulator ("+a"), so the register allocator's
+    // AGPR -> VGPR copies for the epilogue (which fences do not bind) can only read them after it
+    fence();
+    pad_redefine(acc);
+    fence();
+    if (stamp) {
+      const unsigned long long now = __builtin_amdgcn_s_memtime();
+      loop_clk += now - tmark;
+      tmark = now;
+    }
+
+    if (p.act == 0 && p.mode == 0 && p.Zout == nullptr) {
+      // Direct epilogue (every plain product): each lane owns C[m][n..n+3] of 64 fragments and writes it with one
+      // buffer store from the accumulators (bf16: 8 B, fp32: 16 B); one per-lane offset, the fragment row in the
+      // SGPR offset, the fragment column in the instruction's immediate; rows past M fall outside the resource
+      // (dropped), columns past N are masked on the last tile column only.
+      const bool ws_out = OUT_F32 && p.ksplit > 1;
+      const long long ldc = ws_out ? p.N : p.ldc;
+      constexpr int ES = OUT_F32 ? 4 : 2;
+      char* cbase = ws_out ? reinterpret_cast<char*>(p.ws + (long long)ct.split * p.M * p.N)
+                           : reinterpret_cast<char*>(p.C) + ct.coff * ES;
+      const long long corg = ((long long)ct.m0 * ldc + ct.n0) * ES;
+      const long long cext = ((long long)(p.M - ct.m0 - 1) * ldc + (p.N - ct.n0)) * ES;   // bytes to C's end
+      const __amdgpu_buffer_rsrc_t rc = make_brsrc(cbase + corg, cext);
+      const i32x4_t rc4 = make_rsrc(cbase + corg, cext);
+      const __amdgpu_buffer_rsrc_t rr = make_brsrc(p.R ? reinterpret_cast<const char*>(p.R) + ct.coff * ES + corg : cbase, cext);
+      const int ml = lane & 15, nl = 4 * (lane >> 4);
+      const int voff = (int)(((long long)(wm * 128 + ml) * ldc + wn * 128 + nl) * ES);
+      const bool edge = ct.n0 + 256 > p.N;
+      const int nbase = ct.n0 + wn * 128 + nl;
+      const float alpha = p.alpha, beta = ws_out ? 0.f : p.beta;
+      const bool extra = (OUT_F32 && beta != 0.f) || (p.R != nullptr && !ws_out);
+      auto emit = [&](auto exc, auto edc) {
+        constexpr bool EX = decltype(exc)::value, ED = decltype(edc)::value;
+        // one fragment row (8 fragments) at a time: with EX its 8 residual / C loads are issued together and
+        // consumed after, bounded by the fences (unbounded, the scheduler hoisted all 64 loads: 256 VGPRs, spills)
+        static_for<8>([&](auto ic) {
+          constexpr int i = decltype(ic)::value;
+          const int soff = __builtin_amdgcn_readfirstlane((int)(i * 16 * ldc * ES));
+          f32x4_t x[8];
+          if constexpr (EX) {
+            static_for<8>([&](auto jc) {
+              constexpr int j = decltype(jc)::value;
+              if constexpr (OUT_F32) {
+                x[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+                if (beta != 0.f)
+                  x[j] = beta * __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rc, voff, soff + j * 64, 0));
+                if (p.R)
+                  x[j] += __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rr, voff, soff + j * 64, 0));
+              } else {
+                const v2u32_t o = __builtin_amdgcn_raw_buffer_load_b64(rr, voff, soff + j * 32, 0);
+                x[j] = f32x4_t{bf2f(o[0] & 0xffff), bf2f(o[0] >> 16), bf2f(o[1] & 0xffff), bf2f(o[1] >> 16)};
+              }
+            });
+          }
+          static_for<8>([&](auto jc) {
+            constexpr int j = decltype(jc)::value;
+            if (ED && nbase + j * 16 >= p.N) return;
+            f32x4_t v = alpha * acc[i][j];
+            if constexpr (EX) v += x[j];
+            if constexpr (OUT_F32)
+              store16_padded(v, voff, rc4, soff, std::integral_constant<int, j * 64>{});
+            else
+              __builtin_amdgcn_raw_buffer_store_b64(v2u32_t{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])}, rc,
+                                                    voff, soff + j * 32, 0);
+          });
+          fence();
+        });
+      };
+      using T_ = std::true_type;
+      using F_ = std::false_type;
+      if (extra) {
+        if (edge) emit(T_{}, T_{}); else emit(T_{}, F_{});
+      } else {
+        if (edge) emit(F_{}, T_{}); else emit(F_{}, F_{});
+      }
+    } else {
+      // Epilogue through a wave-private 8 KiB LDS region past the two stages (the stages already hold the next
+      // tile's first two K-tiles): 8 rounds of 16 rows x 128 columns fp32, float4 columns XOR-swizzled by row
+      // (conflict-free fragment writes). A round writes one fragment row of accumulators, then a compact runtime
+      // loop reads 8 consecutive outputs per lane and applies epilogue_store8r (one activation switch per round)
+      // with 16-byte global accesses; a fully unrolled per-fragment epilogue inlined the activation switch 64
+      // times (~12k branches), instruction-cache bound and as long as the K loop at K = 2048.
+      float* ep = reinterpret_cast<float*>(smem + 2 * Q_STAGE) + wave * 2048;
+      const float alpha = p.alpha;
+      static_for<8>([&](auto rcc) {
+        constexpr int r = decltype(rcc)::value;
+        static_for<8>([&](auto jc) {
+          constexpr int j = decltype(jc)::value;
+          const int row = lane & 15, c4 = j * 4 + (lane >> 4);
+          *reinterpret_cast<float4*>(ep + row * 128 + ((c4 ^ (row & 7)) << 2)) =
+              make_float4(alpha * acc[r][j][0], alpha * acc[r][j][1], alpha * acc[r][j][2], alpha * acc[r][j][3]);
+        });
+#pragma unroll 1
+        for (int it = 0; it < 4; ++it) {
+          const int row = it * 4 + (lane >> 4), c4 = (lane & 15) * 2;
+          const float4 x0 = *reinterpret_cast<const float4*>(ep + row * 128 + ((c4 ^ (row & 7)) << 2));
+          const float4 x1 = *reinterpret_cast<const float4*>(ep + row * 128 + (((c4 + 1) ^ (row & 7)) << 2));
+          float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+          const int m = ct.m0 + wm * 128 + r * 16 + row, n = ct.n0 + wn * 128 + c4 * 4;
+          if (m < p.M && n < p.N) epilogue_store8r<OUT_F32>(p, ct.coff + (long long)m * p.ldc + n, v);
+        }
+        fence();
+      });
+    }
+    fence();
+    if (stamp) {
+      const unsigned long long now = __builtin_amdgcn_s_memtime();
+      epi_clk += now - tmark;
+    }
+  }
+  vm_wait<0>();   // the last re-staged positions must land before the LDS is released
   if (p.stamps != nullptr) {
     __syncthreads();
     if (stamp) {
-      p.stamps[sbase + 3] = __builtin_amdgcn_s_memtime();
+      p.stamps[sbase + 2] = loop_clk;
+      p.stamps[sbase + 3] = epi_clk;
       p.stamps[sbase + 6] = __builtin_amdgcn_s_memrealtime();
     }
   }
@@ -299,15 +449,18 @@ template <int A_T, int B_T, bool F32>
 hipError_t launch4w(GemmArgs a, int batch, hipStream_t stream) {
   a.tiles_m = (a.M + 255) / 256;
   a.tiles_n = (a.N + 255) / 256;
-  dim3 grid(a.tiles_m * a.tiles_n, batch * a.ksplit);
-  const size_t lds = 2 * Q_STAGE;
+  a.nbatch = batch * a.ksplit;
+  const long long tiles = (long long)a.tiles_m * a.tiles_n * a.nbatch;
+  // one block per CU (32 per XCD); fewer for small launches, keeping a multiple of the 8 XCDs
+  const int grid = (int)(tiles >= 256 ? 256 : ((tiles + 7) / 8) * 8);
+  const size_t lds = 2 * Q_STAGE + 4 * 8192;   // 160 KiB: two stages + the epilogue regions
   auto k = gemm4w_kernel<A_T, B_T, F32>;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
-  hipLaunchKernelGGL(k, grid, dim3(256), lds, stream, a);
+  hipLaunchKernelGGL(k, dim3(grid), dim3(256), lds, stream, a);
   return hipGetLastError();
 }
 

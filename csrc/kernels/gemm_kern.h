@@ -188,6 +188,67 @@ __device__ __forceinline__ void epilogue_store8(const GemmArgs& p, long long idx
   }
 }
 
+// activation of 8 values with ONE inlined switch: a rotation loop (v[0] transformed, the array shifted) keeps every
+// register index static -- for epilogues instantiated many times per kernel (instruction-cache budget)
+__device__ __forceinline__ void act8_fwd(int act, float (&v)[8]) {
+#pragma unroll 1
+  for (int t = 0; t < 8; ++t) {
+    const float x = act_fwd(act, v[0]);
+    v[0] = v[1]; v[1] = v[2]; v[2] = v[3]; v[3] = v[4]; v[4] = v[5]; v[5] = v[6]; v[6] = v[7]; v[7] = x;
+  }
+}
+__device__ __forceinline__ void act8_grad_mul(int act, float (&v)[8], float (&z)[8]) {
+#pragma unroll 1
+  for (int t = 0; t < 8; ++t) {
+    const float x = v[0] * act_grad(act, z[0]);
+    v[0] = v[1]; v[1] = v[2]; v[2] = v[3]; v[3] = v[4]; v[4] = v[5]; v[5] = v[6]; v[6] = v[7]; v[7] = x;
+    z[0] = z[1]; z[1] = z[2]; z[2] = z[3]; z[3] = z[4]; z[4] = z[5]; z[5] = z[6]; z[6] = z[7];
+  }
+}
+
+// epilogue_store8 with the activations applied through act8_*: compact code for the activation GEMMs
+template <bool OUT_F32>
+__device__ __forceinline__ void epilogue_store8r(const GemmArgs& p, long long idx, float (&v)[8]) {
+  if (OUT_F32) {
+    float* C = reinterpret_cast<float*>(p.C) + idx;
+    if (p.beta != 0.f) {
+      const float4 o0 = reinterpret_cast<const float4*>(C)[0], o1 = reinterpret_cast<const float4*>(C)[1];
+      v[0] += p.beta * o0.x; v[1] += p.beta * o0.y; v[2] += p.beta * o0.z; v[3] += p.beta * o0.w;
+      v[4] += p.beta * o1.x; v[5] += p.beta * o1.y; v[6] += p.beta * o1.z; v[7] += p.beta * o1.w;
+    }
+    if (p.R) {
+      const float4* R = reinterpret_cast<const float4*>(reinterpret_cast<const float*>(p.R) + idx);
+      const float4 r0 = R[0], r1 = R[1];
+      v[0] += r0.x; v[1] += r0.y; v[2] += r0.z; v[3] += r0.w; v[4] += r1.x; v[5] += r1.y; v[6] += r1.z; v[7] += r1.w;
+    }
+    if (p.act) act8_fwd(p.act, v);
+    reinterpret_cast<float4*>(C)[0] = make_float4(v[0], v[1], v[2], v[3]);
+    reinterpret_cast<float4*>(C)[1] = make_float4(v[4], v[5], v[6], v[7]);
+  } else {
+    if (p.R) {
+      const uint4 r = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(p.R) + idx);
+      const uint32_t rw[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+      for (int t = 0; t < 4; ++t) { v[2 * t] += bf2f(rw[t] & 0xffff); v[2 * t + 1] += bf2f(rw[t] >> 16); }
+    }
+    if (p.mode == 1) {
+      const uint4 zz = *reinterpret_cast<const uint4*>(p.Zin + idx);
+      const uint32_t zw[4] = {zz.x, zz.y, zz.z, zz.w};
+      float z[8];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) { z[2 * t] = bf2f(zw[t] & 0xffff); z[2 * t + 1] = bf2f(zw[t] >> 16); }
+      act8_grad_mul(p.act, v, z);
+    } else {
+      if (p.Zout)
+        *reinterpret_cast<uint4*>(p.Zout + idx) = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]),
+                                                             pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7]));
+      if (p.act) act8_fwd(p.act, v);
+    }
+    *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(p.C) + idx) =
+        make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7]));
+  }
+}
+
 }  // namespace
 
 // the persistent phase kernel (gemm_pp.hip) for a GemmArgs filled by obst_gemm: plain products on whole tiles

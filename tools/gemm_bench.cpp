@@ -151,6 +151,10 @@ int main(int argc, char** argv) {
       {4096, 2048, 131072, 0, 1, 1, "wgrad 01 4096x2048"},
       {2048, 4096, 131072, 0, 1, 1, "wgrad 01 2048x4096"},
       {4096, 2048, 131072, 1, 0, 1, "wgrad 10 4096x2048"},
+      {4096, 2048, 131072, 1, 1, 1, "wgrad 11 4096x2048"},
+      {2048, 4096, 131072, 1, 1, 1, "wgrad 11 2048x4096"},
+      {2048, 6144, 131072, 1, 1, 1, "wgrad 11 2048x6144"},
+      {131072, 2048, 4096, 0, 1, 0, "dgrad on stored [K][N] weights"},
       {2048, 50304, 131072, 0, 1, 1, "wgrad logits"},
       {8192, 8192, 8192, 0, 0, 0, "8192^3"},
   };
@@ -223,7 +227,7 @@ int main(int argc, char** argv) {
       }
     const double fl = 2.0 * s.M * s.N * (double)s.K;
     if (getenv("STAMPS")) {   // per-block phase breakdown of one gemm4w launch (shader clocks / real time)
-      const long long nblk = (long long)((s.M + 255) / 256) * ((s.N + 255) / 256) * 2;   // upper bound incl. split-K
+      const long long nblk = 256;   // persistent: one block per CU
       unsigned long long* ds;
       CK(hipMalloc(&ds, nblk * 64));
       CK(hipMemset(ds, 0, nblk * 64));
@@ -233,24 +237,25 @@ int main(int argc, char** argv) {
       obst_gemm4w_stamps(nullptr);
       std::vector<unsigned long long> h(nblk * 8);
       CK(hipMemcpy(h.data(), ds, nblk * 64, hipMemcpyDeviceToHost));
-      double pro = 0, loop = 0, epi = 0, span_rt = 0;
+      double pro = 0, loop = 0, epi = 0, span_rt = 0, tiles = 0;
       unsigned long long rt_min = ~0ull, rt_max = 0;
       long long nb = 0;
-      for (long long b = 0; b < nblk; ++b) {
+      for (long long b = 0; b < nblk; ++b) {   // [start, first landed, loop clocks, epilogue clocks, xcc, rt0, rt1, tiles]
         const unsigned long long* t = &h[b * 8];
-        if (!t[0] || !t[3]) continue;
+        if (!t[0] || !t[6]) continue;
         ++nb;
         pro += (double)(t[1] - t[0]);
-        loop += (double)(t[2] - t[1]);
-        epi += (double)(t[3] - t[2]);
+        loop += (double)t[2];
+        epi += (double)t[3];
+        tiles += (double)t[7];
         span_rt += (double)(t[6] - t[5]);
         rt_min = t[5] < rt_min ? t[5] : rt_min;
         rt_max = t[6] > rt_max ? t[6] : rt_max;
       }
-      printf("%-58s stamps: %lld blocks, mean clocks prologue %.0f loop %.0f epilogue %.0f; mean block %.2f us, "
-             "launch span %.1f us, sum(block)/(256*span) %.3f\n",
-             name, nb, pro / nb, loop / nb, epi / nb, span_rt / nb / 100.0, (rt_max - rt_min) / 100.0,
-             span_rt / 256.0 / (double)(rt_max - rt_min));
+      printf("%-58s stamps: %lld blocks, %.1f tiles/block, mean clocks prologue %.0f, per tile loop %.0f epilogue %.0f; "
+             "mean block %.1f us, launch span %.1f us, busy %.3f\n",
+             name, nb, tiles / nb, pro / nb, loop / tiles, epi / tiles, span_rt / nb / 100.0, (rt_max - rt_min) / 100.0,
+             span_rt / nb / (double)(rt_max - rt_min));
       CK(hipFree(ds));
     }
     printf("%-58s TF/s best (mean): hipBLASLt %.0f (%.0f)  phase %.0f (%.0f)  4w %.0f (%.0f)   4w/lt %.3f\n", name,
