@@ -34,7 +34,30 @@ build/runtime/%.o: csrc/runtime/%.cpp $(wildcard csrc/runtime/*.h)
 $(PKG)/_runtime.so: $(ROBJ)
 	g++ $(CXXFLAGS) -shared -o $@ $(ROBJ) -lpthread -lz -ldl
 
+# Sanitizer builds of the threaded host runtime, loaded through OBST_RUNTIME_SO into a stock python
+# with the sanitizer runtime preloaded; `make sancheck` runs the data / runtime CPU tests under both.
+SAN_CXX := g++ -O1 -g -std=c++17 -fPIC -fno-omit-frame-pointer -Wall -Wno-unused-result
+build/san/_runtime_asan.so: $(RSRC) $(wildcard csrc/runtime/*.h)
+	@mkdir -p build/san
+	$(SAN_CXX) -fsanitize=address,undefined -shared -o $@ $(RSRC) -lpthread -lz -ldl
+build/san/_runtime_tsan.so: $(RSRC) $(wildcard csrc/runtime/*.h)
+	@mkdir -p build/san
+	$(SAN_CXX) -fsanitize=thread -shared -o $@ $(RSRC) -lpthread -lz -ldl
+asan: build/san/_runtime_asan.so
+tsan: build/san/_runtime_tsan.so
+SAN_TESTS ?= tests/test_data.py tests/test_runtime_cpu.py
+# under TSan only the tests that drive the native runtime in-process (the REST / subprocess tests spawn uninstrumented
+# interpreters and threads that TSan slows to a crawl)
+TSAN_K ?= not rest_api and not debug_mode and not kv_cache and not fault_injection
+sancheck: asan tsan
+	OBST_RUNTIME_SO=$(CURDIR)/build/san/_runtime_asan.so LD_PRELOAD="$$(g++ -print-file-name=libasan.so) $$(g++ -print-file-name=libubsan.so)" \
+	  ASAN_OPTIONS=detect_leaks=0:halt_on_error=1 UBSAN_OPTIONS=halt_on_error=1:print_stacktrace=1 \
+	  python -m pytest -q -x -m "not gpu" -p no:cacheprovider $(SAN_TESTS)
+	OBST_RUNTIME_SO=$(CURDIR)/build/san/_runtime_tsan.so LD_PRELOAD="$$(g++ -print-file-name=libtsan.so)" \
+	  TSAN_OPTIONS=halt_on_error=1:report_signal_unsafe=0 \
+	  python -m pytest -q -x -m "not gpu" -p no:cacheprovider $(SAN_TESTS) -k "$(TSAN_K)"
+
 clean:
 	rm -rf build $(PKG)/_kernels.so $(PKG)/_runtime.so
 
-.PHONY: all clean
+.PHONY: all clean asan tsan sancheck

@@ -144,6 +144,34 @@ __device__ __forceinline__ bf16x8_t frag(const char* img, int rbase, int kk, int
   return read_frag<1>(img + (rbase >> 7) * (Q_OP / 2), rbase & 127, kk, lane);
 }
 
+// B (output-column) fragment j of a wave's 128 columns at nbase, with the columns permuted inside each pair of
+// fragments: fragment 2p + h, operand row r reads tile column nbase + 32p + 8 (r >> 2) + 4h + (r & 3). The MFMA
+// puts operand rows 4g .. 4g+3 into lane row g's four accumulator registers, so after the pair each lane holds 8
+// CONSECUTIVE output columns nbase + 32p + 8g .. +7 (fragment 2p: +0..3, 2p+1: +4..7) and the epilogue stores
+// 16 bytes per lane without any cross-lane exchange. K-contiguous image: any row order is a gather of rows; the
+// transposed image: each lane of a ds_read_b64_tr_b16 group addresses its own 4-column chunk.
+template <int T>
+__device__ __forceinline__ bf16x8_t frag_b(const char* img, int nbase, int j, int kk, int lane) {
+  const int base = nbase + 32 * (j >> 1) + 4 * (j & 1);
+  if (T == 0) {
+    const int r = base + 8 * ((lane & 15) >> 2) + (lane & 3);
+    const int c = kk * 4 + (lane >> 4);
+    return *reinterpret_cast<const bf16x8_t*>(img + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
+  } else {
+    const char* h = img + (base >> 7) * (Q_OP / 2);
+    const int gg = lane >> 4, i16 = lane & 15, q = i16 >> 2, pp = i16 & 3;
+    const int col = (base & 127) + 8 * pp;          // this lane's 4-column chunk (8-byte half j & 1 of a 16-B chunk)
+    const int c = col >> 3;
+    const int k0 = kk * 32 + 8 * gg + q, k1 = k0 + 4;
+    const int off0 = k0 * 256 + ((c ^ kswz(k0)) << 4) + ((col & 4) << 1);
+    const int off1 = k1 * 256 + ((c ^ kswz(k1)) << 4) + ((col & 4) << 1);
+    s16x4_t v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4_t, h + off0));
+    s16x4_t v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4_t, h + off1));
+    s16x8_t v = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+    return __builtin_bit_cast(bf16x8_t, v);
+  }
+}
+
 // one output tile of the launch: operand bases at its first K-tile, the bytes left in each operand from there
 // (the resource bound that zero-fills rows / columns past the edge), output origin
 struct Tile4 {
@@ -191,7 +219,7 @@ __device__ __forceinline__ Tile4 decode4(const GemmArgs& p, long long L) {
 // ACROSS tile boundaries (positions of a flat (tile, K-tile) sequence), so the next tile's first two K-tiles are
 // in LDS when the current tile's epilogue is done, and its first fragments are read under the current tile's
 // last MFMAs. XCD x owns a contiguous run of logical tiles, dealt to its CUs in rounds.
-template <int A_T, int B_T, bool OUT_F32>
+template <int A_T, int B_T, bool OUT_F32, bool PROF>
 __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs p) {
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -245,9 +273,9 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs p) {
     const char* ia = smem + s * Q_STAGE;
     const char* ib = smem + s * Q_STAGE + Q_OP;
     if constexpr (r == 0) af[0] = frag<A_T>(ia, wm * 128, kk, lane);
-    else if constexpr (r == 1) bf[0] = frag<B_T>(ib, wn * 128, kk, lane);
+    else if constexpr (r == 1) bf[0] = frag_b<B_T>(ib, wn * 128, 0, kk, lane);
     else if constexpr (r < 9) af[r - 1] = frag<A_T>(ia, wm * 128 + (r - 1) * 16, kk, lane);
-    else bf[r - 8] = frag<B_T>(ib, wn * 128 + (r - 8) * 16, kk, lane);
+    else bf[r - 8] = frag_b<B_T>(ib, wn * 128, r - 8, kk, lane);
   };
   using K0 = std::integral_constant<int, 0>;
   using K1 = std::integral_constant<int, 1>;
@@ -256,7 +284,7 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs p) {
   // loop clocks, summed epilogue clocks], the XCC id, [start, end] in 100 MHz real time, tiles
   const bool stamp = p.stamps != nullptr && tid == 0;
   const long long sbase = (long long)blockIdx.x * 8;
-  unsigned long long loop_clk = 0, epi_clk = 0, tmark = 0;
+  unsigned long long loop_clk = 0, epi_clk = 0, tmark = 0, sync1 = 0, sync2 = 0, tw = 0;
   if (stamp) {
     p.stamps[sbase] = __builtin_amdgcn_s_memtime();
     p.stamps[sbase + 4] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11));   // HW_REG_XCC_ID[3:0]
@@ -285,6 +313,8 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs p) {
   static_for<16>([&](auto rc) { read_sub(0, K0{}, rc, a0, b0); fence(); });   // same order as in the loop
 
   int pos = 0;   // flat position of the K-tile being multiplied (its stage is pos & 1)
+  // vmcnt of the first K-tile of a tile (see q == 107): 16 + the previous epilogue's stores, at most 63
+  const int first_wait = (p.act == 0 && p.mode == 0 && p.Zout == nullptr) ? (OUT_F32 ? 63 : 48) : 16;
   for (int rnd = 0; rnd < ntiles; ++rnd) {
     const Tile4 ct = decode4<A_T, B_T>(p, logical(rnd));
     // Accumulator zeroing (VALU writes of AGPRs) -> first MFMA reading them needs wait states the compiler cannot
@@ -308,14 +338,22 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs p) {
         if constexpr (q < 16) read_sub(s, K1{}, qc, a1, b1f);               // substep-1 fragments of position pos
         if constexpr (q == 16) dma_setup();                                 // resources of position pos + 2
         if constexpr (q == 25) {                                            // stage s fully read by every wave
+          if constexpr (PROF) tw = __builtin_amdgcn_s_memtime();
           __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0) as a builtin: the compiler's wait model learns the
           __builtin_amdgcn_s_barrier();          // substep-1 reads are done (asm would leave it waiting again)
+          if constexpr (PROF) sync1 += __builtin_amdgcn_s_memtime() - tw;
         }
         if constexpr (q >= 26 && q < 64 && (q - 26) % 5 == 0) dma16(ra, voa[(q - 26) / 5], stage_a(s) + (q - 26) / 5 * 1024);
         if constexpr (q >= 66 && q < 106 && (q - 66) % 5 == 0) dma16(rb, vob[(q - 66) / 5], stage_b(s) + (q - 66) / 5 * 1024);
         if constexpr (q == 107) {                                           // position pos+1 landed in stage s^1
-          vm_wait<16>();
+          // first K-tile of a tile: the previous tile's epilogue stores sit between that position's DMAs and this
+          // iteration's; count them out instead of waiting for every store (direct epilogue: 32 bf16 / 64 fp32)
+          if constexpr (PROF) tw = __builtin_amdgcn_s_memtime();
+          if (t == 0 && rnd > 0 && first_wait == 48) vm_wait<48>();
+          else if (t == 0 && rnd > 0 && first_wait == 63) vm_wait<63>();
+          else vm_wait<16>();
           __builtin_amdgcn_s_barrier();
+          if constexpr (PROF) sync2 += __builtin_amdgcn_s_memtime() - tw;
         }
         if constexpr (q >= 108 && q < 124)                                  // substep-0 fragments of position pos+1
           read_sub(s ^ 1, K0{}, std::integral_constant<int, q - 108>{}, a0, b0);
@@ -349,45 +387,58 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs p) {
       const __amdgpu_buffer_rsrc_t rc = make_brsrc(cbase + corg, cext);
       const i32x4_t rc4 = make_rsrc(cbase + corg, cext);
       const __amdgpu_buffer_rsrc_t rr = make_brsrc(p.R ? reinterpret_cast<const char*>(p.R) + ct.coff * ES + corg : cbase, cext);
-      const int ml = lane & 15, nl = 4 * (lane >> 4);
-      const int voff = (int)(((long long)(wm * 128 + ml) * ldc + wn * 128 + nl) * ES);
-      const bool edge = ct.n0 + 256 > p.N;
-      const int nbase = ct.n0 + wn * 128 + nl;
+      const int ml = lane & 15, gq = lane >> 4;
       const float alpha = p.alpha, beta = ws_out ? 0.f : p.beta;
+      const bool edge = ct.n0 + 256 > p.N;
       const bool extra = (OUT_F32 && beta != 0.f) || (p.R != nullptr && !ws_out);
+      // fragment pair (2p, 2p+1) = 8 consecutive columns per lane (frag_b): 16 B (bf16) / 2 x 16 B (fp32) stores,
+      // 32 / 64 per wave (64 bf16 stores with the 32 LDS-DMAs in flight overflowed the 63-entry vmcnt)
+      const int voff = (int)(((long long)(wm * 128 + ml) * ldc + wn * 128 + 8 * gq) * ES);
+      const int nbase = ct.n0 + wn * 128 + 8 * gq;
       auto emit = [&](auto exc, auto edc) {
         constexpr bool EX = decltype(exc)::value, ED = decltype(edc)::value;
-        // one fragment row (8 fragments) at a time: with EX its 8 residual / C loads are issued together and
-        // consumed after, bounded by the fences (unbounded, the scheduler hoisted all 64 loads: 256 VGPRs, spills)
+        // one fragment row at a time: with EX its residual / C loads are issued together and consumed after,
+        // bounded by the fences (unbounded, the scheduler hoisted all 64 loads: 256 VGPRs, spills)
         static_for<8>([&](auto ic) {
           constexpr int i = decltype(ic)::value;
           const int soff = __builtin_amdgcn_readfirstlane((int)(i * 16 * ldc * ES));
           f32x4_t x[8];
           if constexpr (EX) {
-            static_for<8>([&](auto jc) {
-              constexpr int j = decltype(jc)::value;
+            static_for<4>([&](auto pc) {
+              constexpr int pp = decltype(pc)::value;
               if constexpr (OUT_F32) {
-                x[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-                if (beta != 0.f)
-                  x[j] = beta * __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rc, voff, soff + j * 64, 0));
-                if (p.R)
-                  x[j] += __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rr, voff, soff + j * 64, 0));
+                x[2 * pp] = x[2 * pp + 1] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+                if (beta != 0.f) {
+                  x[2 * pp] = beta * __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rc, voff, soff + pp * 128, 0));
+                  x[2 * pp + 1] = beta * __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rc, voff, soff + pp * 128 + 16, 0));
+                }
+                if (p.R) {
+                  x[2 * pp] += __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rr, voff, soff + pp * 128, 0));
+                  x[2 * pp + 1] += __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rr, voff, soff + pp * 128 + 16, 0));
+                }
               } else {
-                const v2u32_t o = __builtin_amdgcn_raw_buffer_load_b64(rr, voff, soff + j * 32, 0);
-                x[j] = f32x4_t{bf2f(o[0] & 0xffff), bf2f(o[0] >> 16), bf2f(o[1] & 0xffff), bf2f(o[1] >> 16)};
+                const v4u32_t o = __builtin_amdgcn_raw_buffer_load_b128(rr, voff, soff + pp * 64, 0);
+                x[2 * pp] = f32x4_t{bf2f(o[0] & 0xffff), bf2f(o[0] >> 16), bf2f(o[1] & 0xffff), bf2f(o[1] >> 16)};
+                x[2 * pp + 1] = f32x4_t{bf2f(o[2] & 0xffff), bf2f(o[2] >> 16), bf2f(o[3] & 0xffff), bf2f(o[3] >> 16)};
               }
             });
           }
-          static_for<8>([&](auto jc) {
-            constexpr int j = decltype(jc)::value;
-            if (ED && nbase + j * 16 >= p.N) return;
-            f32x4_t v = alpha * acc[i][j];
-            if constexpr (EX) v += x[j];
-            if constexpr (OUT_F32)
-              store16_padded(v, voff, rc4, soff, std::integral_constant<int, j * 64>{});
-            else
-              __builtin_amdgcn_raw_buffer_store_b64(v2u32_t{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])}, rc,
-                                                    voff, soff + j * 32, 0);
+          static_for<4>([&](auto pc) {
+            constexpr int pp = decltype(pc)::value;
+            if (ED && nbase + pp * 32 >= p.N) return;
+            f32x4_t va = alpha * acc[i][2 * pp], vb = alpha * acc[i][2 * pp + 1];
+            if constexpr (EX) {
+              va += x[2 * pp];
+              vb += x[2 * pp + 1];
+            }
+            if constexpr (OUT_F32) {
+              store16_padded(va, voff, rc4, soff, std::integral_constant<int, pp * 128>{});
+              store16_padded(vb, voff, rc4, soff, std::integral_constant<int, pp * 128 + 16>{});
+            } else {
+              __builtin_amdgcn_raw_buffer_store_b128(v4u32_t{pack_bf16x2(va[0], va[1]), pack_bf16x2(va[2], va[3]),
+                                                             pack_bf16x2(vb[0], vb[1]), pack_bf16x2(vb[2], vb[3])},
+                                                     rc, voff, soff + pp * 64, 0);
+            }
           });
           fence();
         });
@@ -412,7 +463,7 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs p) {
         constexpr int r = decltype(rcc)::value;
         static_for<8>([&](auto jc) {
           constexpr int j = decltype(jc)::value;
-          const int row = lane & 15, c4 = j * 4 + (lane >> 4);
+          const int row = lane & 15, c4 = 8 * (j >> 1) + 2 * (lane >> 4) + (j & 1);   // frag_b column order
           *reinterpret_cast<float4*>(ep + row * 128 + ((c4 ^ (row & 7)) << 2)) =
               make_float4(alpha * acc[r][j][0], alpha * acc[r][j][1], alpha * acc[r][j][2], alpha * acc[r][j][3]);
         });
@@ -440,6 +491,10 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs p) {
     if (stamp) {
       p.stamps[sbase + 2] = loop_clk;
       p.stamps[sbase + 3] = epi_clk;
+      if (PROF) {   // the start / first-landed slots give way to the two sync points' clocks
+        p.stamps[sbase + 0] = sync1;
+        p.stamps[sbase + 1] = sync2;
+      }
       p.stamps[sbase + 6] = __builtin_amdgcn_s_memrealtime();
     }
   }
@@ -454,11 +509,11 @@ hipError_t launch4w(GemmArgs a, int batch, hipStream_t stream) {
   // one block per CU (32 per XCD); fewer for small launches, keeping a multiple of the 8 XCDs
   const int grid = (int)(tiles >= 256 ? 256 : ((tiles + 7) / 8) * 8);
   const size_t lds = 2 * Q_STAGE + 4 * 8192;   // 160 KiB: two stages + the epilogue regions
-  auto k = gemm4w_kernel<A_T, B_T, F32>;
-  static bool attr = false;
-  if (!attr) {
+  auto k = a.stamps ? gemm4w_kernel<A_T, B_T, F32, true> : gemm4w_kernel<A_T, B_T, F32, false>;
+  static bool attr[2] = {false, false};
+  if (!attr[a.stamps != nullptr]) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    attr = true;
+    attr[a.stamps != nullptr] = true;
   }
   hipLaunchKernelGGL(k, dim3(grid), dim3(256), lds, stream, a);
   return hipGetLastError();

@@ -88,7 +88,8 @@ def lib() -> ctypes.CDLL:
         return _LIB
     with _LOCK:
         if _LIB is None:
-            path = os.path.join(_HERE, "_runtime.so")
+            # OBST_RUNTIME_SO: an alternative build of the runtime (the sanitizer builds of `make asan` / `make tsan`)
+            path = os.environ.get("OBST_RUNTIME_SO") or os.path.join(_HERE, "_runtime.so")
             if not os.path.exists(path):
                 raise RuntimeErrorNative(f"native runtime {path} is missing: run `make` in the repository root")
             L = ctypes.CDLL(path)
