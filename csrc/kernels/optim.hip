@@ -239,14 +239,6 @@ __device__ __forceinline__ void apply_elems(const ApplyArgs& a, const OptTensor&
 #pragma unroll
   for (int j = 0; j < V; ++j) {
     if (a.emit_stats) { s2 += g[j] * g[j]; s1 += g[j]; }
-    if (af) {
-      const float v = g[j] * g[j] + 1e-30f;
-      const int r = (e + j) / T.fac_cols, c = (e + j) % T.fac_cols;
-      if (af_rows_win) atomicAdd(wlead + (r - af_r0), v);
-      else atomicAdd(a.af_rows_sum + T.fac_off + r, v);
-      if (af_cols_win) atomicAdd(wlast + c, v);
-      else atomicAdd(a.af_cols_sum + T.fac_off + T.fac_rows + c, v);
-    }
   }
   if (a.final_seg) {
 #pragma unroll
@@ -294,16 +286,11 @@ __global__ __launch_bounds__(NTA) void opt_apply_kernel(ApplyArgs a) {
       for (int i = threadIdx.x; i < W.cnt[d]; i += NTA) wb[i] = 0.f;
     }
   }
-  // adafactor row/column sums of g^2: rows of this chunk in wlead, all columns in wlast (when they fit)
-  const bool af = a.emit_factored && T.fac_rows > 0;
-  const long long af_r0 = af ? ck.start / T.fac_cols : 0;
-  const int af_nr = af ? (int)((ck.start + ck.len - 1) / T.fac_cols - af_r0 + 1) : 0;
-  const bool af_rows_win = af && af_nr <= 3 * WIN_LEAD;
-  const bool af_cols_win = af && T.fac_cols <= WIN_LAST;
-  if (af) {
-    for (int i = threadIdx.x; i < (af_rows_win ? af_nr : 0); i += NTA) wlead[i] = 0.f;
-    for (int i = threadIdx.x; i < (af_cols_win ? T.fac_cols : 0); i += NTA) wlast[i] = 0.f;
-  }
+  // Adafactor's factored statistics of this segment's output are NOT accumulated here: opt_factored_kernel reads
+  // them back from uout in a fixed order (float atomics made the step nondeterministic)
+  const bool af = false;
+  const long long af_r0 = 0;
+  const bool af_rows_win = false, af_cols_win = false;
   __syncthreads();
   const float deb1 = 1.f / (1.f - powf(a.beta1, step_of(a)));
   const float deb2 = 1.f / (1.f - powf(a.beta2, step_of(a)));
@@ -334,13 +321,6 @@ __global__ __launch_bounds__(NTA) void opt_apply_kernel(ApplyArgs a) {
         }
       }
     }
-  }
-  if (af) {
-    __syncthreads();
-    if (af_rows_win)
-      for (int i = threadIdx.x; i < af_nr; i += NTA) atomicAdd(a.af_rows_sum + T.fac_off + af_r0 + i, wlead[i]);
-    if (af_cols_win)
-      for (int i = threadIdx.x; i < T.fac_cols; i += NTA) atomicAdd(a.af_cols_sum + T.fac_off + T.fac_rows + i, wlast[i]);
   }
   if (a.emit_stats) {
     __shared__ float red[8];
@@ -822,31 +802,105 @@ __global__ __launch_bounds__(NTH) void opt_scalar_kernel(const OptTensor* tensor
         break;
       }
       case OP_ADAFACTOR: {
-        // decay rate 1 - step^-0.8 (Shazeer & Stern 2018, eq. in section 7.2), fixed-beta variant if st.a > 0
+        // decay rate 1 - step^-0.8 (Shazeer & Stern 2018, eq. in section 7.2), fixed-beta variant if st.a > 0.
+        // Under TP the sums are of the full tensor (TP-reduced by the caller) and the counts global: flags 8 = the
+        // rows (leading dims) are head-sharded, 16 = the columns (last dim) are. f[6] = sum of the row factors
+        // (partial when rows are sharded: the caller reduces it and recomputes f[5] = f[7] / f[6]).
         const float b2 = st.a > 0.f ? st.a : 1.f - powf(step_count, -0.8f);
         f[4] = b2;
         if (T.fac_rows > 0) {
+          const float rows_g = (float)T.fac_rows * ((T.flags & 8) ? tp_size : 1);
+          const float cols_g = (float)T.fac_cols * ((T.flags & 16) ? tp_size : 1);
           float msum = 0.f;
           for (int r = 0; r < T.fac_rows; ++r) {
             float* R = af_state + T.fac_off + r;
-            *R = *R * b2 + (af_rows_sum[T.fac_off + r] / T.fac_cols) * (1.f - b2);
+            *R = *R * b2 + (af_rows_sum[T.fac_off + r] / cols_g + 1e-30f) * (1.f - b2);
             msum += *R;
           }
           for (int c = 0; c < T.fac_cols; ++c) {
             float* C = af_state + T.fac_off + T.fac_rows + c;
-            *C = *C * b2 + (af_cols_sum[T.fac_off + T.fac_rows + c] / T.fac_rows) * (1.f - b2);
+            *C = *C * b2 + (af_cols_sum[T.fac_off + T.fac_rows + c] / rows_g + 1e-30f) * (1.f - b2);
           }
-          f[5] = T.fac_rows / fmaxf(msum, 1e-30f);
+          f[5] = rows_g / fmaxf(msum, 1e-30f);
+          f[6] = msum;
+          f[7] = rows_g;
         }
         break;
       }
       case OP_ADAFACTOR_CLIP: {
-        const float rms = sqrtf(s[0] / n);
+        const float rms = sqrtf(s[0] / (n * ((T.flags & 4) ? tp_size : 1)));
         f[0] = 1.f / fmaxf(1.f, rms / (st.a > 0.f ? st.a : 1.f));
         break;
       }
       default: break;
     }
+  }
+}
+// ---------------------------------------------------------------------------------------------------------------
+// Adafactor's factored statistics of a segment output u (Shazeer & Stern 2018), deterministic: a tensor is viewed as
+// [R rows][C cols]; a work item is a tile of <= 64 rows x <= 1024 columns. Its 4 waves take every 4th row; a lane
+// owns the 16 columns c0 + lane + 64 k. Per row the lane's squares are summed in k order and reduced across the
+// wave by a fixed butterfly: one partial row sum per (column chunk, row) into rowpart. Column partials are summed
+// over the wave's rows in order, then over the 4 waves in wave order: one partial column sum per (row tile, col)
+// into colpart. opt_factored_fold adds the partials in index order. No float atomics: bitwise reproducible.
+struct FChunk { int t, row0, nrows, col0, ncols, rt, cc, pad; long long cp_off, rp_off; };
+struct FFold { int t, kind, start, len; long long off; int nparts, pad; };   // kind 0: rows, 1: cols
+
+__global__ __launch_bounds__(256) void opt_factored_kernel(const OptTensor* __restrict__ tensors,
+                                                           const FChunk* __restrict__ chunks,
+                                                           const float* __restrict__ u, float* __restrict__ colpart,
+                                                           float* __restrict__ rowpart) {
+  __shared__ float cacc[4][1024];
+  const FChunk ck = chunks[blockIdx.x];
+  const OptTensor T = tensors[ck.t];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const float* base = u + T.off;
+  float cs[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) cs[k] = 0.f;
+  for (int r = w; r < ck.nrows; r += 4) {
+    const float* row = base + (long long)(ck.row0 + r) * T.fac_cols + ck.col0;
+    float x[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int c = lane + 64 * k;
+      x[k] = c < ck.ncols ? row[c] : 0.f;
+    }
+    float rs = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const float q = x[k] * x[k];
+      rs += q;
+      cs[k] += q;
+    }
+    rs = wave_sum(rs);
+    if (lane == 0) rowpart[ck.rp_off + (long long)ck.cc * T.fac_rows + ck.row0 + r] = rs;
+  }
+#pragma unroll
+  for (int k = 0; k < 16; ++k) cacc[w][lane + 64 * k] = cs[k];
+  __syncthreads();
+  for (int c = threadIdx.x; c < ck.ncols; c += 256)
+    colpart[ck.cp_off + (long long)ck.rt * T.fac_cols + ck.col0 + c] =
+        ((cacc[0][c] + cacc[1][c]) + cacc[2][c]) + cacc[3][c];
+}
+
+// af_rows_sum / af_cols_sum (at each tensor's fac_off) = the partials added in index order
+__global__ __launch_bounds__(256) void opt_factored_fold_kernel(const OptTensor* __restrict__ tensors,
+                                                                const FFold* __restrict__ folds,
+                                                                const float* __restrict__ colpart,
+                                                                const float* __restrict__ rowpart,
+                                                                float* __restrict__ af_sums) {
+  const FFold f = folds[blockIdx.x];
+  const OptTensor T = tensors[f.t];
+  const int i = f.start + (int)threadIdx.x;
+  if (threadIdx.x >= (unsigned)f.len) return;
+  float s = 0.f;
+  if (f.kind == 0) {
+    for (int p = 0; p < f.nparts; ++p) s += rowpart[f.off + (long long)p * T.fac_rows + i];
+    af_sums[T.fac_off + i] = s;
+  } else {
+    for (int p = 0; p < f.nparts; ++p) s += colpart[f.off + (long long)p * T.fac_cols + i];
+    af_sums[T.fac_off + T.fac_rows + i] = s;
   }
 }
 }  // namespace
@@ -868,6 +922,7 @@ struct ObstOptDesc {
 static_assert(sizeof(OptTensor) == 88, "OptTensor layout is mirrored in python (optim/fused.py)");
 static_assert(sizeof(Chunk) == 24, "Chunk layout is mirrored in python (optim/fused.py)");
 static_assert(sizeof(RChunk) == 24, "RChunk layout is mirrored in python (optim/fused.py)");
+static_assert(sizeof(FChunk) == 48 && sizeof(FFold) == 32, "FChunk / FFold layouts are mirrored in optim/fused.py");
 
 OBST_API int obst_opt_stats(const ObstOptDesc* d, hipStream_t s) {
   if (!d->part) return -1;
@@ -940,5 +995,16 @@ OBST_API int obst_opt_apply_rows(const ObstOptDesc* d, const void* rchunks, int 
     hipLaunchKernelGGL(opt_rows_kernel<1>, dim3(nrchunks), dim3(RW_NT), 0, s, apply_args(d), (const RChunk*)rchunks);
   else
     hipLaunchKernelGGL(opt_rows_kernel<0>, dim3(nrchunks), dim3(RW_NT), 0, s, apply_args(d), (const RChunk*)rchunks);
+  return (int)hipGetLastError();
+}
+
+// deterministic Adafactor row / column sums of u (the segment output) into d->af_rows_sum (= af_cols_sum buffer)
+OBST_API int obst_opt_factored(const ObstOptDesc* d, const float* u, const void* fchunks, int nfchunks,
+                               const void* folds, int nfolds, float* colpart, float* rowpart, hipStream_t s) {
+  if (nfchunks <= 0) return 0;
+  hipLaunchKernelGGL(opt_factored_kernel, dim3(nfchunks), dim3(256), 0, s, (const OptTensor*)d->tensors,
+                     (const FChunk*)fchunks, u, colpart, rowpart);
+  hipLaunchKernelGGL(opt_factored_fold_kernel, dim3(nfolds), dim3(256), 0, s, (const OptTensor*)d->tensors,
+                     (const FFold*)folds, colpart, rowpart, d->af_rows_sum);
   return (int)hipGetLastError();
 }

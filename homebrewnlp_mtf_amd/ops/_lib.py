@@ -100,6 +100,7 @@ _SIGS = {
     "obst_opt_apply": [ctypes.POINTER(OptDesc), c_p],
     "obst_opt_fold": [ctypes.POINTER(OptDesc), c_p, c_i, c_p],
     "obst_opt_apply_rows": [ctypes.POINTER(OptDesc), c_p, c_i, c_p],
+    "obst_opt_factored": [ctypes.POINTER(OptDesc), c_p, c_p, c_i, c_p, c_i, c_p, c_p, c_p],
     "obst_blaslt_enabled": [],
     "obst_blaslt_set": [c_i],
     "obst_blaslt_splitk_set": [c_i],

@@ -138,6 +138,8 @@ class FusedOptimizer:
                 flags |= 2
             if self.sharded[ti]:
                 flags |= 4
+                if need_af and ndim >= 2:   # Adafactor: which factored axis is head-sharded (optim.hip OP_ADAFACTOR)
+                    flags |= 16 if store.specs[n].tp_dim == len(store.specs[n].local_shape) - 1 else 8
             dims = (shape + [1, 1, 1, 1])[:4]
             so = [sm3_off.get((ti, d), 0) for d in range(4)]
             frows = fcols = 0
@@ -151,6 +153,34 @@ class FusedOptimizer:
             self.tinfo.append((offset, numel, shape, [sm3_off.get((ti, d)) for d in range(ndim)], foff, frows, fcols))
         self.ntensors = len(packed)
         self.nchunks = len(chunks)
+        # Adafactor: work items of the deterministic factored-statistics kernel (optim.hip opt_factored_kernel,
+        # tiles of <= 64 rows x <= 1024 columns) and of its fold, partial-sum slabs, and the TP masks
+        fch, folds = [], []
+        cp_tot = rp_tot = 0
+        af_mask = torch.zeros(max(fac_total, 1), dtype=torch.float32)
+        rows_sharded = []
+        for ti, (offset, numel, shape, _, foff, frows, fcols) in enumerate(self.tinfo):
+            if not frows:
+                continue
+            nrt, ncc = -(-frows // 64), -(-fcols // 1024)
+            cp_off, rp_off = cp_tot, rp_tot
+            cp_tot += nrt * fcols
+            rp_tot += ncc * frows
+            for rt in range(nrt):
+                for cc in range(ncc):
+                    fch.append(struct.pack("<8iqq", ti, rt * 64, min(64, frows - rt * 64), cc * 1024,
+                                           min(1024, fcols - cc * 1024), rt, cc, 0, cp_off, rp_off))
+            for r0 in range(0, frows, 256):
+                folds.append(struct.pack("<4iqii", ti, 0, r0, min(256, frows - r0), rp_off, ncc, 0))
+            for c0 in range(0, fcols, 256):
+                folds.append(struct.pack("<4iqii", ti, 1, c0, min(256, fcols - c0), cp_off, nrt, 0))
+            fl = struct.unpack_from("<qqii", packed[ti])[3]
+            if fl & 16:
+                af_mask[foff:foff + frows] = 1.0          # row sums partial: the columns are sharded
+            if fl & 8:
+                af_mask[foff + frows:foff + frows + fcols] = 1.0   # column sums partial: the rows are sharded
+                rows_sharded.append(ti)
+        self.nfchunks, self.nfolds = len(fch), len(folds)
         # row-tiled apply (optim.hip opt_rows_kernel) for every >= 1-D tensor when the chain has no Adafactor;
         # the generic apply then only runs the 0-dim tensors
         self.use_rows = not need_af and os.environ.get("OBST_OPT_ROWS", "1") != "0"
@@ -209,6 +239,16 @@ class FusedOptimizer:
         self.sm3 = [torch.zeros(self.sm3_total, **f32), torch.zeros(self.sm3_total, **f32)] if need_sm3 else None
         self.af_state = torch.zeros(max(fac_total, 1), **f32) if need_af else None
         self.af_sums = torch.zeros(max(fac_total, 1), **f32) if need_af else None
+        if need_af:
+            self.t_fchunks = torch.tensor(bytearray(b"".join(fch) or b"\0" * 48), dtype=torch.uint8, device=dev)
+            self.t_folds = torch.tensor(bytearray(b"".join(folds) or b"\0" * 32), dtype=torch.uint8, device=dev)
+            self.colpart = torch.empty(max(cp_tot, 1), **f32)
+            self.rowpart = torch.empty(max(rp_tot, 1), **f32)
+            self.af_mask = af_mask.to(dev)
+            rs = torch.zeros(self.ntensors, **f32)
+            rs[rows_sharded] = 1.0
+            self.af_rows_sharded = rs.view(-1, 1)
+            self.af_factored = torch.tensor([1.0 if t[5] else 0.0 for t in self.tinfo], **f32)
         nseg = len(self.segments) + int(self.pre_factored)
         self.u = torch.empty(total, **f32) if nseg > 1 else None
         self.u2 = torch.empty(total, **f32) if nseg > 2 else None
@@ -268,6 +308,24 @@ class FusedOptimizer:
     def _scalar(self, d, stage):
         self._set_stages(d, [stage])
         L.check(L.lib().obst_opt_scalar(d, L.stream_ptr()), "opt_scalar")
+        if stage[0] == "adafactor" and self.tp > 1:
+            # the mean of the row factors over the FULL rows: sum(R) partial where the rows are head-sharded
+            fac = self.facs.view(-1, 8)
+            part = fac[:, 6:7] * self.af_rows_sharded
+            pstate.tp_all_reduce(part)
+            msum = part + fac[:, 6:7] * (1 - self.af_rows_sharded)
+            fac[:, 5:6] = torch.where(self.af_factored.view(-1, 1) > 0, fac[:, 7:8] / msum.clamp(min=1e-30),
+                                      fac[:, 5:6])
+
+    def _factored(self, d, u):
+        """Adafactor row / column sums of the segment output u into af_sums (deterministic), TP-reduced"""
+        L.check(L.lib().obst_opt_factored(d, u.data_ptr(), self.t_fchunks.data_ptr(), self.nfchunks,
+                                          self.t_folds.data_ptr(), self.nfolds, self.colpart.data_ptr(),
+                                          self.rowpart.data_ptr(), L.stream_ptr()), "opt_factored")
+        if self.tp > 1:
+            part = self.af_sums * self.af_mask
+            pstate.tp_all_reduce(part)
+            self.af_sums.copy_(part + self.af_sums * (1 - self.af_mask))
 
     @torch.no_grad()
     def step(self, lr: float, step_count: int, grad_scale: float = 1.0):
@@ -287,13 +345,11 @@ class FusedOptimizer:
         bufs = [self.u, self.u2]
         bi = 0
         if self.pre_factored:
-            self.af_sums.zero_()
             d.uin, d.uout = 0, bufs[bi].data_ptr()
             self._set_stages(d, [])
-            d.final_seg, d.emit_stats, d.emit_factored = 0, 0, 1
+            d.final_seg, d.emit_stats, d.emit_factored = 0, 0, 0
             L.check(lib.obst_opt_apply(d, sp), "opt_apply(pre)")
-            if self.tp > 1:
-                raise NotImplementedError("adafactor under TP")
+            self._factored(d, bufs[bi])
             src, bi = bufs[bi], 1 - bi
         segs = self.segments[1:] if (self.pre_factored and not self.segments[0].stages) else self.segments
         for k, seg in enumerate(segs):
@@ -301,11 +357,9 @@ class FusedOptimizer:
                 self._scalar(d, seg.opener)
             last = k == len(segs) - 1
             d.uin = 0 if src is None else src.data_ptr()
-            if seg.emit_factored:
-                self.af_sums.zero_()
             d.uout = 0 if last else bufs[bi].data_ptr()
             self._set_stages(d, seg.stages)
-            d.final_seg, d.emit_stats, d.emit_factored = int(last), int(seg.emit_stats), int(seg.emit_factored)
+            d.final_seg, d.emit_stats, d.emit_factored = int(last), int(seg.emit_stats), 0
             if self.use_rows:
                 d.part_base = 0
                 L.check(lib.obst_opt_apply_rows(d, self.t_rchunks.data_ptr(), self.nrchunks, sp), "opt_apply_rows")
@@ -317,6 +371,8 @@ class FusedOptimizer:
             if seg.emit_stats:
                 L.check(lib.obst_opt_fold(d, self.rng_rows.data_ptr(), 2, sp), "opt_fold")
                 self._reduce_stats()
+            if seg.emit_factored:
+                self._factored(d, bufs[bi])
             if not last:
                 src, bi = bufs[bi], 1 - bi
         self.store.bump()

@@ -88,7 +88,10 @@ class ReferenceOptimizer:
         return b1 * p1 + g * opt_rsqrt(p2 / (1 - b2 ** sc))
 
     def _adafactor(self, name, g, ctx, arg=None):
-        """Shazeer & Stern 2018: factored second moment over the last two dims, update clipping d=1."""
+        """Shazeer & Stern 2018: factored second moment over [rows = all leading dims, cols = last dim], update
+        clipping d=1. Under TP the factored statistics are those of the FULL tensor: a sharded last dim leaves each
+        rank partial row sums, a sharded leading dim partial column sums and a partial sum of the row factors --
+        each is all-reduced over the TP group and divided by the global count."""
         sc = ctx["step_count"]
         b2 = float(arg) if arg else 1.0 - sc ** -0.8
         if g.dim() >= 2:
@@ -97,10 +100,26 @@ class ReferenceOptimizer:
             g2 = g.reshape(rows, cols)
             R = self._slot(name, "af_rows", g, (rows,))
             C = self._slot(name, "af_cols", g, (cols,))
-            sq = g2 * g2 + 1e-30
-            R.mul_(b2).add_(sq.mean(1) * (1 - b2))
-            C.mul_(b2).add_(sq.mean(0) * (1 - b2))
-            vhat = R.view(-1, 1) * C.view(1, -1) / R.mean()
+            spec = self.store.specs[name]
+            tp = pstate.tp_size()
+            sharded = tp > 1 and spec.tp_dim is not None
+            cols_sharded = sharded and spec.tp_dim == g.dim() - 1
+            rows_sharded = sharded and not cols_sharded
+            sq = g2 * g2
+            rsum, csum = sq.sum(1), sq.sum(0)
+            if cols_sharded:
+                pstate.tp_all_reduce(rsum)
+            if rows_sharded:
+                pstate.tp_all_reduce(csum)
+            ncols = cols * (tp if cols_sharded else 1)
+            nrows = rows * (tp if rows_sharded else 1)
+            R.mul_(b2).add_((rsum / ncols + 1e-30) * (1 - b2))
+            C.mul_(b2).add_((csum / nrows + 1e-30) * (1 - b2))
+            rtot = R.sum()
+            if rows_sharded:
+                rtot = rtot.clone()
+                pstate.tp_all_reduce(rtot)
+            vhat = R.view(-1, 1) * C.view(1, -1) / (rtot / nrows)
             u = (g2 * torch.rsqrt(torch.clamp(vhat, min=1e-30))).reshape(g.shape)
         else:
             v = self._slot(name, "af_v", g)

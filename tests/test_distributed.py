@@ -197,3 +197,20 @@ def test_tp_mixer_block_matches_single_rank():
         full = ref.store.master_view(name)
         diff = (_gather_tp(ranks, name, full.shape, 2) - full).abs().max().item()
         assert diff < 5e-5, f"TP weight {name} differs by {diff}"
+
+
+@pytest.mark.parametrize("chain", ["adafactor-learning_rate", "graft:adam-learning_rate",
+                                   "adaptive_clip:0.003-adafactor:0.9-momentum:0.9:1:0-learning_rate"])
+def test_tp_optimizer_chains_match_single_rank(chain):
+    """Adafactor's factored statistics (row sums partial when the last dim is head-sharded, column sums and the row
+    factor mean partial when a leading dim is) and graft's norms reduce over TP: every shard matches the single
+    rank"""
+    cfg = dict(CFG, optimizer=chain)
+    ranks = _run("tp", cfg)
+    ref, ref_losses = _single(cfg)
+    for a, b in zip(ranks[0]["losses"], ref_losses):
+        assert abs(a - b) < 1e-4, f"TP loss {a} vs single {b}"
+    for name in ranks[0]["specs"]:
+        full = ref.store.master_view(name)
+        diff = (_gather_tp(ranks, name, full.shape, 2) - full).abs().max().item()
+        assert diff < 5e-5, f"{chain}: TP weight {name} differs by {diff}"

@@ -141,3 +141,70 @@ def test_gpu_orthogonal_init_matches_householder(cuda, shape, monkeypatch):
     assert (q - ref).abs().max().item() < 1e-3
     eye = torch.eye(shape[1])
     assert (q.t() @ q - eye).abs().max().item() < 1e-4
+
+
+def test_fused_adafactor_is_bitwise_deterministic(cuda):
+    """the factored row / column sums are folded in a fixed order (no float atomics): two runs from the same state
+    give identical weights"""
+    cfg = dict(GPT, optimizer="adafactor-learning_rate", calculation_dtype="bfloat16")
+    out = []
+    for _ in range(2):
+        torch.manual_seed(1)
+        m = Model(ModelParameter(cfg), cuda)
+        fused = FusedOptimizer(m.store, m.params)
+        g = torch.Generator(device=cuda).manual_seed(3)
+        for step in range(3):
+            m.store.grad.copy_(torch.randn(m.store.grad.shape, generator=g, device=cuda) * 0.01)
+            fused.step(0.01, step + 1)
+        torch.cuda.synchronize()
+        out.append(m.store.master.clone())
+    assert torch.equal(out[0], out[1])
+
+
+def _tp_opt_worker(rank, world, port, chain, out_dir):
+    import os
+    import torch.distributed as dist
+    from homebrewnlp_mtf_amd.parallel import state as pstate
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)   # gloo reduces the (few, small) CUDA tensors
+    mesh = pstate.Mesh(dp=1, tp=world, rank=rank).build_groups()
+    pstate.set_mesh(mesh)
+    cuda = torch.device("cuda:0")
+    cfg = dict(GPT, optimizer=chain, calculation_dtype="bfloat16", weight_decay=0.01, mesh={"dp": 1, "tp": world})
+    torch.manual_seed(1)
+    m = Model(ModelParameter(cfg), cuda)
+    ref_store = copy.copy(m.store)
+    ref_store.master = m.store.master.clone()
+    ref_store.compute = ref_store.master.to(torch.bfloat16)
+    ref_store.grad = torch.randn_like(m.store.grad) * 0.01
+    m.store.grad.copy_(ref_store.grad)
+    fused = FusedOptimizer(m.store, m.params)
+    ref = ReferenceOptimizer(ref_store, m.params)
+    for step in range(3):
+        fused.step(0.01, step + 1)
+        ref.step(0.01, step + 1)
+        g = torch.randn_like(m.store.grad) * 0.01
+        m.store.grad.copy_(g)
+        ref_store.grad.copy_(g)
+    torch.cuda.synchronize()
+    diff = (m.store.master - ref_store.master).abs().max().item()
+    scale = ref_store.master.abs().max().item()
+    torch.save({"diff": diff, "scale": scale}, os.path.join(out_dir, f"r{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("chain", ["adafactor-learning_rate",
+                                   "adaptive_clip:0.003-adafactor:0.9-momentum:0.9:1:0-learning_rate"])
+def test_fused_adafactor_tp2_matches_reference(chain, tmp_path):
+    """TP=2 (two ranks on one GPU): the fused optimizer's TP-reduced factored statistics, global counts and the
+    row-factor mean match the TP-aware reference optimizer (which tests/test_distributed.py pins to one rank)"""
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    mp.spawn(_tp_opt_worker, args=(2, port, chain, str(tmp_path)), nprocs=2, join=True)
+    for r in range(2):
+        res = torch.load(tmp_path / f"r{r}.pt", weights_only=True)
+        assert res["diff"] < 1e-4 * max(res["scale"], 1.0), f"rank {r}: fused vs reference {res['diff']}"
