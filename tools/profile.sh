@@ -13,5 +13,6 @@ STATS=$(find gpurun_out/prof_$TAG -name "*kernel_stats.csv" | head -1)
 python3 tools/prof_summary.py "$STATS" ${PROF_STEPS:-1} > gpurun_out/prof_$TAG/summary.md
 TRACE=$(find gpurun_out/prof_$TAG -name "*kernel_trace.csv" | head -1)
 python3 tools/prof_steps.py "$TRACE" > gpurun_out/prof_$TAG/steps.md && head -30 gpurun_out/prof_$TAG/steps.md
+[ -n "$PROF_SEQ" ] && python3 tools/prof_seq.py "$TRACE" > gpurun_out/prof_$TAG/seq.txt
 find gpurun_out/prof_$TAG -name "*kernel_trace.csv" -delete
 exit $rc
