@@ -124,6 +124,17 @@ int enabled() {
   return g_enabled;
 }
 
+// which products hipBLASLt takes (OBST_LT_SCOPE): 1 every eligible product, 0 bf16-output products only -- the fp32
+// weight gradients and the fused-activation GEMMs then run on the hand-written gemm4w kernel
+int g_scope = -1;
+int scope() {
+  if (g_scope < 0) {
+    const char* e = getenv("OBST_LT_SCOPE");
+    g_scope = e ? atoi(e) : 1;
+  }
+  return g_scope;
+}
+
 hipblasLtMatrixLayout_t layout(hipDataType t, uint64_t rows, uint64_t cols, int64_t ld, int batch, long long stride) {
   hipblasLtMatrixLayout_t l = nullptr;
   if (hipblasLtMatrixLayoutCreate(&l, t, rows, cols, ld) != HIPBLAS_STATUS_SUCCESS) return nullptr;
@@ -226,6 +237,7 @@ Plan make_plan(State& S, const Key& k, const Runner& run_in) {
 // Python layer (ops/raw.py) splits an activation GEMM into a plain hipBLASLt GEMM plus the elementwise kernel.
 int obst_blaslt_gemm(const ObstGemmDesc* d, hipStream_t stream) {
   if (!enabled() || d->tri != 0 || d->kin != 0) return 1;
+  if (d->out_f32 && scope() == 0) return 1;
   int epi = 0;
   if (d->act == 0) {
     if (d->mode != 0 || d->Zout || d->Zin) return 1;
@@ -387,6 +399,13 @@ OBST_API int obst_blaslt_stats(long long* out) {
 }
 
 // runtime switch (tests run the plain GEMM cases on both paths); returns the previous setting
+// v >= 0 sets the scope (OBST_LT_SCOPE); returns the previous one
+OBST_API int obst_blaslt_scope(int v) {
+  const int old = scope();
+  if (v >= 0) g_scope = v;
+  return old;
+}
+
 OBST_API int obst_blaslt_set(int on) {
   const int old = enabled();
   g_enabled = on;

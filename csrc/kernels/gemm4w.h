@@ -372,7 +372,11 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs p) {
       tmark = now;
     }
 
-    if (p.act == 0 && p.mode == 0 && p.Zout == nullptr) {
+    // gelu GEMMs (bf16, no residual) take the direct epilogue too: forward with the pre-activation kept in Zout,
+    // backward C = acc * gelu'(Zin); each variant's activation is straight-line code (no per-value switch)
+    const bool gelu_direct = !OUT_F32 && p.act == ACT_GELU && p.R == nullptr &&
+                             ((p.mode == 0) || (p.mode == 1 && p.Zin != nullptr));
+    if ((p.act == 0 && p.mode == 0 && p.Zout == nullptr) || gelu_direct) {
       // Direct epilogue (every plain product): each lane owns C[m][n..n+3] of 64 fragments and writes it with one
       // buffer store from the accumulators (bf16: 8 B, fp32: 16 B); one per-lane offset, the fragment row in the
       // SGPR offset, the fragment column in the instruction's immediate; rows past M fall outside the resource
@@ -395,14 +399,29 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs p) {
       // 32 / 64 per wave (64 bf16 stores with the 32 LDS-DMAs in flight overflowed the 63-entry vmcnt)
       const int voff = (int)(((long long)(wm * 128 + ml) * ldc + wn * 128 + 8 * gq) * ES);
       const int nbase = ct.n0 + wn * 128 + 8 * gq;
-      auto emit = [&](auto exc, auto edc) {
+      // Zout / Zin share C's leading dimension and batch offset (bf16)
+      const i32x4_t rz4 = make_rsrc(p.Zout ? reinterpret_cast<const char*>(p.Zout) + ct.coff * 2 + corg : cbase, cext);
+      const __amdgpu_buffer_rsrc_t rzi =
+          make_brsrc(p.Zin ? reinterpret_cast<const char*>(p.Zin) + ct.coff * 2 + corg : cbase, cext);
+      const bool zout = p.Zout != nullptr;
+      // AC: 0 no activation, 1 gelu forward (+ Zout), 2 gelu backward (Zin)
+      auto emit = [&](auto exc, auto edc, auto acc_) {
         constexpr bool EX = decltype(exc)::value, ED = decltype(edc)::value;
+        constexpr int AC = decltype(acc_)::value;
         // one fragment row at a time: with EX its residual / C loads are issued together and consumed after,
         // bounded by the fences (unbounded, the scheduler hoisted all 64 loads: 256 VGPRs, spills)
         static_for<8>([&](auto ic) {
           constexpr int i = decltype(ic)::value;
           const int soff = __builtin_amdgcn_readfirstlane((int)(i * 16 * ldc * ES));
           f32x4_t x[8];
+          if constexpr (AC == 2) {
+            static_for<4>([&](auto pc) {
+              constexpr int pp = decltype(pc)::value;
+              const v4u32_t o = __builtin_amdgcn_raw_buffer_load_b128(rzi, voff, soff + pp * 64, 0);
+              x[2 * pp] = f32x4_t{bf2f(o[0] & 0xffff), bf2f(o[0] >> 16), bf2f(o[1] & 0xffff), bf2f(o[1] >> 16)};
+              x[2 * pp + 1] = f32x4_t{bf2f(o[2] & 0xffff), bf2f(o[2] >> 16), bf2f(o[3] & 0xffff), bf2f(o[3] >> 16)};
+            });
+          }
           if constexpr (EX) {
             static_for<4>([&](auto pc) {
               constexpr int pp = decltype(pc)::value;
@@ -431,6 +450,23 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs p) {
               va += x[2 * pp];
               vb += x[2 * pp + 1];
             }
+            if constexpr (AC == 1) {
+              if (zout)
+                store16_padded(v4u32_t{pack_bf16x2(va[0], va[1]), pack_bf16x2(va[2], va[3]),
+                                       pack_bf16x2(vb[0], vb[1]), pack_bf16x2(vb[2], vb[3])},
+                               voff, rz4, soff, std::integral_constant<int, pp * 64>{});
+#pragma unroll
+              for (int t = 0; t < 4; ++t) {
+                va[t] = act_fwd(ACT_GELU, va[t]);
+                vb[t] = act_fwd(ACT_GELU, vb[t]);
+              }
+            } else if constexpr (AC == 2) {
+#pragma unroll
+              for (int t = 0; t < 4; ++t) {
+                va[t] *= act_grad(ACT_GELU, x[2 * pp][t]);
+                vb[t] *= act_grad(ACT_GELU, x[2 * pp + 1][t]);
+              }
+            }
             if constexpr (OUT_F32) {
               store16_padded(va, voff, rc4, soff, std::integral_constant<int, pp * 128>{});
               store16_padded(vb, voff, rc4, soff, std::integral_constant<int, pp * 128 + 16>{});
@@ -446,10 +482,27 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs p) {
       };
       using T_ = std::true_type;
       using F_ = std::false_type;
-      if (extra) {
-        if (edge) emit(T_{}, T_{}); else emit(T_{}, F_{});
+      using A0 = std::integral_constant<int, 0>;
+      if constexpr (!OUT_F32) {
+        if (gelu_direct) {
+          using A1 = std::integral_constant<int, 1>;
+          using A2 = std::integral_constant<int, 2>;
+          if (p.mode == 1) {
+            if (edge) emit(F_{}, T_{}, A2{}); else emit(F_{}, F_{}, A2{});
+          } else {
+            if (edge) emit(F_{}, T_{}, A1{}); else emit(F_{}, F_{}, A1{});
+          }
+        } else if (extra) {
+          if (edge) emit(T_{}, T_{}, A0{}); else emit(T_{}, F_{}, A0{});
+        } else {
+          if (edge) emit(F_{}, T_{}, A0{}); else emit(F_{}, F_{}, A0{});
+        }
       } else {
-        if (edge) emit(F_{}, T_{}); else emit(F_{}, F_{});
+        if (extra) {
+          if (edge) emit(T_{}, T_{}, A0{}); else emit(T_{}, F_{}, A0{});
+        } else {
+          if (edge) emit(F_{}, T_{}, A0{}); else emit(F_{}, F_{}, A0{});
+        }
       }
     } else {
       // Epilogue through a wave-private 8 KiB LDS region past the two stages (the stages already hold the next

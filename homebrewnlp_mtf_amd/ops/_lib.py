@@ -103,6 +103,9 @@ _SIGS = {
     "obst_opt_factored": [ctypes.POINTER(OptDesc), c_p, c_p, c_i, c_p, c_i, c_p, c_p, c_p],
     "obst_blaslt_enabled": [],
     "obst_blaslt_set": [c_i],
+    "obst_blaslt_scope": [c_i],
+    "obst_gemm4w_enabled": [],
+    "obst_gemm4w_set": [c_i],
     "obst_blaslt_splitk_set": [c_i],
     "obst_blaslt_stats": [c_p],
     "obst_glu": [c_p, c_p, c_p, c_p, c_p, c_ll, c_p],

@@ -146,7 +146,7 @@ def tokens_transposed(x2, rows: int, cols: int) -> typing.Optional[torch.Tensor]
     """[rows][cols] bf16 -> [cols][rows] (None where the plain transposed-read GEMM is used instead)"""
     if not _KCONTIG or not raw.on_gpu(x2) or x2.dtype != torch.bfloat16 or rows % 8 or cols % 8:
         return None
-    if raw.lt_enabled():
+    if raw.lt_takes_f32() or raw.g4w_enabled():   # both read the token-strided layouts at full rate
         return None
     out = torch.empty(cols * rows, dtype=x2.dtype, device=x2.device)
     raw.transpose(x2, out, rows, cols, cols, rows)
@@ -165,7 +165,7 @@ def _wgrad_gemm(x2, dy2, gw, plan: LinearPlan, xT=None, dyT=None, beta: float = 
     M, H, K, N = plan.M, plan.H, plan.K, plan.N
     if xT is None:
         xT = tokens_transposed(x2, M, H * K)
-    lt_big = (xT is None and dyT is None and raw.on_gpu(x2) and raw.lt_enabled() and H == 1 and M % 8 == 0
+    lt_big = (xT is None and dyT is None and raw.on_gpu(x2) and raw.lt_takes_f32() and H == 1 and M % 8 == 0
               and K % 8 == 0 and N % 8 == 0)
     if lt_big and N >= 2 * K and N >= 4096:
         # hipBLASLt reads a token-contiguous x ~20 % faster than the token-strided one (tools/bench_wgrad.py); the
@@ -380,7 +380,7 @@ class _DotAttention(torch.autograd.Function):
         dbase = _empty(p_in.canon_o_shape, xc)
         _kqv_dgrad(dkqv, ws, dbase, p_out, act, z)
         baseT = None
-        if raw.on_gpu(base) and raw.lt_enabled() and T % 8 == 0 and K % 8 == 0:
+        if raw.on_gpu(base) and raw.lt_takes_f32() and T % 8 == 0 and K % 8 == 0:
             # one transpose of base serves the three q/k/v weight gradients (tools/bench_wgrad.py: -118 us each
             # against the token-strided layout, for one 122 us transpose)
             baseT = torch.empty(K * T, dtype=base.dtype, device=base.device)

@@ -44,6 +44,35 @@ def lt_enabled() -> int:
     return _LT
 
 
+_LT_SCOPE = None
+
+
+def lt_scope() -> int:
+    """which products hipBLASLt takes when it is on: 1 every eligible one, 0 only the bf16-output products (the fp32
+    weight gradients and the fused-activation GEMMs run on the hand-written gemm4w kernel; OBST_LT_SCOPE)"""
+    global _LT_SCOPE
+    if _LT_SCOPE is None:
+        _LT_SCOPE = int(L.lib().obst_blaslt_scope(-1))
+    return _LT_SCOPE
+
+
+def lt_scope_set(v: int) -> int:
+    global _LT_SCOPE
+    old = int(L.lib().obst_blaslt_scope(int(v)))
+    _LT_SCOPE = int(v)
+    return old
+
+
+def g4w_enabled() -> bool:
+    """the one-wave-per-SIMD 256x256 MFMA kernel (csrc/kernels/gemm4w.h) takes the plain products hipBLASLt declines"""
+    return bool(L.lib().obst_gemm4w_enabled())
+
+
+def lt_takes_f32() -> bool:
+    """hipBLASLt runs the fp32-output (weight-gradient) products"""
+    return lt_enabled() > 0 and lt_scope() > 0
+
+
 def lt_stats() -> typing.Tuple[int, int]:
     """(GEMMs dispatched to hipBLASLt, eligible GEMMs it declined -- those ran on the MFMA kernels)"""
     out = (ctypes.c_longlong * 2)()
@@ -196,7 +225,8 @@ def gemm(a: Operand, b: Operand, c: Operand, M: int, N: int, K: int, batch: typi
         L.check(L.lib().obst_skinny_gemm(a.t.data_ptr(), a.ld, b.t.data_ptr(), b.ld, c.t.data_ptr(), c.ld, M, N, K,
                                          L.ptr(ws), L.stream_ptr()), "skinny_gemm")
         return c.t
-    if (not kin and on_gpu(c.t) and act is not None and tri == 0 and lt_enabled() == 1 and c.t.dtype == torch.bfloat16
+    if (not kin and on_gpu(c.t) and act is not None and tri == 0 and lt_enabled() == 1 and lt_scope() > 0
+            and c.t.dtype == torch.bfloat16
             and b1 * b2 == 1 and c.ld == N and (M * N) % 8 == 0 and c.t.is_contiguous() and c.t.numel() == M * N):
         # activation GEMM on hipBLASLt: plain product, then the elementwise kernel (pre-activation kept in Zout)
         if not act_bwd:
