@@ -137,3 +137,85 @@ def test_video2tfrecord_and_jannet_loader(tmp_path):
     src2 = V.VideoSource(files, p, batch=2, device="cpu", workers=2)
     src2.restore(st)
     assert torch.equal(src2.next()["frame"], nxt["frame"])
+
+
+WORD_VTT = """WEBVTT
+Kind: captions
+Language: en
+
+00:00:00.000 --> 00:00:02.000 align:start position:0%
+hello<00:00:00.500><c> big</c><00:00:01.000><c> world</c>
+
+00:00:02.000 --> 00:00:04.000 align:start position:0%
+again<00:00:02.600><c> and</c><00:00:03.100><c> more</c>
+"""
+
+CUE_VTT = """WEBVTT
+
+1
+00:00:01.000 --> 00:00:03.000
+one two
+three four
+
+2
+00:00:03.000 --> 00:00:04.000
+five
+"""
+
+
+def test_decode_vtt_word_timed_and_cues():
+    import video2tfrecord as V2
+    text, words, stamps = V2.decode_vtt(WORD_VTT)
+    # each piece is stamped with the inline stamp that closes it; the line's last word runs into the next line
+    # text after the last stamp joins the last group
+    assert words == [" hello", " big", " world again", " and more"] and stamps == [0.5, 1.0, 2.6, 3.1]
+    assert text == "".join(words)
+    text, words, stamps = V2.decode_vtt(CUE_VTT)
+    assert words == [" one", " two", " three", " four", " five"]       # cue numbers are not caption text
+    assert stamps == [1.0, 1.5, 2.0, 2.5, 3.0] and text == " one two three four five"
+
+
+def test_split_equal_balances_longest_first():
+    import video2tfrecord as V2
+    ids, dur = V2.split_equal(list("abcdef"), [900, 800, 300, 700, 100, 260], 2)
+    assert ids == [["a", "c", "f"], ["b", "d"]] and dur == [[900, 300, 260], [800, 700]]   # e (100) is too short
+    ids, _ = V2.split_equal(list("ab"), [1, 2], 3, min_duration=0)
+    assert ids == [["b"], ["a"], []]
+
+
+def test_word_split_encoders():
+    import video2tfrecord as V2
+    words = [" hello", " big", " world again"]
+    enc = V2._Tokenizer(None)            # byte-level: one token per byte
+    groups = V2.bpe_with_word_split(enc, words, "".join(words))
+    # a token that is only spaces matches anywhere, so the group before takes it (BPE merges the space into the
+    # next word's token, byte-level tokens keep it separate)
+    assert [bytes(g).decode() for g in groups] == [" hello ", "big ", "world again"]
+    assert V2.char_level_encoder([" hi"]) == [[32, 104, 105]]
+
+
+def test_video2tfrecord_subtitles_and_text_only_frames(tmp_path):
+    """a .vtt next to the video: words reach the frame whose window they end in; overflow beyond
+    language_token_per_frame - 1 tokens goes to text-only skip_frame frames; a separator frame joins two videos"""
+    pytest.importorskip("PIL")
+    import video2tfrecord as V2
+    rng = np.random.default_rng(1)
+    for k in range(2):
+        np.save(tmp_path / f"v{k}.npy", rng.integers(0, 256, (4, 8, 16, 3), dtype=np.uint8))
+        (tmp_path / f"v{k}.vtt").write_text(CUE_VTT)
+    out = tmp_path / "tfr"
+    # 4 frames at 1 fps: windows end at 1, 2, 3, 4 s
+    assert V2.main(["--out", str(out), "--name", "s", "--width", "16", "--height", "8", "--subtitles",
+                    "--encoder", "char", "--fps", "1", "--language-token-per-frame", "4", "--padding-token", "0",
+                    "--concat-token", "7", str(tmp_path / "v0.npy"), str(tmp_path / "v1.npy")]) == 0
+    (f,) = [str(out / n) for n in os.listdir(out)]
+    exs = [T.Example(r) for r in T.read_records(f)]
+    rows = [(e.int64("skip_frame")[0], e.int64("concat")[0], e.int64("mask")[0],
+             bytes(int(t) for t in e.int64("tokens")[:e.int64("mask")[0]] if 0 < int(t) < 256)) for e in exs]
+    half = rows[:len(rows) // 2]
+    # frame 0 (window 0-1 s): nothing stamped before 1.0; frame 1 (-2 s): " one" " two" = 8 chars -> 3 + 3 + 2
+    assert half[0] == (0, 0, 0, b"")
+    assert [r[3] for r in half[1:4]] == [b" on", b"e t", b"wo"] and [r[0] for r in half[1:4]] == [0, 1, 1]
+    sep = rows[len(rows) // 2]
+    assert sep[:3] == (0, 1, 4) and list(exs[len(rows) // 2].int64("tokens")) == [7, 7, 7, 7]
+    assert rows[len(rows) // 2 + 1:] == half
