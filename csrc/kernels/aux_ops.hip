@@ -175,7 +175,7 @@ __global__ __launch_bounds__(NTH) void pkm_gather_bwd_kernel(const int* __restri
     for (int f = lane; f < Fk; f += 64) {
       const float d = bf2f(DY[r * Fk + f]);
       acc += d * bf2f(table[row + f]);
-      atomicAdd(dtable + row + f, d * s);
+      if (dtable) atomicAdd(dtable + row + f, d * s);   // null: dtable by the deterministic sorted scatter
     }
     acc = wave_sum(acc);
     if (lane == 0) dval[r] = acc;

@@ -169,6 +169,87 @@ __global__ __launch_bounds__(NTH) void scatter_sorted_kernel(const int* __restri
   }
 }
 
+// Chunked form of the same (bounded work per block under skewed ids -- a padding id can own tens of thousands of
+// rows): the sorted order is cut into fixed chunks of SC_CH positions. A run of equal ids that lies inside one chunk
+// is summed and added to its table row by that chunk's block. A run that crosses a chunk boundary leaves one partial
+// row per chunk it touches: "head" (the chunk's first run, continued from before) or "tail" (the chunk's last run,
+// continuing after); the fold block of the chunk where the run starts adds its tail and the following heads in chunk
+// order. Every sum has a fixed order: bitwise reproducible. scale (optional, per ORIGINAL row): dy[r] * scale[r].
+constexpr int SC_CH = 64;
+
+__device__ __forceinline__ void sc_row(const bf16_t* DY, const float* scale, long long r, int F, int c0, float (&acc)[8]) {
+  float d[8];
+  unpack8(*reinterpret_cast<const uint4*>(DY + r * F + c0), d);
+  const float sv = scale ? scale[r] : 1.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) acc[e] += d[e] * sv;
+}
+
+__device__ __forceinline__ void sc_add(float* dst, int c0, const float (&acc)[8]) {
+  float4* o = reinterpret_cast<float4*>(dst + c0);
+  float4 a = o[0], b = o[1];
+  a.x += acc[0]; a.y += acc[1]; a.z += acc[2]; a.w += acc[3];
+  b.x += acc[4]; b.y += acc[5]; b.z += acc[6]; b.w += acc[7];
+  o[0] = a;
+  o[1] = b;
+}
+
+__device__ __forceinline__ void sc_put(float* dst, int c0, const float (&acc)[8]) {
+  reinterpret_cast<float4*>(dst + c0)[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+  reinterpret_cast<float4*>(dst + c0)[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
+}
+
+// ws: head [nchunk][F] then tail [nchunk][F]
+__global__ __launch_bounds__(NTH) void scatter_chunk_kernel(const int* __restrict__ sidx, const long long* __restrict__ perm,
+                                                            const bf16_t* __restrict__ DY, const float* __restrict__ scale,
+                                                            float* __restrict__ dE, float* __restrict__ ws, long long T,
+                                                            int F) {
+  const long long c = blockIdx.x, nchunk = gridDim.x;
+  const long long p0 = c * SC_CH, p1 = p0 + SC_CH < T ? p0 + SC_CH : T;
+  const bool from_prev = p0 > 0 && sidx[p0 - 1] == sidx[p0];
+  const bool to_next = p1 < T && sidx[p1] == sidx[p1 - 1];
+  float* head = ws + c * F;
+  float* tail = ws + (nchunk + c) * F;
+  for (int c0 = threadIdx.x * 8; c0 < F; c0 += NTH * 8) {
+    long long i = p0;
+    while (i < p1) {
+      const int key = sidx[i];
+      float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      long long j = i;
+      for (; j < p1 && sidx[j] == key; ++j) sc_row(DY, scale, perm[j], F, c0, acc);
+      const bool first = i == p0 && from_prev, last = j == p1 && to_next;
+      if (first) sc_put(head, c0, acc);            // continued run (also when it spans the whole chunk)
+      else if (last) sc_put(tail, c0, acc);        // run starting here, continuing after
+      else sc_add(dE + (long long)key * F, c0, acc);
+      i = j;
+    }
+  }
+}
+
+__global__ __launch_bounds__(NTH) void scatter_fold_kernel(const int* __restrict__ sidx, float* __restrict__ dE,
+                                                           const float* __restrict__ ws, long long T, int F) {
+  const long long c = blockIdx.x, nchunk = gridDim.x;
+  const long long p0 = c * SC_CH, p1 = p0 + SC_CH < T ? p0 + SC_CH : T;
+  if (!(p1 < T && sidx[p1] == sidx[p1 - 1])) return;                  // the chunk's last run ends here
+  const int key = sidx[p1 - 1];
+  if (p0 > 0 && sidx[p0 - 1] == key && sidx[p0] == key) return;       // the run started in an earlier chunk
+  for (int c0 = threadIdx.x * 8; c0 < F; c0 += NTH * 8) {
+    float acc[8];
+    const float4 a = reinterpret_cast<const float4*>(ws + (nchunk + c) * F + c0)[0];
+    const float4 b = reinterpret_cast<const float4*>(ws + (nchunk + c) * F + c0)[1];
+    acc[0] = a.x; acc[1] = a.y; acc[2] = a.z; acc[3] = a.w; acc[4] = b.x; acc[5] = b.y; acc[6] = b.z; acc[7] = b.w;
+    for (long long k = c + 1; k < nchunk; ++k) {
+      const float4 x = reinterpret_cast<const float4*>(ws + k * F + c0)[0];
+      const float4 y = reinterpret_cast<const float4*>(ws + k * F + c0)[1];
+      acc[0] += x.x; acc[1] += x.y; acc[2] += x.z; acc[3] += x.w; acc[4] += y.x; acc[5] += y.y; acc[6] += y.z;
+      acc[7] += y.w;
+      const long long q1 = (k + 1) * SC_CH < T ? (k + 1) * SC_CH : T;
+      if (sidx[q1 - 1] != key || q1 == T || sidx[q1] != key) break;    // the run ends inside chunk k
+    }
+    sc_add(dE + (long long)key * F, c0, acc);
+  }
+}
+
 // cumulative sum over the sequence axis of x viewed as [outer, S, inner]; reverse for the gradient; cummean
 // divides by (position + 1) (backward of cummean = reverse-cumsum of dy / (pos+1)).
 __global__ __launch_bounds__(NTH) void cumsum_kernel(const bf16_t* __restrict__ X, bf16_t* __restrict__ Y,
@@ -283,6 +364,21 @@ OBST_API int obst_scatter_add_sorted(const int* sidx, const long long* perm, con
   if ((((uintptr_t)DY) | ((uintptr_t)dE)) & 15) return -2;
   hipLaunchKernelGGL(scatter_sorted_kernel, dim3((unsigned)T), dim3(NTH), 0, st, sidx, perm, (const bf16_t*)DY, dE,
                      T, F);
+  return (int)hipGetLastError();
+}
+
+// workspace floats of obst_scatter_add_chunked
+OBST_API long long obst_scatter_ws(long long T, int F) { return 2 * ((T + SC_CH - 1) / SC_CH) * (long long)F; }
+
+// dE[sidx[i]] += DY[perm[i]] (* scale[perm[i]]) over the stable-sorted ids sidx, deterministic, bounded per block
+OBST_API int obst_scatter_add_chunked(const int* sidx, const long long* perm, const void* DY, const float* scale,
+                                      float* dE, long long T, int F, float* ws, hipStream_t st) {
+  if (F % 8 || T <= 0 || !ws) return -1;
+  if ((((uintptr_t)DY) | ((uintptr_t)dE) | ((uintptr_t)ws)) & 15) return -2;
+  const unsigned nchunk = (unsigned)((T + SC_CH - 1) / SC_CH);
+  hipLaunchKernelGGL(scatter_chunk_kernel, dim3(nchunk), dim3(NTH), 0, st, sidx, perm, (const bf16_t*)DY, scale, dE, ws,
+                     T, F);
+  hipLaunchKernelGGL(scatter_fold_kernel, dim3(nchunk), dim3(NTH), 0, st, sidx, dE, ws, T, F);
   return (int)hipGetLastError();
 }
 

@@ -255,7 +255,7 @@ __device__ __forceinline__ void apply_elems(const ApplyArgs& a, const OptTensor&
       a.master[gi] = w[0];
       if (a.compute) a.compute[gi] = f2bf(w[0]);
     }
-  } else {
+  } else if (a.uout) {   // null: a statistics-only segment (graft's probe of its inner stage)
     if (V == 4) *reinterpret_cast<float4*>(a.uout + gi) = make_float4(g[0], g[1], g[2], g[3]);
     else a.uout[gi] = g[0];
   }
@@ -485,7 +485,7 @@ __device__ __forceinline__ void finish_elems(const ApplyArgs& a, const OptTensor
       a.master[gi] = w[0];
       if (a.compute) a.compute[gi] = f2bf(w[0]);
     }
-  } else {
+  } else if (a.uout) {   // null: a statistics-only segment (graft's probe of its inner stage)
     if (V == 4) *reinterpret_cast<float4*>(a.uout + gi) = make_float4(g[0], g[1], g[2], g[3]);
     else a.uout[gi] = g[0];
   }

@@ -89,6 +89,8 @@ _SIGS = {
     "obst_scatter_add_sorted": [c_p, c_p, c_p, c_p, c_ll, c_i, c_p],
     "obst_gather": [c_p, c_p, c_p, c_ll, c_i, c_i, c_p],
     "obst_scatter_add": [c_p, c_p, c_p, c_ll, c_i, c_i, c_p],
+    "obst_scatter_add_chunked": [c_p, c_p, c_p, c_p, c_p, c_ll, c_i, c_p, c_p],
+    "obst_scatter_ws": [c_ll, c_i],
     "obst_cumsum": [c_p, c_p, c_ll, c_i, c_ll, c_i, c_i, c_i, c_p],
     "obst_cast_f32_bf16": [c_p, c_p, c_ll, c_p],
     "obst_transpose": [c_p, c_p, c_ll, c_ll, c_ll, c_ll, c_i, c_ll, c_ll, c_p],
@@ -124,7 +126,7 @@ _SIGS = {
     "obst_skinny_ws": [c_i, c_i, c_i],
     "obst_decode_attn": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_f, c_i, c_p, c_p],
 }
-_RESTYPES = {"obst_norm_bwd_ws": c_ll, "obst_skinny_ws": c_ll}
+_RESTYPES = {"obst_norm_bwd_ws": c_ll, "obst_skinny_ws": c_ll, "obst_scatter_ws": c_ll}
 
 
 def lib():

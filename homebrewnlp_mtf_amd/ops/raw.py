@@ -645,15 +645,31 @@ def scatter_add(idx, dy, dtable, T: int, F: int, V: int):
         _need(dy, T * F - 1, "dy")
         _need(dtable, V * F - 1, "dtable")
         if F % 8 == 0 and dy.data_ptr() % 16 == 0 and dtable.data_ptr() % 16 == 0:
-            # deterministic: stable sort of the (clamped) ids, then one owner block per table row
+            # deterministic: stable sort of the (clamped) ids, then fixed 64-row chunks of the sorted order with a
+            # fixed-order fold of the runs that cross chunks (bounded work per block under skewed ids)
             sidx, perm = torch.sort(idx.reshape(-1)[:T].clamp(0, V - 1).to(torch.int32), stable=True)
-            L.check(L.lib().obst_scatter_add_sorted(sidx.data_ptr(), perm.data_ptr(), dy.data_ptr(),
-                                                    dtable.data_ptr(), T, F, L.stream_ptr()), "scatter_add_sorted")
+            sorted_scatter(sidx, perm, dy, None, dtable, T, F)
             return
         L.check(L.lib().obst_scatter_add(idx.data_ptr(), dy.data_ptr(), dtable.data_ptr(), T, F, V, L.stream_ptr()),
                 "scatter_add")
         return
     dtable.reshape(V, F).index_add_(0, idx.reshape(T).long().clamp(0, V - 1), _f(dy.reshape(T, F)).to(dtable.dtype))
+
+
+_SCATTER_WS = {}
+
+
+def sorted_scatter(sidx, perm, dy, scale, dtable, T: int, F: int):
+    """dtable[sidx[i]] += dy[perm[i]] (* scale[perm[i]]) for stable-sorted int32 ids sidx and int64 perm: the
+    deterministic chunked scatter (csrc/kernels/elementwise.hip scatter_chunk / scatter_fold)"""
+    n = int(L.lib().obst_scatter_ws(T, F))
+    ws = _SCATTER_WS.get(dy.device)
+    if ws is None or ws.numel() < n:
+        ws = torch.empty(max(n, 1 << 16), dtype=torch.float32, device=dy.device)
+        _SCATTER_WS[dy.device] = ws
+    L.check(L.lib().obst_scatter_add_chunked(sidx.data_ptr(), perm.data_ptr(), dy.data_ptr(), L.ptr(scale),
+                                             dtable.data_ptr(), T, F, ws.data_ptr(), L.stream_ptr()),
+            "scatter_add_chunked")
 
 
 def cumsum(x, y, outer: int, S: int, inner: int, reverse: bool, mean: bool, grad: bool):
@@ -823,9 +839,15 @@ def pkm_gather_bwd(idx, val, table, dy, dtable, dval, R: int, H: int, Fk: int, P
         _need(dtable, P * H * Fk - 1, "dtable")
         _need(dy, R * Fk - 1, "dy")
         _need(dval, R - 1, "dval")
+        det = Fk % 8 == 0 and dy.data_ptr() % 16 == 0 and dtable.data_ptr() % 16 == 0 and val.dtype == torch.float32
         L.check(L.lib().obst_pkm_gather_bwd(idx.data_ptr(), val.data_ptr(), table.data_ptr(), dy.data_ptr(),
-                                            dtable.data_ptr(), dval.data_ptr(), R, H, Fk, P, L.stream_ptr()),
-                "pkm_gather_bwd")
+                                            0 if det else dtable.data_ptr(), dval.data_ptr(), R, H, Fk, P,
+                                            L.stream_ptr()), "pkm_gather_bwd")
+        if det:   # dtable rows (value, head) through the deterministic sorted scatter, scaled by val
+            rows = (idx.reshape(-1)[:R].long().clamp(0, P - 1) * H +
+                    torch.arange(R, device=idx.device) % H).to(torch.int32)
+            sidx, perm = torch.sort(rows, stable=True)
+            sorted_scatter(sidx, perm, dy, val.reshape(-1), dtable, R, Fk)
         return None
     rows = idx.reshape(R).long().clamp(0, P - 1) * H + torch.arange(R, device=idx.device) % H
     d = _f(dy.reshape(R, Fk))

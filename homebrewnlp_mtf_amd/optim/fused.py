@@ -45,10 +45,17 @@ class Segment:
         self.stages: typing.List[typing.Tuple[str, tuple]] = []
         self.emit_stats = False
         self.emit_factored = False
+        self.stats_only = False    # no output: graft's probe of its inner stage (only sum(h^2) is kept)
+        self.reuse_input = False   # reads the previous segment's INPUT (graft applies its factor to g, not h)
+        self.save_sq = False       # keep sum(g^2) of the input before this segment's statistics replace it
+
+
+def _graft_inner_ok(args) -> bool:
+    return bool(args) and args[0] in OP and args[0] not in REDUCTIONS and args[0] not in ("graft", "scale", "none")
 
 
 def supported(chain: str) -> bool:
-    return all(n != "graft" for n, _ in parse_chain(chain))
+    return all(n != "graft" or _graft_inner_ok(a) for n, a in parse_chain(chain))
 
 
 def compile_chain(chain: str) -> typing.Tuple[typing.List[Segment], bool, bool]:
@@ -63,6 +70,27 @@ def compile_chain(chain: str) -> typing.Tuple[typing.List[Segment], bool, bool]:
     wc = any(n == "weight_centralisation" for n, _ in stages)
     first = True
     for n, a in stages:
+        if n == "graft":
+            # graft:<inner> (ref src/optimizer/optimizers.py:145-151): u = g * |inner(g)| / |g| per tensor. The
+            # probe segment runs the inner stage (its state advances once) for sum(h^2) only; the next segment
+            # re-reads g and scales it (opener "graft"), then the chain continues
+            if not _graft_inner_ok(a):
+                raise ValueError(f"graft over {a!r} is not fused")
+            if not first:
+                segs[-1].emit_stats = True        # sum(g^2) of the graft input
+            probe = Segment()
+            probe.stages = [(a[0], tuple(a[1:]))]
+            probe.stats_only = probe.emit_stats = probe.save_sq = True
+            apply = Segment()
+            apply.opener = ("graft", ())
+            apply.reuse_input = True
+            apply.stages = [("scale", ())]
+            if first:
+                segs = [probe, apply]
+            else:
+                segs += [probe, apply]
+            first = False
+            continue
         if n in REDUCTIONS:
             if first and n != "adafactor":
                 segs[0].opener = (n, a)          # statistics of the raw gradient come from the stats pass
@@ -249,9 +277,10 @@ class FusedOptimizer:
             rs[rows_sharded] = 1.0
             self.af_rows_sharded = rs.view(-1, 1)
             self.af_factored = torch.tensor([1.0 if t[5] else 0.0 for t in self.tinfo], **f32)
-        nseg = len(self.segments) + int(self.pre_factored)
-        self.u = torch.empty(total, **f32) if nseg > 1 else None
-        self.u2 = torch.empty(total, **f32) if nseg > 2 else None
+        n_out = sum(1 for sg in self.segments[:-1] if not sg.stats_only) + int(self.pre_factored)
+        self.u = torch.empty(total, **f32) if n_out >= 1 else None
+        self.u2 = torch.empty(total, **f32) if n_out >= 2 else None
+        self.graft_g2 = torch.zeros(self.ntensors, **f32) if any(sg.save_sq for sg in self.segments) else None
         self.flip = 0
         # [lr, step_count] on the device: the kernels read them from here, so a captured step (hipGraph replay,
         # Trainer with use_hip_graphs) sees each step's values; ``external_dyn``: the caller fills them
@@ -306,6 +335,12 @@ class FusedOptimizer:
             st.copy_(part + st * (1 - self.shard_mask))
 
     def _scalar(self, d, stage):
+        if stage[0] == "graft":    # F[0] = sqrt(sum h^2 / sum g^2) (0 where g is all zero: no NaN update)
+            st, fac = self.stats.view(-1, 8), self.facs.view(-1, 8)
+            g2 = self.graft_g2
+            fac[:, 0] = torch.where(g2 > 0, torch.sqrt(st[:, 0]) * torch.rsqrt(g2.clamp(min=1e-38)),
+                                    torch.zeros_like(g2))
+            return
         self._set_stages(d, [stage])
         L.check(L.lib().obst_opt_scalar(d, L.stream_ptr()), "opt_scalar")
         if stage[0] == "adafactor" and self.tp > 1:
@@ -341,7 +376,7 @@ class FusedOptimizer:
             self._scalar(d, ("weight_centralisation", ()))
         if self.sm3 is not None:
             self.sm3[1 - self.flip].zero_()
-        src = None    # None = raw gradient
+        src = prev_src = None    # None = raw gradient
         bufs = [self.u, self.u2]
         bi = 0
         if self.pre_factored:
@@ -356,8 +391,13 @@ class FusedOptimizer:
             if seg.opener is not None:
                 self._scalar(d, seg.opener)
             last = k == len(segs) - 1
+            if seg.reuse_input:
+                src = prev_src
+            prev_src = src
+            if seg.save_sq:
+                self.graft_g2.copy_(self.stats.view(-1, 8)[:, 0])
             d.uin = 0 if src is None else src.data_ptr()
-            d.uout = 0 if last else bufs[bi].data_ptr()
+            d.uout = 0 if (last or seg.stats_only) else bufs[bi].data_ptr()
             self._set_stages(d, seg.stages)
             d.final_seg, d.emit_stats, d.emit_factored = int(last), int(seg.emit_stats), 0
             if self.use_rows:
@@ -373,7 +413,7 @@ class FusedOptimizer:
                 self._reduce_stats()
             if seg.emit_factored:
                 self._factored(d, bufs[bi])
-            if not last:
+            if not last and not seg.stats_only:
                 src, bi = bufs[bi], 1 - bi
         self.store.bump()
         if self.sm3 is not None:

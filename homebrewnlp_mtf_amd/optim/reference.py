@@ -191,7 +191,10 @@ class ReferenceOptimizer:
         if opt == "graft":
             inner, *iargs = args
             h = self.apply_stage(name, inner, tuple(iargs), g, w, ctx, grads, global_sq_ref)
-            return g * torch.rsqrt(self._tp_sum(name, (g * g).sum())) * torch.sqrt(self._tp_sum(name, (h * h).sum()))
+            g2 = self._tp_sum(name, (g * g).sum())
+            # an all-zero g gets a zero update (the reference's rsqrt(0) * 0 makes it NaN)
+            return torch.where(g2 > 0, g * torch.rsqrt(g2.clamp(min=1e-38)), torch.zeros_like(g)) * \
+                torch.sqrt(self._tp_sum(name, (h * h).sum()))
         raise ValueError(opt)
 
     # -- checkpoint -----------------------------------------------------------------------------------------------

@@ -284,6 +284,57 @@ def test_gather_scatter(cuda):
     _close(res[str(cuda)][1], res["cpu"][1], 1e-3, 1e-3, "scatter_add")
 
 
+@pytest.mark.parametrize("dist", ["uniform", "zipf", "padding30", "one_id"])
+def test_scatter_add_skewed_ids_deterministic(cuda, dist):
+    """the chunked sorted scatter (64-row chunks, fixed-order fold of runs crossing chunks) on skewed id
+    distributions: matches the fp32 oracle and repeats bitwise"""
+    g = torch.Generator().manual_seed(11)
+    V, Fd, T = 512, 72, 5000
+    if dist == "uniform":
+        idx = torch.randint(0, V, (T,), generator=g)
+    elif dist == "zipf":
+        p = 1.0 / torch.arange(1, V + 1, dtype=torch.float64) ** 1.2
+        idx = torch.multinomial(p / p.sum(), T, replacement=True, generator=g)
+    elif dist == "padding30":
+        idx = torch.randint(0, V, (T,), generator=g)
+        idx[torch.rand(T, generator=g) < 0.3] = 7
+    else:
+        idx = torch.full((T,), 3)
+    idx = idx.to(torch.int32)
+    dy = torch.randn(T * Fd, generator=g).to(BF)
+    ref = torch.zeros(V * Fd)
+    raw.scatter_add(idx, dy, ref, T, Fd, V)
+    outs = []
+    for _ in range(2):
+        dt = torch.ones(V * Fd, device=cuda)
+        raw.scatter_add(idx.to(cuda), dy.to(cuda), dt, T, Fd, V)
+        outs.append(dt)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    _close(outs[0] - 1, ref, 2e-3, 1e-3, f"scatter_add {dist}")
+
+
+def test_pkm_gather_bwd_deterministic(cuda):
+    torch.manual_seed(4)
+    R, H, Fk, P = 3000, 4, 32, 64
+    idx = torch.randint(0, P, (R,), dtype=torch.int32)
+    idx[:1000] = 5                                   # a hot value row
+    val = torch.randn(R)
+    table = torch.randn(P * H * Fk).to(BF)
+    dy = torch.randn(R * Fk).to(BF)
+    dt_ref, dv_ref = torch.zeros(P * H * Fk), torch.zeros(R)
+    raw.pkm_gather_bwd(idx, val, table, dy, dt_ref, dv_ref, R, H, Fk, P)
+    outs = []
+    for _ in range(2):
+        dt, dv = torch.zeros(P * H * Fk, device=cuda), torch.zeros(R, device=cuda)
+        raw.pkm_gather_bwd(idx.to(cuda), val.to(cuda), table.to(cuda), dy.to(cuda), dt, dv, R, H, Fk, P)
+        outs.append((dt, dv))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    _close(outs[0][0], dt_ref, 2e-3, 1e-3, "pkm dtable")
+    _close(outs[0][1], dv_ref, 2e-3, 1e-3, "pkm dval")
+
+
 def test_cumsum(cuda):
     torch.manual_seed(9)
     x = torch.randn(2, 50, 3, 8).to(BF)

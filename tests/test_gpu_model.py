@@ -71,7 +71,8 @@ def test_model_forward_backward(cuda, variant):
                                    "global_l2norm_clip:0.5-novograd-learning_rate",
                                    "sm3-l2norm_clip:0.1-momentum:0.9:1:0-learning_rate",
                                    "adafactor-learning_rate", "gradient_centralisation-value_clip:0.01-adam-"
-                                                              "learning_rate-weight_centralisation"])
+                                                              "learning_rate-weight_centralisation",
+                                   "graft:adam-learning_rate", "value_clip:0.01-graft:sm3-momentum:0.9:1:0-learning_rate"])
 @pytest.mark.parametrize("rows", ["1", "0"], ids=["row_tiled", "generic"])
 def test_fused_optimizer_matches_reference(cuda, chain, rows, monkeypatch):
     monkeypatch.setenv("OBST_OPT_ROWS", rows)

@@ -136,13 +136,19 @@ DET_BLOCKS = {
 }
 
 
-@pytest.mark.parametrize("blocks", sorted(DET_BLOCKS))
-def test_training_is_bitwise_deterministic(cuda, blocks):
+DET_CASES = [(b, CFG["optimizer"]) for b in sorted(DET_BLOCKS)] + [
+    ("gpt", "adafactor-learning_rate"), ("gpt", "graft:adam-learning_rate"), ("pkm", CFG["optimizer"])]
+DET_BLOCKS["pkm"] = [{"layer": ["norm-shift-scale", "product_key_memory"]},
+                     {"layer": ["norm-shift-scale", "attention-dot_product-context"]}]
+
+
+@pytest.mark.parametrize("blocks,optimizer", DET_CASES)
+def test_training_is_bitwise_deterministic(cuda, blocks, optimizer):
     """same seed, same batches -> bit-identical losses, weights and optimizer state after several steps (norm
     parameter gradients, the embedding scatter-add, rezero / MoE reductions and the optimizer statistics are all
     fixed-order reductions; SURVEY 5.2 deterministic-mode requirement)"""
     pstate.set_mesh(pstate.Mesh())
-    cfg = dict(CFG, memory_reduction_strategy="none", block_config=DET_BLOCKS[blocks], experts=8)
+    cfg = dict(CFG, memory_reduction_strategy="none", block_config=DET_BLOCKS[blocks], experts=8, optimizer=optimizer)
     runs = []
     for _ in range(2):
         torch.manual_seed(0)

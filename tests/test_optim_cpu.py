@@ -132,7 +132,14 @@ def test_fused_chain_compilation():
     assert len(segs) == 2 and segs[0].emit_stats and segs[1].opener[0] == "l2norm_clip"
     segs, pre, wc = fused.compile_chain("adafactor-learning_rate")
     assert pre and [s.opener[0] if s.opener else None for s in segs] == [None, "adafactor", "adafactor_clip"]
-    assert not fused.supported("graft:adam-learning_rate")
+    assert fused.supported("graft:adam-learning_rate") and not fused.supported("graft:adafactor-learning_rate")
+    # graft first: probe (inner adam, statistics only) on the raw gradient, then the scaled raw gradient
+    segs, pre, wc = fused.compile_chain("graft:adam-learning_rate")
+    assert [(s.stats_only, s.reuse_input, s.opener) for s in segs] == [(True, False, None), (False, True, ("graft", ()))]
+    assert [n for n, _ in segs[1].stages] == ["scale", "learning_rate"]
+    # graft later in the chain: the segment before emits sum(g^2)
+    segs, pre, wc = fused.compile_chain("value_clip:1-graft:sm3-momentum:0.9:1:0-learning_rate")
+    assert segs[0].emit_stats and segs[1].stats_only and segs[1].save_sq and segs[2].reuse_input
 
 
 def test_grad_accumulation_matches_full_batch():
