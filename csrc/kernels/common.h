@@ -49,8 +49,11 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
   return __builtin_bit_cast(bf16_t, (__bf16)f);
 }
 
+typedef __bf16 obst_bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float obst_f32x2_t __attribute__((ext_vector_type(2)));
+// one v_cvt_pk_bf16_f32 (two scalar conversions + shift + or were four instructions)
 __device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
-  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((obst_f32x2_t{lo, hi}), obst_bf16x2_t));
 }
 
 __device__ __forceinline__ float wave_sum(float v) {
@@ -92,7 +95,10 @@ __device__ __forceinline__ float softplusf_(float x) { return x > 20.f ? x : log
 // the libm tanhf (~30 VALU with range branches) -- the elementwise gelu passes were VALU-bound
 __device__ __forceinline__ float gelu_s(float x) {   // sigmoid(2u), u = k0 (x + k1 x^3)
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  return __frcp_rn(1.f + __expf(-2.f * k0 * (x + k1 * x * x * x)));
+  // v_exp_f32 (2^x) and v_rcp_f32 directly: __frcp_rn is a correctly rounded reciprocal (a Newton sequence), and
+  // the gelu epilogues of the one-wave-per-SIMD GEMM are issue-bound on these instructions
+  const float t = -2.f * k0 * 1.4426950408889634f * (x + k1 * x * x * x);
+  return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(t));
 }
 
 __device__ __forceinline__ float act_fwd(int act, float x) {

@@ -121,7 +121,9 @@ class FusedOptimizer:
         self.names = names
         dev = store.device
         self.tp = pstate.tp_size()
-        chain_names = {n for n, _ in parse_chain(self.chain)}
+        # stage names incl. graft's inner stage (graft:adam needs adam's state)
+        chain_names = {n for n, _ in parse_chain(self.chain)} | {a[0] for n, a in parse_chain(self.chain)
+                                                                 if n == "graft" and a}
         need_sm3 = "sm3" in chain_names
         need_mom = "momentum" in chain_names or "novograd" in chain_names
         need_adam = "adam" in chain_names
@@ -427,7 +429,7 @@ class FusedOptimizer:
         """views of the optimizer state per variable, keyed like the reference's slot variables
         (``<var>/<optimizer string with : -> _>/<slot>``, src/optimizer/backend.py:23-25) and like
         ``ReferenceOptimizer.state_dict`` -- so checkpoints move between the fused and the reference optimizer."""
-        chain = {n for n, _ in parse_chain(self.chain)}
+        chain = {n for n, _ in parse_chain(self.chain)} | {a[0] for n, a in parse_chain(self.chain) if n == "graft" and a}
         opt_str = self.chain.replace(':', '_')
         out: typing.Dict[str, torch.Tensor] = {}
         for ti, name in enumerate(self.names):
