@@ -238,8 +238,7 @@ def feed_forward(args: BlockArgs) -> Act:
         try:
             p1 = F.linear_plan(tuple(x.dims), tuple(D.deduplicate(old1 + new1)), tuple(mdims))
             p2 = F.linear_plan(tuple(mdims), tuple(D.deduplicate(old2 + new2)), tuple(odims))
-            ok = (p1.x_perm is None and p1.o_perm is None and p2.x_perm is None and p2.o_perm is None and
-                  not (pstate.tp_size() > 1 and (p1.row_parallel or p2.row_parallel)))
+            ok = p1.x_perm is None and p1.o_perm is None and p2.x_perm is None and p2.o_perm is None
         except (NotImplementedError, ValueError):
             ok = False
         if ok:
@@ -436,8 +435,6 @@ def _attention_fast_ok(args: BlockArgs, ins, outs) -> bool:
     if len(x.dims) != 4 or x.dims[2:] != list(p.feature_dims) or x.dims[1].name != "sequence":
         return False
     if D.get_attention_dim(p, x.dims).dim != x.dims[1]:
-        return False
-    if pstate.tp_size() > 1 and next((a for a in ins if a in ACTIVATIONS), None) is not None:
         return False
     return True
 

@@ -280,13 +280,25 @@ class _FFN(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w1, w2, p1: LinearPlan, p2: LinearPlan, act, residual, carrier=None):
         xc = x.contiguous()
+        tp = pstate.tp_size() > 1
         z = _empty(p1.canon_o_shape, xc)
         a = _empty(p1.canon_o_shape, xc) if act else z
-        _fwd_gemm(xc, w1, a, p1, act=act, Zout=z if act else None)
-        if p1.row_parallel and pstate.tp_size() > 1:
-            raise NotImplementedError
+        if tp and p1.row_parallel:
+            # W1 contracts the sharded heads: the pre-activation is a partial sum -- reduce it, then activate
+            _fwd_gemm(xc, w1, z, p1)
+            pstate.tp_all_reduce(z)
+            if act:
+                raw.elementwise("act", z, a, act=act)
+        else:
+            _fwd_gemm(xc, w1, a, p1, act=act, Zout=z if act else None)
         y = _empty(p2.canon_o_shape, xc)
-        _fwd_gemm(a, w2, y, p2, R=residual.contiguous() if residual is not None else None)
+        if tp and p2.row_parallel:   # partial output: reduce before the residual joins
+            _fwd_gemm(a, w2, y, p2)
+            pstate.tp_all_reduce(y)
+            if residual is not None:
+                raw.elementwise("add", y, y, z=residual.contiguous())
+        else:
+            _fwd_gemm(a, w2, y, p2, R=residual.contiguous() if residual is not None else None)
         ctx.save_for_backward(xc, w1, w2, z, a if act else None)
         ctx.p1, ctx.p2, ctx.act, ctx.has_res = p1, p2, act, residual is not None
         ctx.carrier = carrier
@@ -299,13 +311,20 @@ class _FFN(torch.autograd.Function):
         a = z if a is None else a
         dy = dy.contiguous()
         # dZ = (dY W2^T) * act'(Z) in ONE gemm epilogue
+        tp = pstate.tp_size() > 1
         dz = _empty(p1.canon_o_shape, dy)
+        # act'(z) is the same on every TP rank (z is replicated), so the fused act-backward epilogue commutes with
+        # the all-reduce of the partial dz (W2 contracting the sharded heads)
         _dgrad_gemm(dy, w2, dz, p2, act=act, Zin=z if act else None)
+        if tp and p2.col_parallel:
+            pstate.tp_all_reduce(dz)
         g2, m2, b2 = _acc_grad_beta(w2)
         _wgrad_gemm(a, dy, g2, p2, beta=b2)
         _done(w2)
         dx = _empty(xc.shape, xc)
         _dgrad_gemm(dz, w1, dx, p1)
+        if tp and p1.col_parallel:
+            pstate.tp_all_reduce(dx)
         g1, m1, b1 = _acc_grad_beta(w1)
         _wgrad_gemm(xc, dz, g1, p1, beta=b1)
         _done(w1)
@@ -341,9 +360,15 @@ class _DotAttention(torch.autograd.Function):
         xc = x.contiguous()
         base = _empty(p_in.canon_o_shape, xc)
         z = _empty(p_in.canon_o_shape, xc) if act else None
-        _fwd_gemm(xc, w_in, base, p_in, act=act, Zout=z)
         if p_in.row_parallel and pstate.tp_size() > 1:
-            pstate.tp_all_reduce(base)
+            # partial sums over the sharded heads: reduce the pre-activation, then activate
+            pre = z if act else base
+            _fwd_gemm(xc, w_in, pre, p_in)
+            pstate.tp_all_reduce(pre)
+            if act:
+                raw.elementwise("act", z, base, act=act)
+        else:
+            _fwd_gemm(xc, w_in, base, p_in, act=act, Zout=z)
         T, K, N = p_out.M, p_out.K, p_out.N
         kqv = _empty([T, 3 * N], xc)
         _kqv_fwd(base, (w_k, w_q, w_v), kqv, p_out)
@@ -394,8 +419,7 @@ class _DotAttention(torch.autograd.Function):
             _done(ws[j])
             outs.append(None if m else g.to(ws[j].dtype))
         if p_out.col_parallel and pstate.tp_size() > 1:
-            if act:
-                raise NotImplementedError("TP + activated attention input")
+            # act'(z) is replicated over TP, so the activation-backward fused into the dgrad commutes with the sum
             pstate.tp_all_reduce(dbase)
         dx = _empty(xc.shape, xc)
         _dgrad_gemm(dbase, w_in, dx, p_in)
@@ -462,6 +486,8 @@ def dot_attention(x, w_in, w_k, w_q, w_v, xdims, w_in_dims, base_dims, w_out_dim
                   residual=None, carrier=None):
     p_in = linear_plan(tuple(xdims), tuple(w_in_dims), tuple(base_dims))
     p_out = linear_plan(tuple(base_dims), tuple(w_out_dims), tuple(xdims))
+    if p_out.H != 1:   # decided before any GEMM or collective runs (the caller falls back to the generic path)
+        raise NotImplementedError("interleaved k|q|v projection needs plain [K][N] weights")
     return _DotAttention.apply(x, w_in, w_k, w_q, w_v, p_in, p_out, act, scale, causal, residual, geo, carrier)
 
 

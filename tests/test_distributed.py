@@ -96,9 +96,14 @@ def test_dp_matches_single_rank():
     assert abs((ranks[0]["losses"][0] + ranks[1]["losses"][0]) / 2 - ref_losses[0]) < 1e-5
 
 
-@pytest.mark.parametrize("strategy", ["none", "revnet"])
+@pytest.mark.parametrize("strategy", ["none", "revnet", "activated_attention_input"])
 def test_tp_matches_single_rank(strategy):
-    cfg = dict(CFG, memory_reduction_strategy=strategy)
+    """fused FFN (W1 contracts the sharded heads: reduce-then-activate; dz reduced after the fused act-backward) and
+    the fused attention block, also with an activated input projection"""
+    cfg = dict(CFG, memory_reduction_strategy="none" if strategy != "revnet" else "revnet")
+    if strategy == "activated_attention_input":
+        cfg["block_config"] = [{"layer": ["norm-shift-scale", "attention-dot_product-context-in:gelu"], "skip": True},
+                               {"layer": ["norm-shift-scale-group", "feed_forward-in:relu"], "skip": True}]
     if strategy == "revnet":
         cfg["block_config"] = [{"layer": ["norm-shift-scale", "attention-dot_product-context"]},
                                {"layer": ["norm-shift-scale-group", "feed_forward-in:gelu"]}]
