@@ -260,7 +260,13 @@ int obst_blaslt_gemm(const ObstGemmDesc* d, hipStream_t stream) {
       return 1;
     }
     // a K-contiguous ([N][K], hipBLASLt op T) B together with a broadcast (stride 0) A faulted with an illegal
-    // address on gfx950 / ROCm 7.2 (M 131072, N 2048, K 4096, batch 3): never issue it; the MFMA kernel runs it
+    // address on gfx950 / ROCm 7.2 (M 131072, N 2048, K 4096, batch 3, C columns interleaved with ldc = 3N and
+    // batch stride N, as the k|q|v projection writes them). The descriptors this file builds for it are in range:
+    // A's layout is [K][M] with ld = lda and stride 0 (every batch reads the same A), B's is [K][N] per batch at
+    // stride K*N, C / D [N][M] at ld 3N and stride N, and the tuning scratch D spans sc * (batch - 1) + (M - 1) *
+    // ldc + N elements. Root cause not isolated (reproducing it means faulting the GPU again), so the guard stays
+    // narrow: only this operand class is declined, and the MFMA kernel runs it
+    // (tests/test_gpu_kernels.py::test_gemm_plain_paths[shared_A_batch_bt0]).
     if (d->b_t == 0 && (sa == 0 || sb == 0)) return 1;
   }
   State& S = state();

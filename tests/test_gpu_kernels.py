@@ -96,7 +96,8 @@ def test_gemm_batched_epilogues(cuda, lt):
         assert n1[0] == n0[0] + 1 and n1[1] == n0[1], (n0, n1)
 
 
-@pytest.mark.parametrize("case", ["residual", "f32_accumulate", "shared_A_batch", "two_level_batch"])
+@pytest.mark.parametrize("case", ["residual", "f32_accumulate", "shared_A_batch", "shared_A_batch_bt0",
+                                  "two_level_batch"])
 def test_gemm_plain_paths(cuda, lt, case):
     """the plain-GEMM shapes the model issues (residual input, fp32 accumulate, q/k/v batch over one input)"""
     torch.manual_seed(5)
@@ -118,6 +119,12 @@ def test_gemm_plain_paths(cuda, lt, case):
             C = torch.zeros(H * M * N, dtype=BF, device=dev)
             raw.gemm(raw.Operand(a, 0, K, 0), raw.Operand(b, 1, N, K * N), raw.Operand(C, 0, N, M * N), M, N, K,
                      batch=(H, 1))
+        elif case == "shared_A_batch_bt0":
+            # the class hipBLASLt faulted on (broadcast A, K-contiguous B, interleaved C columns as in the k|q|v
+            # projection): blaslt.cpp declines it, the MFMA kernel runs it
+            C = torch.zeros(M * H * N, dtype=BF, device=dev)
+            raw.gemm(raw.Operand(a, 0, K, 0), raw.Operand(b, 0, K, K * N), raw.Operand(C, 0, H * N, N), M, N, K,
+                     batch=(H, 1))
         else:                            # batch = (2, H) with compatible strides
             C = torch.zeros(2 * H * 64 * N, dtype=BF, device=dev)
             raw.gemm(raw.Operand(a, 0, K, H * 64 * K, 64 * K), raw.Operand(b, 1, N, 0, K * N),
@@ -126,7 +133,9 @@ def test_gemm_plain_paths(cuda, lt, case):
     torch.cuda.synchronize()
     _close(outs[str(cuda)], outs["cpu"], 5e-2, 3e-2, f"plain gemm {case}")
     n1 = raw.lt_stats()
-    if lt and case != "two_level_batch":   # the path under test really ran on hipBLASLt
+    if lt and case == "shared_A_batch_bt0":   # never issued to hipBLASLt: ran on the MFMA kernel
+        assert n1 == n0, (n0, n1)
+    elif lt and case != "two_level_batch":   # the path under test really ran on hipBLASLt
         assert n1[0] == n0[0] + 1 and n1[1] == n0[1], (n0, n1)
 
 
