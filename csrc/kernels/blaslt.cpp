@@ -105,7 +105,7 @@ State& state() {
 }
 
 int g_enabled = -1;
-long long g_calls = 0, g_declined = 0;   // dispatches taken / eligible calls hipBLASLt had no algorithm for
+long long g_calls = 0, g_declined = 0, g_sk_calls = 0;   // dispatches taken / eligible calls hipBLASLt had no algorithm for
 
 bool debug() {
   static int v = -1;
@@ -359,6 +359,7 @@ int splitk_factor(const ObstGemmDesc* d) {
 }  // namespace
 
 int obst_blaslt_gemm_split(const ObstGemmDesc* d, hipStream_t stream) {
+  if (d->out_f32 && scope() == 0) return 1;     // the fp32 products run on gemm4w (OBST_LT_SCOPE=0)
   const int s = splitk_factor(d);
   if (s < 2 || !enabled()) return obst_blaslt_gemm(d, stream);
   if (!g_sk_ws) {
@@ -385,8 +386,13 @@ int obst_blaslt_gemm_split(const ObstGemmDesc* d, hipStream_t stream) {
   b.beta = 0.f;
   const int r = obst_blaslt_gemm(&b, stream);
   if (r != 0) return r == 1 ? obst_blaslt_gemm(d, stream) : r;
-  return obst_splitk_fold((const float*)g_sk_ws, (float*)d->C, d->M, d->N, d->ldc, s, d->beta, stream) == 0 ? 0 : -300;
+  if (obst_splitk_fold((const float*)g_sk_ws, (float*)d->C, d->M, d->N, d->ldc, s, d->beta, stream) != 0) return -300;
+  ++g_sk_calls;
+  return 0;
 }
+
+// split-K products run (batched slabs + fold), for tests
+OBST_API long long obst_blaslt_splitk_calls() { return g_sk_calls; }
 
 OBST_API int obst_blaslt_enabled() { return enabled(); }
 

@@ -106,6 +106,7 @@ _SIGS = {
     "obst_blaslt_enabled": [],
     "obst_blaslt_set": [c_i],
     "obst_blaslt_scope": [c_i],
+    "obst_blaslt_splitk_calls": [],
     "obst_gemm4w_enabled": [],
     "obst_gemm4w_set": [c_i],
     "obst_blaslt_splitk_set": [c_i],
@@ -126,7 +127,7 @@ _SIGS = {
     "obst_skinny_ws": [c_i, c_i, c_i],
     "obst_decode_attn": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_f, c_i, c_p, c_p],
 }
-_RESTYPES = {"obst_norm_bwd_ws": c_ll, "obst_skinny_ws": c_ll, "obst_scatter_ws": c_ll}
+_RESTYPES = {"obst_norm_bwd_ws": c_ll, "obst_skinny_ws": c_ll, "obst_scatter_ws": c_ll, "obst_blaslt_splitk_calls": c_ll}
 
 
 def lib():

@@ -8,6 +8,7 @@ import math
 import pytest
 import torch
 
+from homebrewnlp_mtf_amd.ops import _lib as L
 from homebrewnlp_mtf_amd.ops import raw
 from homebrewnlp_mtf_amd.ops import functional as F
 
@@ -175,30 +176,57 @@ def test_gemm_oob_rejected(cuda):
 
 
 # ----------------------------------------------------------------------------------------------------------------
-@pytest.mark.parametrize("D", [32, 64, 96, 128])
-@pytest.mark.parametrize("S,causal", [(128, True), (200, True), (256, False), (64, True), (576, True), (1000, False)])
-def test_attention_fwd_bwd(cuda, D, S, causal):
-    torch.manual_seed(D + S)
-    B, H = 2, 3
-    ld = H * D
+def _attention_case(cuda, B, S, H, D, causal, layout):
+    """layout "separate": q, k, v, o each [T][H*D]; "kqv": q, k, v (and dq, dk, dv) column slices of ONE
+    [T][3*H*D] buffer with o / do at their own stride H*D -- the layout training uses (ld != ld_o)"""
+    N = H * D
+    ld = 3 * N if layout == "kqv" else N
     scale = D ** -0.5
-    q, k, v, do = [(torch.randn(B * S * ld) * 0.8).to(BF) for _ in range(4)]
+    T = B * S
+    g = torch.Generator().manual_seed(D + S + H)
+    if layout == "kqv":
+        buf = (torch.randn(T, 3 * N, generator=g) * 0.8).to(BF)
+        k, q, v = buf[:, :N], buf[:, N:2 * N], buf[:, 2 * N:]
+    else:
+        q, k, v = [(torch.randn(T, N, generator=g) * 0.8).to(BF) for _ in range(3)]
+    do = (torch.randn(T, N, generator=g) * 0.8).to(BF)
     res = {}
     for dev in ("cpu", cuda):
-        t = [x.to(dev) for x in (q, k, v, do)]
-        o = torch.zeros(B * S * ld, dtype=BF, device=dev)
+        if layout == "kqv":
+            b = buf.to(dev)
+            t = [b[:, N:2 * N], b[:, :N], b[:, 2 * N:]]
+            dbuf = torch.zeros(T, 3 * N, dtype=BF, device=dev)
+            dq, dk, dv = dbuf[:, N:2 * N], dbuf[:, :N], dbuf[:, 2 * N:]
+        else:
+            t = [x.to(dev).reshape(-1) for x in (q, k, v)]
+            dq, dk, dv = [torch.zeros(T * N, dtype=BF, device=dev) for _ in range(3)]
+        o = torch.zeros(T * N, dtype=BF, device=dev)
         lse = torch.zeros(B * H * S, dtype=torch.float32, device=dev)
-        raw.attn_fwd(t[0], t[1], t[2], o, lse, B, S, H, D, ld, scale, causal)
-        dq, dk, dv = [torch.zeros(B * S * ld, dtype=BF, device=dev) for _ in range(3)]
+        raw.attn_fwd(t[0], t[1], t[2], o, lse, B, S, H, D, ld, scale, causal, ld_o=N)
         delta = torch.zeros(B * H * S, dtype=torch.float32, device=dev)
-        raw.attn_bwd(t[0], t[1], t[2], o, t[3], lse, delta, dq, dk, dv, B, S, H, D, ld, scale, causal)
+        raw.attn_bwd(t[0], t[1], t[2], o, do.reshape(-1).to(dev), lse, delta, dq, dk, dv, B, S, H, D, ld, scale,
+                     causal, ld_o=N)
         res[str(dev)] = (o, lse, dq, dk, dv)
     torch.cuda.synchronize()
-    for name, g, c in zip(["o", "lse", "dq", "dk", "dv"], res[str(cuda)], res["cpu"]):
-        _close(g, c, 3e-2, 3e-2, f"attention D={D} S={S} causal={causal} {name}")
+    for name, gg, c in zip(["o", "lse", "dq", "dk", "dv"], res[str(cuda)], res["cpu"]):
+        _close(gg, c, 3e-2, 3e-2, f"attention B={B} S={S} H={H} D={D} causal={causal} {layout} {name}")
+
+
+@pytest.mark.parametrize("layout", ["separate", "kqv"])
+@pytest.mark.parametrize("D", [32, 64, 96, 128])
+@pytest.mark.parametrize("S,causal", [(128, True), (200, True), (256, False), (64, True), (576, True), (1000, False)])
+def test_attention_fwd_bwd(cuda, D, S, causal, layout):
+    _attention_case(cuda, 2, S, 3, D, causal, layout)
 
 
 @pytest.mark.parametrize("D", [64, 128])
+def test_attention_training_shape(cuda, D):
+    """the step's shape class: S = 2048, H = 16, B = 4, causal, interleaved k|q|v (multi-block causal paths of the
+    forward, dQ and dK/dV kernels against the fp32 oracle)"""
+    _attention_case(cuda, 4, 2048, 16, D, True, "kqv")
+
+
+@pytest.mark.parametrize("D", [64, 96, 128])
 def test_attention_fused_residual(cuda, D):
     """out = bf16(o) + residual written by the forward epilogue == the unfused o, then the elementwise add"""
     torch.manual_seed(3)
@@ -449,8 +477,8 @@ def test_gemm_splitk_wgrad(cuda, a_t, b_t):
 def test_blaslt_splitk_wgrad(cuda, a_t, b_t, beta):
     """hipBLASLt split-K weight gradient (K-slabs as one strided batch + deterministic fold) into a strided fp32 C
     against the fp32 product; bitwise run-to-run"""
-    if not raw.lt_enabled():
-        pytest.skip("hipBLASLt path off")
+    if not raw.lt_takes_f32():
+        pytest.skip("hipBLASLt does not take the fp32 products")
     torch.manual_seed(6)
     M, N, K, ldc = 512, 768, 32768, 1024
     A = (torch.randn(M * K) * 0.5).to(BF)
@@ -463,6 +491,7 @@ def test_blaslt_splitk_wgrad(cuda, a_t, b_t, beta):
     ref = av.float() @ bv.float() + beta * C0[:, :N]
     Ag, Bg = A.to(cuda), B.to(cuda)
     old = raw.lt_splitk_set(True)
+    n0 = L.lib().obst_blaslt_splitk_calls()
     try:
         outs = []
         for _ in range(2):
@@ -473,6 +502,7 @@ def test_blaslt_splitk_wgrad(cuda, a_t, b_t, beta):
         torch.cuda.synchronize()
     finally:
         raw.lt_splitk_set(old)
+    assert L.lib().obst_blaslt_splitk_calls() == n0 + 2, "the split-K path did not run"
     _close(outs[0][:, :N], ref, 5e-2, 1e-2, f"lt splitk {a_t}{b_t}")
     assert torch.equal(outs[0], outs[1])
     assert torch.equal(outs[0][:, N:].cpu(), C0[:, N:]), "columns past N must stay untouched"
