@@ -42,6 +42,12 @@ class KVCache:
         self.mode = "prefill"
         self.pos: typing.Optional[torch.Tensor] = None
         self.idx = 0
+        # sequence-mixing layers other than dot-product attention: the learned token mixer keeps its input
+        # [B, S, H, F] and masked weight, cumsum / cummean their running fp32 sums; keyed by the attention index
+        # (mixers) or ("c", n) (cumsum layers). `unsupported`: a mixing layer ran uncached during the prefill
+        self.states: typing.Dict[typing.Any, dict] = {}
+        self.cidx = 0
+        self.unsupported = False
         # state that outlives one request: cache buffers per layer (reused while the shape stays) and the decode
         # step's hipGraph (Model._decode_graphed), which bakes their addresses in
         self.persist = persist if persist is not None else {"bufs": {}, "graph": None}
@@ -56,6 +62,20 @@ class KVCache:
             old = bufs[i] = (k, v)
             self.persist["graph"] = None
         self.layers[i] = (old[0], old[1], scale)
+
+    def keep_state(self, key, **tensors):
+        """per-layer decode state (persistent buffers reused while shapes stay, like the k / v caches)"""
+        bufs = self.persist["bufs"]
+        old = bufs.get(("state", key))
+        if old is not None and all(k in old and old[k].shape == t.shape and old[k].dtype == t.dtype and
+                                   old[k].device == t.device for k, t in tensors.items()):
+            for k, t in tensors.items():
+                if old[k].data_ptr() != t.data_ptr():
+                    old[k].copy_(t)
+        else:
+            old = bufs[("state", key)] = {k: t.clone() for k, t in tensors.items()}
+            self.persist["graph"] = None
+        self.states[key] = old
 
 
 class Builder:
@@ -93,6 +113,7 @@ class Builder:
         self.dropout_counter = 0
         if self.kv is not None:
             self.kv.idx = 0
+            self.kv.cidx = 0
         if self.register:
             self.use_counts = {}
 

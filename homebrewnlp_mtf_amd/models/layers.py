@@ -409,18 +409,52 @@ def _apply_mask(bias: Act, mask, dim: Dim, tmp: Dim) -> Act:
     return named_einsum([bias, Act(mask, [dim, tmp])], bias.dims)
 
 
-def cumsum(args: BlockArgs) -> Act:
-    """ref spatial.py:26-34."""
+def _cumsum_any(args: BlockArgs, mean: bool) -> Act:
     x = args.tensor
     dim = D.get_attention_dim(args.params, x.dims).dim
-    return Act(F.cumsum(x.t, x.dims.index(dim), mean=False), x.dims)
+    axis = x.dims.index(dim)
+    kv = args.builder.kv
+    if kv is not None and axis == 1 and x.dims[0].name == "batch":
+        # incremental decoding: the running fp32 sums of every position are kept; a decode step adds the new
+        # token's input to the sum at pos - 1
+        key = ("c", kv.cidx)
+        kv.cidx += 1
+        if kv.mode == "prefill":
+            kv.keep_state(key, csum=torch.cumsum(x.t.float(), 1))
+            return Act(F.cumsum(x.t, axis, mean=mean), x.dims)
+        return Act(F.cumsum_step(x.t, kv.states[key]["csum"], kv.pos, mean), x.dims)
+    if kv is not None:
+        kv.unsupported = True
+    return Act(F.cumsum(x.t, axis, mean=mean), x.dims)
+
+
+def cumsum(args: BlockArgs) -> Act:
+    """ref spatial.py:26-34."""
+    return _cumsum_any(args, False)
 
 
 def cummean(args: BlockArgs) -> Act:
     """ref spatial.py:37-39."""
-    x = args.tensor
-    dim = D.get_attention_dim(args.params, x.dims).dim
-    return Act(F.cumsum(x.t, x.dims.index(dim), mean=True), x.dims)
+    return _cumsum_any(args, True)
+
+
+def _mixer_kv(args: BlockArgs, kv, x: Act, dim: Dim, tmp: Dim, causal: bool) -> Act:
+    """the learned token mixer under incremental decoding: the prefill keeps the mixer input [B, S, H, F] and the
+    masked weight; a decode step writes the new token's input at pos[b] and computes output row pos[b] only,
+    y[b, h] = W[h, pos[b], :] · X[b, :, h] (one M = 1 GEMM batched over batch x heads)"""
+    p = args.params
+    i = kv.idx
+    kv.idx += 1
+    if kv.mode == "prefill":
+        bias = embed(args, [p.head_dim, dim, tmp])
+        w = bias.t.detach()
+        wm = torch.tril(w) if causal else w.contiguous()
+        kv.keep_state(i, x=x.t.contiguous(), w=wm)
+        return Act(F.token_mixer(x.t, bias.t, causal), x.dims)
+    st = kv.states[i]
+    full = Dim(dim.name, st["x"].shape[1])
+    embed(args, [p.head_dim, full, anonymize_dim(full)])   # the same variable bookkeeping as the prefill
+    return Act(F.token_mixer_step(x.t, st["x"], st["w"], kv.pos), x.dims)
 
 
 def _attention_fast_ok(args: BlockArgs, ins, outs) -> bool:
@@ -509,8 +543,13 @@ def attention(args: BlockArgs) -> Act:
             pass
 
     if _mixer_fast_ok(args, x, dim):
+        kv = args.builder.kv
+        if kv is not None and causal:
+            return _mixer_kv(args, kv, x, dim, tmp, causal)
         bias = embed(args, [p.head_dim, dim, tmp])
         return Act(F.token_mixer(x.t, bias.t, causal), x.dims)
+    if args.builder.kv is not None:
+        args.builder.kv.unsupported = True     # the composable path below has no incremental form
 
     base = None
     if 'dot_product' in args or 'input_as_value' not in args:

@@ -108,11 +108,13 @@ class Model:
         p = self.params
         cfg = " ".join(str(c.layer) for c in list(p.block_configs) + list(p.input_block_configs) +
                        list(p.output_block_configs))
-        mixing = ("cumsum", "cummean", "convolution", "transpose_sequence_features", "biased_", "scale_attention_map",
-                  "embedded", "positional", "input_as_value", "shared_key_value")
+        # cumsum / cummean and the learned token mixer (biased_attention_map on input_as_value) decode from their
+        # own caches (layers._cumsum_any / _mixer_kv); a layer that runs uncached during the prefill makes it fail
+        mixing = ("convolution", "transpose_sequence_features", "biased_softmax", "scale_attention_map",
+                  "embedded", "positional", "shared_key_value")
         return (p.use_language and not p.use_video and not p.use_initial_position_embedding
                 and not p.input_block_configs and not p.output_block_configs and self.builder.tp_size == 1
-                and "attention" in cfg and not any(m in cfg for m in mixing)
+                and ("attention" in cfg or "cumsum" in cfg or "cummean" in cfg) and not any(m in cfg for m in mixing)
                 and not (p.contrastive_across_samples or p.contrastive_across_token_embeddings))
 
     @torch.no_grad()
@@ -128,8 +130,8 @@ class Model:
         except BaseException:
             self.builder.kv = None
             raise
-        if kv.idx != self.builder.params.attention_idx or kv.idx == 0:
-            self.builder.kv = None          # an attention layer bypassed the cache: not decodable incrementally
+        if kv.idx != self.builder.params.attention_idx or (kv.idx == 0 and kv.cidx == 0) or kv.unsupported:
+            self.builder.kv = None          # a mixing layer bypassed the cache: not decodable incrementally
             raise NotImplementedError("body is not KV-cache decodable")
         kv.mode = "decode"
         return out

@@ -547,6 +547,36 @@ def token_mixer(x, w, causal: bool):
     return _TokenMixer.apply(x, w, causal)
 
 
+@torch.no_grad()
+def token_mixer_step(x_new, xc, wm, pos):
+    """one decode step of the token mixer: x_new [B, 1, H, F] joins the cached inputs xc [B, S, H, F] at pos [B];
+    returns y [B, 1, H, F] with y[b, 0, h] = wm[h, pos[b], :] · xc[b, :, h] (wm masked: entries past pos are 0)"""
+    B, _, H, Fd = x_new.shape
+    S = xc.shape[1]
+    rows = torch.arange(B, device=xc.device)
+    xc[rows, pos] = x_new[:, 0].to(xc.dtype)
+    wr = wm.index_select(1, pos).permute(1, 0, 2).contiguous()        # [B, H, S]: the query rows
+    y = torch.empty(B, 1, H, Fd, dtype=x_new.dtype, device=x_new.device)
+    hf = H * Fd
+    raw.gemm(raw.Operand(wr, 0, S, H * S, S), raw.Operand(xc, 1, hf, S * hf, Fd), raw.Operand(y, 0, hf, hf, Fd),
+             1, Fd, S, batch=(B, H))
+    return y
+
+
+@torch.no_grad()
+def cumsum_step(x_new, csum, pos, mean: bool):
+    """one decode step of cumsum / cummean: csum [B, S, ...] fp32 running sums (updated at pos [B])"""
+    B = x_new.shape[0]
+    rows = torch.arange(B, device=csum.device)
+    prev = csum[rows, (pos - 1).clamp(min=0)]
+    prev = torch.where((pos > 0).view([B] + [1] * (prev.dim() - 1)), prev, torch.zeros_like(prev))
+    cur = prev + x_new[:, 0].float()
+    csum[rows, pos] = cur
+    if mean:
+        cur = cur / (pos + 1).to(cur.dtype).view([B] + [1] * (cur.dim() - 1))
+    return cur.to(x_new.dtype).unsqueeze(1)
+
+
 # ================================================================================================================
 # general attention core on already-projected q, k, v [B, S, H, D] (used by the composable attention path)
 class _AttnCore(torch.autograd.Function):

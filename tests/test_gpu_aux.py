@@ -237,3 +237,33 @@ def test_kv_cache_sampling_gpu(cuda):
     # bf16 logits of a single-token forward vs a full-context forward can flip near-ties: compare prefix agreement
     agree = (a == b).float().mean().item()
     assert agree > 0.95, agree
+
+
+def test_mixer_incremental_sampling_gpu(cuda):
+    """ctx32_mixer's body (RevNet, grouped norms, depth-shared learned token mixer) decodes incrementally on the
+    GPU (M = 1 mixer GEMM over the cached inputs per step) with the full-recompute sampler's tokens"""
+    from homebrewnlp_mtf_amd.parallel import state as pstate
+    from homebrewnlp_mtf_amd.run.infer import Sampler
+    pstate.set_mesh(pstate.Mesh())
+    torch.manual_seed(0)
+    p = ModelParameter(dict(model_mode="gpt", use_video=False, use_language=True, heads=4, features_per_head=64,
+                            depth=2, sequence_length=128, train_batch_size=2, vocab_size=256, group_linear_factor=2,
+                            memory_reduction_strategy="revnet", calculation_dtype="bfloat16",
+                            storage_dtype="bfloat16",
+                            block_config=[{"layer": ["norm-shift-scale-features-group",
+                                                     "bottleneck_group_linear-in:relu-mid:relu-mid:norm-mid:shift-mid:"
+                                                     "scale-mid:features"]},
+                                          {"layer": ["norm-shift-scale-features-group",
+                                                     "attention-biased_attention_map-absolute-input_as_value-shared",
+                                                     "norm-shift-scale-features-group", "activation-gelu",
+                                                     "attention-biased_attention_map-absolute-input_as_value-shared"]}
+                                          ]))
+    m = Model(p, cuda)
+    assert m.supports_kv_cache()
+    x = torch.randint(0, 256, (2, 128, 1), device=cuda)
+    a = Sampler(m, p, cuda).sample(x, [5, 40], 0.0, [90, 128])
+    full = Sampler(m, p, cuda)
+    full.kv_cache = False
+    b = full.sample(x, [5, 40], 0.0, [90, 128])
+    agree = (a == b).float().mean().item()
+    assert agree > 0.95, agree

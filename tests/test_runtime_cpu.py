@@ -219,3 +219,46 @@ def test_kv_cache_decoding_matches_full_recompute(strategy, monkeypatch):
         assert len(calls) == n_dec > 0               # the cached sampler decoded incrementally, the other did not
         assert torch.equal(a, b), (a - b).abs().max()
     assert m.builder.kv is None
+
+
+MIXER_BLOCKS = {
+    # ctx32_mixer's body at toy size (configs/ctx32_mixer.json): group norms, bottleneck, shared learned token mixer
+    "ctx32_mixer": [{"layer": ["norm-shift-scale-features-group",
+                               "bottleneck_group_linear-in:relu-mid:relu-mid:norm-mid:shift-mid:scale-mid:features"]},
+                    {"layer": ["norm-shift-scale-features-group",
+                               "attention-biased_attention_map-absolute-input_as_value-shared",
+                               "norm-shift-scale-features-group", "activation-gelu",
+                               "attention-biased_attention_map-absolute-input_as_value-shared"]}],
+    "cumsum": [{"layer": ["norm-shift-scale", "cumsum", "feed_forward-in:relu"]},
+               {"layer": ["norm-shift-scale", "cummean"]}],
+}
+
+
+@pytest.mark.parametrize("body", sorted(MIXER_BLOCKS))
+def test_mixer_incremental_decoding_matches_full_recompute(body, monkeypatch):
+    """the token-mixer / cumsum / RevNet bodies decode incrementally (per-layer input caches and running sums)
+    with the same tokens as the full recompute"""
+    from homebrewnlp_mtf_amd.ops import functional as F
+    from homebrewnlp_mtf_amd.run.infer import Sampler
+    from homebrewnlp_mtf_amd.models.model import Model
+    pstate.set_mesh(pstate.Mesh())
+    torch.manual_seed(0)
+    p = ModelParameter(dict(CFG, train_batch_size=3, memory_reduction_strategy="revnet", group_linear_factor=2,
+                            block_config=MIXER_BLOCKS[body], vocab_size=64))
+    m = Model(p, "cpu")
+    assert m.supports_kv_cache()
+    calls = []
+    for name in ("token_mixer_step", "cumsum_step"):
+        real = getattr(F, name)
+        monkeypatch.setattr(F, name, (lambda r: lambda *a, **k: (calls.append(1), r(*a, **k))[1])(real))
+    x = torch.randint(0, 64, (3, 16, 1), generator=torch.Generator().manual_seed(4))
+    for temp in (0.0, [0.0, 1.0, 3.0]):
+        cached = Sampler(m, p, "cpu")
+        full = Sampler(m, p, "cpu")
+        full.kv_cache = False
+        a = cached.sample(x, [3, 7, 1], temp, [16, 12, 9])
+        n_dec = len(calls)
+        b = full.sample(x, [3, 7, 1], temp, [16, 12, 9])
+        assert len(calls) == n_dec > 0
+        assert torch.equal(a, b), (a - b).abs().max()
+    assert m.builder.kv is None
