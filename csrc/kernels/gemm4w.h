@@ -479,6 +479,9 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs p) {
           });
           fence();
         });
+        // loads into VGPRs pending at the loop back edge make the compiler's wait model drain vmcnt (the in-flight
+        // LDS-DMAs of the next tile included) at the top of every K-tile: retire them on this path
+        if constexpr (EX || AC == 2) __builtin_amdgcn_s_waitcnt(0x0f70);
       };
       using T_ = std::true_type;
       using F_ = std::false_type;
@@ -532,6 +535,7 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs p) {
         }
         fence();
       });
+      __builtin_amdgcn_s_waitcnt(0x0f70);   // residual / spill reloads retired here (see emit)
     }
     fence();
     if (stamp) {
