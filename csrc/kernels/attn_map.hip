@@ -1,0 +1,477 @@
+// K04 variants: the reference's dot-product attention with learned per-head maps (src/model/spatial.py:54-81)
+// that the main flash kernels (attention.hip) do not take -- an additive map on the logits before the softmax
+// ('biased_softmax'), a multiplicative map on the probabilities after it ('scale_attention_map'), or both -- on
+// token-major [B, S, H, D] q / k / v, without any [B, H, S, S] tensor:
+//
+//   s_qk = scale q.k + b_qk (keys <= query when causal),  m_q / l_q its running max / exp-sum,
+//   o_q  = sum_k c_qk e^{s_qk - m_q} v_k / l_q,   lse_q = m_q + log l_q          (c = 1 without a scale map)
+//
+// Backward (P_qk = e^{s_qk - lse_q}; delta_q = do_q . o_q = sum_k P_qk c_qk (do_q . v_k)):
+//   dv_k = sum_q P_qk c_qk do_q,  dP_qk = do_q . v_k,  ds_qk = P_qk (c_qk dP_qk - delta_q),
+//   dq = scale sum_k ds_qk k_k,  dk = scale sum_q ds_qk q_q,  db = sum_batch ds,  dc = sum_batch P dP.
+//
+// Kernels: forward and dq (+ delta) per (64-query block, head, batch); dk/dv per (64-key block, head, batch
+// slice) walking its batches and query blocks in a fixed order, so the map gradients (sums over the batch)
+// accumulate in place by plain read-modify-write of the workgroup's own key columns -- no atomics; batch slices
+// > 1 write separate partial maps that map_fold_kernel sums in slice order (deterministic).
+//
+// MFMA layout (v_mfma_f32_16x16x32_bf16; C: lane holds column lane & 15, rows 4 (lane >> 4) + r): the query-major
+// kernels compute the score tile transposed (rows = keys, columns = queries), so each lane owns one query and the
+// softmax statistics are lane-local (two xor-shuffles across the 4 lane groups). The probability registers feed the
+// next MFMA's B operand directly under a permuted contraction order -- slots 0-3 = rows 4g..4g+3 of one 16-row
+// tile, slots 4-7 = the same rows of the next -- and the matching A operand is read from a transposed LDS image
+// with the same permutation (frag_tp). The key-major dk/dv kernel does the same with queries and keys swapped.
+#include "common.h"
+
+namespace {
+
+constexpr int TQ = 64;    // queries per workgroup (16 per wave)
+constexpr int TK = 64;    // keys per tile
+constexpr int PADR = 8;   // row pad of the row-major images [64][D + PADR] (16-B fragment reads conflict-free)
+constexpr int PADT = 8;   // row pad of the transposed images [D][64 + PADT]
+
+struct MapArgs {
+  const bf16_t* q;
+  const bf16_t* k;
+  const bf16_t* v;
+  const bf16_t* o;
+  const bf16_t* dO;
+  bf16_t* out;
+  bf16_t* dq;
+  bf16_t* dk;
+  bf16_t* dv;
+  const float* bias;   // [H][S][S] or null
+  const float* cmap;   // [H][S][S] or null
+  float* dbias;        // [bsplit][H][S][S] (zero-initialised) or null
+  float* dcmap;
+  float* lse;          // [B][H][S]
+  float* delta;
+  int B, S, H, bsplit;
+  float scale;
+  int causal;
+};
+
+__device__ __forceinline__ uint4 ld16(const bf16_t* p, bool ok) {
+  return ok ? *reinterpret_cast<const uint4*>(p) : make_uint4(0u, 0u, 0u, 0u);
+}
+
+// rows r0 .. r0+63 (token stride ld) of one head into a row-major image; rows past S are zero
+template <int D>
+__device__ __forceinline__ void stage_rm(bf16_t* img, const bf16_t* g, long long ld, int r0, int S, int tid) {
+  constexpr int CH = D / 8;
+  for (int c = tid; c < 64 * CH; c += 256) {
+    const int r = c / CH, cc = c - r * CH;
+    *reinterpret_cast<uint4*>(img + r * (D + PADR) + cc * 8) = ld16(g + (long long)(r0 + r) * ld + cc * 8, r0 + r < S);
+  }
+}
+// the same rows transposed: img[d][row]
+template <int D>
+__device__ __forceinline__ void stage_tr(bf16_t* img, const bf16_t* g, long long ld, int r0, int S, int tid) {
+  constexpr int CH = D / 8;
+  for (int c = tid; c < 64 * CH; c += 256) {
+    const int r = c & 63, cc = c >> 6;   // neighbouring threads: neighbouring rows = neighbouring LDS halfwords
+    const uint4 v = ld16(g + (long long)(r0 + r) * ld + cc * 8, r0 + r < S);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int t = 0; t < 8; ++t) img[(cc * 8 + t) * (64 + PADT) + r] = (bf16_t)(w[t >> 1] >> (16 * (t & 1)));
+  }
+}
+
+// operand of 16 rows (rb + lane & 15) x 32 contraction elements (kk * 32 + 8 g ..) from a row-major image
+template <int RS>
+__device__ __forceinline__ bf16x8_t frag_rm(const bf16_t* img, int rb, int kk, int lane) {
+  return *reinterpret_cast<const bf16x8_t*>(img + (rb + (lane & 15)) * RS + kk * 32 + 8 * (lane >> 4));
+}
+// A operand of 16 rows of a transposed image over the permuted contraction slots of chunk c:
+// slots 0-3 = columns 32c + 4g .. +3, slots 4-7 = columns 32c + 16 + 4g .. +3
+template <int RS>
+__device__ __forceinline__ bf16x8_t frag_tp(const bf16_t* img, int rb, int c, int lane) {
+  const bf16_t* p = img + (rb + (lane & 15)) * RS + 32 * c + 4 * (lane >> 4);
+  const uint2 lo = *reinterpret_cast<const uint2*>(p);
+  const uint2 hi = *reinterpret_cast<const uint2*>(p + 16);
+  return __builtin_bit_cast(bf16x8_t, make_uint4(lo.x, lo.y, hi.x, hi.y));
+}
+// B operand from two accumulator tiles in C layout (same slot permutation as frag_tp)
+__device__ __forceinline__ bf16x8_t frag_acc(const f32x4_t& t0, const f32x4_t& t1) {
+  return __builtin_bit_cast(bf16x8_t, make_uint4(pack_bf16x2(t0[0], t0[1]), pack_bf16x2(t0[2], t0[3]),
+                                                 pack_bf16x2(t1[0], t1[1]), pack_bf16x2(t1[2], t1[3])));
+}
+__device__ __forceinline__ f32x4_t mfma(const bf16x8_t& a, const bf16x8_t& b, const f32x4_t& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// ------------------------------------------------------------------------------------------------------------------
+template <int D>
+__global__ __launch_bounds__(256) void attn_map_fwd_kernel(MapArgs a) {
+  __shared__ __attribute__((aligned(16))) bf16_t kimg[64 * (D + PADR)];
+  __shared__ __attribute__((aligned(16))) bf16_t vt[D * (64 + PADT)];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
+  const int S = a.S, nqb = (S + TQ - 1) / TQ;
+  const int qb = nqb - 1 - (int)blockIdx.x;   // longest causal rows first
+  const int h = blockIdx.y, b = blockIdx.z;
+  const long long ld = (long long)a.H * D;
+  const long long base = (long long)b * S * ld + (long long)h * D;
+  const int myq = qb * TQ + w * 16 + (lane & 15);
+  const bool qok = myq < S;
+  bf16x8_t qf[D / 32];
+#pragma unroll
+  for (int kk = 0; kk < D / 32; ++kk)
+    qf[kk] = __builtin_bit_cast(bf16x8_t, ld16(a.q + base + (long long)myq * ld + kk * 32 + 8 * g, qok));
+  f32x4_t acc[D / 16];
+#pragma unroll
+  for (int i = 0; i < D / 16; ++i) acc[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const long long mrow = ((long long)h * S + (qok ? myq : 0)) * S;
+  float m = -INFINITY, l = 0.f;
+  const int nkt = a.causal ? qb + 1 : (S + TK - 1) / TK;
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int k0 = kt * TK;
+    __syncthreads();
+    stage_rm<D>(kimg, a.k + base, ld, k0, S, tid);
+    stage_tr<D>(vt, a.v + base, ld, k0, S, tid);
+    __syncthreads();
+    f32x4_t s[4];
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      s[kb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < D / 32; ++kk) s[kb] = mfma(frag_rm<D + PADR>(kimg, kb * 16, kk, lane), qf[kk], s[kb]);
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = k0 + kb * 16 + 4 * g + r;
+        const bool ok = key < S && (!a.causal || key <= myq);
+        float x = s[kb][r] * a.scale;
+        if (a.bias != nullptr && ok) x += a.bias[mrow + key];
+        x = ok ? x : -INFINITY;
+        s[kb][r] = x;
+        mx = fmaxf(mx, x);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mn = fmaxf(m, mx);   // finite: key k0 <= every query of a visited tile
+    const float al = __expf(m - mn);
+    float rs = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = __expf(s[kb][r] - mn);
+        rs += p;
+        float c = 1.f;
+        if (a.cmap != nullptr) {
+          const int key = k0 + kb * 16 + 4 * g + r;
+          if (key < S) c = a.cmap[mrow + key];
+        }
+        s[kb][r] = p * c;
+      }
+    rs += __shfl_xor(rs, 16, 64);
+    rs += __shfl_xor(rs, 32, 64);
+    l = l * al + rs;
+    m = mn;
+#pragma unroll
+    for (int i = 0; i < D / 16; ++i) acc[i] *= al;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const bf16x8_t pb = frag_acc(s[2 * c], s[2 * c + 1]);
+#pragma unroll
+      for (int i = 0; i < D / 16; ++i) acc[i] = mfma(frag_tp<64 + PADT>(vt, i * 16, c, lane), pb, acc[i]);
+    }
+  }
+  if (qok) {
+    const float inv = 1.f / l;
+    bf16_t* orow = a.out + base + (long long)myq * ld + 4 * g;
+#pragma unroll
+    for (int i = 0; i < D / 16; ++i)
+      *reinterpret_cast<uint2*>(orow + i * 16) =
+          make_uint2(pack_bf16x2(acc[i][0] * inv, acc[i][1] * inv), pack_bf16x2(acc[i][2] * inv, acc[i][3] * inv));
+    if (g == 0) a.lse[((long long)b * a.H + h) * S + myq] = m + __logf(l);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------------------------
+// dq per (query block, head, batch); writes delta_q = do_q . o_q first (the dk/dv kernel reads it)
+template <int D>
+__global__ __launch_bounds__(256) void attn_map_dq_kernel(MapArgs a) {
+  __shared__ __attribute__((aligned(16))) bf16_t kimg[64 * (D + PADR)];
+  __shared__ __attribute__((aligned(16))) bf16_t vimg[64 * (D + PADR)];
+  __shared__ __attribute__((aligned(16))) bf16_t kt[D * (64 + PADT)];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
+  const int S = a.S, nqb = (S + TQ - 1) / TQ;
+  const int qb = nqb - 1 - (int)blockIdx.x;
+  const int h = blockIdx.y, b = blockIdx.z;
+  const long long ld = (long long)a.H * D;
+  const long long base = (long long)b * S * ld + (long long)h * D;
+  const int myq = qb * TQ + w * 16 + (lane & 15);
+  const bool qok = myq < S;
+  bf16x8_t qf[D / 32], df[D / 32];
+  float dl = 0.f;
+#pragma unroll
+  for (int kk = 0; kk < D / 32; ++kk) {
+    const long long off = base + (long long)myq * ld + kk * 32 + 8 * g;
+    qf[kk] = __builtin_bit_cast(bf16x8_t, ld16(a.q + off, qok));
+    const uint4 dv4 = ld16(a.dO + off, qok), ov4 = ld16(a.o + off, qok);
+    df[kk] = __builtin_bit_cast(bf16x8_t, dv4);
+    const uint32_t dw[4] = {dv4.x, dv4.y, dv4.z, dv4.w}, ow[4] = {ov4.x, ov4.y, ov4.z, ov4.w};
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+      dl += bf2f((bf16_t)(dw[t] & 0xffff)) * bf2f((bf16_t)(ow[t] & 0xffff)) +
+            bf2f((bf16_t)(dw[t] >> 16)) * bf2f((bf16_t)(ow[t] >> 16));
+  }
+  dl += __shfl_xor(dl, 16, 64);
+  dl += __shfl_xor(dl, 32, 64);
+  const long long srow = ((long long)b * a.H + h) * S;
+  const float lse = qok ? a.lse[srow + myq] : 0.f;
+  if (qok && g == 0) a.delta[srow + myq] = dl;
+  const long long mrow = ((long long)h * S + (qok ? myq : 0)) * S;
+  f32x4_t acc[D / 16];
+#pragma unroll
+  for (int i = 0; i < D / 16; ++i) acc[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const int nkt = a.causal ? qb + 1 : (S + TK - 1) / TK;
+  for (int kti = 0; kti < nkt; ++kti) {
+    const int k0 = kti * TK;
+    __syncthreads();
+    stage_rm<D>(kimg, a.k + base, ld, k0, S, tid);
+    stage_rm<D>(vimg, a.v + base, ld, k0, S, tid);
+    stage_tr<D>(kt, a.k + base, ld, k0, S, tid);
+    __syncthreads();
+    f32x4_t s[4], dp[4];
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      s[kb] = dp[kb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < D / 32; ++kk) {
+        s[kb] = mfma(frag_rm<D + PADR>(kimg, kb * 16, kk, lane), qf[kk], s[kb]);
+        dp[kb] = mfma(frag_rm<D + PADR>(vimg, kb * 16, kk, lane), df[kk], dp[kb]);
+      }
+    }
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = k0 + kb * 16 + 4 * g + r;
+        const bool ok = qok && key < S && (!a.causal || key <= myq);
+        float x = s[kb][r] * a.scale;
+        float c = 1.f;
+        if (ok) {
+          if (a.bias != nullptr) x += a.bias[mrow + key];
+          if (a.cmap != nullptr) c = a.cmap[mrow + key];
+        }
+        const float p = ok ? __expf(x - lse) : 0.f;
+        s[kb][r] = p * (c * dp[kb][r] - dl);
+      }
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const bf16x8_t sb = frag_acc(s[2 * c], s[2 * c + 1]);
+#pragma unroll
+      for (int i = 0; i < D / 16; ++i) acc[i] = mfma(frag_tp<64 + PADT>(kt, i * 16, c, lane), sb, acc[i]);
+    }
+  }
+  if (qok) {
+    bf16_t* row = a.dq + base + (long long)myq * ld + 4 * g;
+    const float sc = a.scale;
+#pragma unroll
+    for (int i = 0; i < D / 16; ++i)
+      *reinterpret_cast<uint2*>(row + i * 16) =
+          make_uint2(pack_bf16x2(acc[i][0] * sc, acc[i][1] * sc), pack_bf16x2(acc[i][2] * sc, acc[i][3] * sc));
+  }
+}
+
+// ------------------------------------------------------------------------------------------------------------------
+// dk / dv per (key block, head, batch slice); map gradients accumulated in place over the slice's batches
+template <int D>
+__global__ __launch_bounds__(256) void attn_map_dkv_kernel(MapArgs a) {
+  __shared__ __attribute__((aligned(16))) bf16_t qimg[64 * (D + PADR)];
+  __shared__ __attribute__((aligned(16))) bf16_t qt[D * (64 + PADT)];
+  __shared__ __attribute__((aligned(16))) bf16_t dimg[64 * (D + PADR)];
+  __shared__ __attribute__((aligned(16))) bf16_t dt[D * (64 + PADT)];
+  __shared__ float lse_s[TQ], dl_s[TQ];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
+  const int S = a.S, nqb = (S + TQ - 1) / TQ;
+  const int kbk = blockIdx.x, h = blockIdx.y, slice = blockIdx.z;
+  const long long ld = (long long)a.H * D;
+  const int myk = kbk * TK + w * 16 + (lane & 15);
+  const bool kok = myk < S;
+  const int bper = (a.B + a.bsplit - 1) / a.bsplit;
+  const int b0 = slice * bper, b1 = min(a.B, b0 + bper);
+  const long long mbase = (long long)h * S * S;
+  const long long pbase = (long long)slice * a.H * S * S + mbase;   // this slice's partial map gradients
+  const int qb_first = a.causal ? kbk : 0;                            // query blocks holding a query >= a key here
+  for (int b = b0; b < b1; ++b) {
+    const long long base = (long long)b * S * ld + (long long)h * D;
+    const long long srow = ((long long)b * a.H + h) * S;
+    bf16x8_t kf[D / 32], vf[D / 32];
+#pragma unroll
+    for (int kk = 0; kk < D / 32; ++kk) {
+      const long long off = base + (long long)myk * ld + kk * 32 + 8 * g;
+      kf[kk] = __builtin_bit_cast(bf16x8_t, ld16(a.k + off, kok));
+      vf[kk] = __builtin_bit_cast(bf16x8_t, ld16(a.v + off, kok));
+    }
+    f32x4_t dk[D / 16], dv[D / 16];
+#pragma unroll
+    for (int i = 0; i < D / 16; ++i) dk[i] = dv[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    for (int qb = qb_first; qb < nqb; ++qb) {
+      const int q0 = qb * TQ;
+      __syncthreads();
+      stage_rm<D>(qimg, a.q + base, ld, q0, S, tid);
+      stage_tr<D>(qt, a.q + base, ld, q0, S, tid);
+      stage_rm<D>(dimg, a.dO + base, ld, q0, S, tid);
+      stage_tr<D>(dt, a.dO + base, ld, q0, S, tid);
+      if (tid < TQ) {
+        const bool ok = q0 + tid < S;
+        lse_s[tid] = ok ? a.lse[srow + q0 + tid] : 0.f;
+        dl_s[tid] = ok ? a.delta[srow + q0 + tid] : 0.f;
+      }
+      __syncthreads();
+      // S / dP tiles [queries][keys]: lane holds key myk, queries q0 + qi * 16 + 4 g + r
+      f32x4_t s[4], dp[4];
+#pragma unroll
+      for (int qi = 0; qi < 4; ++qi) {
+        s[qi] = dp[qi] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < D / 32; ++kk) {
+          s[qi] = mfma(frag_rm<D + PADR>(qimg, qi * 16, kk, lane), kf[kk], s[qi]);
+          dp[qi] = mfma(frag_rm<D + PADR>(dimg, qi * 16, kk, lane), vf[kk], dp[qi]);
+        }
+      }
+#pragma unroll
+      for (int qi = 0; qi < 4; ++qi)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int ql = qi * 16 + 4 * g + r, qq = q0 + ql;
+          const bool inb = kok && qq < S;
+          const bool ok = inb && (!a.causal || myk <= qq);
+          const long long mi = (long long)qq * S + myk;
+          float x = s[qi][r] * a.scale;
+          float c = 1.f;
+          if (ok) {
+            if (a.bias != nullptr) x += a.bias[mbase + mi];
+            if (a.cmap != nullptr) c = a.cmap[mbase + mi];
+          }
+          const float p = ok ? __expf(x - lse_s[ql]) : 0.f;
+          const float ds = p * (c * dp[qi][r] - dl_s[ql]);
+          if (inb) {
+            if (a.dbias != nullptr) a.dbias[pbase + mi] += ds;
+            if (a.dcmap != nullptr) a.dcmap[pbase + mi] += p * dp[qi][r];
+          }
+          s[qi][r] = p * c;
+          dp[qi][r] = ds;
+        }
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const bf16x8_t pb = frag_acc(s[2 * c], s[2 * c + 1]);
+        const bf16x8_t sb = frag_acc(dp[2 * c], dp[2 * c + 1]);
+#pragma unroll
+        for (int i = 0; i < D / 16; ++i) {
+          dv[i] = mfma(frag_tp<64 + PADT>(dt, i * 16, c, lane), pb, dv[i]);
+          dk[i] = mfma(frag_tp<64 + PADT>(qt, i * 16, c, lane), sb, dk[i]);
+        }
+      }
+    }
+    if (kok) {
+      const long long off = base + (long long)myk * ld + 4 * g;
+      const float sc = a.scale;
+#pragma unroll
+      for (int i = 0; i < D / 16; ++i) {
+        *reinterpret_cast<uint2*>(a.dk + off + i * 16) =
+            make_uint2(pack_bf16x2(dk[i][0] * sc, dk[i][1] * sc), pack_bf16x2(dk[i][2] * sc, dk[i][3] * sc));
+        *reinterpret_cast<uint2*>(a.dv + off + i * 16) =
+            make_uint2(pack_bf16x2(dv[i][0], dv[i][1]), pack_bf16x2(dv[i][2], dv[i][3]));
+      }
+    }
+  }
+}
+
+// out[i] = sum over slices s (in order) of part[s][i]
+__global__ __launch_bounds__(256) void map_fold_kernel(const float* part, float* out, long long n, int slices) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  float v = 0.f;
+  for (int s = 0; s < slices; ++s) v += part[s * n + i];
+  out[i] = v;
+}
+
+template <int D>
+hipError_t launch_fwd(const MapArgs& a, hipStream_t st) {
+  const int nqb = (a.S + TQ - 1) / TQ;
+  hipLaunchKernelGGL(attn_map_fwd_kernel<D>, dim3(nqb, a.H, a.B), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+template <int D>
+hipError_t launch_bwd(const MapArgs& a, hipStream_t st) {
+  const int nqb = (a.S + TQ - 1) / TQ;
+  hipLaunchKernelGGL(attn_map_dq_kernel<D>, dim3(nqb, a.H, a.B), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(attn_map_dkv_kernel<D>, dim3(nqb, a.H, a.bsplit), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+struct ObstMapDesc {
+  const void *Q, *K, *V, *O, *dO;
+  void *Out, *dQ, *dK, *dV;
+  const void *bias, *cmap;
+  void *dbias, *dcmap, *dbias_out, *dcmap_out;   // partial maps [bsplit][H][S][S] and the folded [H][S][S]
+  void *LSE, *delta;
+  int B, S, H, D, bsplit;
+  float scale;
+  int causal;
+};
+
+// batch slices of the dk/dv kernel: enough workgroups for 4 per CU, at most 4 partial maps
+OBST_API int obst_attn_map_bsplit(int B, int S, int H) {
+  const long long wg = (long long)((S + TK - 1) / TK) * H;
+  long long s = (1024 + wg - 1) / wg;
+  if (s > 4) s = 4;
+  if (s > B) s = B;
+  return (int)(s < 1 ? 1 : s);
+}
+
+static int fill(MapArgs& a, const ObstMapDesc* d) {
+  if (d->B <= 0 || d->S <= 0 || d->H <= 0 || d->bsplit <= 0) return -1;
+  a.q = (const bf16_t*)d->Q; a.k = (const bf16_t*)d->K; a.v = (const bf16_t*)d->V;
+  a.o = (const bf16_t*)d->O; a.dO = (const bf16_t*)d->dO;
+  a.out = (bf16_t*)d->Out; a.dq = (bf16_t*)d->dQ; a.dk = (bf16_t*)d->dK; a.dv = (bf16_t*)d->dV;
+  a.bias = (const float*)d->bias; a.cmap = (const float*)d->cmap;
+  a.dbias = (float*)d->dbias; a.dcmap = (float*)d->dcmap;
+  a.lse = (float*)d->LSE; a.delta = (float*)d->delta;
+  a.B = d->B; a.S = d->S; a.H = d->H; a.bsplit = d->bsplit; a.scale = d->scale; a.causal = d->causal;
+  return 0;
+}
+
+OBST_API int obst_attn_map_fwd(const ObstMapDesc* d, hipStream_t st) {
+  MapArgs a;
+  if (fill(a, d) != 0) return -1;
+  hipError_t e;
+  switch (d->D) {
+    case 32: e = launch_fwd<32>(a, st); break;
+    case 64: e = launch_fwd<64>(a, st); break;
+    case 96: e = launch_fwd<96>(a, st); break;
+    case 128: e = launch_fwd<128>(a, st); break;
+    default: return -2;
+  }
+  return (int)e;
+}
+
+OBST_API int obst_attn_map_bwd(const ObstMapDesc* d, hipStream_t st) {
+  MapArgs a;
+  if (fill(a, d) != 0) return -1;
+  hipError_t e;
+  switch (d->D) {
+    case 32: e = launch_bwd<32>(a, st); break;
+    case 64: e = launch_bwd<64>(a, st); break;
+    case 96: e = launch_bwd<96>(a, st); break;
+    case 128: e = launch_bwd<128>(a, st); break;
+    default: return -2;
+  }
+  if (e != hipSuccess) return (int)e;
+  const long long n = (long long)d->H * d->S * d->S;
+  const dim3 grid((unsigned)((n + 255) / 256));
+  if (d->dbias && d->dbias_out && d->dbias_out != d->dbias)
+    hipLaunchKernelGGL(map_fold_kernel, grid, dim3(256), 0, st, (const float*)d->dbias, (float*)d->dbias_out, n, d->bsplit);
+  if (d->dcmap && d->dcmap_out && d->dcmap_out != d->dcmap)
+    hipLaunchKernelGGL(map_fold_kernel, grid, dim3(256), 0, st, (const float*)d->dcmap, (float*)d->dcmap_out, n, d->bsplit);
+  return (int)hipGetLastError();
+}

@@ -457,6 +457,11 @@ def _mixer_kv(args: BlockArgs, kv, x: Act, dim: Dim, tmp: Dim, causal: bool) -> 
     return Act(F.token_mixer_step(x.t, st["x"], st["w"], kv.pos), x.dims)
 
 
+# the composable attention path runs its softmax / map variants on the flash kernels (False: the generic named-einsum
+# path with materialised logits -- the CPU tests' reference for the routing)
+FLASH_MAPS = True
+
+
 def _attention_fast_ok(args: BlockArgs, ins, outs) -> bool:
     p = args.params
     x = args.tensor
@@ -567,18 +572,41 @@ def attention(args: BlockArgs) -> Act:
         qry = Act(qry.t * scale, qry.dims)
         if key is None:
             raise ValueError("dot_product attention needs 'context', 'embedded' or 'positional'")
-        # fast core: plain causal/full softmax attention over [batch, seq, heads, fph]
-        plain = not any(k in args for k in ('biased_softmax', 'biased_attention_map', 'scale_attention_map'))
-        if plain and len(x.dims) == 4 and dim == x.dims[1] and qry.dims == x.dims and key.dims == x.dims:
+        # flash core over [batch, seq, heads, fph] for every map combination (no [B, S, heads, S] logits):
+        #   biased_softmax       -> additive [heads, S, S] map inside the softmax (attn_map kernels)
+        #   scale_attention_map  -> multiplicative map on the probabilities (attn_map kernels)
+        #   biased_attention_map -> (P + Bm) V = P V + Bm V: the learned token mixer (K03) on the same values
+        # positional-only keys ([seq, heads, fph]) are broadcast over the batch
+        if (FLASH_MAPS and len(x.dims) == 4 and dim == x.dims[1] and qry.dims == x.dims and x.dims[2] == p.head_dim
+                and (key.dims == x.dims or key.dims == x.dims[1:])):
+            # maps created in the order of the generic path below (variable scopes / checkpoint names)
+            sb = _masked_map(args)[0] if 'biased_softmax' in args else None
+            ab = _masked_map(args) if 'biased_attention_map' in args else None
+            sc = _masked_map(args) if 'scale_attention_map' in args else None
             v = key if 'shared_key_value' in args else (
                 Act(x.t, x.dims) if 'input_as_value' in args else activated_linear_out(args(base)))
-            o = F.attention_core(qry.t, key.t, v.t, 1.0, causal)
+            kt = key.t if key.dims == x.dims else key.t.unsqueeze(0).expand(x.dims[0].size, *key.t.shape)
+            vt = v.t if v.dims == x.dims else v.t.unsqueeze(0).expand(x.dims[0].size, *v.t.shape)
+            cm = _apply_mask(sc[0], sc[1], dim, tmp).t if sc is not None else None
+            if sb is None and cm is None:
+                o = F.attention_core(qry.t, kt, vt, 1.0, causal)
+            else:
+                o = F.attention_map(qry.t, kt, vt, sb.t if sb is not None else None, cm, 1.0, causal)
+            if ab is not None:
+                bm = _apply_mask(ab[0], ab[1], dim, tmp).t
+                if cm is not None:
+                    bm = bm * cm
+                o = o + F.token_mixer(vt.contiguous(), bm, causal)
             return Act(o, x.dims)
         old = D.linear_shapes(p, args, x.dims).old
         logit_dims = D.subtract(x.dims, D.subtract(old, [p.head_dim])) + [tmp]
         logit = named_einsum([qry, anonymize(key, dim)], logit_dims)
         if 'shared_key_value' in args:
-            val = key
+            # V = K attention. The reference keeps the key un-anonymised here (spatial.py:63-64 + :81), so its final
+            # einsum does not contract over keys and yields rowsum(logit) * key_q -- no mixing at all (quirk A19,
+            # fixed: docs/PARITY.md); the flash route above and this path agree on the fixed semantics
+            val = anonymize(key, dim) if key.dims == x.dims else anonymize(
+                Act(key.t.unsqueeze(0).expand(x.dims[0].size, *key.t.shape), x.dims), dim)
     if 'biased_softmax' in args:
         bias, mask = _masked_map(args)
         b = _apply_mask(bias, mask, dim, tmp)

@@ -54,6 +54,13 @@ class AttnDesc(ctypes.Structure):
                 ("ld_o", c_ll), ("Res", c_p), ("Sum", c_p)]
 
 
+class MapDesc(ctypes.Structure):
+    _fields_ = [("Q", c_p), ("K", c_p), ("V", c_p), ("O", c_p), ("dO", c_p),
+                ("Out", c_p), ("dQ", c_p), ("dK", c_p), ("dV", c_p), ("bias", c_p), ("cmap", c_p),
+                ("dbias", c_p), ("dcmap", c_p), ("dbias_out", c_p), ("dcmap_out", c_p), ("LSE", c_p), ("delta", c_p),
+                ("B", c_i), ("S", c_i), ("H", c_i), ("D", c_i), ("bsplit", c_i), ("scale", c_f), ("causal", c_i)]
+
+
 class NormDesc(ctypes.Structure):
     _fields_ = [("X", c_p), ("scale", c_p), ("shift", c_p), ("Y", c_p), ("stats", c_p),
                 ("DY", c_p), ("DX", c_p), ("dscale", c_p), ("dshift", c_p), ("partial", c_p), ("ext", c_p),
@@ -79,6 +86,9 @@ _SIGS = {
     "obst_gemm": [ctypes.POINTER(GemmDesc), c_p],
     "obst_attn_fwd": [ctypes.POINTER(AttnDesc), c_p],
     "obst_attn_bwd": [ctypes.POINTER(AttnDesc), c_p],
+    "obst_attn_map_fwd": [ctypes.POINTER(MapDesc), c_p],
+    "obst_attn_map_bwd": [ctypes.POINTER(MapDesc), c_p],
+    "obst_attn_map_bsplit": [c_i, c_i, c_i],
     "obst_norm_fwd": [ctypes.POINTER(NormDesc), c_p],
     "obst_norm_bwd": [ctypes.POINTER(NormDesc), c_p],
     "obst_norm_partial": [ctypes.POINTER(NormDesc), c_p],

@@ -606,6 +606,52 @@ def attention_core(q, k, v, scale: float, causal: bool):
     return _AttnCore.apply(q, k, v, scale, causal)
 
 
+class _AttnMap(torch.autograd.Function):
+    """flash attention with per-head [H, S, S] maps (raw.attn_map_*): bias added to the scaled logits, cmap
+    multiplied into the softmax probabilities; either may be None. No [B, H, S, S] tensor is formed on the GPU."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, bias, cmap, scale, causal):
+        B, S, H, D = q.shape
+        q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
+        md = torch.float64 if q.dtype == torch.float64 else torch.float32   # fp64: the CPU gradient checks
+        b32 = bias.to(md).contiguous() if bias is not None else None
+        c32 = cmap.to(md).contiguous() if cmap is not None else None
+        o = torch.empty_like(q)
+        lse = torch.empty(B * H * S, dtype=md, device=q.device)
+        raw.attn_map_fwd(q, k, v, o, lse, b32, c32, B, S, H, D, scale, causal)
+        ctx.save_for_backward(q, k, v, o, lse, b32, c32)
+        ctx.cfg = (scale, causal, bias.dtype if bias is not None else None, cmap.dtype if cmap is not None else None)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, o, lse, b32, c32 = ctx.saved_tensors
+        scale, causal, bdt, cdt = ctx.cfg
+        B, S, H, D = q.shape
+        dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+        md = lse.dtype
+        delta = torch.empty(B * H * S, dtype=md, device=q.device)
+        need_b = b32 is not None and ctx.needs_input_grad[3]
+        need_c = c32 is not None and ctx.needs_input_grad[4]
+        db = torch.empty(H, S, S, dtype=md, device=q.device) if need_b else None
+        dc = torch.empty(H, S, S, dtype=md, device=q.device) if need_c else None
+        pb = pc = None
+        if raw.on_gpu(q) and (need_b or need_c):
+            bs = raw.attn_map_bsplit(B, S, H)
+            if bs > 1:
+                pb = torch.zeros(bs, H, S, S, dtype=torch.float32, device=q.device) if need_b else None
+                pc = torch.zeros(bs, H, S, S, dtype=torch.float32, device=q.device) if need_c else None
+        raw.attn_map_bwd(q, k, v, o, do.contiguous(), lse, delta, dq, dk, dv, b32, c32, db, dc, B, S, H, D, scale,
+                         causal, pb, pc)
+        return (dq, dk, dv, db.to(bdt) if db is not None else None, dc.to(cdt) if dc is not None else None,
+                None, None)
+
+
+def attention_map(q, k, v, bias, cmap, scale: float, causal: bool):
+    return _AttnMap.apply(q, k, v, bias, cmap, scale, causal)
+
+
 # ================================================================================================================
 # norm
 class ResidualGrad:

@@ -384,6 +384,111 @@ def attn_bwd(q, k, v, o, do, lse, delta, dq, dk, dv, B, S, H, D, ld, scale: floa
 
 
 # ----------------------------------------------------------------------------------------------------------------
+# attention with learned per-head maps (csrc/kernels/attn_map.hip): contiguous [B, S, H, D] q / k / v / o, fp32
+# [H, S, S] maps -- bias added to the scaled logits before the softmax, cmap multiplied into the probabilities after it
+def attn_map_bsplit(B: int, S: int, H: int) -> int:
+    """batch slices of the dk/dv kernel (= partial map gradients the host allocates)"""
+    return int(L.lib().obst_attn_map_bsplit(B, S, H))
+
+
+def _map_logits(q, k, bias, B, S, H, D, scale, causal):
+    s = torch.einsum("bqhd,bkhd->bhqk", _f(q.view(B, S, H, D)), _f(k.view(B, S, H, D))) * scale
+    if bias is not None:
+        s = s + _f(bias).unsqueeze(0)
+    if causal:
+        s = s.masked_fill(torch.ones(S, S, dtype=torch.bool, device=s.device).triu(1), float("-inf"))
+    return s
+
+
+def attn_map_fwd(q, k, v, o, lse, bias, cmap, B, S, H, D, scale: float, causal: bool):
+    if q.device.type == "meta":
+        return None
+    if on_gpu(q):
+        if D not in (32, 64, 96, 128):
+            raise L.KernelError(f"attention head dim {D} not supported by the HIP kernel (32/64/96/128)")
+        for nm, t in (("q", q), ("k", k), ("v", v), ("o", o)):
+            if t.dtype != torch.bfloat16 or not t.is_contiguous():
+                raise L.KernelError(f"attention map {nm} must be contiguous bf16")
+            _need(t, B * S * H * D - 1, nm)
+        for nm, t in (("bias", bias), ("cmap", cmap)):
+            if t is not None:
+                if t.dtype != torch.float32 or not t.is_contiguous():
+                    raise L.KernelError(f"attention map {nm} must be contiguous fp32")
+                _need(t, H * S * S - 1, nm)
+        _need(lse, B * H * S - 1, "lse")
+        d = L.MapDesc(q.data_ptr(), k.data_ptr(), v.data_ptr(), 0, 0, o.data_ptr(), 0, 0, 0, L.ptr(bias), L.ptr(cmap),
+                      0, 0, 0, 0, lse.data_ptr(), 0, B, S, H, D, 1, float(scale), int(causal))
+        L.check(L.lib().obst_attn_map_fwd(d, L.stream_ptr()), "attn_map_fwd")
+        return
+    s = _map_logits(q, k, bias, B, S, H, D, scale, causal)
+    m = s.logsumexp(-1)
+    p = torch.exp(s - m.unsqueeze(-1))
+    if cmap is not None:
+        p = p * _f(cmap).unsqueeze(0)
+    o.view(B, S, H, D).copy_(torch.einsum("bhqk,bkhd->bqhd", p, _f(v.view(B, S, H, D))))
+    lse.view(B, H, S).copy_(m)
+
+
+def attn_map_bwd(q, k, v, o, do, lse, delta, dq, dk, dv, bias, cmap, dbias, dcmap, B, S, H, D, scale: float,
+                 causal: bool, dbias_part=None, dcmap_part=None):
+    """dbias / dcmap: [H, S, S] fp32 outputs (None: not needed); *_part: zeroed [bsplit, H, S, S] partial maps the
+    dk/dv kernel accumulates into (GPU; None when bsplit == 1 -- the kernel then accumulates into a zeroed dbias)"""
+    if q.device.type == "meta":
+        return None
+    if on_gpu(q):
+        if D not in (32, 64, 96, 128):
+            raise L.KernelError(f"attention head dim {D} not supported by the HIP kernel (32/64/96/128)")
+        for nm, t in (("q", q), ("k", k), ("v", v), ("o", o), ("do", do), ("dq", dq), ("dk", dk), ("dv", dv)):
+            if t.dtype != torch.bfloat16 or not t.is_contiguous():
+                raise L.KernelError(f"attention map {nm} must be contiguous bf16")
+            _need(t, B * S * H * D - 1, nm)
+        bsplit = attn_map_bsplit(B, S, H)
+        for nm, t in (("bias", bias), ("cmap", cmap), ("dbias", dbias), ("dcmap", dcmap)):
+            if t is not None:
+                if t.dtype != torch.float32 or not t.is_contiguous():
+                    raise L.KernelError(f"attention map {nm} must be contiguous fp32")
+                _need(t, H * S * S - 1, nm)
+        parts = []
+        for nm, out, part in (("dbias", dbias, dbias_part), ("dcmap", dcmap, dcmap_part)):
+            if out is None:
+                parts.append(None)
+                continue
+            if bsplit == 1:
+                out.zero_()
+                parts.append(out)
+                continue
+            if part is None or part.dtype != torch.float32 or not part.is_contiguous():
+                raise L.KernelError(f"attention map {nm}: a zeroed fp32 [{bsplit}, H, S, S] partial buffer is needed")
+            _need(part, bsplit * H * S * S - 1, nm + "_part")
+            parts.append(part)
+        _need(lse, B * H * S - 1, "lse")
+        _need(delta, B * H * S - 1, "delta")
+        d = L.MapDesc(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), do.data_ptr(), 0, dq.data_ptr(),
+                      dk.data_ptr(), dv.data_ptr(), L.ptr(bias), L.ptr(cmap), L.ptr(parts[0]), L.ptr(parts[1]),
+                      L.ptr(dbias), L.ptr(dcmap), lse.data_ptr(), delta.data_ptr(), B, S, H, D, bsplit, float(scale),
+                      int(causal))
+        L.check(L.lib().obst_attn_map_bwd(d, L.stream_ptr()), "attn_map_bwd")
+        return
+    s = _map_logits(q, k, bias, B, S, H, D, scale, causal)
+    p = torch.exp(s - lse.view(B, H, S).unsqueeze(-1))
+    c = _f(cmap).unsqueeze(0) if cmap is not None else None
+    qv, kv, vv = (_f(t.view(B, S, H, D)) for t in (q, k, v))
+    dov = _f(do.view(B, S, H, D))
+    dlt = (dov * _f(o.view(B, S, H, D))).sum(-1).permute(0, 2, 1)
+    delta.view(B, H, S).copy_(dlt)
+    pc = p * c if c is not None else p
+    dv.view(B, S, H, D).copy_(torch.einsum("bhqk,bqhd->bkhd", pc, dov))
+    dp = torch.einsum("bqhd,bkhd->bhqk", dov, vv)
+    ds = p * ((dp * c if c is not None else dp) - dlt.unsqueeze(-1))
+    dq.view(B, S, H, D).copy_(torch.einsum("bhqk,bkhd->bqhd", ds, kv) * scale)
+    dk.view(B, S, H, D).copy_(torch.einsum("bhqk,bqhd->bkhd", ds, qv) * scale)
+    if dbias is not None:
+        dbias.copy_(ds.sum(0))
+    if dcmap is not None:
+        dcmap.copy_((p * dp).sum(0))
+
+
+# ----------------------------------------------------------------------------------------------------------------
 # norm (reference normalization.py:22-34); x viewed as [rows, F], params indexed by row % groups
 EPS = 1e-5
 

@@ -195,6 +195,11 @@ VARIANTS = {
                      block_config=[{"layer": ["norm-shift-scale-group", "feed_forward-in:relu-in:glu"]}]),
     "checkpoint": dict(memory_reduction_strategy="checkpoint",
                        block_config=[{"layer": ["norm-shift-scale", "feed_forward-in:tanh"], "skip": True}]),
+    "softmax_maps": dict(block_config=[{"layer": [
+        "attention-biased_softmax-scale_attention_map-biased_attention_map-dot_product-context-absolute"],
+        "skip": True}]),
+    "positional_kv": dict(block_config=[{"layer": ["attention-dot_product-positional-absolute-shared_key_value"],
+                                         "skip": True}]),
     "mixer": dict(memory_reduction_strategy="revnet",
                   block_config=[{"layer": ["norm-shift-scale-group",
                                            "attention-biased_attention_map-absolute-input_as_value-shared",
@@ -412,3 +417,71 @@ def test_cholesky_qr2_matches_sign_corrected_householder():
         assert q is not None
         assert (q - ref).abs().max().item() < 1e-4
         assert torch.allclose(q.t() @ q, torch.eye(shape[1]), atol=1e-5)
+
+
+MAP_LAYERS = ["attention-biased_softmax-dot_product-context-absolute",
+              "attention-scale_attention_map-dot_product-context-absolute",
+              "attention-biased_attention_map-dot_product-context-absolute",
+              "attention-biased_softmax-scale_attention_map-biased_attention_map-dot_product-context-absolute",
+              "attention-biased_softmax-dot_product-embedded-absolute-shared_key_value",
+              "attention-dot_product-positional-absolute",
+              "attention-biased_softmax-dot_product-context-absolute-input_as_value"]
+
+
+@pytest.mark.parametrize("layer", MAP_LAYERS)
+def test_attention_map_routing_matches_generic_path(layer, monkeypatch):
+    """the flash routing of the softmax-map variants (attn_map / token mixer) == the named-einsum path with
+    materialised logits: loss and every parameter gradient, fp64, causal"""
+    from homebrewnlp_mtf_amd.models import layers as LY
+    res = {}
+    for flash in (True, False):
+        monkeypatch.setattr(LY, "FLASH_MAPS", flash)
+        torch.manual_seed(0)
+        cfg = dict(BASE, calculation_dtype="float64", block_config=[{"layer": [layer], "skip": True}])
+        m = Model(ModelParameter(cfg), "cpu")
+        st = m.store
+        st.master = st.master.double()
+        st.grad = st.grad.double()
+        st.compute = st.master
+        st._leaves = {}
+        st.master.copy_(torch.randn_like(st.master) * 0.3)
+        x = torch.randint(0, 50, (2, 8, 1), generator=torch.Generator().manual_seed(1))
+        out = m(x, x)
+        out["loss"].backward()
+        st.fold_leaf_grads()
+        res[flash] = (float(out["loss"].detach()), st.grad.clone(), list(st.order))
+    assert res[True][2] == res[False][2]                 # same variables, same order
+    # the generic path takes its softmax in fp32 (layers.attention), so agreement is to fp32 precision
+    assert abs(res[True][0] - res[False][0]) < 1e-6
+    assert torch.allclose(res[True][1], res[False][1], atol=1e-6, rtol=1e-5)
+
+
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("maps", ["bias", "cmap", "both"])
+def test_attention_map_oracle_gradients(causal, maps):
+    """raw.attn_map_fwd / attn_map_bwd (the fp32 oracle the GPU kernels are tested against) == autograd through
+    softmax(scale q.k + b) * c . v"""
+    from homebrewnlp_mtf_amd.ops import functional as F
+    torch.manual_seed(2)
+    B, S, H, Dh = 2, 7, 3, 4
+    q, k, v = (torch.randn(B, S, H, Dh, dtype=torch.float64, requires_grad=True) for _ in range(3))
+    bias = torch.randn(H, S, S, dtype=torch.float64, requires_grad=True) if maps != "cmap" else None
+    cmap = torch.rand(H, S, S, dtype=torch.float64, requires_grad=True) if maps != "bias" else None
+    scale = 0.7
+    o = F.attention_map(q, k, v, bias, cmap, scale, causal)
+    s = torch.einsum("bqhd,bkhd->bhqk", q, k) * scale
+    if bias is not None:
+        s = s + bias
+    if causal:
+        s = s.masked_fill(torch.ones(S, S, dtype=torch.bool).triu(1), float("-inf"))
+    pr = torch.softmax(s, -1)
+    if cmap is not None:
+        pr = pr * cmap
+    ref = torch.einsum("bhqk,bkhd->bqhd", pr, v)
+    assert torch.allclose(o, ref, atol=1e-12)
+    do = torch.randn_like(o)
+    ins = [t for t in (q, k, v, bias, cmap) if t is not None]
+    g1 = torch.autograd.grad(o, ins, do)
+    g2 = torch.autograd.grad(ref, ins, do)
+    for a, b in zip(g1, g2):
+        assert torch.allclose(a, b, atol=1e-10), (a - b).abs().max()
