@@ -224,17 +224,19 @@ class _Linear(torch.autograd.Function):
             raw.elementwise("act_bwd", z, dz, z=dy, act=act)
             dy = dz
         dx = None
+        pending = pstate._DONE
         if ctx.needs_input_grad[0]:
             dx = _empty(xc.shape, xc)
             _dgrad_gemm(dy, w, dx, plan)
             if plan.col_parallel and pstate.tp_size() > 1:
-                pstate.tp_all_reduce(dx)
+                pending = pstate.tp_all_reduce_async(dx)   # overlaps the weight-gradient GEMM below
             if plan.x_perm is not None:
                 inv = [plan.x_perm.index(i) for i in range(len(plan.x_perm))]
                 dx = dx.permute(inv)
         gw, is_main, beta = _acc_grad_beta(w)
         _wgrad_gemm(xc, dy, gw, plan, beta=beta)
         _done(w)
+        pending.wait()
         return dx, (None if is_main else gw.to(w.dtype)), None, None
 
 
@@ -316,18 +318,19 @@ class _FFN(torch.autograd.Function):
         # act'(z) is the same on every TP rank (z is replicated), so the fused act-backward epilogue commutes with
         # the all-reduce of the partial dz (W2 contracting the sharded heads)
         _dgrad_gemm(dy, w2, dz, p2, act=act, Zin=z if act else None)
-        if tp and p2.col_parallel:
-            pstate.tp_all_reduce(dz)
+        # TP: each data-gradient all-reduce runs on RCCL's stream under the weight-gradient GEMM that follows it
+        pending = pstate.tp_all_reduce_async(dz) if tp and p2.col_parallel else pstate._DONE
         g2, m2, b2 = _acc_grad_beta(w2)
         _wgrad_gemm(a, dy, g2, p2, beta=b2)
         _done(w2)
+        pending.wait()
         dx = _empty(xc.shape, xc)
         _dgrad_gemm(dz, w1, dx, p1)
-        if tp and p1.col_parallel:
-            pstate.tp_all_reduce(dx)
+        pending = pstate.tp_all_reduce_async(dx) if tp and p1.col_parallel else pstate._DONE
         g1, m1, b1 = _acc_grad_beta(w1)
         _wgrad_gemm(xc, dz, g1, p1, beta=b1)
         _done(w1)
+        pending.wait()
         dres = dy if ctx.has_res else None
         if dres is not None and ctx.carrier is not None:   # handed to the block's opening norm (ResidualGrad)
             ctx.carrier.grad, dres = dres, None
@@ -404,6 +407,10 @@ class _DotAttention(torch.autograd.Function):
         ws = (w_k, w_q, w_v)
         dbase = _empty(p_in.canon_o_shape, xc)
         _kqv_dgrad(dkqv, ws, dbase, p_out, act, z)
+        # TP: act'(z) is replicated, so the activation-backward fused into the dgrad commutes with the sum; the
+        # all-reduce of the partial dbase runs on RCCL's stream under the three k/q/v weight-gradient GEMMs
+        pending = (pstate.tp_all_reduce_async(dbase) if p_out.col_parallel and pstate.tp_size() > 1
+                   else pstate._DONE)
         baseT = None
         if raw.on_gpu(base) and raw.lt_takes_f32() and T % 8 == 0 and K % 8 == 0:
             # one transpose of base serves the three q/k/v weight gradients (tools/bench_wgrad.py: -118 us each
@@ -418,9 +425,7 @@ class _DotAttention(torch.autograd.Function):
             raw.gemm(a_op, raw.Operand(dyj, 1, 3 * N), raw.Operand(g, 0, N, K * N), K, N, T, beta=bj)
             _done(ws[j])
             outs.append(None if m else g.to(ws[j].dtype))
-        if p_out.col_parallel and pstate.tp_size() > 1:
-            # act'(z) is replicated over TP, so the activation-backward fused into the dgrad commutes with the sum
-            pstate.tp_all_reduce(dbase)
+        pending.wait()
         dx = _empty(xc.shape, xc)
         _dgrad_gemm(dbase, w_in, dx, p_in)
         g, m, bi = _acc_grad_beta(w_in)

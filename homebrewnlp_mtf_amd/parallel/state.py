@@ -67,3 +67,23 @@ def tp_all_reduce(t: torch.Tensor, op=None) -> torch.Tensor:
         debug.record("tp_all_reduce", t)
         dist.all_reduce(t, op=op or dist.ReduceOp.SUM, group=_MESH.tp_group)
     return t
+
+
+class _Done:
+    def wait(self):
+        return True
+
+
+_DONE = _Done()
+
+
+def tp_all_reduce_async(t: torch.Tensor):
+    """Start an in-place sum over the TP group on RCCL's own stream (it orders itself after the compute stream's
+    work so far) and return the handle; its ``wait()`` makes the compute stream wait for the collective without
+    blocking the host. Work issued in between -- a layer's weight-gradient GEMM after its data-gradient all-reduce
+    started -- runs on the compute stream while the collective moves over xGMI."""
+    if _MESH.tp > 1 and t.device.type != "meta":
+        from ..utils import debug
+        debug.record("tp_all_reduce", t)
+        return dist.all_reduce(t, op=dist.ReduceOp.SUM, group=_MESH.tp_group, async_op=True)
+    return _DONE

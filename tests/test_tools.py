@@ -219,3 +219,18 @@ def test_video2tfrecord_subtitles_and_text_only_frames(tmp_path):
     sep = rows[len(rows) // 2]
     assert sep[:3] == (0, 1, 4) and list(exs[len(rows) // 2].int64("tokens")) == [7, 7, 7, 7]
     assert rows[len(rows) // 2 + 1:] == half
+
+
+def test_comm_probe_gloo_world2():
+    """tools/comm_probe.py: bus-bandwidth rows for every collective over a 2-rank gloo group"""
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, OBST_DIST_BACKEND="gloo", PYTHONPATH=root)
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "2", "--master-addr",
+                        "127.0.0.1", "--master-port", "29517", os.path.join(root, "tools", "comm_probe.py"),
+                        "--sizes-mb", "0.25,1", "--iters", "2", "--warmup", "1", "--dtype", "float32"],
+                       capture_output=True, text=True, env=env, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    rows = [json.loads(line) for line in r.stdout.splitlines() if line.startswith("{")]
+    assert {x["op"] for x in rows} == {"all_reduce", "reduce_scatter", "all_gather", "all_to_all"}
+    assert len(rows) == 8 and all(x["busbw_GBps"] > 0 and x["world"] == 2 for x in rows)
