@@ -211,8 +211,22 @@ __device__ __forceinline__ void scale8(int c, int sl, int F, bool ok, long long 
 // (sum dxh, sum dxh*xh) for the TP all-reduce and returns (phase 1); with `ext_dsum` (phase 2) uses them.
 // Parameter gradients: per-lane register sums; the host sizes the grid so that (rows per grid step) % groups == 0,
 // so every lane only ever sees rows of one group (row % groups is fixed along the grid-stride loop).
+// Wide rows (NCH >= 8: F > 2048 at 64 lanes per row) run one block per CU with 512 VGPRs: the 8 x NCH parameter-
+// gradient sums per lane plus a double-buffered row do not fit the 256 of two blocks per CU. At F = 2048 (NCH 4) two
+// blocks per CU fit without spills once the residual gradient is loaded for the current row (not a row ahead) and
+// the output pairs are packed with the scalar conversions (pk2 below): 411 us per call at 131072 x 2048 against
+// 596 us with one block per CU and 833 us with the ~60 VGPRs the vector-convert pack spilled.
+template <int NCH>
+constexpr int bwd_blocks_per_cu() { return NCH >= 8 ? 1 : 2; }
+
+// two floats -> packed bf16 pair through two scalar conversions: the vector convert (common.h pack_bf16x2) costs
+// this kernel ~60 VGPRs of spills at F = 2048 (register allocation around the v_cvt_pk_bf16_f32 pairs)
+__device__ __forceinline__ uint32_t pk2(float lo, float hi) {
+  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+}
+
 template <int NCH, int LPR>
-__global__ __launch_bounds__(NTH, 2) void norm_bwd_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ DY,
+__global__ __launch_bounds__(NTH, bwd_blocks_per_cu<NCH>()) void norm_bwd_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ DY,
                                                        const float* __restrict__ scale, const float* __restrict__ stats,
                                                        bf16_t* __restrict__ DX, float* __restrict__ dscale,
                                                        float* __restrict__ dshift, long long rows, int F, int groups,
@@ -241,7 +255,7 @@ __global__ __launch_bounds__(NTH, 2) void norm_bwd_kernel(const bf16_t* __restri
   const long long first = ((long long)blockIdx.x * 4 + w) * RPW + sub;
   constexpr int U = NCH == 1 ? 4 : NCH == 2 ? 2 : 1;   // rows per lane group in flight
   // next rows (x, dy, the residual gradient and the row statistics) in flight while this one is processed
-  uint4 nx[U][NCH], nd[U][NCH], nr[U][NCH];
+  uint4 nx[U][NCH], nd[U][NCH];
   float2 nst[U];
   const long long rbase = ((long long)blockIdx.x * 4 + w) * RPW + sub;
   // narrow rows: the lane group's scale is loaded once (all its rows are of group rbase % groups)
@@ -259,7 +273,6 @@ __global__ __launch_bounds__(NTH, 2) void norm_bwd_kernel(const bf16_t* __restri
     const long long row = rbase + u * nw, rc = row < rows ? row : rows - 1;
     load_rawc<NCH, LPR>(X + rc * F, F, sl, nx[u]);
     load_rawc<NCH, LPR>(DY + rc * F, F, sl, nd[u]);
-    if (R) load_rawc<NCH, LPR>(R + rc * F, F, sl, nr[u]);
     nst[u] = *reinterpret_cast<const float2*>(stats + 2 * rc);
   }
   for (long long r0 = rbase - sub; r0 < rows; r0 += U * nw) {
@@ -275,9 +288,11 @@ __global__ __launch_bounds__(NTH, 2) void norm_bwd_kernel(const bf16_t* __restri
     for (int c = 0; c < NCH; ++c) {
       cx[c] = nx[u][c];
       cd[c] = nd[u][c];
-      if (R) cr[c] = nr[u][c];
     }
-    if (R) load_rawc<NCH, LPR>(R + nrc * F, F, sl, nr[u]);
+    // the residual gradient is only read in the second pass: loaded for this row here (its latency hides under the
+    // first pass and the row reductions) instead of a row ahead -- 16 fewer live VGPRs at F = 2048, where the
+    // parameter-gradient sums already hold 64 (a row-ahead copy spilled ~60 VGPRs and doubled the kernel's time)
+    if (R) load_rawc<NCH, LPR>(R + (ok ? row : rows - 1) * F, F, sl, cr);
     load_rawc<NCH, LPR>(X + nrc * F, F, sl, nx[u]);
     load_rawc<NCH, LPR>(DY + nrc * F, F, sl, nd[u]);
     const float mean = ok ? nst[u].x : 0.f, rstd = ok ? nst[u].y : 0.f;
@@ -330,7 +345,7 @@ __global__ __launch_bounds__(NTH, 2) void norm_bwd_kernel(const bf16_t* __restri
         const float g0 = scale ? gsc[j0] : 1.f, g1 = scale ? gsc[j1] : 1.f;
         const float xh0 = (x[j0] - mean) * rstd, xh1 = (x[j1] - mean) * rstd;
         const float d0 = dy[j0] * g0, d1 = dy[j1] * g1;
-        o[j] = pack_bf16x2(rstd * (d0 - m1 - xh0 * m2) + r[j0], rstd * (d1 - m1 - xh1 * m2) + r[j1]);
+        o[j] = pk2(rstd * (d0 - m1 - xh0 * m2) + r[j0], rstd * (d1 - m1 - xh1 * m2) + r[j1]);
       }
       *reinterpret_cast<uint4*>(DX + row * F + col) = make_uint4(o[0], o[1], o[2], o[3]);
     }
@@ -483,10 +498,12 @@ OBST_API int obst_norm_partial(const ObstNormDesc* d, hipStream_t st) {
 }
 
 static int norm_bwd_grid(const ObstNormDesc* d) {
-  // one resident wave of blocks (~170 VGPRs: 2 blocks of 4 waves per CU) grid-strides over the rows; more blocks
-  // only grow the parameter-gradient slab that norm_fold_kernel reads back (2048 blocks: 103 us per fold)
+  // one resident wave of blocks (2 blocks of 4 waves per CU; wide rows: 1, bwd_blocks_per_cu) grid-strides over the
+  // rows; more blocks only grow the parameter-gradient slab that norm_fold_kernel reads back (2048 blocks: 103 us)
+  const int lpr = lanes_per_row(d->F);
+  const int cap = (d->F + lpr * 8 - 1) / (lpr * 8) > 4 ? 256 : 512;
   long long g = (d->rows + 15) / 16;
-  int grid = (int)(g < 512 ? (g < 1 ? 1 : g) : 512);
+  int grid = (int)(g < cap ? (g < 1 ? 1 : g) : cap);
   if (d->groups > 1) {   // rows per grid step (4 waves x 64/LPR rows per block) must be a multiple of groups
     int a = d->groups, b = 4 * (64 / lanes_per_row(d->F));
     while (b) { const int t = a % b; a = b; b = t; }
