@@ -31,6 +31,12 @@
 #include "gemm_kern.h"
 #include <utility>
 
+// G4W_EXP (diagnostic builds of tools/gemm_bench only, never the library): bit 0 drops the K loop's LDS-DMAs, bit 1
+// its fragment reads, bit 2 its two barriers -- which resource bounds the loop (outputs are garbage)
+#ifndef G4W_EXP
+#define G4W_EXP 0
+#endif
+
 namespace {
 
 typedef __attribute__((ext_vector_type(4))) int i32x4_t;
@@ -117,17 +123,23 @@ __device__ __forceinline__ void static_for(F&& f) {
   static_for_impl(f, std::make_integer_sequence<int, N>{});
 }
 
+// chunk swizzle of a K-contiguous B image: frag_b reads rows {0-3, 8-11, 16-19, 24-27} + base per lane group, on
+// which the A images' (row >> 1) & 7 is 2-way bank-conflicted (67 M conflict cycles per 131072x4096x2048 launch);
+// row bits 1, 3 and 4 give the 16 lanes of every ds_read_b128 group distinct bank quads (profiles/r3_gemm4w_bounds.md)
+__device__ __forceinline__ int bswz(int r) { return ((r >> 1) & 1) | (((r >> 3) & 1) << 1) | (((r >> 4) & 1) << 2); }
+
 // per-lane source offsets (bytes, relative to a K-tile's base) of the 8 LDS-DMA pieces this wave stages for one
 // operand -- the same for every tile (edges are handled by the resource's num_records). T = 0: [rows][K] operand,
-// piece P = 8 rows of 128 B; T = 1: [K][rows] operand, piece P = 4 k-rows x 128 columns of half P >> 4.
-template <int T>
+// piece P = 8 rows of 128 B (BI: the B image's swizzle); T = 1: [K][rows] operand, piece P = 4 k-rows x 128 columns
+// of half P >> 4.
+template <int T, bool BI = false>
 __device__ __forceinline__ void piece_offsets(int (&vo)[8], long long ld, int wave, int lane) {
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     const int P = wave * 8 + q;
     if (T == 0) {
       const int row = P * 8 + (lane >> 3);
-      const int c = (lane & 7) ^ ((row >> 1) & 7);
+      const int c = (lane & 7) ^ (BI ? bswz(row) : ((row >> 1) & 7));
       vo[q] = (int)(row * ld * 2) + c * 16;
     } else {
       const int h = P >> 4, kr = (P & 15) * 4 + (lane >> 4);
@@ -156,7 +168,7 @@ __device__ __forceinline__ bf16x8_t frag_b(const char* img, int nbase, int j, in
   if (T == 0) {
     const int r = base + 8 * ((lane & 15) >> 2) + (lane & 3);
     const int c = kk * 4 + (lane >> 4);
-    return *reinterpret_cast<const bf16x8_t*>(img + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
+    return *reinterpret_cast<const bf16x8_t*>(img + r * 128 + ((c ^ bswz(r)) << 4));
   } else {
     const char* h = img + (base >> 7) * (Q_OP / 2);
     const int gg = lane >> 4, i16 = lane & 15, q = i16 >> 2, pp = i16 & 3;
@@ -239,7 +251,7 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs p) {
 
   int voa[8], vob[8];
   piece_offsets<A_T>(voa, p.lda, wave, lane);
-  piece_offsets<B_T>(vob, p.ldb, wave, lane);
+  piece_offsets<B_T, true>(vob, p.ldb, wave, lane);
   const unsigned lds0 = lds_u32(smem);
   // this wave's 8 pieces of an operand image are contiguous: 8 KiB at (wave * 8 KiB)
   auto stage_a = [&](int s) -> unsigned { return lds0 + s * Q_STAGE + wave * 8192; };
@@ -335,16 +347,18 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs p) {
         constexpr int sub = q >> 6, j = (q >> 3) & 7, i = q & 7;
         if constexpr (sub == 0) mfma_acc(acc[i][j], b0[j], a0[i]);
         else mfma_acc(acc[i][j], b1f[j], a1[i]);
-        if constexpr (q < 16) read_sub(s, K1{}, qc, a1, b1f);               // substep-1 fragments of position pos
+        if constexpr (q < 16 && !(G4W_EXP & 2)) read_sub(s, K1{}, qc, a1, b1f);   // substep-1 fragments of pos
         if constexpr (q == 16) dma_setup();                                 // resources of position pos + 2
         if constexpr (q == 25) {                                            // stage s fully read by every wave
           if constexpr (PROF) tw = __builtin_amdgcn_s_memtime();
           __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0) as a builtin: the compiler's wait model learns the
-          __builtin_amdgcn_s_barrier();          // substep-1 reads are done (asm would leave it waiting again)
+          if constexpr (!(G4W_EXP & 4)) __builtin_amdgcn_s_barrier();   // substep-1 reads are done
           if constexpr (PROF) sync1 += __builtin_amdgcn_s_memtime() - tw;
         }
-        if constexpr (q >= 26 && q < 64 && (q - 26) % 5 == 0) dma16(ra, voa[(q - 26) / 5], stage_a(s) + (q - 26) / 5 * 1024);
-        if constexpr (q >= 66 && q < 106 && (q - 66) % 5 == 0) dma16(rb, vob[(q - 66) / 5], stage_b(s) + (q - 66) / 5 * 1024);
+        if constexpr (!(G4W_EXP & 1) && q >= 26 && q < 64 && (q - 26) % 5 == 0)
+          dma16(ra, voa[(q - 26) / 5], stage_a(s) + (q - 26) / 5 * 1024);
+        if constexpr (!(G4W_EXP & 1) && q >= 66 && q < 106 && (q - 66) % 5 == 0)
+          dma16(rb, vob[(q - 66) / 5], stage_b(s) + (q - 66) / 5 * 1024);
         if constexpr (q == 107) {                                           // position pos+1 landed in stage s^1
           // first K-tile of a tile: the previous tile's epilogue stores sit between that position's DMAs and this
           // iteration's; count them out instead of waiting for every store (direct epilogue: 32 bf16 / 64 fp32)
@@ -352,10 +366,10 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs p) {
           if (t == 0 && rnd > 0 && first_wait == 48) vm_wait<48>();
           else if (t == 0 && rnd > 0 && first_wait == 63) vm_wait<63>();
           else vm_wait<16>();
-          __builtin_amdgcn_s_barrier();
+          if constexpr (!(G4W_EXP & 4)) __builtin_amdgcn_s_barrier();
           if constexpr (PROF) sync2 += __builtin_amdgcn_s_memtime() - tw;
         }
-        if constexpr (q >= 108 && q < 124)                                  // substep-0 fragments of position pos+1
+        if constexpr (q >= 108 && q < 124 && !(G4W_EXP & 2))                // substep-0 fragments of position pos+1
           read_sub(s ^ 1, K0{}, std::integral_constant<int, q - 108>{}, a0, b0);
         fence();
       });
