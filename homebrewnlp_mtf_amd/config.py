@@ -91,6 +91,8 @@ _DEFAULTS: typing.Dict[str, typing.Any] = dict(
     log_dict_keys=[],
     # ---- keys new in this framework (MI355X-native runtime) ----
     mesh=None,                   # {"dp": int, "tp": int}; default dp=world, tp=1
+    tp_layout="heads",           # "heads": the reference layout (intermediate replicated over TP); "intermediate":
+                                 # feed-forward weights split over the intermediate axis (layers.feed_forward)
     attention_scale="sequence",  # "sequence" (reference quirk A1, spatial.py:60) or "head" (1/sqrt(fph))
     seed=0,                      # parameter-init seed
     grad_bucket_mb=64,           # DP gradient all-reduce bucket size (xGMI ring per-link bound: SURVEY 5.8)

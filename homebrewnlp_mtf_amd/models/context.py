@@ -125,15 +125,22 @@ class Builder:
     def _global_dims(self, dims: typing.List[Dim]) -> typing.List[Dim]:
         return [self.global_params.head_dim if d == self.params.head_dim else d for d in dims]
 
-    def variable(self, args: "BlockArgs", kind: str, dims: typing.List[Dim], init_factory) -> torch.Tensor:
-        """``init_factory(global_dims) -> init(gen, device)``. Returns the variable as a compute-dtype tensor."""
+    def variable(self, args: "BlockArgs", kind: str, dims: typing.List[Dim], init_factory,
+                 shard: typing.Optional[typing.Tuple[Dim, Dim]] = None) -> torch.Tensor:
+        """``init_factory(global_dims) -> init(gen, device)``. Returns the variable as a compute-dtype tensor.
+        ``shard = (local_dim, global_dim)``: the TP-split axis instead of ``heads`` (dims then hold the global heads)"""
         dims = D.deduplicate(dims)
+
+        def gdims():
+            g = self._global_dims(dims)
+            return [shard[1] if shard is not None and d == shard[0] else d for d in g]
 
         def create() -> str:
             with self.scope(kind):
                 name = self.scope.path
             if self.register:
-                self.store.register(name, self._global_dims(dims), init_factory(self._global_dims(dims)))
+                self.store.register(name, gdims(), init_factory(gdims()),
+                                    shard=shard[1] if shard is not None else None)
             return name
 
         if "shared" in args:

@@ -30,15 +30,19 @@ ACTIVATIONS = ('relu', 'sigmoid', 'tanh', 'gelu', 'lecun_tanh', 'silu', 'mish', 
 
 # ================================================================================================================
 # variables (ref src/model/backend.py:43-118)
-def orthogonal_var(args: BlockArgs, dims: typing.List[Dim], fan_in_dims: typing.Optional[typing.List[Dim]] = None):
+def orthogonal_var(args: BlockArgs, dims: typing.List[Dim], fan_in_dims: typing.Optional[typing.List[Dim]] = None,
+                   shard: typing.Optional[typing.Tuple[Dim, Dim]] = None):
+    """shard = (local, global) dim: TP-split axis other than heads (tp_layout intermediate)"""
     p = args.params
     gb = args.builder
     fan_dims = None if fan_in_dims is None else gb._global_dims(list(fan_in_dims))
+    if fan_dims is not None and shard is not None:
+        fan_dims = [shard[1] if d == shard[0] else d for d in fan_dims]
     sbd = bool(p.scale_by_depth and args.is_last)
 
     def factory(gdims):
         return orthogonal_init([d.size for d in gdims], fan_in_size(fan_dims), sbd, p.depth)
-    return args.builder.variable(args, "orthogonal_var", dims, factory)
+    return args.builder.variable(args, "orthogonal_var", dims, factory, shard=shard)
 
 
 def normal_var(args: BlockArgs, dims: typing.List[Dim], stddev: float = 0.02, mean: float = 0.):
@@ -241,6 +245,25 @@ def feed_forward(args: BlockArgs) -> Act:
             ok = p1.x_perm is None and p1.o_perm is None and p2.x_perm is None and p2.o_perm is None
         except (NotImplementedError, ValueError):
             ok = False
+        tp = pstate.tp_size()
+        if (ok and tp > 1 and p.tp_layout == "intermediate" and list(old1) == list(p.feature_dims)
+                and list(new1) == list(p.intermediate) and len(new1) == 1 and list(old2) == list(new1)
+                and list(new2) == list(p.feature_dims) and new1[0].size % tp == 0 and x.dims[2:] == old1):
+            # intermediate axis split over TP: same variables and global shapes as the heads layout,
+            # sharded along the intermediate instead of the heads (checkpoints reshard between the two)
+            hg = args.builder.global_params.head_dim
+            ig = new1[0]
+            il = Dim(ig.name, ig.size // tp)
+            w1 = _scoped(a_in, "linear", orthogonal_var, a_in, [hg, p.key_dim, il], [hg, p.key_dim], shard=(il, ig))
+            w2 = _scoped(a_out, "linear", orthogonal_var, a_out, [il, hg, p.key_dim], [il], shard=(il, ig))
+            xg = list(x.dims[:2]) + [hg, p.key_dim]
+            res = args.residual if (args.residual is not None and args.residual.dims == odims) else None
+            y = F.ffn_itp(x.t, w1, w2, xg, [hg, p.key_dim, il], list(x.dims[:2]) + [il], [il, hg, p.key_dim], xg,
+                          act_in, residual=res.t if res is not None else None,
+                          carrier=getattr(args, "residual_carrier", None) if res is not None else None)
+            if res is not None:
+                args.residual_consumed = True
+            return Act(y, odims)
         if ok:
             w1 = _scoped(a_in, "linear", orthogonal_var, a_in, list(old1) + list(new1), list(old1))
             w2 = _scoped(a_out, "linear", orthogonal_var, a_out, list(old2) + list(new2), list(old2))

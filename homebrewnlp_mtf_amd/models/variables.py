@@ -154,13 +154,17 @@ class ParamStore:
         self._leaves: typing.Dict[str, torch.Tensor] = {}
 
     # -- registration ---------------------------------------------------------------------------------------------
-    def register(self, name: str, dims: typing.List[Dim], init, trainable: bool = True) -> VarSpec:
+    def register(self, name: str, dims: typing.List[Dim], init, trainable: bool = True,
+                 shard: typing.Optional[Dim] = None) -> VarSpec:
+        """dims: global; the TP-split axis is ``heads`` unless ``shard`` names another one (tp_layout intermediate)"""
         if name in self.specs:
             return self.specs[name]
         if self.finalized:
             raise KeyError(f"variable {name} requested after the parameter store was finalized")
         tp_dim = None
-        if self.tp_size > 1 and self.params.head_dim in dims:
+        if self.tp_size > 1 and shard is not None:
+            tp_dim = list(dims).index(shard)
+        elif self.tp_size > 1 and self.params.head_dim in dims:
             tp_dim = list(dims).index(self.params.head_dim)
         spec = VarSpec(name, dims, init, tp_dim, self.tp_size, trainable)
         self.specs[name] = spec

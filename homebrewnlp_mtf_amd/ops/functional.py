@@ -337,6 +337,65 @@ class _FFN(torch.autograd.Function):
         return (dx, None if m1 else g1.to(w1.dtype), None if m2 else g2.to(w2.dtype), None, None, None, dres, None)
 
 
+class _FFNItp(torch.autograd.Function):
+    """Feed-forward with the intermediate axis split over the TP group (``tp_layout: "intermediate"``):
+    the input's heads are gathered (all-gather [T, d/tp] -> [T, d]), both GEMMs run on this rank's slice of the
+    intermediate, and the partial output is reduce-scattered back to this rank's heads; backward mirrors it
+    (all-gather dy, reduce-scatter dx). Wire bytes per layer and direction: 2 T d (x (tp-1)/tp) against 2 T I for
+    the reference layout's all-reduce of the replicated [T, I] intermediate -- 4x fewer at I = 4d."""
+
+    @staticmethod
+    def forward(ctx, x, w1, w2, p1: LinearPlan, p2: LinearPlan, act, residual, carrier=None):
+        T = p1.M
+        dl = x.numel() // T
+        xf = pstate.tp_gather_rows(x.contiguous().view(T, dl), T, dl)
+        z = _empty(p1.canon_o_shape, xf)
+        a = _empty(p1.canon_o_shape, xf) if act else z
+        _fwd_gemm(xf, w1, a, p1, act=act, Zout=z if act else None)
+        yf = _empty([T, p2.N], xf)
+        _fwd_gemm(a, w2, yf, p2)
+        y = pstate.tp_reduce_scatter_rows(yf, T, dl).view(x.shape)
+        if residual is not None:
+            raw.elementwise("add", y, y, z=residual.contiguous())
+        ctx.save_for_backward(xf, w1, w2, z, a if act else None)
+        ctx.p1, ctx.p2, ctx.act, ctx.has_res, ctx.carrier = p1, p2, act, residual is not None, carrier
+        ctx.xshape = x.shape
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xf, w1, w2, z, a = ctx.saved_tensors
+        p1, p2, act = ctx.p1, ctx.p2, ctx.act
+        a = z if a is None else a
+        T = p1.M
+        dl = dy.numel() // T
+        dyf = pstate.tp_gather_rows(dy.contiguous().view(T, dl), T, dl)
+        dz = _empty(p1.canon_o_shape, dyf)
+        _dgrad_gemm(dyf, w2, dz, p2, act=act, Zin=z if act else None)
+        g2, m2, b2 = _acc_grad_beta(w2)
+        _wgrad_gemm(a, dyf, g2, p2, beta=b2)
+        _done(w2)
+        dxf = _empty([T, p1.H * p1.K], dyf)
+        _dgrad_gemm(dz, w1, dxf, p1)
+        dx = pstate.tp_reduce_scatter_rows(dxf, T, dl).view(ctx.xshape)
+        g1, m1, b1 = _acc_grad_beta(w1)
+        _wgrad_gemm(xf, dz, g1, p1, beta=b1)
+        _done(w1)
+        dres = dy if ctx.has_res else None
+        if dres is not None and ctx.carrier is not None:
+            ctx.carrier.grad, dres = dres, None
+        return (dx, None if m1 else g1.to(w1.dtype), None if m2 else g2.to(w2.dtype), None, None, None, dres, None)
+
+
+def ffn_itp(x, w1, w2, xg_dims, w1dims, mdims, w2dims, og_dims, act, residual=None, carrier=None):
+    """x: this rank's heads; xg_dims / og_dims: the same dims with the global heads (what the GEMMs see)"""
+    p1 = linear_plan(tuple(xg_dims), tuple(w1dims), tuple(mdims))
+    p2 = linear_plan(tuple(mdims), tuple(w2dims), tuple(og_dims))
+    if p1.x_perm is not None or p1.o_perm is not None or p2.x_perm is not None or p2.o_perm is not None:
+        raise NotImplementedError("intermediate-split FFN needs canonical layouts")
+    return _FFNItp.apply(x, w1, w2, p1, p2, act, residual, carrier)
+
+
 def ffn(x, w1, w2, xdims, w1dims, mdims, w2dims, odims, act, residual=None, carrier=None):
     p1 = linear_plan(tuple(xdims), tuple(w1dims), tuple(mdims))
     p2 = linear_plan(tuple(mdims), tuple(w2dims), tuple(odims))

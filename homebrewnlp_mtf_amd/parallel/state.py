@@ -87,3 +87,42 @@ def tp_all_reduce_async(t: torch.Tensor):
         debug.record("tp_all_reduce", t)
         return dist.all_reduce(t, op=dist.ReduceOp.SUM, group=_MESH.tp_group, async_op=True)
     return _DONE
+
+
+def _gloo(group) -> bool:
+    return dist.get_backend(group) == "gloo"
+
+
+def tp_gather_rows(x: torch.Tensor, T: int, inner: int) -> torch.Tensor:
+    """x [T, inner] -- this rank's contiguous block of the columns of a token-major [T, tp * inner] tensor (its heads)
+    -> the whole [T, tp * inner]: one all-gather into [tp][T][inner] and one transposing copy"""
+    tp = _MESH.tp
+    if x.device.type == "meta":   # the registration pass
+        return torch.empty(T, tp * inner, dtype=x.dtype, device="meta")
+    from ..utils import debug
+    debug.record("tp_all_gather", x)
+    src = x.contiguous().view(-1)
+    if _gloo(_MESH.tp_group):   # CPU rehearsal: gloo has no all_gather_into_tensor for every dtype
+        parts = [torch.empty_like(src) for _ in range(tp)]
+        dist.all_gather(parts, src, group=_MESH.tp_group)
+        buf = torch.stack(parts)
+    else:
+        buf = torch.empty(tp * src.numel(), dtype=x.dtype, device=x.device)
+        dist.all_gather_into_tensor(buf, src, group=_MESH.tp_group)
+    return buf.view(tp, T, inner).transpose(0, 1).contiguous().view(T, tp * inner)
+
+
+def tp_reduce_scatter_rows(y: torch.Tensor, T: int, inner: int) -> torch.Tensor:
+    """y [T, tp * inner] partial sums -> this rank's block [T, inner] of their sum over the TP group"""
+    tp = _MESH.tp
+    if y.device.type == "meta":
+        return torch.empty(T, inner, dtype=y.dtype, device="meta")
+    from ..utils import debug
+    debug.record("tp_reduce_scatter", y)
+    src = y.view(T, tp, inner).transpose(0, 1).contiguous()
+    if _gloo(_MESH.tp_group):   # gloo: all-reduce, keep this rank's block
+        dist.all_reduce(src, group=_MESH.tp_group)
+        return src[_MESH.tp_rank].contiguous()
+    out = torch.empty(T * inner, dtype=y.dtype, device=y.device)
+    dist.reduce_scatter_tensor(out, src.view(-1), group=_MESH.tp_group)
+    return out.view(T, inner)

@@ -96,7 +96,7 @@ def test_dp_matches_single_rank():
     assert abs((ranks[0]["losses"][0] + ranks[1]["losses"][0]) / 2 - ref_losses[0]) < 1e-5
 
 
-@pytest.mark.parametrize("strategy", ["none", "revnet", "activated_attention_input"])
+@pytest.mark.parametrize("strategy", ["none", "revnet", "activated_attention_input", "intermediate_layout"])
 def test_tp_matches_single_rank(strategy):
     """fused FFN (W1 contracts the sharded heads: reduce-then-activate; dz reduced after the fused act-backward) and
     the fused attention block, also with an activated input projection"""
@@ -107,7 +107,16 @@ def test_tp_matches_single_rank(strategy):
     if strategy == "revnet":
         cfg["block_config"] = [{"layer": ["norm-shift-scale", "attention-dot_product-context"]},
                                {"layer": ["norm-shift-scale-group", "feed_forward-in:gelu"]}]
+    if strategy == "intermediate_layout":
+        # feed-forward weights split over the intermediate axis (all-gather x, reduce-scatter y)
+        cfg["tp_layout"] = "intermediate"
+        cfg["block_config"] = [{"layer": ["norm-shift-scale", "attention-dot_product-context"], "skip": True},
+                               {"layer": ["norm-shift-scale", "feed_forward-in:gelu"], "skip": True}]
     ranks = _run("tp", cfg)
+    if strategy == "intermediate_layout":
+        ffn = [n for n in ranks[0]["specs"] if "feed_forward" in n]
+        # w1 [heads, fph, I] split on axis 2, w2 [I, heads, fph] on axis 0 -- the intermediate, not the heads
+        assert ffn and {ranks[0]["specs"][n][2] for n in ffn} == {0, 2}
     ref, ref_losses = _single(cfg)
     for r in ranks:
         for a, b in zip(r["losses"], ref_losses):

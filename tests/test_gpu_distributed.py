@@ -45,7 +45,8 @@ def _worker(rank, world, port, mode, out_dir):
     dp, tp = (world, 1) if mode == "dp" else (1, world)
     mesh = pstate.Mesh(dp=dp, tp=tp, rank=rank).build_groups()
     torch.manual_seed(0)
-    tr = Trainer(ModelParameter(dict(CFG, mesh={"dp": dp, "tp": tp})), dev, mesh)
+    extra = {"tp_layout": "intermediate"} if mode == "tp_intermediate" else {}
+    tr = Trainer(ModelParameter(dict(CFG, mesh={"dp": dp, "tp": tp}, **extra)), dev, mesh)
     losses = []
     for i in range(3):
         b = {k: v.to(dev) for k, v in _batch(i).items()}
@@ -86,8 +87,10 @@ def test_gpu_dp_matches_single_rank(cuda):
     assert diff < 1e-3, f"DP weights differ from the single-rank GPU step by {diff}"
 
 
-def test_gpu_tp_matches_single_rank(cuda):
-    ranks = _run("tp")
+@pytest.mark.parametrize("mode", ["tp", "tp_intermediate"])
+def test_gpu_tp_matches_single_rank(cuda, mode):
+    """heads layout, and the intermediate-split feed-forward (all-gather x / reduce-scatter y)"""
+    ranks = _run(mode)
     ref, ref_losses = _single(cuda)
     for r in ranks:
         for a, b in zip(r["losses"], ref_losses):
