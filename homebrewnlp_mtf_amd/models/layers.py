@@ -374,6 +374,11 @@ def bottleneck_group_linear(args: BlockArgs) -> Act:
 
 # ================================================================================================================
 # norm (ref normalization.py:22-34)
+# norms whose normalized dims are not x's trailing dims run the norm kernel on a permuted copy (False: the torch
+# autograd path -- the CPU tests' reference for it)
+NORM_ANY_LAYOUT = True
+
+
 def norm(args: BlockArgs, feature_shape: typing.Optional[typing.List[Dim]] = None) -> Act:
     p = args.params
     x = args.tensor
@@ -394,6 +399,27 @@ def norm(args: BlockArgs, feature_shape: typing.Optional[typing.List[Dim]] = Non
         y = F.norm(x.t, scale, shift, Fsz, groups, tp_stats=tp_stats,
                    carrier=getattr(args, "norm_carrier", None))
         return Act(y, x.dims)
+    # any other layout: permute to [others..., group?, normalized...] (row % groups = the group index), the same
+    # kernel, permute back; parameters are permuted copies to [group?, normalized...] (their gradients flow back
+    # through autograd instead of the fused main-grad accumulation)
+    gdim = [p.head_dim] if group and p.head_dim in feature_shape and p.head_dim in x.dims else []
+    if NORM_ANY_LAYOUT and all(d in x.dims for d in normalized) and (not group or gdim):
+        others = [d for d in x.dims if d not in normalized and d not in gdim]
+        order = others + gdim + normalized
+        perm = [x.dims.index(d) for d in order]
+        xp = x.t.permute(perm).contiguous()
+        pshape = gdim + normalized
+
+        def _param(t):
+            if t is None:
+                return None
+            return t.permute([feature_shape.index(d) for d in pshape]).contiguous() if feature_shape != pshape else t
+        Fsz = int(math.prod(d.size for d in normalized))
+        groups = p.head_dim.size if gdim else 1
+        tp_stats = (not gdim) and p.head_dim in normalized and pstate.tp_size() > 1
+        y = F.norm(xp, _param(scale), _param(shift), Fsz, groups, tp_stats=tp_stats)
+        inv = [order.index(d) for d in x.dims]
+        return Act(y.view([d.size for d in order]).permute(inv), x.dims)
     # general path (torch autograd)
     axes = [x.dims.index(d) for d in normalized]
     xt = x.t.float()

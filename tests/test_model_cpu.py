@@ -485,3 +485,30 @@ def test_attention_map_oracle_gradients(causal, maps):
     g2 = torch.autograd.grad(ref, ins, do)
     for a, b in zip(g1, g2):
         assert torch.allclose(a, b, atol=1e-10), (a - b).abs().max()
+
+
+@pytest.mark.parametrize("layers", [["transpose_sequence_features", "norm-shift-scale", "transpose_sequence_features"],
+                                    ["transpose_sequence_features", "norm-shift-scale-group",
+                                     "transpose_sequence_features"]])
+def test_norm_any_layout_matches_torch_path(layers, monkeypatch):
+    """norms over non-trailing dims run the norm kernel on a permuted copy: loss and gradients == the torch path"""
+    from homebrewnlp_mtf_amd.models import layers as LY
+    res = {}
+    for fast in (True, False):
+        monkeypatch.setattr(LY, "NORM_ANY_LAYOUT", fast)
+        torch.manual_seed(0)
+        m = Model(ModelParameter(dict(BASE, calculation_dtype="float64",
+                                      block_config=[{"layer": layers, "skip": True}])), "cpu")
+        st = m.store
+        st.master = st.master.double()
+        st.grad = st.grad.double()
+        st.compute = st.master
+        st._leaves = {}
+        st.master.copy_(torch.randn_like(st.master) * 0.3 + 0.5)
+        x = torch.randint(0, 50, (2, 8, 1), generator=torch.Generator().manual_seed(3))
+        out = m(x, x)
+        out["loss"].backward()
+        st.fold_leaf_grads()
+        res[fast] = (float(out["loss"].detach()), st.grad.clone())
+    assert abs(res[True][0] - res[False][0]) < 1e-5
+    assert torch.allclose(res[True][1], res[False][1], atol=1e-5, rtol=1e-4)
