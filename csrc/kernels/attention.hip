@@ -1232,7 +1232,7 @@ static int attn_impl() {   // OBST_ATTN_IMPL=1 forces the 16x16x32 kernels (A/B 
 // (the longer blocks lose more to the causal-diagonal imbalance than the deeper ring gains; r2 bench_attn_ab)
 // OBST_ATTN_DKV_KG=2: two 16-key groups per dK/dV wave (half the LDS bytes per MFMA, ~490 registers: one wave per
 // SIMD). A/B only: B64 S2048 H16 D128 causal backward 5.24 -> 6.27 ms (3-deep ring: 6.33) -- without the partner
-// wave the softmax VALU and the LDS waits no longer hide under another wave's MFMAs (r2 tools/gpu_attn_kg.sh)
+// wave the softmax VALU and the LDS waits no longer hide under another wave's MFMAs (r2 tools/lab/gpu_attn_kg.sh)
 static int attn_dkv_kg() {
   static int v = [] { const char* e = getenv("OBST_ATTN_DKV_KG"); return e ? atoi(e) : 1; }();
   return v;

@@ -19,8 +19,9 @@
 // kernels compute the score tile transposed (rows = keys, columns = queries), so each lane owns one query and the
 // softmax statistics are lane-local (two xor-shuffles across the 4 lane groups). The probability registers feed the
 // next MFMA's B operand directly under a permuted contraction order -- slots 0-3 = rows 4g..4g+3 of one 16-row
-// tile, slots 4-7 = the same rows of the next -- and the matching A operand is read from a transposed LDS image
-// with the same permutation (frag_tp). The key-major dk/dv kernel does the same with queries and keys swapped.
+// tile, slots 4-7 = the same rows of the next -- and the matching A operand is read from the same row-major LDS
+// image by the CDNA4 transposing read ds_read_b64_tr_b16 with that permutation (frag_tr): every tile is staged
+// once, row-major. The key-major dk/dv kernel does the same with queries and keys swapped.
 #include "common.h"
 
 namespace {
@@ -28,7 +29,6 @@ namespace {
 constexpr int TQ = 64;    // queries per workgroup (16 per wave)
 constexpr int TK = 64;    // keys per tile
 constexpr int PADR = 8;   // row pad of the row-major images [64][D + PADR] (16-B fragment reads conflict-free)
-constexpr int PADT = 8;   // row pad of the transposed images [D][64 + PADT]
 
 struct MapArgs {
   const bf16_t* q;
@@ -64,17 +64,13 @@ __device__ __forceinline__ void stage_rm(bf16_t* img, const bf16_t* g, long long
     *reinterpret_cast<uint4*>(img + r * (D + PADR) + cc * 8) = ld16(g + (long long)(r0 + r) * ld + cc * 8, r0 + r < S);
   }
 }
-// the same rows transposed: img[d][row]
-template <int D>
-__device__ __forceinline__ void stage_tr(bf16_t* img, const bf16_t* g, long long ld, int r0, int S, int tid) {
-  constexpr int CH = D / 8;
-  for (int c = tid; c < 64 * CH; c += 256) {
-    const int r = c & 63, cc = c >> 6;   // neighbouring threads: neighbouring rows = neighbouring LDS halfwords
-    const uint4 v = ld16(g + (long long)(r0 + r) * ld + cc * 8, r0 + r < S);
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+// map values of keys key0 .. key0 + 3 on one query row (16-byte load when in range; zero past S)
+__device__ __forceinline__ f32x4_t map4(const float* row, int key0, int S) {
+  if ((S & 3) == 0 && key0 + 3 < S) return *reinterpret_cast<const f32x4_t*>(row + key0);
+  f32x4_t v;
 #pragma unroll
-    for (int t = 0; t < 8; ++t) img[(cc * 8 + t) * (64 + PADT) + r] = (bf16_t)(w[t >> 1] >> (16 * (t & 1)));
-  }
+  for (int r = 0; r < 4; ++r) v[r] = key0 + r < S ? row[key0 + r] : 0.f;
+  return v;
 }
 
 // operand of 16 rows (rb + lane & 15) x 32 contraction elements (kk * 32 + 8 g ..) from a row-major image
@@ -82,16 +78,20 @@ template <int RS>
 __device__ __forceinline__ bf16x8_t frag_rm(const bf16_t* img, int rb, int kk, int lane) {
   return *reinterpret_cast<const bf16x8_t*>(img + (rb + (lane & 15)) * RS + kk * 32 + 8 * (lane >> 4));
 }
-// A operand of 16 rows of a transposed image over the permuted contraction slots of chunk c:
-// slots 0-3 = columns 32c + 4g .. +3, slots 4-7 = columns 32c + 16 + 4g .. +3
+// A operand [m = mb + (lane & 15)][k slots of chunk c] from a ROW-MAJOR image [k][m] (row stride RS elements) by
+// the transposing read: per 16-lane group, lane 4q+p addresses row q of a 4-row block at columns 4p..4p+3 and lane i
+// receives column i of the 4 rows (cdna guide T10). Slots 0-3 = rows 32c + 4g .. +3, slots 4-7 = rows 32c + 16 + 4g ..
+// (g = lane >> 4): the permutation frag_acc gives the matching B operand. Called with EXEC all ones only.
 template <int RS>
-__device__ __forceinline__ bf16x8_t frag_tp(const bf16_t* img, int rb, int c, int lane) {
-  const bf16_t* p = img + (rb + (lane & 15)) * RS + 32 * c + 4 * (lane >> 4);
-  const uint2 lo = *reinterpret_cast<const uint2*>(p);
-  const uint2 hi = *reinterpret_cast<const uint2*>(p + 16);
-  return __builtin_bit_cast(bf16x8_t, make_uint4(lo.x, lo.y, hi.x, hi.y));
+__device__ __forceinline__ bf16x8_t frag_tr(const bf16_t* img, int mb, int c, int lane) {
+  const int g = lane >> 4, i = lane & 15;
+  const bf16_t* p0 = img + (32 * c + 4 * g + (i >> 2)) * RS + mb + 4 * (i & 3);
+  const s16x4_t v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4_t, p0));
+  const s16x4_t v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4_t, p0 + 16 * RS));
+  const s16x8_t v = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+  return __builtin_bit_cast(bf16x8_t, v);
 }
-// B operand from two accumulator tiles in C layout (same slot permutation as frag_tp)
+// B operand from two accumulator tiles in C layout (same slot permutation as frag_tr)
 __device__ __forceinline__ bf16x8_t frag_acc(const f32x4_t& t0, const f32x4_t& t1) {
   return __builtin_bit_cast(bf16x8_t, make_uint4(pack_bf16x2(t0[0], t0[1]), pack_bf16x2(t0[2], t0[3]),
                                                  pack_bf16x2(t1[0], t1[1]), pack_bf16x2(t1[2], t1[3])));
@@ -104,7 +104,7 @@ __device__ __forceinline__ f32x4_t mfma(const bf16x8_t& a, const bf16x8_t& b, co
 template <int D>
 __global__ __launch_bounds__(256) void attn_map_fwd_kernel(MapArgs a) {
   __shared__ __attribute__((aligned(16))) bf16_t kimg[64 * (D + PADR)];
-  __shared__ __attribute__((aligned(16))) bf16_t vt[D * (64 + PADT)];
+  __shared__ __attribute__((aligned(16))) bf16_t vimg[64 * (D + PADR)];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
   const int S = a.S, nqb = (S + TQ - 1) / TQ;
   const int qb = nqb - 1 - (int)blockIdx.x;   // longest causal rows first
@@ -127,7 +127,7 @@ __global__ __launch_bounds__(256) void attn_map_fwd_kernel(MapArgs a) {
     const int k0 = kt * TK;
     __syncthreads();
     stage_rm<D>(kimg, a.k + base, ld, k0, S, tid);
-    stage_tr<D>(vt, a.v + base, ld, k0, S, tid);
+    stage_rm<D>(vimg, a.v + base, ld, k0, S, tid);
     __syncthreads();
     f32x4_t s[4];
 #pragma unroll
@@ -138,35 +138,32 @@ __global__ __launch_bounds__(256) void attn_map_fwd_kernel(MapArgs a) {
     }
     float mx = -INFINITY;
 #pragma unroll
-    for (int kb = 0; kb < 4; ++kb)
+    for (int kb = 0; kb < 4; ++kb) {
+      const f32x4_t bv = a.bias != nullptr ? map4(a.bias + mrow, k0 + kb * 16 + 4 * g, S) : f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int key = k0 + kb * 16 + 4 * g + r;
         const bool ok = key < S && (!a.causal || key <= myq);
-        float x = s[kb][r] * a.scale;
-        if (a.bias != nullptr && ok) x += a.bias[mrow + key];
-        x = ok ? x : -INFINITY;
+        const float x = ok ? s[kb][r] * a.scale + bv[r] : -INFINITY;
         s[kb][r] = x;
         mx = fmaxf(mx, x);
       }
+    }
     mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     const float mn = fmaxf(m, mx);   // finite: key k0 <= every query of a visited tile
     const float al = __expf(m - mn);
     float rs = 0.f;
 #pragma unroll
-    for (int kb = 0; kb < 4; ++kb)
+    for (int kb = 0; kb < 4; ++kb) {
+      const f32x4_t cv = a.cmap != nullptr ? map4(a.cmap + mrow, k0 + kb * 16 + 4 * g, S) : f32x4_t{1.f, 1.f, 1.f, 1.f};
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const float p = __expf(s[kb][r] - mn);
         rs += p;
-        float c = 1.f;
-        if (a.cmap != nullptr) {
-          const int key = k0 + kb * 16 + 4 * g + r;
-          if (key < S) c = a.cmap[mrow + key];
-        }
-        s[kb][r] = p * c;
+        s[kb][r] = p * cv[r];
       }
+    }
     rs += __shfl_xor(rs, 16, 64);
     rs += __shfl_xor(rs, 32, 64);
     l = l * al + rs;
@@ -177,7 +174,7 @@ __global__ __launch_bounds__(256) void attn_map_fwd_kernel(MapArgs a) {
     for (int c = 0; c < 2; ++c) {
       const bf16x8_t pb = frag_acc(s[2 * c], s[2 * c + 1]);
 #pragma unroll
-      for (int i = 0; i < D / 16; ++i) acc[i] = mfma(frag_tp<64 + PADT>(vt, i * 16, c, lane), pb, acc[i]);
+      for (int i = 0; i < D / 16; ++i) acc[i] = mfma(frag_tr<D + PADR>(vimg, i * 16, c, lane), pb, acc[i]);
     }
   }
   if (qok) {
@@ -197,7 +194,6 @@ template <int D>
 __global__ __launch_bounds__(256) void attn_map_dq_kernel(MapArgs a) {
   __shared__ __attribute__((aligned(16))) bf16_t kimg[64 * (D + PADR)];
   __shared__ __attribute__((aligned(16))) bf16_t vimg[64 * (D + PADR)];
-  __shared__ __attribute__((aligned(16))) bf16_t kt[D * (64 + PADT)];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
   const int S = a.S, nqb = (S + TQ - 1) / TQ;
   const int qb = nqb - 1 - (int)blockIdx.x;
@@ -235,7 +231,6 @@ __global__ __launch_bounds__(256) void attn_map_dq_kernel(MapArgs a) {
     __syncthreads();
     stage_rm<D>(kimg, a.k + base, ld, k0, S, tid);
     stage_rm<D>(vimg, a.v + base, ld, k0, S, tid);
-    stage_tr<D>(kt, a.k + base, ld, k0, S, tid);
     __syncthreads();
     f32x4_t s[4], dp[4];
 #pragma unroll
@@ -248,25 +243,23 @@ __global__ __launch_bounds__(256) void attn_map_dq_kernel(MapArgs a) {
       }
     }
 #pragma unroll
-    for (int kb = 0; kb < 4; ++kb)
+    for (int kb = 0; kb < 4; ++kb) {
+      const int key0 = k0 + kb * 16 + 4 * g;
+      const f32x4_t bv = a.bias != nullptr ? map4(a.bias + mrow, key0, S) : f32x4_t{0.f, 0.f, 0.f, 0.f};
+      const f32x4_t cv = a.cmap != nullptr ? map4(a.cmap + mrow, key0, S) : f32x4_t{1.f, 1.f, 1.f, 1.f};
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int key = k0 + kb * 16 + 4 * g + r;
+        const int key = key0 + r;
         const bool ok = qok && key < S && (!a.causal || key <= myq);
-        float x = s[kb][r] * a.scale;
-        float c = 1.f;
-        if (ok) {
-          if (a.bias != nullptr) x += a.bias[mrow + key];
-          if (a.cmap != nullptr) c = a.cmap[mrow + key];
-        }
-        const float p = ok ? __expf(x - lse) : 0.f;
-        s[kb][r] = p * (c * dp[kb][r] - dl);
+        const float p = ok ? __expf(s[kb][r] * a.scale + bv[r] - lse) : 0.f;
+        s[kb][r] = p * (cv[r] * dp[kb][r] - dl);
       }
+    }
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       const bf16x8_t sb = frag_acc(s[2 * c], s[2 * c + 1]);
 #pragma unroll
-      for (int i = 0; i < D / 16; ++i) acc[i] = mfma(frag_tp<64 + PADT>(kt, i * 16, c, lane), sb, acc[i]);
+      for (int i = 0; i < D / 16; ++i) acc[i] = mfma(frag_tr<D + PADR>(kimg, i * 16, c, lane), sb, acc[i]);
     }
   }
   if (qok) {
@@ -284,9 +277,7 @@ __global__ __launch_bounds__(256) void attn_map_dq_kernel(MapArgs a) {
 template <int D>
 __global__ __launch_bounds__(256) void attn_map_dkv_kernel(MapArgs a) {
   __shared__ __attribute__((aligned(16))) bf16_t qimg[64 * (D + PADR)];
-  __shared__ __attribute__((aligned(16))) bf16_t qt[D * (64 + PADT)];
   __shared__ __attribute__((aligned(16))) bf16_t dimg[64 * (D + PADR)];
-  __shared__ __attribute__((aligned(16))) bf16_t dt[D * (64 + PADT)];
   __shared__ float lse_s[TQ], dl_s[TQ];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
   const int S = a.S, nqb = (S + TQ - 1) / TQ;
@@ -316,9 +307,7 @@ __global__ __launch_bounds__(256) void attn_map_dkv_kernel(MapArgs a) {
       const int q0 = qb * TQ;
       __syncthreads();
       stage_rm<D>(qimg, a.q + base, ld, q0, S, tid);
-      stage_tr<D>(qt, a.q + base, ld, q0, S, tid);
       stage_rm<D>(dimg, a.dO + base, ld, q0, S, tid);
-      stage_tr<D>(dt, a.dO + base, ld, q0, S, tid);
       if (tid < TQ) {
         const bool ok = q0 + tid < S;
         lse_s[tid] = ok ? a.lse[srow + q0 + tid] : 0.f;
@@ -365,8 +354,8 @@ __global__ __launch_bounds__(256) void attn_map_dkv_kernel(MapArgs a) {
         const bf16x8_t sb = frag_acc(dp[2 * c], dp[2 * c + 1]);
 #pragma unroll
         for (int i = 0; i < D / 16; ++i) {
-          dv[i] = mfma(frag_tp<64 + PADT>(dt, i * 16, c, lane), pb, dv[i]);
-          dk[i] = mfma(frag_tp<64 + PADT>(qt, i * 16, c, lane), sb, dk[i]);
+          dv[i] = mfma(frag_tr<D + PADR>(dimg, i * 16, c, lane), pb, dv[i]);
+          dk[i] = mfma(frag_tr<D + PADR>(qimg, i * 16, c, lane), sb, dk[i]);
         }
       }
     }

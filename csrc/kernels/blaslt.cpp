@@ -4,7 +4,7 @@
 // activation-backward, triangular token mixer) stay on the hand-written MFMA kernels in gemm.hip; the plain
 // products -- data gradients, weight gradients (bf16 x bf16 -> fp32 accumulated into the flat gradient buffer),
 // residual-add projections, logits -- are library GEMMs and go to hipBLASLt, whose gfx950 kernels sustain
-// 1.45-1.6 PFLOP/s on the model's shapes (tools/bench_gemm_k.py). hipBLASLt also reads every operand layout at
+// 1.45-1.6 PFLOP/s on the model's shapes (tools/lab/bench_gemm_k.py). hipBLASLt also reads every operand layout at
 // full rate, so the weight gradient needs no token-contiguous transposes and the forward needs no cached
 // transposed weight copies.
 //

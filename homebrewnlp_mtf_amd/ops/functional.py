@@ -47,7 +47,7 @@ def _acc_grad(w: torch.Tensor) -> typing.Tuple[torch.Tensor, bool]:
 def _acc_grad_beta(w: torch.Tensor) -> typing.Tuple[torch.Tensor, bool, float]:
     """like ``_acc_grad`` plus the GEMM beta: 0 (overwrite) for the first contribution of the step to a flat-buffer
     gradient, 1 (accumulate) after that. hipBLASLt's fp32 weight-gradient GEMM runs up to 13 % faster without the
-    C read-back (tools/bench_wgrad.py, profiles/r2_wgrad_layouts.txt)."""
+    C read-back (tools/lab/bench_wgrad.py, profiles/r2_wgrad_layouts.txt)."""
     mg = getattr(w, "main_grad", None)
     if mg is None:
         return torch.zeros(w.shape, dtype=torch.float32, device=w.device), False, 0.0
@@ -116,7 +116,7 @@ _KCONTIG = __import__("os").environ.get("OBST_TRANSPOSED_OPERANDS", "1") != "0"
 # 1444 TF/s with the weight K-contiguous against 1256 TF/s on the stored [K][N] layout (tools/gemm_census.py,
 # profiles/r2_gemm_census.md); refreshing every copy costs one transpose pass over the bf16 weights per step (~1 ms).
 # Decode-step products (M = 32 tokens) gain too: 6.1-12.4 us against 7.1-21.5 us per projection
-# (tools/bench_skinny.py, profiles/r2_skinny_gemm.txt).
+# (tools/lab/bench_skinny.py, profiles/r2_skinny_gemm.txt).
 _FWD_WT = __import__("os").environ.get("OBST_FWD_WT", "1") != "0"
 # OBST_ATTN_FUSED_RESIDUAL=0: the attention block's residual add as a separate elementwise pass (A/B)
 _ATTN_RES = __import__("os").environ.get("OBST_ATTN_FUSED_RESIDUAL", "1") == "1"
@@ -168,7 +168,7 @@ def _wgrad_gemm(x2, dy2, gw, plan: LinearPlan, xT=None, dyT=None, beta: float = 
     lt_big = (xT is None and dyT is None and raw.on_gpu(x2) and raw.lt_takes_f32() and H == 1 and M % 8 == 0
               and K % 8 == 0 and N % 8 == 0)
     if lt_big and N >= 2 * K and N >= 4096:
-        # hipBLASLt reads a token-contiguous x ~20 % faster than the token-strided one (tools/bench_wgrad.py); the
+        # hipBLASLt reads a token-contiguous x ~20 % faster than the token-strided one (tools/lab/bench_wgrad.py); the
         # saving grows with N while the transpose costs ~K: worth it for the d -> 2d projections
         xT = torch.empty(K * M, dtype=x2.dtype, device=x2.device)
         raw.transpose(x2, xT, M, K, K, M)
@@ -472,7 +472,7 @@ class _DotAttention(torch.autograd.Function):
                    else pstate._DONE)
         baseT = None
         if raw.on_gpu(base) and raw.lt_takes_f32() and T % 8 == 0 and K % 8 == 0:
-            # one transpose of base serves the three q/k/v weight gradients (tools/bench_wgrad.py: -118 us each
+            # one transpose of base serves the three q/k/v weight gradients (tools/lab/bench_wgrad.py: -118 us each
             # against the token-strided layout, for one 122 us transpose)
             baseT = torch.empty(K * T, dtype=base.dtype, device=base.device)
             raw.transpose(base, baseT, T, K, K, T)

@@ -241,7 +241,7 @@ def gemm(a: Operand, b: Operand, c: Operand, M: int, N: int, K: int, batch: typi
             and c.t.dtype == torch.bfloat16 and b1 * b2 == 1 and c.ld == N and (M * N) % 8 == 0
             and c.t.is_contiguous() and c.t.numel() == M * N and R.is_contiguous() and R.numel() == M * N):
         # residual input: hipBLASLt's out-of-place beta*C path runs 2-3x slower than the plain product on some
-        # layouts (tools/bench_gemm_k.py), so the plain product plus the elementwise add is faster
+        # layouts (tools/lab/bench_gemm_k.py), so the plain product plus the elementwise add is faster
         gemm(a, b, c, M, N, K, alpha=alpha)
         elementwise("add", c.t, c.t, z=R)
         return c.t
