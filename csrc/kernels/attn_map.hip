@@ -55,15 +55,31 @@ __device__ __forceinline__ uint4 ld16(const bf16_t* p, bool ok) {
   return ok ? *reinterpret_cast<const uint4*>(p) : make_uint4(0u, 0u, 0u, 0u);
 }
 
-// rows r0 .. r0+63 (token stride ld) of one head into a row-major image; rows past S are zero
+// register staging of one 64-row tile (D / 32 16-byte pieces per thread): the next tile's global loads are issued
+// before the current tile's MFMAs and written to LDS behind the next barrier, so their latency hides under compute
 template <int D>
-__device__ __forceinline__ void stage_rm(bf16_t* img, const bf16_t* g, long long ld, int r0, int S, int tid) {
+struct Rows {
+  uint4 v[D / 32];
+};
+template <int D>
+__device__ __forceinline__ void load_rows(Rows<D>& r, const bf16_t* g, long long ld, int r0, int S, int tid) {
   constexpr int CH = D / 8;
-  for (int c = tid; c < 64 * CH; c += 256) {
-    const int r = c / CH, cc = c - r * CH;
-    *reinterpret_cast<uint4*>(img + r * (D + PADR) + cc * 8) = ld16(g + (long long)(r0 + r) * ld + cc * 8, r0 + r < S);
+#pragma unroll
+  for (int i = 0; i < D / 32; ++i) {
+    const int c = tid + 256 * i, row = c / CH, cc = c - row * CH;
+    r.v[i] = ld16(g + (long long)(r0 + row) * ld + cc * 8, r0 + row < S);
   }
 }
+template <int D>
+__device__ __forceinline__ void store_rows(bf16_t* img, const Rows<D>& r, int tid) {
+  constexpr int CH = D / 8;
+#pragma unroll
+  for (int i = 0; i < D / 32; ++i) {
+    const int c = tid + 256 * i, row = c / CH, cc = c - row * CH;
+    *reinterpret_cast<uint4*>(img + row * (D + PADR) + cc * 8) = r.v[i];
+  }
+}
+
 // map values of keys key0 .. key0 + 3 on one query row (16-byte load when in range; zero past S)
 __device__ __forceinline__ f32x4_t map4(const float* row, int key0, int S) {
   if ((S & 3) == 0 && key0 + 3 < S) return *reinterpret_cast<const f32x4_t*>(row + key0);
@@ -123,12 +139,19 @@ __global__ __launch_bounds__(256) void attn_map_fwd_kernel(MapArgs a) {
   const long long mrow = ((long long)h * S + (qok ? myq : 0)) * S;
   float m = -INFINITY, l = 0.f;
   const int nkt = a.causal ? qb + 1 : (S + TK - 1) / TK;
+  Rows<D> nk, nv;
+  load_rows<D>(nk, a.k + base, ld, 0, S, tid);
+  load_rows<D>(nv, a.v + base, ld, 0, S, tid);
   for (int kt = 0; kt < nkt; ++kt) {
     const int k0 = kt * TK;
     __syncthreads();
-    stage_rm<D>(kimg, a.k + base, ld, k0, S, tid);
-    stage_rm<D>(vimg, a.v + base, ld, k0, S, tid);
+    store_rows<D>(kimg, nk, tid);
+    store_rows<D>(vimg, nv, tid);
     __syncthreads();
+    if (kt + 1 < nkt) {
+      load_rows<D>(nk, a.k + base, ld, k0 + TK, S, tid);
+      load_rows<D>(nv, a.v + base, ld, k0 + TK, S, tid);
+    }
     f32x4_t s[4];
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) {
@@ -226,12 +249,19 @@ __global__ __launch_bounds__(256) void attn_map_dq_kernel(MapArgs a) {
 #pragma unroll
   for (int i = 0; i < D / 16; ++i) acc[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   const int nkt = a.causal ? qb + 1 : (S + TK - 1) / TK;
+  Rows<D> nk, nv;
+  load_rows<D>(nk, a.k + base, ld, 0, S, tid);
+  load_rows<D>(nv, a.v + base, ld, 0, S, tid);
   for (int kti = 0; kti < nkt; ++kti) {
     const int k0 = kti * TK;
     __syncthreads();
-    stage_rm<D>(kimg, a.k + base, ld, k0, S, tid);
-    stage_rm<D>(vimg, a.v + base, ld, k0, S, tid);
+    store_rows<D>(kimg, nk, tid);
+    store_rows<D>(vimg, nv, tid);
     __syncthreads();
+    if (kti + 1 < nkt) {
+      load_rows<D>(nk, a.k + base, ld, k0 + TK, S, tid);
+      load_rows<D>(nv, a.v + base, ld, k0 + TK, S, tid);
+    }
     f32x4_t s[4], dp[4];
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) {
@@ -303,17 +333,45 @@ __global__ __launch_bounds__(256) void attn_map_dkv_kernel(MapArgs a) {
     f32x4_t dk[D / 16], dv[D / 16];
 #pragma unroll
     for (int i = 0; i < D / 16; ++i) dk[i] = dv[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    Rows<D> nq, nd;
+    float nl = 0.f, ndl = 0.f;
+    auto fetch = [&](int qbn) {
+      const int qn = qbn * TQ;
+      load_rows<D>(nq, a.q + base, ld, qn, S, tid);
+      load_rows<D>(nd, a.dO + base, ld, qn, S, tid);
+      if (tid < TQ) {
+        const bool ok = qn + tid < S;
+        nl = ok ? a.lse[srow + qn + tid] : 0.f;
+        ndl = ok ? a.delta[srow + qn + tid] : 0.f;
+      }
+    };
+    if (qb_first < nqb) fetch(qb_first);
     for (int qb = qb_first; qb < nqb; ++qb) {
       const int q0 = qb * TQ;
+      // this tile's map values and the running map-gradient sums, loaded before the staging and the score MFMAs so
+      // their latency hides under them (issued at their use, every read-modify-write paid a full memory round trip)
+      f32x4_t bv[4], cv[4], ob[4], oc[4];
+#pragma unroll
+      for (int qi = 0; qi < 4; ++qi)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int qq = q0 + qi * 16 + 4 * g + r;
+          const bool inb = kok && qq < S;
+          const long long mi = (long long)(inb ? qq : 0) * S + (kok ? myk : 0);
+          bv[qi][r] = a.bias != nullptr && inb ? a.bias[mbase + mi] : 0.f;
+          cv[qi][r] = a.cmap != nullptr && inb ? a.cmap[mbase + mi] : 1.f;
+          ob[qi][r] = a.dbias != nullptr && inb ? a.dbias[pbase + mi] : 0.f;
+          oc[qi][r] = a.dcmap != nullptr && inb ? a.dcmap[pbase + mi] : 0.f;
+        }
       __syncthreads();
-      stage_rm<D>(qimg, a.q + base, ld, q0, S, tid);
-      stage_rm<D>(dimg, a.dO + base, ld, q0, S, tid);
+      store_rows<D>(qimg, nq, tid);
+      store_rows<D>(dimg, nd, tid);
       if (tid < TQ) {
-        const bool ok = q0 + tid < S;
-        lse_s[tid] = ok ? a.lse[srow + q0 + tid] : 0.f;
-        dl_s[tid] = ok ? a.delta[srow + q0 + tid] : 0.f;
+        lse_s[tid] = nl;
+        dl_s[tid] = ndl;
       }
       __syncthreads();
+      if (qb + 1 < nqb) fetch(qb + 1);
       // S / dP tiles [queries][keys]: lane holds key myk, queries q0 + qi * 16 + 4 g + r
       f32x4_t s[4], dp[4];
 #pragma unroll
@@ -333,17 +391,12 @@ __global__ __launch_bounds__(256) void attn_map_dkv_kernel(MapArgs a) {
           const bool inb = kok && qq < S;
           const bool ok = inb && (!a.causal || myk <= qq);
           const long long mi = (long long)qq * S + myk;
-          float x = s[qi][r] * a.scale;
-          float c = 1.f;
-          if (ok) {
-            if (a.bias != nullptr) x += a.bias[mbase + mi];
-            if (a.cmap != nullptr) c = a.cmap[mbase + mi];
-          }
-          const float p = ok ? __expf(x - lse_s[ql]) : 0.f;
+          const float c = cv[qi][r];
+          const float p = ok ? __expf(s[qi][r] * a.scale + bv[qi][r] - lse_s[ql]) : 0.f;
           const float ds = p * (c * dp[qi][r] - dl_s[ql]);
           if (inb) {
-            if (a.dbias != nullptr) a.dbias[pbase + mi] += ds;
-            if (a.dcmap != nullptr) a.dcmap[pbase + mi] += p * dp[qi][r];
+            if (a.dbias != nullptr) a.dbias[pbase + mi] = ob[qi][r] + ds;
+            if (a.dcmap != nullptr) a.dcmap[pbase + mi] = oc[qi][r] + p * dp[qi][r];
           }
           s[qi][r] = p * c;
           dp[qi][r] = ds;
