@@ -274,6 +274,59 @@ __global__ __launch_bounds__(NTH) void moe_bwd_kernel(const bf16_t* __restrict__
 
 // ---------------------------------------------------------------------------------------------------------------
 // K16: y[o][i] = sum_h x[o][h][i]   (inner % 8 == 0, fp32 accumulation)
+// K12 axial positional embedding (reference embedding.py 'axial'): the [n_0 x ... x n_{k-1}, F] table is the
+// product of k factor tables [n_m][F] broadcast over the other axes, out[i_0 .. i_{k-1}][f] = prod_m T_m[i_m][f].
+struct AxialArgs {
+  const bf16_t* t[4];
+  float* g[4];   // backward: fp32 factor gradients
+  int n[4];
+  int k, F;
+};
+
+__global__ __launch_bounds__(NTH) void axial_fwd_kernel(AxialArgs a, bf16_t* __restrict__ out, long long total) {
+  const long long e = (long long)blockIdx.x * NTH + threadIdx.x;
+  if (e >= total) return;
+  const int f = (int)(e % a.F);
+  long long r = e / a.F;
+  float v = 1.f;
+  for (int m = a.k - 1; m >= 0; --m) {   // the last factor is the fastest-varying position axis
+    const int i = (int)(r % a.n[m]);
+    r /= a.n[m];
+    v *= bf2f(a.t[m][(long long)i * a.F + f]);
+  }
+  out[e] = f2bf(v);
+}
+
+// dT_m[i][f] = sum over the other axes (row-major order, fp32) of g[..i..][f] * prod_{m' != m} T_m'[i_m'][f]:
+// one thread per (i, f) of factor m -- a fixed summation order, no atomics
+__global__ __launch_bounds__(NTH) void axial_bwd_kernel(AxialArgs a, const bf16_t* __restrict__ gout, int m) {
+  const long long e = (long long)blockIdx.x * NTH + threadIdx.x;
+  if (e >= (long long)a.n[m] * a.F) return;
+  const int f = (int)(e % a.F), im = (int)(e / a.F);
+  long long others = 1;
+  for (int j = 0; j < a.k; ++j)
+    if (j != m) others *= a.n[j];
+  float acc = 0.f;
+  for (long long o = 0; o < others; ++o) {
+    long long r = o, pos = 0, stride = 1;
+    float prod = 1.f;
+    for (int j = a.k - 1; j >= 0; --j) {   // compose the flat position with index im on axis m
+      int i;
+      if (j == m) {
+        i = im;
+      } else {
+        i = (int)(r % a.n[j]);
+        r /= a.n[j];
+        prod *= bf2f(a.t[j][(long long)i * a.F + f]);
+      }
+      pos += (long long)i * stride;
+      stride *= a.n[j];
+    }
+    acc += bf2f(gout[pos * a.F + f]) * prod;
+  }
+  a.g[m][e] = acc;
+}
+
 __global__ __launch_bounds__(NTH) void sum_axis_kernel(const bf16_t* __restrict__ X, bf16_t* __restrict__ Y,
                                                        long long outer, int H, long long inner) {
   const long long iv = inner / 8, n = outer * iv;
@@ -802,5 +855,42 @@ OBST_API int obst_decode_attn(const void* Q, const void* Kn, const void* Vn, voi
   }
   hipLaunchKernelGGL(decode_attn_kernel, dim3(B * H), dim3(NTH), 0, st, (const bf16_t*)Q, (const bf16_t*)Kn,
                      (const bf16_t*)Vn, (bf16_t*)K, (bf16_t*)V, (bf16_t*)O, pos, S, H, D, scale);
+  return (int)hipGetLastError();
+}
+
+// K12: tables t[0..k-1] ([n_m][F] bf16, k <= 4) -> out [prod n_m][F] bf16
+OBST_API int obst_axial_fwd(const void* const* t, const int* n, int k, int F, void* out, hipStream_t st) {
+  if (k < 1 || k > 4 || F <= 0) return -1;
+  AxialArgs a{};
+  long long total = F;
+  for (int m = 0; m < k; ++m) {
+    if (n[m] <= 0) return -1;
+    a.t[m] = (const bf16_t*)t[m];
+    a.n[m] = n[m];
+    total *= n[m];
+  }
+  a.k = k;
+  a.F = F;
+  hipLaunchKernelGGL(axial_fwd_kernel, dim3((unsigned)((total + NTH - 1) / NTH)), dim3(NTH), 0, st, a, (bf16_t*)out,
+                     total);
+  return (int)hipGetLastError();
+}
+
+// gout [prod n_m][F] bf16 -> g[m] [n_m][F] fp32 for every factor
+OBST_API int obst_axial_bwd(const void* const* t, const int* n, int k, int F, const void* gout, float* const* g,
+                            hipStream_t st) {
+  if (k < 1 || k > 4 || F <= 0) return -1;
+  AxialArgs a{};
+  for (int m = 0; m < k; ++m) {
+    if (n[m] <= 0) return -1;
+    a.t[m] = (const bf16_t*)t[m];
+    a.g[m] = g[m];
+    a.n[m] = n[m];
+  }
+  a.k = k;
+  a.F = F;
+  for (int m = 0; m < k; ++m)
+    hipLaunchKernelGGL(axial_bwd_kernel, dim3((unsigned)(((long long)n[m] * F + NTH - 1) / NTH)), dim3(NTH), 0, st, a,
+                       (const bf16_t*)gout, m);
   return (int)hipGetLastError();
 }

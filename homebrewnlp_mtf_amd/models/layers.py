@@ -759,6 +759,10 @@ def _relative(args: BlockArgs, shape: typing.List[Dim]) -> torch.Tensor:
     return out
 
 
+# axial embeddings on the K12 kernel (False: the named-einsum product -- the CPU tests' reference)
+AXIAL_KERNEL = True
+
+
 def _embed(args: BlockArgs, shape: typing.List[Dim]) -> Act:
     p = args.params
     shape = list(shape)
@@ -782,6 +786,9 @@ def _embed(args: BlockArgs, shape: typing.List[Dim]) -> Act:
                 tdim = Dim(f'_{len(tmp_dims)}', sz)
                 tmp_dims.append(tdim)
                 variables.append(Act(_embed_var(args, [tdim] + list(feature_dims)), [tdim] + list(feature_dims)))
+        if AXIAL_KERNEL and len(variables) <= 4:   # K12: the broadcast product in one kernel (fp32 factor grads)
+            out_t = F.axial_embed([v.t for v in variables], int(math.prod(d.size for d in feature_dims)))
+            return Act(out_t.reshape([d.size for d in shape]), shape)
         out = named_einsum(variables, tmp_dims + list(feature_dims))
         return Act(out.t.reshape([d.size for d in shape]), shape)
     if 'relative' in args:

@@ -129,6 +129,8 @@ _SIGS = {
     "obst_moe_fwd": [c_p, c_p, c_p, c_p, c_ll, c_i, c_i, c_p],
     "obst_moe_bwd": [c_p, c_p, c_p, c_p, c_p, c_ll, c_i, c_i, c_p],
     "obst_sum_axis": [c_p, c_p, c_ll, c_i, c_ll, c_p],
+    "obst_axial_fwd": [c_p, c_p, c_i, c_i, c_p, c_p],
+    "obst_axial_bwd": [c_p, c_p, c_i, c_i, c_p, c_p, c_p],
     "obst_sample": [c_p, c_ll, c_i, c_i, c_p, c_p, c_p, c_p, c_i, c_p, ctypes.c_ulonglong, c_p, c_p],
     "obst_sample_parts": [c_ll, c_i],
     "obst_frames": [c_p, c_i, c_p, c_ll, c_i, c_i, c_i, c_p],

@@ -712,6 +712,32 @@ class _AttnMap(torch.autograd.Function):
                 None, None)
 
 
+class _Axial(torch.autograd.Function):
+    """K12 axial positional embedding: [n_0, .., n_{k-1}, F] = broadcast product of k factor tables [n_m, F]"""
+
+    @staticmethod
+    def forward(ctx, F_, *tables):
+        ts = [t.contiguous() for t in tables]
+        n = [t.numel() // F_ for t in ts]
+        out = torch.empty(math.prod(n) * F_, dtype=ts[0].dtype, device=ts[0].device)
+        raw.axial_fwd(ts, out, F_)
+        ctx.save_for_backward(*ts)
+        ctx.F = F_
+        return out.view(n + [F_])
+
+    @staticmethod
+    def backward(ctx, g):
+        ts = ctx.saved_tensors
+        md = torch.float64 if g.dtype == torch.float64 else torch.float32
+        grads = [torch.empty(t.numel(), dtype=md, device=g.device) for t in ts]
+        raw.axial_bwd(ts, g.contiguous(), grads, ctx.F)
+        return (None,) + tuple(gr.view(t.shape).to(t.dtype) for gr, t in zip(grads, ts))
+
+
+def axial_embed(tables, F: int):
+    return _Axial.apply(F, *tables)
+
+
 def attention_map(q, k, v, bias, cmap, scale: float, causal: bool):
     return _AttnMap.apply(q, k, v, bias, cmap, scale, causal)
 

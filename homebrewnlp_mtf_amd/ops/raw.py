@@ -1023,6 +1023,70 @@ def sum_axis(x, y, outer: int, H: int, inner: int):
     return None
 
 
+# ----------------------------------------------------------------------------------------------------------------
+# K12 axial positional embedding: out[i_0, .., i_{k-1}, f] = prod_m t_m[i_m, f]  (k <= 4 factor tables [n_m, F])
+def axial_fwd(tables, out, F: int):
+    if out.device.type == "meta":
+        return None
+    if on_gpu(out):
+        if not 1 <= len(tables) <= 4:
+            raise L.KernelError("axial embedding: 1-4 factor tables")
+        for t in tables:
+            _bf16_contig("axial table", t)
+        _bf16_contig("axial out", out)
+        n = [t.numel() // F for t in tables]
+        _need(out, math.prod(n) * F - 1, "out")
+        ptrs = (ctypes.c_void_p * 4)(*([t.data_ptr() for t in tables] + [0] * (4 - len(tables))))
+        ns = (ctypes.c_int * 4)(*(n + [1] * (4 - len(n))))
+        L.check(L.lib().obst_axial_fwd(ptrs, ns, len(tables), F, out.data_ptr(), L.stream_ptr()), "axial_fwd")
+        return None
+    acc = None
+    k = len(tables)
+    for m, t in enumerate(tables):
+        shape = [1] * k + [F]
+        shape[m] = t.numel() // F
+        v = _f(t).reshape(shape)
+        acc = v if acc is None else acc * v
+    out.view(acc.shape).copy_(acc)
+    return None
+
+
+def axial_bwd(tables, gout, grads, F: int):
+    """grads[m] [n_m, F] fp32 <- sum over the other axes of gout * prod of the other tables"""
+    if gout.device.type == "meta":
+        return None
+    if on_gpu(gout):
+        for t in tables:
+            _bf16_contig("axial table", t)
+        _bf16_contig("axial grad", gout)
+        n = [t.numel() // F for t in tables]
+        for g, nm in zip(grads, n):
+            if g.dtype != torch.float32 or not g.is_contiguous():
+                raise L.KernelError("axial factor gradients must be contiguous fp32")
+            _need(g, nm * F - 1, "grad")
+        ptrs = (ctypes.c_void_p * 4)(*([t.data_ptr() for t in tables] + [0] * (4 - len(tables))))
+        gp = (ctypes.c_void_p * 4)(*([g.data_ptr() for g in grads] + [0] * (4 - len(grads))))
+        ns = (ctypes.c_int * 4)(*(n + [1] * (4 - len(n))))
+        L.check(L.lib().obst_axial_bwd(ptrs, ns, len(tables), F, gout.data_ptr(), gp, L.stream_ptr()), "axial_bwd")
+        return None
+    k = len(tables)
+    n = [t.numel() // F for t in tables]
+    go = _f(gout).reshape(n + [F])
+    vs = []
+    for m, t in enumerate(tables):
+        shape = [1] * k + [F]
+        shape[m] = n[m]
+        vs.append(_f(t).reshape(shape))
+    for m in range(k):
+        prod = go
+        for j in range(k):
+            if j != m:
+                prod = prod * vs[j]
+        axes = [j for j in range(k) if j != m]
+        grads[m].copy_((prod.sum(axes) if axes else prod).reshape(grads[m].shape))
+    return None
+
+
 def gumbel_scores(logits, temp, seed: int):
     """torch oracle of the sampling kernel's noisy scores: logit - T log(-log u), u = (hash24(r V + v) + 0.5) / 2^24"""
     rows, V = logits.shape

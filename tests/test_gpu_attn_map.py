@@ -106,7 +106,8 @@ GPT = dict(model_mode="gpt", use_video=False, use_language=True, heads=4, featur
 @pytest.mark.parametrize("layer", [
     "attention-biased_softmax-dot_product-context-absolute",
     "attention-biased_softmax-scale_attention_map-biased_attention_map-dot_product-context-absolute",
-    "attention-dot_product-positional-absolute-shared_key_value"])
+    "attention-dot_product-positional-absolute-shared_key_value",
+    "attention-dot_product-embedded-axial"])
 def test_map_variants_model_gpu_matches_cpu(cuda, layer):
     """the softmax-map attention variants train on the GPU through attn_map / token mixer / flash kernels: loss and
     gradients against the CPU fp32 model"""

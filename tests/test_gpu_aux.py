@@ -267,3 +267,29 @@ def test_mixer_incremental_sampling_gpu(cuda):
     b = full.sample(x, [5, 40], 0.0, [90, 128])
     agree = (a == b).float().mean().item()
     assert agree > 0.95, agree
+
+
+@pytest.mark.parametrize("ns", [(32, 64), (16, 8, 16), (2048,)])
+def test_axial_embedding_kernel(cuda, ns):
+    """K12: the broadcast product of the factor tables and the factor gradients against the fp32 oracle"""
+    from homebrewnlp_mtf_amd.ops import raw as R
+    torch.manual_seed(len(ns))
+    F = 256
+    tables = [(torch.randn(n * F) * 0.8 + 0.2).to(torch.bfloat16) for n in ns]
+    total = 1
+    for n in ns:
+        total *= n
+    g = torch.randn(total * F).to(torch.bfloat16)
+    out_c = torch.empty(total * F, dtype=torch.bfloat16)
+    R.axial_fwd(tables, out_c, F)
+    grads_c = [torch.empty(n * F) for n in ns]
+    R.axial_bwd(tables, g, grads_c, F)
+    tg = [t.to(cuda) for t in tables]
+    out_g = torch.empty(total * F, dtype=torch.bfloat16, device=cuda)
+    R.axial_fwd(tg, out_g, F)
+    grads_g = [torch.empty(n * F, device=cuda) for n in ns]
+    R.axial_bwd(tg, g.to(cuda), grads_g, F)
+    torch.cuda.synchronize()
+    assert torch.allclose(out_g.cpu().float(), out_c.float(), atol=1e-2, rtol=1e-2)
+    for a, b in zip(grads_g, grads_c):
+        assert torch.allclose(a.cpu(), b, atol=1e-2 * (total / len(b) * F) ** 0.5, rtol=1e-3)

@@ -512,3 +512,28 @@ def test_norm_any_layout_matches_torch_path(layers, monkeypatch):
         res[fast] = (float(out["loss"].detach()), st.grad.clone())
     assert abs(res[True][0] - res[False][0]) < 1e-5
     assert torch.allclose(res[True][1], res[False][1], atol=1e-5, rtol=1e-4)
+
+
+@pytest.mark.parametrize("layer", ["attention-dot_product-embedded-axial", "attention-dot_product-embedded-axial-3"])
+def test_axial_kernel_matches_einsum(layer, monkeypatch):
+    """K12: the axial factor-product op (raw.axial_fwd / axial_bwd oracle) == the named-einsum product, fp64"""
+    from homebrewnlp_mtf_amd.models import layers as LY
+    res = {}
+    for fast in (True, False):
+        monkeypatch.setattr(LY, "AXIAL_KERNEL", fast)
+        torch.manual_seed(0)
+        m = Model(ModelParameter(dict(BASE, calculation_dtype="float64", sequence_length=16,
+                                      block_config=[{"layer": [layer], "skip": True}])), "cpu")
+        st = m.store
+        st.master = st.master.double()
+        st.grad = st.grad.double()
+        st.compute = st.master
+        st._leaves = {}
+        st.master.copy_(torch.randn_like(st.master) * 0.3)
+        x = torch.randint(0, 50, (2, 16, 1), generator=torch.Generator().manual_seed(5))
+        out = m(x, x)
+        out["loss"].backward()
+        st.fold_leaf_grads()
+        res[fast] = (float(out["loss"].detach()), st.grad.clone())
+    assert abs(res[True][0] - res[False][0]) < 1e-10
+    assert torch.allclose(res[True][1], res[False][1], atol=1e-10, rtol=1e-8)
