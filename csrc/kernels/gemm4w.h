@@ -111,6 +111,11 @@ __device__ __forceinline__ void pad_redefine(f32x4_t (&acc)[8][8]) {
     asm volatile("" : "+a"(acc[i][0]), "+a"(acc[i][1]), "+a"(acc[i][2]), "+a"(acc[i][3]), "+a"(acc[i][4]),
                  "+a"(acc[i][5]), "+a"(acc[i][6]), "+a"(acc[i][7]));
 }
+__device__ __forceinline__ void pad_redefine(f32x4_t (&acc)[8][4]) {
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" : "+a"(acc[0][0]), "+a"(acc[0][1]), "+a"(acc[0][2]), "+a"(acc[0][3]));
+#pragma unroll
+  for (int i = 1; i < 8; ++i) asm volatile("" : "+a"(acc[i][0]), "+a"(acc[i][1]), "+a"(acc[i][2]), "+a"(acc[i][3]));
+}
 
 // compile-time loop: f(std::integral_constant<int, 0>) ... f(<N-1>) -- the K-loop body is 128 MFMA slots, past
 // what #pragma unroll expands, and every register array must stay statically indexed
@@ -132,11 +137,11 @@ __device__ __forceinline__ int bswz(int r) { return ((r >> 1) & 1) | (((r >> 3) 
 // operand -- the same for every tile (edges are handled by the resource's num_records). T = 0: [rows][K] operand,
 // piece P = 8 rows of 128 B (BI: the B image's swizzle); T = 1: [K][rows] operand, piece P = 4 k-rows x 128 columns
 // of half P >> 4.
-template <int T, bool BI = false>
-__device__ __forceinline__ void piece_offsets(int (&vo)[8], long long ld, int wave, int lane) {
+template <int T, bool BI = false, int PPW = 8>
+__device__ __forceinline__ void piece_offsets(int (&vo)[PPW], long long ld, int wave, int lane) {
 #pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    const int P = wave * 8 + q;
+  for (int q = 0; q < PPW; ++q) {
+    const int P = wave * PPW + q;
     if (T == 0) {
       const int row = P * 8 + (lane >> 3);
       const int c = (lane & 7) ^ (BI ? bswz(row) : ((row >> 1) & 7));
@@ -231,11 +236,24 @@ __device__ __forceinline__ Tile4 decode4(const GemmArgs& p, long long L) {
 // ACROSS tile boundaries (positions of a flat (tile, K-tile) sequence), so the next tile's first two K-tiles are
 // in LDS when the current tile's epilogue is done, and its first fragments are read under the current tile's
 // last MFMAs. XCD x owns a contiguous run of logical tiles, dealt to its CUs in rounds.
-template <int A_T, int B_T, bool OUT_F32, bool PROF>
-__global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs p) {
+// NWV = 8 (G8W): two waves per SIMD, each owning 128 x 64 of C (8 x 4 accumulators, 128 AGPRs), 4 LDS-DMA pieces
+// per operand and K-tile per wave and a 64-slot MFMA stream -- a wave's DMA issue cost (~60 cycles per piece, one
+// wave per SIMD: nothing covers it) is hidden by its SIMD partner's MFMAs.
+template <int A_T, int B_T, bool OUT_F32, bool PROF, int NWV = 4>
+__global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
   extern __shared__ __attribute__((aligned(1024))) char smem[];
+  constexpr int WN = NWV == 4 ? 128 : 64;    // output columns per wave
+  constexpr int JB = WN / 16;                // B fragments per substep
+  constexpr int PPW = 32 / NWV;              // LDS-DMA pieces per operand, K-tile and wave
+  constexpr int QS = 16 * JB;                // MFMA slots per K-tile
+  constexpr int NR = 8 + JB;                 // fragment reads per substep
+  constexpr int QB1 = NWV == 4 ? 25 : 14;    // barrier 1
+  constexpr int QA0 = NWV == 4 ? 26 : 15, QB0 = NWV == 4 ? 66 : 31, DQ = NWV == 4 ? 5 : 4;   // DMA slots
+  constexpr int QW = NWV == 4 ? 107 : 50;    // barrier 2
+  constexpr int STW = 8 * (JB / 2);          // direct-epilogue stores per wave (bf16; fp32: twice)
+  constexpr int FW_BF = 2 * PPW + STW, FW_F32 = 2 * PPW + 2 * STW > 63 ? 63 : 2 * PPW + 2 * STW;
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = NWV == 4 ? wave >> 1 : wave & 1, wn = NWV == 4 ? wave & 1 : wave >> 1;
 
   const long long total = (long long)p.tiles_m * p.tiles_n * p.nbatch;
   const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3, nslot = gridDim.x >> 3;
@@ -249,13 +267,13 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs p) {
   const long long astep = A_T == 0 ? 128 : 128 * p.lda;
   const long long bstep = B_T == 0 ? 128 : 128 * p.ldb;
 
-  int voa[8], vob[8];
-  piece_offsets<A_T>(voa, p.lda, wave, lane);
-  piece_offsets<B_T, true>(vob, p.ldb, wave, lane);
+  int voa[PPW], vob[PPW];
+  piece_offsets<A_T, false, PPW>(voa, p.lda, wave, lane);
+  piece_offsets<B_T, true, PPW>(vob, p.ldb, wave, lane);
   const unsigned lds0 = lds_u32(smem);
-  // this wave's 8 pieces of an operand image are contiguous: 8 KiB at (wave * 8 KiB)
-  auto stage_a = [&](int s) -> unsigned { return lds0 + s * Q_STAGE + wave * 8192; };
-  auto stage_b = [&](int s) -> unsigned { return lds0 + s * Q_STAGE + Q_OP + wave * 8192; };
+  // this wave's PPW pieces of an operand image are contiguous: PPW KiB at (wave * PPW KiB)
+  auto stage_a = [&](int s) -> unsigned { return lds0 + s * Q_STAGE + wave * PPW * 1024; };
+  auto stage_b = [&](int s) -> unsigned { return lds0 + s * Q_STAGE + Q_OP + wave * PPW * 1024; };
 
   // DMA cursor: (tile round, K-tile) of the next position to stage; past the last tile it re-stages the last
   // position into the stage nobody reads any more
@@ -276,18 +294,18 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs p) {
     }
   };
 
-  f32x4_t acc[8][8];
-  bf16x8_t a0[8], b0[8], a1[8], b1f[8];
+  f32x4_t acc[8][JB];
+  bf16x8_t a0[8], b0[JB], a1[8], b1f[JB];
 
   // read order of a substep's 16 fragments: A0, B0, A1..A7, B1..B7 (the order the MFMA stream consumes them)
-  auto read_sub = [&](int s, auto kkc, auto rc, bf16x8_t (&af)[8], bf16x8_t (&bf)[8]) {
+  auto read_sub = [&](int s, auto kkc, auto rc, bf16x8_t (&af)[8], bf16x8_t (&bf)[JB]) {
     constexpr int kk = decltype(kkc)::value, r = decltype(rc)::value;
     const char* ia = smem + s * Q_STAGE;
     const char* ib = smem + s * Q_STAGE + Q_OP;
     if constexpr (r == 0) af[0] = frag<A_T>(ia, wm * 128, kk, lane);
-    else if constexpr (r == 1) bf[0] = frag_b<B_T>(ib, wn * 128, 0, kk, lane);
+    else if constexpr (r == 1) bf[0] = frag_b<B_T>(ib, wn * WN, 0, kk, lane);
     else if constexpr (r < 9) af[r - 1] = frag<A_T>(ia, wm * 128 + (r - 1) * 16, kk, lane);
-    else bf[r - 8] = frag_b<B_T>(ib, wn * 128, r - 8, kk, lane);
+    else bf[r - 8] = frag_b<B_T>(ib, wn * WN, r - 8, kk, lane);
   };
   using K0 = std::integral_constant<int, 0>;
   using K1 = std::integral_constant<int, 1>;
@@ -307,26 +325,26 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs p) {
   // prologue: positions 0 and 1 into stages 0 and 1, wait for position 0, read its substep-0 fragments
   dma_setup();
 #pragma unroll
-  for (int q = 0; q < 8; ++q) dma16(ra, voa[q], stage_a(0) + q * 1024);
+  for (int q = 0; q < PPW; ++q) dma16(ra, voa[q], stage_a(0) + q * 1024);
 #pragma unroll
-  for (int q = 0; q < 8; ++q) dma16(rb, vob[q], stage_b(0) + q * 1024);
+  for (int q = 0; q < PPW; ++q) dma16(rb, vob[q], stage_b(0) + q * 1024);
   dma_advance();
   dma_setup();
 #pragma unroll
-  for (int q = 0; q < 8; ++q) dma16(ra, voa[q], stage_a(1) + q * 1024);
+  for (int q = 0; q < PPW; ++q) dma16(ra, voa[q], stage_a(1) + q * 1024);
 #pragma unroll
-  for (int q = 0; q < 8; ++q) dma16(rb, vob[q], stage_b(1) + q * 1024);
+  for (int q = 0; q < PPW; ++q) dma16(rb, vob[q], stage_b(1) + q * 1024);
   dma_advance();
-  vm_wait<16>();
+  vm_wait<2 * PPW>();
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_s_waitcnt(0xc07f);   // nothing (kernel-argument loads) pending in lgkmcnt at the loop entry
   if (stamp) p.stamps[sbase + 1] = __builtin_amdgcn_s_memtime();
   fence();
-  static_for<16>([&](auto rc) { read_sub(0, K0{}, rc, a0, b0); fence(); });   // same order as in the loop
+  static_for<NR>([&](auto rc) { read_sub(0, K0{}, rc, a0, b0); fence(); });   // same order as in the loop
 
   int pos = 0;   // flat position of the K-tile being multiplied (its stage is pos & 1)
   // vmcnt of the first K-tile of a tile (see q == 107): 16 + the previous epilogue's stores, at most 63
-  const int first_wait = (p.act == 0 && p.mode == 0 && p.Zout == nullptr) ? (OUT_F32 ? 63 : 48) : 16;
+  const int first_wait = (p.act == 0 && p.mode == 0 && p.Zout == nullptr) ? (OUT_F32 ? FW_F32 : FW_BF) : 2 * PPW;
   for (int rnd = 0; rnd < ntiles; ++rnd) {
     const Tile4 ct = decode4<A_T, B_T>(p, logical(rnd));
     // Accumulator zeroing (VALU writes of AGPRs) -> first MFMA reading them needs wait states the compiler cannot
@@ -334,43 +352,43 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs p) {
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    static_for<64>([&](auto c) { agpr_opaque(acc[decltype(c)::value >> 3][decltype(c)::value & 7]); });
+      for (int j = 0; j < JB; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    static_for<8 * JB>([&](auto c) { agpr_opaque(acc[decltype(c)::value / JB][decltype(c)::value % JB]); });
     asm volatile("s_nop 4" ::: "memory");
     fence();
     if (stamp) tmark = __builtin_amdgcn_s_memtime();
 
     for (int t = 0; t < nk; ++t, ++pos) {
       const int s = pos & 1;
-      static_for<128>([&](auto qc) {
+      static_for<QS>([&](auto qc) {
         constexpr int q = decltype(qc)::value;
-        constexpr int sub = q >> 6, j = (q >> 3) & 7, i = q & 7;
+        constexpr int sub = q / (8 * JB), j = (q % (8 * JB)) / 8, i = q & 7;
         if constexpr (sub == 0) mfma_acc(acc[i][j], b0[j], a0[i]);
         else mfma_acc(acc[i][j], b1f[j], a1[i]);
-        if constexpr (q < 16 && !(G4W_EXP & 2)) read_sub(s, K1{}, qc, a1, b1f);   // substep-1 fragments of pos
-        if constexpr (q == 16) dma_setup();                                 // resources of position pos + 2
-        if constexpr (q == 25) {                                            // stage s fully read by every wave
+        if constexpr (q < NR && !(G4W_EXP & 2)) read_sub(s, K1{}, qc, a1, b1f);   // substep-1 fragments of pos
+        if constexpr (q == NR) dma_setup();                                 // resources of position pos + 2
+        if constexpr (q == QB1) {                                           // stage s fully read by every wave
           if constexpr (PROF) tw = __builtin_amdgcn_s_memtime();
           __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0) as a builtin: the compiler's wait model learns the
           if constexpr (!(G4W_EXP & 4)) __builtin_amdgcn_s_barrier();   // substep-1 reads are done
           if constexpr (PROF) sync1 += __builtin_amdgcn_s_memtime() - tw;
         }
-        if constexpr (!(G4W_EXP & 1) && q >= 26 && q < 64 && (q - 26) % 5 == 0)
-          dma16(ra, voa[(q - 26) / 5], stage_a(s) + (q - 26) / 5 * 1024);
-        if constexpr (!(G4W_EXP & 1) && q >= 66 && q < 106 && (q - 66) % 5 == 0)
-          dma16(rb, vob[(q - 66) / 5], stage_b(s) + (q - 66) / 5 * 1024);
-        if constexpr (q == 107) {                                           // position pos+1 landed in stage s^1
+        if constexpr (!(G4W_EXP & 1) && q >= QA0 && q < QA0 + DQ * PPW && (q - QA0) % DQ == 0)
+          dma16(ra, voa[(q - QA0) / DQ], stage_a(s) + (q - QA0) / DQ * 1024);
+        if constexpr (!(G4W_EXP & 1) && q >= QB0 && q < QB0 + DQ * PPW && (q - QB0) % DQ == 0)
+          dma16(rb, vob[(q - QB0) / DQ], stage_b(s) + (q - QB0) / DQ * 1024);
+        if constexpr (q == QW) {                                            // position pos+1 landed in stage s^1
           // first K-tile of a tile: the previous tile's epilogue stores sit between that position's DMAs and this
           // iteration's; count them out instead of waiting for every store (direct epilogue: 32 bf16 / 64 fp32)
           if constexpr (PROF) tw = __builtin_amdgcn_s_memtime();
-          if (t == 0 && rnd > 0 && first_wait == 48) vm_wait<48>();
-          else if (t == 0 && rnd > 0 && first_wait == 63) vm_wait<63>();
-          else vm_wait<16>();
+          if (t == 0 && rnd > 0 && first_wait == FW_BF) vm_wait<FW_BF>();
+          else if (t == 0 && rnd > 0 && first_wait == FW_F32) vm_wait<FW_F32>();
+          else vm_wait<2 * PPW>();
           if constexpr (!(G4W_EXP & 4)) __builtin_amdgcn_s_barrier();
           if constexpr (PROF) sync2 += __builtin_amdgcn_s_memtime() - tw;
         }
-        if constexpr (q >= 108 && q < 124 && !(G4W_EXP & 2))                // substep-0 fragments of position pos+1
-          read_sub(s ^ 1, K0{}, std::integral_constant<int, q - 108>{}, a0, b0);
+        if constexpr (q > QW && q <= QW + NR && !(G4W_EXP & 2))             // substep-0 fragments of position pos+1
+          read_sub(s ^ 1, K0{}, std::integral_constant<int, q - QW - 1>{}, a0, b0);
         fence();
       });
       dma_advance();
@@ -407,12 +425,12 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs p) {
       const __amdgpu_buffer_rsrc_t rr = make_brsrc(p.R ? reinterpret_cast<const char*>(p.R) + ct.coff * ES + corg : cbase, cext);
       const int ml = lane & 15, gq = lane >> 4;
       const float alpha = p.alpha, beta = ws_out ? 0.f : p.beta;
-      const bool edge = ct.n0 + 256 > p.N;
+      const bool edge = ct.n0 + wn * WN + WN > p.N;
       const bool extra = (OUT_F32 && beta != 0.f) || (p.R != nullptr && !ws_out);
       // fragment pair (2p, 2p+1) = 8 consecutive columns per lane (frag_b): 16 B (bf16) / 2 x 16 B (fp32) stores,
       // 32 / 64 per wave (64 bf16 stores with the 32 LDS-DMAs in flight overflowed the 63-entry vmcnt)
-      const int voff = (int)(((long long)(wm * 128 + ml) * ldc + wn * 128 + 8 * gq) * ES);
-      const int nbase = ct.n0 + wn * 128 + 8 * gq;
+      const int voff = (int)(((long long)(wm * 128 + ml) * ldc + wn * WN + 8 * gq) * ES);
+      const int nbase = ct.n0 + wn * WN + 8 * gq;
       // Zout / Zin share C's leading dimension and batch offset (bf16)
       const i32x4_t rz4 = make_rsrc(p.Zout ? reinterpret_cast<const char*>(p.Zout) + ct.coff * 2 + corg : cbase, cext);
       const __amdgpu_buffer_rsrc_t rzi =
@@ -429,7 +447,7 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs p) {
           const int soff = __builtin_amdgcn_readfirstlane((int)(i * 16 * ldc * ES));
           f32x4_t x[8];
           if constexpr (AC == 2) {
-            static_for<4>([&](auto pc) {
+            static_for<JB / 2>([&](auto pc) {
               constexpr int pp = decltype(pc)::value;
               const v4u32_t o = __builtin_amdgcn_raw_buffer_load_b128(rzi, voff, soff + pp * 64, 0);
               x[2 * pp] = f32x4_t{bf2f(o[0] & 0xffff), bf2f(o[0] >> 16), bf2f(o[1] & 0xffff), bf2f(o[1] >> 16)};
@@ -437,7 +455,7 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs p) {
             });
           }
           if constexpr (EX) {
-            static_for<4>([&](auto pc) {
+            static_for<JB / 2>([&](auto pc) {
               constexpr int pp = decltype(pc)::value;
               if constexpr (OUT_F32) {
                 x[2 * pp] = x[2 * pp + 1] = f32x4_t{0.f, 0.f, 0.f, 0.f};
@@ -456,7 +474,7 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs p) {
               }
             });
           }
-          static_for<4>([&](auto pc) {
+          static_for<JB / 2>([&](auto pc) {
             constexpr int pp = decltype(pc)::value;
             if (ED && nbase + pp * 32 >= p.N) return;
             f32x4_t va = alpha * acc[i][2 * pp], vb = alpha * acc[i][2 * pp + 1];
@@ -528,23 +546,24 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs p) {
       // loop reads 8 consecutive outputs per lane and applies epilogue_store8r (one activation switch per round)
       // with 16-byte global accesses; a fully unrolled per-fragment epilogue inlined the activation switch 64
       // times (~12k branches), instruction-cache bound and as long as the K loop at K = 2048.
-      float* ep = reinterpret_cast<float*>(smem + 2 * Q_STAGE) + wave * 2048;
+      float* ep = reinterpret_cast<float*>(smem + 2 * Q_STAGE) + wave * 16 * WN;
       const float alpha = p.alpha;
+      constexpr int LPR = WN / 8;   // lanes per 16-row x WN round row (8 outputs each)
       static_for<8>([&](auto rcc) {
         constexpr int r = decltype(rcc)::value;
-        static_for<8>([&](auto jc) {
+        static_for<JB>([&](auto jc) {
           constexpr int j = decltype(jc)::value;
           const int row = lane & 15, c4 = 8 * (j >> 1) + 2 * (lane >> 4) + (j & 1);   // frag_b column order
-          *reinterpret_cast<float4*>(ep + row * 128 + ((c4 ^ (row & 7)) << 2)) =
+          *reinterpret_cast<float4*>(ep + row * WN + ((c4 ^ (row & 7)) << 2)) =
               make_float4(alpha * acc[r][j][0], alpha * acc[r][j][1], alpha * acc[r][j][2], alpha * acc[r][j][3]);
         });
 #pragma unroll 1
-        for (int it = 0; it < 4; ++it) {
-          const int row = it * 4 + (lane >> 4), c4 = (lane & 15) * 2;
-          const float4 x0 = *reinterpret_cast<const float4*>(ep + row * 128 + ((c4 ^ (row & 7)) << 2));
-          const float4 x1 = *reinterpret_cast<const float4*>(ep + row * 128 + (((c4 + 1) ^ (row & 7)) << 2));
+        for (int it = 0; it < 16 * LPR / 64; ++it) {
+          const int row = it * (64 / LPR) + lane / LPR, c4 = (lane % LPR) * 2;
+          const float4 x0 = *reinterpret_cast<const float4*>(ep + row * WN + ((c4 ^ (row & 7)) << 2));
+          const float4 x1 = *reinterpret_cast<const float4*>(ep + row * WN + (((c4 + 1) ^ (row & 7)) << 2));
           float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-          const int m = ct.m0 + wm * 128 + r * 16 + row, n = ct.n0 + wn * 128 + c4 * 4;
+          const int m = ct.m0 + wm * 128 + r * 16 + row, n = ct.n0 + wn * WN + c4 * 4;
           if (m < p.M && n < p.N) epilogue_store8r<OUT_F32>(p, ct.coff + (long long)m * p.ldc + n, v);
         }
         fence();
@@ -572,7 +591,7 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs p) {
   }
 }
 
-template <int A_T, int B_T, bool F32>
+template <int A_T, int B_T, bool F32, int NWV = 4>
 hipError_t launch4w(GemmArgs a, int batch, hipStream_t stream) {
   a.tiles_m = (a.M + 255) / 256;
   a.tiles_n = (a.N + 255) / 256;
@@ -580,20 +599,22 @@ hipError_t launch4w(GemmArgs a, int batch, hipStream_t stream) {
   const long long tiles = (long long)a.tiles_m * a.tiles_n * a.nbatch;
   // one block per CU (32 per XCD); fewer for small launches, keeping a multiple of the 8 XCDs
   const int grid = (int)(tiles >= 256 ? 256 : ((tiles + 7) / 8) * 8);
-  const size_t lds = 2 * Q_STAGE + 4 * 8192;   // 160 KiB: two stages + the epilogue regions
-  auto k = a.stamps ? gemm4w_kernel<A_T, B_T, F32, true> : gemm4w_kernel<A_T, B_T, F32, false>;
+  const size_t lds = 2 * Q_STAGE + 32768;   // 160 KiB: two stages + the epilogue regions (16 rows x 128 fp32 per SIMD)
+  auto k = a.stamps ? gemm4w_kernel<A_T, B_T, F32, true, NWV> : gemm4w_kernel<A_T, B_T, F32, false, NWV>;
   static bool attr[2] = {false, false};
   if (!attr[a.stamps != nullptr]) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr[a.stamps != nullptr] = true;
   }
-  hipLaunchKernelGGL(k, dim3(grid), dim3(256), lds, stream, a);
+  hipLaunchKernelGGL(k, dim3(grid), dim3(64 * NWV), lds, stream, a);
   return hipGetLastError();
 }
 
 }  // namespace
 
 // one operand-layout pair per translation unit (gemm4w_<a_t><b_t>.hip) so the instantiations compile in parallel
+// (NWV = 8 builds and runs correctly but at 597 TF/s on 131072x4096x2048: with 128 AGPRs per wave the 96 fragment
+// VGPRs leave too few registers and the K loop spills -- profiles/r3_gemm4w_bounds.md; only NWV = 4 is instantiated)
 #define OBST_GEMM4W_TU(AT, BT)                                                                                      \
   hipError_t gemm4w_launch_##AT##BT(const gemmk::GemmArgs* a, int out_f32, int batch, hipStream_t stream) {      \
     return out_f32 ? launch4w<AT, BT, true>(*a, batch, stream) : launch4w<AT, BT, false>(*a, batch, stream);    \
