@@ -824,6 +824,13 @@ __device__ __forceinline__ bf16x8_t tr_pair(const char* lds, int o0, int o1) {
   return __builtin_bit_cast(bf16x8_t, v);
 }
 
+#ifndef FWD_KPF
+#define FWD_KPF 2
+#endif
+#ifndef FWD_KPF_FENCE
+#define FWD_KPF_FENCE 1
+#endif
+
 // one 64-key tile for a wave's 32 queries (query n = lane&31 is `q`); l is this lane's partial row sum
 template <bool MASK, int NKT = 2>
 __device__ __forceinline__ void fwd32_tile(const char* sK, const char* sV, const bf16x8_t (&qf)[8],
@@ -834,14 +841,28 @@ __device__ __forceinline__ void fwd32_tile(const char* sK, const char* sV, const
   frag32_offsets(fo, lane);
   f32x16_t s[NKT];
   if (prio) __builtin_amdgcn_s_setprio(1);
+  // the NKT score chains interleaved k-step by k-step, K fragments read FWD_KPF k-steps ahead of their MFMA: with
+  // one chain at a time the compiler re-used one fragment register and every MFMA waited out a full LDS read
+  constexpr int PF = FWD_KPF;
+  bf16x8_t kf[PF + 1][NKT];
 #pragma unroll
-  for (int kt = 0; kt < NKT; ++kt) {
-    s[kt] = f32x16_t{};
+  for (int kt = 0; kt < NKT; ++kt) s[kt] = f32x16_t{};
 #pragma unroll
-    for (int ks = 0; ks < 8; ++ks) {
-      const bf16x8_t kf = *reinterpret_cast<const bf16x8_t*>(sK + fo.k[ks] + kt * 32 * 256);
-      s[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], s[kt], 0, 0, 0);
-    }
+  for (int ks = 0; ks < PF; ++ks)
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt)
+      kf[ks][kt] = *reinterpret_cast<const bf16x8_t*>(sK + fo.k[ks] + kt * 32 * 256);
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks) {
+    if (ks + PF < 8)
+#pragma unroll
+      for (int kt = 0; kt < NKT; ++kt)
+        kf[(ks + PF) % (PF + 1)][kt] = *reinterpret_cast<const bf16x8_t*>(sK + fo.k[ks + PF] + kt * 32 * 256);
+    // fence: the scheduler would otherwise sink each read next to its MFMA (one fragment register, no prefetch)
+    if (FWD_KPF_FENCE) __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt)
+      s[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[ks % (PF + 1)][kt], qf[ks], s[kt], 0, 0, 0);
   }
   if (prio) __builtin_amdgcn_s_setprio(0);
   float mx = -INFINITY;
@@ -1121,6 +1142,93 @@ __device__ __forceinline__ void dkv32_update(const char* sQ, const char* sD, con
   }
 }
 
+// One 64-query chunk of the 32x32 dK/dV kernel as four MFMA phases of 16 MFMAs each, software-pipelined inside the
+// wave (the kernel runs one wave per SIMD: there is no partner wave to hide LDS latency or the softmax VALU):
+//   A: S/dP of sub-chunk 0          B: S/dP of sub-chunk 1  + softmax of sub-chunk 0 (2 elements per k-step)
+//   C: dV/dK update of sub-chunk 0  + softmax of sub-chunk 1        D: dV/dK update of sub-chunk 1
+// Every LDS fragment is read DKV32_PF steps ahead of its MFMA along the flat step sequence, and a sched_barrier per
+// step keeps the compiler from sinking the reads next to their use (the straight-line version waited out a full LDS
+// read in front of 45 of its 64 MFMAs).
+#ifndef DKV32_PF
+#define DKV32_PF 2
+#endif
+__device__ __forceinline__ void dkv32_softmax_pair(f32x16_t& s, f32x16_t& dp, const float (&nl)[16], int r0, int tc,
+                                                   int tq, float c2) {
+#pragma unroll
+  for (int r = r0; r < r0 + 2; ++r) {
+    const int j = 8 * (r >> 2) + (r & 3);
+    float p = fexp2(__builtin_fmaf(s[r], c2, nl[r]));
+    p = (j < tc || j >= tq) ? 0.f : p;
+    s[r] = p;
+    dp[r] = p * dp[r];
+  }
+}
+
+__device__ __forceinline__ void dkv32_chunk_pipe(const char* sQ, const char* sD, const float* sL, const float* sDl,
+                                                 const Frag32& fo, const bf16x8_t (&kf)[8], const bf16x8_t (&vf)[8],
+                                                 f32x16_t (&dk)[4], f32x16_t (&dv)[4], int tc0, int tq0, float c2,
+                                                 int lane) {
+  constexpr int PF = DKV32_PF, NB = PF + 1;
+  const int h = lane >> 5;
+  f32x16_t s[2], dp[2];
+  float nl[2][16];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    s[u] = f32x16_t{};
+#pragma unroll
+    for (int a4 = 0; a4 < 4; ++a4) {
+      const float4 dl = *reinterpret_cast<const float4*>(sDl + u * 32 + 8 * a4 + 4 * h);
+      const float4 lv = *reinterpret_cast<const float4*>(sL + u * 32 + 8 * a4 + 4 * h);
+      dp[u][4 * a4 + 0] = -dl.x; dp[u][4 * a4 + 1] = -dl.y; dp[u][4 * a4 + 2] = -dl.z; dp[u][4 * a4 + 3] = -dl.w;
+      nl[u][4 * a4 + 0] = -lv.x * LOG2E; nl[u][4 * a4 + 1] = -lv.y * LOG2E;
+      nl[u][4 * a4 + 2] = -lv.z * LOG2E; nl[u][4 * a4 + 3] = -lv.w * LOG2E;
+    }
+  }
+  const int tc[2] = {tc0, tc0 - 32}, tq[2] = {tq0, tq0 - 32};
+  // phases A + B: 16 score steps t = 8u + ks
+  bf16x8_t qa[NB], da[NB];
+  auto ld_sc = [&](int t) {
+    const int o = fo.k[t & 7] + (t >> 3) * 32 * 256;
+    qa[t % NB] = *reinterpret_cast<const bf16x8_t*>(sQ + o);
+    da[t % NB] = *reinterpret_cast<const bf16x8_t*>(sD + o);
+  };
+#pragma unroll
+  for (int t = 0; t < PF; ++t) ld_sc(t);
+#pragma unroll
+  for (int t = 0; t < 16; ++t) {
+    if (t + PF < 16) ld_sc(t + PF);
+    __builtin_amdgcn_sched_barrier(0);
+    const int u = t >> 3, ks = t & 7;
+    s[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa[t % NB], kf[ks], s[u], 0, 0, 0);
+    dp[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da[t % NB], vf[ks], dp[u], 0, 0, 0);
+    if (u == 1) dkv32_softmax_pair(s[0], dp[0], nl[0], 2 * ks, tc[0], tq[0], c2);
+  }
+  // phases C + D: 16 update steps t = 8u + 4st + dt; the transposed Vᵀ-side operands: dOᵀ (for dV) and Qᵀ (for dK)
+  bf16x8_t ot[NB], qt[NB];
+  auto ld_up = [&](int t) {
+    const int u = t >> 3, st = (t >> 2) & 1, dt = t & 3;
+    const int kb = u * 32 * 256 + 16 * st * 256;
+    ot[t % NB] = tr_pair(sD, fo.v[dt][0] + kb, fo.v[dt][1] + kb);
+    qt[t % NB] = tr_pair(sQ, fo.v[dt][0] + kb, fo.v[dt][1] + kb);
+  };
+#pragma unroll
+  for (int t = 0; t < PF; ++t) ld_up(t);
+  bf16x8_t pb = pack8(s[0], 0), sb = pack8(dp[0], 0);
+#pragma unroll
+  for (int t = 0; t < 16; ++t) {
+    const int u = t >> 3, st = (t >> 2) & 1, dt = t & 3;
+    if (t + PF < 16) ld_up(t + PF);
+    if (dt == 0 && t > 0) {
+      pb = pack8(s[u], 8 * st);
+      sb = pack8(dp[u], 8 * st);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    dv[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ot[t % NB], pb, dv[dt], 0, 0, 0);
+    dk[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qt[t % NB], sb, dk[dt], 0, 0, 0);
+    if (u == 0) dkv32_softmax_pair(s[1], dp[1], nl[1], 2 * t, tc[1], tq[1], c2);
+  }
+}
+
 __global__ __launch_bounds__(NTH, 1) void attn_bwd_dkv32_kernel(AttnArgs a) {
   constexpr int D = 128;
   constexpr int QC = 64;
@@ -1191,7 +1299,10 @@ __global__ __launch_bounds__(NTH, 1) void attn_bwd_dkv32_kernel(AttnArgs a) {
     const float* sL = reinterpret_cast<const float*>(sQ + 2 * TILE);
     const float* sDl = sL + 64;
     if (c + 1 < nqc) stage(smem + ((c + 1) & 1) * STAGE, q0 + QC);
-    {   // both sub-chunks straight-line: the score MFMAs of sub-chunk 1 overlap the softmax VALU of sub-chunk 0
+    if (DKV32_PF > 0) {
+      const int rel = q0 + 4 * h;
+      dkv32_chunk_pipe(sQ, sD, sL, sDl, fo, kf, vf, dk, dv, a.causal ? key - rel : -1000000, a.S - rel, c2, lane);
+    } else {   // both sub-chunks straight-line: the score MFMAs of sub-chunk 1 overlap the softmax VALU of sub-chunk 0
       f32x16_t s0, dp0, s1, dp1;
       dkv32_scores(sQ, sD, sDl, fo, kf, vf, s0, dp0, 0, lane);
       dkv32_scores(sQ, sD, sDl, fo, kf, vf, s1, dp1, 1, lane);
