@@ -1249,24 +1249,25 @@ __global__ __launch_bounds__(NTH, 1) void attn_bwd_dkv32_kernel(AttnArgs a) {
   const long long base = (long long)b * a.S * a.ld + hd * D;
   const long long sbase = ((long long)b * a.H + hd) * a.S;
   const bf16_t* Qb = a.Q + base;
-  const bf16_t* Db = a.dO + base;
+  const bf16_t* Db = a.dO + (long long)b * a.S * a.ld_o + hd * D;   // dO rows at their own stride (ld_o)
   const int qstart = a.causal ? (kblk / QC) * QC : 0;
   const int nqc = (a.S - qstart + QC - 1) / QC;
   const int wu = __builtin_amdgcn_readfirstlane(w);
-  unsigned soff[4];
+  unsigned soff[4], soffo[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int row = (wu + 4 * i) * 4 + (lane >> 4);
     soff[i] = (unsigned)(row * (int)a.ld + (((lane & 15) ^ swz<128>(row)) << 3)) * 2u;
+    soffo[i] = (unsigned)(row * (int)a.ld_o + (((lane & 15) ^ swz<128>(row)) << 3)) * 2u;
   }
   auto stage = [&](char* buf, int q0) {
     q0 = __builtin_amdgcn_readfirstlane(q0);
     if (q0 + QC <= a.S) {
       stage_full64(buf, Qb + (long long)q0 * a.ld, soff, wu);
-      stage_full64(buf + TILE, Db + (long long)q0 * a.ld, soff, wu);
+      stage_full64(buf + TILE, Db + (long long)q0 * a.ld_o, soffo, wu);
     } else {
       stage_rows64_asm<4>(buf, Qb + (long long)q0 * a.ld, a.ld, a.S - q0, wu, lane);
-      stage_rows64_asm<4>(buf + TILE, Db + (long long)q0 * a.ld, a.ld, a.S - q0, wu, lane);
+      stage_rows64_asm<4>(buf + TILE, Db + (long long)q0 * a.ld_o, a.ld_o, a.S - q0, wu, lane);
     }
     if (wu < 2) {   // wave 0: lse, wave 1: delta (64 x 4 B, lane-linear)
       const float* src = (wu == 0 ? a.LSE : a.delta) + sbase;
@@ -1340,7 +1341,10 @@ static int attn_impl() {   // OBST_ATTN_IMPL=1 forces the 16x16x32 kernels (A/B 
 
 // OBST_ATTN_BWD=2 selects the 32x32x16 dK/dV kernel; 3 (4 / 5: dQ / dK-dV only) the 8-wave blocks with 3-deep LDS
 // rings. A/B only: at B64 S2048 H16 D128 causal the default pair takes 5.23 ms, 3 / 4 / 5 take 5.86 / 5.68 / 5.61 ms
-// (the longer blocks lose more to the causal-diagonal imbalance than the deeper ring gains; r2 bench_attn_ab)
+// (the longer blocks lose more to the causal-diagonal imbalance than the deeper ring gains; r2 bench_attn_ab).
+// Round 3: the 32x32 dK/dV kernel software-pipelined (dkv32_chunk_pipe) and with dO at its own stride, so it also
+// runs on the step's interleaved k|q|v layout: 3.71 ms against 3.01 ms for the default 16x16 kernel at that shape
+// (rocprofv3, profiles/r3_attn_bwd_ab.md) -- one wave per SIMD, ~8k clocks per 64-query chunk for 2k of MFMA
 // OBST_ATTN_DKV_KG=2: two 16-key groups per dK/dV wave (half the LDS bytes per MFMA, ~490 registers: one wave per
 // SIMD). A/B only: B64 S2048 H16 D128 causal backward 5.24 -> 6.27 ms (3-deep ring: 6.33) -- without the partner
 // wave the softmax VALU and the LDS waits no longer hide under another wave's MFMAs (r2 tools/lab/gpu_attn_kg.sh)
@@ -1425,7 +1429,7 @@ int launch_bwd(const AttnArgs& a, hipStream_t st) {
   else
     hipLaunchKernelGGL(attn_bwd_dq_kernel<D>, dim3((a.S + 127) / 128 * a.B * a.H), dim3(NTH), 4 * 64 * Geo<D>::ROWB,
                        st, a);
-  if (D == 128 && attn_bwd_impl() == 2 && a.ld == a.ld_o)   // its Q / dO staging shares one row-offset table
+  if (D == 128 && attn_bwd_impl() == 2)
     hipLaunchKernelGGL(attn_bwd_dkv32_kernel, dim3((a.S + 127) / 128 * a.B * a.H), dim3(NTH), 2 * (2 * 64 * 256 + 512),
                        st, a);
   else if (attn_dkv_ring() == 4)   // 32-query chunks in a 4-deep ring (the same 66 KiB of LDS)

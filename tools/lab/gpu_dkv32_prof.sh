@@ -1,7 +1,10 @@
-# per-kernel times of the attention backward: default dK/dV kernel vs the pipelined 32x32 one (OBST_ATTN_BWD=2)
+# dK/dV A/B: the pipelined 32x32 kernel (OBST_ATTN_BWD=2) against the default 16x16 kernel -- attention tests on the
+# 32x32 path, then per-kernel times (rocprofv3 kernel trace of tools/kbench.py attn; read the .db with sqlite3)
 set -e
-cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
+OBST_ATTN_BWD=2 timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py -k "attn or attention" -x -q --timeout 120 --timeout-method thread > gpurun_out/dkv32_tests.log 2>&1
+tail -2 gpurun_out/dkv32_tests.log
+export TMPDIR=/tmp
 timeout -k 10 180 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_bwd1 -o run -- python3 tools/kbench.py attn > gpurun_out/prof_bwd1.log 2>&1
 OBST_ATTN_BWD=2 timeout -k 10 180 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_bwd2 -o run -- python3 tools/kbench.py attn > gpurun_out/prof_bwd2.log 2>&1
-for v in 1 2; do f=$(find gpurun_out/prof_bwd$v -name '*kernel_stats.csv' | head -1); echo "== bwd$v"; grep -i attn "$f" | cut -d, -f1-5; done
+grep pflops gpurun_out/prof_bwd1.log gpurun_out/prof_bwd2.log
