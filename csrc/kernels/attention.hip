@@ -377,6 +377,13 @@ __global__ __launch_bounds__(NTH) void attn_delta_kernel(AttnArgs a) {
   if (lane == 0) a.delta[((long long)b * a.H + h) * a.S + q] = acc;
 }
 
+#ifndef DKV_UPF
+#define DKV_UPF 0
+#endif
+#ifndef DKV_PF
+#define DKV_PF 2   // score-loop fragment prefetch distance of dq_tile / dkv_chunk (0: the plain loops)
+#endif
+
 // one 64-key tile of the dQ kernel for a wave's 32 queries (two 32-key halves: P needs only the stored LSE, so no
 // state crosses the halves). dP starts from -delta (the accumulator init), so dS = P * dP.
 template <int D, bool MASK, int HALVES = 2>
@@ -397,6 +404,28 @@ __device__ __forceinline__ void dq_tile(const char* sK, const char* sV, const bf
         dp[qt][kk] = f32x4_t{-dlt[qt], -dlt[qt], -dlt[qt], -dlt[qt]};
       }
     if (prio) __builtin_amdgcn_s_setprio(1);
+    if constexpr (DKV_PF > 0 && HALVES == 1) {   // fenced prefetch as in dkv_chunk, steps t = ds * 2 + kk (the
+      // two-half 64-key tile variants spill with it)
+      constexpr int NB = DKV_PF + 1, NT = G::DS * 2;
+      bf16x8_t kf[NB], vf[NB];
+      auto ld = [&](int t) {
+        kf[t % NB] = row_frag<D>(sK, (2 * st + (t & 1)) * 16, t >> 1, lane);
+        vf[t % NB] = row_frag<D>(sV, (2 * st + (t & 1)) * 16, t >> 1, lane);
+      };
+#pragma unroll
+      for (int t = 0; t < DKV_PF; ++t) ld(t);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        if (t + DKV_PF < NT) ld(t + DKV_PF);
+        __builtin_amdgcn_sched_barrier(0);
+        const int ds = t >> 1, kk = t & 1;
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt) {
+          sc[qt][kk] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[t % NB], qf[qt][ds], sc[qt][kk], 0, 0, 0);
+          dp[qt][kk] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[t % NB], df[qt][ds], dp[qt][kk], 0, 0, 0);
+        }
+      }
+    } else {
 #pragma unroll
     for (int ds = 0; ds < G::DS; ++ds) {
 #pragma unroll
@@ -410,6 +439,7 @@ __device__ __forceinline__ void dq_tile(const char* sK, const char* sV, const bf
           dp[qt][kk] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, df[qt][ds], dp[qt][kk], 0, 0, 0);
         }
       }
+    }
     }
     if (prio) __builtin_amdgcn_s_setprio(0);
     bf16x8_t sf[2];
@@ -431,12 +461,27 @@ __device__ __forceinline__ void dq_tile(const char* sK, const char* sV, const bf
       sf[qt] = pack_p(sc[qt][0], sc[qt][1]);
     }
     if (prio) __builtin_amdgcn_s_setprio(1);
+    if constexpr (DKV_PF > 0 && HALVES == 1) {
+      constexpr int NB = DKV_PF + 1;
+      bf16x8_t kt[NB];
+#pragma unroll
+      for (int dt = 0; dt < DKV_PF; ++dt) kt[dt % NB] = tr_frag<D>(sK, st * 32, dt * 16, lane);
+#pragma unroll
+      for (int dt = 0; dt < G::DT; ++dt) {
+        if (dt + DKV_PF < G::DT) kt[(dt + DKV_PF) % NB] = tr_frag<D>(sK, st * 32, (dt + DKV_PF) * 16, lane);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt)
+          acc[dt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kt[dt % NB], sf[qt], acc[dt][qt], 0, 0, 0);
+      }
+    } else {
 #pragma unroll
     for (int dt = 0; dt < G::DT; ++dt) {
       bf16x8_t kf = tr_frag<D>(sK, st * 32, dt * 16, lane);
 #pragma unroll
       for (int qt = 0; qt < 2; ++qt)
         acc[dt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, sf[qt], acc[dt][qt], 0, 0, 0);
+    }
     }
     if (prio) __builtin_amdgcn_s_setprio(0);
   }
@@ -584,6 +629,29 @@ __device__ __forceinline__ void dkv_chunk(const char* sQ, const char* sD, const 
     }
   }
   if (prio) __builtin_amdgcn_s_setprio(1);
+  if constexpr (DKV_PF > 0) {
+    // flat step sequence t = ds * NQT + qt, Q / dO fragments read SPF steps ahead behind scheduling fences
+    constexpr int SPF = DKV_UPF > 0 && DKV_PF > 1 ? 1 : DKV_PF;   // both at 2 spill at 256 VGPRs
+    constexpr int NB = SPF + 1, NT = G::DS * NQT;
+    bf16x8_t qa[NB], da[NB];
+    auto ld = [&](int t) {
+      qa[t % NB] = row_frag<D>(sQ, (t % NQT) * 16, t / NQT, lane);
+      da[t % NB] = row_frag<D>(sD, (t % NQT) * 16, t / NQT, lane);
+    };
+#pragma unroll
+    for (int t = 0; t < SPF; ++t) ld(t);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      if (t + SPF < NT) ld(t + SPF);
+      __builtin_amdgcn_sched_barrier(0);
+      const int ds = t / NQT, qt = t % NQT;
+#pragma unroll
+      for (int j = 0; j < KG; ++j) {
+        sc[j][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa[t % NB], kf[j][ds], sc[j][qt], 0, 0, 0);
+        dp[j][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da[t % NB], vf[j][ds], dp[j][qt], 0, 0, 0);
+      }
+    }
+  } else {
 #pragma unroll
   for (int ds = 0; ds < G::DS; ++ds) {
 #pragma unroll
@@ -596,6 +664,7 @@ __device__ __forceinline__ void dkv_chunk(const char* sQ, const char* sD, const 
         dp[j][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, vf[j][ds], dp[j][qt], 0, 0, 0);
       }
     }
+  }
   }
   if (prio) __builtin_amdgcn_s_setprio(0);
   // sc[j][qt][v] = S[q = q0 + qt*16 + 4g + v][key + 16 j]
@@ -617,6 +686,38 @@ __device__ __forceinline__ void dkv_chunk(const char* sQ, const char* sD, const 
       }
   }
   if (prio) __builtin_amdgcn_s_setprio(1);
+  if constexpr (DKV_UPF > 0) {   // update steps t = st * DT + dt, transposed operands UPF steps ahead
+    // off by default: at 256 VGPRs (two waves per SIMD) it spills one address whose reload's vmcnt(0) then waits
+    // for the next chunk's LDS-DMA in the middle of every chunk
+    constexpr int UPF = DKV_UPF;
+    constexpr int NB = UPF + 1, NT = NQT / 2 * G::DT;
+    bf16x8_t dot[NB], qtr[NB], pb[KG], sb[KG];
+    auto ld = [&](int t) {
+      dot[t % NB] = tr_frag<D>(sD, (t / G::DT) * 32, (t % G::DT) * 16, lane);
+      qtr[t % NB] = tr_frag<D>(sQ, (t / G::DT) * 32, (t % G::DT) * 16, lane);
+    };
+#pragma unroll
+    for (int t = 0; t < UPF; ++t) ld(t);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int st = t / G::DT, dt = t % G::DT;
+      if (t + UPF < NT) ld(t + UPF);
+      if (dt == 0)
+#pragma unroll
+        for (int j = 0; j < KG; ++j) {
+          pb[j] = pack_p(sc[j][2 * st], sc[j][2 * st + 1]);
+          sb[j] = pack_p(dp[j][2 * st], dp[j][2 * st + 1]);
+        }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < KG; ++j) {
+        dv[j][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dot[t % NB], pb[j], dv[j][dt], 0, 0, 0);
+        dk[j][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qtr[t % NB], sb[j], dk[j][dt], 0, 0, 0);
+      }
+    }
+    if (prio) __builtin_amdgcn_s_setprio(0);
+    return;
+  }
 #pragma unroll
   for (int st = 0; st < NQT / 2; ++st) {
     bf16x8_t pb[KG], sb[KG];
