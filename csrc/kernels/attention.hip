@@ -1569,7 +1569,7 @@ static bool fill(AttnArgs& a, const ObstAttnDesc* d) {
   a.ld_o = d->ld_o ? d->ld_o : d->ld;
   a.Res = (const bf16_t*)d->Res; a.Sum = (bf16_t*)d->Sum;
   if ((a.Res == nullptr) != (a.Sum == nullptr)) return false;
-  static const int prio = [] { const char* e = getenv("OBST_ATTN_PRIO"); return e ? atoi(e) : 1; }();
+  static const int prio = [] { const char* e = getenv("OBST_ATTN_PRIO"); return e ? atoi(e) : 3; }();
   a.prio = prio;
   return d->B > 0 && d->S > 0 && d->H > 0 && d->ld % 8 == 0 && d->ld >= (long long)d->H * d->D &&
          a.ld_o % 8 == 0 && a.ld_o >= (long long)d->H * d->D;
