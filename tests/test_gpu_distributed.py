@@ -108,3 +108,21 @@ def test_gpu_tp_matches_single_rank(cuda, mode):
             got = torch.cat([p.view(shp) for p in parts], tp_dim)
         diff = (got - full).abs().max().item()
         assert diff < 1e-3, f"TP weight {name} differs from the single-rank GPU model by {diff}"
+
+
+def test_rccl_collectives_world1():
+    """RCCL itself on the box: a one-rank ``nccl`` process group (RCCL refuses two ranks on one device) brought up
+    with ``device_id`` as bench.py does, every collective of tools/comm_probe.py run on cuda:0 through it"""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, OBST_DIST_BACKEND="nccl", PYTHONPATH=root, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "1", "--master-addr",
+                        "127.0.0.1", "--master-port", str(_free_port()), os.path.join(root, "tools", "comm_probe.py"),
+                        "--sizes-mb", "1,16", "--iters", "2", "--warmup", "1"],
+                       capture_output=True, text=True, env=env, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    rows = [json.loads(line) for line in r.stdout.splitlines() if line.startswith("{")]
+    assert {x["op"] for x in rows} == {"all_reduce", "reduce_scatter", "all_gather", "all_to_all"}
+    assert len(rows) == 8 and all(x["backend"] == "nccl" and x["world"] == 1 and x["us"] > 0 for x in rows)
