@@ -126,3 +126,23 @@ def test_rccl_collectives_world1():
     rows = [json.loads(line) for line in r.stdout.splitlines() if line.startswith("{")]
     assert {x["op"] for x in rows} == {"all_reduce", "reduce_scatter", "all_gather", "all_to_all"}
     assert len(rows) == 8 and all(x["backend"] == "nccl" and x["world"] == 1 and x["us"] > 0 for x in rows)
+
+
+def test_bench_two_rank_rehearsal():
+    """bench.py's N > 1 path as the driver launches it (torch.distributed.run, one process per rank, MAX over ranks,
+    rank 0 prints one JSON line), rehearsed with two gloo ranks sharing cuda:0 at a reduced depth / batch"""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, OBST_DIST_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "2", "--master-addr",
+                        "127.0.0.1", "--master-port", str(_free_port()), os.path.join(root, "bench.py"),
+                        "--gpus", "2", "--steps", "2", "--warmup", "1", "--batch-per-gpu", "2", "--depth", "2"],
+                       capture_output=True, text=True, env=env, timeout=280, cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rows = [json.loads(line) for line in r.stdout.splitlines() if line.startswith("{")]
+    assert len(rows) == 1, r.stdout[-2000:]
+    row = rows[0]
+    assert row["n_gpus"] == 2 and row["steps"] == 2 and row["value"] > 0 and row["ms_per_step"] > 0
+    assert row["config"]["parallelism"] == "dp2" and row["config"]["global_batch"] == 4
