@@ -33,6 +33,9 @@ def on_gpu(t: torch.Tensor) -> bool:
 
 _LT = None
 _RSPLIT = __import__("os").environ.get("OBST_LT_RSPLIT", "0") == "1"   # A/B knob: measured 1 % slower
+# OBST_ACT_G4W=1 (A/B): activation GEMMs on gemm4w with the activation fused into the epilogue while the plain
+# products stay on hipBLASLt (OBST_LT_SCOPE=0 moves the fp32 weight gradients too)
+_ACT_G4W = __import__("os").environ.get("OBST_ACT_G4W", "0") == "1"
 
 
 def lt_enabled() -> int:
@@ -226,6 +229,7 @@ def gemm(a: Operand, b: Operand, c: Operand, M: int, N: int, K: int, batch: typi
                                          L.ptr(ws), L.stream_ptr()), "skinny_gemm")
         return c.t
     if (not kin and on_gpu(c.t) and act is not None and tri == 0 and lt_enabled() == 1 and lt_scope() > 0
+            and not _ACT_G4W
             and c.t.dtype == torch.bfloat16
             and b1 * b2 == 1 and c.ld == N and (M * N) % 8 == 0 and c.t.is_contiguous() and c.t.numel() == M * N):
         # activation GEMM on hipBLASLt: plain product, then the elementwise kernel (pre-activation kept in Zout)
