@@ -377,6 +377,13 @@ __global__ __launch_bounds__(NTH) void attn_delta_kernel(AttnArgs a) {
   if (lane == 0) a.delta[((long long)b * a.H + h) * a.S + q] = acc;
 }
 
+// dK/dV read-ahead: score loop (DKV_SPF) and update loop (DKV_UPF). Both on exceed the 256 VGPRs of two waves per
+// SIMD (a spilled LDS address whose reload's vmcnt(0) waits for the next chunk's DMA). DKV_SPF=0 DKV_UPF=1 cuts the
+// MFMAs behind lgkmcnt(0) from 21 to 10 of 128 and measured the same (3120 / 3088 vs 3086 / 3119 us,
+// profiles/r3_attn_bwd_ab.md): the partner wave hides that latency; the kernel is bound elsewhere
+#ifndef DKV_SPF
+#define DKV_SPF 2
+#endif
 #ifndef DKV_UPF
 #define DKV_UPF 0
 #endif
@@ -629,9 +636,9 @@ __device__ __forceinline__ void dkv_chunk(const char* sQ, const char* sD, const 
     }
   }
   if (prio) __builtin_amdgcn_s_setprio(1);
-  if constexpr (DKV_PF > 0) {
+  if constexpr (DKV_SPF > 0) {
     // flat step sequence t = ds * NQT + qt, Q / dO fragments read SPF steps ahead behind scheduling fences
-    constexpr int SPF = DKV_UPF > 0 && DKV_PF > 1 ? 1 : DKV_PF;   // both at 2 spill at 256 VGPRs
+    constexpr int SPF = DKV_SPF;
     constexpr int NB = SPF + 1, NT = G::DS * NQT;
     bf16x8_t qa[NB], da[NB];
     auto ld = [&](int t) {
@@ -687,8 +694,6 @@ __device__ __forceinline__ void dkv_chunk(const char* sQ, const char* sD, const 
   }
   if (prio) __builtin_amdgcn_s_setprio(1);
   if constexpr (DKV_UPF > 0) {   // update steps t = st * DT + dt, transposed operands UPF steps ahead
-    // off by default: at 256 VGPRs (two waves per SIMD) it spills one address whose reload's vmcnt(0) then waits
-    // for the next chunk's LDS-DMA in the middle of every chunk
     constexpr int UPF = DKV_UPF;
     constexpr int NB = UPF + 1, NT = NQT / 2 * G::DT;
     bf16x8_t dot[NB], qtr[NB], pb[KG], sb[KG];
