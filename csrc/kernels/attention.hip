@@ -86,6 +86,29 @@ __device__ __forceinline__ void stage_rows(char* lds, const bf16_t* g, long long
   }
 }
 
+// Full-tile form of stage_rows for D = 128, 64 rows, 4 waves: piece j = wave + 4i covers rows 4j .. 4j + 3, so a
+// lane's source offset inside the tile depends only on its lane and on j & 1 (the swizzle (row & 7) << 1 of row
+// 4j + (lane >> 4)). The two 32-bit lane offsets are computed once per kernel (lane_off16_128); per piece the address
+// is a wave-uniform base + 4j rows (scalar) + that offset, instead of stage_rows' per-chunk 64-bit row arithmetic
+// (~150 VALU per chunk per wave in the dK/dV kernel, whose loop is VALU-issue bound).
+__device__ __forceinline__ void lane_off16_128(unsigned (&off)[2], long long ld, int lane) {
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const int row = 4 * e + (lane >> 4);   // row & 7 of piece j with j & 1 == e
+    off[e] = (unsigned)((lane >> 4) * (int)ld + (((lane & 15) ^ swz16<128>(row)) << 3)) * 2u;
+  }
+}
+
+__device__ __forceinline__ void stage_full16_128(char* lds, const bf16_t* g, long long ld, const unsigned (&off)[2],
+                                                 int wave) {
+  const char* gb = reinterpret_cast<const char*>(g);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int j = wave + 4 * i;
+    glds16_asm(gb + (long long)(4 * j) * ld * 2 + off[j & 1], lds + j * 1024);
+  }
+}
+
 // 4-byte values (lse / delta rows) for `n` <= 64 consecutive queries: one 256-B piece from wave 0
 __device__ __forceinline__ void stage_f32(char* lds, const float* g, int n, int nvalid, int tid) {
   if (tid >= 0 && tid < 64) {   // one wave, all lanes (n <= 64: lanes past n re-read the last value)
@@ -381,6 +404,9 @@ __global__ __launch_bounds__(NTH) void attn_delta_kernel(AttnArgs a) {
 // SIMD (a spilled LDS address whose reload's vmcnt(0) waits for the next chunk's DMA). DKV_SPF=0 DKV_UPF=1 cuts the
 // MFMAs behind lgkmcnt(0) from 21 to 10 of 128 and measured the same (3120 / 3088 vs 3086 / 3119 us,
 // profiles/r3_attn_bwd_ab.md): the partner wave hides that latency; the kernel is bound elsewhere
+#ifndef DKV_FAST_STAGE
+#define DKV_FAST_STAGE 1   // dK/dV full-tile staging from precomputed lane offsets
+#endif
 #ifndef DKV_SPF
 #define DKV_SPF 2
 #endif
@@ -770,9 +796,22 @@ __global__ __launch_bounds__(NW * 64, KG == 1 ? 2 : 1) void attn_bwd_dkv_kernel(
   const int qstart = a.causal ? (kblk / QC) * QC : 0;
   const int nqc = (a.S - qstart + QC - 1) / QC;
 
+  constexpr bool FAST = D == 128 && QC == 64 && NW == 4 && DKV_FAST_STAGE;
+  unsigned offq[2] = {0u, 0u}, offo[2] = {0u, 0u};
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  if (FAST) {
+    lane_off16_128(offq, a.ld, lane);
+    lane_off16_128(offo, a.ld_o, lane);
+  }
   auto stage = [&](char* st, int q0) {
-    stage_rows<D, QC, NW>(st, a.Q + base + (long long)q0 * a.ld, a.ld, a.S - q0, tid);
-    stage_rows<D, QC, NW>(st + TILE, a.dO + base_o + (long long)q0 * a.ld_o, a.ld_o, a.S - q0, tid);
+    q0 = __builtin_amdgcn_readfirstlane(q0);
+    if (FAST && q0 + QC <= a.S) {
+      stage_full16_128(st, a.Q + base + (long long)q0 * a.ld, a.ld, offq, wu);
+      stage_full16_128(st + TILE, a.dO + base_o + (long long)q0 * a.ld_o, a.ld_o, offo, wu);
+    } else {
+      stage_rows<D, QC, NW>(st, a.Q + base + (long long)q0 * a.ld, a.ld, a.S - q0, tid);
+      stage_rows<D, QC, NW>(st + TILE, a.dO + base_o + (long long)q0 * a.ld_o, a.ld_o, a.S - q0, tid);
+    }
     if (NW == 4) {   // wave 0 stages both
       stage_f32(st + 2 * TILE, a.LSE + sbase + q0, QC, a.S - q0, tid);
       stage_f32(st + 2 * TILE + 256, a.delta + sbase + q0, QC, a.S - q0, tid);
