@@ -99,11 +99,12 @@ __device__ __forceinline__ void lane_off16_128(unsigned (&off)[2], long long ld,
   }
 }
 
+template <int ROWS = 64>   // 64- or 32-row tile: ROWS / 16 pieces per wave
 __device__ __forceinline__ void stage_full16_128(char* lds, const bf16_t* g, long long ld, const unsigned (&off)[2],
                                                  int wave) {
   const char* gb = reinterpret_cast<const char*>(g);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < ROWS / 16; ++i) {
     const int j = wave + 4 * i;
     glds16_asm(gb + (long long)(4 * j) * ld * 2 + off[j & 1], lds + j * 1024);
   }
@@ -543,14 +544,24 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_bwd_dq_kernel(AttnArgs a) {
   const long long base_o = (long long)b * a.S * a.ld_o + h * D;
   const int kend = a.causal ? min(a.S, qblk + QB) : a.S;
   const int nkb = (kend + KT - 1) / KT;
-#pragma unroll
-  for (int st = 0; st < NS - 1; ++st) {
-    if (st < nkb) {
-      stage_rows<D, KT, NW>(smem + st * 2 * TILE, a.K + base + (long long)st * KT * a.ld, a.ld, a.S - st * KT, tid);
-      stage_rows<D, KT, NW>(smem + st * 2 * TILE + TILE, a.V + base + (long long)st * KT * a.ld, a.ld, a.S - st * KT,
-                            tid);
+  // full K / V tiles from per-lane offsets computed once (see stage_full16_128); ragged ones through stage_rows
+  constexpr bool FAST = D == 128 && (KT == 32 || KT == 64) && NW == 4 && DKV_FAST_STAGE;
+  unsigned offk[2] = {0u, 0u};
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  if (FAST) lane_off16_128(offk, a.ld, lane);
+  auto stage_kv = [&](char* dst, int kn) {
+    kn = __builtin_amdgcn_readfirstlane(kn);
+    if (FAST && (kn + 1) * KT <= a.S) {
+      stage_full16_128<KT>(dst, a.K + base + (long long)kn * KT * a.ld, a.ld, offk, wu);
+      stage_full16_128<KT>(dst + TILE, a.V + base + (long long)kn * KT * a.ld, a.ld, offk, wu);
+    } else {
+      stage_rows<D, KT, NW>(dst, a.K + base + (long long)kn * KT * a.ld, a.ld, a.S - kn * KT, tid);
+      stage_rows<D, KT, NW>(dst + TILE, a.V + base + (long long)kn * KT * a.ld, a.ld, a.S - kn * KT, tid);
     }
-  }
+  };
+#pragma unroll
+  for (int st = 0; st < NS - 1; ++st)
+    if (st < nkb) stage_kv(smem + st * 2 * TILE, st);
 
   bf16x8_t qf[2][G::DS], df[2][G::DS];
   float lse2[2], dlt[2];
@@ -590,11 +601,7 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_bwd_dq_kernel(AttnArgs a) {
     const char* sK = smem + (kb % NS) * 2 * TILE;
     const char* sV = sK + TILE;
     const int kn = kb + NS - 1;   // tile issued now; its slot was last read in iteration kb - 1 (behind a barrier)
-    if (kn < nkb) {
-      char* nxt = smem + (kn % NS) * 2 * TILE;
-      stage_rows<D, KT, NW>(nxt, a.K + base + (long long)kn * KT * a.ld, a.ld, a.S - kn * KT, tid);
-      stage_rows<D, KT, NW>(nxt + TILE, a.V + base + (long long)kn * KT * a.ld, a.ld, a.S - kn * KT, tid);
-    }
+    if (kn < nkb) stage_kv(smem + (kn % NS) * 2 * TILE, kn);
     if (!(a.causal && k0 > qw + 31)) {
       const bool need_mask = (a.causal && k0 + KT - 1 > qw) || k0 + KT > a.S;
       if (need_mask)
