@@ -3,10 +3,12 @@
 (BASELINE.json metric), one process per GPU over RCCL.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config configs/gpt_neo_1.3b.json] [--batch-per-gpu B]
+                    [--tp T]
 
 N > 1 is launched by the driver with ``torch.distributed.run`` (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* in the env).
-Weak scaling: every GPU processes ``batch-per-gpu`` (default 64) sequences per step (global batch = B x N, DP over all
-ranks).
+Weak scaling: every DP replica processes ``batch-per-gpu`` sequences per step (global batch = B x N / T). ``--tp T``
+builds the reference's 2-D mesh (``src/dataclass.py:247-252``): ``Mesh(dp=N/T, tp=T)``, heads sharded over T
+contiguous ranks -- BASELINE's GPT-Neo-2.7B at DP4 x TP2 and the 20B-scale config at TP8.
 Each timed step is a full training step: forward, backward, DP all-reduce, fused optimizer update. Data is synthetic
 (uniform random tokens, resident on the device) and the weights are randomly initialised.
 Rank 0 prints ONE JSON line.
@@ -44,7 +46,9 @@ def main():
     # 64 sequences x 2048 tokens per GPU (200 GiB peak of the 288 GiB HBM3E): the optimizer step and the DP all-reduce
     # are per-step costs, so bigger per-GPU shards amortise them (one MI355X: 16 -> 32 -> 48 -> 64 sequences gave
     # 113.5k -> 121.4k -> 122.9k -> 123.6k tokens/s)
-    ap.add_argument("--batch-per-gpu", type=int, default=64, help="0: the config's train_batch_size")
+    ap.add_argument("--batch-per-gpu", type=int, default=None,
+                    help="sequences per DP replica (default: 64 for GPT-Neo-1.3B, else the config's train_batch_size)")
+    ap.add_argument("--tp", type=int, default=1, help="tensor-parallel degree (heads sharded over T ranks)")
     ap.add_argument("--depth", type=int, default=0, help="(debug only: invalidates the headline number)")
     # the whole training step replayed as one hipGraph on a single GPU (1077 -> 1058 ms/step: the ~1500 launches of
     # a step no longer leave host-side gaps); with N > 1 ranks the step stays eager (RCCL all-reduces overlap it)
@@ -70,15 +74,24 @@ def main():
             dist.init_process_group("nccl", device_id=device)
         else:
             dist.init_process_group(backend)
-    mesh = pstate.Mesh(dp=world, tp=1, rank=rank).build_groups()
+    tp = max(int(args.tp), 1)
+    if world % tp:
+        raise SystemExit(f"--tp {tp} does not divide the {world} ranks")
+    dp = world // tp
+    mesh = pstate.Mesh(dp=dp, tp=tp, rank=rank).build_groups()
 
     overrides = {}
     if not os.path.exists(args.config):   # relative to the repository (profilers run from elsewhere)
         args.config = os.path.join(os.path.dirname(os.path.abspath(__file__)), args.config)
     base = load_config(args.config)
+    model_name = os.path.basename(args.config).replace(".json", "")
+    if args.batch_per_gpu is None:
+        args.batch_per_gpu = 64 if model_name == "gpt_neo_1.3b" else 0
     per_gpu = args.batch_per_gpu or base.train_batch_size
-    overrides["train_batch_size"] = per_gpu * world
-    overrides["mesh"] = {"dp": world, "tp": 1}
+    if base.heads % tp:
+        raise SystemExit(f"--tp {tp} does not divide the config's {base.heads} heads")
+    overrides["train_batch_size"] = per_gpu * dp
+    overrides["mesh"] = {"dp": dp, "tp": tp}
     if args.depth:
         overrides["depth"] = args.depth
     if args.hip_graphs:
@@ -104,6 +117,7 @@ def main():
                 dist.barrier()
 
     t_w = time.time()
+    from homebrewnlp_mtf_amd.utils import debug as obst_debug
     for i in range(args.warmup):
         m = trainer.step(batches[i % len(batches)])
         if i == 0:
@@ -113,6 +127,7 @@ def main():
     trainer.prepare_graphs()    # record (not run) any step graph the warm-up has not captured: timed steps replay
     barrier()
     torch.cuda.synchronize()
+    obst_debug.comm_reset()
     t0 = time.perf_counter()
     for i in range(args.steps):
         m = trainer.step(batches[i % len(batches)])
@@ -123,6 +138,11 @@ def main():
     if world > 1:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     elapsed = float(elapsed)
+    peak = torch.tensor([torch.cuda.max_memory_allocated(device) / 2 ** 30], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(peak, op=dist.ReduceOp.MAX)
+    peak = float(peak)
+    comm = obst_debug.comm_bytes()   # collectives issued by this rank's timed steps (host count, replays excluded)
     ms = 1000.0 * elapsed / max(args.steps, 1)
     tokens = params.train_batch_size * S * args.steps
     tps = tokens / elapsed
@@ -131,23 +151,36 @@ def main():
     if rank == 0:
         log(f"loss={float(m['loss']):.4f} acc={float(m['accuracy']):.4f} step={ms:.1f}ms "
             f"tokens/s={tps:.0f} MFU={mfu * 100:.1f}% ({fpt / 1e9:.2f} GFLOP/token)")
-        model = os.path.basename(args.config).replace(".json", "")
+        model = model_name
         metric = ("tokens/sec (whole node), GPT-Neo-1.3B seq2048 bf16" if model == "gpt_neo_1.3b" else
                   f"tokens/sec (whole node), {model} seq{S} bf16")
+        from homebrewnlp_mtf_amd.ops import raw as obst_raw
+        gemm = obst_raw.gemm_backend()
+        if world > 1:
+            per_step = {k: [c / max(args.steps, 1), round(b / max(args.steps, 1) / 2 ** 20, 2)]
+                        for k, (c, b) in comm.items()}
+            log(f"collectives per step on rank 0 ([calls, MiB]): {per_step}")
         print(json.dumps({
             "metric": metric,
             "value": round(tps, 1), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "bf16", "data": "synthetic (uniform random tokens), random-init weights",
             "mfu": round(mfu, 4), "final_loss": round(float(m["loss"]), 4),
+            "peak_mem_gib": round(peak, 2),   # max over ranks of the allocator's peak (288 GB HBM3E per GPU)
             # informational: the plain PyTorch-ROCm eager run of the same model on one MI355X (80,262 tokens/s at
             # batch 32; profiles/r2_torch_baseline.md) -- BASELINE.md publishes no number, so vs_baseline stays null
             "vs_torch_eager_per_gpu": (round(tps / world / TORCH_EAGER_1GPU, 3) if model == "gpt_neo_1.3b" else None),
             "config": {"model": os.path.basename(args.config).replace(".json", "") +
                                 (f"-depth{args.depth}(debug)" if args.depth else ""),
-                       "global_batch": params.train_batch_size, "seq_len": S, "parallelism": f"dp{world}",
+                       "global_batch": params.train_batch_size, "seq_len": S,
+                       "parallelism": f"dp{dp}" + (f"xtp{tp}" if tp > 1 else ""),
                        "params": trainer.store.global_numel(), "optimizer": params.optimizer,
-                       "hip_graphs": bool(params.use_hip_graphs and trainer._graphs_ok())}}), flush=True)
+                       "hip_graphs": bool(params.use_hip_graphs and trainer._graphs_ok()),
+                       # plain GEMMs: "gemm4w" = every product on the hand-written gfx950 kernel (no library GEMM)
+                       "gemm": gemm,
+                       "comm_mib_per_step": ({k: round(b / max(args.steps, 1) / 2 ** 20, 2)
+                                              for k, (c, b) in comm.items()} if world > 1 else None)}}),
+              flush=True)
     if world > 1:
         dist.destroy_process_group()
 

@@ -73,10 +73,30 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_brsrc(const void* base, l
 // LDS-DMA of 16 B per lane into the 1 KiB at LDS address m0 (lane-linear). In inline asm so the compiler neither
 // drains it with a vmcnt(0) before later LDS reads nor reorders it: every consumer waits with an explicit counted
 // vmcnt before the barrier that publishes the stage. One wait state between the M0 write and the LDS-DMA.
+// CP: cache-policy bits of the load (0 none, 1 sc0, 2 sc1, 3 sc0 sc1, 4 nt) -- an operand staged once per CU gains
+// nothing from the CU's L1.
+template <int CP = 0>
 __device__ __forceinline__ void dma16(const i32x4_t& rs, int voff, unsigned m0) {
-  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rs),
-               "s"(__builtin_amdgcn_readfirstlane(m0))
-               : "memory", "m0");
+  const unsigned m = __builtin_amdgcn_readfirstlane(m0);
+  if constexpr (CP == 0)
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rs), "s"(m)
+                 : "memory", "m0");
+  else if constexpr (CP == 1)
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen sc0 lds" ::"v"(voff), "s"(rs),
+                 "s"(m)
+                 : "memory", "m0");
+  else if constexpr (CP == 2)
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen sc1 lds" ::"v"(voff), "s"(rs),
+                 "s"(m)
+                 : "memory", "m0");
+  else if constexpr (CP == 3)
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen sc0 sc1 lds" ::"v"(voff),
+                 "s"(rs), "s"(m)
+                 : "memory", "m0");
+  else
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen nt lds" ::"v"(voff), "s"(rs),
+                 "s"(m)
+                 : "memory", "m0");
 }
 // C += A.B on one 16x16x32 bf16 tile, accumulator pinned to AGPRs: as a builtin, the register allocator re-assigned
 // the 64 loop-carried accumulators every iteration and copied them back through VGPRs at the back edge (512
@@ -239,9 +259,49 @@ __device__ __forceinline__ Tile4 decode4(const GemmArgs& p, long long L) {
 // NWV = 8 (G8W): two waves per SIMD, each owning 128 x 64 of C (8 x 4 accumulators, 128 AGPRs), 4 LDS-DMA pieces
 // per operand and K-tile per wave and a 64-slot MFMA stream -- a wave's DMA issue cost (~60 cycles per piece, one
 // wave per SIMD: nothing covers it) is hidden by its SIMD partner's MFMAs.
-template <int A_T, int B_T, bool OUT_F32, bool PROF, int NWV = 4>
+// Schedule SCH = 1 ("split", the K-loop structure of the library's 256x256x64 gfx950 kernel as read from its code
+// object, profiles/r4_gemm_sched.md): one K-tile = 128 MFMA slots q, four barriers, each operand on its own pair:
+//   q 1..15   substep-1 A fragments of this K-tile          q 20  lgkmcnt(0) + barrier: stage's A image free
+//   q 22..58  A LDS-DMA pieces of position pos+2 (8)        q 24..42 substep-1 B fragments
+//   q 50      lgkmcnt(0) + barrier: stage's B image free     q 61..124 B LDS-DMA pieces (8)
+//   q 67      vmcnt(18) + barrier: A of pos+1 landed         q 69..83 substep-0 A fragments of pos+1
+//   q 104     vmcnt(15) + barrier: B of pos+1 landed         q 106..120 substep-0 B fragments of pos+1
+// vmcnt(18) at q 67 = B(pos+1) 8 + this K-tile's 8 A + 2 B pieces; vmcnt(15) at q 104 = 8 A + 7 B pieces.
+// STG: waves on odd SIMDs run the same stream with every read / DMA one slot later (barriers fixed), so the four
+// SIMDs' LDS-DMA issue and fragment reads do not hit the TA and LDS in the same cycles.
+namespace g4s {
+constexpr int A1[8] = {1, 3, 5, 7, 9, 11, 13, 15};
+constexpr int B1[8] = {24, 27, 30, 33, 36, 38, 40, 42};
+constexpr int DA[8] = {22, 25, 28, 31, 34, 52, 55, 58};
+constexpr int DB[8] = {61, 64, 85, 87, 89, 95, 99, 124};
+constexpr int A0N[8] = {69, 71, 73, 75, 77, 79, 81, 83};
+constexpr int B0N[8] = {106, 108, 110, 112, 114, 116, 118, 120};
+constexpr int SETUP = 18, BAR_A = 20, BAR_B = 50, WA = 67, WB = 104, VA = 18, VB = 15;
+constexpr int idx(const int (&a)[8], int q) {
+  for (int i = 0; i < 8; ++i)
+    if (a[i] == q) return i;
+  return -1;
+}
+}  // namespace g4s
+
+#ifndef G4W_SCH
+#define G4W_SCH 0
+#endif
+#ifndef G4W_STG
+#define G4W_STG 0
+#endif
+#ifndef G4W_CPA
+#define G4W_CPA 0
+#endif
+#ifndef G4W_CPB
+#define G4W_CPB 0
+#endif
+
+template <int A_T, int B_T, bool OUT_F32, bool PROF, int NWV = 4, int SCH = G4W_SCH, bool STG = (G4W_STG != 0),
+          int CPA = G4W_CPA, int CPB = G4W_CPB>
 __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
   extern __shared__ __attribute__((aligned(1024))) char smem[];
+  static_assert(SCH == 0 || NWV == 4, "the split schedule is laid out for one wave per SIMD");
   constexpr int WN = NWV == 4 ? 128 : 64;    // output columns per wave
   constexpr int JB = WN / 16;                // B fragments per substep
   constexpr int PPW = 32 / NWV;              // LDS-DMA pieces per operand, K-tile and wave
@@ -252,6 +312,8 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
   constexpr int QW = NWV == 4 ? 107 : 50;    // barrier 2
   constexpr int STW = 8 * (JB / 2);          // direct-epilogue stores per wave (bf16; fp32: twice)
   constexpr int FW_BF = 2 * PPW + STW, FW_F32 = 2 * PPW + 2 * STW > 63 ? 63 : 2 * PPW + 2 * STW;
+  constexpr int SE = OUT_F32 ? 2 * STW : STW;   // the split schedule's waits after a direct epilogue
+  constexpr int VAF = g4s::VA + SE > 63 ? 63 : g4s::VA + SE, VBF = g4s::VB + SE > 63 ? 63 : g4s::VB + SE;
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = NWV == 4 ? wave >> 1 : wave & 1, wn = NWV == 4 ? wave & 1 : wave >> 1;
 
@@ -274,6 +336,8 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
   // this wave's PPW pieces of an operand image are contiguous: PPW KiB at (wave * PPW KiB)
   auto stage_a = [&](int s) -> unsigned { return lds0 + s * Q_STAGE + wave * PPW * 1024; };
   auto stage_b = [&](int s) -> unsigned { return lds0 + s * Q_STAGE + Q_OP + wave * PPW * 1024; };
+  // SIMD of this wave (HW_ID bits 5:4): the stagger's parity
+  const int simd_odd = STG ? (__builtin_amdgcn_s_getreg((4 << 0) | (4 << 6) | (0 << 11)) & 1) : 0;
 
   // DMA cursor: (tile round, K-tile) of the next position to stage; past the last tile it re-stages the last
   // position into the stage nobody reads any more
@@ -322,259 +386,307 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
     p.stamps[sbase + 7] = ntiles;
   }
 
-  // prologue: positions 0 and 1 into stages 0 and 1, wait for position 0, read its substep-0 fragments
-  dma_setup();
-#pragma unroll
-  for (int q = 0; q < PPW; ++q) dma16(ra, voa[q], stage_a(0) + q * 1024);
-#pragma unroll
-  for (int q = 0; q < PPW; ++q) dma16(rb, vob[q], stage_b(0) + q * 1024);
-  dma_advance();
-  dma_setup();
-#pragma unroll
-  for (int q = 0; q < PPW; ++q) dma16(ra, voa[q], stage_a(1) + q * 1024);
-#pragma unroll
-  for (int q = 0; q < PPW; ++q) dma16(rb, vob[q], stage_b(1) + q * 1024);
-  dma_advance();
-  vm_wait<2 * PPW>();
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_s_waitcnt(0xc07f);   // nothing (kernel-argument loads) pending in lgkmcnt at the loop entry
-  if (stamp) p.stamps[sbase + 1] = __builtin_amdgcn_s_memtime();
-  fence();
-  static_for<NR>([&](auto rc) { read_sub(0, K0{}, rc, a0, b0); fence(); });   // same order as in the loop
-
-  int pos = 0;   // flat position of the K-tile being multiplied (its stage is pos & 1)
-  // vmcnt of the first K-tile of a tile (see q == 107): 16 + the previous epilogue's stores, at most 63
-  const int first_wait = (p.act == 0 && p.mode == 0 && p.Zout == nullptr) ? (OUT_F32 ? FW_F32 : FW_BF) : 2 * PPW;
-  for (int rnd = 0; rnd < ntiles; ++rnd) {
-    const Tile4 ct = decode4<A_T, B_T>(p, logical(rnd));
-    // Accumulator zeroing (VALU writes of AGPRs) -> first MFMA reading them needs wait states the compiler cannot
-    // see through the asm MFMAs; the empty "+a" asms pin the zeros before the pad (no rematerialisation past it)
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < JB; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    static_for<8 * JB>([&](auto c) { agpr_opaque(acc[decltype(c)::value / JB][decltype(c)::value % JB]); });
-    asm volatile("s_nop 4" ::: "memory");
+  // the whole tile walk, its event stream shifted by SH slots on odd SIMDs (STG): two copies of the kernel body
+  // that meet only after the last tile (a branch per K-tile put a phi over the 256 accumulators: spills)
+  auto body = [&](auto shc) {
+    constexpr int SH = decltype(shc)::value;
+    // prologue: positions 0 and 1 into stages 0 and 1, wait for position 0, read its substep-0 fragments
+    dma_setup();
+  #pragma unroll
+    for (int q = 0; q < PPW; ++q) dma16<CPA>(ra, voa[q], stage_a(0) + q * 1024);
+  #pragma unroll
+    for (int q = 0; q < PPW; ++q) dma16<CPB>(rb, vob[q], stage_b(0) + q * 1024);
+    dma_advance();
+    dma_setup();
+  #pragma unroll
+    for (int q = 0; q < PPW; ++q) dma16<CPA>(ra, voa[q], stage_a(1) + q * 1024);
+  #pragma unroll
+    for (int q = 0; q < PPW; ++q) dma16<CPB>(rb, vob[q], stage_b(1) + q * 1024);
+    dma_advance();
+    vm_wait<2 * PPW>();
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // nothing (kernel-argument loads) pending in lgkmcnt at the loop entry
+    if (stamp) p.stamps[sbase + 1] = __builtin_amdgcn_s_memtime();
     fence();
-    if (stamp) tmark = __builtin_amdgcn_s_memtime();
+    static_for<NR>([&](auto rc) { read_sub(0, K0{}, rc, a0, b0); fence(); });   // same order as in the loop
 
-    for (int t = 0; t < nk; ++t, ++pos) {
-      const int s = pos & 1;
-      static_for<QS>([&](auto qc) {
-        constexpr int q = decltype(qc)::value;
-        constexpr int sub = q / (8 * JB), j = (q % (8 * JB)) / 8, i = q & 7;
-        if constexpr (sub == 0) mfma_acc(acc[i][j], b0[j], a0[i]);
-        else mfma_acc(acc[i][j], b1f[j], a1[i]);
-        if constexpr (q < NR && !(G4W_EXP & 2)) read_sub(s, K1{}, qc, a1, b1f);   // substep-1 fragments of pos
-        if constexpr (q == NR) dma_setup();                                 // resources of position pos + 2
-        if constexpr (q == QB1) {                                           // stage s fully read by every wave
-          if constexpr (PROF) tw = __builtin_amdgcn_s_memtime();
-          __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0) as a builtin: the compiler's wait model learns the
-          if constexpr (!(G4W_EXP & 4)) __builtin_amdgcn_s_barrier();   // substep-1 reads are done
-          if constexpr (PROF) sync1 += __builtin_amdgcn_s_memtime() - tw;
-        }
-        if constexpr (!(G4W_EXP & 1) && q >= QA0 && q < QA0 + DQ * PPW && (q - QA0) % DQ == 0)
-          dma16(ra, voa[(q - QA0) / DQ], stage_a(s) + (q - QA0) / DQ * 1024);
-        if constexpr (!(G4W_EXP & 1) && q >= QB0 && q < QB0 + DQ * PPW && (q - QB0) % DQ == 0)
-          dma16(rb, vob[(q - QB0) / DQ], stage_b(s) + (q - QB0) / DQ * 1024);
-        if constexpr (q == QW) {                                            // position pos+1 landed in stage s^1
-          // first K-tile of a tile: the previous tile's epilogue stores sit between that position's DMAs and this
-          // iteration's; count them out instead of waiting for every store (direct epilogue: 32 bf16 / 64 fp32)
-          if constexpr (PROF) tw = __builtin_amdgcn_s_memtime();
-          if (t == 0 && rnd > 0 && first_wait == FW_BF) vm_wait<FW_BF>();
-          else if (t == 0 && rnd > 0 && first_wait == FW_F32) vm_wait<FW_F32>();
-          else vm_wait<2 * PPW>();
-          if constexpr (!(G4W_EXP & 4)) __builtin_amdgcn_s_barrier();
-          if constexpr (PROF) sync2 += __builtin_amdgcn_s_memtime() - tw;
-        }
-        if constexpr (q > QW && q <= QW + NR && !(G4W_EXP & 2))             // substep-0 fragments of position pos+1
-          read_sub(s ^ 1, K0{}, std::integral_constant<int, q - QW - 1>{}, a0, b0);
-        fence();
-      });
-      dma_advance();
-    }
-    // last MFMA -> accumulator reads: the pad redefines every accumulator ("+a"), so the register allocator's
-    // AGPR -> VGPR copies for the epilogue (which fences do not bind) can only read them after it
-    fence();
-    pad_redefine(acc);
-    fence();
-    if (stamp) {
-      const unsigned long long now = __builtin_amdgcn_s_memtime();
-      loop_clk += now - tmark;
-      tmark = now;
-    }
+    int pos = 0;   // flat position of the K-tile being multiplied (its stage is pos & 1)
+    // vmcnt of the first K-tile of a tile (see q == 107): 16 + the previous epilogue's stores, at most 63
+    const int first_wait = (p.act == 0 && p.mode == 0 && p.Zout == nullptr) ? (OUT_F32 ? FW_F32 : FW_BF) : 2 * PPW;
+    const bool relaxed = first_wait != 2 * PPW;   // the previous tile's direct epilogue left its stores counted
+    for (int rnd = 0; rnd < ntiles; ++rnd) {
+      const Tile4 ct = decode4<A_T, B_T>(p, logical(rnd));
+      // Accumulator zeroing (VALU writes of AGPRs) -> first MFMA reading them needs wait states the compiler cannot
+      // see through the asm MFMAs; the empty "+a" asms pin the zeros before the pad (no rematerialisation past it)
+  #pragma unroll
+      for (int i = 0; i < 8; ++i)
+  #pragma unroll
+        for (int j = 0; j < JB; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      static_for<8 * JB>([&](auto c) { agpr_opaque(acc[decltype(c)::value / JB][decltype(c)::value % JB]); });
+      asm volatile("s_nop 4" ::: "memory");
+      fence();
+      if (stamp) tmark = __builtin_amdgcn_s_memtime();
 
-    // gelu GEMMs (bf16, no residual) take the direct epilogue too: forward with the pre-activation kept in Zout,
-    // backward C = acc * gelu'(Zin); each variant's activation is straight-line code (no per-value switch)
-    const bool gelu_direct = !OUT_F32 && p.act == ACT_GELU && p.R == nullptr &&
-                             ((p.mode == 0) || (p.mode == 1 && p.Zin != nullptr));
-    if ((p.act == 0 && p.mode == 0 && p.Zout == nullptr) || gelu_direct) {
-      // Direct epilogue (every plain product): each lane owns C[m][n..n+3] of 64 fragments and writes it with one
-      // buffer store from the accumulators (bf16: 8 B, fp32: 16 B); one per-lane offset, the fragment row in the
-      // SGPR offset, the fragment column in the instruction's immediate; rows past M fall outside the resource
-      // (dropped), columns past N are masked on the last tile column only.
-      const bool ws_out = OUT_F32 && p.ksplit > 1;
-      const long long ldc = ws_out ? p.N : p.ldc;
-      constexpr int ES = OUT_F32 ? 4 : 2;
-      char* cbase = ws_out ? reinterpret_cast<char*>(p.ws + (long long)ct.split * p.M * p.N)
-                           : reinterpret_cast<char*>(p.C) + ct.coff * ES;
-      const long long corg = ((long long)ct.m0 * ldc + ct.n0) * ES;
-      const long long cext = ((long long)(p.M - ct.m0 - 1) * ldc + (p.N - ct.n0)) * ES;   // bytes to C's end
-      const __amdgpu_buffer_rsrc_t rc = make_brsrc(cbase + corg, cext);
-      const i32x4_t rc4 = make_rsrc(cbase + corg, cext);
-      const __amdgpu_buffer_rsrc_t rr = make_brsrc(p.R ? reinterpret_cast<const char*>(p.R) + ct.coff * ES + corg : cbase, cext);
-      const int ml = lane & 15, gq = lane >> 4;
-      const float alpha = p.alpha, beta = ws_out ? 0.f : p.beta;
-      const bool edge = ct.n0 + wn * WN + WN > p.N;
-      const bool extra = (OUT_F32 && beta != 0.f) || (p.R != nullptr && !ws_out);
-      // fragment pair (2p, 2p+1) = 8 consecutive columns per lane (frag_b): 16 B (bf16) / 2 x 16 B (fp32) stores,
-      // 32 / 64 per wave (64 bf16 stores with the 32 LDS-DMAs in flight overflowed the 63-entry vmcnt)
-      const int voff = (int)(((long long)(wm * 128 + ml) * ldc + wn * WN + 8 * gq) * ES);
-      const int nbase = ct.n0 + wn * WN + 8 * gq;
-      // Zout / Zin share C's leading dimension and batch offset (bf16)
-      const i32x4_t rz4 = make_rsrc(p.Zout ? reinterpret_cast<const char*>(p.Zout) + ct.coff * 2 + corg : cbase, cext);
-      const __amdgpu_buffer_rsrc_t rzi =
-          make_brsrc(p.Zin ? reinterpret_cast<const char*>(p.Zin) + ct.coff * 2 + corg : cbase, cext);
-      const bool zout = p.Zout != nullptr;
-      // AC: 0 no activation, 1 gelu forward (+ Zout), 2 gelu backward (Zin)
-      auto emit = [&](auto exc, auto edc, auto acc_) {
-        constexpr bool EX = decltype(exc)::value, ED = decltype(edc)::value;
-        constexpr int AC = decltype(acc_)::value;
-        // one fragment row at a time: with EX its residual / C loads are issued together and consumed after,
-        // bounded by the fences (unbounded, the scheduler hoisted all 64 loads: 256 VGPRs, spills)
-        static_for<8>([&](auto ic) {
-          constexpr int i = decltype(ic)::value;
-          const int soff = __builtin_amdgcn_readfirstlane((int)(i * 16 * ldc * ES));
-          f32x4_t x[8];
-          if constexpr (AC == 2) {
-            static_for<JB / 2>([&](auto pc) {
-              constexpr int pp = decltype(pc)::value;
-              const v4u32_t o = __builtin_amdgcn_raw_buffer_load_b128(rzi, voff, soff + pp * 64, 0);
-              x[2 * pp] = f32x4_t{bf2f(o[0] & 0xffff), bf2f(o[0] >> 16), bf2f(o[1] & 0xffff), bf2f(o[1] >> 16)};
-              x[2 * pp + 1] = f32x4_t{bf2f(o[2] & 0xffff), bf2f(o[2] >> 16), bf2f(o[3] & 0xffff), bf2f(o[3] >> 16)};
-            });
+      // one K-tile (position pos in stage s), its event stream shifted by SH slots (the stagger)
+      auto ktile = [&](int t, int s) {
+        const bool first = t == 0 && rnd > 0 && relaxed;
+        static_for<QS>([&](auto qc) {
+          constexpr int q = decltype(qc)::value;
+          constexpr int sub = q / (8 * JB), j = (q % (8 * JB)) / 8, i = q & 7;
+          if constexpr (sub == 0) mfma_acc(acc[i][j], b0[j], a0[i]);
+          else mfma_acc(acc[i][j], b1f[j], a1[i]);
+          if constexpr (SCH == 0) {
+            if constexpr (q < NR && !(G4W_EXP & 2)) read_sub(s, K1{}, qc, a1, b1f);   // substep-1 fragments of pos
+            if constexpr (q == NR) dma_setup();                                 // resources of position pos + 2
+            if constexpr (q == QB1) {                                           // stage s fully read by every wave
+              if constexpr (PROF) tw = __builtin_amdgcn_s_memtime();
+              __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0) as a builtin: the compiler's wait model learns the
+              if constexpr (!(G4W_EXP & 4)) __builtin_amdgcn_s_barrier();   // substep-1 reads are done
+              if constexpr (PROF) sync1 += __builtin_amdgcn_s_memtime() - tw;
+            }
+            if constexpr (!(G4W_EXP & 1) && q >= QA0 + SH && q < QA0 + SH + DQ * PPW && (q - QA0 - SH) % DQ == 0)
+              dma16<CPA>(ra, voa[(q - QA0 - SH) / DQ], stage_a(s) + (q - QA0 - SH) / DQ * 1024);
+            if constexpr (!(G4W_EXP & 1) && q >= QB0 + SH && q < QB0 + SH + DQ * PPW && (q - QB0 - SH) % DQ == 0)
+              dma16<CPB>(rb, vob[(q - QB0 - SH) / DQ], stage_b(s) + (q - QB0 - SH) / DQ * 1024);
+            if constexpr (q == QW) {                                            // position pos+1 landed in stage s^1
+              // first K-tile of a tile: the previous tile's epilogue stores sit between that position's DMAs and
+              // this iteration's; count them out instead of waiting for every store (direct epilogue: 32 bf16 /
+              // 64 fp32)
+              if constexpr (PROF) tw = __builtin_amdgcn_s_memtime();
+              if (first) vm_wait<OUT_F32 ? FW_F32 : FW_BF>();
+              else vm_wait<2 * PPW>();
+              if constexpr (!(G4W_EXP & 4)) __builtin_amdgcn_s_barrier();
+              if constexpr (PROF) sync2 += __builtin_amdgcn_s_memtime() - tw;
+            }
+            if constexpr (q > QW && q <= QW + NR && !(G4W_EXP & 2))             // substep-0 fragments of pos+1
+              read_sub(s ^ 1, K0{}, std::integral_constant<int, q - QW - 1>{}, a0, b0);
+          } else {
+            const char* ia = smem + s * Q_STAGE;
+            const char* ib = ia + Q_OP;
+            constexpr int ra1 = g4s::idx(g4s::A1, q - SH), rb1 = g4s::idx(g4s::B1, q - SH);
+            constexpr int da = g4s::idx(g4s::DA, q - SH), db = g4s::idx(g4s::DB, q - SH);
+            constexpr int ra0 = g4s::idx(g4s::A0N, q - SH), rb0 = g4s::idx(g4s::B0N, q - SH);
+            if constexpr (ra1 >= 0) a1[ra1] = frag<A_T>(ia, wm * 128 + ra1 * 16, 1, lane);
+            if constexpr (rb1 >= 0) b1f[rb1] = frag_b<B_T>(ib, wn * WN, rb1, 1, lane);
+            if constexpr (q == g4s::SETUP) dma_setup();
+            if constexpr (q == g4s::BAR_A || q == g4s::BAR_B) {   // every wave done reading this stage's A / B image
+              if constexpr (PROF) tw = __builtin_amdgcn_s_memtime();
+              __builtin_amdgcn_s_waitcnt(0xc07f);
+              __builtin_amdgcn_s_barrier();
+              if constexpr (PROF) sync1 += __builtin_amdgcn_s_memtime() - tw;
+            }
+            if constexpr (da >= 0) dma16<CPA>(ra, voa[da], stage_a(s) + da * 1024);
+            if constexpr (db >= 0) dma16<CPB>(rb, vob[db], stage_b(s) + db * 1024);
+            if constexpr (q == g4s::WA || q == g4s::WB) {   // A / B image of position pos+1 landed in stage s^1
+              if constexpr (PROF) tw = __builtin_amdgcn_s_memtime();
+              if (first) vm_wait<q == g4s::WA ? VAF : VBF>();
+              else vm_wait<q == g4s::WA ? g4s::VA : g4s::VB>();
+              __builtin_amdgcn_s_barrier();
+              if constexpr (PROF) sync2 += __builtin_amdgcn_s_memtime() - tw;
+            }
+            if constexpr (ra0 >= 0) a0[ra0] = frag<A_T>(smem + (s ^ 1) * Q_STAGE, wm * 128 + ra0 * 16, 0, lane);
+            if constexpr (rb0 >= 0) b0[rb0] = frag_b<B_T>(smem + (s ^ 1) * Q_STAGE + Q_OP, wn * WN, rb0, 0, lane);
           }
-          if constexpr (EX) {
-            static_for<JB / 2>([&](auto pc) {
-              constexpr int pp = decltype(pc)::value;
-              if constexpr (OUT_F32) {
-                x[2 * pp] = x[2 * pp + 1] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-                if (beta != 0.f) {
-                  x[2 * pp] = beta * __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rc, voff, soff + pp * 128, 0));
-                  x[2 * pp + 1] = beta * __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rc, voff, soff + pp * 128 + 16, 0));
-                }
-                if (p.R) {
-                  x[2 * pp] += __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rr, voff, soff + pp * 128, 0));
-                  x[2 * pp + 1] += __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rr, voff, soff + pp * 128 + 16, 0));
-                }
-              } else {
-                const v4u32_t o = __builtin_amdgcn_raw_buffer_load_b128(rr, voff, soff + pp * 64, 0);
-                x[2 * pp] = f32x4_t{bf2f(o[0] & 0xffff), bf2f(o[0] >> 16), bf2f(o[1] & 0xffff), bf2f(o[1] >> 16)};
-                x[2 * pp + 1] = f32x4_t{bf2f(o[2] & 0xffff), bf2f(o[2] >> 16), bf2f(o[3] & 0xffff), bf2f(o[3] >> 16)};
-              }
-            });
-          }
-          static_for<JB / 2>([&](auto pc) {
-            constexpr int pp = decltype(pc)::value;
-            if (ED && nbase + pp * 32 >= p.N) return;
-            f32x4_t va = alpha * acc[i][2 * pp], vb = alpha * acc[i][2 * pp + 1];
-            if constexpr (EX) {
-              va += x[2 * pp];
-              vb += x[2 * pp + 1];
-            }
-            if constexpr (AC == 1) {
-              if (zout)
-                store16_padded(v4u32_t{pack_bf16x2(va[0], va[1]), pack_bf16x2(va[2], va[3]),
-                                       pack_bf16x2(vb[0], vb[1]), pack_bf16x2(vb[2], vb[3])},
-                               voff, rz4, soff, std::integral_constant<int, pp * 64>{});
-#pragma unroll
-              for (int t = 0; t < 4; ++t) {
-                va[t] = act_fwd(ACT_GELU, va[t]);
-                vb[t] = act_fwd(ACT_GELU, vb[t]);
-              }
-            } else if constexpr (AC == 2) {
-#pragma unroll
-              for (int t = 0; t < 4; ++t) {
-                va[t] *= act_grad(ACT_GELU, x[2 * pp][t]);
-                vb[t] *= act_grad(ACT_GELU, x[2 * pp + 1][t]);
-              }
-            }
-            if constexpr (OUT_F32) {
-              store16_padded(va, voff, rc4, soff, std::integral_constant<int, pp * 128>{});
-              store16_padded(vb, voff, rc4, soff, std::integral_constant<int, pp * 128 + 16>{});
-            } else {
-              // the same unpadded-hazard as the fp32 stores (garbage in ~1% of the bf16 outputs, measured)
-              store16_padded(v4u32_t{pack_bf16x2(va[0], va[1]), pack_bf16x2(va[2], va[3]), pack_bf16x2(vb[0], vb[1]),
-                                     pack_bf16x2(vb[2], vb[3])},
-                             voff, rc4, soff, std::integral_constant<int, pp * 64>{});
-            }
-          });
           fence();
         });
-        // loads into VGPRs pending at the loop back edge make the compiler's wait model drain vmcnt (the in-flight
-        // LDS-DMAs of the next tile included) at the top of every K-tile: retire them on this path
-        if constexpr (EX || AC == 2) __builtin_amdgcn_s_waitcnt(0x0f70);
       };
-      using T_ = std::true_type;
-      using F_ = std::false_type;
-      using A0 = std::integral_constant<int, 0>;
-      if constexpr (!OUT_F32) {
-        if (gelu_direct) {
-          using A1 = std::integral_constant<int, 1>;
-          using A2 = std::integral_constant<int, 2>;
-          if (p.mode == 1) {
-            if (edge) emit(F_{}, T_{}, A2{}); else emit(F_{}, F_{}, A2{});
+
+      for (int t = 0; t < nk; ++t, ++pos) {
+        const int s = pos & 1;
+        ktile(t, s);
+        dma_advance();
+      }
+      // last MFMA -> accumulator reads: the pad redefines every accumulator ("+a"), so the register allocator's
+      // AGPR -> VGPR copies for the epilogue (which fences do not bind) can only read them after it
+      fence();
+      pad_redefine(acc);
+      fence();
+      if (stamp) {
+        const unsigned long long now = __builtin_amdgcn_s_memtime();
+        loop_clk += now - tmark;
+        tmark = now;
+      }
+
+      // gelu GEMMs (bf16, no residual) take the direct epilogue too: forward with the pre-activation kept in Zout,
+      // backward C = acc * gelu'(Zin); each variant's activation is straight-line code (no per-value switch)
+      const bool gelu_direct = !OUT_F32 && p.act == ACT_GELU && p.R == nullptr &&
+                               ((p.mode == 0) || (p.mode == 1 && p.Zin != nullptr));
+      if ((p.act == 0 && p.mode == 0 && p.Zout == nullptr) || gelu_direct) {
+        // Direct epilogue (every plain product): each lane owns C[m][n..n+3] of 64 fragments and writes it with one
+        // buffer store from the accumulators (bf16: 8 B, fp32: 16 B); one per-lane offset, the fragment row in the
+        // SGPR offset, the fragment column in the instruction's immediate; rows past M fall outside the resource
+        // (dropped), columns past N are masked on the last tile column only.
+        const bool ws_out = OUT_F32 && p.ksplit > 1;
+        const long long ldc = ws_out ? p.N : p.ldc;
+        constexpr int ES = OUT_F32 ? 4 : 2;
+        char* cbase = ws_out ? reinterpret_cast<char*>(p.ws + (long long)ct.split * p.M * p.N)
+                             : reinterpret_cast<char*>(p.C) + ct.coff * ES;
+        const long long corg = ((long long)ct.m0 * ldc + ct.n0) * ES;
+        const long long cext = ((long long)(p.M - ct.m0 - 1) * ldc + (p.N - ct.n0)) * ES;   // bytes to C's end
+        const __amdgpu_buffer_rsrc_t rc = make_brsrc(cbase + corg, cext);
+        const i32x4_t rc4 = make_rsrc(cbase + corg, cext);
+        const __amdgpu_buffer_rsrc_t rr = make_brsrc(p.R ? reinterpret_cast<const char*>(p.R) + ct.coff * ES + corg : cbase, cext);
+        const int ml = lane & 15, gq = lane >> 4;
+        const float alpha = p.alpha, beta = ws_out ? 0.f : p.beta;
+        const bool edge = ct.n0 + wn * WN + WN > p.N;
+        const bool extra = (OUT_F32 && beta != 0.f) || (p.R != nullptr && !ws_out);
+        // fragment pair (2p, 2p+1) = 8 consecutive columns per lane (frag_b): 16 B (bf16) / 2 x 16 B (fp32) stores,
+        // 32 / 64 per wave (64 bf16 stores with the 32 LDS-DMAs in flight overflowed the 63-entry vmcnt)
+        const int voff = (int)(((long long)(wm * 128 + ml) * ldc + wn * WN + 8 * gq) * ES);
+        const int nbase = ct.n0 + wn * WN + 8 * gq;
+        // Zout / Zin share C's leading dimension and batch offset (bf16)
+        const i32x4_t rz4 = make_rsrc(p.Zout ? reinterpret_cast<const char*>(p.Zout) + ct.coff * 2 + corg : cbase, cext);
+        const __amdgpu_buffer_rsrc_t rzi =
+            make_brsrc(p.Zin ? reinterpret_cast<const char*>(p.Zin) + ct.coff * 2 + corg : cbase, cext);
+        const bool zout = p.Zout != nullptr;
+        // AC: 0 no activation, 1 gelu forward (+ Zout), 2 gelu backward (Zin)
+        auto emit = [&](auto exc, auto edc, auto acc_) {
+          constexpr bool EX = decltype(exc)::value, ED = decltype(edc)::value;
+          constexpr int AC = decltype(acc_)::value;
+          // one fragment row at a time: with EX its residual / C loads are issued together and consumed after,
+          // bounded by the fences (unbounded, the scheduler hoisted all 64 loads: 256 VGPRs, spills)
+          static_for<8>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            const int soff = __builtin_amdgcn_readfirstlane((int)(i * 16 * ldc * ES));
+            f32x4_t x[8];
+            if constexpr (AC == 2) {
+              static_for<JB / 2>([&](auto pc) {
+                constexpr int pp = decltype(pc)::value;
+                const v4u32_t o = __builtin_amdgcn_raw_buffer_load_b128(rzi, voff, soff + pp * 64, 0);
+                x[2 * pp] = f32x4_t{bf2f(o[0] & 0xffff), bf2f(o[0] >> 16), bf2f(o[1] & 0xffff), bf2f(o[1] >> 16)};
+                x[2 * pp + 1] = f32x4_t{bf2f(o[2] & 0xffff), bf2f(o[2] >> 16), bf2f(o[3] & 0xffff), bf2f(o[3] >> 16)};
+              });
+            }
+            if constexpr (EX) {
+              static_for<JB / 2>([&](auto pc) {
+                constexpr int pp = decltype(pc)::value;
+                if constexpr (OUT_F32) {
+                  x[2 * pp] = x[2 * pp + 1] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+                  if (beta != 0.f) {
+                    x[2 * pp] = beta * __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rc, voff, soff + pp * 128, 0));
+                    x[2 * pp + 1] = beta * __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rc, voff, soff + pp * 128 + 16, 0));
+                  }
+                  if (p.R) {
+                    x[2 * pp] += __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rr, voff, soff + pp * 128, 0));
+                    x[2 * pp + 1] += __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rr, voff, soff + pp * 128 + 16, 0));
+                  }
+                } else {
+                  const v4u32_t o = __builtin_amdgcn_raw_buffer_load_b128(rr, voff, soff + pp * 64, 0);
+                  x[2 * pp] = f32x4_t{bf2f(o[0] & 0xffff), bf2f(o[0] >> 16), bf2f(o[1] & 0xffff), bf2f(o[1] >> 16)};
+                  x[2 * pp + 1] = f32x4_t{bf2f(o[2] & 0xffff), bf2f(o[2] >> 16), bf2f(o[3] & 0xffff), bf2f(o[3] >> 16)};
+                }
+              });
+            }
+            static_for<JB / 2>([&](auto pc) {
+              constexpr int pp = decltype(pc)::value;
+              if (ED && nbase + pp * 32 >= p.N) return;
+              f32x4_t va = alpha * acc[i][2 * pp], vb = alpha * acc[i][2 * pp + 1];
+              if constexpr (EX) {
+                va += x[2 * pp];
+                vb += x[2 * pp + 1];
+              }
+              if constexpr (AC == 1) {
+                if (zout)
+                  store16_padded(v4u32_t{pack_bf16x2(va[0], va[1]), pack_bf16x2(va[2], va[3]),
+                                         pack_bf16x2(vb[0], vb[1]), pack_bf16x2(vb[2], vb[3])},
+                                 voff, rz4, soff, std::integral_constant<int, pp * 64>{});
+  #pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                  va[t] = act_fwd(ACT_GELU, va[t]);
+                  vb[t] = act_fwd(ACT_GELU, vb[t]);
+                }
+              } else if constexpr (AC == 2) {
+  #pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                  va[t] *= act_grad(ACT_GELU, x[2 * pp][t]);
+                  vb[t] *= act_grad(ACT_GELU, x[2 * pp + 1][t]);
+                }
+              }
+              if constexpr (OUT_F32) {
+                store16_padded(va, voff, rc4, soff, std::integral_constant<int, pp * 128>{});
+                store16_padded(vb, voff, rc4, soff, std::integral_constant<int, pp * 128 + 16>{});
+              } else {
+                // the same unpadded-hazard as the fp32 stores (garbage in ~1% of the bf16 outputs, measured)
+                store16_padded(v4u32_t{pack_bf16x2(va[0], va[1]), pack_bf16x2(va[2], va[3]), pack_bf16x2(vb[0], vb[1]),
+                                       pack_bf16x2(vb[2], vb[3])},
+                               voff, rc4, soff, std::integral_constant<int, pp * 64>{});
+              }
+            });
+            fence();
+          });
+          // loads into VGPRs pending at the loop back edge make the compiler's wait model drain vmcnt (the in-flight
+          // LDS-DMAs of the next tile included) at the top of every K-tile: retire them on this path. On an edge tile
+          // a wave may skip stores past N, and the next tile's relaxed counted waits (which assume every store was
+          // issued) would then pass before that wave's own DMAs of the next position landed: retire them here too.
+          if constexpr (EX || AC == 2 || ED) __builtin_amdgcn_s_waitcnt(0x0f70);
+        };
+        using T_ = std::true_type;
+        using F_ = std::false_type;
+        using A0 = std::integral_constant<int, 0>;
+        if constexpr (!OUT_F32) {
+          if (gelu_direct) {
+            using A1 = std::integral_constant<int, 1>;
+            using A2 = std::integral_constant<int, 2>;
+            if (p.mode == 1) {
+              if (edge) emit(F_{}, T_{}, A2{}); else emit(F_{}, F_{}, A2{});
+            } else {
+              if (edge) emit(F_{}, T_{}, A1{}); else emit(F_{}, F_{}, A1{});
+            }
+          } else if (extra) {
+            if (edge) emit(T_{}, T_{}, A0{}); else emit(T_{}, F_{}, A0{});
           } else {
-            if (edge) emit(F_{}, T_{}, A1{}); else emit(F_{}, F_{}, A1{});
+            if (edge) emit(F_{}, T_{}, A0{}); else emit(F_{}, F_{}, A0{});
           }
-        } else if (extra) {
-          if (edge) emit(T_{}, T_{}, A0{}); else emit(T_{}, F_{}, A0{});
         } else {
-          if (edge) emit(F_{}, T_{}, A0{}); else emit(F_{}, F_{}, A0{});
+          if (extra) {
+            if (edge) emit(T_{}, T_{}, A0{}); else emit(T_{}, F_{}, A0{});
+          } else {
+            if (edge) emit(F_{}, T_{}, A0{}); else emit(F_{}, F_{}, A0{});
+          }
         }
       } else {
-        if (extra) {
-          if (edge) emit(T_{}, T_{}, A0{}); else emit(T_{}, F_{}, A0{});
-        } else {
-          if (edge) emit(F_{}, T_{}, A0{}); else emit(F_{}, F_{}, A0{});
-        }
-      }
-    } else {
-      // Epilogue through a wave-private 8 KiB LDS region past the two stages (the stages already hold the next
-      // tile's first two K-tiles): 8 rounds of 16 rows x 128 columns fp32, float4 columns XOR-swizzled by row
-      // (conflict-free fragment writes). A round writes one fragment row of accumulators, then a compact runtime
-      // loop reads 8 consecutive outputs per lane and applies epilogue_store8r (one activation switch per round)
-      // with 16-byte global accesses; a fully unrolled per-fragment epilogue inlined the activation switch 64
-      // times (~12k branches), instruction-cache bound and as long as the K loop at K = 2048.
-      float* ep = reinterpret_cast<float*>(smem + 2 * Q_STAGE) + wave * 16 * WN;
-      const float alpha = p.alpha;
-      constexpr int LPR = WN / 8;   // lanes per 16-row x WN round row (8 outputs each)
-      static_for<8>([&](auto rcc) {
-        constexpr int r = decltype(rcc)::value;
-        static_for<JB>([&](auto jc) {
-          constexpr int j = decltype(jc)::value;
-          const int row = lane & 15, c4 = 8 * (j >> 1) + 2 * (lane >> 4) + (j & 1);   // frag_b column order
-          *reinterpret_cast<float4*>(ep + row * WN + ((c4 ^ (row & 7)) << 2)) =
-              make_float4(alpha * acc[r][j][0], alpha * acc[r][j][1], alpha * acc[r][j][2], alpha * acc[r][j][3]);
+        // Epilogue through a wave-private 8 KiB LDS region past the two stages (the stages already hold the next
+        // tile's first two K-tiles): 8 rounds of 16 rows x 128 columns fp32, float4 columns XOR-swizzled by row
+        // (conflict-free fragment writes). A round writes one fragment row of accumulators, then a compact runtime
+        // loop reads 8 consecutive outputs per lane and applies epilogue_store8r (one activation switch per round)
+        // with 16-byte global accesses; a fully unrolled per-fragment epilogue inlined the activation switch 64
+        // times (~12k branches), instruction-cache bound and as long as the K loop at K = 2048.
+        float* ep = reinterpret_cast<float*>(smem + 2 * Q_STAGE) + wave * 16 * WN;
+        const float alpha = p.alpha;
+        constexpr int LPR = WN / 8;   // lanes per 16-row x WN round row (8 outputs each)
+        static_for<8>([&](auto rcc) {
+          constexpr int r = decltype(rcc)::value;
+          static_for<JB>([&](auto jc) {
+            constexpr int j = decltype(jc)::value;
+            const int row = lane & 15, c4 = 8 * (j >> 1) + 2 * (lane >> 4) + (j & 1);   // frag_b column order
+            *reinterpret_cast<float4*>(ep + row * WN + ((c4 ^ (row & 7)) << 2)) =
+                make_float4(alpha * acc[r][j][0], alpha * acc[r][j][1], alpha * acc[r][j][2], alpha * acc[r][j][3]);
+          });
+  #pragma unroll 1
+          for (int it = 0; it < 16 * LPR / 64; ++it) {
+            const int row = it * (64 / LPR) + lane / LPR, c4 = (lane % LPR) * 2;
+            const float4 x0 = *reinterpret_cast<const float4*>(ep + row * WN + ((c4 ^ (row & 7)) << 2));
+            const float4 x1 = *reinterpret_cast<const float4*>(ep + row * WN + (((c4 + 1) ^ (row & 7)) << 2));
+            float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+            const int m = ct.m0 + wm * 128 + r * 16 + row, n = ct.n0 + wn * WN + c4 * 4;
+            if (m < p.M && n < p.N) epilogue_store8r<OUT_F32>(p, ct.coff + (long long)m * p.ldc + n, v);
+          }
+          fence();
         });
-#pragma unroll 1
-        for (int it = 0; it < 16 * LPR / 64; ++it) {
-          const int row = it * (64 / LPR) + lane / LPR, c4 = (lane % LPR) * 2;
-          const float4 x0 = *reinterpret_cast<const float4*>(ep + row * WN + ((c4 ^ (row & 7)) << 2));
-          const float4 x1 = *reinterpret_cast<const float4*>(ep + row * WN + (((c4 + 1) ^ (row & 7)) << 2));
-          float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-          const int m = ct.m0 + wm * 128 + r * 16 + row, n = ct.n0 + wn * WN + c4 * 4;
-          if (m < p.M && n < p.N) epilogue_store8r<OUT_F32>(p, ct.coff + (long long)m * p.ldc + n, v);
-        }
-        fence();
-      });
-      __builtin_amdgcn_s_waitcnt(0x0f70);   // residual / spill reloads retired here (see emit)
+        __builtin_amdgcn_s_waitcnt(0x0f70);   // residual / spill reloads retired here (see emit)
+      }
+      fence();
+      if (stamp) {
+        const unsigned long long now = __builtin_amdgcn_s_memtime();
+        epi_clk += now - tmark;
+      }
     }
-    fence();
-    if (stamp) {
-      const unsigned long long now = __builtin_amdgcn_s_memtime();
-      epi_clk += now - tmark;
-    }
+  };
+  if constexpr (STG) {
+    if (simd_odd) body(std::integral_constant<int, 1>{});
+    else body(std::integral_constant<int, 0>{});
+  } else {
+    body(std::integral_constant<int, 0>{});
   }
   vm_wait<0>();   // the last re-staged positions must land before the LDS is released
   if (p.stamps != nullptr) {

@@ -36,7 +36,8 @@ def padded_vocab(params: ModelParameter) -> int:
 class Model:
     def __init__(self, params: ModelParameter, device: typing.Union[str, torch.device] = "cpu",
                  tp_rank: int = 0, tp_size: int = 1, dtype: typing.Optional[torch.dtype] = None,
-                 init_device: typing.Optional[torch.device] = None, local_batch: typing.Optional[int] = None):
+                 init_device: typing.Optional[torch.device] = None, local_batch: typing.Optional[int] = None,
+                 finalize: bool = True):
         self.params = params
         self.device = torch.device(device)
         self.dtype = dtype or params.torch_calculation_dtype
@@ -54,8 +55,9 @@ class Model:
         with torch.no_grad():
             self._forward(self._dummy_inputs("meta"))
         self.builder.register = False
-        self.builder.store.finalize(self.device, self.dtype, init_device=init_device)
         self.store = self.builder.store
+        if finalize:   # finalize=False: shapes only (memory sizing, utils/memory.py) -- no buffers are allocated
+            self.store.finalize(self.device, self.dtype, init_device=init_device)
 
     # ---------------------------------------------------------------------------------------------------------------
     def _dummy_inputs(self, device):

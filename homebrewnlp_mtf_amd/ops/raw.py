@@ -47,6 +47,14 @@ def lt_enabled() -> int:
     return _LT
 
 
+def gemm_backend() -> str:
+    """which kernels run the plain GEMMs: "gemm4w" (the hand-written gfx950 MFMA kernel only) or
+    "hipblaslt+gemm4w" (the library takes the products OBST_LT_SCOPE gives it)"""
+    if not L.available():
+        return "torch-cpu"
+    return "hipblaslt+gemm4w" if lt_enabled() > 0 else "gemm4w"
+
+
 _LT_SCOPE = None
 
 

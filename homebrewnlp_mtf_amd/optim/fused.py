@@ -23,6 +23,7 @@ import torch.distributed as dist
 
 from ..ops import _lib as L
 from ..parallel import state as pstate
+from ..utils import debug
 from .chain import parse_chain
 
 OP = dict(none=0, adaptive_clip=1, l2norm_clip=2, global_l2norm_clip=3, value_clip=4, gradient_centralisation=5,
@@ -420,8 +421,9 @@ class FusedOptimizer:
         self.store.bump()
         if self.sm3 is not None:
             if self.tp > 1 and self.sm3_red_start < self.sm3_total:
-                dist.all_reduce(self.sm3[1 - self.flip][self.sm3_red_start:], op=dist.ReduceOp.MAX,
-                                group=pstate.mesh().tp_group)
+                red = self.sm3[1 - self.flip][self.sm3_red_start:]
+                debug.record("tp_all_reduce_max", red)
+                dist.all_reduce(red, op=dist.ReduceOp.MAX, group=pstate.mesh().tp_group)
             self.flip = 1 - self.flip
 
     # ------------------------------------------------------------------------------------------------------------

@@ -67,12 +67,13 @@ class GradSync:
         self.launched[bi] = True
         lo, hi, _ = self.buckets[bi]
         t = self.store.grad[lo:hi]
-        debug.record("dp_all_reduce", t)
         if self.dtype != torch.float32:
             low = t.to(self.dtype)
+            debug.record("dp_all_reduce", low)
             work = dist.all_reduce(low, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
             self.works.append((work, t, low))
         else:
+            debug.record("dp_all_reduce", t)
             work = dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
             self.works.append((work, None, None))
 

@@ -5,6 +5,8 @@
 * collective-sequence check: with ``OBST_COLLECTIVE_CHECK=1`` every explicit collective folds (kind, numel, dtype)
   into a running hash; ``verify()`` all-gathers the hashes and raises on the first rank whose sequence diverged --
   the RevNet + TP + DP deadlock hazard of SURVEY §7.5 item 2, caught as an error instead of a hang.
+* collective byte counter (always on, host arithmetic only): ``comm_bytes()`` returns the payload bytes per
+  collective kind issued since the last ``comm_reset()`` -- ``bench.py`` prints bytes per step at N > 1.
 """
 from __future__ import annotations
 
@@ -21,6 +23,8 @@ _ROCTX_ON = os.environ.get("OBST_ROCTX", "0") == "1"
 CHECK = os.environ.get("OBST_COLLECTIVE_CHECK", "0") == "1"
 _hash = hashlib.sha256()
 _count = 0
+_bytes: dict = {}
+_calls: dict = {}
 
 
 def _roctx():
@@ -48,8 +52,10 @@ def range_(name: str):
 
 
 def record(kind: str, t: torch.Tensor):
-    """fold one collective into the sequence hash (no-op unless OBST_COLLECTIVE_CHECK=1)"""
+    """count one collective's payload bytes; fold it into the sequence hash with OBST_COLLECTIVE_CHECK=1"""
     global _count
+    _bytes[kind] = _bytes.get(kind, 0) + t.numel() * t.element_size()
+    _calls[kind] = _calls.get(kind, 0) + 1
     if not CHECK:
         return
     _hash.update(f"{kind}:{t.numel()}:{t.dtype}|".encode())
@@ -73,3 +79,13 @@ def verify(group=None) -> int:
     _hash = hashlib.sha256()
     _count = 0
     return n
+
+
+def comm_bytes() -> dict:
+    """{kind: [calls, payload bytes]} of the collectives recorded since the last ``comm_reset()``"""
+    return {k: [_calls[k], _bytes[k]] for k in sorted(_bytes)}
+
+
+def comm_reset():
+    _bytes.clear()
+    _calls.clear()

@@ -128,21 +128,70 @@ def test_rccl_collectives_world1():
     assert len(rows) == 8 and all(x["backend"] == "nccl" and x["world"] == 1 and x["us"] > 0 for x in rows)
 
 
-def test_bench_two_rank_rehearsal():
+def _bench_rehearsal(world, extra, timeout=280):
     """bench.py's N > 1 path as the driver launches it (torch.distributed.run, one process per rank, MAX over ranks,
-    rank 0 prints one JSON line), rehearsed with two gloo ranks sharing cuda:0 at a reduced depth / batch"""
+    rank 0 prints one JSON line), rehearsed with gloo ranks sharing cuda:0"""
     import json
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, OBST_DIST_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0")
-    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "2", "--master-addr",
-                        "127.0.0.1", "--master-port", str(_free_port()), os.path.join(root, "bench.py"),
-                        "--gpus", "2", "--steps", "2", "--warmup", "1", "--batch-per-gpu", "2", "--depth", "2"],
-                       capture_output=True, text=True, env=env, timeout=280, cwd=root)
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", str(world),
+                        "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+                        os.path.join(root, "bench.py"), "--gpus", str(world), "--steps", "2", "--warmup", "1"] + extra,
+                       capture_output=True, text=True, env=env, timeout=timeout, cwd=root)
     assert r.returncode == 0, r.stderr[-3000:]
     rows = [json.loads(line) for line in r.stdout.splitlines() if line.startswith("{")]
     assert len(rows) == 1, r.stdout[-2000:]
     row = rows[0]
-    assert row["n_gpus"] == 2 and row["steps"] == 2 and row["value"] > 0 and row["ms_per_step"] > 0
+    assert row["n_gpus"] == world and row["steps"] == 2 and row["value"] > 0 and row["ms_per_step"] > 0
+    return row
+
+
+def test_bench_two_rank_rehearsal():
+    row = _bench_rehearsal(2, ["--batch-per-gpu", "2", "--depth", "2"])
     assert row["config"]["parallelism"] == "dp2" and row["config"]["global_batch"] == 4
+    assert row["config"]["comm_mib_per_step"]["dp_all_reduce"] > 0
+
+
+@pytest.mark.parametrize("world,tp", [(2, 2), (4, 2)])
+def test_bench_tp_rehearsal(world, tp):
+    """BASELINE config 4 (GPT-Neo-2.7B at DP x TP2) through bench.py --tp: heads over TP pairs, DP across them"""
+    row = _bench_rehearsal(world, ["--tp", str(tp), "--config", "configs/gpt_neo_2.7b.json", "--batch-per-gpu", "1",
+                                   "--depth", "2"])
+    dp = world // tp
+    assert row["config"]["parallelism"] == (f"dp{dp}xtp{tp}")
+    assert row["config"]["global_batch"] == dp
+    comm = row["config"]["comm_mib_per_step"]
+    assert comm["tp_all_reduce"] > 0
+    assert (comm.get("dp_all_reduce", 0) > 0) == (dp > 1)
+
+
+def test_gpt_neo_20b_tp8_fits_per_rank():
+    """BASELINE config 5 (20B-scale at TP8): eight gloo ranks share cuda:0, each holding exactly its TP8 shard (one
+    rank of the 8-GPU job). Two depths separate the per-layer bytes (masters, grads, slots, activations) from the
+    rest; extrapolated to the config's 44 layers and 8 sequences the per-rank peak must fit one MI355X's 288 GB,
+    and the CPU estimator (utils/memory.py, tests/test_memory.py) must not be optimistic."""
+    from homebrewnlp_mtf_amd.config import load_config
+    from homebrewnlp_mtf_amd.utils import memory
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cfg = os.path.join(root, "configs", "gpt_neo_20b_scale.json")
+    peaks = {}
+    for depth in (2, 4):
+        row = _bench_rehearsal(8, ["--tp", "8", "--config", cfg, "--batch-per-gpu", "1", "--depth", str(depth)],
+                               timeout=600)
+        assert row["config"]["parallelism"] == "dp1xtp8"
+        peaks[depth] = row["peak_mem_gib"] * 2 ** 30
+    per_layer = (peaks[4] - peaks[2]) / 2
+    rest = peaks[2] - 2 * per_layer
+    full = load_config(cfg)
+    est1 = memory.estimate(load_config(cfg, {"depth": 4, "train_batch_size": 1}), dp=1, tp=8)
+    est8 = memory.estimate(full, dp=1, tp=8)
+    # measured at batch 1 -> the config's batch 8: the activation share of a layer grows with the tokens
+    act1 = est1["activation_bytes_per_layer"]
+    layer8 = per_layer + (est8["activation_bytes_per_layer"] - act1)
+    predicted = rest + (est8["activation_bytes_other"] - est1["activation_bytes_other"]) + full.depth * layer8
+    print(f"20B TP8 rank: {per_layer / 2**30:.2f} GiB per layer at batch 1, rest {rest / 2**30:.2f} GiB; "
+          f"extrapolated {predicted / 1e9:.1f} GB; estimator {est8['total_bytes'] / 1e9:.1f} GB")
+    assert predicted <= 288e9
+    assert est8["total_bytes"] >= 0.9 * predicted
