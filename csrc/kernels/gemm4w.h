@@ -98,6 +98,20 @@ __device__ __forceinline__ void dma16(const i32x4_t& rs, int voff, unsigned m0) 
                  "s"(m)
                  : "memory", "m0");
 }
+// the same with m0 = stage base (SGPR) + OFF in one SALU op (the K loop's form: no temporary, no s_mov)
+#define OBST_DMA16O(BITS)                                                                                          \
+  asm volatile("s_add_u32 m0, %2, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen" BITS " lds" ::"v"(voff),   \
+               "s"(rs), "s"(sbase), "n"(OFF)                                                                      \
+               : "memory", "m0")
+template <int CP, int OFF>
+__device__ __forceinline__ void dma16o(const i32x4_t& rs, int voff, unsigned sbase) {
+  if constexpr (CP == 0) OBST_DMA16O("");
+  else if constexpr (CP == 1) OBST_DMA16O(" sc0");
+  else if constexpr (CP == 2) OBST_DMA16O(" sc1");
+  else if constexpr (CP == 3) OBST_DMA16O(" sc0 sc1");
+  else OBST_DMA16O(" nt");
+}
+#undef OBST_DMA16O
 // C += A.B on one 16x16x32 bf16 tile, accumulator pinned to AGPRs: as a builtin, the register allocator re-assigned
 // the 64 loop-carried accumulators every iteration and copied them back through VGPRs at the back edge (512
 // registers, spills); a tied "+a" operand keeps each one in place. Hazards the compiler cannot see inside the asm
@@ -220,10 +234,13 @@ struct Tile4 {
 };
 
 template <int A_T, int B_T>
-__device__ __forceinline__ Tile4 decode4(const GemmArgs& p, long long L) {
-  const int ntile = p.tiles_m * p.tiles_n;
+__device__ __forceinline__ Tile4 decode4(const GemmArgs& p, long long L64) {
+  // unsigned 32-bit index arithmetic (a launch has < 2^31 tiles): the 64-bit divisions were ~170 SALU ops on the
+  // MFMA stream's critical path at every tile switch
+  const unsigned L = (unsigned)L64;
+  const unsigned ntile = (unsigned)(p.tiles_m * p.tiles_n);
   const int bid = (int)(L % ntile);
-  const long long ybat = L / ntile;
+  const unsigned ybat = L / ntile;
   const int GROUP = 4;   // tile rows per N sweep: neighbouring CUs of an XCD share A panels and B panels
   const int per_group = GROUP * p.tiles_n;
   const int first_m = (bid / per_group) * GROUP;
@@ -233,9 +250,9 @@ __device__ __forceinline__ Tile4 decode4(const GemmArgs& p, long long L) {
   const int tn = (bid % per_group) / gsz;
   T.m0 = tm * 256;
   T.n0 = tn * 256;
-  T.split = (int)(ybat % p.ksplit);
-  const long long bidx = ybat / p.ksplit;
-  const long long b1 = bidx / p.nb2, b2 = bidx % p.nb2;
+  T.split = (int)(ybat % (unsigned)p.ksplit);
+  const unsigned bidx = ybat / (unsigned)p.ksplit;
+  const long long b1 = bidx / (unsigned)p.nb2, b2 = bidx % (unsigned)p.nb2;
   const long long kbeg = (long long)T.split * (p.K / p.ksplit);
   const bf16_t* A = p.A + b1 * p.a_s1 + b2 * p.a_s2;
   const bf16_t* B = p.B + b1 * p.b_s1 + b2 * p.b_s2;
@@ -274,6 +291,9 @@ constexpr int A1[8] = {1, 3, 5, 7, 9, 11, 13, 15};
 constexpr int B1[8] = {24, 27, 30, 33, 36, 38, 40, 42};
 constexpr int DA[8] = {22, 25, 28, 31, 34, 52, 55, 58};
 constexpr int DB[8] = {61, 64, 85, 87, 89, 95, 99, 124};
+// SCH = 2 ("burst"): each operand's 8 pieces back to back (one per 2 MFMAs) right behind the barrier that frees it
+constexpr int DA2[8] = {22, 24, 26, 28, 30, 32, 34, 36};
+constexpr int DB2[8] = {52, 54, 56, 58, 60, 62, 64, 66};
 constexpr int A0N[8] = {69, 71, 73, 75, 77, 79, 81, 83};
 constexpr int B0N[8] = {106, 108, 110, 112, 114, 116, 118, 120};
 constexpr int SETUP = 18, BAR_A = 20, BAR_B = 50, WA = 67, WB = 104, VA = 18, VB = 15;
@@ -310,10 +330,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
   constexpr int QB1 = NWV == 4 ? 25 : 14;    // barrier 1
   constexpr int QA0 = NWV == 4 ? 26 : 15, QB0 = NWV == 4 ? 66 : 31, DQ = NWV == 4 ? 5 : 4;   // DMA slots
   constexpr int QW = NWV == 4 ? 107 : 50;    // barrier 2
-  constexpr int STW = 8 * (JB / 2);          // direct-epilogue stores per wave (bf16; fp32: twice)
-  constexpr int FW_BF = 2 * PPW + STW, FW_F32 = 2 * PPW + 2 * STW > 63 ? 63 : 2 * PPW + 2 * STW;
-  constexpr int SE = OUT_F32 ? 2 * STW : STW;   // the split schedule's waits after a direct epilogue
-  constexpr int VAF = g4s::VA + SE > 63 ? 63 : g4s::VA + SE, VBF = g4s::VB + SE > 63 ? 63 : g4s::VB + SE;
+  constexpr int VA = SCH == 2 ? 24 : g4s::VA, VB = SCH == 2 ? 16 : g4s::VB;   // pieces younger than the awaited
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = NWV == 4 ? wave >> 1 : wave & 1, wn = NWV == 4 ? wave & 1 : wave >> 1;
 
@@ -341,20 +358,45 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
 
   // DMA cursor: (tile round, K-tile) of the next position to stage; past the last tile it re-stages the last
   // position into the stage nobody reads any more
+  // (the cursor's operand bases and bytes left advance by one K step in SALU adds; the resource clamps the bytes
+  // left with a 32-bit select -- a K-tile's setup was ~30 VALU/SALU ops of 64-bit signed compares at one slot)
   int d_rnd = 0, d_kt = 0;
-  Tile4 dt = decode4<A_T, B_T>(p, logical(0));
+  unsigned long long cur_a, cur_b, rem_a, rem_b;
+  auto cursor_tile = [&](const Tile4& T) {
+    cur_a = (unsigned long long)T.a;
+    cur_b = (unsigned long long)T.b;
+    rem_a = (unsigned long long)T.arem;   // > 0 at every position the cursor visits
+    rem_b = (unsigned long long)T.brem;
+  };
+  cursor_tile(decode4<A_T, B_T>(p, logical(0)));
+  auto rsrc_of = [](unsigned long long base, unsigned long long rem) {
+    i32x4_t r;
+    r[0] = (int)(unsigned)base;
+    r[1] = (int)(unsigned)(base >> 32);
+    unsigned hi = (unsigned)(rem >> 32);
+    asm volatile("" : "+s"(hi));   // an opaque SGPR: the clamp stays a 32-bit SALU select (not a VALU 64-bit compare)
+    r[2] = hi ? -1 : (int)(unsigned)rem;
+    r[3] = 0x00020000;
+    return r;
+  };
   i32x4_t ra, rb;
   auto dma_setup = [&]() {   // resources of the cursor's K-tile
-    ra = make_rsrc(dt.a + d_kt * astep, dt.arem - d_kt * astep);
-    rb = make_rsrc(dt.b + d_kt * bstep, dt.brem - d_kt * bstep);
+    ra = rsrc_of(cur_a, rem_a);
+    rb = rsrc_of(cur_b, rem_b);
   };
   auto dma_advance = [&]() {
     if (d_kt + 1 < nk) {
       ++d_kt;
+      cur_a += astep;
+      rem_a -= astep;
+      cur_b += bstep;
+      rem_b -= bstep;
     } else if (d_rnd + 1 < ntiles) {
+      // once per tile: the volatile asm keeps the compiler from if-converting the decode into every K-tile
+      asm volatile("");
       ++d_rnd;
       d_kt = 0;
-      dt = decode4<A_T, B_T>(p, logical(d_rnd));
+      cursor_tile(decode4<A_T, B_T>(p, logical(d_rnd)));
     }
   };
 
@@ -411,9 +453,6 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
     static_for<NR>([&](auto rc) { read_sub(0, K0{}, rc, a0, b0); fence(); });   // same order as in the loop
 
     int pos = 0;   // flat position of the K-tile being multiplied (its stage is pos & 1)
-    // vmcnt of the first K-tile of a tile (see q == 107): 16 + the previous epilogue's stores, at most 63
-    const int first_wait = (p.act == 0 && p.mode == 0 && p.Zout == nullptr) ? (OUT_F32 ? FW_F32 : FW_BF) : 2 * PPW;
-    const bool relaxed = first_wait != 2 * PPW;   // the previous tile's direct epilogue left its stores counted
     for (int rnd = 0; rnd < ntiles; ++rnd) {
       const Tile4 ct = decode4<A_T, B_T>(p, logical(rnd));
       // Accumulator zeroing (VALU writes of AGPRs) -> first MFMA reading them needs wait states the compiler cannot
@@ -428,8 +467,12 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
       if (stamp) tmark = __builtin_amdgcn_s_memtime();
 
       // one K-tile (position pos in stage s), its event stream shifted by SH slots (the stagger)
-      auto ktile = [&](int t, int s) {
-        const bool first = t == 0 && rnd > 0 && relaxed;
+      // The waits count the pieces younger than the awaited ones in the steady state. At the first K-tile of a
+      // tile the previous tile's epilogue stores sit in between, so the same count also waits for the older stores
+      // -- issued ~60 MFMAs earlier, they have retired by then; a relaxed count for that K-tile needs a runtime
+      // branch at every wait or a second copy of the K-tile, and the copy's phi over the 256 accumulators spills.
+      auto ktile = [&](int s) {
+        const unsigned sa = stage_a(s), sb = stage_b(s);
         static_for<QS>([&](auto qc) {
           constexpr int q = decltype(qc)::value;
           constexpr int sub = q / (8 * JB), j = (q % (8 * JB)) / 8, i = q & 7;
@@ -445,16 +488,15 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
               if constexpr (PROF) sync1 += __builtin_amdgcn_s_memtime() - tw;
             }
             if constexpr (!(G4W_EXP & 1) && q >= QA0 + SH && q < QA0 + SH + DQ * PPW && (q - QA0 - SH) % DQ == 0)
-              dma16<CPA>(ra, voa[(q - QA0 - SH) / DQ], stage_a(s) + (q - QA0 - SH) / DQ * 1024);
+              dma16o<CPA, (q - QA0 - SH) / DQ * 1024>(ra, voa[(q - QA0 - SH) / DQ], sa);
             if constexpr (!(G4W_EXP & 1) && q >= QB0 + SH && q < QB0 + SH + DQ * PPW && (q - QB0 - SH) % DQ == 0)
-              dma16<CPB>(rb, vob[(q - QB0 - SH) / DQ], stage_b(s) + (q - QB0 - SH) / DQ * 1024);
+              dma16o<CPB, (q - QB0 - SH) / DQ * 1024>(rb, vob[(q - QB0 - SH) / DQ], sb);
             if constexpr (q == QW) {                                            // position pos+1 landed in stage s^1
               // first K-tile of a tile: the previous tile's epilogue stores sit between that position's DMAs and
               // this iteration's; count them out instead of waiting for every store (direct epilogue: 32 bf16 /
               // 64 fp32)
               if constexpr (PROF) tw = __builtin_amdgcn_s_memtime();
-              if (first) vm_wait<OUT_F32 ? FW_F32 : FW_BF>();
-              else vm_wait<2 * PPW>();
+              vm_wait<2 * PPW>();
               if constexpr (!(G4W_EXP & 4)) __builtin_amdgcn_s_barrier();
               if constexpr (PROF) sync2 += __builtin_amdgcn_s_memtime() - tw;
             }
@@ -464,7 +506,8 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
             const char* ia = smem + s * Q_STAGE;
             const char* ib = ia + Q_OP;
             constexpr int ra1 = g4s::idx(g4s::A1, q - SH), rb1 = g4s::idx(g4s::B1, q - SH);
-            constexpr int da = g4s::idx(g4s::DA, q - SH), db = g4s::idx(g4s::DB, q - SH);
+            constexpr int da = g4s::idx(SCH == 2 ? g4s::DA2 : g4s::DA, q - SH);
+            constexpr int db = g4s::idx(SCH == 2 ? g4s::DB2 : g4s::DB, q - SH);
             constexpr int ra0 = g4s::idx(g4s::A0N, q - SH), rb0 = g4s::idx(g4s::B0N, q - SH);
             if constexpr (ra1 >= 0) a1[ra1] = frag<A_T>(ia, wm * 128 + ra1 * 16, 1, lane);
             if constexpr (rb1 >= 0) b1f[rb1] = frag_b<B_T>(ib, wn * WN, rb1, 1, lane);
@@ -475,12 +518,11 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
               __builtin_amdgcn_s_barrier();
               if constexpr (PROF) sync1 += __builtin_amdgcn_s_memtime() - tw;
             }
-            if constexpr (da >= 0) dma16<CPA>(ra, voa[da], stage_a(s) + da * 1024);
-            if constexpr (db >= 0) dma16<CPB>(rb, vob[db], stage_b(s) + db * 1024);
+            if constexpr (da >= 0) dma16o<CPA, (da < 0 ? 0 : da) * 1024>(ra, voa[da], sa);
+            if constexpr (db >= 0) dma16o<CPB, (db < 0 ? 0 : db) * 1024>(rb, vob[db], sb);
             if constexpr (q == g4s::WA || q == g4s::WB) {   // A / B image of position pos+1 landed in stage s^1
               if constexpr (PROF) tw = __builtin_amdgcn_s_memtime();
-              if (first) vm_wait<q == g4s::WA ? VAF : VBF>();
-              else vm_wait<q == g4s::WA ? g4s::VA : g4s::VB>();
+              vm_wait<q == g4s::WA ? VA : VB>();
               __builtin_amdgcn_s_barrier();
               if constexpr (PROF) sync2 += __builtin_amdgcn_s_memtime() - tw;
             }
@@ -493,7 +535,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
 
       for (int t = 0; t < nk; ++t, ++pos) {
         const int s = pos & 1;
-        ktile(t, s);
+        ktile(s);
         dma_advance();
       }
       // last MFMA -> accumulator reads: the pad redefines every accumulator ("+a"), so the register allocator's
@@ -615,10 +657,9 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
             fence();
           });
           // loads into VGPRs pending at the loop back edge make the compiler's wait model drain vmcnt (the in-flight
-          // LDS-DMAs of the next tile included) at the top of every K-tile: retire them on this path. On an edge tile
-          // a wave may skip stores past N, and the next tile's relaxed counted waits (which assume every store was
-          // issued) would then pass before that wave's own DMAs of the next position landed: retire them here too.
-          if constexpr (EX || AC == 2 || ED) __builtin_amdgcn_s_waitcnt(0x0f70);
+          // LDS-DMAs of the next tile included) at the top of every K-tile: retire them on this path. (Stores
+          // skipped past N on an edge tile only shorten the queue the K loop's counted waits were derived for.)
+          if constexpr (EX || AC == 2) __builtin_amdgcn_s_waitcnt(0x0f70);
         };
         using T_ = std::true_type;
         using F_ = std::false_type;

@@ -544,6 +544,45 @@ def _attention_kv(kv, x: Act, w_in, ws, w_in_dims, base_dims, w_out_dims, act_in
     return Act(o, x.dims)
 
 
+class _Fold:
+    """[d0, ..., dim, ..., heads, fph] -> [B', S, heads, fph] with the attention dim second and every other spatial
+    dim folded into the batch, so attention over a non-sequence axis (video ``three_axes``: height / width; ref
+    ``src/utils_mtf.py:418-422`` cycles the attention dim) runs on the same flash kernels as sequence attention.
+    Identity (no copy) when the attention dim already is dims[1] of a 4-d tensor."""
+
+    def __init__(self, dims, dim: Dim, feat):
+        lead = list(dims[:-len(feat)])
+        self.ai = lead.index(dim)
+        self.nlead = len(lead)
+        self.order = [i for i in range(self.nlead) if i != self.ai] + [self.ai] + \
+            list(range(self.nlead, len(dims)))
+        self.perm_shape = [dims[i].size for i in self.order]
+        self.identity = self.order == list(range(len(dims))) and self.nlead == 2
+        self.B = int(math.prod(d.size for i, d in enumerate(lead) if i != self.ai))
+        self.S = dim.size
+        self.feat = [d.size for d in feat]
+        self.inv = [self.order.index(i) for i in range(len(dims))]
+
+    def fwd(self, t: torch.Tensor) -> torch.Tensor:
+        if self.identity:
+            return t
+        return t.permute(self.order).reshape([self.B, self.S] + self.feat).contiguous()
+
+    def back(self, t: torch.Tensor) -> torch.Tensor:
+        if self.identity:
+            return t
+        return t.reshape(self.perm_shape).permute(self.inv).contiguous()
+
+
+def _fold_of(p, dims, dim: Dim) -> typing.Optional[_Fold]:
+    feat = list(p.feature_dims)
+    if len(feat) != 2 or feat[0] != p.head_dim or list(dims[-2:]) != feat or dims[0].name != "batch":
+        return None
+    if dim not in dims[1:-2]:
+        return None
+    return _Fold(dims, dim, feat)
+
+
 def _mixer_fast_ok(args: BlockArgs, x: Act, dim: Dim) -> bool:
     """the learned causal token mixer (biased_attention_map on the input as value) as one batched GEMM (K03)"""
     p = args.params
@@ -602,6 +641,13 @@ def attention(args: BlockArgs) -> Act:
             return _mixer_kv(args, kv, x, dim, tmp, causal)
         bias = embed(args, [p.head_dim, dim, tmp])
         return Act(F.token_mixer(x.t, bias.t, causal), x.dims)
+    fold = _fold_of(p, x.dims, dim) if FLASH_MAPS else None
+    if (fold is not None and not fold.identity and args.builder.kv is None and 'biased_attention_map' in args
+            and 'input_as_value' in args and not any(k in args for k in ('dot_product', 'biased_softmax',
+                                                                           'scale_attention_map'))):
+        # the learned token mixer over a non-sequence axis: the same K03 kernel on the folded input
+        bias = embed(args, [p.head_dim, dim, tmp])
+        return Act(fold.back(F.token_mixer(fold.fwd(x.t), bias.t, causal)), x.dims)
     if args.builder.kv is not None:
         args.builder.kv.unsupported = True     # the composable path below has no incremental form
 
@@ -626,27 +672,29 @@ def attention(args: BlockArgs) -> Act:
         #   scale_attention_map  -> multiplicative map on the probabilities (attn_map kernels)
         #   biased_attention_map -> (P + Bm) V = P V + Bm V: the learned token mixer (K03) on the same values
         # positional-only keys ([seq, heads, fph]) are broadcast over the batch
-        if (FLASH_MAPS and len(x.dims) == 4 and dim == x.dims[1] and qry.dims == x.dims and x.dims[2] == p.head_dim
-                and (key.dims == x.dims or key.dims == x.dims[1:])):
+        fold = _fold_of(p, x.dims, dim) if FLASH_MAPS else None
+        kdims_pos = [dim] + list(x.dims[-2:])   # positional-only keys: [attention dim, heads, fph]
+        if fold is not None and qry.dims == x.dims and (key.dims == x.dims or key.dims == kdims_pos):
             # maps created in the order of the generic path below (variable scopes / checkpoint names)
             sb = _masked_map(args)[0] if 'biased_softmax' in args else None
             ab = _masked_map(args) if 'biased_attention_map' in args else None
             sc = _masked_map(args) if 'scale_attention_map' in args else None
             v = key if 'shared_key_value' in args else (
                 Act(x.t, x.dims) if 'input_as_value' in args else activated_linear_out(args(base)))
-            kt = key.t if key.dims == x.dims else key.t.unsqueeze(0).expand(x.dims[0].size, *key.t.shape)
-            vt = v.t if v.dims == x.dims else v.t.unsqueeze(0).expand(x.dims[0].size, *v.t.shape)
+            kt = fold.fwd(key.t) if key.dims == x.dims else key.t.unsqueeze(0).expand(fold.B, *key.t.shape)
+            vt = fold.fwd(v.t) if v.dims == x.dims else v.t.unsqueeze(0).expand(fold.B, *v.t.shape)
+            qt = fold.fwd(qry.t)
             cm = _apply_mask(sc[0], sc[1], dim, tmp).t if sc is not None else None
             if sb is None and cm is None:
-                o = F.attention_core(qry.t, kt, vt, 1.0, causal)
+                o = F.attention_core(qt, kt, vt, 1.0, causal)
             else:
-                o = F.attention_map(qry.t, kt, vt, sb.t if sb is not None else None, cm, 1.0, causal)
+                o = F.attention_map(qt, kt, vt, sb.t if sb is not None else None, cm, 1.0, causal)
             if ab is not None:
                 bm = _apply_mask(ab[0], ab[1], dim, tmp).t
                 if cm is not None:
                     bm = bm * cm
                 o = o + F.token_mixer(vt.contiguous(), bm, causal)
-            return Act(o, x.dims)
+            return Act(fold.back(o), x.dims)
         old = D.linear_shapes(p, args, x.dims).old
         logit_dims = D.subtract(x.dims, D.subtract(old, [p.head_dim])) + [tmp]
         logit = named_einsum([qry, anonymize(key, dim)], logit_dims)

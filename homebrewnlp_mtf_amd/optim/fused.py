@@ -52,11 +52,19 @@ class Segment:
 
 
 def _graft_inner_ok(args) -> bool:
-    return bool(args) and args[0] in OP and args[0] not in REDUCTIONS and args[0] not in ("graft", "scale", "none")
+    """graft:<inner> is fused for every inner stage but Adafactor (its factored statistics need their own pre-pass)
+    and the pseudo-stages. A reducing inner stage (novograd, the clips, centralisation) opens the probe segment with
+    its own per-tensor factors from the statistics of the graft input -- the same statistics graft keeps."""
+    return (bool(args) and args[0] in OP and args[0] not in ("adafactor", "adafactor_clip", "graft", "scale", "none"))
 
 
 def supported(chain: str) -> bool:
     return all(n != "graft" or _graft_inner_ok(a) for n, a in parse_chain(chain))
+
+
+def unsupported_reason(chain: str) -> str:
+    bad = [a[0] if a else "" for n, a in parse_chain(chain) if n == "graft" and not _graft_inner_ok(a)]
+    return f"graft over {bad[0]!r} is not fused" if bad else "supported"
 
 
 def compile_chain(chain: str) -> typing.Tuple[typing.List[Segment], bool, bool]:
@@ -81,6 +89,8 @@ def compile_chain(chain: str) -> typing.Tuple[typing.List[Segment], bool, bool]:
                 segs[-1].emit_stats = True        # sum(g^2) of the graft input
             probe = Segment()
             probe.stages = [(a[0], tuple(a[1:]))]
+            if a[0] in REDUCTIONS:   # the inner stage's per-tensor factors from the graft input's statistics
+                probe.opener = (a[0], tuple(a[1:]))
             probe.stats_only = probe.emit_stats = probe.save_sq = True
             apply = Segment()
             apply.opener = ("graft", ())

@@ -44,6 +44,10 @@ class Trainer:
             f"({len(self.store.specs)} tensors), local {self.store.numel() / 1e6:.2f}M")
         if use_fused is None:
             use_fused = self.device.type == "cuda" and fused_opt.supported(params.optimizer)
+            if self.device.type == "cuda" and not use_fused:
+                log(f"WARNING: optimizer chain {params.optimizer!r} has no fused HIP plan "
+                    f"({fused_opt.unsupported_reason(params.optimizer)}): the whole step falls back to the "
+                    f"per-tensor torch ReferenceOptimizer on the GPU")
         self.opt = fused_opt.FusedOptimizer(self.store, params) if use_fused else ReferenceOptimizer(self.store,
                                                                                                         params)
         self.grad_sync = GradSync(self.store, self.mesh.dp_group, self.mesh.dp, params.grad_bucket_mb,

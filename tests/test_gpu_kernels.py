@@ -33,6 +33,14 @@ def lt(request, cuda):
     raw.lt_set(old)
 
 
+def g4w_calls() -> int:
+    """dispatches the hand-written one-wave-per-SIMD gemm4w kernel has taken so far"""
+    import ctypes
+    f = L.lib().obst_gemm4w_calls
+    f.restype = ctypes.c_longlong
+    return int(f())
+
+
 # ----------------------------------------------------------------------------------------------------------------
 @pytest.mark.parametrize("a_t,b_t", [(0, 0), (0, 1), (1, 0), (1, 1)])
 @pytest.mark.parametrize("M,N,K", [(128, 128, 64), (200, 136, 72), (512, 384, 256), (64, 8, 8)])
@@ -387,10 +395,12 @@ def test_cumsum(cuda):
 
 @pytest.mark.parametrize("K", [64, 128, 576])
 @pytest.mark.parametrize("a_t,b_t", [(0, 0), (0, 1), (1, 0), (1, 1)])
-def test_gemm_big_tile(cuda, a_t, b_t, K):
+def test_gemm_big_tile(cuda, lt, a_t, b_t, K):
     """shapes that take the 256x256 LDS-DMA kernels (>= 512 tiles), incl. ragged M/N edges; K = 576 runs the
-    phase kernel's steady state (counted vmcnt) for 7 K-tiles. Repeats must be bitwise identical (race screen)."""
+    K loop's steady state (counted vmcnt) for 9 K-tiles. Repeats must be bitwise identical (race screen). On the
+    "mfma" leg every product must run on gemm4w (persistent, direct and beta epilogues)."""
     torch.manual_seed(21 + a_t + 2 * b_t + K)
+    c0 = g4w_calls()
     M, N = 4160, 8128
     A = (torch.randn(M * K) * 0.5).to(BF)
     B = (torch.randn(N * K) * 0.5).to(BF)
@@ -414,6 +424,41 @@ def test_gemm_big_tile(cuda, a_t, b_t, K):
     raw.gemm(raw.Operand(Ad, a_t, lda), raw.Operand(Bd, b_t, ldb), raw.Operand(Cf, 0, N), M, N, K, beta=1.0)
     torch.cuda.synchronize()
     _close(Cf.view(M, N), ref + 1, 2e-2, 2e-2, f"gemm256 f32 {a_t}{b_t} K{K}")
+    if lt == 0:
+        assert g4w_calls() - c0 == 5, "the MFMA leg did not run gemm4w"
+
+
+@pytest.mark.parametrize("a_t,b_t", [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("out_f32", [False, True])
+def test_gemm4w_ragged(cuda, a_t, b_t, out_f32):
+    """gemm4w directly (hipBLASLt off) on ragged M / N -- 1, 17, 255, 257 rows (decode-sized products up to one row
+    past a tile), padded ldc -- bf16 and fp32 outputs, batched, against the fp32 oracle"""
+    old = raw.lt_set(False)
+    try:
+        for M, N, K, nb in ((1, 264, 128, 3), (17, 8, 64, 2), (255, 520, 192, 1), (257, 256, 320, 2)):
+            if a_t == 1 and M % 8:
+                continue   # a [K][M] operand needs 16-byte rows
+            torch.manual_seed(M + N + K)
+            ldc = N + 8
+            A = (torch.randn(nb * M * K) * 0.5).to(BF)
+            B = (torch.randn(nb * N * K) * 0.5).to(BF)
+            lda = K if a_t == 0 else M
+            ldb = K if b_t == 0 else N
+            av = A.view(nb, M, K) if a_t == 0 else A.view(nb, K, M).transpose(1, 2)
+            bv = B.view(nb, N, K).transpose(1, 2) if b_t == 0 else B.view(nb, K, N)
+            ref = av.float() @ bv.float()
+            dt = torch.float32 if out_f32 else BF
+            C = torch.full((nb * M * ldc,), 7.0, dtype=dt, device=cuda)
+            c0 = g4w_calls()
+            raw.gemm(raw.Operand(A.to(cuda), a_t, lda, M * K), raw.Operand(B.to(cuda), b_t, ldb, N * K),
+                     raw.Operand(C, 0, ldc, M * ldc), M, N, K, batch=(nb, 1))
+            torch.cuda.synchronize()
+            assert g4w_calls() - c0 == 1, f"{M}x{N}x{K} did not run gemm4w"
+            Cv = C.view(nb, M, ldc)
+            _close(Cv[:, :, :N], ref, 3e-2 * math.sqrt(K / 64), 2e-2, f"gemm4w {a_t}{b_t} {M}x{N}x{K} f32={out_f32}")
+            assert torch.all(Cv[:, :, N:].float().cpu() == 7.0), "wrote past N into the ldc padding"
+    finally:
+        raw.lt_set(old)
 
 
 @pytest.mark.parametrize("out_f32", [False, True])
@@ -453,11 +498,14 @@ def _persistent_cases(cuda, a_t, b_t, out_f32):
         assert torch.equal(outs[0], outs[1]), "run-to-run difference"
 
 
-@pytest.mark.parametrize("a_t,b_t", [(0, 0), (1, 1)])
-def test_gemm_splitk_wgrad(cuda, a_t, b_t):
-    """few output tiles + long K + fp32 accumulate: the phase kernel splits K into a workspace and reduces"""
+@pytest.mark.parametrize("a_t,b_t,M,N,K", [(0, 0, 1024, 1536, 16384), (1, 1, 1024, 1536, 16384),
+                                           (1, 0, 512, 768, 131072), (0, 1, 512, 768, 131072)])
+def test_gemm_splitk_wgrad(cuda, lt, a_t, b_t, M, N, K):
+    """few output tiles + long K + fp32 accumulate into C (beta = 1): K is split over the persistent grid into fp32
+    slabs and folded deterministically (gemm4w split-K + splitk_reduce_kernel on the "mfma" leg; K = 131072 is the
+    weight gradient of a 64 x 2048-token step, ks = 8)"""
     torch.manual_seed(5)
-    M, N, K = 1024, 1536, 16384
+    c0 = g4w_calls()
     A = (torch.randn(M * K) * 0.5).to(BF)
     B = (torch.randn(N * K) * 0.5).to(BF)
     lda = K if a_t == 0 else M
@@ -469,7 +517,9 @@ def test_gemm_splitk_wgrad(cuda, a_t, b_t):
     raw.gemm(raw.Operand(A.to(cuda), a_t, lda), raw.Operand(B.to(cuda), b_t, ldb), raw.Operand(Cf, 0, N), M, N, K,
              beta=1.0)
     torch.cuda.synchronize()
-    _close(Cf.view(M, N), ref, 5e-2, 1e-2, f"splitk {a_t}{b_t}")
+    _close(Cf.view(M, N), ref, 5e-2 * math.sqrt(K / 16384), 1e-2, f"splitk {a_t}{b_t} K{K}")
+    if lt == 0:
+        assert g4w_calls() - c0 == 1, "the MFMA leg did not run gemm4w"
 
 
 @pytest.mark.parametrize("a_t,b_t", [(0, 1), (1, 0), (0, 0)])

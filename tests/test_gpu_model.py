@@ -28,8 +28,17 @@ def _pair(cfg, cuda):
     return m_cpu, m_gpu
 
 
+@pytest.fixture(params=[0, 1], ids=["mfma", "hipblaslt"])
+def lt(request, cuda):
+    """plain GEMMs on the hand-written MFMA kernels (0) or on hipBLASLt (1)"""
+    from homebrewnlp_mtf_amd.ops import raw
+    old = raw.lt_set(request.param)
+    yield request.param
+    raw.lt_set(old)
+
+
 @pytest.mark.parametrize("variant", ["gpt", "gpt_d96", "revnet", "mixer"])
-def test_model_forward_backward(cuda, variant):
+def test_model_forward_backward(cuda, lt, variant):
     cfg = dict(GPT)
     if variant == "gpt_d96":     # GPT-Neo 20B-scale head dim
         cfg.update(features_per_head=96)
@@ -72,7 +81,8 @@ def test_model_forward_backward(cuda, variant):
                                    "sm3-l2norm_clip:0.1-momentum:0.9:1:0-learning_rate",
                                    "adafactor-learning_rate", "gradient_centralisation-value_clip:0.01-adam-"
                                                               "learning_rate-weight_centralisation",
-                                   "graft:adam-learning_rate", "value_clip:0.01-graft:sm3-momentum:0.9:1:0-learning_rate"])
+                                   "graft:adam-learning_rate", "value_clip:0.01-graft:sm3-momentum:0.9:1:0-learning_rate",
+                                   "graft:novograd-learning_rate", "sm3-graft:adaptive_clip:0.01-learning_rate"])
 @pytest.mark.parametrize("rows", ["1", "0"], ids=["row_tiled", "generic"])
 def test_fused_optimizer_matches_reference(cuda, chain, rows, monkeypatch):
     monkeypatch.setenv("OBST_OPT_ROWS", rows)

@@ -537,3 +537,43 @@ def test_axial_kernel_matches_einsum(layer, monkeypatch):
         res[fast] = (float(out["loss"].detach()), st.grad.clone())
     assert abs(res[True][0] - res[False][0]) < 1e-10
     assert torch.allclose(res[True][1], res[False][1], atol=1e-10, rtol=1e-8)
+
+
+@pytest.mark.parametrize("layers", [
+    ["attention-dot_product-context", "attention-dot_product-context", "attention-dot_product-context"],
+    ["attention-biased_softmax-dot_product-context-absolute", "attention-dot_product-positional-absolute",
+     "attention-biased_attention_map-absolute-input_as_value"]])
+def test_three_axes_attention_routing_matches_generic_path(layers, monkeypatch):
+    """video ``three_axes``: the attention dim cycles over time / height / width (ref src/utils_mtf.py:418-422);
+    the non-sequence axes go through the flash kernels by folding every other spatial axis into the batch
+    (layers._Fold). Loss and every gradient equal the named-einsum path's, fp64."""
+    from homebrewnlp_mtf_amd.models import layers as LY
+    res = {}
+    for flash in (True, False):
+        monkeypatch.setattr(LY, "FLASH_MAPS", flash)
+        torch.manual_seed(0)
+        cfg = dict(model_mode="jannet", use_video=True, use_language=False, heads=2, features_per_head=8, depth=1,
+                   sequence_length=4, time_patch=1, frame_width=16, frame_height=8, patch_size=4, color_channels=3,
+                   three_axes=True, token_patch_size=1, vocab_size=32, train_batch_size=2,
+                   intermediate_feed_forward_multiplier=2, memory_reduction_strategy="none",
+                   calculation_dtype="float64", experts=4,
+                   block_config=[{"layer": [la], "skip": True} for la in layers])
+        p = ModelParameter(cfg)
+        m = Model(p, "cpu")
+        st = m.store
+        st.master = st.master.double()
+        st.grad = st.grad.double()
+        st.compute = st.master
+        st._leaves = {}
+        st.master.copy_(torch.randn_like(st.master) * 0.3)
+        g = torch.Generator().manual_seed(3)
+        frame = torch.randint(0, 256, [2, p.time_patch_size + 1, p.frame_height_patch, p.frame_width_patch,
+                                       p.channel_color_size], dtype=torch.uint8, generator=g)
+        out = m(frame=frame, vid_msk_src=torch.ones(2, p.time_patch_size, dtype=torch.bool),
+                vid_msk_tgt=torch.ones(2, p.time_patch_size, dtype=torch.bool))
+        out["loss"].backward()
+        st.fold_leaf_grads()
+        res[flash] = (float(out["loss"].detach()), st.grad.clone(), list(st.order))
+    assert res[True][2] == res[False][2]
+    assert abs(res[True][0] - res[False][0]) < 1e-6 * max(1.0, abs(res[False][0]))
+    assert torch.allclose(res[True][1], res[False][1], atol=1e-6, rtol=1e-5)

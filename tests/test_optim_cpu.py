@@ -140,6 +140,13 @@ def test_fused_chain_compilation():
     # graft later in the chain: the segment before emits sum(g^2)
     segs, pre, wc = fused.compile_chain("value_clip:1-graft:sm3-momentum:0.9:1:0-learning_rate")
     assert segs[0].emit_stats and segs[1].stats_only and segs[1].save_sq and segs[2].reuse_input
+    # graft over a reducing inner stage: the probe opens with the inner stage's own factors
+    assert fused.supported("graft:novograd-learning_rate") and fused.supported("graft:adaptive_clip:0.1")
+    segs, pre, wc = fused.compile_chain("graft:novograd-learning_rate")
+    assert segs[0].stats_only and segs[0].opener == ("novograd", ()) and segs[1].opener == ("graft", ())
+    segs, pre, wc = fused.compile_chain("sm3-graft:adaptive_clip:0.01-learning_rate")
+    assert segs[0].emit_stats and segs[1].opener == ("adaptive_clip", ("0.01",)) and segs[1].save_sq
+    assert "adafactor" in fused.unsupported_reason("graft:adafactor-learning_rate")
 
 
 def test_grad_accumulation_matches_full_batch():

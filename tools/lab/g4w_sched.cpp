@@ -48,7 +48,7 @@ __global__ void fill_kernel(uint16_t* p, size_t n, uint32_t seed) {
   }
 }
 
-template <int A_T, int B_T, bool F32, int SCH, bool STG, int CPA, int CPB>
+template <int A_T, int B_T, bool F32, int SCH, bool STG, int CPA, int CPB, bool PROF = false>
 hipError_t launch_v(GemmArgs a, hipStream_t st) {
   a.tiles_m = (a.M + 255) / 256;
   a.tiles_n = (a.N + 255) / 256;
@@ -56,7 +56,7 @@ hipError_t launch_v(GemmArgs a, hipStream_t st) {
   const long long tiles = (long long)a.tiles_m * a.tiles_n * a.nbatch;
   const int grid = (int)(tiles >= 256 ? 256 : ((tiles + 7) / 8) * 8);
   const size_t lds = 2 * Q_STAGE + 32768;
-  auto k = gemm4w_kernel<A_T, B_T, F32, false, 4, SCH, STG, CPA, CPB>;
+  auto k = gemm4w_kernel<A_T, B_T, F32, PROF, 4, SCH, STG, CPA, CPB>;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -73,21 +73,20 @@ struct Shape {
 typedef hipError_t (*Launch)(GemmArgs, hipStream_t);
 struct Variant {
   const char* name;
-  Launch l00b, l01b;
+  Launch l00b, l01b, l00b_prof;
 };
 
 #define V(NAME, SCH, STG, CPA, CPB)                                                                  \
   Variant {                                                                                          \
-    NAME, launch_v<0, 0, false, SCH, STG, CPA, CPB>, launch_v<0, 1, false, SCH, STG, CPA, CPB>      \
+    NAME, launch_v<0, 0, false, SCH, STG, CPA, CPB>, launch_v<0, 1, false, SCH, STG, CPA, CPB>,     \
+        launch_v<0, 0, false, SCH, STG, CPA, CPB, true>                                              \
   }
 static const Variant variants[] = {
     V("sch0", 0, false, 0, 0),
-    V("sch0 stg", 0, true, 0, 0),
     V("sch1", 1, false, 0, 0),
-    V("sch1 stg", 1, true, 0, 0),
-    V("sch1 stg cp31", 1, true, 3, 1),
-    V("sch0 cp31", 0, false, 3, 1),
-    V("sch1 stg cp44", 1, true, 4, 4),
+    V("sch2", 2, false, 0, 0),
+    V("sch1 cp31", 1, false, 3, 1),
+    V("sch2 cp31", 2, false, 3, 1),
 };
 constexpr int NV = sizeof(variants) / sizeof(variants[0]);
 
@@ -101,6 +100,13 @@ static GemmArgs args_of(const Shape& s, const void* A, const void* B, void* C) {
   a.M = s.M; a.N = s.N; a.K = s.K; a.nb2 = 1;
   a.alpha = 1.f; a.beta = 0.f; a.ksplit = 1;
   return a;
+}
+
+static bool wanted(int v) {   // G4W_ONLY=0,2: run only these variants
+  const char* e = getenv("G4W_ONLY");
+  if (!e || !*e) return true;
+  std::string l = std::string(",") + e + ",";
+  return l.find("," + std::to_string(v) + ",") != std::string::npos;
 }
 
 static Launch pick(const Variant& v, const Shape& s) {
@@ -156,7 +162,7 @@ int main(int argc, char** argv) {
     const GemmArgs a = args_of(s, A, B, C1);
     for (int v = 0; v < NV; ++v) {
       Launch l = pick(variants[v], s);
-      if (!l) continue;
+      if (!l || !wanted(v) || getenv("SKIP_CHECK")) continue;
       CK(hipMemsetAsync(C1, 0, nc * es, st));
       CK(l(a, st));
       CK(hipStreamSynchronize(st));
@@ -191,7 +197,7 @@ int main(int argc, char** argv) {
     for (int r = 0; r < rounds; ++r)
       for (int v = 0; v <= NV; ++v) {
         Launch l = v < NV ? pick(variants[v], s) : nullptr;
-        if (v < NV && !l) continue;
+        if (v < NV && (!l || !wanted(v))) continue;
         auto go = [&]() { if (v < NV) (void)l(a, st); else run_lt(s, A, B, C1, st); };
         go();
         CK(hipEventRecord(e0, st));
@@ -213,6 +219,36 @@ int main(int argc, char** argv) {
       const double med = x[x.size() / 2], best = x[0];
       printf("%-44s %-16s median %8.1f us  best %8.1f us  %6.0f TF/s  vs lt %.3f\n", name,
              v < NV ? variants[v].name : "hipBLASLt", med * 1e3, best * 1e3, fl / med / 1e9, lt_med / med);
+    }
+    if (getenv("STAMPS") && s.a_t == 0 && s.b_t == 0 && !s.f32) {
+      // per-block [sync1 clocks (lgkmcnt + barrier waits), sync2 clocks (vmcnt + barrier waits), loop clocks,
+      // epilogue clocks, xcc, realtime start, realtime end, tiles] of one PROF-build launch per variant
+      unsigned long long* ds;
+      CK(hipMalloc(&ds, 256 * 64));
+      for (int v = 0; v < NV; ++v) {
+        if (!wanted(v)) continue;
+        GemmArgs b = a;
+        b.stamps = ds;
+        for (int w = 0; w < 3; ++w) CK(variants[v].l00b_prof(b, st));   // warm clocks
+        CK(hipMemset(ds, 0, 256 * 64));
+        CK(variants[v].l00b_prof(b, st));
+        CK(hipStreamSynchronize(st));
+        std::vector<unsigned long long> h(256 * 8);
+        CK(hipMemcpy(h.data(), ds, 256 * 64, hipMemcpyDeviceToHost));
+        double s1 = 0, s2 = 0, loop = 0, epi = 0, tiles = 0, rt = 0;
+        int nb = 0;
+        for (int i = 0; i < 256; ++i) {
+          const unsigned long long* t = &h[i * 8];
+          if (!t[6]) continue;
+          ++nb;
+          s1 += t[0]; s2 += t[1]; loop += t[2]; epi += t[3]; tiles += t[7]; rt += (double)(t[6] - t[5]);
+        }
+        const double nkt = s.K / 64.0;
+        printf("%-44s %-16s stamps: per K-tile loop %.0f clk (sync1 %.0f, sync2 %.0f), epilogue %.0f clk/tile, "
+               "clock %.2f GHz\n", name, variants[v].name, loop / tiles / nkt, s1 / tiles / nkt, s2 / tiles / nkt,
+               epi / tiles, (loop + epi) / (rt / 100.0) / 1e3 / nb * nb);
+      }
+      CK(hipFree(ds));
     }
     CK(hipFree(A));
     CK(hipFree(B));
