@@ -1,5 +1,6 @@
 #!/bin/bash
-# Round-end GPU check: all GPU tests, smoke, the headline bench (default and OBST_GEMM_LT=0), step profile.
+# Round-end GPU check: all GPU tests, smoke, the headline bench (default and OBST_GEMM_LT=1), step profile, and the
+# kernel perf-regression gate (tools/kbench.py --check profiles/kbench_floor.json: exit 1 on a > 5 % regression).
 set -o pipefail
 cd "$(dirname "$0")/.."
 export HSA_ENABLE_IPC_MODE_LEGACY=0
@@ -12,4 +13,8 @@ timeout -k 10 500 python -u bench.py --steps 20 --warmup 5 > gpurun_out/bench_fi
 tail -1 gpurun_out/bench_final.log
 OBST_GEMM_LT=0 timeout -k 10 400 python -u bench.py --steps 10 --warmup 3 > gpurun_out/bench_final_lt0.log 2>&1 || { echo "bench lt0 failed"; tail -20 gpurun_out/bench_final_lt0.log; exit 1; }
 tail -1 gpurun_out/bench_final_lt0.log
-bash tools/profile.sh r3f --steps 6 --warmup 3
+bash tools/profile.sh ${PROFILE_TAG:-r4f} --steps 6 --warmup 3 || exit 1
+timeout -k 10 400 python -u tools/kbench.py all --check profiles/kbench_floor.json > gpurun_out/kbench.log 2>&1
+rc=$?
+grep "REGRESSION\|kbench check" gpurun_out/kbench.log
+exit $rc

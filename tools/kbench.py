@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Maintained kernel harness: the training step's hot kernels at their GPT-Neo-1.3B shapes, one JSON line each.
 
-  python tools/kbench.py [gemm|attn|attn_map|norm|ew|all] [--reps N] [--tokens T]
+  python tools/kbench.py [gemm|attn|attn_map|norm|ew|all] [--reps N] [--tokens T] [--check profiles/kbench_floor.json]
 
 * gemm      -- every plain product of the step (fwd / dgrad / fp32 wgrad / logits) on hipBLASLt and on the
                hand-written gemm4w kernel, interleaved in one process (cdna guide §5.4 rule 24): TF/s and ratio.
@@ -11,6 +11,9 @@
 * attn_map  -- the biased_softmax / scale_attention_map kernels (csrc/kernels/attn_map.hip) at the same shape.
 * norm      -- norm fwd / bwd (+ residual gradient, + parameter gradients): GB/s of the bytes each must move.
 * ew        -- the streaming elementwise kernels (gelu fwd / bwd, add): GB/s.
+
+--check FLOOR.json (the perf-regression gate of tools/gpu_final.sh): every emitted line whose key (kernel, shape) has
+floors in the file must reach each floored metric within --tol (default 5 %); the exit status is 1 otherwise.
 
 The profiles under profiles/ quote these numbers; the one-off A/B scripts next to it (bench_*.py, gpu_*.sh) are the
 lab notes behind individual measurements (tools/README.md).
@@ -44,8 +47,28 @@ def timed(fn, reps: int) -> float:
     return e0.elapsed_time(e1) * 1e3 / reps
 
 
+EMITTED = []
+
+
 def emit(**kw):
+    EMITTED.append(kw)
     print(json.dumps(kw), flush=True)
+
+
+def line_key(row: dict) -> str:
+    return row["kernel"] + (f" {row['shape']}" if "shape" in row else "")
+
+
+def check(rows, floors: dict, tol: float = 0.05):
+    """-> list of (key, metric, value, floor) for every floored metric below floor * (1 - tol); higher is better for
+    every metric in the floor file (TF/s, PF/s, GB/s)"""
+    bad = []
+    for row in rows:
+        for metric, floor in floors.get(line_key(row), {}).items():
+            v = row.get(metric)
+            if v is None or v < floor * (1.0 - tol):
+                bad.append((line_key(row), metric, v, floor))
+    return bad
 
 
 def bench_gemm(T: int, reps: int):
@@ -165,6 +188,8 @@ def main(argv=None):
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--tokens", type=int, default=131072, help="tokens per step (GPT-Neo-1.3B: 64 x 2048)")
     ap.add_argument("--batch", type=int, default=64, help="attention batch at S 2048")
+    ap.add_argument("--check", default=None, help="floor file: fail on a regression past --tol")
+    ap.add_argument("--tol", type=float, default=0.05)
     a = ap.parse_args(argv)
     todo = ["gemm", "attn", "attn_map", "norm", "ew"] if a.what == "all" else [a.what]
     for w in todo:
@@ -178,6 +203,17 @@ def main(argv=None):
             bench_norm(a.tokens, a.reps)
         else:
             bench_ew(a.tokens, a.reps)
+    if a.check:
+        with open(a.check) as f:
+            floors = json.load(f)["floors"]
+        bad = check(EMITTED, floors, a.tol)
+        seen = {line_key(r) for r in EMITTED}
+        for key, metric, v, floor in bad:
+            print(f"REGRESSION {key}: {metric} {v} < floor {floor} - {a.tol:.0%}", flush=True)
+        n = sum(len(m) for k, m in floors.items() if k in seen)
+        print(f"kbench check: {n - len(bad)}/{n} floored metrics pass", flush=True)
+        if bad:
+            sys.exit(1)
 
 
 if __name__ == "__main__":
