@@ -228,3 +228,19 @@ def test_tp_optimizer_chains_match_single_rank(chain):
         full = ref.store.master_view(name)
         diff = (_gather_tp(ranks, name, full.shape, 2) - full).abs().max().item()
         assert diff < 5e-5, f"{chain}: TP weight {name} differs by {diff}"
+
+
+def test_dp_bf16_wire_close_to_fp32_wire():
+    """allreduce_dtype="bfloat16" (opt-in; fp32 by default): the DP buckets travel as bf16 (half the xGMI bytes) and
+    are summed back into the fp32 gradient buffer. After two steps the fp32 masters stay within bf16 rounding of the
+    gradients of the fp32-wire run, and the two replicas stay identical."""
+    fp = _run("dp")
+    bf = _run("dp", dict(CFG, allreduce_dtype="bfloat16"))
+    assert torch.equal(bf[0]["master"], bf[1]["master"]), "bf16-wire DP replicas diverged"
+    init = _single(dict(CFG, learning_rate=0.0))[0].store.master
+    upd_fp = fp[0]["master"] - init
+    upd_bf = bf[0]["master"] - init
+    rel = (upd_bf - upd_fp).norm() / upd_fp.norm()
+    assert 0 < rel < 2e-2, f"bf16 wire moved the update by {rel:.3g} relative"
+    for a, b in zip(fp[0]["losses"], bf[0]["losses"]):
+        assert abs(a - b) < 1e-3 * abs(a)
