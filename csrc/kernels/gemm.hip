@@ -527,14 +527,16 @@ OBST_API int obst_gemm(const ObstGemmDesc* d, hipStream_t stream) {
   const bool big = impl > 0 && d->K % 64 == 0 && d->M >= 256 && d->N >= 256 &&
                    big_tiles * a.ksplit >= (a.ksplit > 1 ? 256 : 512) &&
                    (d->a_t == 0 || d->M % 8 == 0) && (d->b_t == 0 || d->N % 8 == 0);
-  // one-wave-per-SIMD kernel (gemm4w.hip): every plain product (no triangle, no split contraction index)
-  if (g4w_enabled() && d->tri == 0 && d->K % 64 == 0 && (d->a_t == 0 || d->M % 8 == 0) &&
-      (d->b_t == 0 || d->N % 8 == 0)) {
+  // one-wave-per-SIMD kernel (gemm4w.hip): every plain product and the triangular-A ones (tri 1 / 2: the token
+  // mixer, K03 -- each output tile runs only its K range); not the split contraction index or tri 3
+  if (g4w_enabled() && (d->tri == 0 || d->tri == 1 || d->tri == 2) && d->K % 64 == 0 &&
+      (d->a_t == 0 || d->M % 8 == 0) && (d->b_t == 0 || d->N % 8 == 0)) {
     // split-K for fp32 products with few output tiles (the weight gradients): the persistent kernel runs
     // ceil(tiles * ks / 256) rounds of K / ks each; a split costs a deterministic fold over ks fp32 slabs. Pick the
     // ks of least modelled time (1.25 us per 64-deep K-tile of a tile, ~5 TB/s for the fold), workspace <= 1 GiB.
     int ks = 1;
-    if (ksplit_env > 0 && big_tiles < 512 && d->out_f32 && !d->R && !d->act && d->mode == 0 && batch == 1) {
+    if (ksplit_env > 0 && big_tiles < 512 && d->out_f32 && !d->R && !d->act && d->mode == 0 && batch == 1 &&
+        d->tri == 0) {
       const double per_k = 1.25 / 64.0;   // us per K element of one tile
       double best = 1e300;
       for (int c = 1; c <= 8; c *= 2) {

@@ -231,6 +231,7 @@ struct Tile4 {
   long long arem, brem;
   long long coff;
   int m0, n0, split;
+  int nk;   // K-tiles of this tile (the K range of a triangular A, see decode4)
 };
 
 template <int A_T, int B_T>
@@ -238,22 +239,42 @@ __device__ __forceinline__ Tile4 decode4(const GemmArgs& p, long long L64) {
   // unsigned 32-bit index arithmetic (a launch has < 2^31 tiles): the 64-bit divisions were ~170 SALU ops on the
   // MFMA stream's critical path at every tile switch
   const unsigned L = (unsigned)L64;
-  const unsigned ntile = (unsigned)(p.tiles_m * p.tiles_n);
-  const int bid = (int)(L % ntile);
-  const unsigned ybat = L / ntile;
-  const int GROUP = 4;   // tile rows per N sweep: neighbouring CUs of an XCD share A panels and B panels
-  const int per_group = GROUP * p.tiles_n;
-  const int first_m = (bid / per_group) * GROUP;
-  const int gsz = min(p.tiles_m - first_m, GROUP);
   Tile4 T;
-  const int tm = first_m + (bid % per_group) % gsz;
-  const int tn = (bid % per_group) / gsz;
+  int tm, tn;
+  unsigned ybat;
+  if (p.tri == 0) {
+    const unsigned ntile = (unsigned)(p.tiles_m * p.tiles_n);
+    const int bid = (int)(L % ntile);
+    ybat = L / ntile;
+    const int GROUP = 4;   // tile rows per N sweep: neighbouring CUs of an XCD share A panels and B panels
+    const int per_group = GROUP * p.tiles_n;
+    const int first_m = (bid / per_group) * GROUP;
+    const int gsz = min(p.tiles_m - first_m, GROUP);
+    tm = first_m + (bid % per_group) % gsz;
+    tn = (bid % per_group) / gsz;
+  } else {
+    // triangular A (tri 1: A[m][k] = 0 for k > m, tri 2: for k < m): tile rows in order of decreasing K range,
+    // the slowest index, so every round of the block-cyclic walk (logical4) holds tiles of equal work
+    const unsigned per_row = (unsigned)p.tiles_n * (unsigned)p.nbatch;
+    const int tmr = (int)(L / per_row);
+    const unsigned rest = L % per_row;
+    ybat = rest / (unsigned)p.tiles_n;
+    tn = (int)(rest % (unsigned)p.tiles_n);
+    tm = p.tri == 1 ? p.tiles_m - 1 - tmr : tmr;
+  }
   T.m0 = tm * 256;
   T.n0 = tn * 256;
   T.split = (int)(ybat % (unsigned)p.ksplit);
   const unsigned bidx = ybat / (unsigned)p.ksplit;
   const long long b1 = bidx / (unsigned)p.nb2, b2 = bidx % (unsigned)p.nb2;
-  const long long kbeg = (long long)T.split * (p.K / p.ksplit);
+  long long kbeg = (long long)T.split * (p.K / p.ksplit);
+  T.nk = p.K / p.ksplit / 64;
+  if (p.tri == 1) {            // k < min(K, m0 + 256)
+    T.nk = min(p.K, T.m0 + 256) / 64;
+  } else if (p.tri == 2) {     // k >= m0
+    kbeg = T.m0;
+    T.nk = (p.K - T.m0) / 64;
+  }
   const bf16_t* A = p.A + b1 * p.a_s1 + b2 * p.a_s2;
   const bf16_t* B = p.B + b1 * p.b_s1 + b2 * p.b_s2;
   // extent of each operand (elements from its batch base): [M][lda] rows / [K][lda] k-rows
@@ -337,12 +358,15 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
   const long long total = (long long)p.tiles_m * p.tiles_n * p.nbatch;
   const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3, nslot = gridDim.x >> 3;
   const long long Q = total >> 3, Rm = total & 7;
-  const long long base = xcd < Rm ? xcd * (Q + 1) : Rm * (Q + 1) + (xcd - Rm) * Q;
-  const long long len = Q + (xcd < Rm ? 1 : 0);
-  const int ntiles = (int)(len > slot ? (len - slot + nslot - 1) / nslot : 0);   // tiles of this block
-  if (ntiles == 0) return;
-  auto logical = [&](int r) { return base + slot + (long long)r * nslot; };
-  const int nk = p.K / p.ksplit / 64;
+  // dense: XCD x walks a contiguous run of tiles (L2 sharing of A / B panels); triangular: block-cyclic over the
+  // whole grid (decode4 orders the tiles by work, so each round is balanced)
+  const bool cyc = p.tri != 0;
+  const long long start = cyc ? 0 : xcd < Rm ? xcd * (Q + 1) : Rm * (Q + 1) + (xcd - Rm) * Q;
+  const long long len = cyc ? total : Q + (xcd < Rm ? 1 : 0);
+  const long long first = cyc ? blockIdx.x : slot;
+  const long long stride = cyc ? gridDim.x : nslot;
+  const int ntiles = (int)(len > first ? (len - first + stride - 1) / stride : 0);   // tiles of this block
+  auto logical = [&](int r) { return start + first + (long long)r * stride; };
   const long long astep = A_T == 0 ? 128 : 128 * p.lda;
   const long long bstep = B_T == 0 ? 128 : 128 * p.ldb;
 
@@ -360,9 +384,10 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
   // position into the stage nobody reads any more
   // (the cursor's operand bases and bytes left advance by one K step in SALU adds; the resource clamps the bytes
   // left with a 32-bit select -- a K-tile's setup was ~30 VALU/SALU ops of 64-bit signed compares at one slot)
-  int d_rnd = 0, d_kt = 0;
+  int d_rnd = 0, d_kt = 0, d_nk = 0;
   unsigned long long cur_a, cur_b, rem_a, rem_b;
   auto cursor_tile = [&](const Tile4& T) {
+    d_nk = T.nk;
     cur_a = (unsigned long long)T.a;
     cur_b = (unsigned long long)T.b;
     rem_a = (unsigned long long)T.arem;   // > 0 at every position the cursor visits
@@ -385,7 +410,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
     rb = rsrc_of(cur_b, rem_b);
   };
   auto dma_advance = [&]() {
-    if (d_kt + 1 < nk) {
+    if (d_kt + 1 < d_nk) {
       ++d_kt;
       cur_a += astep;
       rem_a -= astep;
@@ -533,7 +558,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
         });
       };
 
-      for (int t = 0; t < nk; ++t, ++pos) {
+      for (int t = 0; t < ct.nk; ++t, ++pos) {
         const int s = pos & 1;
         ktile(s);
         dma_advance();

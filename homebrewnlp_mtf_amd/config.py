@@ -94,6 +94,8 @@ _DEFAULTS: typing.Dict[str, typing.Any] = dict(
     tp_layout="heads",           # "heads": the reference layout (intermediate replicated over TP); "intermediate":
                                  # feed-forward weights split over the intermediate axis (layers.feed_forward)
     attention_scale="sequence",  # "sequence" (reference quirk A1, spatial.py:60) or "head" (1/sqrt(fph))
+    shared_key_value_mixing=True,  # shared_key_value attention mixes the keys (P K); False: the reference's
+                                   # rowsum(P) * key (quirk A19, spatial.py:63-64,81 -- no mixing, docs/PARITY.md)
     seed=0,                      # parameter-init seed
     grad_bucket_mb=64,           # DP gradient all-reduce bucket size (xGMI ring per-link bound: SURVEY 5.8)
     allreduce_dtype="float32",   # dtype gradients travel in over RCCL

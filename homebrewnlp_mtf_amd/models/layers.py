@@ -672,7 +672,8 @@ def attention(args: BlockArgs) -> Act:
         #   scale_attention_map  -> multiplicative map on the probabilities (attn_map kernels)
         #   biased_attention_map -> (P + Bm) V = P V + Bm V: the learned token mixer (K03) on the same values
         # positional-only keys ([seq, heads, fph]) are broadcast over the batch
-        fold = _fold_of(p, x.dims, dim) if FLASH_MAPS else None
+        quirk_a19 = 'shared_key_value' in args and not p.shared_key_value_mixing
+        fold = _fold_of(p, x.dims, dim) if FLASH_MAPS and not quirk_a19 else None
         kdims_pos = [dim] + list(x.dims[-2:])   # positional-only keys: [attention dim, heads, fph]
         if fold is not None and qry.dims == x.dims and (key.dims == x.dims or key.dims == kdims_pos):
             # maps created in the order of the generic path below (variable scopes / checkpoint names)
@@ -700,10 +701,12 @@ def attention(args: BlockArgs) -> Act:
         logit = named_einsum([qry, anonymize(key, dim)], logit_dims)
         if 'shared_key_value' in args:
             # V = K attention. The reference keeps the key un-anonymised here (spatial.py:63-64 + :81), so its final
-            # einsum does not contract over keys and yields rowsum(logit) * key_q -- no mixing at all (quirk A19,
-            # fixed: docs/PARITY.md); the flash route above and this path agree on the fixed semantics
-            val = anonymize(key, dim) if key.dims == x.dims else anonymize(
-                Act(key.t.unsqueeze(0).expand(x.dims[0].size, *key.t.shape), x.dims), dim)
+            # einsum does not contract over keys and yields rowsum(logit) * key_q -- no mixing at all (quirk A19).
+            # Fixed by default (shared_key_value_mixing, docs/PARITY.md; the flash route above agrees); with the
+            # switch off the reference's einsum is reproduced for checkpoints trained with it
+            full = key if key.dims == x.dims else Act(key.t.unsqueeze(0).expand(x.dims[0].size, *key.t.shape),
+                                                      x.dims)
+            val = anonymize(full, dim) if p.shared_key_value_mixing else full
     if 'biased_softmax' in args:
         bias, mask = _masked_map(args)
         b = _apply_mask(bias, mask, dim, tmp)

@@ -670,6 +670,16 @@ def attention_core(q, k, v, scale: float, causal: bool):
     return _AttnCore.apply(q, k, v, scale, causal)
 
 
+_MAP_WS = {}
+
+
+def _map_workspace(device, numel: int) -> torch.Tensor:
+    ws = _MAP_WS.get(device)
+    if ws is None or ws.numel() < numel:
+        ws = _MAP_WS[device] = torch.empty(numel, dtype=torch.float32, device=device)
+    return ws[:numel]
+
+
 class _AttnMap(torch.autograd.Function):
     """flash attention with per-head [H, S, S] maps (raw.attn_map_*): bias added to the scaled logits, cmap
     multiplied into the softmax probabilities; either may be None. No [B, H, S, S] tensor is formed on the GPU."""
@@ -704,8 +714,14 @@ class _AttnMap(torch.autograd.Function):
         if raw.on_gpu(q) and (need_b or need_c):
             bs = raw.attn_map_bsplit(B, S, H)
             if bs > 1:
-                pb = torch.zeros(bs, H, S, S, dtype=torch.float32, device=q.device) if need_b else None
-                pc = torch.zeros(bs, H, S, S, dtype=torch.float32, device=q.device) if need_c else None
+                # the per-batch-slice partial map gradients live in one cached workspace (reused by every layer's
+                # backward, stream-ordered; ~1 GiB per map at S 2048 H 16 bsplit 4 was allocated per call)
+                n = bs * H * S * S
+                ws = _map_workspace(q.device, n * (int(need_b) + int(need_c)))
+                ws.zero_()
+                parts = iter(ws.split(n))
+                pb = next(parts).view(bs, H, S, S) if need_b else None
+                pc = next(parts).view(bs, H, S, S) if need_c else None
         raw.attn_map_bwd(q, k, v, o, do.contiguous(), lse, delta, dq, dk, dv, b32, c32, db, dc, B, S, H, D, scale,
                          causal, pb, pc)
         return (dq, dk, dv, db.to(bdt) if db is not None else None, dc.to(cdt) if dc is not None else None,

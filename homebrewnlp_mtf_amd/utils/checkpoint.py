@@ -76,8 +76,22 @@ def _slot_tp_dim(slot_key: str, var_tp: typing.Optional[int], slot_shape, var_sh
     if leaf.startswith("dim"):
         return (0 if int(leaf[3:]) == var_tp else None), True
     if leaf in ("af_rows", "af_cols"):
-        return None, False
+        # Adafactor factors of [rows = leading dims flattened, cols = last dim] (optim/reference.py _adafactor):
+        # the factor over the sharded axis is local, the other one is the TP-reduced (replicated) statistic
+        last = len(var_shape) - 1
+        if leaf == "af_cols":
+            return (0 if var_tp == last else None), True
+        # af_rows: replicated when the last dim is sharded; else sharded along var_tp of the rows' unflattened view
+        # [leading dims] (a sharded middle dim interleaves the local rows: re-sliced through that view, _TP_VIEW)
+        return (None, True) if var_tp == last else (var_tp, True)
     return None, True      # scalars (TP-summed statistics) are replicated
+
+
+def _tp_view(slot_key: str, var_tp, var_shape):
+    """the unflattened local shape a flattened sharded slot is re-sliced in (Adafactor row factors), or None"""
+    if var_tp is not None and slot_key.rsplit("/", 1)[-1] == "af_rows" and var_tp != len(var_shape) - 1:
+        return [int(d) for d in var_shape[:-1]]
+    return None
 
 
 def _named_tensors(trainer) -> typing.Dict[str, typing.Tuple[torch.Tensor, dict]]:
@@ -95,11 +109,16 @@ def _named_tensors(trainer) -> typing.Dict[str, typing.Tuple[torch.Tensor, dict]
         var = key.split("/" + trainer.params.optimizer.replace(":", "_") + "/", 1)[0]
         s = store.specs[var]
         tp_dim, ok = _slot_tp_dim(key, s.tp_dim, t.shape, s.local_shape)
+        view = _tp_view(key, s.tp_dim, s.local_shape)
         glob = list(t.shape)
-        if tp_dim is not None:
+        if view is not None:
+            glob = [int(t.numel()) * tp]
+        elif tp_dim is not None:
             glob[tp_dim] *= tp
-        out[key] = (t, {"kind": "slot", "shape": list(t.shape), "global_shape": glob, "tp_dim": tp_dim,
-                        "resliceable": ok})
+        meta = {"kind": "slot", "shape": list(t.shape), "global_shape": glob, "tp_dim": tp_dim, "resliceable": ok}
+        if view is not None:
+            meta["tp_view"] = view
+        out[key] = (t, meta)
     return out
 
 
@@ -206,9 +225,12 @@ def restore(trainer, path: str, strict: bool = True) -> typing.Tuple[int, typing
             info = index0[n]
             if not info["resliceable"]:
                 raise ValueError(f"{n} cannot be re-sliced from TP={old_tp} to TP={mesh.tp}")
-            full = torch.cat([p[n] for p in parts], info["tp_dim"])
+            view = info.get("tp_view")
+            full = torch.cat([p[n].view(view) if view else p[n] for p in parts], info["tp_dim"])
             k = full.shape[info["tp_dim"]] // mesh.tp
             loaded[n] = full.narrow(info["tp_dim"], mesh.tp_rank * k, k).contiguous()
+            if view:
+                loaded[n] = loaded[n].reshape(-1)
     lazy = {}
     with torch.no_grad():
         for n in wanted:

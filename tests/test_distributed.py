@@ -244,3 +244,41 @@ def test_dp_bf16_wire_close_to_fp32_wire():
     assert 0 < rel < 2e-2, f"bf16 wire moved the update by {rel:.3g} relative"
     for a, b in zip(fp[0]["losses"], bf[0]["losses"]):
         assert abs(a - b) < 1e-3 * abs(a)
+
+
+def _ckpt_worker(rank, world, port, cfg, out_dir):
+    from homebrewnlp_mtf_amd.utils import checkpoint
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+    mesh = pstate.Mesh(dp=1, tp=world, rank=rank).build_groups()
+    tr = Trainer(ModelParameter(dict(cfg, mesh={"dp": 1, "tp": world})), "cpu", mesh)
+    for _ in range(2):
+        tr.step(_batch(cfg))
+    checkpoint.save(tr, out_dir, 2)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_adafactor_checkpoint_tp2_restores_at_tp1(tmp_path):
+    """an Adafactor run saved at TP2 restores at TP1 (the factor over the sharded axis re-sliced, the TP-reduced one
+    replicated) and continues like the single-rank run"""
+    from homebrewnlp_mtf_amd.utils import checkpoint
+    cfg = dict(CFG, optimizer="adafactor-learning_rate")
+    mp.spawn(_ckpt_worker, args=(2, _free_port(), cfg, str(tmp_path)), nprocs=2, join=True)
+    ref, _ = _single(cfg)                      # two steps at TP1
+    pstate.set_mesh(pstate.Mesh())
+    torch.manual_seed(0)
+    tr = Trainer(ModelParameter(dict(cfg)), "cpu")
+    path = checkpoint.latest(str(tmp_path)) if hasattr(checkpoint, "latest") else None
+    if path is None:
+        path = os.path.join(str(tmp_path), sorted(d for d in os.listdir(tmp_path) if not d.endswith(".tmp")
+                                                  and os.path.isdir(os.path.join(tmp_path, d)))[-1])
+    step, _ = checkpoint.restore(tr, path)
+    assert step == 2
+    assert (tr.store.master - ref.store.master).abs().max().item() < 2e-5
+    b = _batch(cfg)
+    l_ref = float(ref.step(b)["loss"])
+    l_new = float(tr.step(b)["loss"])
+    assert abs(l_ref - l_new) < 1e-4 * abs(l_ref)
+    assert (tr.store.master - ref.store.master).abs().max().item() < 5e-5

@@ -568,9 +568,12 @@ def test_token_mixer_big_tiles(cuda, causal):
     w = (torch.randn(H, S, S) * 0.05).to(BF)
     dy = (torch.randn(B, S, H, Fd) * 0.5).to(BF)
     xg, wg = x.to(cuda).requires_grad_(True), w.to(cuda).requires_grad_(True)
+    c0 = g4w_calls()
     y = F.token_mixer(xg, wg, causal)
     y.backward(dy.to(cuda))
     torch.cuda.synchronize()
+    # y = tril(W) x and dx = tril(W)^T dy on gemm4w (per-tile K ranges); dW (split contraction index) elsewhere
+    assert g4w_calls() - c0 == 2
     xf, wf = x.float().requires_grad_(True), w.float().requires_grad_(True)
     wm = torch.tril(wf) if causal else wf
     ref = torch.einsum("hst,bthf->bshf", wm, xf)

@@ -577,3 +577,34 @@ def test_three_axes_attention_routing_matches_generic_path(layers, monkeypatch):
     assert res[True][2] == res[False][2]
     assert abs(res[True][0] - res[False][0]) < 1e-6 * max(1.0, abs(res[False][0]))
     assert torch.allclose(res[True][1], res[False][1], atol=1e-6, rtol=1e-5)
+
+
+@pytest.mark.parametrize("mixing", [True, False])
+def test_shared_key_value_modes(mixing, monkeypatch):
+    """quirk A19 behind ``shared_key_value_mixing``: True (default) mixes the keys, False reproduces the reference's
+    rowsum(P) * key. Each mode gives the same loss / gradients with and without the flash routing (fp64), and the
+    two modes differ."""
+    from homebrewnlp_mtf_amd.models import layers as LY
+    layer = "attention-biased_softmax-dot_product-embedded-absolute-shared_key_value"
+    res = {}
+    for mode in (mixing, not mixing):
+        for flash in (True, False):
+            monkeypatch.setattr(LY, "FLASH_MAPS", flash)
+            torch.manual_seed(0)
+            cfg = dict(BASE, calculation_dtype="float64", shared_key_value_mixing=mode,
+                       block_config=[{"layer": [layer], "skip": True}])
+            m = Model(ModelParameter(cfg), "cpu")
+            st = m.store
+            st.master = st.master.double()
+            st.grad = st.grad.double()
+            st.compute = st.master
+            st._leaves = {}
+            st.master.copy_(torch.randn_like(st.master) * 0.3)
+            x = torch.randint(0, 50, (2, 8, 1), generator=torch.Generator().manual_seed(1))
+            out = m(x, x)
+            out["loss"].backward()
+            st.fold_leaf_grads()
+            res[(mode, flash)] = (float(out["loss"].detach()), st.grad.clone())
+    a, b = res[(mixing, True)], res[(mixing, False)]
+    assert abs(a[0] - b[0]) < 1e-6 and torch.allclose(a[1], b[1], atol=1e-6, rtol=1e-5)
+    assert abs(res[(True, False)][0] - res[(False, False)][0]) > 1e-6

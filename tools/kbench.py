@@ -100,6 +100,34 @@ def bench_gemm(T: int, reps: int):
         del A, B, C
 
 
+def bench_mixer(reps: int):
+    """the learned token mixer's GEMMs (K03, ctx32_mixer: 32 x 2048 tokens, 8 heads x 256): y = tril(W) x
+    (tri 1) and dx = tril(W)^T dy (tri 2) on gemm4w against the persistent phase kernel (OBST_GEMM_4W=0 path);
+    effective TF/s count only the causal half"""
+    import ctypes
+    from homebrewnlp_mtf_amd.ops import _lib as L
+    B, S, H, Fd = 32, 2048, 8, 256
+    dev = torch.device("cuda")
+    x = (torch.randn(B * S * H * Fd, device=dev) * 0.5).to(BF)
+    w = torch.tril((torch.randn(H, S, S, device=dev) * 0.05)).to(BF).reshape(-1)
+    y = torch.empty_like(x)
+    hf = H * Fd
+    fl = B * H * S * S * Fd   # 2 * S * S / 2 per (batch, head, feature)
+    for name, a_t, tri in (("mixer y=tril(W)x", 0, 1), ("mixer dx=tril(W)^T dy", 1, 2)):
+        def run():
+            raw.gemm(raw.Operand(w, a_t, S, 0, S * S), raw.Operand(x, 1, hf, S * hf, Fd),
+                     raw.Operand(y, 0, hf, S * hf, Fd), S, Fd, S, batch=(B, H), tri=tri)
+        t = {}
+        for rnd in range(2):
+            for on in (0, 1):
+                old = L.lib().obst_gemm4w_set(on)
+                t[on] = min(t.get(on, 1e30), timed(run, reps))
+                L.lib().obst_gemm4w_set(old)
+        emit(kernel="gemm", shape=name, us_phase=round(t[0], 1), us_gemm4w=round(t[1], 1),
+             tflops_phase=round(fl / t[0] / 1e6, 1), tflops_gemm4w=round(fl / t[1] / 1e6, 1),
+             gemm4w_over_phase=round(t[0] / t[1], 3))
+
+
 def _qkv(B, S, H, D, dev):
     ld = 3 * H * D
     buf = (torch.randn(B * S * ld, device=dev) * 0.5).to(BF)
@@ -184,17 +212,19 @@ def bench_ew(T: int, reps: int):
 
 def main(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", nargs="?", default="all", choices=["gemm", "attn", "attn_map", "norm", "ew", "all"])
+    ap.add_argument("what", nargs="?", default="all", choices=["gemm", "mixer", "attn", "attn_map", "norm", "ew", "all"])
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--tokens", type=int, default=131072, help="tokens per step (GPT-Neo-1.3B: 64 x 2048)")
     ap.add_argument("--batch", type=int, default=64, help="attention batch at S 2048")
     ap.add_argument("--check", default=None, help="floor file: fail on a regression past --tol")
     ap.add_argument("--tol", type=float, default=0.05)
     a = ap.parse_args(argv)
-    todo = ["gemm", "attn", "attn_map", "norm", "ew"] if a.what == "all" else [a.what]
+    todo = ["gemm", "mixer", "attn", "attn_map", "norm", "ew"] if a.what == "all" else [a.what]
     for w in todo:
         if w == "gemm":
             bench_gemm(a.tokens, a.reps)
+        elif w == "mixer":
+            bench_mixer(a.reps)
         elif w == "attn":
             bench_attn(a.batch, a.reps)
         elif w == "attn_map":

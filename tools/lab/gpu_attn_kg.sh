@@ -5,5 +5,5 @@ for kg in 2; do
   tail -1 gpurun_out/kg_test$kg.log
 done
 for kg in 1 2 1 2; do
-  echo "KG=$kg"; OBST_ATTN_DKV_KG=$kg B=64 timeout -k 10 120 python -u tools/bench_attn.py 2>&1 | grep attn || exit 1
+  echo "KG=$kg"; OBST_ATTN_DKV_KG=$kg B=64 timeout -k 10 120 python -u tools/lab/bench_attn.py 2>&1 | grep attn || exit 1
 done

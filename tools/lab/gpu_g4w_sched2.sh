@@ -16,3 +16,5 @@ for P in "$P1" "$P2"; do
   G4W_ONLY=1,2 SKIP_CHECK=1 timeout -s KILL 90 rocprofv3 --pmc $P -d $R/gpurun_out/g4w/p$i -o run --output-format csv -- $R/bin/g4w_sched 1 2 "fwd d->2d" > $R/gpurun_out/g4w/p$i.log 2>&1 || { echo "pmc pass $i failed"; tail -3 $R/gpurun_out/g4w/p$i.log; exit 1; }
 done
 python3 $R/tools/pmc_summary.py $R/gpurun_out/g4w > $R/gpurun_out/g4w/pmc.txt && cat $R/gpurun_out/g4w/pmc.txt
+cd $R && timeout -k 10 300 python -u tools/kbench.py mixer > $R/gpurun_out/g4w/mixer.txt 2>&1 && cat $R/gpurun_out/g4w/mixer.txt
+timeout -k 10 600 python -u -m pytest tests/test_gpu_kernels.py -x -q --timeout 120 --timeout-method thread -k "gemm or mixer" > $R/gpurun_out/g4w/tests.txt 2>&1; tail -3 $R/gpurun_out/g4w/tests.txt

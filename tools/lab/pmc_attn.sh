@@ -13,7 +13,7 @@ i=0
 for P in "$P1" "$P2"; do
   i=$((i+1))
   timeout -k 10 180 rocprofv3 --kernel-trace --pmc $P --output-format csv -d $ROOT/gpurun_out/pmc_attn/p$i \
-    --kernel-include-regex "${KREGEX:-attn_}" -- python3 $ROOT/tools/bench_attn.py > $ROOT/gpurun_out/pmc_attn/p$i.log 2>&1 \
+    --kernel-include-regex "${KREGEX:-attn_}" -- python3 $ROOT/tools/lab/bench_attn.py > $ROOT/gpurun_out/pmc_attn/p$i.log 2>&1 \
     || { echo "pass $i failed"; tail -20 $ROOT/gpurun_out/pmc_attn/p$i.log; exit 1; }
 done
 python3 $ROOT/tools/pmc_summary.py $ROOT/gpurun_out/pmc_attn > $ROOT/gpurun_out/pmc_attn/summary.txt

@@ -1,6 +1,6 @@
 #!/bin/bash
 # PMC counters (two passes, kernel trace only) of the kernels matching KREGEX while running a python tool:
-#   TAG=name KREGEX=regex pmc_cmd.sh tools/bench_norm.py [args]
+#   TAG=name KREGEX=regex pmc_cmd.sh tools/lab/bench_norm.py [args]
 set -o pipefail
 cd "$(dirname "$0")/../.."
 export HSA_ENABLE_IPC_MODE_LEGACY=0

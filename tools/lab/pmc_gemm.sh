@@ -13,7 +13,7 @@ i=0
 for P in "$P1" "$P2"; do
   i=$((i+1))
   timeout -k 10 120 rocprofv3 --kernel-trace --pmc $P --output-format csv -d $ROOT/gpurun_out/pmc_$TAG/p$i \
-    --kernel-include-regex "${KREGEX:-gemm|Cijk}" -- python3 $ROOT/tools/gemm_one.py "$@" > $ROOT/gpurun_out/pmc_$TAG/p$i.log 2>&1 \
+    --kernel-include-regex "${KREGEX:-gemm|Cijk}" -- python3 $ROOT/tools/lab/gemm_one.py "$@" > $ROOT/gpurun_out/pmc_$TAG/p$i.log 2>&1 \
     || { echo "pass $i failed"; tail -20 $ROOT/gpurun_out/pmc_$TAG/p$i.log; exit 1; }
 done
 python3 $ROOT/tools/pmc_summary.py $ROOT/gpurun_out/pmc_$TAG > $ROOT/gpurun_out/pmc_$TAG/summary.txt
