@@ -338,10 +338,22 @@ constexpr int idx(const int (&a)[8], int q) {
 #define G4W_CPB 0
 #endif
 
+#ifndef G4W_OPT
+#define G4W_OPT 0
+#endif
+// OPT bits (schedule options under A/B, tools/lab/g4w_sched.cpp):
+//   1 RELAX: the first K-tile of every tile is a separate (peeled) copy whose waits count the previous tile's
+//     direct-epilogue stores out (S = 32 bf16 / 64 fp32 stores per wave) instead of waiting for their write
+//     acknowledgements; the prologue issues S stores to an empty buffer resource (dropped by the hardware, but
+//     counted) so the first tile's first K-tile sees the same queue, and every epilogue that issues a different
+//     number of stores (edge tiles, activations, residuals, the LDS path) drains vmcnt at its end
+//   2 STAGGER: blocks start (slot & 7) / 8 of a tile apart (s_sleep), so the CUs' epilogue store bursts do not
+//     coincide on the fabric
 template <int A_T, int B_T, bool OUT_F32, bool PROF, int NWV = 4, int SCH = G4W_SCH, bool STG = (G4W_STG != 0),
-          int CPA = G4W_CPA, int CPB = G4W_CPB>
+          int CPA = G4W_CPA, int CPB = G4W_CPB, int OPT = G4W_OPT>
 __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
   extern __shared__ __attribute__((aligned(1024))) char smem[];
+  constexpr bool RELAX = (OPT & 1) != 0, STAGGER = (OPT & 2) != 0;
   static_assert(SCH == 0 || NWV == 4, "the split schedule is laid out for one wave per SIMD");
   constexpr int WN = NWV == 4 ? 128 : 64;    // output columns per wave
   constexpr int JB = WN / 16;                // B fragments per substep
@@ -352,6 +364,9 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
   constexpr int QA0 = NWV == 4 ? 26 : 15, QB0 = NWV == 4 ? 66 : 31, DQ = NWV == 4 ? 5 : 4;   // DMA slots
   constexpr int QW = NWV == 4 ? 107 : 50;    // barrier 2
   constexpr int VA = SCH == 2 ? 24 : g4s::VA, VB = SCH == 2 ? 16 : g4s::VB;   // pieces younger than the awaited
+  constexpr int SE = RELAX ? (OUT_F32 ? 64 : 32) : 0;   // stores of a plain direct epilogue per wave (RELAX)
+  constexpr int VAF = VA + SE > 63 ? 63 : VA + SE, VBF = VB + SE > 63 ? 63 : VB + SE;
+  constexpr int V0F = 2 * PPW + SE > 63 ? 63 : 2 * PPW + SE;
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = NWV == 4 ? wave >> 1 : wave & 1, wn = NWV == 4 ? wave & 1 : wave >> 1;
 
@@ -366,6 +381,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
   const long long first = cyc ? blockIdx.x : slot;
   const long long stride = cyc ? gridDim.x : nslot;
   const int ntiles = (int)(len > first ? (len - first + stride - 1) / stride : 0);   // tiles of this block
+  if (ntiles == 0) return;   // (a small launch: the grid is rounded up to the 8 XCDs)
   auto logical = [&](int r) { return start + first + (long long)r * stride; };
   const long long astep = A_T == 0 ? 128 : 128 * p.lda;
   const long long bstep = B_T == 0 ? 128 : 128 * p.ldb;
@@ -457,6 +473,9 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
   // that meet only after the last tile (a branch per K-tile put a phi over the 256 accumulators: spills)
   auto body = [&](auto shc) {
     constexpr int SH = decltype(shc)::value;
+    if constexpr (STAGGER) {   // ~1/8 of a 2048-deep tile per slot step
+      for (int d = 0; d < 3 * (slot & 7); ++d) __builtin_amdgcn_s_sleep(64);
+    }
     // prologue: positions 0 and 1 into stages 0 and 1, wait for position 0, read its substep-0 fragments
     dma_setup();
   #pragma unroll
@@ -470,7 +489,15 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
   #pragma unroll
     for (int q = 0; q < PPW; ++q) dma16<CPB>(rb, vob[q], stage_b(1) + q * 1024);
     dma_advance();
-    vm_wait<2 * PPW>();
+    if constexpr (RELAX) {   // SE stores into an empty resource: dropped, but counted like an epilogue's
+      const i32x4_t nul = make_rsrc(p.C, 0);
+      static_for<SE>([&](auto) {
+        store16_padded(v4u32_t{0u, 0u, 0u, 0u}, 0, nul, 0, std::integral_constant<int, 0>{});
+      });
+      vm_wait<V0F>();
+    } else {
+      vm_wait<2 * PPW>();
+    }
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_s_waitcnt(0xc07f);   // nothing (kernel-argument loads) pending in lgkmcnt at the loop entry
     if (stamp) p.stamps[sbase + 1] = __builtin_amdgcn_s_memtime();
@@ -496,7 +523,8 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
       // tile the previous tile's epilogue stores sit in between, so the same count also waits for the older stores
       // -- issued ~60 MFMAs earlier, they have retired by then; a relaxed count for that K-tile needs a runtime
       // branch at every wait or a second copy of the K-tile, and the copy's phi over the 256 accumulators spills.
-      auto ktile = [&](int s) {
+      auto ktile = [&](auto fc, int s) {
+        constexpr bool FIRST = decltype(fc)::value && RELAX;
         const unsigned sa = stage_a(s), sb = stage_b(s);
         static_for<QS>([&](auto qc) {
           constexpr int q = decltype(qc)::value;
@@ -521,7 +549,8 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
               // this iteration's; count them out instead of waiting for every store (direct epilogue: 32 bf16 /
               // 64 fp32)
               if constexpr (PROF) tw = __builtin_amdgcn_s_memtime();
-              vm_wait<2 * PPW>();
+              if constexpr (FIRST) vm_wait<V0F>();
+              else vm_wait<2 * PPW>();
               if constexpr (!(G4W_EXP & 4)) __builtin_amdgcn_s_barrier();
               if constexpr (PROF) sync2 += __builtin_amdgcn_s_memtime() - tw;
             }
@@ -547,7 +576,8 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
             if constexpr (db >= 0) dma16o<CPB, (db < 0 ? 0 : db) * 1024>(rb, vob[db], sb);
             if constexpr (q == g4s::WA || q == g4s::WB) {   // A / B image of position pos+1 landed in stage s^1
               if constexpr (PROF) tw = __builtin_amdgcn_s_memtime();
-              vm_wait<q == g4s::WA ? VA : VB>();
+              if constexpr (FIRST) vm_wait<q == g4s::WA ? VAF : VBF>();
+              else vm_wait<q == g4s::WA ? VA : VB>();
               __builtin_amdgcn_s_barrier();
               if constexpr (PROF) sync2 += __builtin_amdgcn_s_memtime() - tw;
             }
@@ -558,10 +588,19 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
         });
       };
 
-      for (int t = 0; t < ct.nk; ++t, ++pos) {
-        const int s = pos & 1;
-        ktile(s);
+      if constexpr (RELAX) {   // the first K-tile peeled (sequential copies: no phi over the accumulators)
+        ktile(std::true_type{}, pos & 1);
         dma_advance();
+        ++pos;
+        for (int t = 1; t < ct.nk; ++t, ++pos) {
+          ktile(std::false_type{}, pos & 1);
+          dma_advance();
+        }
+      } else {
+        for (int t = 0; t < ct.nk; ++t, ++pos) {
+          ktile(std::false_type{}, pos & 1);
+          dma_advance();
+        }
       }
       // last MFMA -> accumulator reads: the pad redefines every accumulator ("+a"), so the register allocator's
       // AGPR -> VGPR copies for the epilogue (which fences do not bind) can only read them after it
@@ -595,6 +634,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
         const __amdgpu_buffer_rsrc_t rr = make_brsrc(p.R ? reinterpret_cast<const char*>(p.R) + ct.coff * ES + corg : cbase, cext);
         const int ml = lane & 15, gq = lane >> 4;
         const float alpha = p.alpha, beta = ws_out ? 0.f : p.beta;
+
         const bool edge = ct.n0 + wn * WN + WN > p.N;
         const bool extra = (OUT_F32 && beta != 0.f) || (p.R != nullptr && !ws_out);
         // fragment pair (2p, 2p+1) = 8 consecutive columns per lane (frag_b): 16 B (bf16) / 2 x 16 B (fp32) stores,
@@ -684,7 +724,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
           // loads into VGPRs pending at the loop back edge make the compiler's wait model drain vmcnt (the in-flight
           // LDS-DMAs of the next tile included) at the top of every K-tile: retire them on this path. (Stores
           // skipped past N on an edge tile only shorten the queue the K loop's counted waits were derived for.)
-          if constexpr (EX || AC == 2) __builtin_amdgcn_s_waitcnt(0x0f70);
+          if constexpr (EX || AC == 2 || (RELAX && (ED || AC != 0))) __builtin_amdgcn_s_waitcnt(0x0f70);
         };
         using T_ = std::true_type;
         using F_ = std::false_type;

@@ -48,7 +48,7 @@ __global__ void fill_kernel(uint16_t* p, size_t n, uint32_t seed) {
   }
 }
 
-template <int A_T, int B_T, bool F32, int SCH, bool STG, int CPA, int CPB, bool PROF = false>
+template <int A_T, int B_T, bool F32, int SCH, bool STG, int CPA, int CPB, int OPT, bool PROF = false>
 hipError_t launch_v(GemmArgs a, hipStream_t st) {
   a.tiles_m = (a.M + 255) / 256;
   a.tiles_n = (a.N + 255) / 256;
@@ -56,7 +56,7 @@ hipError_t launch_v(GemmArgs a, hipStream_t st) {
   const long long tiles = (long long)a.tiles_m * a.tiles_n * a.nbatch;
   const int grid = (int)(tiles >= 256 ? 256 : ((tiles + 7) / 8) * 8);
   const size_t lds = 2 * Q_STAGE + 32768;
-  auto k = gemm4w_kernel<A_T, B_T, F32, PROF, 4, SCH, STG, CPA, CPB>;
+  auto k = gemm4w_kernel<A_T, B_T, F32, PROF, 4, SCH, STG, CPA, CPB, OPT>;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -76,17 +76,17 @@ struct Variant {
   Launch l00b, l01b, l00b_prof;
 };
 
-#define V(NAME, SCH, STG, CPA, CPB)                                                                  \
+#define V(NAME, SCH, STG, CPA, CPB, OPT)                                                             \
   Variant {                                                                                          \
-    NAME, launch_v<0, 0, false, SCH, STG, CPA, CPB>, launch_v<0, 1, false, SCH, STG, CPA, CPB>,     \
-        launch_v<0, 0, false, SCH, STG, CPA, CPB, true>                                              \
+    NAME, launch_v<0, 0, false, SCH, STG, CPA, CPB, OPT>, launch_v<0, 1, false, SCH, STG, CPA, CPB, OPT>, \
+        launch_v<0, 0, false, SCH, STG, CPA, CPB, OPT, true>                                         \
   }
 static const Variant variants[] = {
-    V("sch0", 0, false, 0, 0),
-    V("sch1", 1, false, 0, 0),
-    V("sch2", 2, false, 0, 0),
-    V("sch1 cp31", 1, false, 3, 1),
-    V("sch2 cp31", 2, false, 3, 1),
+    V("sch0", 0, false, 3, 1, 0),
+    V("sch1", 1, false, 3, 1, 0),
+    V("sch1 relax", 1, false, 3, 1, 1),
+    V("sch1 relax stag", 1, false, 3, 1, 3),
+    V("sch0 relax", 0, false, 3, 1, 1),
 };
 constexpr int NV = sizeof(variants) / sizeof(variants[0]);
 
