@@ -119,15 +119,18 @@ __device__ __forceinline__ void dma16o(const i32x4_t& rs, int voff, unsigned sba
 __device__ __forceinline__ void mfma_acc(f32x4_t& c, const bf16x8_t& a, const bf16x8_t& b) {
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
 }
-// 16-byte buffer store of v at voff + soff + IMM with two wait states behind it. A store of more than 8 bytes
+// 16-byte buffer store of v at voff + IMM (range-checked: past num_records it is dropped) with five wait states
+// behind it. A store of more than 8 bytes
 // reads its data VGPRs after issue; the compiler pads the VALU overwrite of them only when soffset is a constant
 // (its rule exempts an SGPR soffset), and on gfx950 the unpadded SGPR-soffset stores wrote corrupted data (1 of the
-// 64 fp32 fragments per wave, measured). In asm the pad travels with the store.
+// 64 fp32 fragments per wave, measured; with two wait states 12 % of a gelu epilogue's pre-activation side output was
+// still corrupted in round 4, when the next v_cvt_pk / v_pk_mul rewrote the data VGPRs right behind the pad). In asm
+// the pad travels with the store.
 template <int IMM, typename V>
-__device__ __forceinline__ void store16_padded(const V& v, int voff, const i32x4_t& rs, int soff,
+__device__ __forceinline__ void store16_padded(const V& v, int voff, const i32x4_t& rs,
                                                std::integral_constant<int, IMM>) {
-  asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen offset:%4\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(rs),
-               "s"(soff), "n"(IMM)
+  asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen offset:%3\n\ts_nop 4" ::"v"(v), "v"(voff), "s"(rs),
+               "n"(IMM)
                : "memory");
 }
 #pragma clang diagnostic pop
@@ -326,20 +329,20 @@ constexpr int idx(const int (&a)[8], int q) {
 }  // namespace g4s
 
 #ifndef G4W_SCH
-#define G4W_SCH 0
+#define G4W_SCH 1   // the split schedule (profiles/r4_gemm_sched.md): 0.91-0.98x of hipBLASLt vs 0.89-0.93x for 0
 #endif
 #ifndef G4W_STG
 #define G4W_STG 0
 #endif
 #ifndef G4W_CPA
-#define G4W_CPA 0
+#define G4W_CPA 3   // sc0 sc1 on the A stream, sc0 on B (as the library's kernel; within 0.3 %)
 #endif
 #ifndef G4W_CPB
-#define G4W_CPB 0
+#define G4W_CPB 1
 #endif
 
 #ifndef G4W_OPT
-#define G4W_OPT 0
+#define G4W_OPT 1   // RELAX (+0.3-0.9 %)
 #endif
 // OPT bits (schedule options under A/B, tools/lab/g4w_sched.cpp):
 //   1 RELAX: the first K-tile of every tile is a separate (peeled) copy whose waits count the previous tile's
@@ -492,7 +495,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
     if constexpr (RELAX) {   // SE stores into an empty resource: dropped, but counted like an epilogue's
       const i32x4_t nul = make_rsrc(p.C, 0);
       static_for<SE>([&](auto) {
-        store16_padded(v4u32_t{0u, 0u, 0u, 0u}, 0, nul, 0, std::integral_constant<int, 0>{});
+        store16_padded(v4u32_t{0u, 0u, 0u, 0u}, 0, nul, std::integral_constant<int, 0>{});
       });
       vm_wait<V0F>();
     } else {
@@ -654,12 +657,14 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
           // bounded by the fences (unbounded, the scheduler hoisted all 64 loads: 256 VGPRs, spills)
           static_for<8>([&](auto ic) {
             constexpr int i = decltype(ic)::value;
-            const int soff = __builtin_amdgcn_readfirstlane((int)(i * 16 * ldc * ES));
+            // the fragment row goes into the VGPR offset: a raw buffer's range check covers the VGPR offset and
+            // the immediate but not soffset, so rows past M (ragged M) must be in voff to be dropped
+            const int vrow = voff + (int)(i * 16 * ldc * ES);
             f32x4_t x[8];
             if constexpr (AC == 2) {
               static_for<JB / 2>([&](auto pc) {
                 constexpr int pp = decltype(pc)::value;
-                const v4u32_t o = __builtin_amdgcn_raw_buffer_load_b128(rzi, voff, soff + pp * 64, 0);
+                const v4u32_t o = __builtin_amdgcn_raw_buffer_load_b128(rzi, vrow + pp * 64, 0, 0);
                 x[2 * pp] = f32x4_t{bf2f(o[0] & 0xffff), bf2f(o[0] >> 16), bf2f(o[1] & 0xffff), bf2f(o[1] >> 16)};
                 x[2 * pp + 1] = f32x4_t{bf2f(o[2] & 0xffff), bf2f(o[2] >> 16), bf2f(o[3] & 0xffff), bf2f(o[3] >> 16)};
               });
@@ -670,15 +675,15 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
                 if constexpr (OUT_F32) {
                   x[2 * pp] = x[2 * pp + 1] = f32x4_t{0.f, 0.f, 0.f, 0.f};
                   if (beta != 0.f) {
-                    x[2 * pp] = beta * __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rc, voff, soff + pp * 128, 0));
-                    x[2 * pp + 1] = beta * __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rc, voff, soff + pp * 128 + 16, 0));
+                    x[2 * pp] = beta * __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rc, vrow + pp * 128, 0, 0));
+                    x[2 * pp + 1] = beta * __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rc, vrow + pp * 128 + 16, 0, 0));
                   }
                   if (p.R) {
-                    x[2 * pp] += __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rr, voff, soff + pp * 128, 0));
-                    x[2 * pp + 1] += __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rr, voff, soff + pp * 128 + 16, 0));
+                    x[2 * pp] += __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rr, vrow + pp * 128, 0, 0));
+                    x[2 * pp + 1] += __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rr, vrow + pp * 128 + 16, 0, 0));
                   }
                 } else {
-                  const v4u32_t o = __builtin_amdgcn_raw_buffer_load_b128(rr, voff, soff + pp * 64, 0);
+                  const v4u32_t o = __builtin_amdgcn_raw_buffer_load_b128(rr, vrow + pp * 64, 0, 0);
                   x[2 * pp] = f32x4_t{bf2f(o[0] & 0xffff), bf2f(o[0] >> 16), bf2f(o[1] & 0xffff), bf2f(o[1] >> 16)};
                   x[2 * pp + 1] = f32x4_t{bf2f(o[2] & 0xffff), bf2f(o[2] >> 16), bf2f(o[3] & 0xffff), bf2f(o[3] >> 16)};
                 }
@@ -696,7 +701,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
                 if (zout)
                   store16_padded(v4u32_t{pack_bf16x2(va[0], va[1]), pack_bf16x2(va[2], va[3]),
                                          pack_bf16x2(vb[0], vb[1]), pack_bf16x2(vb[2], vb[3])},
-                                 voff, rz4, soff, std::integral_constant<int, pp * 64>{});
+                                 vrow, rz4, std::integral_constant<int, pp * 64>{});
   #pragma unroll
                 for (int t = 0; t < 4; ++t) {
                   va[t] = act_fwd(ACT_GELU, va[t]);
@@ -710,13 +715,13 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
                 }
               }
               if constexpr (OUT_F32) {
-                store16_padded(va, voff, rc4, soff, std::integral_constant<int, pp * 128>{});
-                store16_padded(vb, voff, rc4, soff, std::integral_constant<int, pp * 128 + 16>{});
+                store16_padded(va, vrow, rc4, std::integral_constant<int, pp * 128>{});
+                store16_padded(vb, vrow, rc4, std::integral_constant<int, pp * 128 + 16>{});
               } else {
                 // the same unpadded-hazard as the fp32 stores (garbage in ~1% of the bf16 outputs, measured)
                 store16_padded(v4u32_t{pack_bf16x2(va[0], va[1]), pack_bf16x2(va[2], va[3]), pack_bf16x2(vb[0], vb[1]),
                                        pack_bf16x2(vb[2], vb[3])},
-                               voff, rc4, soff, std::integral_constant<int, pp * 64>{});
+                               vrow, rc4, std::integral_constant<int, pp * 64>{});
               }
             });
             fence();
