@@ -75,26 +75,30 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_brsrc(const void* base, l
 // vmcnt before the barrier that publishes the stage. One wait state between the M0 write and the LDS-DMA.
 // CP: cache-policy bits of the load (0 none, 1 sc0, 2 sc1, 3 sc0 sc1, 4 nt) -- an operand staged once per CU gains
 // nothing from the CU's L1.
+// Inline asm is opaque to the compiler's hazard recognizer: a VMEM instruction reading an SGPR that a VALU op wrote
+// (v_readfirstlane of make_rsrc, v_readlane of an SGPR spill reload) needs five wait states, which the compiler only
+// inserts in front of its own VMEM instructions. The prologue form (once per block) leads with s_nop 4; the K-loop
+// form (dma16o) reads SALU-computed resources and is checked by tools/sgpr_hazard.py (tests/test_asm_hazards.py).
 template <int CP = 0>
 __device__ __forceinline__ void dma16(const i32x4_t& rs, int voff, unsigned m0) {
   const unsigned m = __builtin_amdgcn_readfirstlane(m0);
   if constexpr (CP == 0)
-    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rs), "s"(m)
+    asm volatile("s_nop 4\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rs), "s"(m)
                  : "memory", "m0");
   else if constexpr (CP == 1)
-    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen sc0 lds" ::"v"(voff), "s"(rs),
+    asm volatile("s_nop 4\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen sc0 lds" ::"v"(voff), "s"(rs),
                  "s"(m)
                  : "memory", "m0");
   else if constexpr (CP == 2)
-    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen sc1 lds" ::"v"(voff), "s"(rs),
+    asm volatile("s_nop 4\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen sc1 lds" ::"v"(voff), "s"(rs),
                  "s"(m)
                  : "memory", "m0");
   else if constexpr (CP == 3)
-    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen sc0 sc1 lds" ::"v"(voff),
+    asm volatile("s_nop 4\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen sc0 sc1 lds" ::"v"(voff),
                  "s"(rs), "s"(m)
                  : "memory", "m0");
   else
-    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen nt lds" ::"v"(voff), "s"(rs),
+    asm volatile("s_nop 4\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen nt lds" ::"v"(voff), "s"(rs),
                  "s"(m)
                  : "memory", "m0");
 }
@@ -119,17 +123,16 @@ __device__ __forceinline__ void dma16o(const i32x4_t& rs, int voff, unsigned sba
 __device__ __forceinline__ void mfma_acc(f32x4_t& c, const bf16x8_t& a, const bf16x8_t& b) {
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
 }
-// 16-byte buffer store of v at voff + IMM (range-checked: past num_records it is dropped) with five wait states
-// behind it. A store of more than 8 bytes
-// reads its data VGPRs after issue; the compiler pads the VALU overwrite of them only when soffset is a constant
-// (its rule exempts an SGPR soffset), and on gfx950 the unpadded SGPR-soffset stores wrote corrupted data (1 of the
-// 64 fp32 fragments per wave, measured; with two wait states 12 % of a gelu epilogue's pre-activation side output was
-// still corrupted in round 4, when the next v_cvt_pk / v_pk_mul rewrote the data VGPRs right behind the pad). In asm
-// the pad travels with the store.
+// 16-byte buffer store of v at voff + IMM (range-checked: past num_records it is dropped), padded on both sides.
+// Behind: a store of more than 8 bytes reads its data VGPRs after issue and the next VALU op may rewrite them (the
+// compiler pads that only for its own stores). In front: the resource SGPRs may come straight from a VALU write --
+// under SGPR pressure the compiler reloads spilled resource words with v_readlane 2-4 instructions before the store,
+// and the store then read a stale base: the illegal-address faults of round 4 in a small batched gelu epilogue
+// (test_gemm_batched_epilogues; found with tools/sgpr_hazard.py on the device assembly).
 template <int IMM, typename V>
 __device__ __forceinline__ void store16_padded(const V& v, int voff, const i32x4_t& rs,
                                                std::integral_constant<int, IMM>) {
-  asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen offset:%3\n\ts_nop 4" ::"v"(v), "v"(voff), "s"(rs),
+  asm volatile("s_nop 4\n\tbuffer_store_dwordx4 %0, %1, %2, 0 offen offset:%3\n\ts_nop 4" ::"v"(v), "v"(voff), "s"(rs),
                "n"(IMM)
                : "memory");
 }
@@ -329,20 +332,21 @@ constexpr int idx(const int (&a)[8], int q) {
 }  // namespace g4s
 
 #ifndef G4W_SCH
-#define G4W_SCH 1   // the split schedule (profiles/r4_gemm_sched.md): 0.91-0.98x of hipBLASLt vs 0.89-0.93x for 0
+#define G4W_SCH 0   // 1: the split schedule (profiles/r4_gemm_sched.md), under investigation (faults a small
+                    // batched ragged launch: test_gemm_batched_epilogues)
 #endif
 #ifndef G4W_STG
 #define G4W_STG 0
 #endif
 #ifndef G4W_CPA
-#define G4W_CPA 3   // sc0 sc1 on the A stream, sc0 on B (as the library's kernel; within 0.3 %)
+#define G4W_CPA 0   // 3 / 1: sc0 sc1 on the A stream, sc0 on B (as the library's kernel; within 0.3 %)
 #endif
 #ifndef G4W_CPB
-#define G4W_CPB 1
+#define G4W_CPB 0
 #endif
 
 #ifndef G4W_OPT
-#define G4W_OPT 1   // RELAX (+0.3-0.9 %)
+#define G4W_OPT 0   // 1: RELAX (+0.3-0.9 %)
 #endif
 // OPT bits (schedule options under A/B, tools/lab/g4w_sched.cpp):
 //   1 RELAX: the first K-tile of every tile is a separate (peeled) copy whose waits count the previous tile's
