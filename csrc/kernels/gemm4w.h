@@ -32,7 +32,8 @@
 #include <utility>
 
 // G4W_EXP (diagnostic builds of tools/gemm_bench only, never the library): bit 0 drops the K loop's LDS-DMAs, bit 1
-// its fragment reads, bit 2 its two barriers -- which resource bounds the loop (outputs are garbage)
+// its fragment reads, bit 2 its two barriers -- which resource bounds the loop (outputs are garbage); bit 3 drops the
+// direct epilogue's stores (what the epilogue costs without them)
 #ifndef G4W_EXP
 #define G4W_EXP 0
 #endif
@@ -132,6 +133,7 @@ __device__ __forceinline__ void mfma_acc(f32x4_t& c, const bf16x8_t& a, const bf
 template <int IMM, typename V>
 __device__ __forceinline__ void store16_padded(const V& v, int voff, const i32x4_t& rs,
                                                std::integral_constant<int, IMM>) {
+  if constexpr ((G4W_EXP & 8) != 0) return;   // diagnostic: an epilogue without its stores
   asm volatile("s_nop 4\n\tbuffer_store_dwordx4 %0, %1, %2, 0 offen offset:%3\n\ts_nop 4" ::"v"(v), "v"(voff), "s"(rs),
                "n"(IMM)
                : "memory");
@@ -332,8 +334,7 @@ constexpr int idx(const int (&a)[8], int q) {
 }  // namespace g4s
 
 #ifndef G4W_SCH
-#define G4W_SCH 0   // 1: the split schedule (profiles/r4_gemm_sched.md), under investigation (faults a small
-                    // batched ragged launch: test_gemm_batched_epilogues)
+#define G4W_SCH 1   // the split schedule (profiles/r4_gemm_sched.md): 1-5 % over SCH 0 on every measured shape
 #endif
 #ifndef G4W_STG
 #define G4W_STG 0
@@ -346,7 +347,7 @@ constexpr int idx(const int (&a)[8], int q) {
 #endif
 
 #ifndef G4W_OPT
-#define G4W_OPT 0   // 1: RELAX (+0.3-0.9 %)
+#define G4W_OPT 0   // 1: RELAX, 4: LATE -- both within +-1 % of plain SCH 1 (profiles/r4_gemm_sched.md)
 #endif
 // OPT bits (schedule options under A/B, tools/lab/g4w_sched.cpp):
 //   1 RELAX: the first K-tile of every tile is a separate (peeled) copy whose waits count the previous tile's
@@ -360,7 +361,8 @@ template <int A_T, int B_T, bool OUT_F32, bool PROF, int NWV = 4, int SCH = G4W_
           int CPA = G4W_CPA, int CPB = G4W_CPB, int OPT = G4W_OPT>
 __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
   extern __shared__ __attribute__((aligned(1024))) char smem[];
-  constexpr bool RELAX = (OPT & 1) != 0, STAGGER = (OPT & 2) != 0;
+  constexpr bool RELAX = (OPT & 1) != 0, STAGGER = (OPT & 2) != 0, LATE = (OPT & 4) != 0;
+  static_assert(!(RELAX && LATE), "RELAX peels the first K-tile, LATE the last: not both");
   static_assert(SCH == 0 || NWV == 4, "the split schedule is laid out for one wave per SIMD");
   constexpr int WN = NWV == 4 ? 128 : 64;    // output columns per wave
   constexpr int JB = WN / 16;                // B fragments per substep
@@ -468,7 +470,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
   // loop clocks, summed epilogue clocks], the XCC id, [start, end] in 100 MHz real time, tiles
   const bool stamp = p.stamps != nullptr && tid == 0;
   const long long sbase = (long long)blockIdx.x * 8;
-  unsigned long long loop_clk = 0, epi_clk = 0, tmark = 0, sync1 = 0, sync2 = 0, tw = 0;
+  unsigned long long loop_clk = 0, epi_clk = 0, tmark = 0, sync1 = 0, sync2 = 0, tw = 0, epi_issue = 0;
   if (stamp) {
     p.stamps[sbase] = __builtin_amdgcn_s_memtime();
     p.stamps[sbase + 4] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11));   // HW_REG_XCC_ID[3:0]
@@ -509,7 +511,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
     __builtin_amdgcn_s_waitcnt(0xc07f);   // nothing (kernel-argument loads) pending in lgkmcnt at the loop entry
     if (stamp) p.stamps[sbase + 1] = __builtin_amdgcn_s_memtime();
     fence();
-    static_for<NR>([&](auto rc) { read_sub(0, K0{}, rc, a0, b0); fence(); });   // same order as in the loop
+    if constexpr (!LATE) static_for<NR>([&](auto rc) { read_sub(0, K0{}, rc, a0, b0); fence(); });   // loop order
 
     int pos = 0;   // flat position of the K-tile being multiplied (its stage is pos & 1)
     for (int rnd = 0; rnd < ntiles; ++rnd) {
@@ -523,6 +525,9 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
       static_for<8 * JB>([&](auto c) { agpr_opaque(acc[decltype(c)::value / JB][decltype(c)::value % JB]); });
       asm volatile("s_nop 4" ::: "memory");
       fence();
+      // LATE: this tile's first substep-0 fragments are read here, not by the previous tile's last K-tile (whose
+      // 64 fragment VGPRs then stayed live through the epilogue: spills, and each reload waited on vmcnt)
+      if constexpr (LATE) static_for<NR>([&](auto rc) { read_sub(pos & 1, K0{}, rc, a0, b0); fence(); });
       if (stamp) tmark = __builtin_amdgcn_s_memtime();
 
       // one K-tile (position pos in stage s), its event stream shifted by SH slots (the stagger)
@@ -530,8 +535,9 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
       // tile the previous tile's epilogue stores sit in between, so the same count also waits for the older stores
       // -- issued ~60 MFMAs earlier, they have retired by then; a relaxed count for that K-tile needs a runtime
       // branch at every wait or a second copy of the K-tile, and the copy's phi over the 256 accumulators spills.
-      auto ktile = [&](auto fc, int s) {
+      auto ktile = [&](auto fc, auto lc, int s) {
         constexpr bool FIRST = decltype(fc)::value && RELAX;
+        constexpr bool NEXT0 = !(decltype(lc)::value && LATE);   // read pos+1's substep-0 fragments in this K-tile
         const unsigned sa = stage_a(s), sb = stage_b(s);
         static_for<QS>([&](auto qc) {
           constexpr int q = decltype(qc)::value;
@@ -561,7 +567,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
               if constexpr (!(G4W_EXP & 4)) __builtin_amdgcn_s_barrier();
               if constexpr (PROF) sync2 += __builtin_amdgcn_s_memtime() - tw;
             }
-            if constexpr (q > QW && q <= QW + NR && !(G4W_EXP & 2))             // substep-0 fragments of pos+1
+            if constexpr (NEXT0 && q > QW && q <= QW + NR && !(G4W_EXP & 2))   // substep-0 fragments of pos+1
               read_sub(s ^ 1, K0{}, std::integral_constant<int, q - QW - 1>{}, a0, b0);
           } else {
             const char* ia = smem + s * Q_STAGE;
@@ -588,24 +594,36 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
               __builtin_amdgcn_s_barrier();
               if constexpr (PROF) sync2 += __builtin_amdgcn_s_memtime() - tw;
             }
-            if constexpr (ra0 >= 0) a0[ra0] = frag<A_T>(smem + (s ^ 1) * Q_STAGE, wm * 128 + ra0 * 16, 0, lane);
-            if constexpr (rb0 >= 0) b0[rb0] = frag_b<B_T>(smem + (s ^ 1) * Q_STAGE + Q_OP, wn * WN, rb0, 0, lane);
+            if constexpr (NEXT0 && ra0 >= 0)
+              a0[ra0] = frag<A_T>(smem + (s ^ 1) * Q_STAGE, wm * 128 + ra0 * 16, 0, lane);
+            if constexpr (NEXT0 && rb0 >= 0)
+              b0[rb0] = frag_b<B_T>(smem + (s ^ 1) * Q_STAGE + Q_OP, wn * WN, rb0, 0, lane);
           }
           fence();
         });
       };
 
+      using T_ = std::true_type;
+      using F_ = std::false_type;
       if constexpr (RELAX) {   // the first K-tile peeled (sequential copies: no phi over the accumulators)
-        ktile(std::true_type{}, pos & 1);
+        ktile(T_{}, F_{}, pos & 1);
         dma_advance();
         ++pos;
         for (int t = 1; t < ct.nk; ++t, ++pos) {
-          ktile(std::false_type{}, pos & 1);
+          ktile(F_{}, F_{}, pos & 1);
           dma_advance();
         }
+      } else if constexpr (LATE) {   // the last K-tile peeled
+        for (int t = 0; t < ct.nk - 1; ++t, ++pos) {
+          ktile(F_{}, F_{}, pos & 1);
+          dma_advance();
+        }
+        ktile(F_{}, T_{}, pos & 1);
+        dma_advance();
+        ++pos;
       } else {
         for (int t = 0; t < ct.nk; ++t, ++pos) {
-          ktile(std::false_type{}, pos & 1);
+          ktile(F_{}, F_{}, pos & 1);
           dma_advance();
         }
       }
@@ -646,7 +664,12 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
         const bool extra = (OUT_F32 && beta != 0.f) || (p.R != nullptr && !ws_out);
         // fragment pair (2p, 2p+1) = 8 consecutive columns per lane (frag_b): 16 B (bf16) / 2 x 16 B (fp32) stores,
         // 32 / 64 per wave (64 bf16 stores with the 32 LDS-DMAs in flight overflowed the 63-entry vmcnt)
-        const int voff = (int)(((long long)(wm * 128 + ml) * ldc + wn * WN + 8 * gq) * ES);
+        // leading dimension through an opaque SGPR: the per-lane offsets below are then computed here, per tile
+        // (a few VALU ops) -- hoisted out of the tile loop they stayed live across the K loop, spilled to scratch,
+        // and every reload's vmcnt wait also waited for the next tile's in-flight LDS-DMAs
+        int ldcs = (int)ldc;
+        asm volatile("" : "+s"(ldcs));
+        const int voff = ((wm * 128 + ml) * ldcs + wn * WN + 8 * gq) * ES;
         const int nbase = ct.n0 + wn * WN + 8 * gq;
         // Zout / Zin share C's leading dimension and batch offset (bf16)
         const i32x4_t rz4 = make_rsrc(p.Zout ? reinterpret_cast<const char*>(p.Zout) + ct.coff * 2 + corg : cbase, cext);
@@ -663,7 +686,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
             constexpr int i = decltype(ic)::value;
             // the fragment row goes into the VGPR offset: a raw buffer's range check covers the VGPR offset and
             // the immediate but not soffset, so rows past M (ragged M) must be in voff to be dropped
-            const int vrow = voff + (int)(i * 16 * ldc * ES);
+            const int vrow = voff + i * 16 * ES * ldcs;
             f32x4_t x[8];
             if constexpr (AC == 2) {
               static_for<JB / 2>([&](auto pc) {
@@ -730,13 +753,14 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
             });
             fence();
           });
+          if constexpr (PROF) {
+            if (stamp) epi_issue += __builtin_amdgcn_s_memtime() - tmark;   // every store of the direct path issued
+          }
           // loads into VGPRs pending at the loop back edge make the compiler's wait model drain vmcnt (the in-flight
           // LDS-DMAs of the next tile included) at the top of every K-tile: retire them on this path. (Stores
           // skipped past N on an edge tile only shorten the queue the K loop's counted waits were derived for.)
           if constexpr (EX || AC == 2 || (RELAX && (ED || AC != 0))) __builtin_amdgcn_s_waitcnt(0x0f70);
         };
-        using T_ = std::true_type;
-        using F_ = std::false_type;
         using A0 = std::integral_constant<int, 0>;
         if constexpr (!OUT_F32) {
           if (gelu_direct) {
@@ -809,9 +833,10 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
     if (stamp) {
       p.stamps[sbase + 2] = loop_clk;
       p.stamps[sbase + 3] = epi_clk;
-      if (PROF) {   // the start / first-landed slots give way to the two sync points' clocks
+      if (PROF) {   // the start / first-landed / XCC slots give way to the sync points' and store-issue clocks
         p.stamps[sbase + 0] = sync1;
         p.stamps[sbase + 1] = sync2;
+        p.stamps[sbase + 4] = epi_issue;
       }
       p.stamps[sbase + 6] = __builtin_amdgcn_s_memrealtime();
     }

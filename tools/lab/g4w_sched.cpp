@@ -73,20 +73,20 @@ struct Shape {
 typedef hipError_t (*Launch)(GemmArgs, hipStream_t);
 struct Variant {
   const char* name;
-  Launch l00b, l01b, l00b_prof;
+  Launch l00b, l01b, l00b_prof, l11f;
 };
 
 #define V(NAME, SCH, STG, CPA, CPB, OPT)                                                             \
   Variant {                                                                                          \
     NAME, launch_v<0, 0, false, SCH, STG, CPA, CPB, OPT>, launch_v<0, 1, false, SCH, STG, CPA, CPB, OPT>, \
-        launch_v<0, 0, false, SCH, STG, CPA, CPB, OPT, true>                                         \
+        launch_v<0, 0, false, SCH, STG, CPA, CPB, OPT, true>, launch_v<1, 1, true, SCH, STG, CPA, CPB, OPT> \
   }
 static const Variant variants[] = {
-    V("sch0", 0, false, 3, 1, 0),
-    V("sch1", 1, false, 3, 1, 0),
-    V("sch1 relax", 1, false, 3, 1, 1),
-    V("sch1 relax stag", 1, false, 3, 1, 3),
-    V("sch0 relax", 0, false, 3, 1, 1),
+    V("sch0", 0, false, 0, 0, 0),
+    V("sch0 late", 0, false, 0, 0, 4),
+    V("sch1", 1, false, 0, 0, 0),
+    V("sch1 late", 1, false, 0, 0, 4),
+    V("sch1 relax", 1, false, 0, 0, 1),
 };
 constexpr int NV = sizeof(variants) / sizeof(variants[0]);
 
@@ -112,6 +112,7 @@ static bool wanted(int v) {   // G4W_ONLY=0,2: run only these variants
 static Launch pick(const Variant& v, const Shape& s) {
   if (s.a_t == 0 && s.b_t == 0 && !s.f32) return v.l00b;
   if (s.a_t == 0 && s.b_t == 1 && !s.f32) return v.l01b;
+  if (s.a_t == 1 && s.b_t == 1 && s.f32) return v.l11f;
   return nullptr;
 }
 
@@ -143,6 +144,7 @@ int main(int argc, char** argv) {
       {131072, 50304, 2048, 0, 0, 0, "logits"},
       {8192, 8192, 8192, 0, 0, 0, "8192^3"},
       {131072, 2048, 4096, 0, 1, 0, "dgrad [K][N] weights"},
+      {2048, 8192, 131072, 1, 1, 1, "wgrad d x 4d"},
   };
   for (const Shape& s : shapes) {
     char name[160];
@@ -235,18 +237,18 @@ int main(int argc, char** argv) {
         CK(hipStreamSynchronize(st));
         std::vector<unsigned long long> h(256 * 8);
         CK(hipMemcpy(h.data(), ds, 256 * 64, hipMemcpyDeviceToHost));
-        double s1 = 0, s2 = 0, loop = 0, epi = 0, tiles = 0, rt = 0;
+        double s1 = 0, s2 = 0, loop = 0, epi = 0, tiles = 0, rt = 0, iss = 0;
         int nb = 0;
         for (int i = 0; i < 256; ++i) {
           const unsigned long long* t = &h[i * 8];
           if (!t[6]) continue;
           ++nb;
-          s1 += t[0]; s2 += t[1]; loop += t[2]; epi += t[3]; tiles += t[7]; rt += (double)(t[6] - t[5]);
+          s1 += t[0]; s2 += t[1]; loop += t[2]; epi += t[3]; iss += t[4]; tiles += t[7]; rt += (double)(t[6] - t[5]);
         }
         const double nkt = s.K / 64.0;
         printf("%-44s %-16s stamps: per K-tile loop %.0f clk (sync1 %.0f, sync2 %.0f), epilogue %.0f clk/tile, "
-               "clock %.2f GHz\n", name, variants[v].name, loop / tiles / nkt, s1 / tiles / nkt, s2 / tiles / nkt,
-               epi / tiles, (loop + epi) / (rt / 100.0) / 1e3 / nb * nb);
+               "(stores issued after %.0f), clock %.2f GHz\n", name, variants[v].name, loop / tiles / nkt, s1 / tiles / nkt,
+               s2 / tiles / nkt, epi / tiles, iss / tiles, (loop + epi) / (rt / 100.0) / 1e3 / nb * nb);
       }
       CK(hipFree(ds));
     }
