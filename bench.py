@@ -53,6 +53,8 @@ def main():
     # the whole training step replayed as one hipGraph on a single GPU (1077 -> 1058 ms/step: the ~1500 launches of
     # a step no longer leave host-side gaps); with N > 1 ranks the step stays eager (RCCL all-reduces overlap it)
     ap.add_argument("--hip-graphs", type=int, default=1, help="1: replay the captured training step (1 GPU)")
+    ap.add_argument("--hip-graphs-dist", type=int, default=0,
+                    help="1: capture the step with N > 1 ranks too (RCCL collectives inside the graph; opt-in)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -96,6 +98,7 @@ def main():
         overrides["depth"] = args.depth
     if args.hip_graphs:
         overrides["use_hip_graphs"] = True
+        overrides["hip_graphs_distributed"] = bool(args.hip_graphs_dist)
     params = load_config(args.config, overrides)
     torch.manual_seed(1234 + rank)
     trainer = Trainer(params, device, mesh)
@@ -143,6 +146,9 @@ def main():
         dist.all_reduce(peak, op=dist.ReduceOp.MAX)
     peak = float(peak)
     comm = obst_debug.comm_bytes()   # collectives issued by this rank's timed steps (host count, replays excluded)
+    graphs = bool(params.use_hip_graphs and trainer._graphs_ok())
+    if graphs and world > 1:         # replays run no host code: per-step counts recorded at capture time
+        comm = {k: [c * args.steps, b * args.steps] for k, (c, b) in getattr(trainer, "graph_comm", {}).items()}
     ms = 1000.0 * elapsed / max(args.steps, 1)
     tokens = params.train_batch_size * S * args.steps
     tps = tokens / elapsed
@@ -175,7 +181,7 @@ def main():
                        "global_batch": params.train_batch_size, "seq_len": S,
                        "parallelism": f"dp{dp}" + (f"xtp{tp}" if tp > 1 else ""),
                        "params": trainer.store.global_numel(), "optimizer": params.optimizer,
-                       "hip_graphs": bool(params.use_hip_graphs and trainer._graphs_ok()),
+                       "hip_graphs": graphs,
                        # plain GEMMs: "gemm4w" = every product on the hand-written gfx950 kernel (no library GEMM)
                        "gemm": gemm,
                        "comm_mib_per_step": ({k: round(b / max(args.steps, 1) / 2 ** 20, 2)

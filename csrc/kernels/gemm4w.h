@@ -33,7 +33,8 @@
 
 // G4W_EXP (diagnostic builds of tools/gemm_bench only, never the library): bit 0 drops the K loop's LDS-DMAs, bit 1
 // its fragment reads, bit 2 its two barriers -- which resource bounds the loop (outputs are garbage); bit 3 drops the
-// direct epilogue's stores (what the epilogue costs without them)
+// direct epilogue's stores (what the epilogue costs without them), bit 4 sends every product through the LDS-path
+// epilogue
 #ifndef G4W_EXP
 #define G4W_EXP 0
 #endif
@@ -130,14 +131,22 @@ __device__ __forceinline__ void mfma_acc(f32x4_t& c, const bf16x8_t& a, const bf
 // under SGPR pressure the compiler reloads spilled resource words with v_readlane 2-4 instructions before the store,
 // and the store then read a stale base: the illegal-address faults of round 4 in a small batched gelu epilogue
 // (test_gemm_batched_epilogues; found with tools/sgpr_hazard.py on the device assembly).
-template <int IMM, typename V>
+// SC: cache-policy bits of the store (0 none, 1 sc0, 2 sc1, 3 sc0 sc1, 4 nt)
+#define OBST_ST16(BITS)                                                                                           \
+  asm volatile("s_nop 4\n\tbuffer_store_dwordx4 %0, %1, %2, 0 offen offset:%3" BITS "\n\ts_nop 4" ::"v"(v), "v"(voff), \
+               "s"(rs), "n"(IMM)                                                                                   \
+               : "memory")
+template <int IMM, int SC = 0, typename V>
 __device__ __forceinline__ void store16_padded(const V& v, int voff, const i32x4_t& rs,
                                                std::integral_constant<int, IMM>) {
   if constexpr ((G4W_EXP & 8) != 0) return;   // diagnostic: an epilogue without its stores
-  asm volatile("s_nop 4\n\tbuffer_store_dwordx4 %0, %1, %2, 0 offen offset:%3\n\ts_nop 4" ::"v"(v), "v"(voff), "s"(rs),
-               "n"(IMM)
-               : "memory");
+  if constexpr (SC == 0) OBST_ST16("");
+  else if constexpr (SC == 1) OBST_ST16(" sc0");
+  else if constexpr (SC == 2) OBST_ST16(" sc1");
+  else if constexpr (SC == 3) OBST_ST16(" sc0 sc1");
+  else OBST_ST16(" nt");
 }
+#undef OBST_ST16
 #pragma clang diagnostic pop
 
 __device__ __forceinline__ void fence() { __builtin_amdgcn_sched_barrier(0); }
@@ -362,6 +371,7 @@ template <int A_T, int B_T, bool OUT_F32, bool PROF, int NWV = 4, int SCH = G4W_
 __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   constexpr bool RELAX = (OPT & 1) != 0, STAGGER = (OPT & 2) != 0, LATE = (OPT & 4) != 0;
+  constexpr int SC = (OPT >> 3) & 7;   // cache policy of the direct epilogue's C stores
   static_assert(!(RELAX && LATE), "RELAX peels the first K-tile, LATE the last: not both");
   static_assert(SCH == 0 || NWV == 4, "the split schedule is laid out for one wave per SIMD");
   constexpr int WN = NWV == 4 ? 128 : 64;    // output columns per wave
@@ -642,7 +652,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
       // backward C = acc * gelu'(Zin); each variant's activation is straight-line code (no per-value switch)
       const bool gelu_direct = !OUT_F32 && p.act == ACT_GELU && p.R == nullptr &&
                                ((p.mode == 0) || (p.mode == 1 && p.Zin != nullptr));
-      if ((p.act == 0 && p.mode == 0 && p.Zout == nullptr) || gelu_direct) {
+      if (!(G4W_EXP & 16) && ((p.act == 0 && p.mode == 0 && p.Zout == nullptr) || gelu_direct)) {
         // Direct epilogue (every plain product): each lane owns C[m][n..n+3] of 64 fragments and writes it with one
         // buffer store from the accumulators (bf16: 8 B, fp32: 16 B); one per-lane offset, the fragment row in the
         // SGPR offset, the fragment column in the instruction's immediate; rows past M fall outside the resource
@@ -742,13 +752,13 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
                 }
               }
               if constexpr (OUT_F32) {
-                store16_padded(va, vrow, rc4, std::integral_constant<int, pp * 128>{});
-                store16_padded(vb, vrow, rc4, std::integral_constant<int, pp * 128 + 16>{});
+                store16_padded<pp * 128, SC>(va, vrow, rc4, std::integral_constant<int, pp * 128>{});
+                store16_padded<pp * 128 + 16, SC>(vb, vrow, rc4, std::integral_constant<int, pp * 128 + 16>{});
               } else {
                 // the same unpadded-hazard as the fp32 stores (garbage in ~1% of the bf16 outputs, measured)
-                store16_padded(v4u32_t{pack_bf16x2(va[0], va[1]), pack_bf16x2(va[2], va[3]), pack_bf16x2(vb[0], vb[1]),
-                                       pack_bf16x2(vb[2], vb[3])},
-                               vrow, rc4, std::integral_constant<int, pp * 64>{});
+                store16_padded<pp * 64, SC>(v4u32_t{pack_bf16x2(va[0], va[1]), pack_bf16x2(va[2], va[3]),
+                                                    pack_bf16x2(vb[0], vb[1]), pack_bf16x2(vb[2], vb[3])},
+                                           vrow, rc4, std::integral_constant<int, pp * 64>{});
               }
             });
             fence();

@@ -100,6 +100,9 @@ _DEFAULTS: typing.Dict[str, typing.Any] = dict(
     grad_bucket_mb=64,           # DP gradient all-reduce bucket size (xGMI ring per-link bound: SURVEY 5.8)
     allreduce_dtype="float32",   # dtype gradients travel in over RCCL
     use_hip_graphs=False,        # capture the whole training step in hipGraphs (Trainer._graph_step; 1 GPU, no dropout)
+    # also capture with world > 1 (the RCCL all-reduces inside the graph; opt-in: RCCL graph capture is exercised only
+    # where several GPUs are visible, which the 1-GPU test boxes are not)
+    hip_graphs_distributed=False,
     kv_cache=True,               # incremental decoding over per-layer KV caches for causal-attention bodies (Sampler)
     decode_hip_graphs=True,      # replay the single-token decode step from a hipGraph (Model._decode_graphed)
     log_every=10, metrics_path=None, pad_vocab_to=128,

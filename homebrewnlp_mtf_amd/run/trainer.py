@@ -115,8 +115,12 @@ class Trainer:
     def _graphs_ok(self) -> bool:
         p = self.params
         dropout = p.input_dropout > 0 or "dropout" in str(p.block_config)
+        # world > 1: RCCL collectives can be captured (async all-reduce + wait become graph nodes), but only on the
+        # nccl backend and only as an opt-in (hip_graphs_distributed): gloo runs on the host and cannot be captured
+        multi_ok = self.mesh.world == 1 or (bool(getattr(p, "hip_graphs_distributed", False)) and dist.is_initialized()
+                                            and dist.get_backend() == "nccl")
         return (self.device.type == "cuda" and isinstance(self.opt, fused_opt.FusedOptimizer)
-                and self.mesh.world == 1 and int(p.grad_accumulation) == 1 and not dropout
+                and multi_ok and int(p.grad_accumulation) == 1 and not dropout
                 and not getattr(self.store, "leaf_grads_seen", False) and not debug.CHECK)
 
     def _graph_step(self, batch: typing.Dict[str, torch.Tensor]) -> typing.Dict[str, torch.Tensor]:
@@ -155,8 +159,13 @@ class Trainer:
         self.opt.flip = parity
         graph = torch.cuda.CUDAGraph()
         torch.cuda.synchronize(self.device)
+        before = debug.comm_bytes()
         with torch.cuda.graph(graph, pool=g["pool"]):
             out = self._step_body(g["inputs"], lr)
+        # collectives recorded while capturing = what every replay issues (replays run no host code to count them)
+        after = debug.comm_bytes()
+        self.graph_comm = {k: (c - before.get(k, (0, 0))[0], b - before.get(k, (0, 0))[1])
+                           for k, (c, b) in after.items() if c != before.get(k, (0, 0))[0]}
         self.opt.flip = keep     # capture ran the host side of the step (buffer flip) but executed nothing
         g["graphs"][parity] = (graph, out)
         log(f"captured the training step in a hipGraph (SM3 parity {parity})")

@@ -82,11 +82,11 @@ struct Variant {
         launch_v<0, 0, false, SCH, STG, CPA, CPB, OPT, true>, launch_v<1, 1, true, SCH, STG, CPA, CPB, OPT> \
   }
 static const Variant variants[] = {
-    V("sch0", 0, false, 0, 0, 0),
-    V("sch0 late", 0, false, 0, 0, 4),
     V("sch1", 1, false, 0, 0, 0),
-    V("sch1 late", 1, false, 0, 0, 4),
-    V("sch1 relax", 1, false, 0, 0, 1),
+    V("sch1 st sc0", 1, false, 0, 0, 8),
+    V("sch1 st sc1", 1, false, 0, 0, 16),
+    V("sch1 st sc0sc1", 1, false, 0, 0, 24),
+    V("sch1 st nt", 1, false, 0, 0, 32),
 };
 constexpr int NV = sizeof(variants) / sizeof(variants[0]);
 
