@@ -372,6 +372,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   constexpr bool RELAX = (OPT & 1) != 0, STAGGER = (OPT & 2) != 0, LATE = (OPT & 4) != 0;
   constexpr int SC = (OPT >> 3) & 7;   // cache policy of the direct epilogue's C stores
+  constexpr bool ROWS = (OPT & 64) != 0;   // plain products: C rows staged through LDS, row-contiguous stores
   static_assert(!(RELAX && LATE), "RELAX peels the first K-tile, LATE the last: not both");
   static_assert(SCH == 0 || NWV == 4, "the split schedule is laid out for one wave per SIMD");
   constexpr int WN = NWV == 4 ? 128 : 64;    // output columns per wave
@@ -690,6 +691,49 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
         auto emit = [&](auto exc, auto edc, auto acc_) {
           constexpr bool EX = decltype(exc)::value, ED = decltype(edc)::value;
           constexpr int AC = decltype(acc_)::value;
+          if constexpr (ROWS && AC == 0 && !EX) {
+            // ROWS: a lane's accumulators hold one row's 16-byte column chunk each, 16 rows per store instruction
+            // (64-byte pieces of 16 rows). Staged through the wave's LDS region instead, every store instruction
+            // writes whole 256 / 512-byte row segments (4 / 2 rows): full cache lines for the write path.
+            constexpr int CPR = WN * ES / 16;   // 16-byte chunks per row of the wave's tile: 16 (bf16) / 32 (fp32)
+            constexpr int RPI = 64 / CPR;       // rows per store instruction
+            char* epb = smem + 2 * Q_STAGE + wave * 16 * WN * 4;
+            const int rr0 = lane / CPR, cc = lane % CPR;
+            const int vb = ((wm * 128 + rr0) * ldcs + wn * WN + cc * (16 / ES)) * ES;
+            const bool colok = !ED || ct.n0 + wn * WN + cc * (16 / ES) < p.N;
+            static_for<8>([&](auto ic) {
+              constexpr int i = decltype(ic)::value;
+              if constexpr (OUT_F32) {
+                static_for<JB>([&](auto jc) {
+                  constexpr int j = decltype(jc)::value;
+                  const int c4 = 8 * (j >> 1) + 2 * gq + (j & 1);   // frag_b column order, 16-byte units
+                  *reinterpret_cast<f32x4_t*>(epb + ml * (CPR * 16) + ((c4 ^ ml) & (CPR - 1)) * 16) =
+                      alpha * acc[i][j];
+                });
+              } else {
+                static_for<JB / 2>([&](auto pc) {
+                  constexpr int pp = decltype(pc)::value;
+                  const f32x4_t va = alpha * acc[i][2 * pp], vb2 = alpha * acc[i][2 * pp + 1];
+                  *reinterpret_cast<v4u32_t*>(epb + ml * (CPR * 16) + (((pp * 4 + gq) ^ ml) & (CPR - 1)) * 16) =
+                      v4u32_t{pack_bf16x2(va[0], va[1]), pack_bf16x2(va[2], va[3]), pack_bf16x2(vb2[0], vb2[1]),
+                              pack_bf16x2(vb2[2], vb2[3])};
+                });
+              }
+              static_for<16 / RPI>([&](auto rc) {
+                constexpr int r = decltype(rc)::value;
+                const int R = r * RPI + rr0;
+                const v4u32_t v = *reinterpret_cast<const v4u32_t*>(epb + R * (CPR * 16) + ((cc ^ R) & (CPR - 1)) * 16);
+                const int vro = vb + (i * 16 + r * RPI) * ES * ldcs;
+                if (colok) store16_padded<0, SC>(v, vro, rc4, std::integral_constant<int, 0>{});
+              });
+              fence();
+            });
+            if constexpr (PROF) {
+              if (stamp) epi_issue += __builtin_amdgcn_s_memtime() - tmark;
+            }
+            if constexpr (RELAX && ED) __builtin_amdgcn_s_waitcnt(0x0f70);   // masked stores: a different count
+            return;
+          }
           // one fragment row at a time: with EX its residual / C loads are issued together and consumed after,
           // bounded by the fences (unbounded, the scheduler hoisted all 64 loads: 256 VGPRs, spills)
           static_for<8>([&](auto ic) {

@@ -142,6 +142,44 @@ def _fwd_gemm(x2, w, y2, plan: LinearPlan, act=None, R=None, Zout=None):
              M, N, K, batch=(H, 1), act=act, R=R, Zout=Zout)
 
 
+# Row-parallel forward under TP (the weight contracts the sharded heads: every rank holds a partial sum of the whole
+# output): the product runs in OBST_TP_CHUNKS token blocks and each block's all-reduce starts on RCCL's stream as soon
+# as its GEMM is done, so the next block's GEMM overlaps it -- only the last block's all-reduce stays exposed. Blocks
+# stay >= 4096 tokens (a whole number of 256-row tiles, ~full-rate GEMMs).
+_TP_CHUNKS = max(int(__import__("os").environ.get("OBST_TP_CHUNKS", "4")), 1)
+_TP_MIN_ROWS = int(__import__("os").environ.get("OBST_TP_MIN_ROWS", "4096"))   # (tests: tiny blocks)
+
+
+def tp_chunks(M: int) -> typing.List[typing.Tuple[int, int]]:
+    """[m0, m1) token blocks of the chunked row-parallel forward"""
+    c = _TP_CHUNKS
+    while c > 1 and (M // c < _TP_MIN_ROWS):
+        c //= 2
+    step = -(-M // c)
+    step = -(-step // 256) * 256 if _TP_MIN_ROWS >= 256 else step
+    return [(m0, min(m0 + step, M)) for m0 in range(0, M, step)]
+
+
+def _fwd_gemm_reduced(x2, w, y2, plan: LinearPlan):
+    """y2 = x2 . w summed over the TP group (row-parallel plan): token blocks, each block's all-reduce overlapping
+    the next block's GEMM (identity reduction when tp == 1)"""
+    if pstate.tp_size() == 1 or x2.device.type == "meta":
+        _fwd_gemm(x2, w, y2, plan)
+        pstate.tp_all_reduce(y2)
+        return
+    M, H, K, N = plan.M, plan.H, plan.K, plan.N
+    xf, yf = x2.reshape(M, H * K), y2.view(M, H * N)
+    wt = _wT(w, plan, None, False)
+    bop = raw.Operand(wt, 0, K, K * N) if wt is not None else raw.Operand(w, 1, N, K * N)
+    pending = []
+    for m0, m1 in tp_chunks(M):
+        yc = yf[m0:m1]
+        raw.gemm(raw.Operand(xf[m0:m1], 0, H * K, K), bop, raw.Operand(yc, 0, H * N, N), m1 - m0, N, K, batch=(H, 1))
+        pending.append(pstate.tp_all_reduce_async(yc))
+    for h in pending:
+        h.wait()
+
+
 def tokens_transposed(x2, rows: int, cols: int) -> typing.Optional[torch.Tensor]:
     """[rows][cols] bf16 -> [cols][rows] (None where the plain transposed-read GEMM is used instead)"""
     if not _KCONTIG or not raw.on_gpu(x2) or x2.dtype != torch.bfloat16 or rows % 8 or cols % 8:
@@ -200,11 +238,12 @@ class _Linear(torch.autograd.Function):
         xc = x.permute(plan.x_perm).contiguous() if plan.x_perm is not None else x.contiguous()
         y = _empty(plan.canon_o_shape, xc)
         z = _empty(plan.canon_o_shape, xc) if act else None
-        _fwd_gemm(xc, w, y, plan, act=act, Zout=z)
         if plan.row_parallel and pstate.tp_size() > 1:
             if act:
                 raise NotImplementedError("activation fused into a heads-contracting linear under TP")
-            pstate.tp_all_reduce(y)
+            _fwd_gemm_reduced(xc, w, y, plan)
+        else:
+            _fwd_gemm(xc, w, y, plan, act=act, Zout=z)
         ctx.save_for_backward(xc, w, z)
         ctx.plan, ctx.act = plan, act
         if plan.o_perm is not None:
@@ -287,16 +326,14 @@ class _FFN(torch.autograd.Function):
         a = _empty(p1.canon_o_shape, xc) if act else z
         if tp and p1.row_parallel:
             # W1 contracts the sharded heads: the pre-activation is a partial sum -- reduce it, then activate
-            _fwd_gemm(xc, w1, z, p1)
-            pstate.tp_all_reduce(z)
+            _fwd_gemm_reduced(xc, w1, z, p1)
             if act:
                 raw.elementwise("act", z, a, act=act)
         else:
             _fwd_gemm(xc, w1, a, p1, act=act, Zout=z if act else None)
         y = _empty(p2.canon_o_shape, xc)
         if tp and p2.row_parallel:   # partial output: reduce before the residual joins
-            _fwd_gemm(a, w2, y, p2)
-            pstate.tp_all_reduce(y)
+            _fwd_gemm_reduced(a, w2, y, p2)
             if residual is not None:
                 raw.elementwise("add", y, y, z=residual.contiguous())
         else:

@@ -96,8 +96,9 @@ def test_dp_matches_single_rank():
     assert abs((ranks[0]["losses"][0] + ranks[1]["losses"][0]) / 2 - ref_losses[0]) < 1e-5
 
 
-@pytest.mark.parametrize("strategy", ["none", "revnet", "activated_attention_input", "intermediate_layout"])
-def test_tp_matches_single_rank(strategy):
+@pytest.mark.parametrize("strategy", ["none", "revnet", "activated_attention_input", "intermediate_layout",
+                                      "chunked_forward_reduce"])
+def test_tp_matches_single_rank(strategy, monkeypatch):
     """fused FFN (W1 contracts the sharded heads: reduce-then-activate; dz reduced after the fused act-backward) and
     the fused attention block, also with an activated input projection"""
     cfg = dict(CFG, memory_reduction_strategy="none" if strategy != "revnet" else "revnet")
@@ -112,6 +113,9 @@ def test_tp_matches_single_rank(strategy):
         cfg["tp_layout"] = "intermediate"
         cfg["block_config"] = [{"layer": ["norm-shift-scale", "attention-dot_product-context"], "skip": True},
                                {"layer": ["norm-shift-scale", "feed_forward-in:gelu"], "skip": True}]
+    if strategy == "chunked_forward_reduce":
+        # row-parallel forwards in 16-token blocks, each block's all-reduce overlapping the next block's GEMM
+        monkeypatch.setenv("OBST_TP_MIN_ROWS", "16")
     ranks = _run("tp", cfg)
     if strategy == "intermediate_layout":
         ffn = [n for n in ranks[0]["specs"] if "feed_forward" in n]

@@ -83,10 +83,10 @@ struct Variant {
   }
 static const Variant variants[] = {
     V("sch1", 1, false, 0, 0, 0),
-    V("sch1 st sc0", 1, false, 0, 0, 8),
     V("sch1 st sc1", 1, false, 0, 0, 16),
-    V("sch1 st sc0sc1", 1, false, 0, 0, 24),
     V("sch1 st nt", 1, false, 0, 0, 32),
+    V("sch1 rows", 1, false, 0, 0, 64),
+    V("sch1 rows sc1", 1, false, 0, 0, 80),
 };
 constexpr int NV = sizeof(variants) / sizeof(variants[0]);
 
