@@ -146,6 +146,29 @@ __device__ __forceinline__ void store16_padded(const V& v, int voff, const i32x4
   else if constexpr (SC == 3) OBST_ST16(" sc0 sc1");
   else OBST_ST16(" nt");
 }
+// the same without a memory clobber: LDS reads / writes of the epilogue may move across it (data dependences
+// still order it after the LDS read that produces its value)
+#define OBST_ST16NC(BITS)                                                                                      \
+  asm volatile("s_nop 4\n\tbuffer_store_dwordx4 %0, %1, %2, 0 offen" BITS "\n\ts_nop 4" ::"v"(v), "v"(voff), \
+               "s"(rs))
+template <int SC = 0, typename V>
+__device__ __forceinline__ void store16_nc(const V& v, int voff, const i32x4_t& rs_) {
+  if constexpr ((G4W_EXP & 8) != 0) return;
+  // uniform by construction, but in the activation epilogues the register allocator had the resource in VGPRs
+  // ("illegal VGPR to SGPR copy"): read it back into SGPRs (a no-op copy when it is already scalar; the s_nop 4 in
+  // front of the store covers the VALU-write -> VMEM-read hazard otherwise)
+  i32x4_t rs;
+  rs[0] = __builtin_amdgcn_readfirstlane(rs_[0]);
+  rs[1] = __builtin_amdgcn_readfirstlane(rs_[1]);
+  rs[2] = __builtin_amdgcn_readfirstlane(rs_[2]);
+  rs[3] = __builtin_amdgcn_readfirstlane(rs_[3]);
+  if constexpr (SC == 0) OBST_ST16NC("");
+  else if constexpr (SC == 1) OBST_ST16NC(" sc0");
+  else if constexpr (SC == 2) OBST_ST16NC(" sc1");
+  else if constexpr (SC == 3) OBST_ST16NC(" sc0 sc1");
+  else OBST_ST16NC(" nt");
+}
+#undef OBST_ST16NC
 #undef OBST_ST16
 #pragma clang diagnostic pop
 
@@ -373,6 +396,10 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
   constexpr bool RELAX = (OPT & 1) != 0, STAGGER = (OPT & 2) != 0, LATE = (OPT & 4) != 0;
   constexpr int SC = (OPT >> 3) & 7;   // cache policy of the direct epilogue's C stores
   constexpr bool ROWS = (OPT & 64) != 0;   // plain products: C rows staged through LDS, row-contiguous stores
+  // DEFER: a tile's last K-tile issues no LDS-DMA; its position (the next tile's second K-tile) is staged after the
+  // epilogue's stores, so the stores do not queue behind 32 in-flight 1 KiB loads per wave
+  constexpr bool DEFER = (OPT & 128) != 0;
+  static_assert(!(RELAX && DEFER), "RELAX counts the epilogue stores out of the first K-tile's waits: not with DEFER");
   static_assert(!(RELAX && LATE), "RELAX peels the first K-tile, LATE the last: not both");
   static_assert(SCH == 0 || NWV == 4, "the split schedule is laid out for one wave per SIMD");
   constexpr int WN = NWV == 4 ? 128 : 64;    // output columns per wave
@@ -549,6 +576,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
       auto ktile = [&](auto fc, auto lc, int s) {
         constexpr bool FIRST = decltype(fc)::value && RELAX;
         constexpr bool NEXT0 = !(decltype(lc)::value && LATE);   // read pos+1's substep-0 fragments in this K-tile
+        constexpr bool NODMA = decltype(lc)::value && DEFER;     // deferred: no DMA (and pos+1's wait counts drop)
         const unsigned sa = stage_a(s), sb = stage_b(s);
         static_for<QS>([&](auto qc) {
           constexpr int q = decltype(qc)::value;
@@ -557,16 +585,18 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
           else mfma_acc(acc[i][j], b1f[j], a1[i]);
           if constexpr (SCH == 0) {
             if constexpr (q < NR && !(G4W_EXP & 2)) read_sub(s, K1{}, qc, a1, b1f);   // substep-1 fragments of pos
-            if constexpr (q == NR) dma_setup();                                 // resources of position pos + 2
+            if constexpr (q == NR && !NODMA) dma_setup();                       // resources of position pos + 2
             if constexpr (q == QB1) {                                           // stage s fully read by every wave
               if constexpr (PROF) tw = __builtin_amdgcn_s_memtime();
               __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0) as a builtin: the compiler's wait model learns the
               if constexpr (!(G4W_EXP & 4)) __builtin_amdgcn_s_barrier();   // substep-1 reads are done
               if constexpr (PROF) sync1 += __builtin_amdgcn_s_memtime() - tw;
             }
-            if constexpr (!(G4W_EXP & 1) && q >= QA0 + SH && q < QA0 + SH + DQ * PPW && (q - QA0 - SH) % DQ == 0)
+            if constexpr (!NODMA && !(G4W_EXP & 1) && q >= QA0 + SH && q < QA0 + SH + DQ * PPW &&
+                          (q - QA0 - SH) % DQ == 0)
               dma16o<CPA, (q - QA0 - SH) / DQ * 1024>(ra, voa[(q - QA0 - SH) / DQ], sa);
-            if constexpr (!(G4W_EXP & 1) && q >= QB0 + SH && q < QB0 + SH + DQ * PPW && (q - QB0 - SH) % DQ == 0)
+            if constexpr (!NODMA && !(G4W_EXP & 1) && q >= QB0 + SH && q < QB0 + SH + DQ * PPW &&
+                          (q - QB0 - SH) % DQ == 0)
               dma16o<CPB, (q - QB0 - SH) / DQ * 1024>(rb, vob[(q - QB0 - SH) / DQ], sb);
             if constexpr (q == QW) {                                            // position pos+1 landed in stage s^1
               // first K-tile of a tile: the previous tile's epilogue stores sit between that position's DMAs and
@@ -574,6 +604,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
               // 64 fp32)
               if constexpr (PROF) tw = __builtin_amdgcn_s_memtime();
               if constexpr (FIRST) vm_wait<V0F>();
+              else if constexpr (NODMA) vm_wait<0>();   // nothing issued after pos+1's pieces
               else vm_wait<2 * PPW>();
               if constexpr (!(G4W_EXP & 4)) __builtin_amdgcn_s_barrier();
               if constexpr (PROF) sync2 += __builtin_amdgcn_s_memtime() - tw;
@@ -589,18 +620,19 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
             constexpr int ra0 = g4s::idx(g4s::A0N, q - SH), rb0 = g4s::idx(g4s::B0N, q - SH);
             if constexpr (ra1 >= 0) a1[ra1] = frag<A_T>(ia, wm * 128 + ra1 * 16, 1, lane);
             if constexpr (rb1 >= 0) b1f[rb1] = frag_b<B_T>(ib, wn * WN, rb1, 1, lane);
-            if constexpr (q == g4s::SETUP) dma_setup();
+            if constexpr (q == g4s::SETUP && !NODMA) dma_setup();
             if constexpr (q == g4s::BAR_A || q == g4s::BAR_B) {   // every wave done reading this stage's A / B image
               if constexpr (PROF) tw = __builtin_amdgcn_s_memtime();
               __builtin_amdgcn_s_waitcnt(0xc07f);
               __builtin_amdgcn_s_barrier();
               if constexpr (PROF) sync1 += __builtin_amdgcn_s_memtime() - tw;
             }
-            if constexpr (da >= 0) dma16o<CPA, (da < 0 ? 0 : da) * 1024>(ra, voa[da], sa);
-            if constexpr (db >= 0) dma16o<CPB, (db < 0 ? 0 : db) * 1024>(rb, vob[db], sb);
+            if constexpr (!NODMA && da >= 0) dma16o<CPA, (da < 0 ? 0 : da) * 1024>(ra, voa[da], sa);
+            if constexpr (!NODMA && db >= 0) dma16o<CPB, (db < 0 ? 0 : db) * 1024>(rb, vob[db], sb);
             if constexpr (q == g4s::WA || q == g4s::WB) {   // A / B image of position pos+1 landed in stage s^1
               if constexpr (PROF) tw = __builtin_amdgcn_s_memtime();
               if constexpr (FIRST) vm_wait<q == g4s::WA ? VAF : VBF>();
+              else if constexpr (NODMA) vm_wait<q == g4s::WA ? PPW : 0>();   // younger: pos+1's B pieces only
               else vm_wait<q == g4s::WA ? VA : VB>();
               __builtin_amdgcn_s_barrier();
               if constexpr (PROF) sync2 += __builtin_amdgcn_s_memtime() - tw;
@@ -624,13 +656,13 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
           ktile(F_{}, F_{}, pos & 1);
           dma_advance();
         }
-      } else if constexpr (LATE) {   // the last K-tile peeled
+      } else if constexpr (LATE || DEFER) {   // the last K-tile peeled
         for (int t = 0; t < ct.nk - 1; ++t, ++pos) {
           ktile(F_{}, F_{}, pos & 1);
           dma_advance();
         }
         ktile(F_{}, T_{}, pos & 1);
-        dma_advance();
+        if constexpr (!DEFER) dma_advance();   // DEFER: the cursor's position is staged after the epilogue
         ++pos;
       } else {
         for (int t = 0; t < ct.nk; ++t, ++pos) {
@@ -671,7 +703,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
         const int ml = lane & 15, gq = lane >> 4;
         const float alpha = p.alpha, beta = ws_out ? 0.f : p.beta;
 
-        const bool edge = ct.n0 + wn * WN + WN > p.N;
+        const bool edge = !ROWS && ct.n0 + wn * WN + WN > p.N;   // ROWS masks columns per lane in one copy
         const bool extra = (OUT_F32 && beta != 0.f) || (p.R != nullptr && !ws_out);
         // fragment pair (2p, 2p+1) = 8 consecutive columns per lane (frag_b): 16 B (bf16) / 2 x 16 B (fp32) stores,
         // 32 / 64 per wave (64 bf16 stores with the 32 LDS-DMAs in flight overflowed the 63-entry vmcnt)
@@ -691,47 +723,125 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
         auto emit = [&](auto exc, auto edc, auto acc_) {
           constexpr bool EX = decltype(exc)::value, ED = decltype(edc)::value;
           constexpr int AC = decltype(acc_)::value;
-          if constexpr (ROWS && AC == 0 && !EX) {
-            // ROWS: a lane's accumulators hold one row's 16-byte column chunk each, 16 rows per store instruction
-            // (64-byte pieces of 16 rows). Staged through the wave's LDS region instead, every store instruction
-            // writes whole 256 / 512-byte row segments (4 / 2 rows): full cache lines for the write path.
+          if constexpr (ROWS) {
+            // ROWS: a lane's accumulators hold one row's 16-byte column chunk each, so a direct store instruction
+            // writes 64-byte pieces of 16 rows; the store path takes ~4x longer for that pattern than for whole row
+            // segments (tools/lab/store_bench.cpp: 8.3k vs 2.2k clocks per 256 x 256 bf16 tile and CU). Staged
+            // through the wave's LDS region, each store instruction writes 4 (bf16) / 2 (fp32) rows of 256 / 512 B,
+            // and the epilogue's side inputs (residual, Zin, C for beta) are read in the same row layout.
+            // bf16: alpha * acc staged as bf16 (the output precision) in two 4 KiB buffers, the next fragment row
+            // written while this one is read back; fp32: one 8 KiB buffer.
             constexpr int CPR = WN * ES / 16;   // 16-byte chunks per row of the wave's tile: 16 (bf16) / 32 (fp32)
             constexpr int RPI = 64 / CPR;       // rows per store instruction
+            constexpr int NRD = 16 / RPI;       // store instructions per fragment row
             char* epb = smem + 2 * Q_STAGE + wave * 16 * WN * 4;
             const int rr0 = lane / CPR, cc = lane % CPR;
             const int vb = ((wm * 128 + rr0) * ldcs + wn * WN + cc * (16 / ES)) * ES;
-            const bool colok = !ED || ct.n0 + wn * WN + cc * (16 / ES) < p.N;
-            static_for<8>([&](auto ic) {
+            const bool colok = ct.n0 + wn * WN + cc * (16 / ES) < p.N;   // (every tile: one ROWS copy per variant)
+            auto write_row = [&](auto ic, char* buf) {
               constexpr int i = decltype(ic)::value;
               if constexpr (OUT_F32) {
                 static_for<JB>([&](auto jc) {
                   constexpr int j = decltype(jc)::value;
                   const int c4 = 8 * (j >> 1) + 2 * gq + (j & 1);   // frag_b column order, 16-byte units
-                  *reinterpret_cast<f32x4_t*>(epb + ml * (CPR * 16) + ((c4 ^ ml) & (CPR - 1)) * 16) =
+                  *reinterpret_cast<f32x4_t*>(buf + ml * (CPR * 16) + ((c4 ^ ml) & (CPR - 1)) * 16) =
                       alpha * acc[i][j];
                 });
               } else {
                 static_for<JB / 2>([&](auto pc) {
                   constexpr int pp = decltype(pc)::value;
                   const f32x4_t va = alpha * acc[i][2 * pp], vb2 = alpha * acc[i][2 * pp + 1];
-                  *reinterpret_cast<v4u32_t*>(epb + ml * (CPR * 16) + (((pp * 4 + gq) ^ ml) & (CPR - 1)) * 16) =
+                  *reinterpret_cast<v4u32_t*>(buf + ml * (CPR * 16) + (((pp * 4 + gq) ^ ml) & (CPR - 1)) * 16) =
                       v4u32_t{pack_bf16x2(va[0], va[1]), pack_bf16x2(va[2], va[3]), pack_bf16x2(vb2[0], vb2[1]),
                               pack_bf16x2(vb2[2], vb2[3])};
                 });
               }
-              static_for<16 / RPI>([&](auto rc) {
-                constexpr int r = decltype(rc)::value;
-                const int R = r * RPI + rr0;
-                const v4u32_t v = *reinterpret_cast<const v4u32_t*>(epb + R * (CPR * 16) + ((cc ^ R) & (CPR - 1)) * 16);
-                const int vro = vb + (i * 16 + r * RPI) * ES * ldcs;
-                if (colok) store16_padded<0, SC>(v, vro, rc4, std::integral_constant<int, 0>{});
+            };
+            auto unpack8 = [](const v4u32_t& o, float (&x)[8]) {
+              static_for<4>([&](auto tc) {
+                constexpr int t = decltype(tc)::value;
+                x[2 * t] = bf2f(o[t] & 0xffff);
+                x[2 * t + 1] = bf2f(o[t] >> 16);
               });
-              fence();
-            });
+            };
+            auto read_store_row = [&](auto ic, const char* buf) {
+              constexpr int i = decltype(ic)::value;
+              v4u32_t v[NRD], side[NRD], cold[NRD];
+              int vro[NRD];
+              static_for<NRD>([&](auto rk) {   // every read first: one LDS latency per fragment row
+                constexpr int r = decltype(rk)::value;
+                const int R = r * RPI + rr0;
+                vro[r] = vb + (i * 16 + r * RPI) * ES * ldcs;
+                v[r] = *reinterpret_cast<const v4u32_t*>(buf + R * (CPR * 16) + ((cc ^ R) & (CPR - 1)) * 16);
+                if constexpr (AC == 2) side[r] = __builtin_amdgcn_raw_buffer_load_b128(rzi, vro[r], 0, 0);
+                if constexpr (EX) {
+                  side[r] = __builtin_amdgcn_raw_buffer_load_b128(rr, vro[r], 0, 0);
+                  if constexpr (OUT_F32) cold[r] = __builtin_amdgcn_raw_buffer_load_b128(rc, vro[r], 0, 0);
+                }
+              });
+              // the outputs first, then every store (activation code between the stores moved the resource
+              // operands into VGPRs: "illegal VGPR to SGPR copy")
+              v4u32_t out[NRD];
+              static_for<NRD>([&](auto rk) {
+                constexpr int r = decltype(rk)::value;
+                if constexpr (AC == 0 && !EX) {
+                  out[r] = v[r];
+                } else if constexpr (OUT_F32) {   // EX: beta * C (+ R), fp32
+                  f32x4_t x = __builtin_bit_cast(f32x4_t, v[r]);
+                  if (beta != 0.f) x += beta * __builtin_bit_cast(f32x4_t, cold[r]);
+                  if (p.R) x += __builtin_bit_cast(f32x4_t, side[r]);
+                  out[r] = __builtin_bit_cast(v4u32_t, x);
+                } else {
+                  float x[8];
+                  unpack8(v[r], x);
+                  if constexpr (EX) {
+                    float y[8];
+                    unpack8(side[r], y);
+                    static_for<8>([&](auto tc) { x[decltype(tc)::value] += y[decltype(tc)::value]; });
+                  }
+                  if constexpr (AC == 1) {
+                    static_for<8>([&](auto tc) { x[decltype(tc)::value] = act_fwd(ACT_GELU, x[decltype(tc)::value]); });
+                  } else if constexpr (AC == 2) {
+                    float z[8];
+                    unpack8(side[r], z);
+                    static_for<8>([&](auto tc) {
+                      constexpr int t = decltype(tc)::value;
+                      x[t] *= act_grad(ACT_GELU, z[t]);
+                    });
+                  }
+                  out[r] = v4u32_t{pack_bf16x2(x[0], x[1]), pack_bf16x2(x[2], x[3]), pack_bf16x2(x[4], x[5]),
+                                   pack_bf16x2(x[6], x[7])};
+                }
+              });
+              static_for<NRD>([&](auto rk) {
+                constexpr int r = decltype(rk)::value;
+                if constexpr (AC == 1) {
+                  if (zout && colok) store16_nc<SC>(v[r], vro[r], rz4);   // the bf16 pre-activation
+                }
+                if (colok) store16_nc<SC>(out[r], vro[r], rc4);
+              });
+            };
+            if constexpr (!OUT_F32) {
+              char* const bufs[2] = {epb, epb + 16 * CPR * 16};
+              write_row(std::integral_constant<int, 0>{}, bufs[0]);
+              static_for<8>([&](auto ic) {
+                constexpr int i = decltype(ic)::value;
+                if constexpr (i + 1 < 8) write_row(std::integral_constant<int, i + 1>{}, bufs[(i + 1) & 1]);
+                read_store_row(ic, bufs[i & 1]);
+                fence();
+              });
+            } else {
+              static_for<8>([&](auto ic) {
+                write_row(ic, epb);
+                read_store_row(ic, epb);
+                fence();
+              });
+            }
             if constexpr (PROF) {
               if (stamp) epi_issue += __builtin_amdgcn_s_memtime() - tmark;
             }
-            if constexpr (RELAX && ED) __builtin_amdgcn_s_waitcnt(0x0f70);   // masked stores: a different count
+            // loads into VGPRs (residual / Zin / C) retired here, as in the fragment-layout path below
+            if constexpr (EX || AC == 2 || (RELAX && (ED || AC != 0))) __builtin_amdgcn_s_waitcnt(0x0f70);
             return;
           }
           // one fragment row at a time: with EX its residual / C loads are issued together and consumed after,
@@ -872,6 +982,20 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
       if (stamp) {
         const unsigned long long now = __builtin_amdgcn_s_memtime();
         epi_clk += now - tmark;
+      }
+      if constexpr (DEFER) {   // the last K-tile's deferred position, into the stage that K-tile read (parity pos+1)
+        dma_setup();
+        const unsigned sa = stage_a((pos + 1) & 1), sb = stage_b((pos + 1) & 1);
+        static_for<PPW>([&](auto qc) {
+          constexpr int q = decltype(qc)::value;
+          dma16o<CPA, q * 1024>(ra, voa[q], sa);
+        });
+        static_for<PPW>([&](auto qc) {
+          constexpr int q = decltype(qc)::value;
+          dma16o<CPB, q * 1024>(rb, vob[q], sb);
+        });
+        dma_advance();
+        fence();
       }
     }
   };

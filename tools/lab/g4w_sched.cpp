@@ -83,10 +83,9 @@ struct Variant {
   }
 static const Variant variants[] = {
     V("sch1", 1, false, 0, 0, 0),
-    V("sch1 st sc1", 1, false, 0, 0, 16),
-    V("sch1 st nt", 1, false, 0, 0, 32),
     V("sch1 rows", 1, false, 0, 0, 64),
-    V("sch1 rows sc1", 1, false, 0, 0, 80),
+    V("sch1 defer rows", 1, false, 0, 0, 192),
+    V("sch1 rows late", 1, false, 0, 0, 68),
 };
 constexpr int NV = sizeof(variants) / sizeof(variants[0]);
 
@@ -145,6 +144,10 @@ int main(int argc, char** argv) {
       {8192, 8192, 8192, 0, 0, 0, "8192^3"},
       {131072, 2048, 4096, 0, 1, 0, "dgrad [K][N] weights"},
       {2048, 8192, 131072, 1, 1, 1, "wgrad d x 4d"},
+      {512, 512, 2048, 0, 0, 0, "few tiles (4)"},
+      {2048, 1024, 2048, 0, 0, 0, "few tiles (32)"},
+      {131072, 4096, 128, 0, 0, 0, "K sweep 128"},
+      {131072, 4096, 512, 0, 0, 0, "K sweep 512"},
   };
   for (const Shape& s : shapes) {
     char name[160];
