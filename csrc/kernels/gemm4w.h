@@ -206,19 +206,22 @@ __device__ __forceinline__ void static_for(F&& f) {
 // which the A images' (row >> 1) & 7 is 2-way bank-conflicted (67 M conflict cycles per 131072x4096x2048 launch);
 // row bits 1, 3 and 4 give the 16 lanes of every ds_read_b128 group distinct bank quads (profiles/r3_gemm4w_bounds.md)
 __device__ __forceinline__ int bswz(int r) { return ((r >> 1) & 1) | (((r >> 3) & 1) << 1) | (((r >> 4) & 1) << 2); }
+// TLAY (row-layout accumulators, see frag_b): the 16 lanes of a fragment read rows j, 8 + j, ..., 120 + j -- row bits
+// 3..5 give each group of 8 lanes distinct 16-byte chunks of its bank half
+__device__ __forceinline__ int bswz2(int r) { return (r >> 3) & 7; }
 
 // per-lane source offsets (bytes, relative to a K-tile's base) of the 8 LDS-DMA pieces this wave stages for one
 // operand -- the same for every tile (edges are handled by the resource's num_records). T = 0: [rows][K] operand,
 // piece P = 8 rows of 128 B (BI: the B image's swizzle); T = 1: [K][rows] operand, piece P = 4 k-rows x 128 columns
 // of half P >> 4.
-template <int T, bool BI = false, int PPW = 8>
+template <int T, bool BI = false, int PPW = 8, bool TL = false>
 __device__ __forceinline__ void piece_offsets(int (&vo)[PPW], long long ld, int wave, int lane) {
 #pragma unroll
   for (int q = 0; q < PPW; ++q) {
     const int P = wave * PPW + q;
     if (T == 0) {
       const int row = P * 8 + (lane >> 3);
-      const int c = (lane & 7) ^ (BI ? bswz(row) : ((row >> 1) & 7));
+      const int c = (lane & 7) ^ (BI ? (TL ? bswz2(row) : bswz(row)) : ((row >> 1) & 7));
       vo[q] = (int)(row * ld * 2) + c * 16;
     } else {
       const int h = P >> 4, kr = (P & 15) * 4 + (lane >> 4);
@@ -241,8 +244,20 @@ __device__ __forceinline__ bf16x8_t frag(const char* img, int rbase, int kk, int
 // CONSECUTIVE output columns nbase + 32p + 8g .. +7 (fragment 2p: +0..3, 2p+1: +4..7) and the epilogue stores
 // 16 bytes per lane without any cross-lane exchange. K-contiguous image: any row order is a gather of rows; the
 // transposed image: each lane of a ds_read_b64_tr_b16 group addresses its own 4-column chunk.
-template <int T>
+//
+// TL (K-contiguous B only): fragment j, operand column l reads tile column nbase + 8 l + j, and the MFMA takes the A
+// fragment first. A lane's accumulators then hold rows 4g .. 4g+3 of its row block, and over the 8 fragments the 8
+// CONSECUTIVE columns nbase + 8 l .. +7: lanes 0..15 of a store instruction write 256 contiguous bytes of one row
+// (bf16; 4 rows per instruction) -- the row-contiguous pattern the store path takes ~4x faster than 64-byte pieces
+// of 16 rows (tools/lab/store_bench.cpp). (The transposed image cannot: a ds_read_b64_tr_b16 group hands each lane
+// 4 consecutive columns of one fragment.)
+template <int T, bool TL = false>
 __device__ __forceinline__ bf16x8_t frag_b(const char* img, int nbase, int j, int kk, int lane) {
+  if constexpr (TL && T == 0) {
+    const int r = nbase + 8 * (lane & 15) + j;
+    const int c = kk * 4 + (lane >> 4);
+    return *reinterpret_cast<const bf16x8_t*>(img + r * 128 + ((c ^ bswz2(r)) << 4));
+  }
   const int base = nbase + 32 * (j >> 1) + 4 * (j & 1);
   if (T == 0) {
     const int r = base + 8 * ((lane & 15) >> 2) + (lane & 3);
@@ -396,10 +411,9 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
   constexpr bool RELAX = (OPT & 1) != 0, STAGGER = (OPT & 2) != 0, LATE = (OPT & 4) != 0;
   constexpr int SC = (OPT >> 3) & 7;   // cache policy of the direct epilogue's C stores
   constexpr bool ROWS = (OPT & 64) != 0;   // plain products: C rows staged through LDS, row-contiguous stores
-  // DEFER: a tile's last K-tile issues no LDS-DMA; its position (the next tile's second K-tile) is staged after the
-  // epilogue's stores, so the stores do not queue behind 32 in-flight 1 KiB loads per wave
-  constexpr bool DEFER = (OPT & 128) != 0;
-  static_assert(!(RELAX && DEFER), "RELAX counts the epilogue stores out of the first K-tile's waits: not with DEFER");
+  // TLAY: row-layout accumulators for K-contiguous B (frag_b): row-contiguous epilogue stores without data movement
+  constexpr bool TLAY = B_T == 0 && NWV == 4 && (OPT & 256) == 0 && !ROWS;
+
   static_assert(!(RELAX && LATE), "RELAX peels the first K-tile, LATE the last: not both");
   static_assert(SCH == 0 || NWV == 4, "the split schedule is laid out for one wave per SIMD");
   constexpr int WN = NWV == 4 ? 128 : 64;    // output columns per wave
@@ -435,7 +449,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
 
   int voa[PPW], vob[PPW];
   piece_offsets<A_T, false, PPW>(voa, p.lda, wave, lane);
-  piece_offsets<B_T, true, PPW>(vob, p.ldb, wave, lane);
+  piece_offsets<B_T, true, PPW, TLAY>(vob, p.ldb, wave, lane);
   const unsigned lds0 = lds_u32(smem);
   // this wave's PPW pieces of an operand image are contiguous: PPW KiB at (wave * PPW KiB)
   auto stage_a = [&](int s) -> unsigned { return lds0 + s * Q_STAGE + wave * PPW * 1024; };
@@ -497,9 +511,9 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
     const char* ia = smem + s * Q_STAGE;
     const char* ib = smem + s * Q_STAGE + Q_OP;
     if constexpr (r == 0) af[0] = frag<A_T>(ia, wm * 128, kk, lane);
-    else if constexpr (r == 1) bf[0] = frag_b<B_T>(ib, wn * WN, 0, kk, lane);
+    else if constexpr (r == 1) bf[0] = frag_b<B_T, TLAY>(ib, wn * WN, 0, kk, lane);
     else if constexpr (r < 9) af[r - 1] = frag<A_T>(ia, wm * 128 + (r - 1) * 16, kk, lane);
-    else bf[r - 8] = frag_b<B_T>(ib, wn * WN, r - 8, kk, lane);
+    else bf[r - 8] = frag_b<B_T, TLAY>(ib, wn * WN, r - 8, kk, lane);
   };
   using K0 = std::integral_constant<int, 0>;
   using K1 = std::integral_constant<int, 1>;
@@ -576,27 +590,29 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
       auto ktile = [&](auto fc, auto lc, int s) {
         constexpr bool FIRST = decltype(fc)::value && RELAX;
         constexpr bool NEXT0 = !(decltype(lc)::value && LATE);   // read pos+1's substep-0 fragments in this K-tile
-        constexpr bool NODMA = decltype(lc)::value && DEFER;     // deferred: no DMA (and pos+1's wait counts drop)
         const unsigned sa = stage_a(s), sb = stage_b(s);
         static_for<QS>([&](auto qc) {
           constexpr int q = decltype(qc)::value;
           constexpr int sub = q / (8 * JB), j = (q % (8 * JB)) / 8, i = q & 7;
-          if constexpr (sub == 0) mfma_acc(acc[i][j], b0[j], a0[i]);
-          else mfma_acc(acc[i][j], b1f[j], a1[i]);
+          if constexpr (TLAY) {   // A first: row-layout accumulators (frag_b)
+            if constexpr (sub == 0) mfma_acc(acc[i][j], a0[i], b0[j]);
+            else mfma_acc(acc[i][j], a1[i], b1f[j]);
+          } else {
+            if constexpr (sub == 0) mfma_acc(acc[i][j], b0[j], a0[i]);
+            else mfma_acc(acc[i][j], b1f[j], a1[i]);
+          }
           if constexpr (SCH == 0) {
             if constexpr (q < NR && !(G4W_EXP & 2)) read_sub(s, K1{}, qc, a1, b1f);   // substep-1 fragments of pos
-            if constexpr (q == NR && !NODMA) dma_setup();                       // resources of position pos + 2
+            if constexpr (q == NR) dma_setup();                                 // resources of position pos + 2
             if constexpr (q == QB1) {                                           // stage s fully read by every wave
               if constexpr (PROF) tw = __builtin_amdgcn_s_memtime();
               __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0) as a builtin: the compiler's wait model learns the
               if constexpr (!(G4W_EXP & 4)) __builtin_amdgcn_s_barrier();   // substep-1 reads are done
               if constexpr (PROF) sync1 += __builtin_amdgcn_s_memtime() - tw;
             }
-            if constexpr (!NODMA && !(G4W_EXP & 1) && q >= QA0 + SH && q < QA0 + SH + DQ * PPW &&
-                          (q - QA0 - SH) % DQ == 0)
+            if constexpr (!(G4W_EXP & 1) && q >= QA0 + SH && q < QA0 + SH + DQ * PPW && (q - QA0 - SH) % DQ == 0)
               dma16o<CPA, (q - QA0 - SH) / DQ * 1024>(ra, voa[(q - QA0 - SH) / DQ], sa);
-            if constexpr (!NODMA && !(G4W_EXP & 1) && q >= QB0 + SH && q < QB0 + SH + DQ * PPW &&
-                          (q - QB0 - SH) % DQ == 0)
+            if constexpr (!(G4W_EXP & 1) && q >= QB0 + SH && q < QB0 + SH + DQ * PPW && (q - QB0 - SH) % DQ == 0)
               dma16o<CPB, (q - QB0 - SH) / DQ * 1024>(rb, vob[(q - QB0 - SH) / DQ], sb);
             if constexpr (q == QW) {                                            // position pos+1 landed in stage s^1
               // first K-tile of a tile: the previous tile's epilogue stores sit between that position's DMAs and
@@ -604,7 +620,6 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
               // 64 fp32)
               if constexpr (PROF) tw = __builtin_amdgcn_s_memtime();
               if constexpr (FIRST) vm_wait<V0F>();
-              else if constexpr (NODMA) vm_wait<0>();   // nothing issued after pos+1's pieces
               else vm_wait<2 * PPW>();
               if constexpr (!(G4W_EXP & 4)) __builtin_amdgcn_s_barrier();
               if constexpr (PROF) sync2 += __builtin_amdgcn_s_memtime() - tw;
@@ -619,20 +634,19 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
             constexpr int db = g4s::idx(SCH == 2 ? g4s::DB2 : g4s::DB, q - SH);
             constexpr int ra0 = g4s::idx(g4s::A0N, q - SH), rb0 = g4s::idx(g4s::B0N, q - SH);
             if constexpr (ra1 >= 0) a1[ra1] = frag<A_T>(ia, wm * 128 + ra1 * 16, 1, lane);
-            if constexpr (rb1 >= 0) b1f[rb1] = frag_b<B_T>(ib, wn * WN, rb1, 1, lane);
-            if constexpr (q == g4s::SETUP && !NODMA) dma_setup();
+            if constexpr (rb1 >= 0) b1f[rb1] = frag_b<B_T, TLAY>(ib, wn * WN, rb1, 1, lane);
+            if constexpr (q == g4s::SETUP) dma_setup();
             if constexpr (q == g4s::BAR_A || q == g4s::BAR_B) {   // every wave done reading this stage's A / B image
               if constexpr (PROF) tw = __builtin_amdgcn_s_memtime();
               __builtin_amdgcn_s_waitcnt(0xc07f);
               __builtin_amdgcn_s_barrier();
               if constexpr (PROF) sync1 += __builtin_amdgcn_s_memtime() - tw;
             }
-            if constexpr (!NODMA && da >= 0) dma16o<CPA, (da < 0 ? 0 : da) * 1024>(ra, voa[da], sa);
-            if constexpr (!NODMA && db >= 0) dma16o<CPB, (db < 0 ? 0 : db) * 1024>(rb, vob[db], sb);
+            if constexpr (!(G4W_EXP & 1) && da >= 0) dma16o<CPA, (da < 0 ? 0 : da) * 1024>(ra, voa[da], sa);
+            if constexpr (!(G4W_EXP & 1) && db >= 0) dma16o<CPB, (db < 0 ? 0 : db) * 1024>(rb, vob[db], sb);
             if constexpr (q == g4s::WA || q == g4s::WB) {   // A / B image of position pos+1 landed in stage s^1
               if constexpr (PROF) tw = __builtin_amdgcn_s_memtime();
               if constexpr (FIRST) vm_wait<q == g4s::WA ? VAF : VBF>();
-              else if constexpr (NODMA) vm_wait<q == g4s::WA ? PPW : 0>();   // younger: pos+1's B pieces only
               else vm_wait<q == g4s::WA ? VA : VB>();
               __builtin_amdgcn_s_barrier();
               if constexpr (PROF) sync2 += __builtin_amdgcn_s_memtime() - tw;
@@ -640,7 +654,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
             if constexpr (NEXT0 && ra0 >= 0)
               a0[ra0] = frag<A_T>(smem + (s ^ 1) * Q_STAGE, wm * 128 + ra0 * 16, 0, lane);
             if constexpr (NEXT0 && rb0 >= 0)
-              b0[rb0] = frag_b<B_T>(smem + (s ^ 1) * Q_STAGE + Q_OP, wn * WN, rb0, 0, lane);
+              b0[rb0] = frag_b<B_T, TLAY>(smem + (s ^ 1) * Q_STAGE + Q_OP, wn * WN, rb0, 0, lane);
           }
           fence();
         });
@@ -656,13 +670,13 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
           ktile(F_{}, F_{}, pos & 1);
           dma_advance();
         }
-      } else if constexpr (LATE || DEFER) {   // the last K-tile peeled
+      } else if constexpr (LATE) {   // the last K-tile peeled
         for (int t = 0; t < ct.nk - 1; ++t, ++pos) {
           ktile(F_{}, F_{}, pos & 1);
           dma_advance();
         }
         ktile(F_{}, T_{}, pos & 1);
-        if constexpr (!DEFER) dma_advance();   // DEFER: the cursor's position is staged after the epilogue
+        dma_advance();
         ++pos;
       } else {
         for (int t = 0; t < ct.nk; ++t, ++pos) {
@@ -723,6 +737,101 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
         auto emit = [&](auto exc, auto edc, auto acc_) {
           constexpr bool EX = decltype(exc)::value, ED = decltype(edc)::value;
           constexpr int AC = decltype(acc_)::value;
+          if constexpr (TLAY) {
+            // row-layout accumulators (frag_b): lane (ml, gq) holds rows 16 i + 4 gq + r (r = 0..3) of the wave's
+            // block at columns 8 ml .. +7 (acc[i][0..7][r]); every store / side load covers 4 rows x 256 B (bf16) or
+            // 4 rows x 2 x 16 B per 32-byte chunk (fp32)
+            const int vt = ((wm * 128 + 4 * gq) * ldcs + wn * WN + 8 * ml) * ES;
+            const bool colok = !ED || ct.n0 + wn * WN + 8 * ml < p.N;
+            static_for<8>([&](auto ic) {
+              constexpr int i = decltype(ic)::value;
+              int vro[4];
+              v4u32_t side[4], side2[4], cl0[4], cl1[4];
+              static_for<4>([&](auto rk) {   // side inputs of the 4 rows first
+                constexpr int r = decltype(rk)::value;
+                vro[r] = vt + (16 * i + r) * ES * ldcs;
+                if constexpr (AC == 2) side[r] = __builtin_amdgcn_raw_buffer_load_b128(rzi, vro[r], 0, 0);
+                if constexpr (EX) {
+                  side[r] = __builtin_amdgcn_raw_buffer_load_b128(rr, vro[r], 0, 0);
+                  if constexpr (OUT_F32) {
+                    side2[r] = __builtin_amdgcn_raw_buffer_load_b128(rr, vro[r] + 16, 0, 0);
+                    if (beta != 0.f) {
+                      cl0[r] = __builtin_amdgcn_raw_buffer_load_b128(rc, vro[r], 0, 0);
+                      cl1[r] = __builtin_amdgcn_raw_buffer_load_b128(rc, vro[r] + 16, 0, 0);
+                    }
+                  }
+                }
+              });
+              v4u32_t o0[4], o1[4], zo[4];
+              static_for<4>([&](auto rk) {
+                constexpr int r = decltype(rk)::value;
+                float x[8];
+                static_for<8>([&](auto jc) {
+                  constexpr int j = decltype(jc)::value;
+                  x[j] = alpha * acc[i][j][r];
+                });
+                if constexpr (OUT_F32) {
+                  if constexpr (EX) {
+                    const f32x4_t ra = __builtin_bit_cast(f32x4_t, side[r]), rb = __builtin_bit_cast(f32x4_t, side2[r]);
+                    if (beta != 0.f) {
+                      const f32x4_t ca = __builtin_bit_cast(f32x4_t, cl0[r]), cb = __builtin_bit_cast(f32x4_t, cl1[r]);
+                      static_for<4>([&](auto tc) {
+                        constexpr int t = decltype(tc)::value;
+                        x[t] += beta * ca[t];
+                        x[4 + t] += beta * cb[t];
+                      });
+                    }
+                    if (p.R) {
+                      static_for<4>([&](auto tc) {
+                        constexpr int t = decltype(tc)::value;
+                        x[t] += ra[t];
+                        x[4 + t] += rb[t];
+                      });
+                    }
+                  }
+                  o0[r] = __builtin_bit_cast(v4u32_t, f32x4_t{x[0], x[1], x[2], x[3]});
+                  o1[r] = __builtin_bit_cast(v4u32_t, f32x4_t{x[4], x[5], x[6], x[7]});
+                } else {
+                  if constexpr (EX) {
+                    static_for<4>([&](auto tc) {
+                      constexpr int t = decltype(tc)::value;
+                      x[2 * t] += bf2f(side[r][t] & 0xffff);
+                      x[2 * t + 1] += bf2f(side[r][t] >> 16);
+                    });
+                  }
+                  if constexpr (AC == 1) {
+                    zo[r] = v4u32_t{pack_bf16x2(x[0], x[1]), pack_bf16x2(x[2], x[3]), pack_bf16x2(x[4], x[5]),
+                                    pack_bf16x2(x[6], x[7])};
+                    static_for<8>([&](auto tc) { x[decltype(tc)::value] = act_fwd(ACT_GELU, x[decltype(tc)::value]); });
+                  } else if constexpr (AC == 2) {
+                    static_for<4>([&](auto tc) {
+                      constexpr int t = decltype(tc)::value;
+                      x[2 * t] *= act_grad(ACT_GELU, bf2f(side[r][t] & 0xffff));
+                      x[2 * t + 1] *= act_grad(ACT_GELU, bf2f(side[r][t] >> 16));
+                    });
+                  }
+                  o0[r] = v4u32_t{pack_bf16x2(x[0], x[1]), pack_bf16x2(x[2], x[3]), pack_bf16x2(x[4], x[5]),
+                                  pack_bf16x2(x[6], x[7])};
+                }
+              });
+              static_for<4>([&](auto rk) {   // then every store (no activation code between them)
+                constexpr int r = decltype(rk)::value;
+                if constexpr (AC == 1) {
+                  if (zout && colok) store16_nc<SC>(zo[r], vro[r], rz4);
+                }
+                if (colok) {
+                  store16_nc<SC>(o0[r], vro[r], rc4);
+                  if constexpr (OUT_F32) store16_nc<SC>(o1[r], vro[r] + 16, rc4);
+                }
+              });
+              fence();
+            });
+            if constexpr (PROF) {
+              if (stamp) epi_issue += __builtin_amdgcn_s_memtime() - tmark;
+            }
+            if constexpr (EX || AC == 2 || (RELAX && (ED || AC != 0))) __builtin_amdgcn_s_waitcnt(0x0f70);
+            return;
+          }
           if constexpr (ROWS) {
             // ROWS: a lane's accumulators hold one row's 16-byte column chunk each, so a direct store instruction
             // writes 64-byte pieces of 16 rows; the store path takes ~4x longer for that pattern than for whole row
@@ -959,12 +1068,23 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
         constexpr int LPR = WN / 8;   // lanes per 16-row x WN round row (8 outputs each)
         static_for<8>([&](auto rcc) {
           constexpr int r = decltype(rcc)::value;
-          static_for<JB>([&](auto jc) {
-            constexpr int j = decltype(jc)::value;
-            const int row = lane & 15, c4 = 8 * (j >> 1) + 2 * (lane >> 4) + (j & 1);   // frag_b column order
-            *reinterpret_cast<float4*>(ep + row * WN + ((c4 ^ (row & 7)) << 2)) =
-                make_float4(alpha * acc[r][j][0], alpha * acc[r][j][1], alpha * acc[r][j][2], alpha * acc[r][j][3]);
-          });
+          if constexpr (TLAY) {   // rows 4 gq + t, columns 8 ml .. +7 (acc[r][0..7][t])
+            static_for<4>([&](auto tc) {
+              constexpr int t = decltype(tc)::value;
+              const int row = 4 * (lane >> 4) + t, c4 = 2 * (lane & 15);
+              *reinterpret_cast<float4*>(ep + row * WN + ((c4 ^ (row & 7)) << 2)) =
+                  make_float4(alpha * acc[r][0][t], alpha * acc[r][1][t], alpha * acc[r][2][t], alpha * acc[r][3][t]);
+              *reinterpret_cast<float4*>(ep + row * WN + (((c4 + 1) ^ (row & 7)) << 2)) =
+                  make_float4(alpha * acc[r][4][t], alpha * acc[r][5][t], alpha * acc[r][6][t], alpha * acc[r][7][t]);
+            });
+          } else {
+            static_for<JB>([&](auto jc) {
+              constexpr int j = decltype(jc)::value;
+              const int row = lane & 15, c4 = 8 * (j >> 1) + 2 * (lane >> 4) + (j & 1);   // frag_b column order
+              *reinterpret_cast<float4*>(ep + row * WN + ((c4 ^ (row & 7)) << 2)) =
+                  make_float4(alpha * acc[r][j][0], alpha * acc[r][j][1], alpha * acc[r][j][2], alpha * acc[r][j][3]);
+            });
+          }
   #pragma unroll 1
           for (int it = 0; it < 16 * LPR / 64; ++it) {
             const int row = it * (64 / LPR) + lane / LPR, c4 = (lane % LPR) * 2;
@@ -982,20 +1102,6 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
       if (stamp) {
         const unsigned long long now = __builtin_amdgcn_s_memtime();
         epi_clk += now - tmark;
-      }
-      if constexpr (DEFER) {   // the last K-tile's deferred position, into the stage that K-tile read (parity pos+1)
-        dma_setup();
-        const unsigned sa = stage_a((pos + 1) & 1), sb = stage_b((pos + 1) & 1);
-        static_for<PPW>([&](auto qc) {
-          constexpr int q = decltype(qc)::value;
-          dma16o<CPA, q * 1024>(ra, voa[q], sa);
-        });
-        static_for<PPW>([&](auto qc) {
-          constexpr int q = decltype(qc)::value;
-          dma16o<CPB, q * 1024>(rb, vob[q], sb);
-        });
-        dma_advance();
-        fence();
       }
     }
   };

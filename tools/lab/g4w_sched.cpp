@@ -82,10 +82,10 @@ struct Variant {
         launch_v<0, 0, false, SCH, STG, CPA, CPB, OPT, true>, launch_v<1, 1, true, SCH, STG, CPA, CPB, OPT> \
   }
 static const Variant variants[] = {
-    V("sch1", 1, false, 0, 0, 0),
-    V("sch1 rows", 1, false, 0, 0, 64),
-    V("sch1 defer rows", 1, false, 0, 0, 192),
-    V("sch1 rows late", 1, false, 0, 0, 68),
+    V("sch1 tlay", 1, false, 0, 0, 0),
+    V("sch1 old", 1, false, 0, 0, 256),
+    V("sch1 tlay relax", 1, false, 0, 0, 1),
+    V("sch0 tlay", 0, false, 0, 0, 0),
 };
 constexpr int NV = sizeof(variants) / sizeof(variants[0]);
 
