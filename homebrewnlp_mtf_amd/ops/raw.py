@@ -39,8 +39,8 @@ _ACT_G4W = __import__("os").environ.get("OBST_ACT_G4W", "0") == "1"
 
 
 def lt_enabled() -> int:
-    """plain GEMMs run on hipBLASLt (csrc/kernels/blaslt.cpp; OBST_GEMM_LT=0 keeps every GEMM on the MFMA kernels,
-    2 tries hipBLASLt's own GELU epilogues instead of the plain GEMM + elementwise split)"""
+    """0 (default): every GEMM on the hand-written gfx950 MFMA kernels (gemm4w); OBST_GEMM_LT=1 hands the plain
+    products to hipBLASLt (csrc/kernels/blaslt.cpp, A/B only), 2 also tries its own GELU epilogues"""
     global _LT
     if _LT is None:
         _LT = int(L.lib().obst_blaslt_enabled())
