@@ -399,6 +399,30 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(float* __restrict__ 
   }
 }
 
+// batched split-K fold: C[b] (+ beta C[b]) = sum_s ws[b][s] for nb = nb1 x nb2 batches (C batch strides c_s1 / c_s2)
+__global__ __launch_bounds__(256) void splitk_reduce_batched_kernel(float* __restrict__ C, const float* __restrict__ ws,
+                                                                    long long mn, long long ldc, int N, int ks,
+                                                                    float beta, int nb, int nb2, long long c_s1,
+                                                                    long long c_s2) {
+  const long long nv = mn / 4, tot = nv * nb;
+  for (long long u = (long long)blockIdx.x * 256 + threadIdx.x; u < tot; u += (long long)gridDim.x * 256) {
+    const long long b = u / nv, v = u % nv;
+    const long long e = v * 4, m = e / N, n = e % N;
+    const float* wb = ws + b * ks * mn;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int s = 0; s < ks; ++s) {
+      const float4 w = reinterpret_cast<const float4*>(wb + s * mn)[v];
+      acc.x += w.x; acc.y += w.y; acc.z += w.z; acc.w += w.w;
+    }
+    float4* c = reinterpret_cast<float4*>(C + (b / nb2) * c_s1 + (b % nb2) * c_s2 + m * ldc + n);
+    if (beta != 0.f) {
+      const float4 o = *c;
+      acc.x += beta * o.x; acc.y += beta * o.y; acc.z += beta * o.z; acc.w += beta * o.w;
+    }
+    *c = acc;
+  }
+}
+
 float* splitk_workspace(size_t bytes) {
   static float* buf = nullptr;
   static size_t cap = 0;
@@ -535,19 +559,21 @@ OBST_API int obst_gemm(const ObstGemmDesc* d, hipStream_t stream) {
     // ceil(tiles * ks / 256) rounds of K / ks each; a split costs a deterministic fold over ks fp32 slabs. Pick the
     // ks of least modelled time (1.25 us per 64-deep K-tile of a tile, ~5 TB/s for the fold), workspace <= 1 GiB.
     int ks = 1;
-    if (ksplit_env > 0 && big_tiles < 512 && d->out_f32 && !d->R && !d->act && d->mode == 0 && batch == 1 &&
-        d->tri == 0) {
+    // batched products too (the per-head group-linear weight gradients: few tiles per batch); C batch strides must
+    // keep 16-byte alignment for the fold
+    if (ksplit_env > 0 && big_tiles < 512 && d->out_f32 && !d->R && !d->act && d->mode == 0 && d->tri == 0 &&
+        (batch == 1 || (d->c_s1 % 4 == 0 && d->c_s2 % 4 == 0 && d->ldc % 4 == 0))) {
       const double per_k = 1.25 / 64.0;   // us per K element of one tile
       double best = 1e300;
-      for (int c = 1; c <= 8; c *= 2) {
-        if (d->K % (64 * c) || (c > 1 && d->K / c < 512) || (size_t)c * d->M * d->N * 4 > (1ull << 30)) continue;
+      for (int c = 1; c <= 16; c *= 2) {
+        if (d->K % (64 * c) || (c > 1 && d->K / c < 512) || (size_t)c * batch * d->M * d->N * 4 > (1ull << 30)) continue;
         const double rounds = (double)((big_tiles * c + 255) / 256);
         const double t = rounds * (d->K / c) * per_k +
-                         (c > 1 ? (double)(c + (d->beta != 0.f ? 2 : 1)) * d->M * d->N * 4.0 / 5e6 : 0.0);
+                         (c > 1 ? (double)(c + (d->beta != 0.f ? 2 : 1)) * batch * d->M * d->N * 4.0 / 5e6 : 0.0);
         if (t < best * 0.98) { best = t; ks = c; }
       }
       if (ks > 1) {
-        a.ws = splitk_workspace((size_t)ks * d->M * d->N * sizeof(float));
+        a.ws = splitk_workspace((size_t)ks * batch * d->M * d->N * sizeof(float));
         if (!a.ws) ks = 1;
       }
     }
@@ -555,8 +581,13 @@ OBST_API int obst_gemm(const ObstGemmDesc* d, hipStream_t stream) {
     e = gemm4w_launch(&a, d->a_t, d->b_t, d->out_f32, batch, stream);
     if (e == hipSuccess && d->out_f32 && a.ksplit > 1) {
       const long long mn = (long long)a.M * a.N;
-      hipLaunchKernelGGL(splitk_reduce_kernel, dim3(2048), dim3(256), 0, stream, reinterpret_cast<float*>(a.C), a.ws,
-                         mn, a.ldc, a.N, a.ksplit, a.beta);
+      if (batch == 1)
+        hipLaunchKernelGGL(splitk_reduce_kernel, dim3(2048), dim3(256), 0, stream, reinterpret_cast<float*>(a.C),
+                           a.ws, mn, a.ldc, a.N, a.ksplit, a.beta);
+      else
+        hipLaunchKernelGGL(splitk_reduce_batched_kernel, dim3(2048), dim3(256), 0, stream,
+                           reinterpret_cast<float*>(a.C), a.ws, mn, a.ldc, a.N, a.ksplit, a.beta, batch, a.nb2,
+                           a.c_s1, a.c_s2);
       e = hipGetLastError();
     }
     ++g_4w_calls;

@@ -285,7 +285,7 @@ struct Tile4 {
   const char* b;
   long long arem, brem;
   long long coff;
-  int m0, n0, split;
+  int m0, n0, split, wsi;
   int nk;   // K-tiles of this tile (the K range of a triangular A, see decode4)
 };
 
@@ -319,8 +319,9 @@ __device__ __forceinline__ Tile4 decode4(const GemmArgs& p, long long L64) {
   }
   T.m0 = tm * 256;
   T.n0 = tn * 256;
-  T.split = (int)(ybat % (unsigned)p.ksplit);
+  T.split = (int)(ybat % (unsigned)p.ksplit);   // split-K slab: ws [batch][split][M][N] (fold: splitk_reduce)
   const unsigned bidx = ybat / (unsigned)p.ksplit;
+  T.wsi = (int)ybat;
   const long long b1 = bidx / (unsigned)p.nb2, b2 = bidx % (unsigned)p.nb2;
   long long kbeg = (long long)T.split * (p.K / p.ksplit);
   T.nk = p.K / p.ksplit / 64;
@@ -707,7 +708,8 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
         const bool ws_out = OUT_F32 && p.ksplit > 1;
         const long long ldc = ws_out ? p.N : p.ldc;
         constexpr int ES = OUT_F32 ? 4 : 2;
-        char* cbase = ws_out ? reinterpret_cast<char*>(p.ws + (long long)ct.split * p.M * p.N)
+        // split-K partials: slab (batch, split) = ybat of the tile (decode4: ybat = batch * ksplit + split)
+        char* cbase = ws_out ? reinterpret_cast<char*>(p.ws + (long long)ct.wsi * p.M * p.N)
                              : reinterpret_cast<char*>(p.C) + ct.coff * ES;
         const long long corg = ((long long)ct.m0 * ldc + ct.n0) * ES;
         const long long cext = ((long long)(p.M - ct.m0 - 1) * ldc + (p.N - ct.n0)) * ES;   // bytes to C's end

@@ -522,6 +522,28 @@ def test_gemm_splitk_wgrad(cuda, lt, a_t, b_t, M, N, K):
         assert g4w_calls() - c0 == 1, "the MFMA leg did not run gemm4w"
 
 
+@pytest.mark.parametrize("beta", [0.0, 1.0])
+def test_gemm4w_batched_splitk(cuda, beta):
+    """batched fp32 weight gradients with few tiles per batch (the per-head group linear: gw[h] = x[:, h]^T dy[:, h]):
+    gemm4w splits K into per-(batch, split) fp32 slabs and folds them per batch into the strided C"""
+    torch.manual_seed(8)
+    H, K, N, M = 4, 256, 512, 16384    # gw[h][K][N] over M tokens: 4 x 2 tiles per launch without the split
+    x = (torch.randn(M, H, K) * 0.5).to(BF)
+    dy = (torch.randn(M, H, N) * 0.5).to(BF)
+    ref = torch.einsum("mhk,mhn->hkn", x.float(), dy.float()) + (2.0 if beta else 0.0)
+    old = raw.lt_set(0)
+    try:
+        c0 = g4w_calls()
+        G = torch.full((H, K, N), 2.0, dtype=torch.float32, device=cuda)
+        raw.gemm(raw.Operand(x.to(cuda), 1, H * K, K), raw.Operand(dy.to(cuda), 1, H * N, N),
+                 raw.Operand(G, 0, N, K * N), K, N, M, batch=(H, 1), beta=beta)
+        torch.cuda.synchronize()
+        assert g4w_calls() - c0 == 1
+    finally:
+        raw.lt_set(old)
+    _close(G.cpu(), ref, 5e-2 * math.sqrt(M / 16384), 1e-2, f"batched split-K beta {beta}")
+
+
 @pytest.mark.parametrize("a_t,b_t", [(0, 1), (1, 0), (0, 0)])
 @pytest.mark.parametrize("beta", [0.0, 1.0])
 def test_blaslt_splitk_wgrad(cuda, a_t, b_t, beta):
