@@ -696,9 +696,12 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
         tmark = now;
       }
 
-      // gelu GEMMs (bf16, no residual) take the direct epilogue too: forward with the pre-activation kept in Zout,
-      // backward C = acc * gelu'(Zin); each variant's activation is straight-line code (no per-value switch)
-      const bool gelu_direct = !OUT_F32 && p.act == ACT_GELU && p.R == nullptr &&
+      // gelu / relu GEMMs (bf16, no residual) take the direct epilogue too: forward with the pre-activation kept in
+      // Zout, backward C = acc * act'(Zin); each variant's activation is straight-line code (no per-value switch).
+      // (relu through the LDS-path epilogue was 768 us per 65536 x 4096 x 256 product of ctx32_mixer: 179 TF/s)
+      // (relu on the row-layout path only: with both activations the fragment-layout copies hit the compiler's
+      // "illegal VGPR to SGPR copy")
+      const bool gelu_direct = !OUT_F32 && (p.act == ACT_GELU || (TLAY && p.act == ACT_RELU)) && p.R == nullptr &&
                                ((p.mode == 0) || (p.mode == 1 && p.Zin != nullptr));
       if (!(G4W_EXP & 16) && ((p.act == 0 && p.mode == 0 && p.Zout == nullptr) || gelu_direct)) {
         // Direct epilogue (every plain product): each lane owns C[m][n..n+3] of 64 fragments and writes it with one
@@ -719,7 +722,8 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
         const int ml = lane & 15, gq = lane >> 4;
         const float alpha = p.alpha, beta = ws_out ? 0.f : p.beta;
 
-        const bool edge = !ROWS && ct.n0 + wn * WN + WN > p.N;   // ROWS masks columns per lane in one copy
+        // ROWS / TLAY mask columns per lane at run time in one copy of each variant
+        const bool edge = !ROWS && !TLAY && ct.n0 + wn * WN + WN > p.N;
         const bool extra = (OUT_F32 && beta != 0.f) || (p.R != nullptr && !ws_out);
         // fragment pair (2p, 2p+1) = 8 consecutive columns per lane (frag_b): 16 B (bf16) / 2 x 16 B (fp32) stores,
         // 32 / 64 per wave (64 bf16 stores with the 32 LDS-DMAs in flight overflowed the 63-entry vmcnt)
@@ -738,13 +742,16 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
         // AC: 0 no activation, 1 gelu forward (+ Zout), 2 gelu backward (Zin)
         auto emit = [&](auto exc, auto edc, auto acc_) {
           constexpr bool EX = decltype(exc)::value, ED = decltype(edc)::value;
-          constexpr int AC = decltype(acc_)::value;
+          constexpr int AC_ = decltype(acc_)::value;
+          // AC_: 1 / 2 gelu forward / backward, 3 / 4 relu forward / backward -> AC (1 forward, 2 backward) + ACTK
+          constexpr int AC = AC_ == 0 ? 0 : (AC_ == 1 || AC_ == 3) ? 1 : 2;
+          constexpr int ACTK = AC_ >= 3 ? ACT_RELU : ACT_GELU;
           if constexpr (TLAY) {
             // row-layout accumulators (frag_b): lane (ml, gq) holds rows 16 i + 4 gq + r (r = 0..3) of the wave's
             // block at columns 8 ml .. +7 (acc[i][0..7][r]); every store / side load covers 4 rows x 256 B (bf16) or
             // 4 rows x 2 x 16 B per 32-byte chunk (fp32)
             const int vt = ((wm * 128 + 4 * gq) * ldcs + wn * WN + 8 * ml) * ES;
-            const bool colok = !ED || ct.n0 + wn * WN + 8 * ml < p.N;
+            const bool colok = ct.n0 + wn * WN + 8 * ml < p.N;
             static_for<8>([&](auto ic) {
               constexpr int i = decltype(ic)::value;
               int vro[4];
@@ -804,12 +811,12 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
                   if constexpr (AC == 1) {
                     zo[r] = v4u32_t{pack_bf16x2(x[0], x[1]), pack_bf16x2(x[2], x[3]), pack_bf16x2(x[4], x[5]),
                                     pack_bf16x2(x[6], x[7])};
-                    static_for<8>([&](auto tc) { x[decltype(tc)::value] = act_fwd(ACT_GELU, x[decltype(tc)::value]); });
+                    static_for<8>([&](auto tc) { x[decltype(tc)::value] = act_fwd(ACTK, x[decltype(tc)::value]); });
                   } else if constexpr (AC == 2) {
                     static_for<4>([&](auto tc) {
                       constexpr int t = decltype(tc)::value;
-                      x[2 * t] *= act_grad(ACT_GELU, bf2f(side[r][t] & 0xffff));
-                      x[2 * t + 1] *= act_grad(ACT_GELU, bf2f(side[r][t] >> 16));
+                      x[2 * t] *= act_grad(ACTK, bf2f(side[r][t] & 0xffff));
+                      x[2 * t + 1] *= act_grad(ACTK, bf2f(side[r][t] >> 16));
                     });
                   }
                   o0[r] = v4u32_t{pack_bf16x2(x[0], x[1]), pack_bf16x2(x[2], x[3]), pack_bf16x2(x[4], x[5]),
@@ -911,13 +918,13 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
                     static_for<8>([&](auto tc) { x[decltype(tc)::value] += y[decltype(tc)::value]; });
                   }
                   if constexpr (AC == 1) {
-                    static_for<8>([&](auto tc) { x[decltype(tc)::value] = act_fwd(ACT_GELU, x[decltype(tc)::value]); });
+                    static_for<8>([&](auto tc) { x[decltype(tc)::value] = act_fwd(ACTK, x[decltype(tc)::value]); });
                   } else if constexpr (AC == 2) {
                     float z[8];
                     unpack8(side[r], z);
                     static_for<8>([&](auto tc) {
                       constexpr int t = decltype(tc)::value;
-                      x[t] *= act_grad(ACT_GELU, z[t]);
+                      x[t] *= act_grad(ACTK, z[t]);
                     });
                   }
                   out[r] = v4u32_t{pack_bf16x2(x[0], x[1]), pack_bf16x2(x[2], x[3]), pack_bf16x2(x[4], x[5]),
@@ -1006,14 +1013,14 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
                                  vrow, rz4, std::integral_constant<int, pp * 64>{});
   #pragma unroll
                 for (int t = 0; t < 4; ++t) {
-                  va[t] = act_fwd(ACT_GELU, va[t]);
-                  vb[t] = act_fwd(ACT_GELU, vb[t]);
+                  va[t] = act_fwd(ACTK, va[t]);
+                  vb[t] = act_fwd(ACTK, vb[t]);
                 }
               } else if constexpr (AC == 2) {
   #pragma unroll
                 for (int t = 0; t < 4; ++t) {
-                  va[t] *= act_grad(ACT_GELU, x[2 * pp][t]);
-                  vb[t] *= act_grad(ACT_GELU, x[2 * pp + 1][t]);
+                  va[t] *= act_grad(ACTK, x[2 * pp][t]);
+                  vb[t] *= act_grad(ACTK, x[2 * pp + 1][t]);
                 }
               }
               if constexpr (OUT_F32) {
@@ -1038,13 +1045,20 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
         };
         using A0 = std::integral_constant<int, 0>;
         if constexpr (!OUT_F32) {
-          if (gelu_direct) {
+          if (gelu_direct && p.act == ACT_GELU) {
             using A1 = std::integral_constant<int, 1>;
             using A2 = std::integral_constant<int, 2>;
             if (p.mode == 1) {
               if (edge) emit(F_{}, T_{}, A2{}); else emit(F_{}, F_{}, A2{});
             } else {
               if (edge) emit(F_{}, T_{}, A1{}); else emit(F_{}, F_{}, A1{});
+            }
+          } else if (gelu_direct) {   // relu (TLAY only)
+            if constexpr (TLAY) {
+              using A3 = std::integral_constant<int, 3>;
+              using A4 = std::integral_constant<int, 4>;
+              if (p.mode == 1) emit(F_{}, F_{}, A4{});
+              else emit(F_{}, F_{}, A3{});
             }
           } else if (extra) {
             if (edge) emit(T_{}, T_{}, A0{}); else emit(T_{}, F_{}, A0{});

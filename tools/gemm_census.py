@@ -26,21 +26,21 @@ _on = [False]
 
 
 def _wrapped(a, b, c, M, N, K, batch=(1, 1), alpha=1.0, beta=0.0, act=None, act_bwd=False, R=None, Zout=None,
-             Zin=None, tri=0):
+             Zin=None, tri=0, **kw):
     if not _on[0]:
-        return _orig(a, b, c, M, N, K, batch, alpha, beta, act, act_bwd, R, Zout, Zin, tri)
+        return _orig(a, b, c, M, N, K, batch, alpha, beta, act, act_bwd, R, Zout, Zin, tri, **kw)
     frame = {"nested": False}
     if _stack:
         _stack[-1]["nested"] = True
     _stack.append(frame)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
-    out = _orig(a, b, c, M, N, K, batch, alpha, beta, act, act_bwd, R, Zout, Zin, tri)
+    out = _orig(a, b, c, M, N, K, batch, alpha, beta, act, act_bwd, R, Zout, Zin, tri, **kw)
     e1.record()
     _stack.pop()
     if not frame["nested"]:
         sig = (M, N, K, a.trans, b.trans, a.ld, b.ld, str(c.t.dtype)[6:], beta != 0.0, R is not None,
-               batch[0] * batch[1], act or "", int(act_bwd), tri)
+               batch[0] * batch[1], act or "", int(act_bwd), tri, int(kw.get("kin", 0) or 0))
         _records.append((sig, e0, e1))
     return out
 
