@@ -395,7 +395,8 @@ constexpr int idx(const int (&a)[8], int q) {
 #endif
 
 #ifndef G4W_OPT
-#define G4W_OPT 0   // 1: RELAX, 4: LATE -- both within +-1 % of plain SCH 1 (profiles/r4_gemm_sched.md)
+#define G4W_OPT 0   // 4: LATE (row layout: epilogue 8.6k -> 6.5k clocks, +0.5-1 % per shape in the lab, but the
+                    // step measured 137.2k vs 138.8k tokens/s: off); 1: RELAX
 #endif
 // OPT bits (schedule options under A/B, tools/lab/g4w_sched.cpp):
 //   1 RELAX: the first K-tile of every tile is a separate (peeled) copy whose waits count the previous tile's

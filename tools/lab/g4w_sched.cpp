@@ -83,9 +83,9 @@ struct Variant {
   }
 static const Variant variants[] = {
     V("sch1 tlay", 1, false, 0, 0, 0),
-    V("sch1 old", 1, false, 0, 0, 256),
+    V("sch1 tlay stag", 1, false, 0, 0, 2),
     V("sch1 tlay relax", 1, false, 0, 0, 1),
-    V("sch0 tlay", 0, false, 0, 0, 0),
+    V("sch1 tlay late", 1, false, 0, 0, 4),
 };
 constexpr int NV = sizeof(variants) / sizeof(variants[0]);
 
