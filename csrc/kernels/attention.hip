@@ -851,7 +851,16 @@ __global__ __launch_bounds__(NW * 64, KG == 1 ? 2 : 1) void attn_bwd_dkv_kernel(
   const int key = kw + i;
   vm_wait<0>();   // staged tiles (asm LDS-DMA: the compiler does not track them) have landed
   __syncthreads();
-  for (int c = 0; c < nqc; ++c) {
+  // Chunks in three branch-free runs: masked (causal diagonal band of the whole block, or every chunk when the block's
+  // keys run past S), unmasked, masked (a ragged last chunk). A per-chunk masked / unmasked branch merged the dK / dV
+  // accumulators of its two arms: 64 v_mov per chunk in a VALU-bound kernel (profiles/r3_attn_bwd_ab.md). A chunk
+  // entirely before a wave's keys contributes exactly zero under the mask, so no per-wave skip either.
+  const bool all_mask = kblk + KB > a.S;
+  const int c_diag = a.causal ? min(nqc, (kblk + KB - 1 - qstart + QC - 1) / QC) : 0;
+  const int cm1 = all_mask ? nqc : c_diag;
+  const int cm2 = all_mask ? nqc : max(cm1, (qstart + nqc * QC > a.S) ? nqc - 1 : nqc);
+  auto chunk = [&](int c, auto mk) {
+    constexpr bool MK = decltype(mk)::value;
     const int q0 = qstart + c * QC;
     const char* sQ = smem + (c % NS) * STAGE;
     const char* sD = sQ + TILE;
@@ -859,13 +868,7 @@ __global__ __launch_bounds__(NW * 64, KG == 1 ? 2 : 1) void attn_bwd_dkv_kernel(
     const float* sDl = sL + 64;
     const int cn = c + NS - 1;
     if (cn < nqc) stage(smem + (cn % NS) * STAGE, qstart + cn * QC);
-    if (!(a.causal && q0 + QC - 1 < kw)) {  // every query of this chunk precedes this wave's keys
-      const bool need_mask = (a.causal && q0 < kw + KW - 1) || q0 + QC > a.S || kw + KW > a.S;
-      if (need_mask)
-        dkv_chunk<D, true, KG, QC / 16>(sQ, sD, sL, sDl, kf, vf, dk, dv, q0, key, a.S, a.causal, c2, lane, a.prio & 1);
-      else
-        dkv_chunk<D, false, KG, QC / 16>(sQ, sD, sL, sDl, kf, vf, dk, dv, q0, key, a.S, a.causal, c2, lane, a.prio & 1);
-    }
+    dkv_chunk<D, MK, KG, QC / 16>(sQ, sD, sL, sDl, kf, vf, dk, dv, q0, key, a.S, a.causal, c2, lane, a.prio & 1);
     // chunk c + 1 must have landed; chunks c + 2 .. c + NS - 2 may stay in flight across the barrier. Per chunk a
     // wave issues PPW pieces, plus the lse / delta pieces: NW = 4 wave 0 issues both, NW = 8 waves 0 and 1 one each
     const int ahead = min(NS - 2, nqc - 2 - c);
@@ -881,7 +884,10 @@ __global__ __launch_bounds__(NW * 64, KG == 1 ? 2 : 1) void attn_bwd_dkv_kernel(
       vm_wait<0>();
     }
     __syncthreads();
-  }
+  };
+  for (int c = 0; c < cm1; ++c) chunk(c, std::true_type{});
+  for (int c = cm1; c < cm2; ++c) chunk(c, std::false_type{});
+  for (int c = cm2; c < nqc; ++c) chunk(c, std::true_type{});
   if constexpr (D == 128 && NW * 2 * KW * 256 <= NS * STAGE) {   // dK, dV through LDS as whole rows (epi_put)
     char* sk = smem + w * 2 * KW * 256;
     char* sv = sk + KW * 256;
