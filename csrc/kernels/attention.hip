@@ -596,19 +596,18 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_bwd_dq_kernel(AttnArgs a) {
   const float c2 = a.scale * LOG2E;
   vm_wait<0>();   // staged tiles (asm LDS-DMA: the compiler does not track them) have landed
   __syncthreads();
-  for (int kb = 0; kb < nkb; ++kb) {
+  // key tiles in two branch-free runs: unmasked, then masked (the causal diagonal band of the whole block, and a ragged
+  // last tile). A per-tile branch merged the dQ accumulators of its two arms (v_mov per tile); a tile past a wave's
+  // queries contributes exactly zero under the mask, and the block waits for its slowest wave at every barrier anyway
+  const int kbm = a.causal ? min(nkb, (qblk + 1) / KT) : ((nkb * KT > a.S) ? nkb - 1 : nkb);
+  auto tile = [&](int kb, auto mk) {
+    constexpr bool MK = decltype(mk)::value;
     const int k0 = kb * KT;
     const char* sK = smem + (kb % NS) * 2 * TILE;
     const char* sV = sK + TILE;
     const int kn = kb + NS - 1;   // tile issued now; its slot was last read in iteration kb - 1 (behind a barrier)
     if (kn < nkb) stage_kv(smem + (kn % NS) * 2 * TILE, kn);
-    if (!(a.causal && k0 > qw + 31)) {
-      const bool need_mask = (a.causal && k0 + KT - 1 > qw) || k0 + KT > a.S;
-      if (need_mask)
-        dq_tile<D, true, KT / 32>(sK, sV, qf, df, lse2, dlt, acc, k0, qw, a.S, a.causal, c2, lane, a.prio & 2);
-      else
-        dq_tile<D, false, KT / 32>(sK, sV, qf, df, lse2, dlt, acc, k0, qw, a.S, a.causal, c2, lane, a.prio & 2);
-    }
+    dq_tile<D, MK, KT / 32>(sK, sV, qf, df, lse2, dlt, acc, k0, qw, a.S, a.causal, c2, lane, a.prio & 2);
     // tile kb + 1 must have landed; tiles kb + 2 .. kb + NS - 2 may stay in flight across the barrier (counted
     // wait: the only vector-memory ops of this loop are the DMA pieces, PPW per wave per tile)
     const int ahead = min(NS - 2, nkb - 2 - kb);
@@ -616,6 +615,16 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_bwd_dq_kernel(AttnArgs a) {
     else if (NS >= 3 && ahead >= 1) vm_wait<PPW>();
     else vm_wait<0>();
     __syncthreads();
+  };
+  if (a.prio & 4) {   // A/B (OBST_ATTN_PRIO bit 2): the per-tile masked-or-not branch of rounds 1-3
+    for (int kb = 0; kb < nkb; ++kb) {
+      const int k0 = kb * KT;
+      if ((a.causal && k0 + KT - 1 > qw) || k0 + KT > a.S) tile(kb, std::true_type{});
+      else tile(kb, std::false_type{});
+    }
+  } else {
+    for (int kb = 0; kb < kbm; ++kb) tile(kb, std::false_type{});
+    for (int kb = kbm; kb < nkb; ++kb) tile(kb, std::true_type{});
   }
   if constexpr (D == 128 && NW * 32 * 256 <= NS * 2 * TILE) {   // dQ through LDS as whole rows (epi_put)
     char* so = smem + w * 32 * 256;
@@ -885,9 +894,17 @@ __global__ __launch_bounds__(NW * 64, KG == 1 ? 2 : 1) void attn_bwd_dkv_kernel(
     }
     __syncthreads();
   };
-  for (int c = 0; c < cm1; ++c) chunk(c, std::true_type{});
-  for (int c = cm1; c < cm2; ++c) chunk(c, std::false_type{});
-  for (int c = cm2; c < nqc; ++c) chunk(c, std::true_type{});
+  if (a.prio & 4) {   // A/B (OBST_ATTN_PRIO bit 2): the per-chunk masked-or-not branch of rounds 1-3
+    for (int c = 0; c < nqc; ++c) {
+      const int q0 = qstart + c * QC;
+      if ((a.causal && q0 < kw + KW - 1) || q0 + QC > a.S || kw + KW > a.S) chunk(c, std::true_type{});
+      else chunk(c, std::false_type{});
+    }
+  } else {
+    for (int c = 0; c < cm1; ++c) chunk(c, std::true_type{});
+    for (int c = cm1; c < cm2; ++c) chunk(c, std::false_type{});
+    for (int c = cm2; c < nqc; ++c) chunk(c, std::true_type{});
+  }
   if constexpr (D == 128 && NW * 2 * KW * 256 <= NS * STAGE) {   // dK, dV through LDS as whole rows (epi_put)
     char* sk = smem + w * 2 * KW * 256;
     char* sv = sk + KW * 256;
