@@ -616,7 +616,7 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_bwd_dq_kernel(AttnArgs a) {
     else vm_wait<0>();
     __syncthreads();
   };
-  if (a.prio & 4) {   // A/B (OBST_ATTN_PRIO bit 2): the per-tile masked-or-not branch of rounds 1-3
+  if (a.prio & 8) {   // A/B (OBST_ATTN_PRIO bit 3): the per-tile masked-or-not branch of rounds 1-3
     for (int kb = 0; kb < nkb; ++kb) {
       const int k0 = kb * KT;
       if ((a.causal && k0 + KT - 1 > qw) || k0 + KT > a.S) tile(kb, std::true_type{});
@@ -894,7 +894,7 @@ __global__ __launch_bounds__(NW * 64, KG == 1 ? 2 : 1) void attn_bwd_dkv_kernel(
     }
     __syncthreads();
   };
-  if (a.prio & 4) {   // A/B (OBST_ATTN_PRIO bit 2): the per-chunk masked-or-not branch of rounds 1-3
+  if (a.prio & 8) {   // A/B (OBST_ATTN_PRIO bit 3): the per-chunk masked-or-not branch of rounds 1-3
     for (int c = 0; c < nqc; ++c) {
       const int q0 = qstart + c * QC;
       if ((a.causal && q0 < kw + KW - 1) || q0 + QC > a.S || kw + KW > a.S) chunk(c, std::true_type{});
@@ -1176,23 +1176,34 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd32_kernel(AttnArgs a)
   const float c2 = a.scale * LOG2E;
   vm_wait<0>();
   __syncthreads();
-  for (int kb = 0; kb < nkb; ++kb) {
+  // key tiles in two branch-free runs, unmasked then the block's masked band (as in the backward kernels): the
+  // per-tile branch merged O, m and l of its two arms. Fully masked tiles of the lower waves add exactly nothing (the
+  // first tile, key 0, makes every row's running max finite) and run while those waves would wait at the barrier.
+  const int kbm = a.causal ? min(nkb, (qblk + 1) / KT) : ((nkb * KT > a.S) ? nkb - 1 : nkb);
+  auto tile = [&](int kb, auto mk) {
+    constexpr bool MK = decltype(mk)::value;
     const int k0 = kb * KT;
     const char* sK = smem + (kb % NS) * 2 * TILE;
     const char* sV = sK + TILE;
     const int kn = kb + NS - 1;   // its slot was last read in iteration kb - 1 (behind the barrier)
     if (kn < nkb) stage(smem + (kn % NS) * 2 * TILE, kn * KT);
-    if (!(a.causal && k0 > qw + 31)) {
-      const bool need_mask = (a.causal && k0 + KT - 1 > qw) || k0 + KT > a.S;
-      if (need_mask) fwd32_tile<true, KT / 32>(sK, sV, qf, o, m, l, k0, q, a.S, a.causal, c2, lane, a.prio & 4);
-      else fwd32_tile<false, KT / 32>(sK, sV, qf, o, m, l, k0, q, a.S, a.causal, c2, lane, a.prio & 4);
-    }
+    fwd32_tile<MK, KT / 32>(sK, sV, qf, o, m, l, k0, q, a.S, a.causal, c2, lane, a.prio & 4);
     // tile kb + 1 has landed; tiles kb + 2 .. kb + NS - 2 may stay in flight (2 NP pieces per wave per tile)
     const int ahead = min(NS - 2, nkb - 2 - kb);
     if (NS >= 4 && ahead >= 2) vm_wait<4 * NP>();
     else if (NS >= 3 && ahead >= 1) vm_wait<2 * NP>();
     else vm_wait<0>();
     __syncthreads();
+  };
+  if (!(a.prio & 16)) {   // (bit 4 selects the branch-free runs, under validation; bit 3 is the backward's A/B)
+    for (int kb = 0; kb < nkb; ++kb) {   // the per-tile branch of rounds 1-3
+      const int k0 = kb * KT;
+      if ((a.causal && k0 + KT - 1 > qw) || k0 + KT > a.S) tile(kb, std::true_type{});
+      else tile(kb, std::false_type{});
+    }
+  } else {
+    for (int kb = 0; kb < kbm; ++kb) tile(kb, std::false_type{});
+    for (int kb = kbm; kb < nkb; ++kb) tile(kb, std::true_type{});
   }
   l = xh_sum(l);
   const float inv = 1.f / l;
