@@ -1195,11 +1195,23 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd32_kernel(AttnArgs a)
     else vm_wait<0>();
     __syncthreads();
   };
-  if (!(a.prio & 16)) {   // (bit 4 selects the branch-free runs, under validation; bit 3 is the backward's A/B)
-    for (int kb = 0; kb < nkb; ++kb) {   // the per-tile branch of rounds 1-3
+  if (!(a.prio & 16)) {   // default: the per-tile branch with its skip of the tiles past a wave's queries (bit 4,
+    // the branch-free runs, measured within 1 %: profiles/r4_attn_branchfree_ab.txt)
+    for (int kb = 0; kb < nkb; ++kb) {
       const int k0 = kb * KT;
-      if ((a.causal && k0 + KT - 1 > qw) || k0 + KT > a.S) tile(kb, std::true_type{});
-      else tile(kb, std::false_type{});
+      if (a.causal && k0 > qw + 31) {   // nothing of this tile for this wave: keep the ring's staging and barrier
+        const int kn = kb + NS - 1;
+        if (kn < nkb) stage(smem + (kn % NS) * 2 * TILE, kn * KT);
+        const int ahead = min(NS - 2, nkb - 2 - kb);
+        if (NS >= 4 && ahead >= 2) vm_wait<4 * NP>();
+        else if (NS >= 3 && ahead >= 1) vm_wait<2 * NP>();
+        else vm_wait<0>();
+        __syncthreads();
+      } else if ((a.causal && k0 + KT - 1 > qw) || k0 + KT > a.S) {
+        tile(kb, std::true_type{});
+      } else {
+        tile(kb, std::false_type{});
+      }
     }
   } else {
     for (int kb = 0; kb < kbm; ++kb) tile(kb, std::false_type{});
