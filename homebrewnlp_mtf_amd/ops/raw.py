@@ -186,13 +186,18 @@ class Operand(typing.NamedTuple):
 # OBST_SKINNY_GEMM=1: decode-step projections (M <= 32 tokens) on the MFMA weight-streaming kernel
 # (csrc/kernels/skinny.hip) instead of hipBLASLt. Both read the cached K-contiguous weight copy; graph-replayed per
 # call the kernel takes 6.0-15.4 us where hipBLASLt takes 5.3-12.4 us on the GPT-Neo-1.3B projections (70 vs 32 us
-# on the 50304-wide logits, profiles/r2_skinny_gemm.txt), so it stays opt-in.
-_SKINNY = __import__("os").environ.get("OBST_SKINNY_GEMM", "0") == "1"
+# on the 50304-wide logits, profiles/r2_skinny_gemm.txt) -- with hipBLASLt as the default it stayed opt-in.
+# Default ("auto"): on whenever hipBLASLt is off (the default) -- a 32-row product on gemm4w fills one 256-row tile
+# row per N tile, a few CUs for ~50 us where the weight-streaming kernel takes 6-15 us.
+_SKINNY_ENV = __import__("os").environ.get("OBST_SKINNY_GEMM", "auto")
+_SKINNY = None if _SKINNY_ENV == "auto" else _SKINNY_ENV == "1"
 _SKINNY_WS: typing.Dict[typing.Any, torch.Tensor] = {}
 
 
 def skinny_ok(M: int, N: int, K: int) -> bool:
-    return _SKINNY and 0 < M <= 32 and N % 16 == 0 and K % 32 == 0
+    if not (0 < M <= 32 and N % 16 == 0 and K % 32 == 0):
+        return False
+    return _SKINNY if _SKINNY is not None else lt_enabled() == 0
 
 
 def _skinny_ws(device, n: int) -> typing.Optional[torch.Tensor]:
