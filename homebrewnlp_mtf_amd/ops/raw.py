@@ -241,11 +241,15 @@ def gemm(a: Operand, b: Operand, c: Operand, M: int, N: int, K: int, batch: typi
         L.check(L.lib().obst_skinny_gemm(a.t.data_ptr(), a.ld, b.t.data_ptr(), b.ld, c.t.data_ptr(), c.ld, M, N, K,
                                          L.ptr(ws), L.stream_ptr()), "skinny_gemm")
         return c.t
-    if (not kin and on_gpu(c.t) and act is not None and tri == 0 and lt_enabled() == 1 and lt_scope() > 0
-            and not _ACT_G4W
+    if (not kin and on_gpu(c.t) and act is not None and tri == 0
+            and ((lt_enabled() == 1 and lt_scope() > 0 and not _ACT_G4W)
+                 # decode-step activation products: the skinny kernel + the elementwise pass (a 32-row product with
+                 # a fused epilogue on gemm4w keeps a 256-row tile row on a few CUs: ~45 us a call)
+                 or (skinny_ok(M, N, K) and R is None and alpha == 1.0 and a.trans == 0 and b.trans == 0))
             and c.t.dtype == torch.bfloat16
             and b1 * b2 == 1 and c.ld == N and (M * N) % 8 == 0 and c.t.is_contiguous() and c.t.numel() == M * N):
-        # activation GEMM on hipBLASLt: plain product, then the elementwise kernel (pre-activation kept in Zout)
+        # activation GEMM on hipBLASLt / the skinny kernel: plain product, then the elementwise kernel (pre-activation
+        # kept in Zout)
         if not act_bwd:
             z = Zout if Zout is not None else torch.empty(M * N, dtype=torch.bfloat16, device=c.t.device)
             gemm(a, b, Operand(z, 0, N), M, N, K, alpha=alpha, R=R)
