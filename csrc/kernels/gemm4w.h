@@ -11,11 +11,11 @@
 //  * A K-tile (BK = 64) is two k-substeps of 32. Fragments of substep 0 and substep 1 live in separate registers
 //    (2 x 128 VGPRs), so the LDS image of tile t is dead as soon as its substep-1 fragments are read -- after 16
 //    of the tile's 128 MFMAs. From then on the same LDS stage receives tile t+2 by LDS-DMA (buffer_load ... lds,
-//    16 B per lane, 1 KiB per wave-instruction, source address = SGPR resource + one constant per-lane offset),
-//    interleaved one piece per ~5 MFMAs. Two LDS stages of 64 KiB; two barriers per K-tile:
-//      barrier 1 (after the substep-1 reads, lgkmcnt(0)): every wave is done reading stage s -> DMA into it;
-//      barrier 2 (after a counted vmcnt(16): this tile's 16 DMAs stay in flight): tile t+1 has landed in stage
-//      s^1 -> the substep-0 fragments of tile t+1 are read under the last 20 MFMAs of tile t.
+//    16 B per lane, 1 KiB per wave-instruction, source address = SGPR resource + one constant per-lane offset).
+//    Two LDS stages of 64 KiB. Default schedule (SCH 1, the K-loop structure of hipBLASLt's 256x256x64 gfx950 kernel
+//    as read from its code object, profiles/r4_gemm_sched.md): per-operand barrier pairs -- A / B image of stage s
+//    free (lgkmcnt(0) + barrier), then DMA bursts into it; A / B of tile t+1 landed (counted vmcnt + barrier), then
+//    its substep-0 fragments are read under the last MFMAs of tile t. SCH 0 is the round-3 two-barrier schedule.
 //    The instruction order is pinned with sched_barrier(0) fences; the compiler only allocates registers and
 //    counts lgkmcnt for the fragment reads. Out-of-range prefetches (t+2 >= nk) re-read the last tile into the
 //    stage nobody reads any more, so the loop has no branches.
@@ -23,9 +23,15 @@
 //    conflict-free ds_read_b128 fragment reads); row-contiguous operands ([K][rows]) as two [64 k][128 rows]
 //    halves (256-B rows, chunk ^= kswz(k)) read with the CDNA4 transposing ds_read_b64_tr_b16. The swizzle lives
 //    in the per-lane SOURCE address (LDS-DMA writes lane-linearly).
-//  * The MFMA is issued as mfma(B, A) so each lane ends with 4 consecutive output columns of one row; the
-//    epilogue (alpha, beta, residual, activation with pre-activation output, activation backward, fp32 split-K
-//    slabs) is the shared epilogue_store of gemm_kern.h.
+//  * Accumulator layout. K-contiguous B (TLAY, the default for it): the MFMA takes the A fragment first and B
+//    fragment j reads tile columns 8 l + j, so a lane holds 4 rows x 8 consecutive columns and every epilogue store
+//    instruction writes 4 rows x 256 B (the store path takes ~4x longer for 16 rows x 64 B, store_bench.cpp).
+//    Transposed B: mfma(B, A) with paired column permutation, each lane 8 consecutive columns of one row.
+//  * Epilogues: direct from the accumulators for plain products, gelu / relu forward (+ pre-activation output) and
+//    backward, residual, fp32 accumulate and split-K slabs (batched too); the rest through a wave-private LDS region
+//    and the shared epilogue_store of gemm_kern.h.
+//  * Hand-written buffer ops lead with s_nop 4: the resource SGPRs may come straight from a VALU write (spill
+//    reloads), which the compiler's hazard recognizer does not pad for inline asm (tools/sgpr_hazard.py).
 #pragma once
 #include "common.h"
 #include "gemm_kern.h"
