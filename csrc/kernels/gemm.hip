@@ -560,9 +560,11 @@ OBST_API int obst_gemm(const ObstGemmDesc* d, hipStream_t stream) {
     // ks of least modelled time (1.25 us per 64-deep K-tile of a tile, ~5 TB/s for the fold), workspace <= 1 GiB.
     int ks = 1;
     // batched products too (the per-head group-linear weight gradients: few tiles per batch); C batch strides must
-    // keep 16-byte alignment for the fold
+    // keep 16-byte alignment for the fold. The folds index float4s of rows (m = e / N, e < M * N / 4): N and ldc
+    // must be multiples of 4 (the entry checks already require 8; restated here so the fold's own contract is local)
     if (ksplit_env > 0 && big_tiles < 512 && d->out_f32 && !d->R && !d->act && d->mode == 0 && d->tri == 0 &&
-        (batch == 1 || (d->c_s1 % 4 == 0 && d->c_s2 % 4 == 0 && d->ldc % 4 == 0))) {
+        d->N % 4 == 0 && d->ldc % 4 == 0 &&
+        (batch == 1 || (d->c_s1 % 4 == 0 && d->c_s2 % 4 == 0))) {
       const double per_k = 1.25 / 64.0;   // us per K element of one tile
       double best = 1e300;
       for (int c = 1; c <= 16; c *= 2) {

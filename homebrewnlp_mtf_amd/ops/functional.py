@@ -145,8 +145,10 @@ def _fwd_gemm(x2, w, y2, plan: LinearPlan, act=None, R=None, Zout=None):
 # Row-parallel forward under TP (the weight contracts the sharded heads: every rank holds a partial sum of the whole
 # output): the product runs in OBST_TP_CHUNKS token blocks and each block's all-reduce starts on RCCL's stream as soon
 # as its GEMM is done, so the next block's GEMM overlaps it -- only the last block's all-reduce stays exposed. Blocks
-# stay >= 4096 tokens (a whole number of 256-row tiles, ~full-rate GEMMs).
-_TP_CHUNKS = max(int(__import__("os").environ.get("OBST_TP_CHUNKS", "4")), 1)
+# stay >= 4096 tokens (a whole number of 256-row tiles, ~full-rate GEMMs). Opt-in (default 1 block): the persistent
+# GEMM loses about the run time of any kernel that holds CUs beside it (profiles/r4_cu_contention.md) and splitting
+# adds tile tails, so the overlap is unproven until a TP > 1 RCCL measurement shows a gain.
+_TP_CHUNKS = max(int(__import__("os").environ.get("OBST_TP_CHUNKS", "1")), 1)
 _TP_MIN_ROWS = int(__import__("os").environ.get("OBST_TP_MIN_ROWS", "4096"))   # (tests: tiny blocks)
 
 
@@ -711,10 +713,20 @@ _MAP_WS = {}
 
 
 def _map_workspace(device, numel: int) -> torch.Tensor:
+    """per-device fp32 scratch of the attention-map backward (reused across calls). Grown only outside stream
+    capture: a buffer first allocated under capture belongs to the graph's private pool, so it is handed out for
+    that capture alone and never cached for eager calls (the trainer's eager warm-up step sizes the cache)."""
     ws = _MAP_WS.get(device)
     if ws is None or ws.numel() < numel:
+        if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+            return torch.empty(numel, dtype=torch.float32, device=device)
         ws = _MAP_WS[device] = torch.empty(numel, dtype=torch.float32, device=device)
     return ws[:numel]
+
+
+def release_workspaces() -> None:
+    """drop the cached per-device scratch buffers (attention-map backward); the next call re-allocates"""
+    _MAP_WS.clear()
 
 
 class _AttnMap(torch.autograd.Function):

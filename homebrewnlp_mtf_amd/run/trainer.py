@@ -181,6 +181,15 @@ class Trainer:
                 self._capture(parity, learning_rate(self.params, self.global_step))
         return True
 
+    def close(self) -> None:
+        """release the captured step graphs (and their private memory pool) and the ops' cached scratch buffers"""
+        from ..ops import functional as F
+        self._graph = None
+        F.release_workspaces()
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+            torch.cuda.empty_cache()
+
     # ---------------------------------------------------------------------------------------------------------------
     def _multi_loss_step(self, batch):
         """token and video losses get separate (DP-averaged) gradients, combined per SURVEY A8 -- the reference

@@ -116,6 +116,7 @@ def test_tp_matches_single_rank(strategy, monkeypatch):
     if strategy == "chunked_forward_reduce":
         # row-parallel forwards in 16-token blocks, each block's all-reduce overlapping the next block's GEMM
         monkeypatch.setenv("OBST_TP_MIN_ROWS", "16")
+        monkeypatch.setenv("OBST_TP_CHUNKS", "4")   # opt-in (default 1 block)
     ranks = _run("tp", cfg)
     if strategy == "intermediate_layout":
         ffn = [n for n in ranks[0]["specs"] if "feed_forward" in n]

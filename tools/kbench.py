@@ -59,6 +59,27 @@ def line_key(row: dict) -> str:
     return row["kernel"] + (f" {row['shape']}" if "shape" in row else "")
 
 
+def section_of(key: str) -> str:
+    """the kbench section (command-line `what`) that emits a floor key"""
+    if key.startswith("gemm"):
+        return "gemm"
+    if key.startswith("mixer"):
+        return "mixer"
+    if key.startswith("attention_map"):
+        return "attn_map"
+    if key.startswith("attention"):
+        return "attn"
+    if key.startswith("norm"):
+        return "norm"
+    return "ew"
+
+
+def missing(floors: dict, seen: set, sections) -> list:
+    """floor keys of the sections that ran but that no emitted row carries (a renamed / dropped kernel or shape
+    must not silently skip its floor)"""
+    return sorted(k for k in floors if section_of(k) in sections and k not in seen)
+
+
 def check(rows, floors: dict, tol: float = 0.05):
     """-> list of (key, metric, value, floor) for every floored metric below floor * (1 - tol); higher is better for
     every metric in the floor file (TF/s, PF/s, GB/s)"""
@@ -240,9 +261,12 @@ def main(argv=None):
         seen = {line_key(r) for r in EMITTED}
         for key, metric, v, floor in bad:
             print(f"REGRESSION {key}: {metric} {v} < floor {floor} - {a.tol:.0%}", flush=True)
+        gone = missing(floors, seen, todo)
+        for key in gone:
+            print(f"MISSING {key}: floored but not emitted by its section", flush=True)
         n = sum(len(m) for k, m in floors.items() if k in seen)
-        print(f"kbench check: {n - len(bad)}/{n} floored metrics pass", flush=True)
-        if bad:
+        print(f"kbench check: {n - len(bad)}/{n} floored metrics pass, {len(gone)} floored keys missing", flush=True)
+        if bad or gone:
             sys.exit(1)
 
 

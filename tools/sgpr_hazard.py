@@ -21,8 +21,17 @@ WAIT = 5
 LLVM = "/opt/rocm/lib/llvm/bin"
 
 
+# SALU / control ops that read SGPRs but write none (their first operand is a source): they do not end a hazard
+NO_SDST = ("s_cmp", "s_bitcmp", "s_cbranch", "s_branch", "s_setreg", "s_setprio", "s_sleep", "s_sendmsg", "s_trap",
+           "s_waitcnt", "s_barrier", "s_nop", "s_endpgm", "s_set_gpr_idx", "s_dcache", "s_icache", "s_incperflevel",
+           "s_decperflevel", "s_ttracedata", "s_setkill")
+M0 = -1   # m0 (the LDS-DMA destination base) as a pseudo-SGPR
+
+
 def sgprs(tok):
     tok = tok.strip()
+    if tok == "m0":
+        return {M0}
     m = re.match(r"s\[(\d+):(\d+)\]$", tok)
     if m:
         return set(range(int(m.group(1)), int(m.group(2)) + 1))
@@ -61,8 +70,14 @@ def scan(text, name="<asm>"):
         op = line.split()[0]
         args = line[len(op):].split(",")
         ws = int(args[0], 0) + 1 if op == "s_nop" else 1
-        if op.startswith("buffer_") and len(args) >= 4:
-            reads = sgprs(args[2]) | sgprs(args[3].split()[0])
+        lds = op.startswith("buffer_") and re.search(r"\slds\b", line) is not None
+        if op.startswith("buffer_") and (len(args) >= 4 or (lds and len(args) >= 3)):
+            # LDS-DMA form `buffer_load_dwordx4 vaddr, srsrc, soffset offen lds` (no VGPR destination; reads m0)
+            # vs `buffer_op vdata, vaddr, srsrc, soffset ...`
+            if lds and len(args) == 3:
+                reads = sgprs(args[1]) | sgprs(args[2].split()[0]) | {M0}
+            else:
+                reads = sgprs(args[2]) | sgprs(args[3].split()[0]) | ({M0} if lds else set())
             for w, age, src in hist:
                 if w & reads and age < WAIT:
                     out.append(f"{name}:{ln}: {line}  <- {src} ({age} wait states) in {func[:70]}")
@@ -70,8 +85,8 @@ def scan(text, name="<asm>"):
             w = sgprs(args[0])
             if w:
                 hist.append((w, -ws, f"{op} {args[0].strip()}"))
-        if op.startswith("s_") and args and op not in ("s_nop", "s_waitcnt", "s_barrier"):
-            w = sgprs(args[0])   # an SALU rewrite of the SGPR ends its hazard
+        if op.startswith("s_") and args and not op.startswith(NO_SDST):
+            w = sgprs(args[0])   # an SALU rewrite of the SGPR ends its hazard (only ops with an SGPR destination)
             hist = [(h - w, a, s) for h, a, s in hist if h - w]
         hist = [(h, a + ws, s) for h, a, s in hist if a + ws < 16]
     return out
