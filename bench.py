@@ -185,7 +185,12 @@ def main():
                        # plain GEMMs: "gemm4w" = every product on the hand-written gfx950 kernel (no library GEMM)
                        "gemm": gemm,
                        "comm_mib_per_step": ({k: round(b / max(args.steps, 1) / 2 ** 20, 2)
-                                              for k, (c, b) in comm.items()} if world > 1 else None)}}),
+                                              for k, (c, b) in comm.items()} if world > 1 else None),
+                       # DP gradient reduction: buckets per step and wire dtype (bf16 = fp32-accumulated slices)
+                       "dp_buckets": len(trainer.grad_sync.buckets) if dp > 1 else None,
+                       "dp_wire": params.allreduce_dtype if dp > 1 else None,
+                       "dp_wire_mib_per_step": (round(trainer.grad_sync.wire_bytes_per_step() / 2 ** 20, 1)
+                                                if dp > 1 else None)}}),
               flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -97,8 +97,10 @@ _DEFAULTS: typing.Dict[str, typing.Any] = dict(
     shared_key_value_mixing=True,  # shared_key_value attention mixes the keys (P K); False: the reference's
                                    # rowsum(P) * key (quirk A19, spatial.py:63-64,81 -- no mixing, docs/PARITY.md)
     seed=0,                      # parameter-init seed
-    grad_bucket_mb=64,           # DP gradient all-reduce bucket size (xGMI ring per-link bound: SURVEY 5.8)
-    allreduce_dtype="float32",   # dtype gradients travel in over RCCL
+    grad_bucket_mb=0,            # DP gradient bucket size in MiB of fp32; 0: the buffer in 12 buckets (>= 16 MiB)
+    allreduce_dtype="bfloat16",  # DP wire dtype: bf16 with fp32 accumulation (all-to-all + sum + all-gather), or
+                                 # "float32" (one fp32 all-reduce per bucket)
+    force_grad_sync=False,       # run the DP collectives at world 1 too (tests of the capture path on one GPU)
     use_hip_graphs=False,        # capture the whole training step in hipGraphs (Trainer._graph_step; 1 GPU, no dropout)
     # also capture with world > 1 (the RCCL all-reduces inside the graph; opt-in: RCCL graph capture is exercised only
     # where several GPUs are visible, which the 1-GPU test boxes are not)

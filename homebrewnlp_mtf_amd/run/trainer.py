@@ -52,7 +52,8 @@ class Trainer:
                                                                                                         params)
         self.grad_sync = GradSync(self.store, self.mesh.dp_group, self.mesh.dp, params.grad_bucket_mb,
                                   {"float32": torch.float32, "bfloat16": torch.bfloat16}[params.allreduce_dtype],
-                                  use_counts=self.model.builder.use_counts)
+                                  use_counts=self.model.builder.use_counts,
+                                  force=bool(getattr(params, "force_grad_sync", False)))
         self.global_step = int(params.current_step)
 
     # ---------------------------------------------------------------------------------------------------------------

@@ -20,6 +20,7 @@ CFG = dict(model_mode="gpt", use_video=False, use_language=True, heads=4, featur
            sequence_length=16, train_batch_size=4, vocab_size=64, intermediate_feed_forward_multiplier=2,
            memory_reduction_strategy="none", calculation_dtype="float32", learning_rate=0.01,
            optimizer="adaptive_clip:0.003-sm3-momentum:0.9:1:1-learning_rate", weight_decay=0.01,
+           allreduce_dtype="float32",   # exactness checks against one rank; the bf16 wire has its own test
            block_config=[{"layer": ["norm-shift-scale", "attention-dot_product-context"], "skip": True},
                          {"layer": ["norm-shift-scale-group", "feed_forward-in:gelu"], "skip": True}])
 
@@ -52,7 +53,8 @@ def _worker(rank, world, port, cfg, mode, out_dir):
     for _ in range(2):
         m = tr.step(b)
         losses.append(float(m["loss"]))
-    torch.save({"master": tr.store.master.clone(), "losses": losses,
+    torch.save({"master": tr.store.master.clone(), "losses": losses, "wire": tr.grad_sync.wire_bytes_per_step(),
+                "buckets": len(tr.grad_sync.buckets),
                 "specs": {n: (s.offset, s.numel, s.tp_dim) for n, s in tr.store.specs.items()}},
                os.path.join(out_dir, f"r{rank}.pt"))
     dist.barrier()
@@ -174,7 +176,7 @@ def test_collective_sequence_check():
 MIXER_CFG = dict(model_mode="gpt", use_video=False, use_language=True, heads=4, features_per_head=8, depth=2,
                  sequence_length=16, train_batch_size=4, vocab_size=32, group_linear_factor=2,
                  intermediate_feed_forward_multiplier=1, memory_reduction_strategy="revnet",
-                 calculation_dtype="float32", learning_rate=0.01,
+                 calculation_dtype="float32", learning_rate=0.01, allreduce_dtype="float32",
                  optimizer="adaptive_clip:0.003-sm3-momentum:0.9:1:1-learning_rate",
                  block_config=[{"layer": ["norm-shift-scale-features-group",
                                           "bottleneck_group_linear-in:relu-mid:relu-mid:norm-mid:shift-mid:scale-mid:features"]},
@@ -236,10 +238,10 @@ def test_tp_optimizer_chains_match_single_rank(chain):
 
 
 def test_dp_bf16_wire_close_to_fp32_wire():
-    """allreduce_dtype="bfloat16" (opt-in; fp32 by default): the DP buckets travel as bf16 (half the xGMI bytes) and
-    are summed back into the fp32 gradient buffer. After two steps the fp32 masters stay within bf16 rounding of the
-    gradients of the fp32-wire run, and the two replicas stay identical."""
-    fp = _run("dp")
+    """allreduce_dtype="bfloat16" (the default): the DP buckets travel as bf16 (half the xGMI bytes) -- all-to-all,
+    fp32 sum of this rank's slice, all-gather -- and land in the fp32 gradient buffer. After two steps the fp32
+    masters stay within bf16 rounding of the fp32-wire run's update, and the two replicas stay identical."""
+    fp = _run("dp", dict(CFG, allreduce_dtype="float32"))
     bf = _run("dp", dict(CFG, allreduce_dtype="bfloat16"))
     assert torch.equal(bf[0]["master"], bf[1]["master"]), "bf16-wire DP replicas diverged"
     init = _single(dict(CFG, learning_rate=0.0))[0].store.master
@@ -247,8 +249,39 @@ def test_dp_bf16_wire_close_to_fp32_wire():
     upd_bf = bf[0]["master"] - init
     rel = (upd_bf - upd_fp).norm() / upd_fp.norm()
     assert 0 < rel < 2e-2, f"bf16 wire moved the update by {rel:.3g} relative"
+    assert bf[0]["wire"] * 2 == fp[0]["wire"] or abs(bf[0]["wire"] * 2 - fp[0]["wire"]) < 64, (bf[0]["wire"],
+                                                                                               fp[0]["wire"])
     for a, b in zip(fp[0]["losses"], bf[0]["losses"]):
         assert abs(a - b) < 1e-3 * abs(a)
+
+
+def test_dp_buckets_sized_from_the_model():
+    """grad_bucket_mb = 0 (default): the gradient buffer in ~12 buckets of >= 16 MiB (GPT-Neo-1.3B: 12 reductions a
+    step instead of ~80 fixed 64 MiB ones); an explicit size still wins"""
+    from homebrewnlp_mtf_amd.parallel.grad_sync import GradSync, bucket_cap
+
+    class _Spec:
+        def __init__(self, offset, numel):
+            self.offset, self.numel = offset, numel
+
+    class _Store:
+        def __init__(self, sizes):
+            self.order = [f"v{i}" for i in range(len(sizes))]
+            self.specs, o = {}, 0
+            for n, k in zip(self.order, sizes):
+                self.specs[n] = _Spec(o, k)
+                o += k
+            self.grad = torch.zeros(o)
+
+    # 1.34 B parameters in 218 tensors, roughly GPT-Neo-1.3B's size mix
+    sizes = [50304 * 2048] + [2048 * 6144, 2048 * 2048, 2048 * 8192, 8192 * 2048, 2048, 2048] * 24 + [2048, 2048]
+    gs = GradSync(_Store(sizes), None, 8)
+    assert 10 <= len(gs.buckets) <= 13, len(gs.buckets)
+    assert bucket_cap(1000, 0) == 16 * 2 ** 20 // 4            # small models: one >= 16 MiB bucket
+    assert len(GradSync(_Store(sizes), None, 8, bucket_mb=64).buckets) > 60
+    # every variable in exactly one bucket, buckets contiguous and in reverse registration order
+    seen = [v for _, _, vs in gs.buckets for v in vs]
+    assert sorted(seen) == sorted(gs.store.order) and seen[0] == gs.store.order[-1]
 
 
 def _ckpt_worker(rank, world, port, cfg, out_dir):

@@ -37,7 +37,7 @@ def _batch(i):
     return {"token_x": toks[:, :-1].contiguous(), "token_y": toks[:, 1:].contiguous()}
 
 
-def _worker(rank, world, port, mode, out_dir):
+def _worker(rank, world, port, mode, out_dir, wire="bfloat16"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     dev = torch.device("cuda", 0)
@@ -46,7 +46,7 @@ def _worker(rank, world, port, mode, out_dir):
     mesh = pstate.Mesh(dp=dp, tp=tp, rank=rank).build_groups()
     torch.manual_seed(0)
     extra = {"tp_layout": "intermediate"} if mode == "tp_intermediate" else {}
-    tr = Trainer(ModelParameter(dict(CFG, mesh={"dp": dp, "tp": tp}, **extra)), dev, mesh)
+    tr = Trainer(ModelParameter(dict(CFG, mesh={"dp": dp, "tp": tp}, allreduce_dtype=wire, **extra)), dev, mesh)
     losses = []
     for i in range(3):
         b = {k: v.to(dev) for k, v in _batch(i).items()}
@@ -62,9 +62,9 @@ def _worker(rank, world, port, mode, out_dir):
     dist.destroy_process_group()
 
 
-def _run(mode):
+def _run(mode, wire="bfloat16"):
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(2, _free_port(), mode, d), nprocs=2, join=True)
+        mp.spawn(_worker, args=(2, _free_port(), mode, d, wire), nprocs=2, join=True)
         return [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True) for r in range(2)]
 
 
@@ -77,8 +77,11 @@ def _single(cuda):
     return tr, losses
 
 
-def test_gpu_dp_matches_single_rank(cuda):
-    ranks = _run("dp")
+@pytest.mark.parametrize("wire", ["bfloat16", "float32"])
+def test_gpu_dp_matches_single_rank(cuda, wire):
+    """both DP wires: bf16 with fp32 accumulation (default; all-to-all + side-stream fp32 sum + all-gather) and the
+    fp32 all-reduce"""
+    ranks = _run("dp", wire)
     ref, ref_losses = _single(cuda)
     assert torch.equal(ranks[0]["master"], ranks[1]["master"]), "DP replicas diverged"
     for i in range(3):   # each rank's loss is its half-batch mean
@@ -128,6 +131,25 @@ def test_rccl_collectives_world1():
     assert len(rows) == 8 and all(x["backend"] == "nccl" and x["world"] == 1 and x["us"] > 0 for x in rows)
 
 
+def test_rccl_graph_capture_world1():
+    """RCCL inside captured graphs on a one-rank nccl group (tools/graph_capture_probe.py): an async all_reduce +
+    wait captured and replayed equals eager, and the Trainer's whole-step capture with the DP collectives inside
+    (hip_graphs_distributed, GradSync forced on at world 1, bf16 wire with its side stream) matches the eager run"""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=root, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "1", "--master-addr",
+                        "127.0.0.1", "--master-port", str(_free_port()),
+                        os.path.join(root, "tools", "graph_capture_probe.py")],
+                       capture_output=True, text=True, env=env, timeout=240)
+    rows = [json.loads(line) for line in r.stdout.splitlines() if line.startswith("{")]
+    assert rows, r.stderr[-3000:]
+    print(rows[0])
+    assert r.returncode == 0 and rows[0]["ok"], rows[0]
+
+
 def _bench_rehearsal(world, extra, timeout=280):
     """bench.py's N > 1 path as the driver launches it (torch.distributed.run, one process per rank, MAX over ranks,
     rank 0 prints one JSON line), rehearsed with gloo ranks sharing cuda:0"""
@@ -151,7 +173,8 @@ def _bench_rehearsal(world, extra, timeout=280):
 def test_bench_two_rank_rehearsal():
     row = _bench_rehearsal(2, ["--batch-per-gpu", "2", "--depth", "2"])
     assert row["config"]["parallelism"] == "dp2" and row["config"]["global_batch"] == 4
-    assert row["config"]["comm_mib_per_step"]["dp_all_reduce"] > 0
+    assert row["config"]["comm_mib_per_step"]["dp_all_to_all"] > 0   # the bf16 wire (default)
+    assert row["config"]["dp_buckets"] >= 1 and row["config"]["dp_wire"] == "bfloat16"
 
 
 @pytest.mark.parametrize("world,tp", [(2, 2), (4, 2)])
@@ -164,7 +187,7 @@ def test_bench_tp_rehearsal(world, tp):
     assert row["config"]["global_batch"] == dp
     comm = row["config"]["comm_mib_per_step"]
     assert comm["tp_all_reduce"] > 0
-    assert (comm.get("dp_all_reduce", 0) > 0) == (dp > 1)
+    assert (comm.get("dp_all_to_all", 0) > 0) == (dp > 1)
 
 
 def test_gpt_neo_20b_tp8_fits_per_rank():

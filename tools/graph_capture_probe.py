@@ -1,0 +1,95 @@
+"""RCCL collectives inside a captured hipGraph, on a one-rank ``nccl`` group (the 1-GPU box; the 8-GPU bench runs the
+same code with ``--hip-graphs-dist 1``):
+
+  1. an async ``all_reduce`` + ``wait`` captured in ``torch.cuda.graph`` and replayed matches the eager result;
+  2. the bf16-wire DP reduction (all-to-all, fp32 slice sum on a side stream, all-gather; parallel/grad_sync.py) and
+     the whole training step captured by ``Trainer`` (``use_hip_graphs`` + ``hip_graphs_distributed``, GradSync forced
+     on at world 1) give the eager Trainer's losses and weights.
+
+  python -m torch.distributed.run --nproc-per-node 1 --master-addr 127.0.0.1 tools/graph_capture_probe.py
+
+Prints one JSON line with the checks; exit status 1 when one fails.
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    from homebrewnlp_mtf_amd.config import ModelParameter
+    from homebrewnlp_mtf_amd.parallel import state as pstate
+    from homebrewnlp_mtf_amd.run.trainer import Trainer
+
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", device_id=dev)
+    out = {}
+
+    # 1. async all_reduce + wait inside a captured graph
+    x = torch.arange(1 << 20, dtype=torch.float32, device=dev)
+    y = torch.empty_like(x)
+    eager = x * 3.0
+    dist.all_reduce(eager)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):   # warm-up outside capture (communicator init, RCCL plans)
+        y.copy_(x * 3.0)
+        dist.all_reduce(y, async_op=True).wait()
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        y.copy_(x * 3.0)
+        w = dist.all_reduce(y, async_op=True)
+        w.wait()
+        z = y + 1.0
+    y.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    out["captured_all_reduce"] = bool(torch.equal(z, eager + 1.0))
+
+    # 2. Trainer step captured with the DP collectives inside (world 1, GradSync forced on)
+    cfg = dict(model_mode="gpt", use_video=False, use_language=True, heads=4, features_per_head=64, depth=2,
+               sequence_length=128, train_batch_size=4, vocab_size=512, intermediate_feed_forward_multiplier=2,
+               memory_reduction_strategy="none", calculation_dtype="bfloat16", learning_rate=1e-4,
+               optimizer="adaptive_clip:0.003-sm3-momentum:0.9:1:1-learning_rate", grad_bucket_mb=0.25,
+               force_grad_sync=True, allreduce_dtype="bfloat16",
+               block_config=[{"layer": ["norm-shift-scale", "attention-dot_product-context"], "skip": True},
+                             {"layer": ["norm-shift-scale", "feed_forward-in:gelu"], "skip": True}])
+    gen = torch.Generator().manual_seed(5)
+    batches = []
+    for _ in range(6):
+        t = torch.randint(0, 512, (4, 129, 1), generator=gen)
+        batches.append({"token_x": t[:, :-1].contiguous().to(dev), "token_y": t[:, 1:].contiguous().to(dev)})
+    runs = []
+    for graphs in (False, True):
+        mesh = pstate.Mesh(dp=1, tp=1, rank=0).build_groups()
+        torch.manual_seed(0)
+        tr = Trainer(ModelParameter(dict(cfg, use_hip_graphs=graphs, hip_graphs_distributed=graphs)), dev, mesh)
+        losses = [float(tr.step(b)["loss"]) for b in batches]
+        torch.cuda.synchronize()
+        runs.append((tr, losses, getattr(tr, "_graph", None)))
+    (e, le, _), (c, lc, gstate) = runs
+    out["buckets"] = len(c.grad_sync.buckets)
+    out["graphs_captured"] = 0 if not gstate else len(gstate["graphs"])
+    out["graph_comm"] = {k: list(v) for k, v in getattr(c, "graph_comm", {}).items()}
+    out["loss_eager"], out["loss_graph"] = le, lc
+    out["max_loss_diff"] = max(abs(a - b) for a, b in zip(le, lc))
+    out["max_weight_diff"] = float((e.store.master - c.store.master).abs().max())
+    ok = (out["captured_all_reduce"] and out["graphs_captured"] == 2 and out["max_loss_diff"] < 1e-3
+          and out["max_weight_diff"] < 1e-4 and "dp_all_to_all" in out["graph_comm"])
+    out["ok"] = bool(ok)
+    print(json.dumps(out), flush=True)
+    dist.destroy_process_group()
+    sys.exit(0 if ok else 1)
+
+
+if __name__ == "__main__":
+    main()
