@@ -1,108 +1,135 @@
-// Skinny-M GEMM for KV-cache decode steps: C[M][N] = A[M][K] . W[K][N] for M <= 32 tokens, bf16 in / bf16 out,
-// on v_mfma_f32_16x16x32_bf16 with the weight read ONCE for all M rows.
+// Skinny-M GEMM for KV-cache decode steps: C[M][N] = epilogue(A[M][K] . W[K][N]) for M <= 32 tokens, bf16 in /
+// bf16 out, on v_mfma_f32_16x16x32_bf16 with the weight read ONCE for all M rows (reference decode loop:
+// src/run/inference.py:76-97 -- every projection of a decode step is one of these).
 //
-// The op is weight-bandwidth bound (M = 32 FMAs per weight element). The weight comes in as the framework's cached
-// K-contiguous copy Wt[N][K] (ParamStore.transposed), so both MFMA operands load straight from global memory into
-// registers with 16-byte loads and no LDS staging (cdna_hip_programming.md §5, 'GEMV / M <= 16 decode weights':
-// operand streamed once, loads straight to VGPRs, deep unroll):
-//   MFMA A = Wt tile: lane l holds Wt[n0 + (l & 15)][k + 8 (l >> 4) .. +8]   (16 rows x 64 contiguous bytes)
+// The op is weight-bandwidth bound (M = 32 FMAs per weight element): a 32 x 2048 x 4096 product streams 16 MiB of
+// weight, ~2.7 us at 6 TB/s. What bounds a naive kernel is the bytes in flight (Little's law: ~6 TB/s x ~2-3 us of
+// loaded-chip latency = ~15 MiB), so every wave issues ALL its weight loads of a batch before its first MFMA:
+//   block = 8 waves on 16 columns of C (16 rows of the K-contiguous weight copy Wt[N][K]); wave w takes a contiguous
+//   run of 32-deep k-steps, in batches of NS = 8 steps: 8 weight loads (16 B per lane, 16 rows x 64 B each) and 16
+//   activation loads (L2-resident, shared by every block) are in flight before the 16 MFMAs of the batch.
+//   Split-K over blocks (grid.y) brings the grid to >= 256 blocks for the narrow shapes; its fp32 slabs are summed in
+//   slab order by a second kernel (deterministic).
+//   MFMA A = Wt tile: lane l holds Wt[n0 + (l & 15)][k + 8 (l >> 4) .. +8]
 //   MFMA B = A^T    : lane l holds A[t0 + (l & 15)][k + 8 (l >> 4) .. +8]    (tokens t0 = 0 and 16: two MFMAs)
-//   D[n][t]         : lane l holds rows n0 + 4 (l >> 4) + i, column t0 + (l & 15) -> C[t][n .. n+3] (8-byte store)
-// Block = 4 waves on one 16-column tile of C; wave w takes the 32-deep k-steps s = w, w + 4, ... of the block's K
-// range (4 steps per unrolled iteration: 4 weight + 8 activation loads in flight per lane), the 4 wave sums are
-// added through LDS in wave order. KSPLIT > 1 splits K over blocks (grid.y) into fp32 partial slabs that a second
-// kernel adds in slab order: the result is deterministic either way.
+//   D[n][t]         : lane l holds rows n0 + 4 (l >> 4) + i, column t0 + (l & 15)
+// Loads are raw buffer loads: rows t >= M and the steps past a wave's range read at an offset past the resource
+// (returned as zeros, no branch around the load). The 8 waves' partial sums meet in LDS; the epilogue (alpha,
+// residual R, pre-activation Zout, activation) runs on 4 consecutive columns per thread with 8-byte stores.
 #include "common.h"
 
 namespace {
 
 constexpr int SK_NT = 16;     // C columns (weight rows of Wt) per block
-constexpr int SK_W = 4;       // waves per block
-constexpr int SK_U = 4;       // k-steps (of 32) per unrolled iteration
+constexpr int SK_W = 8;       // waves per block
+constexpr int SK_NS = 8;      // k-steps (of 32) per wave and batch: all their loads in flight before the MFMAs
+constexpr unsigned SK_OOR = 0x80000000u;   // a buffer offset past any resource: the load returns zeros
 
-__device__ __forceinline__ bf16x8_t ld8(const bf16_t* p) {
-  return __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(p));
+typedef __attribute__((ext_vector_type(4))) unsigned v4u32s_t;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t sk_rsrc(const void* base, long long nbytes) {
+  const int n = (int)(unsigned)(nbytes <= 0 ? 0ull : nbytes >= 0x7fffffffll ? 0x7fffffffull : (unsigned long long)nbytes);
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, n, 0x00020000);
+}
+
+__device__ __forceinline__ bf16x8_t sk_ld(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(bf16x8_t, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
+}
+
+// v = act(alpha * acc + R); Zout <- alpha * acc + R (pre-activation), 4 consecutive columns
+__device__ __forceinline__ void sk_epilogue(float (&v)[4], long long idx, const bf16_t* R, bf16_t* Zout, bf16_t* C,
+                                            float alpha, int act) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] *= alpha;
+  if (R) {
+    const uint2 r = *reinterpret_cast<const uint2*>(R + idx);
+    v[0] += bf2f(r.x & 0xffff); v[1] += bf2f(r.x >> 16); v[2] += bf2f(r.y & 0xffff); v[3] += bf2f(r.y >> 16);
+  }
+  if (Zout) *reinterpret_cast<uint2*>(Zout + idx) = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+  if (act) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = act_fwd(act, v[i]);
+  }
+  *reinterpret_cast<uint2*>(C + idx) = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
 }
 
 __global__ __launch_bounds__(SK_W * 64) void skinny_mfma_kernel(const bf16_t* __restrict__ A, int lda,
                                                                 const bf16_t* __restrict__ Wt, int ldw,
                                                                 bf16_t* __restrict__ C, int ldc,
-                                                                float* __restrict__ ws, int M, int N, int K,
-                                                                int kchunk) {
+                                                                float* __restrict__ ws, const bf16_t* R,
+                                                                bf16_t* Zout, float alpha, int act, int M, int N,
+                                                                int K, int kchunk) {
   if (__builtin_amdgcn_wavefrontsize() != 64) __builtin_trap();   // fragment maps below are wave64 maps
-  __shared__ float red[SK_W][64][8];
+  __shared__ f32x4_t red[SK_W][2][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = lane & 15, q = lane >> 4;
   const int n0 = blockIdx.x * SK_NT;
   const int kb = blockIdx.y * kchunk, ke = min(K, kb + kchunk);
-  const bf16_t* wrow = Wt + (long long)(n0 + r) * ldw + 8 * q;
-  const bool t0ok = r < M, t1ok = r + 16 < M;
-  const bf16_t* a0 = A + (long long)(t0ok ? r : 0) * lda + 8 * q;
-  const bf16_t* a1 = A + (long long)(t1ok ? r + 16 : 0) * lda + 8 * q;
-  const bf16x8_t zero = __builtin_bit_cast(bf16x8_t, make_uint4(0, 0, 0, 0));
-  f32x4_t acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
   const int nsteps = (ke - kb) / 32;
-  int s = w;
-  for (; s + (SK_U - 1) * SK_W < nsteps; s += SK_U * SK_W) {
-    bf16x8_t wf[SK_U], x0[SK_U], x1[SK_U];
+  const int per = (nsteps + SK_W - 1) / SK_W;                // this wave's k-steps: [s0, s1)
+  const int s0 = min(w * per, nsteps), s1 = min(s0 + per, nsteps);
+  const __amdgpu_buffer_rsrc_t rw = sk_rsrc(Wt, ((long long)(N - 1) * ldw + K) * 2);
+  const __amdgpu_buffer_rsrc_t ra = sk_rsrc(A, ((long long)(M - 1) * lda + K) * 2);   // rows >= M: past the end
+  const unsigned wbase = (unsigned)(((long long)(n0 + r) * ldw + kb + 8 * q) * 2);
+  const unsigned a0base = (unsigned)(((long long)r * lda + kb + 8 * q) * 2);
+  const unsigned a1base = (unsigned)(((long long)(r + 16) * lda + kb + 8 * q) * 2);
+  f32x4_t acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  for (int b = s0; b < s1; b += SK_NS) {
+    bf16x8_t wf[SK_NS], x0[SK_NS], x1[SK_NS];
 #pragma unroll
-    for (int u = 0; u < SK_U; ++u) {
-      const int k = kb + (s + u * SK_W) * 32;
-      wf[u] = ld8(wrow + k);
-      x0[u] = t0ok ? ld8(a0 + k) : zero;
-      x1[u] = t1ok ? ld8(a1 + k) : zero;
+    for (int u = 0; u < SK_NS; ++u) {   // every weight load of the batch first
+      const bool ok = b + u < s1;
+      wf[u] = sk_ld(rw, ok ? wbase + (b + u) * 64 : SK_OOR);
     }
 #pragma unroll
-    for (int u = 0; u < SK_U; ++u) {
+    for (int u = 0; u < SK_NS; ++u) {
+      const bool ok = b + u < s1;
+      x0[u] = sk_ld(ra, ok ? a0base + (b + u) * 64 : SK_OOR);
+      x1[u] = sk_ld(ra, ok ? a1base + (b + u) * 64 : SK_OOR);
+    }
+#pragma unroll
+    for (int u = 0; u < SK_NS; ++u) {
       acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[u], x0[u], acc0, 0, 0, 0);
       acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[u], x1[u], acc1, 0, 0, 0);
     }
   }
-  for (; s < nsteps; s += SK_W) {
-    const int k = kb + s * 32;
-    const bf16x8_t wf = ld8(wrow + k);
-    const bf16x8_t x0 = t0ok ? ld8(a0 + k) : zero, x1 = t1ok ? ld8(a1 + k) : zero;
-    acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, x0, acc0, 0, 0, 0);
-    acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, x1, acc1, 0, 0, 0);
-  }
-#pragma unroll
-  for (int i = 0; i < 4; ++i) { red[w][lane][i] = acc0[i]; red[w][lane][4 + i] = acc1[i]; }
+  red[w][0][lane] = acc0;
+  red[w][1][lane] = acc1;
   __syncthreads();
-  if (w != 0) return;
-  float v[8];
+  if (threadIdx.x >= 128) return;
+  // thread (h, L): tokens t = (L & 15) + 16 h, columns n0 + 4 (L >> 4) .. +3, summed over the waves in order
+  const int L = threadIdx.x & 63, h = threadIdx.x >> 6;
+  f32x4_t s = red[0][h][L];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) v[i] = red[0][lane][i] + red[1][lane][i] + red[2][lane][i] + red[3][lane][i];
-  const int n = n0 + 4 * q;                 // this lane's 4 consecutive columns
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int t = r + 16 * h;
-    if (t >= M) continue;
-    const float* vv = v + 4 * h;
-    if (ws) {
-      *reinterpret_cast<float4*>(ws + ((long long)blockIdx.y * M + t) * N + n) = make_float4(vv[0], vv[1], vv[2], vv[3]);
-    } else {
-      const uint2 o = make_uint2(pack_bf16x2(vv[0], vv[1]), pack_bf16x2(vv[2], vv[3]));
-      *reinterpret_cast<uint2*>(C + (long long)t * ldc + n) = o;
-    }
+  for (int i = 1; i < SK_W; ++i) s += red[i][h][L];
+  const int t = (L & 15) + 16 * h, n = n0 + 4 * (L >> 4);
+  if (t >= M) return;
+  if (ws) {
+    *reinterpret_cast<f32x4_t*>(ws + ((long long)blockIdx.y * M + t) * N + n) = s;
+  } else {
+    float v[4] = {s[0], s[1], s[2], s[3]};
+    sk_epilogue(v, (long long)t * ldc + n, R, Zout, C, alpha, act);
   }
 }
 
-// C[t][n] = sum over slabs s (in order) of ws[s][t][n]
+// C[t][n..n+3] = epilogue(sum over slabs s (in order) of ws[s][t][n..n+3])
 __global__ __launch_bounds__(256) void skinny_combine_kernel(const float* __restrict__ ws, bf16_t* __restrict__ C,
-                                                             int ldc, int M, int N, int KS) {
-  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= (long long)M * N) return;
-  const int m = (int)(i / N), n = (int)(i % N);
-  float s = 0.f;
-  for (int k = 0; k < KS; ++k) s += ws[(long long)k * M * N + i];
-  C[(long long)m * ldc + n] = f2bf(s);
+                                                             int ldc, const bf16_t* R, bf16_t* Zout, float alpha,
+                                                             int act, int M, int N, int KS) {
+  const long long i4 = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i4 * 4 >= (long long)M * N) return;
+  const int m = (int)(i4 * 4 / N), n = (int)(i4 * 4 % N);
+  f32x4_t s = *reinterpret_cast<const f32x4_t*>(ws + i4 * 4);
+  for (int k = 1; k < KS; ++k) s += *reinterpret_cast<const f32x4_t*>(ws + (long long)k * M * N + i4 * 4);
+  float v[4] = {s[0], s[1], s[2], s[3]};
+  sk_epilogue(v, (long long)m * ldc + n, R, Zout, C, alpha, act);
 }
 
 int ksplit_for(int M, int N, int K) {
-  // enough blocks to put a block on most CUs (256), each block still streaming >= 256 k per wave-step range
+  // >= 256 blocks (one per CU) for the narrow shapes while every wave keeps >= 2 k-steps
   const int tiles = N / SK_NT;
   int ks = 1;
-  while (tiles * ks < 256 && K / (ks * 2) >= 1024 && ks < 8) ks *= 2;
+  while (tiles * ks < 256 && (K / 32) / (ks * 2) >= 2 * SK_W && ks < 16) ks *= 2;
   return ks;
 }
 
@@ -115,22 +142,26 @@ OBST_API long long obst_skinny_ws(int M, int N, int K) {
 }
 
 // A [M][K] (lda), Wt [N][K] (ldw: the K-contiguous weight copy), C [M][N] (ldc); M <= 32, N % 16 == 0, K % 32 == 0,
-// 16-byte aligned A / Wt rows; ws: obst_skinny_ws(M, N, K) floats (or null when that is 0)
+// 16-byte aligned A / Wt rows; ws: obst_skinny_ws(M, N, K) floats (or null when that is 0). Epilogue:
+// C = act(alpha * A.W + R), Zout = alpha * A.W + R (R / Zout: bf16 in C's layout, or null; act: ACT_*).
 OBST_API int obst_skinny_gemm(const void* A, int lda, const void* Wt, int ldw, void* C, int ldc, int M, int N, int K,
-                              float* ws, hipStream_t st) {
+                              float* ws, const void* R, void* Zout, float alpha, int act, hipStream_t st) {
   if (M <= 0 || M > 32 || N <= 0 || K <= 0 || N % SK_NT || K % 32 || lda % 8 || ldw % 8 || ldc % 4 || lda < K ||
-      ldw < K || ldc < N)
+      ldw < K || ldc < N || act < 0 || act > ACT_EXP)
     return -1;
-  if ((((uintptr_t)A) | ((uintptr_t)Wt)) & 15 || ((uintptr_t)C) & 7) return -2;
+  if ((((uintptr_t)A) | ((uintptr_t)Wt)) & 15 || (((uintptr_t)C) | (uintptr_t)R | (uintptr_t)Zout) & 7) return -2;
+  if (((long long)(N - 1) * ldw + K) * 2 >= 0x7fffffffll || ((long long)(M - 1) * lda + K) * 2 >= 0x7fffffffll)
+    return -4;   // 32-bit buffer offsets
   const int ks = ksplit_for(M, N, K);
   if (ks > 1 && !ws) return -3;
   const int kchunk = (K / 32 + ks - 1) / ks * 32;
   hipLaunchKernelGGL(skinny_mfma_kernel, dim3(N / SK_NT, ks), dim3(SK_W * 64), 0, st, (const bf16_t*)A, lda,
-                     (const bf16_t*)Wt, ldw, (bf16_t*)C, ldc, ks > 1 ? ws : nullptr, M, N, K, kchunk);
+                     (const bf16_t*)Wt, ldw, (bf16_t*)C, ldc, ks > 1 ? ws : nullptr, (const bf16_t*)R, (bf16_t*)Zout,
+                     alpha, act, M, N, K, kchunk);
   if (ks > 1) {
-    const long long total = (long long)M * N;
-    hipLaunchKernelGGL(skinny_combine_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, ws,
-                       (bf16_t*)C, ldc, M, N, ks);
+    const long long total4 = (long long)M * N / 4;
+    hipLaunchKernelGGL(skinny_combine_kernel, dim3((unsigned)((total4 + 255) / 256)), dim3(256), 0, st, ws,
+                       (bf16_t*)C, ldc, (const bf16_t*)R, (bf16_t*)Zout, alpha, act, M, N, ks);
   }
   return (int)hipGetLastError();
 }

@@ -135,7 +135,7 @@ _SIGS = {
     "obst_sample_parts": [c_ll, c_i],
     "obst_frames": [c_p, c_i, c_p, c_ll, c_i, c_i, c_i, c_p],
     "obst_l1": [c_p, c_p, c_p, c_ll, c_ll, c_p, c_p, c_p, c_f, c_p],
-    "obst_skinny_gemm": [c_p, c_i, c_p, c_i, c_p, c_i, c_i, c_i, c_i, c_p, c_p],
+    "obst_skinny_gemm": [c_p, c_i, c_p, c_i, c_p, c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_f, c_i, c_p],
     "obst_skinny_ws": [c_i, c_i, c_i],
     "obst_decode_attn": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_f, c_i, c_p, c_p],
 }

@@ -228,24 +228,29 @@ def gemm(a: Operand, b: Operand, c: Operand, M: int, N: int, K: int, batch: typi
     b1, b2 = batch
     if kin and (a.trans or b.trans or K % kin):
         raise L.KernelError("split contraction index needs K-contiguous operands and K % kin == 0")
-    if (not kin and on_gpu(c.t) and skinny_ok(M, N, K) and act is None and R is None and Zout is None and Zin is None
-            and tri == 0 and b1 * b2 == 1 and alpha == 1.0 and a.trans == 0 and b.trans == 0
+    if (not kin and on_gpu(c.t) and skinny_ok(M, N, K) and not act_bwd and Zin is None
+            and tri == 0 and b1 * b2 == 1 and a.trans == 0 and b.trans == 0
             and c.t.dtype == torch.bfloat16 and a.t.dtype == torch.bfloat16 and b.t.dtype == torch.bfloat16
+            and (R is None or R.dtype == torch.bfloat16) and (Zout is None or Zout.dtype == torch.bfloat16)
             and a.ld % 8 == 0 and b.ld % 8 == 0 and c.ld % 4 == 0 and a.ld >= K and b.ld >= K and c.ld >= N
-            and a.t.data_ptr() % 16 == 0 and b.t.data_ptr() % 16 == 0 and c.t.data_ptr() % 8 == 0):
-        # decode-step projection (M = batch tokens) against the K-contiguous weight: MFMA weight-streaming kernel
+            and a.t.data_ptr() % 16 == 0 and b.t.data_ptr() % 16 == 0 and c.t.data_ptr() % 8 == 0
+            and (R is None or R.data_ptr() % 8 == 0) and (Zout is None or Zout.data_ptr() % 8 == 0)):
+        # decode-step projection (M = batch tokens) against the K-contiguous weight: the MFMA weight-streaming kernel
+        # with the epilogue fused (alpha, residual R, pre-activation Zout, activation; R / Zout in C's layout)
         _need(a.t, (M - 1) * a.ld + K - 1, "A")
         _need(b.t, (N - 1) * b.ld + K - 1, "B")
-        _need(c.t, (M - 1) * c.ld + N - 1, "C")
+        for nm, t in (("C", c.t), ("R", R), ("Zout", Zout)):
+            _need(t, (M - 1) * c.ld + N - 1, nm)
         ws = _skinny_ws(c.t.device, int(L.lib().obst_skinny_ws(M, N, K)))
         L.check(L.lib().obst_skinny_gemm(a.t.data_ptr(), a.ld, b.t.data_ptr(), b.ld, c.t.data_ptr(), c.ld, M, N, K,
-                                         L.ptr(ws), L.stream_ptr()), "skinny_gemm")
+                                         L.ptr(ws), L.ptr(R), L.ptr(Zout), float(alpha), ACTS[act],
+                                         L.stream_ptr()), "skinny_gemm")
         return c.t
     if (not kin and on_gpu(c.t) and act is not None and tri == 0
             and ((lt_enabled() == 1 and lt_scope() > 0 and not _ACT_G4W)
-                 # decode-step activation products: the skinny kernel + the elementwise pass (a 32-row product with
-                 # a fused epilogue on gemm4w keeps a 256-row tile row on a few CUs: ~45 us a call)
-                 or (skinny_ok(M, N, K) and R is None and alpha == 1.0 and a.trans == 0 and b.trans == 0))
+                 # decode-step activation backward: the skinny kernel + the elementwise pass
+                 or (act_bwd and skinny_ok(M, N, K) and R is None and alpha == 1.0 and a.trans == 0
+                     and b.trans == 0))
             and c.t.dtype == torch.bfloat16
             and b1 * b2 == 1 and c.ld == N and (M * N) % 8 == 0 and c.t.is_contiguous() and c.t.numel() == M * N):
         # activation GEMM on hipBLASLt / the skinny kernel: plain product, then the elementwise kernel (pre-activation

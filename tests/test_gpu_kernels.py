@@ -629,6 +629,32 @@ def test_skinny_gemm_matches_fp32(cuda, M, K, N, monkeypatch):
     _close(c.view(M, N).float().cpu(), ref, 2e-2, 2e-2, f"skinny {M}x{K}x{N}")
 
 
+@pytest.mark.parametrize("M,K,N,ks_expected", [(32, 4096, 2048, True), (5, 2048, 4096, False),
+                                                (32, 2048, 8192, False)])
+def test_skinny_gemm_fused_epilogue(cuda, M, K, N, ks_expected, monkeypatch):
+    """the decode-step GEMM with its epilogue fused (split-K: in the combine kernel): C = gelu(alpha A.W + R) with the
+    pre-activation in Zout, against the fp32 reference; the guard words around C / Zout stay untouched"""
+    monkeypatch.setattr(raw, "_SKINNY", True)
+    assert (L.lib().obst_skinny_ws(M, N, K) > 0) == ks_expected
+    g = torch.Generator().manual_seed(M + N)
+    a = torch.randn(M, K, generator=g).bfloat16()
+    w = (torch.randn(K, N, generator=g) / math.sqrt(K)).bfloat16()
+    r = torch.randn(M, N, generator=g).bfloat16()
+    pad = 64
+    c = torch.full((M * N + 2 * pad,), float("nan"), dtype=torch.bfloat16, device=cuda)
+    z = torch.full((M * N + 2 * pad,), float("nan"), dtype=torch.bfloat16, device=cuda)
+    raw.gemm(raw.Operand(a.to(cuda).flatten(), 0, K), raw.Operand(w.t().contiguous().to(cuda).flatten(), 0, K),
+             raw.Operand(c[pad:pad + M * N], 0, N), M, N, K, alpha=0.5, act="gelu", R=r.to(cuda).flatten(),
+             Zout=z[pad:pad + M * N])
+    torch.cuda.synchronize()
+    pre = 0.5 * (a.float() @ w.float()) + r.float()
+    ref = torch.nn.functional.gelu(pre, approximate="tanh")
+    _close(z[pad:pad + M * N].view(M, N).float().cpu(), pre, 2e-2, 2e-2, "skinny Zout")
+    _close(c[pad:pad + M * N].view(M, N).float().cpu(), ref, 2e-2, 2e-2, "skinny gelu(C)")
+    for t in (c, z):
+        assert torch.isnan(t[:pad].float()).all() and torch.isnan(t[pad + M * N:].float()).all()
+
+
 @pytest.mark.parametrize("out_f32", [False, True])
 def test_gemm_split_contraction_index(cuda, out_f32):
     """C[h] = A_h · B_hᵀ with the contraction over (b, f) pairs of [B, S, H, F] tensors read in place (kin = F)"""
