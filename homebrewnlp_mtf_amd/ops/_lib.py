@@ -137,9 +137,11 @@ _SIGS = {
     "obst_l1": [c_p, c_p, c_p, c_ll, c_ll, c_p, c_p, c_p, c_f, c_p],
     "obst_skinny_gemm": [c_p, c_i, c_p, c_i, c_p, c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_f, c_i, c_p],
     "obst_skinny_ws": [c_i, c_i, c_i],
+    "obst_calib_mfma": [c_p, c_i, c_p],
+    "obst_calib_mfma_flops": [c_i],
     "obst_decode_attn": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_f, c_i, c_p, c_p],
 }
-_RESTYPES = {"obst_norm_bwd_ws": c_ll, "obst_skinny_ws": c_ll, "obst_scatter_ws": c_ll, "obst_blaslt_splitk_calls": c_ll}
+_RESTYPES = {"obst_calib_mfma_flops": ctypes.c_double, "obst_norm_bwd_ws": c_ll, "obst_skinny_ws": c_ll, "obst_scatter_ws": c_ll, "obst_blaslt_splitk_calls": c_ll}
 
 
 def lib():

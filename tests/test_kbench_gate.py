@@ -25,5 +25,34 @@ def test_round3_norm_bwd_regression_fails_the_gate():
     bad = kbench.check([regressed], floors)
     assert bad and bad[0][0] == "norm_bwd" and bad[0][1] == "gbps"
     # within tolerance passes; an unfloored line is ignored
-    assert kbench.check([dict(ok, gbps=ok["gbps"] * 0.96)], floors) == []
+    assert kbench.check([dict(ok, gbps=ok["gbps"] * 0.98)], floors) == []
     assert kbench.check([{"kernel": "new_kernel", "gbps": 1.0}], floors) == []
+
+
+def test_ratio_floors_are_box_independent():
+    """a key with ratio floors is judged on metric / same-process calibration: the same kernel on a slower box (lower
+    absolute number, proportionally lower calibration) passes; a real regression at the same calibration fails"""
+    floors = {"gemm fwd": {"tflops_gemm4w": 1400.0}}
+    ratios = {"gemm fwd": {"tflops_gemm4w": 0.70}}
+    row = {"kernel": "gemm", "shape": "fwd", "tflops_gemm4w": 1400.0, "ratio_tflops_gemm4w": 0.70}
+    slow_box = dict(row, tflops_gemm4w=1260.0, ratio_tflops_gemm4w=0.70)      # 10 % lower clock, same code
+    regressed = dict(row, tflops_gemm4w=1330.0, ratio_tflops_gemm4w=0.665)    # 5 % slower at the same clock
+    assert kbench.check([slow_box], floors, 0.03, ratios) == []
+    assert kbench.check([slow_box], floors, 0.03) != []                      # absolute floors would flag the box
+    assert kbench.check([regressed], floors, 0.03, ratios)
+
+
+def test_missing_floored_key_is_reported():
+    floors = {"gemm fwd": {"tflops_gemm4w": 1.0}, "attention": {"pflops_fwd": 1.0}, "norm_fwd": {"gbps": 1.0}}
+    assert kbench.missing(floors, {"attention"}, ["gemm", "attn"]) == ["gemm fwd"]
+    assert kbench.missing(floors, {"attention", "gemm fwd"}, ["gemm", "attn"]) == []
+
+
+def test_rows_get_calibration_ratios():
+    kbench.PENDING.clear()
+    kbench.EMITTED.clear()
+    kbench.emit(kernel="attention", pflops_fwd=0.8, gbps=3000.0)
+    kbench.flush_rows({"mfma_tflops": 2000.0, "copy_gbps": 5000.0})
+    r = kbench.EMITTED[-1]
+    assert r["ratio_pflops_fwd"] == 0.4 and r["ratio_gbps"] == 0.6
+    kbench.EMITTED.clear()

@@ -12,8 +12,19 @@
 * norm      -- norm fwd / bwd (+ residual gradient, + parameter gradients): GB/s of the bytes each must move.
 * ew        -- the streaming elementwise kernels (gelu fwd / bwd, add): GB/s.
 
+Timing: every number is the MEDIAN of --reps (default 20) individually timed calls after two warm-up calls; where
+two implementations are compared their samples are interleaved call by call (cdna guide §5.4 rule 24).
+
+Calibration (same process): a bare bf16 MFMA loop on random register operands (csrc/kernels/calib.hip; TF/s) and a
+512 MiB device copy (GB/s), measured before and after each section. Every emitted line carries the two and the
+ratio of each metric to its calibration (``ratio_<metric>``): compute metrics (TF/s, PF/s) over the MFMA loop, memory
+metrics (GB/s) over the copy. Devices differ by up to ~12 % on an MFMA loop at the same code (MI355X_MICROARCH.md,
+'DVFS give-back' item 5), so the gate compares ratios.
+
 --check FLOOR.json (the perf-regression gate of tools/gpu_final.sh): every emitted line whose key (kernel, shape) has
-floors in the file must reach each floored metric within --tol (default 5 %); the exit status is 1 otherwise.
+floors in the file must reach each floored ratio (``ratios``; the absolute ``floors`` where a key has no ratio)
+within --tol (default 3 %), and every floored key of a section that ran must have been emitted; the exit status is
+1 otherwise. --write-floors PATH writes the observed ratios as a new floor file.
 
 The profiles under profiles/ quote these numbers; the one-off A/B scripts next to it (bench_*.py, gpu_*.sh) are the
 lab notes behind individual measurements (tools/README.md).
@@ -24,6 +35,7 @@ import argparse
 import json
 import os
 import sys
+import typing
 
 import torch
 
@@ -33,26 +45,81 @@ from homebrewnlp_mtf_amd.ops import raw  # noqa: E402
 BF = torch.bfloat16
 
 
+def timed_many(fns, reps: int):
+    """median microseconds per call of each fn: `reps` samples, the fns interleaved call by call, every call timed
+    by its own pair of events (after two warm-up calls each)"""
+    for fn in fns:
+        for _ in range(2):
+            fn()
+    torch.cuda.synchronize()
+    evs = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+           for _ in fns]
+    for r in range(reps):
+        for i, fn in enumerate(fns):
+            evs[i][r][0].record()
+            fn()
+            evs[i][r][1].record()
+    torch.cuda.synchronize()
+    out = []
+    for i in range(len(fns)):
+        t = sorted(a.elapsed_time(b) * 1e3 for a, b in evs[i])
+        out.append(t[len(t) // 2])
+    return out
+
+
 def timed(fn, reps: int) -> float:
-    """mean microseconds per call over `reps` calls after two warm-up calls"""
-    for _ in range(2):
-        fn()
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(reps):
-        fn()
-    e1.record()
-    torch.cuda.synchronize()
-    return e0.elapsed_time(e1) * 1e3 / reps
+    """median microseconds per call over `reps` individually timed calls after two warm-up calls"""
+    return timed_many([fn], reps)[0]
+
+
+CALIB = {}
+
+
+def calibrate(reps: int = 20):
+    """same-process calibration: bf16 MFMA loop TF/s (csrc/kernels/calib.hip) and a 512 MiB device copy GB/s"""
+    from homebrewnlp_mtf_amd.ops import _lib as L
+    dev = torch.device("cuda")
+    sink = torch.empty(256 * 256, device=dev)
+    iters = 4096
+    fl = float(L.lib().obst_calib_mfma_flops(iters))
+    us = timed(lambda: L.check(L.lib().obst_calib_mfma(sink.data_ptr(), iters, L.stream_ptr()), "calib"), reps)
+    src = torch.randn(128 * 2 ** 20, device=dev)
+    dst = torch.empty_like(src)
+    cus = timed(lambda: dst.copy_(src), reps)
+    return {"mfma_tflops": fl / us / 1e6, "copy_gbps": 2 * src.numel() * 4 / cus / 1e3}
+
+
+def section_calib(before: dict, after: dict) -> dict:
+    return {k: (before[k] + after[k]) / 2 for k in before}
 
 
 EMITTED = []
+PENDING = []
 
 
 def emit(**kw):
-    EMITTED.append(kw)
-    print(json.dumps(kw), flush=True)
+    """queue a row; flush_rows() attaches the section's calibration and ratios and prints it"""
+    PENDING.append(kw)
+
+
+def metric_kind(metric: str) -> str:
+    return "copy_gbps" if metric.startswith("gbps") else "mfma_tflops"
+
+
+def metric_scale(metric: str) -> float:
+    """to TF/s (compute) or GB/s (memory)"""
+    return 1000.0 if metric.startswith("pflops") else 1.0
+
+
+def flush_rows(cal: dict):
+    for kw in PENDING:
+        kw["calib_mfma_tflops"] = round(cal["mfma_tflops"], 1)
+        kw["calib_copy_gbps"] = round(cal["copy_gbps"], 1)
+        for m in [k for k in kw if k.startswith(("tflops", "pflops", "gbps")) and isinstance(kw[k], (int, float))]:
+            kw["ratio_" + m] = round(kw[m] * metric_scale(m) / cal[metric_kind(m)], 4)
+        EMITTED.append(kw)
+        print(json.dumps(kw), flush=True)
+    PENDING.clear()
 
 
 def line_key(row: dict) -> str:
@@ -80,15 +147,23 @@ def missing(floors: dict, seen: set, sections) -> list:
     return sorted(k for k in floors if section_of(k) in sections and k not in seen)
 
 
-def check(rows, floors: dict, tol: float = 0.05):
+def check(rows, floors: dict, tol: float = 0.03, ratios: typing.Optional[dict] = None):
     """-> list of (key, metric, value, floor) for every floored metric below floor * (1 - tol); higher is better for
-    every metric in the floor file (TF/s, PF/s, GB/s)"""
+    every metric in the floor file (TF/s, PF/s, GB/s and their calibration ratios). A key with ratio floors is
+    checked on its ratios (box-independent), one without on its absolute floors."""
     bad = []
+    ratios = ratios or {}
     for row in rows:
-        for metric, floor in floors.get(line_key(row), {}).items():
+        key = line_key(row)
+        table = ratios.get(key)
+        if table:
+            table = {"ratio_" + m: f for m, f in table.items()}
+        else:
+            table = floors.get(key, {})
+        for metric, floor in table.items():
             v = row.get(metric)
             if v is None or v < floor * (1.0 - tol):
-                bad.append((line_key(row), metric, v, floor))
+                bad.append((key, metric, v, floor))
     return bad
 
 
@@ -107,13 +182,13 @@ def bench_gemm(T: int, reps: int):
         B = (torch.randn(N * K, device=dev) * 0.5).to(BF)
         C = torch.zeros(M * N, device=dev, dtype=torch.float32 if f32 else BF)
         ops = (raw.Operand(A, at, K if at == 0 else M), raw.Operand(B, bt, K if bt == 0 else N), raw.Operand(C, 0, N))
-        t = {}
-        for rnd in range(2):   # interleaved: library, hand-written, library, hand-written
-            for lt in (1, 0):
-                old = raw.lt_set(lt)
-                us = timed(lambda: raw.gemm(*ops, M, N, K), reps)
+        def with_lt(on):
+            def run():
+                old = raw.lt_set(on)
+                raw.gemm(*ops, M, N, K)
                 raw.lt_set(old)
-                t[lt] = min(t.get(lt, 1e30), us)
+            return run
+        t = dict(zip((1, 0), timed_many([with_lt(1), with_lt(0)], reps)))   # interleaved call by call
         fl = 2.0 * M * N * K
         emit(kernel="gemm", shape=name, M=M, N=N, K=K, a_t=at, b_t=bt, out_f32=f32,
              us_hipblaslt=round(t[1], 1), us_gemm4w=round(t[0], 1), tflops_hipblaslt=round(fl / t[1] / 1e6, 1),
@@ -138,12 +213,13 @@ def bench_mixer(reps: int):
         def run():
             raw.gemm(raw.Operand(w, a_t, S, 0, S * S), raw.Operand(x, 1, hf, S * hf, Fd),
                      raw.Operand(y, 0, hf, S * hf, Fd), S, Fd, S, batch=(B, H), tri=tri)
-        t = {}
-        for rnd in range(2):
-            for on in (0, 1):
+        def with_g4w(on):
+            def go():
                 old = L.lib().obst_gemm4w_set(on)
-                t[on] = min(t.get(on, 1e30), timed(run, reps))
+                run()
                 L.lib().obst_gemm4w_set(old)
+            return go
+        t = dict(zip((0, 1), timed_many([with_g4w(0), with_g4w(1)], reps)))
         emit(kernel="gemm", shape=name, us_phase=round(t[0], 1), us_gemm4w=round(t[1], 1),
              tflops_phase=round(fl / t[0] / 1e6, 1), tflops_gemm4w=round(fl / t[1] / 1e6, 1),
              gemm4w_over_phase=round(t[0] / t[1], 3))
@@ -234,14 +310,16 @@ def bench_ew(T: int, reps: int):
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("what", nargs="?", default="all", choices=["gemm", "mixer", "attn", "attn_map", "norm", "ew", "all"])
-    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--tokens", type=int, default=131072, help="tokens per step (GPT-Neo-1.3B: 64 x 2048)")
     ap.add_argument("--batch", type=int, default=64, help="attention batch at S 2048")
     ap.add_argument("--check", default=None, help="floor file: fail on a regression past --tol")
-    ap.add_argument("--tol", type=float, default=0.05)
+    ap.add_argument("--tol", type=float, default=0.03)
+    ap.add_argument("--write-floors", default=None, help="write the observed ratios as a floor file")
     a = ap.parse_args(argv)
     todo = ["gemm", "mixer", "attn", "attn_map", "norm", "ew"] if a.what == "all" else [a.what]
     for w in todo:
+        cal0 = calibrate()
         if w == "gemm":
             bench_gemm(a.tokens, a.reps)
         elif w == "mixer":
@@ -254,10 +332,24 @@ def main(argv=None):
             bench_norm(a.tokens, a.reps)
         else:
             bench_ew(a.tokens, a.reps)
+        flush_rows(section_calib(cal0, calibrate()))
+    if a.write_floors:
+        out = {"source": "tools/kbench.py --write-floors: observed ratios to the same-process calibration (median of "
+                         f"{a.reps} samples)", "floors": {}, "ratios": {}}
+        for r in EMITTED:
+            k = line_key(r)
+            for m in [m for m in r if m.startswith(("tflops", "pflops", "gbps"))]:
+                if m.endswith(("hipblaslt", "phase")):
+                    continue   # reference implementations are reported, not floored
+                out["floors"].setdefault(k, {})[m] = r[m]
+                out["ratios"].setdefault(k, {})[m] = r["ratio_" + m]
+        with open(a.write_floors, "w") as f:
+            json.dump(out, f, indent=1)
     if a.check:
         with open(a.check) as f:
-            floors = json.load(f)["floors"]
-        bad = check(EMITTED, floors, a.tol)
+            spec = json.load(f)
+        floors, ratios = spec["floors"], spec.get("ratios", {})
+        bad = check(EMITTED, floors, a.tol, ratios)
         seen = {line_key(r) for r in EMITTED}
         for key, metric, v, floor in bad:
             print(f"REGRESSION {key}: {metric} {v} < floor {floor} - {a.tol:.0%}", flush=True)
