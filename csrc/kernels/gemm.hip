@@ -473,6 +473,7 @@ OBST_API int obst_gemm4w_set(int on) {
   return old;
 }
 OBST_API long long obst_gemm4w_calls() { return g_4w_calls; }
+
 OBST_API int obst_gemm4w_enabled() { return g4w_enabled(); }
 // diagnostics: device buffer of 5 u64 per block (gemm4w.h) filled by the following gemm4w launches; null: off
 static unsigned long long* g_4w_stamps = nullptr;

@@ -13,3 +13,4 @@ hipError_t gemm4w_launch(const gemmk::GemmArgs* a, int a_t, int b_t, int out_f32
   if (a_t == 1 && b_t == 0) return gemm4w_launch_10(a, out_f32, batch, stream);
   return gemm4w_launch_11(a, out_f32, batch, stream);
 }
+

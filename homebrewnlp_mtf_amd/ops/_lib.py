@@ -119,6 +119,7 @@ _SIGS = {
     "obst_blaslt_splitk_calls": [],
     "obst_gemm4w_enabled": [],
     "obst_gemm4w_set": [c_i],
+
     "obst_blaslt_splitk_set": [c_i],
     "obst_blaslt_stats": [c_p],
     "obst_glu": [c_p, c_p, c_p, c_p, c_p, c_ll, c_p],

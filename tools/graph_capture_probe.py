@@ -32,7 +32,27 @@ def main():
     torch.cuda.set_device(dev)
     dist.init_process_group("nccl", device_id=dev)
     out = {}
+    try:
+        _capture_all_reduce(dev, out)
+    except Exception as e:   # report, then continue with the trainer check
+        import traceback
+        out["captured_all_reduce"] = False
+        out["error_all_reduce"] = traceback.format_exc()[-1500:]
+    try:
+        _capture_trainer(dev, out, ModelParameter, pstate, Trainer)
+    except Exception as e:
+        import traceback
+        out["graphs_captured"] = 0
+        out["error_trainer"] = traceback.format_exc()[-2500:]
+    ok = (out.get("captured_all_reduce") and out.get("graphs_captured") == 2 and out.get("max_loss_diff", 1) < 1e-3
+          and out.get("max_weight_diff", 1) < 1e-4 and "dp_all_to_all" in out.get("graph_comm", {}))
+    out["ok"] = bool(ok)
+    print(json.dumps(out), flush=True)
+    dist.destroy_process_group()
+    sys.exit(0 if ok else 1)
 
+
+def _capture_all_reduce(dev, out):
     # 1. async all_reduce + wait inside a captured graph
     x = torch.arange(1 << 20, dtype=torch.float32, device=dev)
     y = torch.empty_like(x)
@@ -55,6 +75,8 @@ def main():
     torch.cuda.synchronize()
     out["captured_all_reduce"] = bool(torch.equal(z, eager + 1.0))
 
+
+def _capture_trainer(dev, out, ModelParameter, pstate, Trainer):
     # 2. Trainer step captured with the DP collectives inside (world 1, GradSync forced on)
     cfg = dict(model_mode="gpt", use_video=False, use_language=True, heads=4, features_per_head=64, depth=2,
                sequence_length=128, train_batch_size=4, vocab_size=512, intermediate_feed_forward_multiplier=2,
@@ -83,12 +105,6 @@ def main():
     out["loss_eager"], out["loss_graph"] = le, lc
     out["max_loss_diff"] = max(abs(a - b) for a, b in zip(le, lc))
     out["max_weight_diff"] = float((e.store.master - c.store.master).abs().max())
-    ok = (out["captured_all_reduce"] and out["graphs_captured"] == 2 and out["max_loss_diff"] < 1e-3
-          and out["max_weight_diff"] < 1e-4 and "dp_all_to_all" in out["graph_comm"])
-    out["ok"] = bool(ok)
-    print(json.dumps(out), flush=True)
-    dist.destroy_process_group()
-    sys.exit(0 if ok else 1)
 
 
 if __name__ == "__main__":

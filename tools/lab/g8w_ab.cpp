@@ -2,7 +2,7 @@
 // one process, interleaved rounds on the same random operands (cdna guide §5.4 rule 24), every variant's output
 // checked against the library's on a strided sample of rows.
 //
-//   build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -Icsrc/kernels tools/lab/g8w_ab.cpp -o bin/g8w_ab \
+//   build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -Icsrc/kernels -Itools/lab tools/lab/g8w_ab.cpp -o bin/g8w_ab \
 //            -Lhomebrewnlp_mtf_amd -l:_kernels.so -Wl,-rpath,'$ORIGIN/../homebrewnlp_mtf_amd'
 //   run:   bin/g8w_ab [rounds] [reps] [shape filter]      (G8_ONLY=0,2: variants)
 #include "gemm8w.h"

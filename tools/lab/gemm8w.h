@@ -95,11 +95,37 @@ __device__ __forceinline__ bf16x8_t g8_frag_b(const char* img, int nbase, int j,
 
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Winline-asm"
+// dma16o with 5 wait states in front: the first piece of a group reads a resource that v_readfirstlane may have
+// written right before it (VALU -> SGPR -> VMEM needs five; tools/sgpr_hazard.py)
+#define OBST_DMA16P(BITS)                                                                                          \
+  asm volatile("s_nop 4\n\ts_add_u32 m0, %2, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen" BITS " lds" ::"v"(voff), \
+               "s"(rs), "s"(sbase), "n"(OFF)                                                                      \
+               : "memory", "m0")
+template <int CP, int OFF>
+__device__ __forceinline__ void dma16p(const i32x4_t& rs, int voff, unsigned sbase) {
+  if constexpr (CP == 0) OBST_DMA16P("");
+  else if constexpr (CP == 1) OBST_DMA16P(" sc0");
+  else if constexpr (CP == 2) OBST_DMA16P(" sc1");
+  else if constexpr (CP == 3) OBST_DMA16P(" sc0 sc1");
+  else OBST_DMA16P(" nt");
+}
+#undef OBST_DMA16P
 // the first MFMA of a tile: C = A.B (source C = 0), accumulator register kept in place ("+a")
 __device__ __forceinline__ void mfma_zero(f32x4_t& c, const bf16x8_t& a, const bf16x8_t& b) {
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "+a"(c) : "v"(a), "v"(b));
 }
 #pragma clang diagnostic pop
+
+// a buffer resource whose words are forced into SGPRs (v_readfirstlane; a no-op for values already scalar): under
+// SGPR pressure the allocator kept epilogue pointers in VGPRs ("illegal VGPR to SGPR copy" at the store)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_brsrc_u(const void* base, long long nbytes) {
+  const unsigned long long a = (unsigned long long)base;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a), hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+  const int n = __builtin_amdgcn_readfirstlane(
+      (int)(unsigned)(nbytes <= 0 ? 0ull : nbytes >= 0xffffffffll ? 0xffffffffull : (unsigned long long)nbytes));
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((unsigned long long)hi << 32) | lo), 0, n,
+                                           0x00020000);
+}
 
 __device__ __forceinline__ void pad_redefine48(f32x4_t (&acc)[4][8]) {
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" : "+a"(acc[0][0]), "+a"(acc[0][1]), "+a"(acc[0][2]), "+a"(acc[0][3]),
@@ -121,7 +147,7 @@ template <int A_T, int B_T, bool OUT_F32, bool PROF, int OPT = G8W_OPT, int CPA 
 __global__ __launch_bounds__(512, 2) void gemm8w_kernel(GemmArgs p) {
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   constexpr bool PRIO = (OPT & 1) != 0, DMAFIRST = (OPT & 2) != 0, CPRIO = (OPT & 4) != 0;
-  constexpr int S = OUT_F32 ? 32 : 16;   // direct-epilogue stores per wave
+  constexpr int S = 32;                  // direct-epilogue stores per wave, every variant (see epilogue_v)
   constexpr int VF = 8 + S;              // vmcnt of the first K-tile's load phases
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int grp = wave >> 2, wq = wave & 3;
@@ -149,7 +175,9 @@ __global__ __launch_bounds__(512, 2) void gemm8w_kernel(GemmArgs p) {
   const unsigned long long step = tro ? 128ull * (unsigned long long)ldo : 128ull;   // one 64-deep K-tile
   const unsigned long long koff = tro ? 64ull * (unsigned long long)ldo : 64ull;    // its second half
   const unsigned lds0 = lds_u32(smem);
-  auto sbase_of = [&](int s) -> unsigned { return lds0 + s * G8_SLOT + grp * G8_OP + wq * 4096; };
+  auto sbase_of = [&](int s) -> unsigned {
+    return __builtin_amdgcn_readfirstlane(lds0 + s * G8_SLOT + grp * G8_OP + wq * 4096);
+  };
 
   int d_rnd = 0, d_kt = 0, d_nk = 0;
   unsigned long long cur, rem;
@@ -159,13 +187,14 @@ __global__ __launch_bounds__(512, 2) void gemm8w_kernel(GemmArgs p) {
     rem = opa ? (unsigned long long)T.arem : (unsigned long long)T.brem;
   };
   cursor_tile(decode4<A_T, B_T>(p, logical(0)));
+  // (readfirstlane: a no-op on values the allocator keeps in SGPRs; it turns an "illegal VGPR to SGPR copy" into a
+  // v_readfirstlane when SGPR pressure moved one to a VGPR -- tools/sgpr_hazard.py checks the DMA behind it)
   auto rsrc_of = [](unsigned long long base, unsigned long long rm) {
     i32x4_t r;
-    r[0] = (int)(unsigned)base;
-    r[1] = (int)(unsigned)(base >> 32);
-    unsigned hi = (unsigned)(rm >> 32);
-    asm volatile("" : "+s"(hi));
-    r[2] = hi ? -1 : (int)(unsigned)rm;
+    r[0] = __builtin_amdgcn_readfirstlane((int)(unsigned)base);
+    r[1] = __builtin_amdgcn_readfirstlane((int)(unsigned)(base >> 32));
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(rm >> 32));
+    r[2] = hi ? -1 : __builtin_amdgcn_readfirstlane((int)(unsigned)rm);
     r[3] = 0x00020000;
     return r;
   };
@@ -182,26 +211,28 @@ __global__ __launch_bounds__(512, 2) void gemm8w_kernel(GemmArgs p) {
     }
   };
   // this wave's 4 pieces of half `half` of the cursor's K-tile into ring slot s
-  auto dma = [&](int half, int s) {
+  auto dma = [&](int half, int s) __attribute__((always_inline)) {
     const unsigned long long o = half ? koff : 0ull;
     const i32x4_t rs = rsrc_of(cur + o, rem - o);
     const unsigned sb = sbase_of(s);
     if (CPA == CPB || opa) {
       static_for<4>([&](auto qc) {
         constexpr int q = decltype(qc)::value;
-        dma16o<CPA, q * 1024>(rs, vo[q], sb);
+        if constexpr (q == 0) dma16p<CPA, 0>(rs, vo[q], sb);
+        else dma16o<CPA, q * 1024>(rs, vo[q], sb);
       });
     } else {
       static_for<4>([&](auto qc) {
         constexpr int q = decltype(qc)::value;
-        dma16o<CPB, q * 1024>(rs, vo[q], sb);
+        if constexpr (q == 0) dma16p<CPB, 0>(rs, vo[q], sb);
+        else dma16o<CPB, q * 1024>(rs, vo[q], sb);
       });
     }
   };
 
   f32x4_t acc[4][8];
   bf16x8_t af[4], bfr[8];
-  auto read_frags = [&](int s) {
+  auto read_frags = [&](int s) __attribute__((always_inline)) {
     const char* img = smem + s * G8_SLOT;
     static_for<4>([&](auto ic) {
       constexpr int i = decltype(ic)::value;
@@ -212,7 +243,7 @@ __global__ __launch_bounds__(512, 2) void gemm8w_kernel(GemmArgs p) {
       bfr[j] = g8_frag_b<B_T>(img + G8_OP, wn * 128, j, lane);
     });
   };
-  auto lphase = [&](int rs, int ds, int half, auto vwc) {
+  auto lphase = [&](int rs, int ds, int half, auto vwc) __attribute__((always_inline)) {
     constexpr int VW = decltype(vwc)::value;
     if constexpr (DMAFIRST) {
       dma(half, ds);
@@ -230,7 +261,7 @@ __global__ __launch_bounds__(512, 2) void gemm8w_kernel(GemmArgs p) {
     __builtin_amdgcn_s_barrier();
     fence();
   };
-  auto cphase = [&](auto zc) {
+  auto cphase = [&](auto zc) __attribute__((always_inline)) {
     constexpr bool ZERO = decltype(zc)::value;
     if constexpr (CPRIO) __builtin_amdgcn_s_setprio(1);
     static_for<32>([&](auto qc) {
@@ -253,12 +284,17 @@ __global__ __launch_bounds__(512, 2) void gemm8w_kernel(GemmArgs p) {
     fence();
   };
 
-  // direct epilogue of one tile from the accumulators (alpha; fp32 / bf16; split-K slab); S stores per wave (rows
-  // past M fall outside the resource and are dropped, columns past N are skipped)
-  auto epilogue = [&](const Tile4& ct) {
-    fence();
-    pad_redefine48(acc);
-    fence();
+  // Direct epilogue of one tile from the accumulators. Every variant leaves EXACTLY S stores in the vmcnt queue (the
+  // first K-tile's counted waits assume S ops younger than the awaited pieces): stores of masked columns go to an
+  // offset past the resource (dropped by the range check, still counted), plain bf16 products pad with 16 such
+  // stores, and the side-input loads (R, Zin, beta * C) are compiler-visible -- the compiler waits for them before
+  // their use, so none is left outstanding. Rows past M fall outside the resource.
+  //   EX: residual R and / or beta * C (fp32);  AC: 0 none, 1 activation forward (+ Zout pre-activation), 2 backward
+  //   (C = v * act'(Zin)); ACTK: the activation (gelu / relu)
+  auto epilogue_v = [&](const Tile4& ct, auto exc, auto acc_, auto actk) __attribute__((always_inline)) {
+    constexpr bool EX = decltype(exc)::value;
+    constexpr int AC = decltype(acc_)::value;
+    constexpr int ACTK = decltype(actk)::value;
     const bool ws_out = OUT_F32 && p.ksplit > 1;
     const long long ldc = ws_out ? p.N : p.ldc;
     constexpr int ES = OUT_F32 ? 4 : 2;
@@ -266,64 +302,117 @@ __global__ __launch_bounds__(512, 2) void gemm8w_kernel(GemmArgs p) {
                          : reinterpret_cast<char*>(p.C) + ct.coff * ES;
     const long long corg = ((long long)ct.m0 * ldc + ct.n0) * ES;
     const long long cext = ((long long)(p.M - ct.m0 - 1) * ldc + (p.N - ct.n0)) * ES;
-    const __amdgpu_buffer_rsrc_t rc = make_brsrc(cbase + corg, cext);
-    const float alpha = p.alpha;
-    int ldcs = (int)ldc;
-    asm volatile("" : "+s"(ldcs));
+    const __amdgpu_buffer_rsrc_t rc = make_brsrc_u(cbase + corg, cext);
+    const __amdgpu_buffer_rsrc_t rr =
+        make_brsrc_u(p.R ? reinterpret_cast<const char*>(p.R) + ct.coff * ES + corg : cbase + corg, cext);
+    const __amdgpu_buffer_rsrc_t rz = make_brsrc_u(
+        (AC == 1 && p.Zout) ? reinterpret_cast<const char*>(p.Zout) + ct.coff * 2 + corg
+                            : (AC == 2 ? reinterpret_cast<const char*>(p.Zin) + ct.coff * 2 + corg : cbase + corg),
+        (AC == 1 && !p.Zout) ? 0 : cext);   // no Zout: its stores go nowhere (still counted)
+    const float alpha = p.alpha, beta = ws_out ? 0.f : p.beta;
+    const int ldcs = __builtin_amdgcn_readfirstlane((int)ldc);
     const int ml = lane & 15, gq = lane >> 4;
-    if constexpr (B_T == 0) {
-      // lane (ml, gq): rows 16 i + 4 gq + r of the wave's 64, columns 8 ml .. +7 of its 128 (acc[i][0..7][r])
-      const int vt = ((wm * 64 + 4 * gq) * ldcs + wn * 128 + 8 * ml) * ES;
-      const bool colok = ct.n0 + wn * 128 + 8 * ml < p.N;
-      static_for<4>([&](auto ic) {
-        constexpr int i = decltype(ic)::value;
-        v4u32_t o0[4], o1[4];
-        static_for<4>([&](auto rk) {
-          constexpr int r = decltype(rk)::value;
-          float x[8];
-          static_for<8>([&](auto jc) { x[decltype(jc)::value] = alpha * acc[i][decltype(jc)::value][r]; });
-          if constexpr (OUT_F32) {
-            o0[r] = __builtin_bit_cast(v4u32_t, f32x4_t{x[0], x[1], x[2], x[3]});
-            o1[r] = __builtin_bit_cast(v4u32_t, f32x4_t{x[4], x[5], x[6], x[7]});
-          } else {
-            o0[r] = v4u32_t{pack_bf16x2(x[0], x[1]), pack_bf16x2(x[2], x[3]), pack_bf16x2(x[4], x[5]),
-                            pack_bf16x2(x[6], x[7])};
+    // per-lane origin of the 8 consecutive columns of store (i, u): row ro(i, u), column offset
+    //   B_T == 0 (TLAY): u = r, row 16 i + 4 gq + r, columns 8 ml .. +7 (acc[i][0..7][r])
+    //   B_T == 1: u = pp, row 16 i + ml, columns 32 pp + 8 gq .. +7 (acc[i][2 pp][0..3], acc[i][2 pp + 1][0..3])
+    const int row0 = B_T == 0 ? wm * 64 + 4 * gq : wm * 64 + ml;
+    const int col0 = B_T == 0 ? wn * 128 + 8 * ml : wn * 128 + 8 * gq;
+    // one 8-column row segment (i, u) at a time: the VGPR half of two waves per SIMD is 128 registers (the
+    // accumulators take the 128 AGPRs), so the side inputs, the arithmetic and the stores stay segment-local
+    static_for<16>([&](auto sc) {
+      constexpr int i = decltype(sc)::value >> 2, u = decltype(sc)::value & 3;
+      const int row = row0 + 16 * i + (B_T == 0 ? u : 0);
+      const int col = col0 + (B_T == 0 ? 0 : 32 * u);
+      const int off = ct.n0 + col < p.N ? (row * ldcs + col) * ES : (int)0x80000000u;
+      float x[8];
+      static_for<8>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        if constexpr (B_T == 0) x[j] = alpha * acc[i][j][u];
+        else x[j] = alpha * acc[i][2 * u + (j >> 2)][j & 3];
+      });
+      if constexpr (OUT_F32) {
+        if constexpr (EX) {
+          if (p.R) {
+            const f32x4_t r0 = __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rr, off, 0, 0));
+            const f32x4_t r1 = __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rr, off + 16, 0, 0));
+            static_for<4>([&](auto tc) {
+              constexpr int t = decltype(tc)::value;
+              x[t] += r0[t];
+              x[4 + t] += r1[t];
+            });
           }
-        });
-        if (colok) {
-          static_for<4>([&](auto rk) {
-            constexpr int r = decltype(rk)::value;
-            const int vo_ = vt + (16 * i + r) * ES * ldcs;
-            __builtin_amdgcn_raw_buffer_store_b128(o0[r], rc, vo_, 0, 0);
-            if constexpr (OUT_F32) __builtin_amdgcn_raw_buffer_store_b128(o1[r], rc, vo_ + 16, 0, 0);
+          if (beta != 0.f) {
+            const f32x4_t c0 = __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rc, off, 0, 0));
+            const f32x4_t c1 = __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rc, off + 16, 0, 0));
+            static_for<4>([&](auto tc) {
+              constexpr int t = decltype(tc)::value;
+              x[t] += beta * c0[t];
+              x[4 + t] += beta * c1[t];
+            });
+          }
+        }
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32_t, f32x4_t{x[0], x[1], x[2], x[3]}), rc, off, 0,
+                                               0);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32_t, f32x4_t{x[4], x[5], x[6], x[7]}), rc,
+                                               off + 16, 0, 0);
+      } else {
+        if constexpr (EX) {
+          const v4u32_t rv = __builtin_amdgcn_raw_buffer_load_b128(rr, off, 0, 0);
+          static_for<4>([&](auto tc) {
+            constexpr int t = decltype(tc)::value;
+            x[2 * t] += bf2f(rv[t] & 0xffff);
+            x[2 * t + 1] += bf2f(rv[t] >> 16);
           });
         }
-        fence();
-      });
+        if constexpr (AC == 1) {
+          const v4u32_t zo = v4u32_t{pack_bf16x2(x[0], x[1]), pack_bf16x2(x[2], x[3]), pack_bf16x2(x[4], x[5]),
+                                     pack_bf16x2(x[6], x[7])};
+          __builtin_amdgcn_raw_buffer_store_b128(zo, rz, off, 0, 0);
+          static_for<8>([&](auto tc) { x[decltype(tc)::value] = act_fwd(ACTK, x[decltype(tc)::value]); });
+        } else if constexpr (AC == 2) {
+          const v4u32_t zv = __builtin_amdgcn_raw_buffer_load_b128(rz, off, 0, 0);
+          static_for<4>([&](auto tc) {
+            constexpr int t = decltype(tc)::value;
+            x[2 * t] *= act_grad(ACTK, bf2f(zv[t] & 0xffff));
+            x[2 * t + 1] *= act_grad(ACTK, bf2f(zv[t] >> 16));
+          });
+        }
+        const v4u32_t o = v4u32_t{pack_bf16x2(x[0], x[1]), pack_bf16x2(x[2], x[3]), pack_bf16x2(x[4], x[5]),
+                                  pack_bf16x2(x[6], x[7])};
+        __builtin_amdgcn_raw_buffer_store_b128(o, rc, off, 0, 0);
+        if constexpr (AC != 1) __builtin_amdgcn_raw_buffer_store_b128(o, rc, (int)0x80000000u, 0, 0);   // count pad
+      }
+      if constexpr ((decltype(sc)::value & 3) == 3) fence();
+    });
+  };
+  auto epilogue = [&](const Tile4& ct) __attribute__((always_inline)) {
+    fence();
+    pad_redefine48(acc);
+    fence();
+    using F0 = std::false_type;
+    using T0 = std::true_type;
+    using A0 = std::integral_constant<int, 0>;
+    using A1 = std::integral_constant<int, 1>;
+    using A2 = std::integral_constant<int, 2>;
+    using KG = std::integral_constant<int, ACT_GELU>;
+    using KR = std::integral_constant<int, ACT_RELU>;
+    const bool ex = (OUT_F32 && p.ksplit <= 1 && p.beta != 0.f) || p.R != nullptr;
+    if constexpr (OUT_F32) {
+      if (ex) epilogue_v(ct, T0{}, A0{}, KG{});
+      else epilogue_v(ct, F0{}, A0{}, KG{});
     } else {
-      // lane (ml, gq): row 16 i + ml, columns 32 pp + 8 gq .. +7 (fragments 2 pp, 2 pp + 1)
-      const int vt = ((wm * 64 + ml) * ldcs + wn * 128 + 8 * gq) * ES;
-      const int nb = ct.n0 + wn * 128 + 8 * gq;
-      static_for<4>([&](auto ic) {
-        constexpr int i = decltype(ic)::value;
-        static_for<4>([&](auto pc) {
-          constexpr int pp = decltype(pc)::value;
-          const f32x4_t va = alpha * acc[i][2 * pp], vb = alpha * acc[i][2 * pp + 1];
-          if (nb + 32 * pp < p.N) {
-            const int vo_ = vt + i * 16 * ES * ldcs + pp * 32 * ES;
-            if constexpr (OUT_F32) {
-              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32_t, va), rc, vo_, 0, 0);
-              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32_t, vb), rc, vo_ + 16, 0, 0);
-            } else {
-              __builtin_amdgcn_raw_buffer_store_b128(
-                  v4u32_t{pack_bf16x2(va[0], va[1]), pack_bf16x2(va[2], va[3]), pack_bf16x2(vb[0], vb[1]),
-                          pack_bf16x2(vb[2], vb[3])},
-                  rc, vo_, 0, 0);
-            }
-          }
-        });
-        fence();
-      });
+      // (the dispatcher sends an activation here only without a residual: gemm8w_supported)
+      if (p.act == ACT_GELU) {
+        if (p.mode == 1) epilogue_v(ct, F0{}, A2{}, KG{});
+        else epilogue_v(ct, F0{}, A1{}, KG{});
+      } else if (p.act == ACT_RELU) {
+        if (p.mode == 1) epilogue_v(ct, F0{}, A2{}, KR{});
+        else epilogue_v(ct, F0{}, A1{}, KR{});
+      } else if (ex) {
+        epilogue_v(ct, T0{}, A0{}, KG{});
+      } else {
+        epilogue_v(ct, F0{}, A0{}, KG{});
+      }
     }
     fence();
   };
@@ -410,3 +499,9 @@ hipError_t launch8w(GemmArgs a, int batch, hipStream_t stream) {
 }
 
 }  // namespace
+
+// one operand-layout pair per translation unit (gemm8w_<a_t><b_t>.hip)
+#define OBST_GEMM8W_TU(AT, BT)                                                                                      \
+  hipError_t gemm8w_launch_##AT##BT(const gemmk::GemmArgs* a, int out_f32, int batch, hipStream_t stream) {      \
+    return out_f32 ? launch8w<AT, BT, true>(*a, batch, stream) : launch8w<AT, BT, false>(*a, batch, stream);    \
+  }
