@@ -25,7 +25,7 @@ build/kernels/%.o: csrc/kernels/%.cpp $(wildcard csrc/kernels/*.h)
 	$(HIPCC) -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-result -c $< -o $@
 
 $(PKG)/_kernels.so: $(KOBJ)
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(KOBJ) -L/opt/rocm/lib -lhipblaslt -Wl,-rpath,/opt/rocm/lib
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(KOBJ)
 
 build/runtime/%.o: csrc/runtime/%.cpp $(wildcard csrc/runtime/*.h)
 	@mkdir -p build/runtime

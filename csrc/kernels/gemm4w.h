@@ -295,7 +295,24 @@ struct Tile4 {
   int nk;   // K-tiles of this tile (the K range of a triangular A, see decode4)
 };
 
-template <int A_T, int B_T>
+// split contraction index (GemmArgs::kin > 0, K-contiguous operands): contraction index k lives at element
+// (k / kin) * sk + k % kin of a row -- the token mixer's weight gradient contracts over (batch, feature) pairs of a
+// [B, S, H, F] tensor in place (kin = F, sk = S * H * F). Whole 64-deep K-tiles lie inside one kin block, and every
+// split-K slab starts on a block boundary (obst_gemm), so a slab's first element is split * kin_bps * sk -- no
+// runtime division (which the compiler would run in VGPRs and then feed to the SGPR-only asm operands).
+template <bool KIN>
+__device__ __forceinline__ long long kin_map(long long k, int split, const GemmArgs& p, long long sk) {
+  return KIN ? (long long)split * p.kin_bps * sk : k;
+}
+
+// output tiles of a launch: tri 3 (only C[m][n], n <= m, receives the product; M == N) walks the lower-triangle tiles
+// (the diagonal included) of every batch
+__host__ __device__ __forceinline__ long long tiles_total(const GemmArgs& p) {
+  const long long per = p.tri == 3 ? (long long)p.tiles_m * (p.tiles_m + 1) / 2 : (long long)p.tiles_m * p.tiles_n;
+  return per * p.nbatch;
+}
+
+template <int A_T, int B_T, bool KIN = false>
 __device__ __forceinline__ Tile4 decode4(const GemmArgs& p, long long L64) {
   // unsigned 32-bit index arithmetic (a launch has < 2^31 tiles): the 64-bit divisions were ~170 SALU ops on the
   // MFMA stream's critical path at every tile switch
@@ -303,7 +320,19 @@ __device__ __forceinline__ Tile4 decode4(const GemmArgs& p, long long L64) {
   Tile4 T;
   int tm, tn;
   unsigned ybat;
-  if (p.tri == 0) {
+  if (KIN && p.tri == 3) {
+    // (the split-index instantiation only: the causal mixer weight gradient)
+    // lower-triangle tiles of each batch, row by row: tile row tm holds tm + 1 tiles (tn <= tm); all of equal work
+    const unsigned per = (unsigned)(p.tiles_m * (p.tiles_m + 1) / 2);
+    unsigned bid = L % per;
+    ybat = L / per;
+    tm = 0;
+    while (bid > (unsigned)tm) {   // at most tiles_m steps, once per tile switch
+      bid -= (unsigned)tm + 1;
+      ++tm;
+    }
+    tn = (int)bid;
+  } else if (p.tri == 0) {
     const unsigned ntile = (unsigned)(p.tiles_m * p.tiles_n);
     const int bid = (int)(L % ntile);
     ybat = L / ntile;
@@ -339,11 +368,14 @@ __device__ __forceinline__ Tile4 decode4(const GemmArgs& p, long long L64) {
   }
   const bf16_t* A = p.A + b1 * p.a_s1 + b2 * p.a_s2;
   const bf16_t* B = p.B + b1 * p.b_s1 + b2 * p.b_s2;
-  // extent of each operand (elements from its batch base): [M][lda] rows / [K][lda] k-rows
-  const long long aext = A_T == 0 ? (long long)(p.M - 1) * p.lda + p.K : (long long)(p.K - 1) * p.lda + p.M;
-  const long long bext = B_T == 0 ? (long long)(p.N - 1) * p.ldb + p.K : (long long)(p.K - 1) * p.ldb + p.N;
-  const long long aoff = A_T == 0 ? (long long)T.m0 * p.lda + kbeg : kbeg * p.lda + T.m0;
-  const long long boff = B_T == 0 ? (long long)T.n0 * p.ldb + kbeg : kbeg * p.ldb + T.n0;
+  // extent of each operand (elements from its batch base): [M][lda] rows / [K][lda] k-rows; with a split
+  // contraction index (K-contiguous only) a row spans (K / kin - 1) * sk + kin elements
+  const long long kext_a = KIN ? (long long)(p.kin_bps * p.ksplit - 1) * p.a_sk + p.kin : p.K;   // K / kin blocks
+  const long long kext_b = KIN ? (long long)(p.kin_bps * p.ksplit - 1) * p.b_sk + p.kin : p.K;
+  const long long aext = A_T == 0 ? (long long)(p.M - 1) * p.lda + kext_a : (long long)(p.K - 1) * p.lda + p.M;
+  const long long bext = B_T == 0 ? (long long)(p.N - 1) * p.ldb + kext_b : (long long)(p.K - 1) * p.ldb + p.N;
+  const long long aoff = A_T == 0 ? (long long)T.m0 * p.lda + kin_map<KIN>(kbeg, T.split, p, p.a_sk) : kbeg * p.lda + T.m0;
+  const long long boff = B_T == 0 ? (long long)T.n0 * p.ldb + kin_map<KIN>(kbeg, T.split, p, p.b_sk) : kbeg * p.ldb + T.n0;
   T.a = reinterpret_cast<const char*>(A + aoff);
   T.b = reinterpret_cast<const char*>(B + boff);
   T.arem = (aext - aoff) * 2;
@@ -413,10 +445,12 @@ constexpr int idx(const int (&a)[8], int q) {
 //   2 STAGGER: blocks start (slot & 7) / 8 of a tile apart (s_sleep), so the CUs' epilogue store bursts do not
 //     coincide on the fabric
 template <int A_T, int B_T, bool OUT_F32, bool PROF, int NWV = 4, int SCH = G4W_SCH, bool STG = (G4W_STG != 0),
-          int CPA = G4W_CPA, int CPB = G4W_CPB, int OPT = G4W_OPT>
+          int CPA = G4W_CPA, int CPB = G4W_CPB, int OPT = G4W_OPT, bool KINT = false>
 __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   constexpr bool RELAX = (OPT & 1) != 0, STAGGER = (OPT & 2) != 0, LATE = (OPT & 4) != 0;
+  // split contraction index (+ tri 3): its own instantiation, so the plain kernel carries none of it
+  constexpr bool KIN = KINT && A_T == 0 && B_T == 0;
   constexpr int SC = (OPT >> 3) & 7;   // cache policy of the direct epilogue's C stores
   constexpr bool ROWS = (OPT & 64) != 0;   // plain products: C rows staged through LDS, row-contiguous stores
   // TLAY: row-layout accumulators for K-contiguous B (frag_b): row-contiguous epilogue stores without data movement
@@ -439,12 +473,12 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = NWV == 4 ? wave >> 1 : wave & 1, wn = NWV == 4 ? wave & 1 : wave >> 1;
 
-  const long long total = (long long)p.tiles_m * p.tiles_n * p.nbatch;
+  const long long total = KIN ? tiles_total(p) : (long long)p.tiles_m * p.tiles_n * p.nbatch;
   const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3, nslot = gridDim.x >> 3;
   const long long Q = total >> 3, Rm = total & 7;
-  // dense: XCD x walks a contiguous run of tiles (L2 sharing of A / B panels); triangular: block-cyclic over the
-  // whole grid (decode4 orders the tiles by work, so each round is balanced)
-  const bool cyc = p.tri != 0;
+  // dense: XCD x walks a contiguous run of tiles (L2 sharing of A / B panels); triangular A: block-cyclic over the
+  // whole grid (decode4 orders the tiles by work, so each round is balanced); tri 3: tiles of equal work, dense walk
+  const bool cyc = KIN ? (p.tri == 1 || p.tri == 2) : p.tri != 0;
   const long long start = cyc ? 0 : xcd < Rm ? xcd * (Q + 1) : Rm * (Q + 1) + (xcd - Rm) * Q;
   const long long len = cyc ? total : Q + (xcd < Rm ? 1 : 0);
   const long long first = cyc ? blockIdx.x : slot;
@@ -469,16 +503,20 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
   // position into the stage nobody reads any more
   // (the cursor's operand bases and bytes left advance by one K step in SALU adds; the resource clamps the bytes
   // left with a 32-bit select -- a K-tile's setup was ~30 VALU/SALU ops of 64-bit signed compares at one slot)
-  int d_rnd = 0, d_kt = 0, d_nk = 0;
+  int d_rnd = 0, d_kt = 0, d_nk = 0, d_kin = 0;   // d_kin: K-tiles left in the cursor's kin block
   unsigned long long cur_a, cur_b, rem_a, rem_b;
+  // split contraction index: at a kin-block boundary the cursor also jumps over the rest of the outer stride
+  // (only the K-contiguous pair can carry a split contraction index: obst_gemm; the other layouts compile it out)
+  const int kin_tiles = KIN ? p.kin >> 6 : 0;
   auto cursor_tile = [&](const Tile4& T) {
     d_nk = T.nk;
+    d_kin = kin_tiles;   // (slabs start on kin-block boundaries)
     cur_a = (unsigned long long)T.a;
     cur_b = (unsigned long long)T.b;
     rem_a = (unsigned long long)T.arem;   // > 0 at every position the cursor visits
     rem_b = (unsigned long long)T.brem;
   };
-  cursor_tile(decode4<A_T, B_T>(p, logical(0)));
+  cursor_tile(decode4<A_T, B_T, KIN>(p, logical(0)));
   auto rsrc_of = [](unsigned long long base, unsigned long long rem) {
     i32x4_t r;
     r[0] = (int)(unsigned)base;
@@ -501,12 +539,21 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
       rem_a -= astep;
       cur_b += bstep;
       rem_b -= bstep;
+      if (KIN && --d_kin == 0) {   // (uniform; p.kin == 0 for every product but the mixer weight gradient)
+        d_kin = kin_tiles;
+        const unsigned long long ajump = (unsigned long long)(p.a_sk - p.kin) * 2;
+        const unsigned long long bjump = (unsigned long long)(p.b_sk - p.kin) * 2;
+        cur_a += ajump;
+        rem_a -= ajump;
+        cur_b += bjump;
+        rem_b -= bjump;
+      }
     } else if (d_rnd + 1 < ntiles) {
       // once per tile: the volatile asm keeps the compiler from if-converting the decode into every K-tile
       asm volatile("");
       ++d_rnd;
       d_kt = 0;
-      cursor_tile(decode4<A_T, B_T>(p, logical(d_rnd)));
+      cursor_tile(decode4<A_T, B_T, KIN>(p, logical(d_rnd)));
     }
   };
 
@@ -575,7 +622,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
 
     int pos = 0;   // flat position of the K-tile being multiplied (its stage is pos & 1)
     for (int rnd = 0; rnd < ntiles; ++rnd) {
-      const Tile4 ct = decode4<A_T, B_T>(p, logical(rnd));
+      const Tile4 ct = decode4<A_T, B_T, KIN>(p, logical(rnd));
       // Accumulator zeroing (VALU writes of AGPRs) -> first MFMA reading them needs wait states the compiler cannot
       // see through the asm MFMAs; the empty "+a" asms pin the zeros before the pad (no rematerialisation past it)
   #pragma unroll
@@ -1155,15 +1202,22 @@ hipError_t launch4w(GemmArgs a, int batch, hipStream_t stream) {
   a.tiles_m = (a.M + 255) / 256;
   a.tiles_n = (a.N + 255) / 256;
   a.nbatch = batch * a.ksplit;
-  const long long tiles = (long long)a.tiles_m * a.tiles_n * a.nbatch;
+  const long long tiles = tiles_total(a);
   // one block per CU (32 per XCD); fewer for small launches, keeping a multiple of the 8 XCDs
   const int grid = (int)(tiles >= 256 ? 256 : ((tiles + 7) / 8) * 8);
   const size_t lds = 2 * Q_STAGE + 32768;   // 160 KiB: two stages + the epilogue regions (16 rows x 128 fp32 per SIMD)
   auto k = a.stamps ? gemm4w_kernel<A_T, B_T, F32, true, NWV> : gemm4w_kernel<A_T, B_T, F32, false, NWV>;
-  static bool attr[2] = {false, false};
-  if (!attr[a.stamps != nullptr]) {
+  int which = a.stamps != nullptr;
+  if constexpr (A_T == 0 && B_T == 0) {
+    if (a.kin) {   // the split contraction index (token-mixer weight gradient) has its own instantiation
+      k = gemm4w_kernel<A_T, B_T, F32, false, NWV, G4W_SCH, (G4W_STG != 0), G4W_CPA, G4W_CPB, G4W_OPT, true>;
+      which = 2;
+    }
+  }
+  static bool attr[3] = {false, false, false};
+  if (!attr[which]) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    attr[a.stamps != nullptr] = true;
+    attr[which] = true;
   }
   hipLaunchKernelGGL(k, dim3(grid), dim3(64 * NWV), lds, stream, a);
   return hipGetLastError();

@@ -1,5 +1,5 @@
-// Host-side GEMM descriptor shared by the MFMA kernels (gemm.hip) and the hipBLASLt path (blaslt.cpp); the ctypes
-// mirror is GemmDesc in homebrewnlp_mtf_amd/ops/_lib.py.
+// Host-side GEMM descriptor of the MFMA kernels (gemm.hip, gemm4w.h); the ctypes mirror is GemmDesc in
+// homebrewnlp_mtf_amd/ops/_lib.py. (tools/lab/blaslt.cpp, the hipBLASLt A/B harness, takes the same descriptor.)
 #pragma once
 struct ObstGemmDesc {
   const void* A; const void* B; void* C; const void* R; void* Zout; const void* Zin;
@@ -9,13 +9,11 @@ struct ObstGemmDesc {
   int a_t, b_t, out_f32, act, mode;
   float alpha, beta;
   int tri;
-  // split contraction index (MFMA phase kernel, K-contiguous operands only): k -> (k / kin) * sk + k % kin, i.e.
+  // split contraction index (gemm4w, K-contiguous operands only): k -> (k / kin) * sk + k % kin, i.e.
   // K = (outer, inner) with inner blocks of kin contiguous elements and an outer stride a_sk / b_sk (0: plain K)
   int kin;
   long long a_sk, b_sk;
 };
 
-// plain GEMMs through hipBLASLt: 0 done, 1 not eligible (run the MFMA kernels), < 0 hipBLASLt error
+// (tools/lab only) the same products through hipBLASLt: 0 done, 1 not eligible, < 0 hipBLASLt error
 int obst_blaslt_gemm(const ObstGemmDesc* d, hipStream_t stream);
-// the same, with the fp32 weight-gradient products of few output tiles split over K (blaslt.cpp)
-int obst_blaslt_gemm_split(const ObstGemmDesc* d, hipStream_t stream);

@@ -1,5 +1,5 @@
-// Shared by the MFMA GEMM translation units (gemm.hip: 128x128 and phase kernels and the dispatcher;
-// gemm_pp.hip: the persistent phase kernel, split out so the two heavy template sets compile in parallel).
+// Shared by the MFMA GEMM translation units (gemm.hip: the 128x128 kernel and the dispatcher; gemm4w*.hip: the
+// one-wave-per-SIMD 256x256 kernel).
 #pragma once
 #include "common.h"
 
@@ -17,11 +17,12 @@ struct GemmArgs {
   int act, mode;          // mode 0: out = act(alpha*acc + R); mode 1: out = (alpha*acc + R) * act'(Zin)
   int tri;                // 0 dense; 1 A lower-triangular (A[m][k] = 0 for k > m); 2 A upper-triangular (k < m);
                           // 3 only C[m][n] with n <= m is produced (strictly-upper outputs get no contribution)
-  int ksplit;             // phase kernel only: K split over blockIdx.y; partial tiles go to `ws` [split][M][N]
+  int ksplit;             // gemm4w: K split into ksplit slabs; partial tiles go to `ws` [batch][split][M][N]
   float* ws;              // split-K workspace (fp32), summed into C by splitk_reduce_kernel
-  int kin;                // phase kernel only: split contraction index, see ObstGemmDesc (0: plain K)
+  int kin;                // gemm4w: split contraction index, see ObstGemmDesc (0: plain K)
   long long a_sk, b_sk;
-  int nbatch;             // persistent phase kernel: batches (the grid is one block per CU)
+  int kin_bps;            // kin blocks per split-K slab (K / ksplit / kin; slabs start on block boundaries)
+  int nbatch;             // gemm4w: batches x splits (the grid is one block per CU)
   unsigned long long* stamps;   // gemm4w diagnostics: per-block timestamps (null: off)
 };
 }  // namespace gemmk
@@ -54,45 +55,6 @@ __device__ __forceinline__ bf16x8_t read_frag(const char* lds, int rbase, int kk
     s16x4_t v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4_t, lds + off1));
     s16x8_t v = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
     return __builtin_bit_cast(bf16x8_t, v);
-  }
-}
-
-
-constexpr int BM2 = 256, BN2 = 256, NT2 = 512;
-
-__device__ __forceinline__ void glds16(const bf16_t* src, char* lds_base) {
-  __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
-                                   (void __attribute__((address_space(3)))*)lds_base, 16, 0, 0);
-}
-
-
-constexpr int PIECE = 16384;
-
-__device__ __forceinline__ void bar() {
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
-
-template <int T, bool IS_A>
-__device__ __forceinline__ void stage_piece(char* img, const bf16_t* X, long long ld, int base0, int R, long long k0,
-                                            int q, int wave, int lane) {
-#pragma unroll
-  for (int rd = 0; rd < 2; ++rd) {
-    const int jj = rd * 8 + wave;            // 1 KiB sub-piece
-    const bf16_t* src;
-    if (T == 0) {                            // [128 rows][64 k], 128-B rows
-      const int lr = jj * 8 + (lane >> 3), pc = lane & 7;
-      const int c = pc ^ ((lr >> 1) & 7);
-      const int row = min(base0 + q * 128 + lr, R - 1);
-      src = X + (long long)row * ld + k0 + c * 8;
-    } else {                                 // [64 k][128 cols], 256-B rows
-      const int kr = jj * 4 + (lane >> 4), pc = lane & 15;
-      const int lc = (pc ^ kswz(kr)) * 8;
-      const int col = min(base0 + q * 128 + lc, R - 8);
-      src = X + (long long)(k0 + kr) * ld + col;
-    }
-    glds16(src, img + jj * 1024);
   }
 }
 
@@ -251,7 +213,5 @@ __device__ __forceinline__ void epilogue_store8r(const GemmArgs& p, long long id
 
 }  // namespace
 
-// the persistent phase kernel (gemm_pp.hip) for a GemmArgs filled by obst_gemm: plain products on whole tiles
-hipError_t gemm_pp_launch(const gemmk::GemmArgs* a, int a_t, int b_t, int out_f32, int batch, hipStream_t stream);
 // the one-wave-per-SIMD 256x256 kernel (gemm4w.hip) for a GemmArgs filled by obst_gemm (ksplit / ws set)
 hipError_t gemm4w_launch(const gemmk::GemmArgs* a, int a_t, int b_t, int out_f32, int batch, hipStream_t stream);

@@ -113,15 +113,7 @@ _SIGS = {
     "obst_opt_fold": [ctypes.POINTER(OptDesc), c_p, c_i, c_p],
     "obst_opt_apply_rows": [ctypes.POINTER(OptDesc), c_p, c_i, c_p],
     "obst_opt_factored": [ctypes.POINTER(OptDesc), c_p, c_p, c_i, c_p, c_i, c_p, c_p, c_p],
-    "obst_blaslt_enabled": [],
-    "obst_blaslt_set": [c_i],
-    "obst_blaslt_scope": [c_i],
-    "obst_blaslt_splitk_calls": [],
-    "obst_gemm4w_enabled": [],
-    "obst_gemm4w_set": [c_i],
 
-    "obst_blaslt_splitk_set": [c_i],
-    "obst_blaslt_stats": [c_p],
     "obst_glu": [c_p, c_p, c_p, c_p, c_p, c_ll, c_p],
     "obst_pkm_top1": [c_p, c_p, c_p, c_p, c_p, c_ll, c_i, c_i, c_p],
     "obst_pkm_top1_bwd": [c_p, c_p, c_p, c_p, c_p, c_p, c_ll, c_i, c_i, c_p],
@@ -142,7 +134,7 @@ _SIGS = {
     "obst_calib_mfma_flops": [c_i],
     "obst_decode_attn": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_f, c_i, c_p, c_p],
 }
-_RESTYPES = {"obst_calib_mfma_flops": ctypes.c_double, "obst_norm_bwd_ws": c_ll, "obst_skinny_ws": c_ll, "obst_scatter_ws": c_ll, "obst_blaslt_splitk_calls": c_ll}
+_RESTYPES = {"obst_calib_mfma_flops": ctypes.c_double, "obst_norm_bwd_ws": c_ll, "obst_skinny_ws": c_ll, "obst_scatter_ws": c_ll}
 
 
 def lib():

@@ -106,18 +106,13 @@ def linear_plan(xdims: tuple, wdims: tuple, odims: tuple) -> LinearPlan:
     return LinearPlan(list(xdims), list(wdims), list(odims))
 
 
-# Operand layouts on the GPU. Plain GEMMs run on hipBLASLt (raw.lt_enabled()), which reads every layout at full
-# rate: no copies. The fused-epilogue GEMMs run on the MFMA kernels, whose K-contiguous (ds_read_b128) path is
-# 25-35 % faster than the transposed-read path, so for those the forward reads a cached [N][K] copy of the weight;
-# with hipBLASLt off, the weight gradient also reads token-contiguous transposes of x and dy
-# (`OBST_TRANSPOSED_OPERANDS=0` turns the copies off for A/B measurements).
+# Operand layouts on the GPU. The MFMA kernels' K-contiguous (ds_read_b128) path beats the transposed-read path and
+# lets gemm4w keep its row-layout (TLAY) epilogue, so the forward reads a cached [N][K] copy of the weight; gemm4w
+# reads the token-strided layouts of the weight gradient at full rate, so x and dy are not transposed
+# (`OBST_TRANSPOSED_OPERANDS=0` turns the weight copies off for A/B measurements).
 _KCONTIG = __import__("os").environ.get("OBST_TRANSPOSED_OPERANDS", "1") != "0"
-# hipBLASLt forward GEMMs also read the cached [N][K] weight copy: on the GPT-Neo-1.3B step the same product runs
-# 1444 TF/s with the weight K-contiguous against 1256 TF/s on the stored [K][N] layout (tools/gemm_census.py,
-# profiles/r2_gemm_census.md); refreshing every copy costs one transpose pass over the bf16 weights per step (~1 ms).
-# Decode-step products (M = 32 tokens) gain too: 6.1-12.4 us against 7.1-21.5 us per projection
-# (tools/lab/bench_skinny.py, profiles/r2_skinny_gemm.txt).
-_FWD_WT = __import__("os").environ.get("OBST_FWD_WT", "1") != "0"
+# Refreshing every copy costs one transpose pass over the bf16 weights per step (~1 ms); decode-step products
+# (M = 32 tokens, skinny.hip) need the K-contiguous copy too.
 # OBST_ATTN_FUSED_RESIDUAL=0: the attention block's residual add as a separate elementwise pass (A/B)
 _ATTN_RES = __import__("os").environ.get("OBST_ATTN_FUSED_RESIDUAL", "1") == "1"
 
@@ -126,9 +121,6 @@ def _wT(w, plan: LinearPlan, act=None, has_r: bool = False):
     store = getattr(w, "store", None)
     if not _KCONTIG or store is None or not raw.on_gpu(w) or w.dtype != torch.bfloat16:
         return None
-    if raw.lt_enabled() and (act is None or (act == "gelu" and not has_r)):   # runs on hipBLASLt (blaslt.cpp)
-        if not _FWD_WT:
-            return None
     if plan.K % 8 or plan.N % 8:
         return None
     return store.transposed(w.var_name, plan.H, plan.K, plan.N)
@@ -186,7 +178,7 @@ def tokens_transposed(x2, rows: int, cols: int) -> typing.Optional[torch.Tensor]
     """[rows][cols] bf16 -> [cols][rows] (None where the plain transposed-read GEMM is used instead)"""
     if not _KCONTIG or not raw.on_gpu(x2) or x2.dtype != torch.bfloat16 or rows % 8 or cols % 8:
         return None
-    if raw.lt_takes_f32() or raw.g4w_enabled():   # both read the token-strided layouts at full rate
+    if raw.on_gpu(x2):   # gemm4w reads the token-strided layouts at full rate
         return None
     out = torch.empty(cols * rows, dtype=x2.dtype, device=x2.device)
     raw.transpose(x2, out, rows, cols, cols, rows)
@@ -205,21 +197,6 @@ def _wgrad_gemm(x2, dy2, gw, plan: LinearPlan, xT=None, dyT=None, beta: float = 
     M, H, K, N = plan.M, plan.H, plan.K, plan.N
     if xT is None:
         xT = tokens_transposed(x2, M, H * K)
-    lt_big = (xT is None and dyT is None and raw.on_gpu(x2) and raw.lt_takes_f32() and H == 1 and M % 8 == 0
-              and K % 8 == 0 and N % 8 == 0)
-    if lt_big and N >= 2 * K and N >= 4096:
-        # hipBLASLt reads a token-contiguous x ~20 % faster than the token-strided one (tools/lab/bench_wgrad.py); the
-        # saving grows with N while the transpose costs ~K: worth it for the d -> 2d projections
-        xT = torch.empty(K * M, dtype=x2.dtype, device=x2.device)
-        raw.transpose(x2, xT, M, K, K, M)
-    elif lt_big and K >= 2 * N and K >= 4096:
-        # the 2d -> d projections: token-contiguous dy (the narrow operand, cheap to transpose) -- T 131072,
-        # 4096 -> 2048: 1562 us (+ 220 us transpose) against 2041 us token-strided (profiles/r2_wgrad_layouts.txt)
-        dyT = torch.empty(N * M, dtype=dy2.dtype, device=dy2.device)
-        raw.transpose(dy2, dyT, M, N, N, M)
-        raw.gemm(raw.Operand(x2, 1, K, K * M), raw.Operand(dyT, 0, M, N * M), raw.Operand(gw, 0, N, K * N),
-                 K, N, M, beta=beta)
-        return
     if xT is not None and dyT is None:
         dyT = tokens_transposed(dy2, M, H * N)
     if xT is not None and dyT is not None:
@@ -509,12 +486,7 @@ class _DotAttention(torch.autograd.Function):
         # all-reduce of the partial dbase runs on RCCL's stream under the three k/q/v weight-gradient GEMMs
         pending = (pstate.tp_all_reduce_async(dbase) if p_out.col_parallel and pstate.tp_size() > 1
                    else pstate._DONE)
-        baseT = None
-        if raw.on_gpu(base) and raw.lt_takes_f32() and T % 8 == 0 and K % 8 == 0:
-            # one transpose of base serves the three q/k/v weight gradients (tools/lab/bench_wgrad.py: -118 us each
-            # against the token-strided layout, for one 122 us transpose)
-            baseT = torch.empty(K * T, dtype=base.dtype, device=base.device)
-            raw.transpose(base, baseT, T, K, K, T)
+        baseT = None   # (gemm4w reads the token-strided base at full rate: no transpose)
         outs = []
         for j in range(3):
             g, m, bj = _acc_grad_beta(ws[j])
@@ -633,7 +605,7 @@ class _TokenMixer(torch.autograd.Function):
         # dW[h] = dy_h · x_hᵀ over (batch, features), both read in place from [B, S, H, F]: the contraction index
         # (b, f) is split (kin = F contiguous features, outer stride S*H*F), so no [H][S][B*F] copies are made
         kk = B * Fd
-        if raw.on_gpu(dy) and Fd % 64 == 0 and S >= 256:
+        if raw.on_gpu(dy) and Fd % 64 == 0 and S % 8 == 0:
             raw.gemm(raw.Operand(dy, 0, hf, 0, Fd), raw.Operand(xc, 0, hf, 0, Fd), raw.Operand(g, 0, S, 0, S * S),
                      S, S, kk, batch=(1, H), beta=1.0, tri=3 if ctx.causal else 0, kin=Fd, a_sk=S * hf, b_sk=S * hf)
         else:

@@ -31,78 +31,17 @@ def on_gpu(t: torch.Tensor) -> bool:
     return t.device.type == "cuda"
 
 
-_LT = None
-_RSPLIT = __import__("os").environ.get("OBST_LT_RSPLIT", "0") == "1"   # A/B knob: measured 1 % slower
-# OBST_ACT_G4W=1 (A/B): activation GEMMs on gemm4w with the activation fused into the epilogue while the plain
-# products stay on hipBLASLt (OBST_LT_SCOPE=0 moves the fp32 weight gradients too)
-_ACT_G4W = __import__("os").environ.get("OBST_ACT_G4W", "0") == "1"
-
-
-def lt_enabled() -> int:
-    """0 (default): every GEMM on the hand-written gfx950 MFMA kernels (gemm4w); OBST_GEMM_LT=1 hands the plain
-    products to hipBLASLt (csrc/kernels/blaslt.cpp, A/B only), 2 also tries its own GELU epilogues"""
-    global _LT
-    if _LT is None:
-        _LT = int(L.lib().obst_blaslt_enabled())
-    return _LT
-
-
 def gemm_backend() -> str:
-    """which kernels run the plain GEMMs: "gemm4w" (the hand-written gfx950 MFMA kernel only) or
-    "hipblaslt+gemm4w" (the library takes the products OBST_LT_SCOPE gives it)"""
+    """which kernels run the GEMMs: "gemm4w" (every product on the hand-written gfx950 MFMA kernels -- gemm4w, the
+    128x128 fallback and the decode-step skinny kernel; no library GEMM is linked)"""
     if not L.available():
         return "torch-cpu"
-    return "hipblaslt+gemm4w" if lt_enabled() > 0 else "gemm4w"
+    return "gemm4w"
 
 
-_LT_SCOPE = None
-
-
-def lt_scope() -> int:
-    """which products hipBLASLt takes when it is on: 1 every eligible one, 0 only the bf16-output products (the fp32
-    weight gradients and the fused-activation GEMMs run on the hand-written gemm4w kernel; OBST_LT_SCOPE)"""
-    global _LT_SCOPE
-    if _LT_SCOPE is None:
-        _LT_SCOPE = int(L.lib().obst_blaslt_scope(-1))
-    return _LT_SCOPE
-
-
-def lt_scope_set(v: int) -> int:
-    global _LT_SCOPE
-    old = int(L.lib().obst_blaslt_scope(int(v)))
-    _LT_SCOPE = int(v)
-    return old
-
-
-def g4w_enabled() -> bool:
-    """the one-wave-per-SIMD 256x256 MFMA kernel (csrc/kernels/gemm4w.h) takes the plain products hipBLASLt declines"""
-    return bool(L.lib().obst_gemm4w_enabled())
-
-
-def lt_takes_f32() -> bool:
-    """hipBLASLt runs the fp32-output (weight-gradient) products"""
-    return lt_enabled() > 0 and lt_scope() > 0
-
-
-def lt_stats() -> typing.Tuple[int, int]:
-    """(GEMMs dispatched to hipBLASLt, eligible GEMMs it declined -- those ran on the MFMA kernels)"""
-    out = (ctypes.c_longlong * 2)()
-    L.lib().obst_blaslt_stats(ctypes.addressof(out))
-    return int(out[0]), int(out[1])
-
-
-def lt_set(on: bool) -> bool:
-    """switch the hipBLASLt path at run time (tests); returns the previous setting"""
-    global _LT
-    old = int(L.lib().obst_blaslt_set(int(on)))
-    _LT = int(on)
-    return old
-
-
-def lt_splitk_set(on: bool) -> bool:
-    """switch the split-K fp32 weight-gradient path of the hipBLASLt dispatch (few output tiles, K >= 16384: one
-    strided batch over K-slabs + a deterministic fold; OBST_LT_SPLITK) at run time; returns the previous setting"""
-    return bool(L.lib().obst_blaslt_splitk_set(int(on)))
+def gemm4w_calls() -> int:
+    """products dispatched to gemm4w so far (tests assert which kernel ran)"""
+    return int(L.lib().obst_gemm4w_calls())
 
 
 def _room(t: torch.Tensor) -> int:
@@ -183,12 +122,9 @@ class Operand(typing.NamedTuple):
     s2: int = 0
 
 
-# OBST_SKINNY_GEMM=1: decode-step projections (M <= 32 tokens) on the MFMA weight-streaming kernel
-# (csrc/kernels/skinny.hip) instead of hipBLASLt. Both read the cached K-contiguous weight copy; graph-replayed per
-# call the kernel takes 6.0-15.4 us where hipBLASLt takes 5.3-12.4 us on the GPT-Neo-1.3B projections (70 vs 32 us
-# on the 50304-wide logits, profiles/r2_skinny_gemm.txt) -- with hipBLASLt as the default it stayed opt-in.
-# Default ("auto"): on whenever hipBLASLt is off (the default) -- a 32-row product on gemm4w fills one 256-row tile
-# row per N tile, a few CUs for ~50 us where the weight-streaming kernel takes 6-15 us.
+# Decode-step projections (M <= 32 tokens) run on the MFMA weight-streaming kernel (csrc/kernels/skinny.hip) against
+# the cached K-contiguous weight copy, epilogue fused: a 32-row product on gemm4w would fill one 256-row tile row per
+# N tile on a few CUs. OBST_SKINNY_GEMM=0 sends them to gemm4w (A/B only).
 _SKINNY_ENV = __import__("os").environ.get("OBST_SKINNY_GEMM", "auto")
 _SKINNY = None if _SKINNY_ENV == "auto" else _SKINNY_ENV == "1"
 _SKINNY_WS: typing.Dict[typing.Any, torch.Tensor] = {}
@@ -197,7 +133,7 @@ _SKINNY_WS: typing.Dict[typing.Any, torch.Tensor] = {}
 def skinny_ok(M: int, N: int, K: int) -> bool:
     if not (0 < M <= 32 and N % 16 == 0 and K % 32 == 0):
         return False
-    return _SKINNY if _SKINNY is not None else lt_enabled() == 0
+    return _SKINNY if _SKINNY is not None else True
 
 
 def _skinny_ws(device, n: int) -> typing.Optional[torch.Tensor]:
@@ -247,14 +183,11 @@ def gemm(a: Operand, b: Operand, c: Operand, M: int, N: int, K: int, batch: typi
                                          L.stream_ptr()), "skinny_gemm")
         return c.t
     if (not kin and on_gpu(c.t) and act is not None and tri == 0
-            and ((lt_enabled() == 1 and lt_scope() > 0 and not _ACT_G4W)
-                 # decode-step activation backward: the skinny kernel + the elementwise pass
-                 or (act_bwd and skinny_ok(M, N, K) and R is None and alpha == 1.0 and a.trans == 0
-                     and b.trans == 0))
+            # decode-step activation backward: the skinny kernel + the elementwise pass
+            and (act_bwd and skinny_ok(M, N, K) and R is None and alpha == 1.0 and a.trans == 0 and b.trans == 0)
             and c.t.dtype == torch.bfloat16
             and b1 * b2 == 1 and c.ld == N and (M * N) % 8 == 0 and c.t.is_contiguous() and c.t.numel() == M * N):
-        # activation GEMM on hipBLASLt / the skinny kernel: plain product, then the elementwise kernel (pre-activation
-        # kept in Zout)
+        # activation backward of a decode-step product: plain product, then the elementwise kernel
         if not act_bwd:
             z = Zout if Zout is not None else torch.empty(M * N, dtype=torch.bfloat16, device=c.t.device)
             gemm(a, b, Operand(z, 0, N), M, N, K, alpha=alpha, R=R)
@@ -262,14 +195,6 @@ def gemm(a: Operand, b: Operand, c: Operand, M: int, N: int, K: int, batch: typi
         else:
             gemm(a, b, c, M, N, K, alpha=alpha, R=R)
             elementwise("act_bwd", Zin, c.t, z=c.t, act=act)    # in place: C = C * act'(Zin)
-        return c.t
-    if (not kin and on_gpu(c.t) and R is not None and act is None and tri == 0 and lt_enabled() == 1 and _RSPLIT
-            and c.t.dtype == torch.bfloat16 and b1 * b2 == 1 and c.ld == N and (M * N) % 8 == 0
-            and c.t.is_contiguous() and c.t.numel() == M * N and R.is_contiguous() and R.numel() == M * N):
-        # residual input: hipBLASLt's out-of-place beta*C path runs 2-3x slower than the plain product on some
-        # layouts (tools/lab/bench_gemm_k.py), so the plain product plus the elementwise add is faster
-        gemm(a, b, c, M, N, K, alpha=alpha)
-        elementwise("add", c.t, c.t, z=R)
         return c.t
     if on_gpu(c.t):
         out_f32 = c.t.dtype == torch.float32

@@ -25,12 +25,6 @@ def _close(gpu, ref, atol, rtol, what=""):
     assert bad == 0, f"{what}: {bad}/{r.numel()} out of tolerance, max err {err.max().item():.4g}"
 
 
-@pytest.fixture(params=[0, 1], ids=["mfma", "hipblaslt"])
-def lt(request, cuda):
-    """plain GEMMs on the MFMA kernels (0) or on hipBLASLt (1)"""
-    old = raw.lt_set(request.param)
-    yield request.param
-    raw.lt_set(old)
 
 
 def g4w_calls() -> int:
@@ -44,7 +38,7 @@ def g4w_calls() -> int:
 # ----------------------------------------------------------------------------------------------------------------
 @pytest.mark.parametrize("a_t,b_t", [(0, 0), (0, 1), (1, 0), (1, 1)])
 @pytest.mark.parametrize("M,N,K", [(128, 128, 64), (200, 136, 72), (512, 384, 256), (64, 8, 8)])
-def test_gemm_layouts(cuda, lt, a_t, b_t, M, N, K):
+def test_gemm_layouts(cuda, a_t, b_t, M, N, K):
     torch.manual_seed(M + N + K + 10 * a_t + b_t)
     A = (torch.randn(M * K) * 0.5).to(BF)
     B = (torch.randn(N * K) * 0.5).to(BF)
@@ -70,14 +64,13 @@ def test_gemm_identity_asymmetric(cuda):
     assert torch.equal(Cg.view(n, n).cpu(), B)
 
 
-def test_gemm_batched_epilogues(cuda, lt):
+def test_gemm_batched_epilogues(cuda):
     torch.manual_seed(3)
     H, M, K, N = 3, 96, 64, 40
     A = (torch.randn(M, H, K) * 0.5).to(BF)            # [M][H][K] -> batch stride K, ld H*K
     B = (torch.randn(H, K, N) * 0.5).to(BF)            # [H][K][N]
     R = (torch.randn(M, H, N) * 0.5).to(BF)
     outs = {}
-    n0 = raw.lt_stats()
     for dev in ("cpu", cuda):
         C = torch.zeros(M, H, N, dtype=BF, device=dev)
         Z = torch.zeros(M, H, N, dtype=BF, device=dev)
@@ -100,19 +93,15 @@ def test_gemm_batched_epilogues(cuda, lt):
     torch.cuda.synchronize()
     for name, g, c in zip(["C", "Z", "D", "G", "C2", "Z2", "D2"], outs[str(cuda)], outs["cpu"]):
         _close(g, c, 5e-2, 3e-2, f"batched epilogue {name}")
-    n1 = raw.lt_stats()
-    if lt:   # G on hipBLASLt (the batched activation GEMMs C, D, C2, D2 stay on the fused MFMA kernel)
-        assert n1[0] == n0[0] + 1 and n1[1] == n0[1], (n0, n1)
 
 
 @pytest.mark.parametrize("case", ["residual", "f32_accumulate", "shared_A_batch", "shared_A_batch_bt0",
                                   "two_level_batch"])
-def test_gemm_plain_paths(cuda, lt, case):
+def test_gemm_plain_paths(cuda, case):
     """the plain-GEMM shapes the model issues (residual input, fp32 accumulate, q/k/v batch over one input)"""
     torch.manual_seed(5)
     M, K, N, H = 256, 192, 136, 3
     outs = {}
-    n0 = raw.lt_stats()
     A = (torch.randn(M * H * K) * 0.5).to(BF)
     B = (torch.randn(H * K * N) * 0.5).to(BF)
     R = (torch.randn(M * H * N) * 0.5).to(BF)
@@ -129,8 +118,7 @@ def test_gemm_plain_paths(cuda, lt, case):
             raw.gemm(raw.Operand(a, 0, K, 0), raw.Operand(b, 1, N, K * N), raw.Operand(C, 0, N, M * N), M, N, K,
                      batch=(H, 1))
         elif case == "shared_A_batch_bt0":
-            # the class hipBLASLt faulted on (broadcast A, K-contiguous B, interleaved C columns as in the k|q|v
-            # projection): blaslt.cpp declines it, the MFMA kernel runs it
+            # broadcast A, K-contiguous B, interleaved C columns as in the k|q|v projection
             C = torch.zeros(M * H * N, dtype=BF, device=dev)
             raw.gemm(raw.Operand(a, 0, K, 0), raw.Operand(b, 0, K, K * N), raw.Operand(C, 0, H * N, N), M, N, K,
                      batch=(H, 1))
@@ -141,17 +129,12 @@ def test_gemm_plain_paths(cuda, lt, case):
         outs[str(dev)] = C
     torch.cuda.synchronize()
     _close(outs[str(cuda)], outs["cpu"], 5e-2, 3e-2, f"plain gemm {case}")
-    n1 = raw.lt_stats()
-    if lt and case == "shared_A_batch_bt0":   # never issued to hipBLASLt: ran on the MFMA kernel
-        assert n1 == n0, (n0, n1)
-    elif lt and case != "two_level_batch":   # the path under test really ran on hipBLASLt
-        assert n1[0] == n0[0] + 1 and n1[1] == n0[1], (n0, n1)
 
 
 @pytest.mark.parametrize("act_bwd", [False, True])
 @pytest.mark.parametrize("with_r", [False, True])
 @pytest.mark.parametrize("act", ["gelu", "relu"])
-def test_gemm_activation_split(cuda, lt, act_bwd, with_r, act):
+def test_gemm_activation_split(cuda, act_bwd, with_r, act):
     """activation GEMMs as the model issues them (contiguous, unbatched): hipBLASLt + elementwise or fused MFMA
     (gelu and relu take gemm4w's direct epilogue without a residual; ragged N = 520 masks columns per lane)"""
     torch.manual_seed(9)
@@ -161,7 +144,6 @@ def test_gemm_activation_split(cuda, lt, act_bwd, with_r, act):
     R = (torch.randn(M * N) * 0.5).to(BF)
     Zi = (torch.randn(M * N) * 1.5).to(BF)
     outs = {}
-    n0 = raw.lt_stats()
     for dev in ("cpu", cuda):
         C = torch.zeros(M * N, dtype=BF, device=dev)
         Z = torch.zeros(M * N, dtype=BF, device=dev)
@@ -172,9 +154,6 @@ def test_gemm_activation_split(cuda, lt, act_bwd, with_r, act):
     torch.cuda.synchronize()
     for name, g, c in zip("CZ", outs[str(cuda)], outs["cpu"]):
         _close(g, c, 5e-2, 3e-2, f"activation gemm {act} {name} bwd={act_bwd} R={with_r}")
-    n1 = raw.lt_stats()
-    if lt and act == "gelu":
-        assert n1[0] == n0[0] + 1, (n0, n1)
 
 
 def test_gemm_oob_rejected(cuda):
@@ -397,7 +376,7 @@ def test_cumsum(cuda):
 
 @pytest.mark.parametrize("K", [64, 128, 576])
 @pytest.mark.parametrize("a_t,b_t", [(0, 0), (0, 1), (1, 0), (1, 1)])
-def test_gemm_big_tile(cuda, lt, a_t, b_t, K):
+def test_gemm_big_tile(cuda, a_t, b_t, K):
     """shapes that take the 256x256 LDS-DMA kernels (>= 512 tiles), incl. ragged M/N edges; K = 576 runs the
     K loop's steady state (counted vmcnt) for 9 K-tiles. Repeats must be bitwise identical (race screen). On the
     "mfma" leg every product must run on gemm4w (persistent, direct and beta epilogues)."""
@@ -426,8 +405,7 @@ def test_gemm_big_tile(cuda, lt, a_t, b_t, K):
     raw.gemm(raw.Operand(Ad, a_t, lda), raw.Operand(Bd, b_t, ldb), raw.Operand(Cf, 0, N), M, N, K, beta=1.0)
     torch.cuda.synchronize()
     _close(Cf.view(M, N), ref + 1, 2e-2, 2e-2, f"gemm256 f32 {a_t}{b_t} K{K}")
-    if lt == 0:
-        assert g4w_calls() - c0 == 5, "the MFMA leg did not run gemm4w"
+    assert g4w_calls() - c0 == 5, "gemm4w did not run"
 
 
 @pytest.mark.parametrize("a_t,b_t", [(0, 0), (0, 1), (1, 0), (1, 1)])
@@ -435,49 +413,78 @@ def test_gemm_big_tile(cuda, lt, a_t, b_t, K):
 def test_gemm4w_ragged(cuda, a_t, b_t, out_f32):
     """gemm4w directly (hipBLASLt off) on ragged M / N -- 1, 17, 255, 257 rows (decode-sized products up to one row
     past a tile), padded ldc -- bf16 and fp32 outputs, batched, against the fp32 oracle"""
-    old = raw.lt_set(False)
-    try:
-        for M, N, K, nb in ((1, 264, 128, 3), (17, 8, 64, 2), (255, 520, 192, 1), (257, 256, 320, 2)):
-            if a_t == 1 and M % 8:
-                continue   # a [K][M] operand needs 16-byte rows
-            torch.manual_seed(M + N + K)
-            ldc = N + 8
-            A = (torch.randn(nb * M * K) * 0.5).to(BF)
-            B = (torch.randn(nb * N * K) * 0.5).to(BF)
-            lda = K if a_t == 0 else M
-            ldb = K if b_t == 0 else N
-            av = A.view(nb, M, K) if a_t == 0 else A.view(nb, K, M).transpose(1, 2)
-            bv = B.view(nb, N, K).transpose(1, 2) if b_t == 0 else B.view(nb, K, N)
-            ref = av.float() @ bv.float()
-            dt = torch.float32 if out_f32 else BF
-            C = torch.full((nb * M * ldc,), 7.0, dtype=dt, device=cuda)
-            c0 = g4w_calls()
-            raw.gemm(raw.Operand(A.to(cuda), a_t, lda, M * K), raw.Operand(B.to(cuda), b_t, ldb, N * K),
-                     raw.Operand(C, 0, ldc, M * ldc), M, N, K, batch=(nb, 1))
-            torch.cuda.synchronize()
-            assert g4w_calls() - c0 == 1, f"{M}x{N}x{K} did not run gemm4w"
-            Cv = C.view(nb, M, ldc)
-            _close(Cv[:, :, :N], ref, 3e-2 * math.sqrt(K / 64), 2e-2, f"gemm4w {a_t}{b_t} {M}x{N}x{K} f32={out_f32}")
-            assert torch.all(Cv[:, :, N:].float().cpu() == 7.0), "wrote past N into the ldc padding"
-    finally:
-        raw.lt_set(old)
+    for M, N, K, nb in ((1, 264, 128, 3), (17, 8, 64, 2), (255, 520, 192, 1), (257, 256, 320, 2)):
+        if a_t == 1 and M % 8:
+            continue   # a [K][M] operand needs 16-byte rows
+        torch.manual_seed(M + N + K)
+        ldc = N + 8
+        A = (torch.randn(nb * M * K) * 0.5).to(BF)
+        B = (torch.randn(nb * N * K) * 0.5).to(BF)
+        lda = K if a_t == 0 else M
+        ldb = K if b_t == 0 else N
+        av = A.view(nb, M, K) if a_t == 0 else A.view(nb, K, M).transpose(1, 2)
+        bv = B.view(nb, N, K).transpose(1, 2) if b_t == 0 else B.view(nb, K, N)
+        ref = av.float() @ bv.float()
+        dt = torch.float32 if out_f32 else BF
+        C = torch.full((nb * M * ldc,), 7.0, dtype=dt, device=cuda)
+        c0 = g4w_calls()
+        raw.gemm(raw.Operand(A.to(cuda), a_t, lda, M * K), raw.Operand(B.to(cuda), b_t, ldb, N * K),
+                 raw.Operand(C, 0, ldc, M * ldc), M, N, K, batch=(nb, 1))
+        torch.cuda.synchronize()
+        assert g4w_calls() - c0 == 1, f"{M}x{N}x{K} did not run gemm4w"
+        Cv = C.view(nb, M, ldc)
+        _close(Cv[:, :, :N], ref, 3e-2 * math.sqrt(K / 64), 2e-2, f"gemm4w {a_t}{b_t} {M}x{N}x{K} f32={out_f32}")
+        assert torch.all(Cv[:, :, N:].float().cpu() == 7.0), "wrote past N into the ldc padding"
+
+
+@pytest.mark.parametrize("a_t,b_t,M,N,K", [(0, 0, 1024, 1536, 16384), (1, 1, 1024, 1536, 16384),
+                                           (1, 0, 512, 768, 131072), (0, 1, 512, 768, 131072)])
+def test_gemm_splitk_wgrad(cuda, a_t, b_t, M, N, K):
+    """few output tiles + long K + fp32 accumulate into C (beta = 1): K is split over the persistent grid into fp32
+    slabs and folded deterministically (gemm4w split-K + splitk_reduce_kernel on the "mfma" leg; K = 131072 is the
+    weight gradient of a 64 x 2048-token step, ks = 8)"""
+    torch.manual_seed(5)
+    c0 = g4w_calls()
+    A = (torch.randn(M * K) * 0.5).to(BF)
+    B = (torch.randn(N * K) * 0.5).to(BF)
+    lda = K if a_t == 0 else M
+    ldb = K if b_t == 0 else N
+    av = A.view(M, K) if a_t == 0 else A.view(K, M).t()
+    bv = B.view(N, K).t() if b_t == 0 else B.view(K, N)
+    ref = av.float() @ bv.float() + 2.0
+    Cf = torch.full((M * N,), 2.0, dtype=torch.float32, device=cuda)
+    raw.gemm(raw.Operand(A.to(cuda), a_t, lda), raw.Operand(B.to(cuda), b_t, ldb), raw.Operand(Cf, 0, N), M, N, K,
+             beta=1.0)
+    torch.cuda.synchronize()
+    _close(Cf.view(M, N), ref, 5e-2 * math.sqrt(K / 16384), 1e-2, f"splitk {a_t}{b_t} K{K}")
+    assert g4w_calls() - c0 == 1, "gemm4w did not run"
+
+
+@pytest.mark.parametrize("beta", [0.0, 1.0])
+def test_gemm4w_batched_splitk(cuda, beta):
+    """batched fp32 weight gradients with few tiles per batch (the per-head group linear: gw[h] = x[:, h]^T dy[:, h]):
+    gemm4w splits K into per-(batch, split) fp32 slabs and folds them per batch into the strided C"""
+    torch.manual_seed(8)
+    H, K, N, M = 4, 256, 512, 16384    # gw[h][K][N] over M tokens: 4 x 2 tiles per launch without the split
+    x = (torch.randn(M, H, K) * 0.5).to(BF)
+    dy = (torch.randn(M, H, N) * 0.5).to(BF)
+    ref = torch.einsum("mhk,mhn->hkn", x.float(), dy.float()) + (2.0 if beta else 0.0)
+    c0 = g4w_calls()
+    G = torch.full((H, K, N), 2.0, dtype=torch.float32, device=cuda)
+    raw.gemm(raw.Operand(x.to(cuda), 1, H * K, K), raw.Operand(dy.to(cuda), 1, H * N, N),
+             raw.Operand(G, 0, N, K * N), K, N, M, batch=(H, 1), beta=beta)
+    torch.cuda.synchronize()
+    assert g4w_calls() - c0 == 1
+    _close(G.cpu(), ref, 5e-2 * math.sqrt(M / 16384), 1e-2, f"batched split-K beta {beta}")
 
 
 @pytest.mark.parametrize("out_f32", [False, True])
 @pytest.mark.parametrize("a_t,b_t", [(0, 0), (0, 1), (1, 0), (1, 1)])
 def test_gemm_persistent(cuda, a_t, b_t, out_f32):
-    """(hipBLASLt off) the persistent phase kernel (whole 256x256 tiles, >= 512 of them): 6 tiles per batch x 90 batches = 540 tiles
-    (uneven per XCD, a partial last round per CU), 5 K-tiles; then tri = 3 (lower-triangle outputs) on square
-    tiles. Repeats are bitwise identical."""
+    """many whole 256x256 tiles: 6 tiles per batch x 90 batches = 540 tiles (uneven per XCD, a partial last round
+    per CU), 5 K-tiles; then tri = 3 (only the lower triangle of C receives the product) on square tiles (the
+    128x128 kernel; gemm4w takes tri 3 with a split contraction index only). Repeats are bitwise identical."""
     torch.manual_seed(7 + a_t + 2 * b_t + 4 * out_f32)
-    old = raw.lt_set(False)
-    try:
-        _persistent_cases(cuda, a_t, b_t, out_f32)
-    finally:
-        raw.lt_set(old)
-
-
-def _persistent_cases(cuda, a_t, b_t, out_f32):
     for M, N, K, nb, tri in ((768, 512, 320, 90, 0), (512, 512, 320, 140, 3)):
         A = (torch.randn(nb * M * K) * 0.5).to(BF)
         B = (torch.randn(nb * N * K) * 0.5).to(BF)
@@ -500,91 +507,36 @@ def _persistent_cases(cuda, a_t, b_t, out_f32):
         assert torch.equal(outs[0], outs[1]), "run-to-run difference"
 
 
-@pytest.mark.parametrize("a_t,b_t,M,N,K", [(0, 0, 1024, 1536, 16384), (1, 1, 1024, 1536, 16384),
-                                           (1, 0, 512, 768, 131072), (0, 1, 512, 768, 131072)])
-def test_gemm_splitk_wgrad(cuda, lt, a_t, b_t, M, N, K):
-    """few output tiles + long K + fp32 accumulate into C (beta = 1): K is split over the persistent grid into fp32
-    slabs and folded deterministically (gemm4w split-K + splitk_reduce_kernel on the "mfma" leg; K = 131072 is the
-    weight gradient of a 64 x 2048-token step, ks = 8)"""
-    torch.manual_seed(5)
-    c0 = g4w_calls()
-    A = (torch.randn(M * K) * 0.5).to(BF)
-    B = (torch.randn(N * K) * 0.5).to(BF)
-    lda = K if a_t == 0 else M
-    ldb = K if b_t == 0 else N
-    av = A.view(M, K) if a_t == 0 else A.view(K, M).t()
-    bv = B.view(N, K).t() if b_t == 0 else B.view(K, N)
-    ref = av.float() @ bv.float() + 2.0
-    Cf = torch.full((M * N,), 2.0, dtype=torch.float32, device=cuda)
-    raw.gemm(raw.Operand(A.to(cuda), a_t, lda), raw.Operand(B.to(cuda), b_t, ldb), raw.Operand(Cf, 0, N), M, N, K,
-             beta=1.0)
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("S,Bb", [(512, 8), (1024, 4)])
+def test_gemm4w_split_index_tri3_splitk(cuda, causal, S, Bb):
+    """the mixer weight-gradient form on gemm4w with few tiles: kin = F contraction read in place, tri 3 (causal)
+    lower-triangle tiles, fp32 accumulate into C (beta 1) through the split-K slabs and their masked fold; the upper
+    triangle keeps its old values"""
+    torch.manual_seed(S + Bb)
+    H, Fd = 2, 128
+    hf = H * Fd
+    a = (torch.randn(Bb, S, H, Fd) * 0.5).to(BF)
+    b = (torch.randn(Bb, S, H, Fd) * 0.5).to(BF)
+    c0v = torch.randn(H, S, S)
+    c = c0v.to(cuda).flatten().contiguous()
+    n0 = g4w_calls()
+    raw.gemm(raw.Operand(a.to(cuda).flatten(), 0, hf, 0, Fd), raw.Operand(b.to(cuda).flatten(), 0, hf, 0, Fd),
+             raw.Operand(c, 0, S, 0, S * S), S, S, Bb * Fd, batch=(1, H), beta=1.0, tri=3 if causal else 0,
+             kin=Fd, a_sk=S * hf, b_sk=S * hf)
     torch.cuda.synchronize()
-    _close(Cf.view(M, N), ref, 5e-2 * math.sqrt(K / 16384), 1e-2, f"splitk {a_t}{b_t} K{K}")
-    if lt == 0:
-        assert g4w_calls() - c0 == 1, "the MFMA leg did not run gemm4w"
-
-
-@pytest.mark.parametrize("beta", [0.0, 1.0])
-def test_gemm4w_batched_splitk(cuda, beta):
-    """batched fp32 weight gradients with few tiles per batch (the per-head group linear: gw[h] = x[:, h]^T dy[:, h]):
-    gemm4w splits K into per-(batch, split) fp32 slabs and folds them per batch into the strided C"""
-    torch.manual_seed(8)
-    H, K, N, M = 4, 256, 512, 16384    # gw[h][K][N] over M tokens: 4 x 2 tiles per launch without the split
-    x = (torch.randn(M, H, K) * 0.5).to(BF)
-    dy = (torch.randn(M, H, N) * 0.5).to(BF)
-    ref = torch.einsum("mhk,mhn->hkn", x.float(), dy.float()) + (2.0 if beta else 0.0)
-    old = raw.lt_set(0)
-    try:
-        c0 = g4w_calls()
-        G = torch.full((H, K, N), 2.0, dtype=torch.float32, device=cuda)
-        raw.gemm(raw.Operand(x.to(cuda), 1, H * K, K), raw.Operand(dy.to(cuda), 1, H * N, N),
-                 raw.Operand(G, 0, N, K * N), K, N, M, batch=(H, 1), beta=beta)
-        torch.cuda.synchronize()
-        assert g4w_calls() - c0 == 1
-    finally:
-        raw.lt_set(old)
-    _close(G.cpu(), ref, 5e-2 * math.sqrt(M / 16384), 1e-2, f"batched split-K beta {beta}")
-
-
-@pytest.mark.parametrize("a_t,b_t", [(0, 1), (1, 0), (0, 0)])
-@pytest.mark.parametrize("beta", [0.0, 1.0])
-def test_blaslt_splitk_wgrad(cuda, a_t, b_t, beta):
-    """hipBLASLt split-K weight gradient (K-slabs as one strided batch + deterministic fold) into a strided fp32 C
-    against the fp32 product; bitwise run-to-run"""
-    if not raw.lt_takes_f32():
-        pytest.skip("hipBLASLt does not take the fp32 products")
-    torch.manual_seed(6)
-    M, N, K, ldc = 512, 768, 32768, 1024
-    A = (torch.randn(M * K) * 0.5).to(BF)
-    B = (torch.randn(N * K) * 0.5).to(BF)
-    lda = K if a_t == 0 else M
-    ldb = K if b_t == 0 else N
-    av = A.view(M, K) if a_t == 0 else A.view(K, M).t()
-    bv = B.view(N, K).t() if b_t == 0 else B.view(K, N)
-    C0 = torch.randn(M, ldc)
-    ref = av.float() @ bv.float() + beta * C0[:, :N]
-    Ag, Bg = A.to(cuda), B.to(cuda)
-    old = raw.lt_splitk_set(True)
-    n0 = L.lib().obst_blaslt_splitk_calls()
-    try:
-        outs = []
-        for _ in range(2):
-            Cf = C0.to(cuda).reshape(-1).contiguous()
-            raw.gemm(raw.Operand(Ag, a_t, lda), raw.Operand(Bg, b_t, ldb), raw.Operand(Cf, 0, ldc), M, N, K,
-                     beta=beta)
-            outs.append(Cf.view(M, ldc))
-        torch.cuda.synchronize()
-    finally:
-        raw.lt_splitk_set(old)
-    assert L.lib().obst_blaslt_splitk_calls() == n0 + 2, "the split-K path did not run"
-    _close(outs[0][:, :N], ref, 5e-2, 1e-2, f"lt splitk {a_t}{b_t}")
-    assert torch.equal(outs[0], outs[1])
-    assert torch.equal(outs[0][:, N:].cpu(), C0[:, N:]), "columns past N must stay untouched"
+    assert g4w_calls() - n0 == 1
+    prod = torch.einsum("bshf,bthf->hst", a.float(), b.float())
+    if causal:
+        prod = prod * torch.ones(S, S).tril()
+    _close(c.view(H, S, S).cpu(), prod + c0v, 3e-2, 2e-2, f"kin tri3 splitk S={S} causal={causal}")
 
 
 @pytest.mark.parametrize("causal", [True, False])
 def test_token_mixer_big_tiles(cuda, causal):
-    """K03 through the 256x256 phase kernel (>= 512 tiles) incl. the triangular tile skipping (tri = 1/2/3)"""
+    """K03 on gemm4w: y = tril(W) x and dx = tril(W)^T dy with per-tile K ranges (tri 1 / 2), and the weight
+    gradient dW = dy . x^T over the split contraction index (kin = F, read in place from [B, S, H, F]) into the
+    lower-triangle tiles only (tri 3) for the causal mixer"""
     from homebrewnlp_mtf_amd.ops import functional as F
     torch.manual_seed(3)
     B, S, H, Fd = 16, 1024, 8, 256
@@ -596,8 +548,8 @@ def test_token_mixer_big_tiles(cuda, causal):
     y = F.token_mixer(xg, wg, causal)
     y.backward(dy.to(cuda))
     torch.cuda.synchronize()
-    # y = tril(W) x and dx = tril(W)^T dy on gemm4w (per-tile K ranges); dW (split contraction index) elsewhere
-    assert g4w_calls() - c0 == 2
+    # y, dx and dW: all three products on gemm4w (no phase kernel left)
+    assert g4w_calls() - c0 == 3
     xf, wf = x.float().requires_grad_(True), w.float().requires_grad_(True)
     wm = torch.tril(wf) if causal else wf
     ref = torch.einsum("hst,bthf->bshf", wm, xf)

@@ -28,17 +28,8 @@ def _pair(cfg, cuda):
     return m_cpu, m_gpu
 
 
-@pytest.fixture(params=[0, 1], ids=["mfma", "hipblaslt"])
-def lt(request, cuda):
-    """plain GEMMs on the hand-written MFMA kernels (0) or on hipBLASLt (1)"""
-    from homebrewnlp_mtf_amd.ops import raw
-    old = raw.lt_set(request.param)
-    yield request.param
-    raw.lt_set(old)
-
-
 @pytest.mark.parametrize("variant", ["gpt", "gpt_d96", "revnet", "mixer"])
-def test_model_forward_backward(cuda, lt, variant):
+def test_model_forward_backward(cuda, variant):
     cfg = dict(GPT)
     if variant == "gpt_d96":     # GPT-Neo 20B-scale head dim
         cfg.update(features_per_head=96)

@@ -164,19 +164,13 @@ def test_training_is_bitwise_deterministic(cuda, blocks, optimizer):
     assert torch.equal(runs[0].store.grad, runs[1].store.grad)
 
 
-@pytest.mark.parametrize("name,lt", [("gpt_neo_1.3b", 0), ("gpt_neo_1.3b", 1), ("gpt_neo_2.7b", 0),
-                                     ("gpt_neo_20b_scale", 0), ("ctx32_mixer", 0), ("big32_mixer", 0),
-                                     ("group32_mixer", 0)])
-def test_shipped_config_trains_on_gpu(cuda, name, lt):
+@pytest.mark.parametrize("name", ["gpt_neo_1.3b", "gpt_neo_2.7b", "gpt_neo_20b_scale", "ctx32_mixer", "big32_mixer",
+                                  "group32_mixer"])
+def test_shipped_config_trains_on_gpu(cuda, name):
     """every shipped language config runs its real layer shapes (head dims 96 / 128, mixer widths) through the HIP
-    kernels: two layers, one sequence, one data-parallel rank; lt = 0: every GEMM on the hand-written kernels"""
+    kernels: two layers, one sequence, one data-parallel rank"""
     from homebrewnlp_mtf_amd.config import load_config
-    from homebrewnlp_mtf_amd.ops import raw
-    old_lt = raw.lt_set(lt)
-    try:
-        _shipped_config_trains(cuda, name, load_config)
-    finally:
-        raw.lt_set(old_lt)
+    _shipped_config_trains(cuda, name, load_config)
 
 
 def _shipped_config_trains(cuda, name, load_config):

@@ -3,7 +3,8 @@
 // path against hipBLASLt and a small-shape fp32 CPU check of every layout.
 //
 //   build: hipcc -O2 --offload-arch=gfx950 tools/gemm_bench.cpp -o build/gemm_bench \
-//            -Lhomebrewnlp_mtf_amd -l:_kernels.so -Wl,-rpath,'$ORIGIN/../homebrewnlp_mtf_amd'
+//            -Lhomebrewnlp_mtf_amd -l:_kernels.so -Wl,-rpath,'$ORIGIN/../homebrewnlp_mtf_amd' \
+//            tools/lab/blaslt.cpp -lhipblaslt
 //   run:   build/gemm_bench [rounds] [reps] [shape-filter substring]
 #include <hip/hip_runtime.h>
 #include <math.h>
@@ -19,7 +20,7 @@
 
 extern "C" int obst_gemm(const ObstGemmDesc* d, hipStream_t stream);
 extern "C" int obst_blaslt_set(int on);
-extern "C" int obst_gemm4w_set(int on);
+int obst_blaslt_gemm(const ObstGemmDesc* d, hipStream_t stream);   // tools/lab/blaslt.cpp (linked in)
 extern "C" long long obst_gemm4w_calls();
 extern "C" void obst_gemm4w_stamps(unsigned long long* dev);
 
@@ -60,10 +61,9 @@ struct Shape {
   const char* what;
 };
 
-// mode: 0 hipBLASLt, 1 phase kernels (4w off), 2 gemm4w
+// mode: 0 hipBLASLt (tools/lab/blaslt.cpp), else the framework's dispatch (gemm4w)
 static int run(const Shape& s, const void* A, const void* B, void* C, int mode, hipStream_t st) {
   obst_blaslt_set(mode == 0);
-  obst_gemm4w_set(mode == 2);
   ObstGemmDesc d;
   memset(&d, 0, sizeof(d));
   d.A = A; d.B = B; d.C = C;
@@ -73,7 +73,7 @@ static int run(const Shape& s, const void* A, const void* B, void* C, int mode, 
   d.M = s.M; d.N = s.N; d.K = s.K; d.batch1 = d.batch2 = 1;
   d.a_t = s.a_t; d.b_t = s.b_t; d.out_f32 = s.f32;
   d.alpha = 1.f; d.beta = 0.f;
-  return obst_gemm(&d, st);
+  return mode == 0 ? obst_blaslt_gemm(&d, st) : obst_gemm(&d, st);
 }
 
 static void host_check(hipStream_t st, int K) {

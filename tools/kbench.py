@@ -3,8 +3,8 @@
 
   python tools/kbench.py [gemm|attn|attn_map|norm|ew|all] [--reps N] [--tokens T] [--check profiles/kbench_floor.json]
 
-* gemm      -- every plain product of the step (fwd / dgrad / fp32 wgrad / logits) on hipBLASLt and on the
-               hand-written gemm4w kernel, interleaved in one process (cdna guide §5.4 rule 24): TF/s and ratio.
+* gemm      -- every plain product of the step (fwd / dgrad / fp32 wgrad / logits) on the hand-written gemm4w
+               kernel: TF/s (the hipBLASLt A/B lives in tools/lab/g4w_sched.cpp; no library GEMM is linked).
                The per-tile clock breakdown of gemm4w lives in the C++ harness (tools/gemm_bench.cpp, STAMPS=1).
 * attn      -- flash attention fwd / bwd (B, S 2048, H 16, D 128, causal, interleaved k|q|v as in the step):
                effective causal PF/s (fwd 2 units, bwd 5 units of B*H*S*S/2*D*2 FLOPs).
@@ -128,10 +128,10 @@ def line_key(row: dict) -> str:
 
 def section_of(key: str) -> str:
     """the kbench section (command-line `what`) that emits a floor key"""
+    if key.startswith(("mixer", "gemm mixer")):
+        return "mixer"
     if key.startswith("gemm"):
         return "gemm"
-    if key.startswith("mixer"):
-        return "mixer"
     if key.startswith("attention_map"):
         return "attn_map"
     if key.startswith("attention"):
@@ -182,47 +182,38 @@ def bench_gemm(T: int, reps: int):
         B = (torch.randn(N * K, device=dev) * 0.5).to(BF)
         C = torch.zeros(M * N, device=dev, dtype=torch.float32 if f32 else BF)
         ops = (raw.Operand(A, at, K if at == 0 else M), raw.Operand(B, bt, K if bt == 0 else N), raw.Operand(C, 0, N))
-        def with_lt(on):
-            def run():
-                old = raw.lt_set(on)
-                raw.gemm(*ops, M, N, K)
-                raw.lt_set(old)
-            return run
-        t = dict(zip((1, 0), timed_many([with_lt(1), with_lt(0)], reps)))   # interleaved call by call
+        us = timed(lambda: raw.gemm(*ops, M, N, K), reps)
         fl = 2.0 * M * N * K
-        emit(kernel="gemm", shape=name, M=M, N=N, K=K, a_t=at, b_t=bt, out_f32=f32,
-             us_hipblaslt=round(t[1], 1), us_gemm4w=round(t[0], 1), tflops_hipblaslt=round(fl / t[1] / 1e6, 1),
-             tflops_gemm4w=round(fl / t[0] / 1e6, 1), gemm4w_over_hipblaslt=round(t[1] / t[0], 3))
+        emit(kernel="gemm", shape=name, M=M, N=N, K=K, a_t=at, b_t=bt, out_f32=f32, us_gemm4w=round(us, 1),
+             tflops_gemm4w=round(fl / us / 1e6, 1))
         del A, B, C
 
 
 def bench_mixer(reps: int):
-    """the learned token mixer's GEMMs (K03, ctx32_mixer: 32 x 2048 tokens, 8 heads x 256): y = tril(W) x
-    (tri 1) and dx = tril(W)^T dy (tri 2) on gemm4w against the persistent phase kernel (OBST_GEMM_4W=0 path);
-    effective TF/s count only the causal half"""
-    import ctypes
-    from homebrewnlp_mtf_amd.ops import _lib as L
+    """the learned token mixer's GEMMs (K03, ctx32_mixer: 32 x 2048 tokens, 8 heads x 256) on gemm4w: y = tril(W) x
+    (tri 1), dx = tril(W)^T dy (tri 2) and the weight gradient dW = dy . x^T over the split (batch, feature)
+    contraction index into the lower-triangle tiles (kin = F, tri 3); effective TF/s count only the causal half"""
     B, S, H, Fd = 32, 2048, 8, 256
     dev = torch.device("cuda")
     x = (torch.randn(B * S * H * Fd, device=dev) * 0.5).to(BF)
     w = torch.tril((torch.randn(H, S, S, device=dev) * 0.05)).to(BF).reshape(-1)
     y = torch.empty_like(x)
+    gw = torch.zeros(H * S * S, device=dev)
     hf = H * Fd
     fl = B * H * S * S * Fd   # 2 * S * S / 2 per (batch, head, feature)
     for name, a_t, tri in (("mixer y=tril(W)x", 0, 1), ("mixer dx=tril(W)^T dy", 1, 2)):
         def run():
             raw.gemm(raw.Operand(w, a_t, S, 0, S * S), raw.Operand(x, 1, hf, S * hf, Fd),
                      raw.Operand(y, 0, hf, S * hf, Fd), S, Fd, S, batch=(B, H), tri=tri)
-        def with_g4w(on):
-            def go():
-                old = L.lib().obst_gemm4w_set(on)
-                run()
-                L.lib().obst_gemm4w_set(old)
-            return go
-        t = dict(zip((0, 1), timed_many([with_g4w(0), with_g4w(1)], reps)))
-        emit(kernel="gemm", shape=name, us_phase=round(t[0], 1), us_gemm4w=round(t[1], 1),
-             tflops_phase=round(fl / t[0] / 1e6, 1), tflops_gemm4w=round(fl / t[1] / 1e6, 1),
-             gemm4w_over_phase=round(t[0] / t[1], 3))
+        us = timed(run, reps)
+        emit(kernel="gemm", shape=name, us_gemm4w=round(us, 1), tflops_gemm4w=round(fl / us / 1e6, 1))
+
+    def wgrad():
+        raw.gemm(raw.Operand(y, 0, hf, 0, Fd), raw.Operand(x, 0, hf, 0, Fd), raw.Operand(gw, 0, S, 0, S * S),
+                 S, S, B * Fd, batch=(1, H), beta=1.0, tri=3, kin=Fd, a_sk=S * hf, b_sk=S * hf)
+    us = timed(wgrad, reps)
+    emit(kernel="gemm", shape="mixer dW=dy.x^T (kin, tri 3)", us_gemm4w=round(us, 1),
+         tflops_gemm4w=round(fl / us / 1e6, 1))
 
 
 def _qkv(B, S, H, D, dev):

@@ -3,7 +3,8 @@
 // library's on a strided sample of rows.
 //
 //   build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -Icsrc/kernels tools/lab/g4w_sched.cpp -o bin/g4w_sched \
-//            -Lhomebrewnlp_mtf_amd -l:_kernels.so -Wl,-rpath,'$ORIGIN/../homebrewnlp_mtf_amd'
+//            -Lhomebrewnlp_mtf_amd -l:_kernels.so -Wl,-rpath,'$ORIGIN/../homebrewnlp_mtf_amd' \
+//            tools/lab/blaslt.cpp -lhipblaslt
 //   run:   bin/g4w_sched [rounds] [reps] [shape filter]
 #include "gemm4w.h"
 
@@ -20,6 +21,7 @@
 
 extern "C" int obst_gemm(const ObstGemmDesc* d, hipStream_t stream);
 extern "C" int obst_blaslt_set(int on);
+int obst_blaslt_gemm(const ObstGemmDesc* d, hipStream_t stream);   // tools/lab/blaslt.cpp (linked in)
 extern "C" int obst_gemm4w_set(int on);
 
 #define CK(x)                                                                    \
@@ -126,7 +128,7 @@ static int run_lt(const Shape& s, const void* A, const void* B, void* C, hipStre
   d.M = s.M; d.N = s.N; d.K = s.K; d.batch1 = d.batch2 = 1;
   d.a_t = s.a_t; d.b_t = s.b_t; d.out_f32 = s.f32;
   d.alpha = 1.f; d.beta = 0.f;
-  return obst_gemm(&d, st);
+  return obst_blaslt_gemm(&d, st);
 }
 
 int main(int argc, char** argv) {

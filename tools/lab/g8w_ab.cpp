@@ -3,7 +3,8 @@
 // checked against the library's on a strided sample of rows.
 //
 //   build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -Icsrc/kernels -Itools/lab tools/lab/g8w_ab.cpp -o bin/g8w_ab \
-//            -Lhomebrewnlp_mtf_amd -l:_kernels.so -Wl,-rpath,'$ORIGIN/../homebrewnlp_mtf_amd'
+//            -Lhomebrewnlp_mtf_amd -l:_kernels.so -Wl,-rpath,'$ORIGIN/../homebrewnlp_mtf_amd' \
+//            tools/lab/blaslt.cpp -lhipblaslt
 //   run:   bin/g8w_ab [rounds] [reps] [shape filter]      (G8_ONLY=0,2: variants)
 #include "gemm8w.h"
 
@@ -20,6 +21,7 @@
 
 extern "C" int obst_gemm(const ObstGemmDesc* d, hipStream_t stream);
 extern "C" int obst_blaslt_set(int on);
+int obst_blaslt_gemm(const ObstGemmDesc* d, hipStream_t stream);   // tools/lab/blaslt.cpp (linked in)
 
 #define CK(x)                                                                    \
   do {                                                                           \
@@ -128,7 +130,7 @@ static int run_lt(const Shape& s, const void* A, const void* B, void* C, hipStre
   d.M = s.M; d.N = s.N; d.K = s.K; d.batch1 = d.batch2 = 1;
   d.a_t = s.a_t; d.b_t = s.b_t; d.out_f32 = s.f32;
   d.alpha = 1.f; d.beta = 0.f;
-  return obst_gemm(&d, st);
+  return obst_blaslt_gemm(&d, st);
 }
 
 int main(int argc, char** argv) {
