@@ -6,9 +6,10 @@ same code with ``--hip-graphs-dist 1``):
      the whole training step captured by ``Trainer`` (``use_hip_graphs`` + ``hip_graphs_distributed``, GradSync forced
      on at world 1) give the eager Trainer's losses and weights.
 
-  python -m torch.distributed.run --nproc-per-node 1 --master-addr 127.0.0.1 tools/graph_capture_probe.py
+  python -m torch.distributed.run --nproc-per-node 1 --master-addr 127.0.0.1 tools/graph_capture_probe.py [--part P]
 
-Prints one JSON line with the checks; exit status 1 when one fails.
+--part: all_reduce | all_to_all | all_gather | side_stream | trainer | all (default). Prints one JSON line per part as
+it completes (a crash inside a capture still leaves the earlier lines); exit status 1 when one fails.
 """
 from __future__ import annotations
 
@@ -27,29 +28,96 @@ def main():
     from homebrewnlp_mtf_amd.parallel import state as pstate
     from homebrewnlp_mtf_amd.run.trainer import Trainer
 
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--part", default="all")
+    part = ap.parse_args().part
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     dist.init_process_group("nccl", device_id=dev)
-    out = {}
-    try:
-        _capture_all_reduce(dev, out)
-    except Exception as e:   # report, then continue with the trainer check
-        import traceback
-        out["captured_all_reduce"] = False
-        out["error_all_reduce"] = traceback.format_exc()[-1500:]
-    try:
-        _capture_trainer(dev, out, ModelParameter, pstate, Trainer)
-    except Exception as e:
-        import traceback
-        out["graphs_captured"] = 0
-        out["error_trainer"] = traceback.format_exc()[-2500:]
-    ok = (out.get("captured_all_reduce") and out.get("graphs_captured") == 2 and out.get("max_loss_diff", 1) < 1e-3
-          and out.get("max_weight_diff", 1) < 1e-4 and "dp_all_to_all" in out.get("graph_comm", {}))
-    out["ok"] = bool(ok)
-    print(json.dumps(out), flush=True)
+    ok_all = True
+    for name, fn in (("all_reduce", _capture_all_reduce), ("all_to_all", _capture_all_to_all),
+                     ("all_gather", _capture_all_gather), ("side_stream", _capture_side_stream),
+                     ("trainer", lambda d, o: _capture_trainer(d, o, ModelParameter, pstate, Trainer))):
+        if part not in ("all", name):
+            continue
+        out = {"part": name}
+        try:
+            fn(dev, out)
+        except Exception:
+            import traceback
+            out["error"] = traceback.format_exc()[-2500:]
+        if name == "trainer":
+            out["ok"] = bool("error" not in out and out.get("graphs_captured") == 2
+                             and out.get("max_loss_diff", 1) < 1e-3 and out.get("max_weight_diff", 1) < 1e-4
+                             and "dp_all_to_all" in out.get("graph_comm", {}))
+        else:
+            out["ok"] = bool("error" not in out and out.get("equal"))
+        ok_all &= out["ok"]
+        print(json.dumps(out), flush=True)
     dist.destroy_process_group()
-    sys.exit(0 if ok else 1)
+    sys.exit(0 if ok_all else 1)
+
+
+def _capture(dev, fn):
+    """warm fn up eagerly on a side stream, capture it, replay once"""
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        fn()
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        fn()
+    torch.cuda.synchronize()
+    g.replay()
+    torch.cuda.synchronize()
+    return g
+
+
+def _capture_all_to_all(dev, out):
+    x = torch.arange(1 << 20, dtype=torch.float32, device=dev).to(torch.bfloat16)
+    y = torch.empty_like(x)
+    g = _capture(dev, lambda: dist.all_to_all_single(y, x, async_op=True).wait())
+    y.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    out["equal"] = bool(torch.equal(y, x))
+
+
+def _capture_all_gather(dev, out):
+    x = torch.arange(1 << 20, dtype=torch.float32, device=dev).to(torch.bfloat16)
+    y = torch.empty_like(x)
+    g = _capture(dev, lambda: dist.all_gather_into_tensor(y, x, async_op=True).wait())
+    y.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    out["equal"] = bool(torch.equal(y, x))
+
+
+def _capture_side_stream(dev, out):
+    """the bf16 wire's shape: cast on the capture stream, the collectives + fp32 sum on a side stream, join"""
+    x = torch.randn(1 << 20, device=dev)
+    send = torch.empty(1 << 20, dtype=torch.bfloat16, device=dev)
+    recv = torch.empty_like(send)
+    side = torch.cuda.Stream()
+
+    def step():
+        send.copy_(x)
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            dist.all_to_all_single(recv, send, async_op=True).wait()
+            send.copy_(recv.float() * 2)
+            w = dist.all_gather_into_tensor(recv, send, async_op=True)
+        w.wait()
+        torch.cuda.current_stream().wait_stream(side)
+    g = _capture(dev, step)
+    recv.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    out["equal"] = bool(torch.equal(recv, (x.to(torch.bfloat16).float() * 2).to(torch.bfloat16)))
 
 
 def _capture_all_reduce(dev, out):
@@ -73,7 +141,7 @@ def _capture_all_reduce(dev, out):
     y.zero_()
     g.replay()
     torch.cuda.synchronize()
-    out["captured_all_reduce"] = bool(torch.equal(z, eager + 1.0))
+    out["equal"] = bool(torch.equal(z, eager + 1.0))
 
 
 def _capture_trainer(dev, out, ModelParameter, pstate, Trainer):

@@ -79,8 +79,8 @@ def calibrate(reps: int = 20):
     """same-process calibration: bf16 MFMA loop TF/s (csrc/kernels/calib.hip) and a 512 MiB device copy GB/s"""
     from homebrewnlp_mtf_amd.ops import _lib as L
     dev = torch.device("cuda")
-    sink = torch.empty(256 * 256, device=dev)
-    iters = 4096
+    sink = torch.empty(2048 * 256, device=dev)
+    iters = 1024
     fl = float(L.lib().obst_calib_mfma_flops(iters))
     us = timed(lambda: L.check(L.lib().obst_calib_mfma(sink.data_ptr(), iters, L.stream_ptr()), "calib"), reps)
     src = torch.randn(128 * 2 ** 20, device=dev)
