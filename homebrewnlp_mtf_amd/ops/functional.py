@@ -605,7 +605,13 @@ class _TokenMixer(torch.autograd.Function):
         # dW[h] = dy_h · x_hᵀ over (batch, features), both read in place from [B, S, H, F]: the contraction index
         # (b, f) is split (kin = F contiguous features, outer stride S*H*F), so no [H][S][B*F] copies are made
         kk = B * Fd
-        if raw.on_gpu(dy) and Fd % 64 == 0 and S % 8 == 0:
+        if raw.on_gpu(dy) and B == 1:
+            # one sequence: the contraction runs over the F contiguous features of each row -- plain row-strided
+            # operands, no split index
+            raw.gemm(raw.Operand(dy, 0, hf, 0, Fd), raw.Operand(xc, 0, hf, 0, Fd), raw.Operand(g, 0, S, 0, S * S),
+                     S, S, Fd, batch=(1, H), beta=1.0, tri=3 if ctx.causal else 0)
+        elif raw.on_gpu(dy) and Fd % 64 == 0 and S % 8 == 0 and (B % 2 == 0 or not ctx.causal):
+            # (the causal product runs as >= 2 split-K slabs that start on whole (b, f) blocks: B even)
             raw.gemm(raw.Operand(dy, 0, hf, 0, Fd), raw.Operand(xc, 0, hf, 0, Fd), raw.Operand(g, 0, S, 0, S * S),
                      S, S, kk, batch=(1, H), beta=1.0, tri=3 if ctx.causal else 0, kin=Fd, a_sk=S * hf, b_sk=S * hf)
         else:

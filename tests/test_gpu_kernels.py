@@ -532,14 +532,17 @@ def test_gemm4w_split_index_tri3_splitk(cuda, causal, S, Bb):
     _close(c.view(H, S, S).cpu(), prod + c0v, 3e-2, 2e-2, f"kin tri3 splitk S={S} causal={causal}")
 
 
+@pytest.mark.parametrize("B,S", [(16, 1024), (1, 512), (3, 512)])
 @pytest.mark.parametrize("causal", [True, False])
-def test_token_mixer_big_tiles(cuda, causal):
+def test_token_mixer_big_tiles(cuda, causal, B, S):
     """K03 on gemm4w: y = tril(W) x and dx = tril(W)^T dy with per-tile K ranges (tri 1 / 2), and the weight
     gradient dW = dy . x^T over the split contraction index (kin = F, read in place from [B, S, H, F]) into the
-    lower-triangle tiles only (tri 3) for the causal mixer"""
+    lower-triangle tiles only (tri 3) for the causal mixer. One sequence: the weight gradient is a plain row-strided
+    product (no split index); an odd batch of the causal mixer cannot start its split-K slabs on whole (b, f) blocks
+    and takes the copied [H][S][B*F] operands -- both causal forms then run tri 3 on the 128x128 kernel"""
     from homebrewnlp_mtf_amd.ops import functional as F
     torch.manual_seed(3)
-    B, S, H, Fd = 16, 1024, 8, 256
+    H, Fd = 8, 256
     x = (torch.randn(B, S, H, Fd) * 0.5).to(BF)
     w = (torch.randn(H, S, S) * 0.05).to(BF)
     dy = (torch.randn(B, S, H, Fd) * 0.5).to(BF)
@@ -549,7 +552,7 @@ def test_token_mixer_big_tiles(cuda, causal):
     y.backward(dy.to(cuda))
     torch.cuda.synchronize()
     # y, dx and dW: all three products on gemm4w (no phase kernel left)
-    assert g4w_calls() - c0 == 3
+    assert g4w_calls() - c0 == (2 if causal and B % 2 else 3)
     xf, wf = x.float().requires_grad_(True), w.float().requires_grad_(True)
     wm = torch.tril(wf) if causal else wf
     ref = torch.einsum("hst,bthf->bshf", wm, xf)
