@@ -15,6 +15,7 @@ all: $(PKG)/_kernels.so $(if $(RSRC),$(PKG)/_runtime.so,)
 # attention: no SLP vectorisation -- adjacent f32 adds / multiplies packed into v_pk_*_f32 cost more issue cycles
 # than two scalar ops beside MFMAs (MI355X_MICROARCH.md, 'price of one filler beside MFMAs')
 build/kernels/attention.o: HIPFLAGS += -fno-slp-vectorize
+build/kernels/attn_fwd64.o: HIPFLAGS += -fno-slp-vectorize
 
 build/kernels/%.o: csrc/kernels/%.hip $(wildcard csrc/kernels/*.h)
 	@mkdir -p build/kernels
