@@ -33,11 +33,21 @@ namespace {
 #ifndef FWD64_KPF
 #define FWD64_KPF 2   // K fragments read this many k-steps ahead of their MFMA
 #endif
+#ifndef FWD64_NS
+#define FWD64_NS 4    // LDS ring slots of 64-key K/V tiles (32 KiB each): NS - 3 tiles in flight past the next one
+#endif
 #ifndef FWD64_VPF
 #define FWD64_VPF 2   // Vᵀ fragments read this many MFMAs ahead
 #endif
 
 #define FENCE() __builtin_amdgcn_sched_barrier(0)
+
+// timing-only ablations (wrong results): 1 no exp, 2 no max/sum, 4 no per-step barrier, 8 no fences, 16 no K/V
+// staging after the prologue, 32 fragments read from LDS once per phase (the MFMAs reuse them), 64 per-block cycle
+// stamps (prologue, steps, epilogue, step count) written over LSE[4 * block ..]
+#ifndef FWD64_DBG
+#define FWD64_DBG 0
+#endif
 
 // Oᵀ tile += Vᵀ·P with the accumulator pinned in AGPRs (NOP: 2 wait states for a P packed just before)
 template <bool NOP = false>
@@ -80,8 +90,9 @@ __device__ __forceinline__ void f64_qk(const char* sK, const bf16x8_t (&qf)[8], 
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
       if (QK) {
-        if (ks + PF < 8)
+        if (ks + PF < 8 && !(FWD64_DBG & 32))
           kf[(ks + PF) % (PF + 1)][kt] = *reinterpret_cast<const bf16x8_t*>(sK + fo.k[ks + PF] + kt * 32 * 256);
+        if ((FWD64_DBG & 32) && ks >= PF) kf[ks % (PF + 1)][kt] = kf[kt % PF][kt];
         if (ks == 0) mfma_s<true>(sn[kt], kf[0][kt], qf[0]);
         else mfma_s<false>(sn[kt], kf[ks % (PF + 1)][kt], qf[ks]);
       }
@@ -89,9 +100,10 @@ __device__ __forceinline__ void f64_qk(const char* sK, const bf16x8_t (&qf)[8], 
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
           const int e = ks * 4 + kt * 2 + i;
-          se[e >> 4][e & 15] = fexp2(__builtin_fmaf(se[e >> 4][e & 15], c2, nm));
+          if (FWD64_DBG & 1) se[e >> 4][e & 15] = __builtin_fmaf(se[e >> 4][e & 15], c2, nm);
+          else se[e >> 4][e & 15] = fexp2(__builtin_fmaf(se[e >> 4][e & 15], c2, nm));
         }
-      if (QK) FENCE();   // source order = issue order (the asm MFMAs' hazards are kept by that order)
+      if (QK && !(FWD64_DBG & 8)) FENCE();   // source order = issue order (the asm MFMAs' hazards are kept by that order)
     }
   }
 }
@@ -127,15 +139,16 @@ __device__ __forceinline__ void f64_pv(const char* sV, const f32x16_t (&p)[2], f
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     if (PV) {
-      if (i + PF < 16) vf[(i + PF) % (PF + 1)] = vread(i + PF);
+      if (i + PF < 16 && !(FWD64_DBG & 32)) vf[(i + PF) % (PF + 1)] = vread(i + PF);
+      if ((FWD64_DBG & 32) && i >= PF) vf[i % (PF + 1)] = vf[i % PF];
       if (i == 0) mfma_o<true>(o[0], vf[0], __builtin_bit_cast(bf16x8_t, pk[0]));
       else mfma_o(o[i & 3], vf[i % (PF + 1)], __builtin_bit_cast(bf16x8_t, pk[i >> 2]));
       const int g = (i >> 2) + 1;   // the next 8-key group: packed beside this group's MFMAs 0 and 1
       if (g < 4 && (i & 3) < 2) pack_half(p[g >> 1], g & 1, pk[g], i & 3);
-      rs += p[i >> 3][2 * (i & 7)] + p[i >> 3][2 * (i & 7) + 1];
+      if (!(FWD64_DBG & 2)) rs += p[i >> 3][2 * (i & 7)] + p[i >> 3][2 * (i & 7) + 1];
     }
-    if (MX) mx = max3f(mx, sm[i >> 3][2 * (i & 7)], sm[i >> 3][2 * (i & 7) + 1]);
-    if (PV) FENCE();
+    if (MX && !(FWD64_DBG & 2)) mx = max3f(mx, sm[i >> 3][2 * (i & 7)], sm[i >> 3][2 * (i & 7) + 1]);
+    if (PV && !(FWD64_DBG & 8)) FENCE();
   }
 }
 
@@ -180,10 +193,14 @@ __device__ __forceinline__ void f64_rescale(float mx, float& m, float& l, f32x16
 }
 
 __global__ __launch_bounds__(256, 1) void attn_fwd64_kernel(AttnArgs a) {
-  constexpr int D = 128, KT = 64, NS = 4, NW = 4, NP = 4, QB = 256;
+  constexpr int D = 128, KT = 64, NS = FWD64_NS, NW = 4, NP = 4, QB = 256;
+  constexpr int AH = NS - 2;       // tiles staged ahead: step j stages tile j + AH into the slot of tile j - 2
+  static_assert(NS == 4 || NS == 5, "ring of 4 (128 KiB) or 5 (160 KiB) tiles");
   constexpr int TILE = KT * 256;   // bytes of one 64-key K (or V) tile
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, n = lane & 31;
+  const long long t0 = (FWD64_DBG & 64) ? (long long)__builtin_readcyclecounter() : 0;
+  long long t1 = 0, t2 = 0;
   const int nx = (a.S + QB - 1) / QB;
   int bx, bh;
   attn_block(nx, bx, bh);
@@ -226,6 +243,12 @@ __global__ __launch_bounds__(256, 1) void attn_fwd64_kernel(AttnArgs a) {
       stage_rows64_asm<NP, NW>(buf + TILE, Vb + (long long)k0 * a.ld, a.ld, a.S - k0, wu, lane);
     }
   };
+  // vmcnt wait leaving the y youngest tiles' DMA pieces (2 NP each) in flight (y < NS - 2)
+  auto wait_younger = [&](int y) {
+    if (NS >= 5 && y >= 2) vm_wait<(NS >= 5 ? 4 : 2) * NP>();
+    else if (y >= 1) vm_wait<2 * NP>();
+    else vm_wait<0>();
+  };
   stage(0);
   bf16x8_t qf[2][8];
   {
@@ -237,10 +260,11 @@ __global__ __launch_bounds__(256, 1) void attn_fwd64_kernel(AttnArgs a) {
       qf[1][ks] = *reinterpret_cast<const bf16x8_t*>(a.Q + base + r1 * a.ld + ks * 16 + 8 * h);
     }
   }
-  if (nkb > 1) stage(1);
-  // tile 0 and Q have landed once at most tile 1's 2 NP pieces are in flight
-  if (nkb > 1) vm_wait<2 * NP>();
-  else vm_wait<0>();
+#pragma unroll
+  for (int t = 1; t < AH; ++t)
+    if (t < nkb) stage(t);
+  // tile 0 and Q have landed once at most the younger tiles' 2 NP pieces each are in flight
+  wait_younger(min(AH, nkb) - 1);
   // the Q fragments move to AGPRs once (tied no-op asm: the copy is the compiler's) and stay there as MFMA sources
 #pragma unroll
   for (int qa = 0; qa < 2; ++qa)
@@ -255,19 +279,19 @@ __global__ __launch_bounds__(256, 1) void attn_fwd64_kernel(AttnArgs a) {
   for (int dt = 0; dt < 4; ++dt) o0[dt] = o1[dt] = f32x16_t{};
   float m0 = NEG_BIG, m1 = NEG_BIG, l0 = 0.f, l1 = 0.f;
   const float c2 = a.scale * LOG2E;
-  auto sync = [&](int j) {   // tile j + 1 (read by step j + 1) has landed; tile j + 2 may stay in flight
-    if (j + 2 < nkb) vm_wait<2 * NP>();
-    else vm_wait<0>();
-    __syncthreads();
+  if (FWD64_DBG & 64) t1 = (long long)__builtin_readcyclecounter();
+  auto sync = [&](int j) {   // tile j + 1 (read by step j + 1) has landed; tiles j + 2 .. j + AH may stay in flight
+    wait_younger(max(0, min(j + AH, nkb - 1) - (j + 1)));
+    if (!(FWD64_DBG & 4)) __syncthreads();
   };
-  // step j: stage tile j + 2 (into the slot of tile j - 2); A/B finish half 1 of tile j - 1 beside half 0 of tile
+  // step j: stage tile j + AH (into the slot of tile j - 2); A/B finish half 1 of tile j - 1 beside half 0 of tile
   // j, C/D run half 1 of tile j beside the rest of half 0; wait for tile j + 1, barrier. The steps of a wave: 0 (no
   // half 1 to finish), the steady ones [1, nu), the masked tile, the drain (last + 1) and idle ones -- each a loop or
   // branch of its own so the steady loop carries no role tests.
   int j = 0;
   if (last >= 0) {
     {   // step 0: scores of half 0 of tile 0, then C/D of tile 0
-      if (2 < nkb) stage(2);
+      if (AH < nkb) stage(AH);
       float mx0 = -INFINITY, mx1 = -INFINITY, rs0 = 0.f, rs1 = 0.f;
       f64_qk<true, false>(smem, qf[0], s0, s1, 0.f, c2, fo);
       o_settle();
@@ -287,7 +311,7 @@ __global__ __launch_bounds__(256, 1) void attn_fwd64_kernel(AttnArgs a) {
       ++j;
     }
     for (; j < nu; ++j) {   // steady steps: tile j unmasked, half 1 of tile j - 1 pending
-      if (j + 2 < nkb) stage(j + 2);
+      if (j + AH < nkb && !(FWD64_DBG & 16)) stage(j + AH);
       const char* sK = smem + (j % NS) * 2 * TILE;
       const char* sVp = smem + ((j + NS - 1) % NS) * 2 * TILE + TILE;
       float mx0 = -INFINITY, mx1 = -INFINITY, rs0 = 0.f, rs1 = 0.f;
@@ -302,7 +326,7 @@ __global__ __launch_bounds__(256, 1) void attn_fwd64_kernel(AttnArgs a) {
       sync(j);
     }
     if (j == last) {   // the masked tile (j >= 1 here)
-      if (j + 2 < nkb) stage(j + 2);
+      if (j + AH < nkb && !(FWD64_DBG & 16)) stage(j + AH);
       const char* sK = smem + (j % NS) * 2 * TILE;
       const char* sVp = smem + ((j + NS - 1) % NS) * 2 * TILE + TILE;
       float mx0 = -INFINITY, mx1 = -INFINITY, rs0 = 0.f, rs1 = 0.f;
@@ -320,7 +344,7 @@ __global__ __launch_bounds__(256, 1) void attn_fwd64_kernel(AttnArgs a) {
       ++j;
     }
     {   // drain: half 1 of the last tile
-      if (j + 2 < nkb) stage(j + 2);
+      if (j + AH < nkb && !(FWD64_DBG & 16)) stage(j + AH);
       const char* sVp = smem + ((j + NS - 1) % NS) * 2 * TILE + TILE;
       float rs1 = 0.f, mx0 = 0.f;
       f64_qk<false, true>(smem, qf[0], s0, s1, -m1, c2, fo);
@@ -331,10 +355,11 @@ __global__ __launch_bounds__(256, 1) void attn_fwd64_kernel(AttnArgs a) {
     }
   }
   for (; j <= nkb; ++j) {   // idle steps: the block's staging and barriers
-    if (j + 2 < nkb) stage(j + 2);
+    if (j + AH < nkb && !(FWD64_DBG & 16)) stage(j + AH);
     sync(j);
   }
   o_settle();
+  if (FWD64_DBG & 64) t2 = (long long)__builtin_readcyclecounter();
   // epilogue: O = Oᵀ/l through LDS as whole 256-byte rows (the ring is idle after the last barrier)
   const float lt0 = xh_sum(l0), lt1 = xh_sum(l1);
   const float inv[2] = {1.f / lt0, 1.f / lt1};
@@ -378,12 +403,20 @@ __global__ __launch_bounds__(256, 1) void attn_fwd64_kernel(AttnArgs a) {
       }
     }
   }
+  if ((FWD64_DBG & 64) && tid == 0) {
+    const long long t3 = (long long)__builtin_readcyclecounter();
+    float* st = a.LSE + 4 * (long long)blockIdx.x;
+    st[0] = (float)(t1 - t0);
+    st[1] = (float)(t2 - t1);
+    st[2] = (float)(t3 - t2);
+    st[3] = (float)(nkb + 1);
+  }
 }
 
 }  // namespace
 
 int attn_fwd64_launch(const void* args, hipStream_t st) {
   const AttnArgs& a = *static_cast<const AttnArgs*>(args);
-  hipLaunchKernelGGL(attn_fwd64_kernel, dim3((a.S + 255) / 256 * a.B * a.H), dim3(256), 4 * 2 * 64 * 256, st, a);
+  hipLaunchKernelGGL(attn_fwd64_kernel, dim3((a.S + 255) / 256 * a.B * a.H), dim3(256), FWD64_NS * 2 * 64 * 256, st, a);
   return (int)hipGetLastError();
 }

@@ -43,7 +43,10 @@ def main():
                                ld_o=H * D)
     res = {"fwd": [], "bwd": []}
     for rep in range(5):
+        only = os.environ.get("ONLY", "")
         for name, fn, units in (("fwd", fwd, 2), ("bwd", bwd, 5)):
+            if only and name != only:
+                continue
             fn()
             torch.cuda.synchronize()
             t = time.perf_counter()
@@ -54,6 +57,8 @@ def main():
             dt = (time.perf_counter() - t) / n
             res[name].append((dt * 1e3, units * unit / dt / 1e12))
     for name, v in res.items():
+        if not v:
+            continue
         v.sort()
         ms, tf = v[len(v) // 2]
         print(f"attn {name} B{B} S{S} H{H} D{D} causal={causal} kqv={int(kqv)} res={int(res_t is not None)}: {ms:.3f} ms  {tf:.0f} TFLOP/s (useful)")
