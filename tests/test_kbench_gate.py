@@ -18,7 +18,8 @@ def test_floor_file_covers_the_hot_kernels():
 def test_round3_norm_bwd_regression_fails_the_gate():
     with open(os.path.join(ROOT, "profiles", "kbench_floor.json")) as f:
         floors = json.load(f)["floors"]
-    ok = {"kernel": "norm_bwd", "rows": 131072, "F": 2048, "us": 349.2, "gbps": 4612.5}
+    gb = floors["norm_bwd"]["gbps"]   # a run at the floor itself
+    ok = {"kernel": "norm_bwd", "rows": 131072, "F": 2048, "us": round(3 * 131072 * 2048 * 2 / gb / 1e3, 1), "gbps": gb}
     # round 3's spill regression: 431 -> 833 us per call
     regressed = dict(ok, us=833.0, gbps=round(3 * 131072 * 2048 * 2 / 833.0 / 1e3, 1))
     assert kbench.check([ok], floors) == []
