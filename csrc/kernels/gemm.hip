@@ -164,6 +164,8 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(GemmArgs p) {
           for (int t = 0; t < 4; ++t) v[t] = act_fwd(p.act, v[t]);
         }
         *reinterpret_cast<float4*>(C) = make_float4(v[0], v[1], v[2], v[3]);
+        if (p.Zout)   // its bf16 copy
+          *reinterpret_cast<uint2*>(p.Zout + idx) = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
       } else {
         if (p.mode == 1) {
           if (p.R) {
@@ -325,7 +327,9 @@ OBST_API int obst_gemm(const ObstGemmDesc* d, hipStream_t stream) {
   const bool tri3_ok = d->tri != 3 || (d->kin && d->out_f32 && d->act == 0 && d->mode == 0 && !d->R && !d->Zout &&
                                        d->K % 128 == 0 && d->N % 4 == 0 && d->ldc % 4 == 0 &&
                                        (batch == 1 || (d->c_s1 % 4 == 0 && d->c_s2 % 4 == 0)));
-  if (d->K % 64 == 0 && tri3_ok && (d->a_t == 0 || d->M % 8 == 0) && (d->b_t == 0 || d->N % 8 == 0)) {
+  // an fp32 output's bf16 copy (Zout) comes from gemm4w's direct epilogue (no activation, no split-K)
+  const bool zcopy_ok = !(d->out_f32 && d->Zout) || (d->act == 0 && d->mode == 0 && d->a_t == 0);
+  if (d->K % 64 == 0 && tri3_ok && zcopy_ok && (d->a_t == 0 || d->M % 8 == 0) && (d->b_t == 0 || d->N % 8 == 0)) {
     // split-K for fp32 products with few output tiles (the weight gradients): the persistent kernel runs
     // ceil(tiles * ks / 256) rounds of K / ks each; a split costs a deterministic fold over ks fp32 slabs. Pick the
     // ks of least modelled time (1.25 us per 64-deep K-tile of a tile, ~5 TB/s for the fold), workspace <= 1 GiB.
@@ -335,7 +339,7 @@ OBST_API int obst_gemm(const ObstGemmDesc* d, hipStream_t stream) {
     // batched products too (the per-head group-linear weight gradients: few tiles per batch); C batch strides must
     // keep 16-byte alignment for the fold. The folds index float4s of rows (m = e / N, e < M * N / 4): N and ldc
     // must be multiples of 4 (the entry checks already require 8; restated here so the fold's own contract is local)
-    if ((big_tiles < 512 || d->tri == 3) && d->out_f32 && !d->R && !d->act && d->mode == 0 &&
+    if ((big_tiles < 512 || d->tri == 3) && d->out_f32 && !d->R && !d->Zout && !d->act && d->mode == 0 &&
         (d->tri == 0 || d->tri == 3) && d->N % 4 == 0 && d->ldc % 4 == 0 &&
         (batch == 1 || (d->c_s1 % 4 == 0 && d->c_s2 % 4 == 0))) {
       const double per_k = 1.25 / 64.0;   // us per K element of one tile

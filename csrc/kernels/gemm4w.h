@@ -445,7 +445,7 @@ constexpr int idx(const int (&a)[8], int q) {
 //   2 STAGGER: blocks start (slot & 7) / 8 of a tile apart (s_sleep), so the CUs' epilogue store bursts do not
 //     coincide on the fabric
 template <int A_T, int B_T, bool OUT_F32, bool PROF, int NWV = 4, int SCH = G4W_SCH, bool STG = (G4W_STG != 0),
-          int CPA = G4W_CPA, int CPB = G4W_CPB, int OPT = G4W_OPT, bool KINT = false>
+          int CPA = G4W_CPA, int CPB = G4W_CPB, int OPT = G4W_OPT, bool KINT = false, bool ZCP = false>
 __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   constexpr bool RELAX = (OPT & 1) != 0, STAGGER = (OPT & 2) != 0, LATE = (OPT & 4) != 0;
@@ -455,6 +455,8 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
   constexpr bool ROWS = (OPT & 64) != 0;   // plain products: C rows staged through LDS, row-contiguous stores
   // TLAY: row-layout accumulators for K-contiguous B (frag_b): row-contiguous epilogue stores without data movement
   constexpr bool TLAY = B_T == 0 && NWV == 4 && (OPT & 256) == 0 && !ROWS;
+  // fp32 output + its bf16 copy in Zout (the fused RevNet stream update): its own instantiation as well
+  constexpr bool ZCOPY = ZCP && OUT_F32 && !ROWS;
 
   static_assert(!(RELAX && LATE), "RELAX peels the first K-tile, LATE the last: not both");
   static_assert(SCH == 0 || NWV == 4, "the split schedule is laid out for one wave per SIMD");
@@ -757,7 +759,9 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
       // "illegal VGPR to SGPR copy")
       const bool gelu_direct = !OUT_F32 && (p.act == ACT_GELU || (TLAY && p.act == ACT_RELU)) && p.R == nullptr &&
                                ((p.mode == 0) || (p.mode == 1 && p.Zin != nullptr));
-      if (!(G4W_EXP & 16) && ((p.act == 0 && p.mode == 0 && p.Zout == nullptr) || gelu_direct)) {
+      // fp32 products with Zout (its bf16 copy, the fused RevNet stream update) take the direct path
+      const bool zcopy_direct = ZCOPY && p.act == 0 && p.mode == 0 && p.ksplit == 1;
+      if (!(G4W_EXP & 16) && ((p.act == 0 && p.mode == 0 && p.Zout == nullptr) || gelu_direct || zcopy_direct)) {
         // Direct epilogue (every plain product): each lane owns C[m][n..n+3] of 64 fragments and writes it with one
         // buffer store from the accumulators (bf16: 8 B, fp32: 16 B); one per-lane offset, the fragment row in the
         // SGPR offset, the fragment column in the instruction's immediate; rows past M fall outside the resource
@@ -789,7 +793,11 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
         const int voff = ((wm * 128 + ml) * ldcs + wn * WN + 8 * gq) * ES;
         const int nbase = ct.n0 + wn * WN + 8 * gq;
         // Zout / Zin share C's leading dimension and batch offset (bf16)
-        const i32x4_t rz4 = make_rsrc(p.Zout ? reinterpret_cast<const char*>(p.Zout) + ct.coff * 2 + corg : cbase, cext);
+        // (fp32 C, row layout: Zout is the output's bf16 copy, C's geometry at 2 bytes per element)
+        constexpr bool ZC = ZCOPY;
+        const i32x4_t rz4 = make_rsrc(p.Zout ? reinterpret_cast<const char*>(p.Zout) + ct.coff * 2 + (ZC ? corg / 2 : corg)
+                                             : cbase,
+                                      ZC ? cext / 2 : cext);
         const __amdgpu_buffer_rsrc_t rzi =
             make_brsrc(p.Zin ? reinterpret_cast<const char*>(p.Zin) + ct.coff * 2 + corg : cbase, cext);
         const bool zout = p.Zout != nullptr;
@@ -854,6 +862,9 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
                   }
                   o0[r] = __builtin_bit_cast(v4u32_t, f32x4_t{x[0], x[1], x[2], x[3]});
                   o1[r] = __builtin_bit_cast(v4u32_t, f32x4_t{x[4], x[5], x[6], x[7]});
+                  if constexpr (ZCOPY)
+                    zo[r] = v4u32_t{pack_bf16x2(x[0], x[1]), pack_bf16x2(x[2], x[3]), pack_bf16x2(x[4], x[5]),
+                                    pack_bf16x2(x[6], x[7])};
                 } else {
                   if constexpr (EX) {
                     static_for<4>([&](auto tc) {
@@ -884,7 +895,12 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
                 }
                 if (colok) {
                   store16_nc<SC>(o0[r], vro[r], rc4);
-                  if constexpr (OUT_F32) store16_nc<SC>(o1[r], vro[r] + 16, rc4);
+                  if constexpr (OUT_F32) {
+                    store16_nc<SC>(o1[r], vro[r] + 16, rc4);
+                    if constexpr (ZCOPY) {
+                      if (zout) store16_nc<SC>(zo[r], vro[r] >> 1, rz4);   // the bf16 copy (2 of C's 4 bytes)
+                    }
+                  }
                 }
               });
               fence();
@@ -1080,6 +1096,10 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
               if constexpr (OUT_F32) {
                 store16_padded<pp * 128, SC>(va, vrow, rc4, std::integral_constant<int, pp * 128>{});
                 store16_padded<pp * 128 + 16, SC>(vb, vrow, rc4, std::integral_constant<int, pp * 128 + 16>{});
+                if (ZCOPY && zout)   // the bf16 copy: the same element offsets at 2 of C's 4 bytes
+                  store16_padded<pp * 64, SC>(v4u32_t{pack_bf16x2(va[0], va[1]), pack_bf16x2(va[2], va[3]),
+                                                      pack_bf16x2(vb[0], vb[1]), pack_bf16x2(vb[2], vb[3])},
+                                             vrow >> 1, rz4, std::integral_constant<int, pp * 64>{});
               } else {
                 // the same unpadded-hazard as the fp32 stores (garbage in ~1% of the bf16 outputs, measured)
                 store16_padded<pp * 64, SC>(v4u32_t{pack_bf16x2(va[0], va[1]), pack_bf16x2(va[2], va[3]),
@@ -1214,7 +1234,13 @@ hipError_t launch4w(GemmArgs a, int batch, hipStream_t stream) {
       which = 2;
     }
   }
-  static bool attr[3] = {false, false, false};
+  if constexpr (F32 && A_T == 0) {
+    if (a.Zout) {   // fp32 output + bf16 copy (RevNet stream update: A is the activation or the mixer weight)
+      k = gemm4w_kernel<A_T, B_T, F32, false, NWV, G4W_SCH, (G4W_STG != 0), G4W_CPA, G4W_CPB, G4W_OPT, false, true>;
+      which = 3;
+    }
+  }
+  static bool attr[4] = {false, false, false, false};
   if (!attr[which]) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr[which] = true;

@@ -7,7 +7,8 @@ namespace gemmk {   // external linkage: gemm.hip hands a filled GemmArgs to gem
 struct GemmArgs {
   const bf16_t* A; const bf16_t* B; void* C;
   const void* R;          // residual added before the activation (same dtype/layout as C) or null
-  bf16_t* Zout;           // pre-activation output (bf16, layout of C) or null
+  bf16_t* Zout;           // bf16 C: pre-activation output; fp32 C: bf16 copy of the output (layout of C; gemm4w
+                          // row-layout direct epilogue and the 128x128 kernel only) or null
   const bf16_t* Zin;      // saved pre-activation for the activation-backward epilogue (layout of C)
   long long lda, ldb, ldc;
   long long a_s1, a_s2, b_s1, b_s2, c_s1, c_s2;

@@ -225,14 +225,17 @@ __device__ __forceinline__ uint32_t pk2(float lo, float hi) {
   return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
 }
 
-template <int NCH, int LPR>
-__global__ __launch_bounds__(NTH, bwd_blocks_per_cu<NCH>()) void norm_bwd_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ DY,
+// F32R: the RevNet stream form (fp32 gradient R32 added, dx written in fp32 to DX32 and as its bf16 copy to DX) --
+// its own instantiation, so the plain kernel keeps its register budget
+template <int NCH, int LPR, bool F32R>
+__device__ __forceinline__ void norm_bwd_body(const bf16_t* __restrict__ X, const bf16_t* __restrict__ DY,
                                                        const float* __restrict__ scale, const float* __restrict__ stats,
                                                        bf16_t* __restrict__ DX, float* __restrict__ dscale,
                                                        float* __restrict__ dshift, long long rows, int F, int groups,
                                                        int Ffull, float* __restrict__ partial_out,
                                                        const float* __restrict__ ext_dsum,
-                                                       const bf16_t* __restrict__ R, float* __restrict__ ws) {
+                                                       const bf16_t* __restrict__ R, float* __restrict__ ws,
+                                                       const float* __restrict__ R32, float* __restrict__ DX32) {
   constexpr int RPW = 64 / LPR;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* red_s = reinterpret_cast<float*>(smem);           // [4 waves][F] dscale partials, then dshift
@@ -337,6 +340,23 @@ __global__ __launch_bounds__(NTH, bwd_blocks_per_cu<NCH>()) void norm_bwd_kernel
       unpack8(cx[c], x);
       unpack8(cd[c], dy);
       float r[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if constexpr (F32R) {   // the RevNet stream gradient (fp32): dx in fp32 to DX32, its bf16 copy to DX
+        const float4 ra = reinterpret_cast<const float4*>(R32 + row * F + col)[0];
+        const float4 rb = reinterpret_cast<const float4*>(R32 + row * F + col)[1];
+        r[0] = ra.x; r[1] = ra.y; r[2] = ra.z; r[3] = ra.w; r[4] = rb.x; r[5] = rb.y; r[6] = rb.z; r[7] = rb.w;
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float g = scale ? gsc[j] : 1.f;
+          const float xh = (x[j] - mean) * rstd;
+          v[j] = rstd * (dy[j] * g - m1 - xh * m2) + r[j];
+        }
+        *reinterpret_cast<uint4*>(DX + row * F + col) =
+            make_uint4(pk2(v[0], v[1]), pk2(v[2], v[3]), pk2(v[4], v[5]), pk2(v[6], v[7]));
+        reinterpret_cast<float4*>(DX32 + row * F + col)[0] = make_float4(v[0], v[1], v[2], v[3]);
+        reinterpret_cast<float4*>(DX32 + row * F + col)[1] = make_float4(v[4], v[5], v[6], v[7]);
+        continue;
+      }
       if (R) unpack8(cr[c], r);   // the block's residual-input gradient, summed here instead of in a separate pass
       uint32_t o[4];
 #pragma unroll
@@ -390,6 +410,24 @@ __global__ __launch_bounds__(NTH, bwd_blocks_per_cu<NCH>()) void norm_bwd_kernel
       __syncthreads();
     }
   }
+}
+
+#define NORM_BWD_PARAMS                                                                                          \
+  const bf16_t *__restrict__ X, const bf16_t *__restrict__ DY, const float *__restrict__ scale,                \
+      const float *__restrict__ stats, bf16_t *__restrict__ DX, float *__restrict__ dscale,                    \
+      float *__restrict__ dshift, long long rows, int F, int groups, int Ffull, float *__restrict__ partial_out, \
+      const float *__restrict__ ext_dsum, const bf16_t *__restrict__ R, float *__restrict__ ws,               \
+      const float *__restrict__ R32, float *__restrict__ DX32
+#define NORM_BWD_ARGS X, DY, scale, stats, DX, dscale, dshift, rows, F, groups, Ffull, partial_out, ext_dsum, R, ws, R32, DX32
+
+template <int NCH, int LPR>
+__global__ __launch_bounds__(NTH, bwd_blocks_per_cu<NCH>()) void norm_bwd_kernel(NORM_BWD_PARAMS) {
+  norm_bwd_body<NCH, LPR, false>(NORM_BWD_ARGS);
+}
+
+template <int NCH, int LPR>
+__global__ __launch_bounds__(NTH, bwd_blocks_per_cu<NCH>()) void norm_bwd32_kernel(NORM_BWD_PARAMS) {
+  norm_bwd_body<NCH, LPR, true>(NORM_BWD_ARGS);
 }
 
 // deterministic fold of the parameter-gradient slab: out[g][f] += sum over partial rows p = g, g + period, ... (in
@@ -448,6 +486,8 @@ struct ObstNormDesc {
   long long rows; int F; int groups; int Ffull; float eps;
   const void* R;                      // backward: gradient added to DX (residual input of the block) or null
   float* ws;                          // backward with parameter gradients: obst_norm_bwd_ws(desc) floats
+  const float* R32;                   // backward: fp32 gradient added to DX (the RevNet stream gradient) or null
+  float* DX32;                        // backward with R32: DX in fp32 (DX then holds its bf16 copy)
 };
 
 #define NORM_DISPATCH_L(KERNEL, LPR, GRID, LDSB, ...)                                               \
@@ -525,15 +565,21 @@ OBST_API long long obst_norm_bwd_ws(const ObstNormDesc* d) {
 
 OBST_API int obst_norm_bwd(const ObstNormDesc* d, hipStream_t st) {
   if (d->F % 8 || d->rows <= 0) return -1;
+  if ((d->R && d->R32) || (d->DX32 && !d->R32)) return -4;
   const bool params = norm_bwd_params(d);
   if (params && !d->ws) return -3;
   // reduction scratch [8][LPR*8] floats (<= 16 KiB), plus the staged scale ([F] floats) for wide rows
   const int nch = (d->F + lanes_per_row(d->F) * 8 - 1) / (lanes_per_row(d->F) * 8);
   const size_t lds = (size_t)8 * lanes_per_row(d->F) * 8 * 4 + (nch > 2 && d->scale && d->groups == 1 ? d->F * 4 : 0);
   const int grid = norm_bwd_grid(d);
-  NORM_DISPATCH(norm_bwd_kernel, dim3(grid), lds, (const bf16_t*)d->X, (const bf16_t*)d->DY, d->scale, d->stats,
-                (bf16_t*)d->DX, d->dscale, d->dshift, d->rows, d->F, d->groups, d->Ffull, d->partial, d->ext,
-                (const bf16_t*)d->R, d->ws);
+  if (d->R32)
+    NORM_DISPATCH(norm_bwd32_kernel, dim3(grid), lds, (const bf16_t*)d->X, (const bf16_t*)d->DY, d->scale, d->stats,
+                  (bf16_t*)d->DX, d->dscale, d->dshift, d->rows, d->F, d->groups, d->Ffull, d->partial, d->ext,
+                  (const bf16_t*)d->R, d->ws, d->R32, d->DX32);
+  else
+    NORM_DISPATCH(norm_bwd_kernel, dim3(grid), lds, (const bf16_t*)d->X, (const bf16_t*)d->DY, d->scale, d->stats,
+                  (bf16_t*)d->DX, d->dscale, d->dshift, d->rows, d->F, d->groups, d->Ffull, d->partial, d->ext,
+                  (const bf16_t*)d->R, d->ws, d->R32, d->DX32);
   if (params) {
     const long long parts = d->groups > 1 ? (long long)grid * 4 * (64 / lanes_per_row(d->F)) : grid;
     const long long nout = 2LL * d->groups * d->F;

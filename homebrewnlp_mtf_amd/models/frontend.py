@@ -16,8 +16,8 @@ from .layers import LAYER_FUNCTIONS
 _FUSABLE_LAST = ("feed_forward", "attention")
 
 
-def run_layers(builder: Builder, layers: typing.List[str], x: Act, residual: typing.Optional[Act] = None
-               ) -> typing.Tuple[Act, bool]:
+def run_layers(builder: Builder, layers: typing.List[str], x: Act, residual: typing.Optional[Act] = None,
+               stream_sink=None, grad_sink=None) -> typing.Tuple[Act, bool]:
     out = x
     consumed = False
     seen: typing.Dict[str, int] = {}
@@ -42,16 +42,21 @@ def run_layers(builder: Builder, layers: typing.List[str], x: Act, residual: typ
             args.residual_carrier = carrier
         if idx == 1 and carrier is not None:
             args.norm_carrier = carrier
+        if idx == n and stream_sink is not None:
+            args.stream_sink = stream_sink   # consumed (sink.out32 set) only by a layer that can fuse it
+        if idx == 1 and grad_sink is not None and name == "norm":
+            args.grad_sink = grad_sink       # the norm on the block input itself
         with builder.scope(name + '_'):
             out = LAYER_FUNCTIONS[name](args)
         consumed = consumed or getattr(args, "residual_consumed", False)
     return out, consumed
 
 
-def block_body(builder: Builder, config: BlockConfig, x: Act) -> Act:
+def block_body(builder: Builder, config: BlockConfig, x: Act, stream_sink=None, grad_sink=None) -> Act:
     """the block's layers (+ skip), run inside an already-entered block scope"""
     skip = config.skip and config.memory_reduction_strategy in ("none", "checkpoint")
-    out, consumed = run_layers(builder, list(config.layer), x, residual=x if skip else None)
+    out, consumed = run_layers(builder, list(config.layer), x, residual=x if skip else None,
+                               stream_sink=stream_sink, grad_sink=grad_sink)
     if skip and not consumed:
         out = Act(F.add(out.t, x.t), out.dims)
     return out

@@ -87,7 +87,8 @@ def anonymize(a: Act, dim: Dim) -> Act:
 
 # ================================================================================================================
 # linear (ref backend.py:108-118, basic.py:33-34)
-def linear(args: BlockArgs, old: typing.List[Dim], new: typing.List[Dim], act: typing.Optional[str] = None) -> Act:
+def linear(args: BlockArgs, old: typing.List[Dim], new: typing.List[Dim], act: typing.Optional[str] = None,
+           sink=None) -> Act:
     x = args.tensor
     w = _scoped(args, "linear", orthogonal_var, args, list(old) + list(new), list(old))
     wdims = D.deduplicate(list(old) + list(new))
@@ -101,7 +102,7 @@ def linear(args: BlockArgs, old: typing.List[Dim], new: typing.List[Dim], act: t
         if act and plan.row_parallel and tp:   # all-reduce must precede the activation
             y = F.activation(F.linear(x.t, w, x.dims, wdims, odims), act)
         else:
-            y = F.linear(x.t, w, x.dims, wdims, odims, act=act)
+            y = F.linear(x.t, w, x.dims, wdims, odims, act=act, sink=sink)
         return Act(y, odims)
     hd = args.params.head_dim
     xt = x.t
@@ -187,9 +188,15 @@ def mixture_of_experts(args: BlockArgs) -> Act:
 
 def activated_linear(args: BlockArgs, prefix: str) -> Act:
     """ref basic.py:47-57."""
+    # (only an out-projection can be a block's last product)
+    sink = getattr(args, "stream_sink", None) if prefix == 'out:' else None
     args = args([a[len(prefix):] for a in args if a.startswith(prefix)])
     ff = mixture_of_experts if 'mixture_of_experts' in args else wrapped_linear
     act = _activation_name(args)
+    if sink is not None and ff is wrapped_linear and act is None and _plain(list(args)):
+        # the block's last product: the RevNet stream update rides in its epilogue (F.StreamSink)
+        old, new = D.linear_shapes(args.params, args, args.tensor.dims)
+        return linear(args, old, new, sink=sink)
     if ff is wrapped_linear and act is not None and act != "mtf_mish":
         old, new = D.linear_shapes(args.params, args, args.tensor.dims)
         out = linear(args, old, new, act=act)   # activation fused into the GEMM epilogue
@@ -366,9 +373,11 @@ def feed_forward_product_key_memory(args: BlockArgs) -> Act:
 
 def bottleneck_group_linear(args: BlockArgs) -> Act:
     """ref basic.py:122-126."""
+    sink = getattr(args, "stream_sink", None)
     args = args(activated_linear_in(args))
     args.name_extras.extend(['group', 'mid:group', 'out:group'])
     args = args(activated_linear(args, 'mid:'))
+    args.stream_sink = sink
     return activated_linear_out(args)
 
 
@@ -397,7 +406,7 @@ def norm(args: BlockArgs, feature_shape: typing.Optional[typing.List[Dim]] = Non
         groups = p.head_dim.size if group else 1
         tp_stats = (not group) and p.head_dim in normalized and pstate.tp_size() > 1
         y = F.norm(x.t, scale, shift, Fsz, groups, tp_stats=tp_stats,
-                   carrier=getattr(args, "norm_carrier", None))
+                   carrier=getattr(args, "norm_carrier", None), grad_sink=getattr(args, "grad_sink", None))
         return Act(y, x.dims)
     # any other layout: permute to [others..., group?, normalized...] (row % groups = the group index), the same
     # kernel, permute back; parameters are permuted copies to [group?, normalized...] (their gradients flow back
@@ -640,7 +649,7 @@ def attention(args: BlockArgs) -> Act:
         if kv is not None and causal:
             return _mixer_kv(args, kv, x, dim, tmp, causal)
         bias = embed(args, [p.head_dim, dim, tmp])
-        return Act(F.token_mixer(x.t, bias.t, causal), x.dims)
+        return Act(F.token_mixer(x.t, bias.t, causal, sink=getattr(args, "stream_sink", None)), x.dims)
     fold = _fold_of(p, x.dims, dim) if FLASH_MAPS else None
     if (fold is not None and not fold.identity and args.builder.kv is None and 'biased_attention_map' in args
             and 'input_as_value' in args and not any(k in args for k in ('dot_product', 'biased_softmax',

@@ -17,6 +17,7 @@ import typing
 
 import torch
 
+from ..ops import functional as F
 from ..ops import raw
 from ..utils import debug
 from .context import Act, Builder
@@ -29,11 +30,19 @@ class Block:
         self.stack = stack + [block_scope_name(depth, config_idx)]
         self.dims = dims
 
-    def __call__(self, x: torch.Tensor) -> torch.Tensor:
+    def __call__(self, x: torch.Tensor, sink=None, gsink=None) -> torch.Tensor:
         b = self.builder
         b.depth_idx, b.config_idx = self.depth, self.config_idx
         with b.scope.restore(self.stack), debug.range_(self.stack[-1]):
-            return block_body(b, self.config, Act(x, self.dims)).t
+            return block_body(b, self.config, Act(x, self.dims), stream_sink=sink, grad_sink=gsink).t
+
+
+# OBST_REV_FUSE=0: the RevNet stream updates as separate mix_f32 passes (A/B)
+_REV_FUSE = __import__("os").environ.get("OBST_REV_FUSE", "1") != "0"
+
+
+def _sink(r32: torch.Tensor, alpha: float):
+    return F.StreamSink(r32, alpha) if _REV_FUSE and raw.on_gpu(r32) else None
 
 
 def _stream_dtype(dt: torch.dtype) -> torch.dtype:
@@ -61,8 +70,15 @@ class _RevStack(torch.autograd.Function):
             if mode == "revnet" and low:
                 x2b = raw.to_bf16(x2)
                 for f in blocks:
-                    nb = torch.empty_like(x2b)
-                    nx2 = raw.mix_f32(x1, f(x2b), 1.0, 1.0, yb=nb)   # y2 = x1 + F(x2), plus its bf16 copy
+                    # y2 = x1 + F(x2) and its bf16 copy: from the block's last GEMM when it can take the update
+                    # (F.StreamSink), else one mix_f32 pass
+                    sink = _sink(x1, 1.0)
+                    fx = f(x2b, sink)
+                    if sink is not None and sink.out32 is not None:
+                        nx2, nb = sink.out32, fx
+                    else:
+                        nb = torch.empty_like(x2b)
+                        nx2 = raw.mix_f32(x1, fx, 1.0, 1.0, yb=nb)
                     x1, x2, x2b = x2, nx2, nb
             else:
                 for f in blocks:
@@ -90,16 +106,30 @@ class _RevStack(torch.autograd.Function):
                 if bf:
                     y1b = raw.to_bf16(y1) if y1b is None else y1b
                     g2b = raw.to_bf16(g2) if g2b is None else g2b
+                # the recomputed F's last GEMM can also produce the reconstruction x1 = y2 - F(x2) (and its bf16
+                # copy); its output is then that copy, and the backward below still receives dL/dF = g2 for it
+                sink = _sink(y2, -1.0) if bf else None
+                # and the norm opening the block can produce dx2 = g1 + dF/dx2 in fp32 with its bf16 copy
+                gsink = F.GradSink(g1) if sink is not None else None
                 with torch.enable_grad():
                     x2 = (y1b if bf else y1.to(dt)).detach().requires_grad_(True)
-                    fx = f(x2)
+                    fx = f(x2, sink, gsink)
                 torch.autograd.backward(fx, g2b if bf else g2.to(dt))
                 if bf:
                     # x1 = y2 - F(x2) and dx2 = g1 + dF/dx2, each with its bf16 copy for the next (earlier) block
-                    nb1 = torch.empty_like(y1b)
-                    x1 = raw.mix_f32(y2, fx.detach(), 1.0, -1.0, yb=nb1)
+                    if sink is not None and sink.out32 is not None:
+                        x1, nb1 = sink.out32, fx.detach()
+                    else:
+                        nb1 = torch.empty_like(y1b)
+                        x1 = raw.mix_f32(y2, fx.detach(), 1.0, -1.0, yb=nb1)
                     if x2.grad is None:
                         dx2, nb2 = g1, None
+                    elif gsink is not None and gsink.out32 is not None:
+                        if x2.grad.data_ptr() == gsink.ptr:
+                            dx2, nb2 = gsink.out32, x2.grad
+                        else:   # another gradient reached x2 besides the norm's (or autograd copied it): x2.grad
+                            # already holds g1 (summed in bf16) -- correct, at bf16 precision
+                            dx2, nb2 = x2.grad.float(), x2.grad
                     else:
                         nb2 = torch.empty_like(y1b)
                         dx2 = raw.mix_f32(g1, x2.grad, 1.0, 1.0, yb=nb2)

@@ -126,12 +126,12 @@ def _wT(w, plan: LinearPlan, act=None, has_r: bool = False):
     return store.transposed(w.var_name, plan.H, plan.K, plan.N)
 
 
-def _fwd_gemm(x2, w, y2, plan: LinearPlan, act=None, R=None, Zout=None):
+def _fwd_gemm(x2, w, y2, plan: LinearPlan, act=None, R=None, Zout=None, alpha: float = 1.0):
     M, H, K, N = plan.M, plan.H, plan.K, plan.N
     wt = _wT(w, plan, act, R is not None)
     bop = raw.Operand(wt, 0, K, K * N) if wt is not None else raw.Operand(w, 1, N, K * N)
     raw.gemm(raw.Operand(x2, 0, H * K, K), bop, raw.Operand(y2, 0, H * N, N),
-             M, N, K, batch=(H, 1), act=act, R=R, Zout=Zout)
+             M, N, K, batch=(H, 1), act=act, R=R, Zout=Zout, alpha=alpha)
 
 
 # Row-parallel forward under TP (the weight contracts the sharded heads: every rank holds a partial sum of the whole
@@ -211,17 +211,48 @@ def _wgrad_gemm(x2, dy2, gw, plan: LinearPlan, xT=None, dyT=None, beta: float = 
              K, N, M, batch=(H, 1), beta=beta)
 
 
+class StreamSink:
+    """The RevNet stream update of a block fused into the block's last GEMM (ref src/model/revnet.py:20-49):
+    out32 = r32 + alpha * F(x) in fp32 and its bf16 copy come out of that GEMM's epilogue, replacing the separate
+    mix_f32 pass over the fp32 stream (forward: y2 = x1 + F(x2), alpha 1; backward reconstruction x1 = y2 - F(x2),
+    alpha -1). The op that takes it returns the bf16 copy as its output -- a value autograd never reads: the RevNet
+    stack back-propagates dL/dF through that op explicitly -- and leaves the fp32 tensor in ``out32``."""
+
+    def __init__(self, r32: torch.Tensor, alpha: float):
+        self.r32, self.alpha = r32, float(alpha)
+        self.out32: typing.Optional[torch.Tensor] = None
+
+    def usable(self, y_shape, device) -> bool:
+        """a fresh fp32 [.., y] buffer of the op's output shape on the GPU, nothing consumed yet"""
+        return (self.out32 is None and raw.on_gpu(self.r32) and self.r32.dtype == torch.float32
+                and self.r32.is_contiguous() and self.r32.numel() == math.prod(y_shape)
+                and self.r32.device == device)
+
+    def run(self, y_shape, device, gemm) -> torch.Tensor:
+        """gemm(out32, out16): the fused product; returns the bf16 copy"""
+        y16 = torch.empty(y_shape, dtype=torch.bfloat16, device=device)
+        y32 = torch.empty(y_shape, dtype=torch.float32, device=device)
+        gemm(y32, y16)
+        self.out32 = y32
+        return y16
+
+
 class _Linear(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, plan: LinearPlan, act):
+    def forward(ctx, x, w, plan: LinearPlan, act, sink: typing.Optional[StreamSink] = None):
         xc = x.permute(plan.x_perm).contiguous() if plan.x_perm is not None else x.contiguous()
-        y = _empty(plan.canon_o_shape, xc)
         z = _empty(plan.canon_o_shape, xc) if act else None
         if plan.row_parallel and pstate.tp_size() > 1:
             if act:
                 raise NotImplementedError("activation fused into a heads-contracting linear under TP")
+            y = _empty(plan.canon_o_shape, xc)
             _fwd_gemm_reduced(xc, w, y, plan)
+        elif (sink is not None and act is None and plan.o_perm is None
+              and sink.usable(plan.canon_o_shape, xc.device)):
+            y = sink.run(plan.canon_o_shape, xc.device,
+                         lambda y32, y16: _fwd_gemm(xc, w, y32, plan, R=sink.r32, Zout=y16, alpha=sink.alpha))
         else:
+            y = _empty(plan.canon_o_shape, xc)
             _fwd_gemm(xc, w, y, plan, act=act, Zout=z)
         ctx.save_for_backward(xc, w, z)
         ctx.plan, ctx.act = plan, act
@@ -255,13 +286,13 @@ class _Linear(torch.autograd.Function):
         _wgrad_gemm(xc, dy, gw, plan, beta=beta)
         _done(w)
         pending.wait()
-        return dx, (None if is_main else gw.to(w.dtype)), None, None
+        return dx, (None if is_main else gw.to(w.dtype)), None, None, None
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, xdims: DimList, wdims: DimList, odims: DimList,
-           act: typing.Optional[str] = None) -> torch.Tensor:
+           act: typing.Optional[str] = None, sink: typing.Optional[StreamSink] = None) -> torch.Tensor:
     plan = linear_plan(tuple(xdims), tuple(wdims), tuple(odims))
-    return _Linear.apply(x, w, plan, act)
+    return _Linear.apply(x, w, plan, act, sink)
 
 
 class _TPReduce(torch.autograd.Function):
@@ -573,7 +604,7 @@ def dot_attention(x, w_in, w_k, w_q, w_v, xdims, w_in_dims, base_dims, w_out_dim
 # (tri flags of the GEMM), so forward and dgrad run ~half the dense FLOPs and dW only fills the lower triangle.
 class _TokenMixer(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, causal: bool):
+    def forward(ctx, x, w, causal: bool, sink: typing.Optional[StreamSink] = None):
         B, S, H, Fd = x.shape
         xc = x.contiguous()
         store = getattr(w, "store", None)
@@ -582,10 +613,17 @@ class _TokenMixer(torch.autograd.Function):
             wm = store.derived(w.var_name, f"tril@{w.data_ptr()}", lambda: torch.tril(w.detach()))
         else:
             wm = torch.tril(w) if causal else w.contiguous()
-        y = torch.empty_like(xc)
         hf = H * Fd
-        raw.gemm(raw.Operand(wm, 0, S, 0, S * S), raw.Operand(xc, 1, hf, S * hf, Fd), raw.Operand(y, 0, hf, S * hf, Fd),
-                 S, Fd, S, batch=(B, H), tri=1 if causal else 0)
+
+        def product(y, R=None, Zout=None, alpha=1.0):
+            raw.gemm(raw.Operand(wm, 0, S, 0, S * S), raw.Operand(xc, 1, hf, S * hf, Fd),
+                     raw.Operand(y, 0, hf, S * hf, Fd), S, Fd, S, batch=(B, H), tri=1 if causal else 0,
+                     R=R, Zout=Zout, alpha=alpha)
+        if sink is not None and sink.usable(xc.shape, xc.device):
+            y = sink.run(xc.shape, xc.device, lambda y32, y16: product(y32, R=sink.r32, Zout=y16, alpha=sink.alpha))
+        else:
+            y = torch.empty_like(xc)
+            product(y)
         ctx.save_for_backward(xc, wm, w)
         ctx.causal = causal
         return y
@@ -620,12 +658,12 @@ class _TokenMixer(torch.autograd.Function):
             raw.gemm(raw.Operand(dyp, 0, kk, 0, S * kk), raw.Operand(xp, 0, kk, 0, S * kk),
                      raw.Operand(g, 0, S, 0, S * S), S, S, kk, batch=(1, H), beta=1.0, tri=3 if ctx.causal else 0)
         _done(w)
-        return dx, (None if m else g.to(w.dtype)), None
+        return dx, (None if m else g.to(w.dtype)), None, None
 
 
-def token_mixer(x, w, causal: bool):
-    """x [B, S, H, F], w [H, S, S] (query, key)"""
-    return _TokenMixer.apply(x, w, causal)
+def token_mixer(x, w, causal: bool, sink: typing.Optional[StreamSink] = None):
+    """x [B, S, H, F], w [H, S, S] (query, key); sink: the RevNet stream update fused into the product"""
+    return _TokenMixer.apply(x, w, causal, sink)
 
 
 @torch.no_grad()
@@ -798,9 +836,25 @@ class ResidualGrad:
         self.grad = None
 
 
+class GradSink:
+    """The RevNet stream gradient of a block input (ref src/model/revnet.py:51-120): the norm opening the block
+    adds the fp32 stream gradient g32 into its dx inside the backward kernel and writes the sum in fp32 (``out32``)
+    plus the bf16 copy it returns as dx -- replacing the separate dx2 = g1 + dF/dx2 mix_f32 pass. ``ptr`` is that
+    bf16 tensor's address: the stack checks that the input's .grad is exactly it (no other gradient was summed in)."""
+
+    def __init__(self, g32: torch.Tensor):
+        self.g32 = g32
+        self.out32: typing.Optional[torch.Tensor] = None
+        self.ptr = 0
+
+    def usable(self, x: torch.Tensor) -> bool:
+        return (self.out32 is None and raw.on_gpu(self.g32) and self.g32.dtype == torch.float32
+                and self.g32.is_contiguous() and self.g32.numel() == x.numel() and self.g32.device == x.device)
+
+
 class _Norm(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, scale, shift, F, groups, tp_stats, carrier=None):
+    def forward(ctx, x, scale, shift, F, groups, tp_stats, carrier=None, grad_sink=None):
         xc = x.contiguous()
         rows = xc.numel() // F
         y = torch.empty_like(xc)
@@ -823,6 +877,7 @@ class _Norm(torch.autograd.Function):
         ctx.cfg = (F, groups, rows, Ffull, tp_stats)
         ctx.sm32 = sm32
         ctx.carrier = carrier
+        ctx.grad_sink = grad_sink
         return y
 
     @staticmethod
@@ -843,16 +898,24 @@ class _Norm(torch.autograd.Function):
         if ctx.carrier is not None and ctx.carrier.grad is not None:
             R = ctx.carrier.grad.contiguous()
             ctx.carrier.grad = None
-        raw.norm_bwd(xc, dy, ctx.sm32, stats, dx, gsc, gsh, rows, F, groups, Ffull, ext_dsum=ext, R=R)
+        sink = ctx.grad_sink
+        if sink is not None and R is None and ext is None and sink.usable(xc):
+            dx32 = torch.empty(xc.shape, dtype=torch.float32, device=xc.device)
+            raw.norm_bwd(xc, dy, ctx.sm32, stats, dx, gsc, gsh, rows, F, groups, Ffull, R32=sink.g32, dx32=dx32)
+            sink.out32, sink.ptr = dx32, dx.data_ptr()
+        else:
+            raw.norm_bwd(xc, dy, ctx.sm32, stats, dx, gsc, gsh, rows, F, groups, Ffull, ext_dsum=ext, R=R)
+        ctx.grad_sink = None
         for t in (scale, shift):
             if t is not None:
                 _done(t)
         return (dx, None if msc else gsc.view(scale.shape).to(scale.dtype),
-                None if msh else gsh.view(shift.shape).to(shift.dtype), None, None, None, None)
+                None if msh else gsh.view(shift.shape).to(shift.dtype), None, None, None, None, None)
 
 
-def norm(x, scale, shift, F: int, groups: int, tp_stats: bool = False, carrier: typing.Optional[ResidualGrad] = None):
-    return _Norm.apply(x, scale, shift, F, groups, tp_stats, carrier)
+def norm(x, scale, shift, F: int, groups: int, tp_stats: bool = False, carrier: typing.Optional[ResidualGrad] = None,
+         grad_sink: typing.Optional[GradSink] = None):
+    return _Norm.apply(x, scale, shift, F, groups, tp_stats, carrier, grad_sink)
 
 
 # ================================================================================================================

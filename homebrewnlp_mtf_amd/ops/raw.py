@@ -158,6 +158,7 @@ def gemm(a: Operand, b: Operand, c: Operand, M: int, N: int, K: int, batch: typi
     outer strides a_sk / b_sk -- a product over (batch, feature) pairs of a [B, S, H, F] tensor reads it in place.
 
     epilogue (act_bwd False): v = alpha*acc (+ beta*C if C is fp32) (+ R); Zout <- v; C <- act(v)
+      (fp32 C without activation: Zout <- bf16(v), the output's bf16 copy -- the fused RevNet stream update)
     epilogue (act_bwd True) : C <- (alpha*acc + R) * act'(Zin)"""
     if c.t.device.type == "meta":
         return c.t
@@ -203,7 +204,8 @@ def gemm(a: Operand, b: Operand, c: Operand, M: int, N: int, K: int, batch: typi
                 raise L.KernelError(f"gemm operand {nm} must be bfloat16 on the GPU, got {t.dtype}")
         if not out_f32 and c.t.dtype != torch.bfloat16:
             raise L.KernelError(f"gemm output must be bf16 or fp32, got {c.t.dtype}")
-        if (R is not None or Zout is not None or Zin is not None) and out_f32 and (Zout is not None or act_bwd):
+        if out_f32 and (act_bwd or (Zout is not None and act is not None)):
+            # (fp32 output with Zout and no activation: Zout is the output's bf16 copy)
             raise L.KernelError("pre-activation output / activation-backward epilogue need a bf16 output")
         bo = (b1 - 1) * a.s1 + (b2 - 1) * a.s2
         kext_a = (K // kin - 1) * a_sk + kin - 1 if kin else K - 1
@@ -494,10 +496,11 @@ def norm_partial(x, out, rows: int, F: int):
 
 
 def norm_bwd(x, dy, scale, stats, dx, dscale, dshift, rows: int, F: int, groups: int, Ffull: int = 0,
-             partial=None, ext_dsum=None, R=None):
+             partial=None, ext_dsum=None, R=None, R32=None, dx32=None):
     """dx (and parameter grads accumulated into fp32 dscale/dshift). With `partial` set, only the per-row partial
     sums (sum dxh, sum dxh*xh) are written (TP phase 1); phase 2 passes them back as `ext_dsum`. R (same layout as
-    dx) is added to dx."""
+    dx) is added to dx. R32 / dx32 (fp32, together, instead of R): dx32 = dx + R32 in fp32 and dx its bf16 copy (the
+    RevNet stream gradient, F.GradSink)."""
     if x.device.type == "meta":
         return None
     Ffull = Ffull or F
@@ -514,8 +517,16 @@ def norm_bwd(x, dy, scale, stats, dx, dscale, dshift, rows: int, F: int, groups:
             if R.dtype != torch.bfloat16 or not R.is_contiguous():
                 raise L.KernelError("norm_bwd residual gradient must be contiguous bf16")
             _need(R, rows * F - 1, "R")
+        if (R32 is None) != (dx32 is None) or (R32 is not None and R is not None):
+            raise L.KernelError("norm_bwd: R32 and dx32 come together, without R")
+        for nm, t in (("R32", R32), ("dx32", dx32)):
+            if t is not None:
+                if t.dtype != torch.float32 or not t.is_contiguous():
+                    raise L.KernelError(f"norm_bwd {nm} must be contiguous fp32")
+                _need(t, rows * F - 1, nm)
         d = L.NormDesc(x.data_ptr(), L.ptr(scale), 0, 0, stats.data_ptr(), dy.data_ptr(), L.ptr(dx), L.ptr(dscale),
                        L.ptr(dshift), L.ptr(partial), L.ptr(ext_dsum), rows, F, groups, Ffull, EPS, L.ptr(R))
+        d.R32, d.DX32 = L.ptr(R32), L.ptr(dx32)
         nws = int(L.lib().obst_norm_bwd_ws(d))
         ws = torch.empty(max(nws, 1), dtype=torch.float32, device=x.device) if nws else None
         d.ws = L.ptr(ws)     # parameter-gradient partial slab, folded in a fixed order (no float atomics)
@@ -542,6 +553,9 @@ def norm_bwd(x, dy, scale, stats, dx, dscale, dshift, rows: int, F: int, groups:
     out = st[:, 1:2] * (dxh - s1 / Ffull - xh * s2 / Ffull)
     if R is not None:
         out = out + _f(R.reshape(rows, F))
+    if R32 is not None:
+        out = out + R32.reshape(rows, F).to(out.dtype)
+        dx32.reshape(rows, F).copy_(out)
     dx.reshape(rows, F).copy_(out)
 
 

@@ -258,6 +258,34 @@ def test_norm(cuda, F_, groups, nrows):
         _close(g, c, 3e-2, 2e-2, f"norm F={F_} {name}")
 
 
+@pytest.mark.parametrize("F_,groups,nrows", [(256, 8, 300), (2048, 1, 96), (64, 4, 1000)])
+def test_norm_bwd_fp32_stream_gradient(cuda, F_, groups, nrows):
+    """the RevNet stream-gradient form of the norm backward (F.GradSink): dx32 = dx + g32 in fp32 (its own kernel
+    instantiation), dx = its bf16 copy"""
+    torch.manual_seed(F_ + groups)
+    rows = nrows * groups
+    x = (torch.randn(rows * F_) * 2 + 0.3).to(BF)
+    dy = torch.randn(rows * F_).to(BF)
+    g32 = torch.randn(rows * F_) * 3
+    sc = torch.randn(groups * F_) * 0.1 + 1
+    res = {}
+    for dev in ("cpu", cuda):
+        y = torch.zeros(rows * F_, dtype=BF, device=dev)
+        st = torch.zeros(2 * rows, device=dev)
+        raw.norm_fwd(x.to(dev), sc.to(dev), None, y, st, rows, F_, groups)
+        dx = torch.zeros(rows * F_, dtype=BF, device=dev)
+        dx32 = torch.full((rows * F_,), float("nan"), device=dev)
+        dsc = torch.zeros(groups * F_, device=dev)
+        raw.norm_bwd(x.to(dev), dy.to(dev), sc.to(dev), st, dx, dsc, None, rows, F_, groups, R32=g32.to(dev),
+                     dx32=dx32)
+        res[str(dev)] = (dx32, dsc, dx)
+    torch.cuda.synchronize()
+    for name, g, c in zip(["dx32", "dscale"], res[str(cuda)][:2], res["cpu"][:2]):
+        _close(g, c, 3e-2, 2e-2, f"norm stream gradient F={F_} {name}")
+    dx32, _, dx = res[str(cuda)]
+    assert torch.equal(dx.cpu(), dx32.cpu().to(BF)), "dx is not the bf16 copy of dx32"
+
+
 @pytest.mark.parametrize("op,act", [("act", "gelu"), ("act", "relu"), ("act_bwd", "gelu"), ("act_bwd", "mish"),
                                     ("act", "silu"), ("act", "lecun_tanh"), ("add", None), ("axpby", None),
                                     ("mul", None), ("dropout", None), ("act_bwd", "softsign")])
@@ -623,3 +651,31 @@ def test_gemm_split_contraction_index(cuda, out_f32):
              raw.Operand(c, 0, S, 0, S * S), S, S, Bb * Fd, batch=(1, H), kin=Fd, a_sk=S * hf, b_sk=S * hf)
     ref = torch.einsum("bshf,bthf->hst", a.float(), b.float())
     _close(c.view(H, S, S).float().cpu(), ref, 3e-2, 2e-2, "split-index gemm")
+
+
+@pytest.mark.parametrize("b_t,tri,batch", [(0, 0, (3, 1)), (1, 1, (2, 3)), (1, 0, (1, 1))])
+@pytest.mark.parametrize("alpha", [1.0, -1.0])
+def test_gemm_fp32_stream_update_with_bf16_copy(cuda, b_t, tri, batch, alpha):
+    """the fused RevNet stream update (F.StreamSink): C = R + alpha * A.B in fp32 with Zout = bf16(C), written by
+    gemm4w's own instantiation (row layout for K-contiguous B, fragment layout for the mixer's N-contiguous B)"""
+    torch.manual_seed(11)
+    M, N, K = 512, 256, 512
+    b1, b2 = batch
+    nb = b1 * b2
+    a = (torch.randn(nb, M, K) * 0.3).to(BF)
+    if tri:
+        a = torch.tril(a)
+    bm = (torch.randn(nb, K, N) * 0.3).to(BF)
+    r = torch.randn(nb, M, N)
+    bs = bm.transpose(1, 2).contiguous() if b_t == 0 else bm     # stored [N][K] (K-contiguous) or [K][N]
+    c = torch.full((nb, M, N), float("nan"), device=cuda)
+    z = torch.full((nb, M, N), float("nan"), device=cuda).to(BF)
+    c0 = g4w_calls()
+    raw.gemm(raw.Operand(a.to(cuda), 0, K, b2 * M * K, M * K),
+             raw.Operand(bs.to(cuda), b_t, K if b_t == 0 else N, b2 * K * N, K * N),
+             raw.Operand(c, 0, N, b2 * M * N, M * N), M, N, K, batch=batch, alpha=alpha, R=r.to(cuda), Zout=z, tri=tri)
+    torch.cuda.synchronize()
+    assert g4w_calls() - c0 == 1
+    ref = r + alpha * torch.matmul(a.float(), bm.float())
+    _close(c, ref, 2e-2, 1e-2, f"stream update b_t={b_t} tri={tri}")
+    assert torch.equal(z.cpu(), c.cpu().to(BF)), "Zout is not the bf16 copy of C"

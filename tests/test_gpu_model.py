@@ -6,6 +6,7 @@ import torch
 
 from homebrewnlp_mtf_amd.config import ModelParameter
 from homebrewnlp_mtf_amd.models.model import Model
+from homebrewnlp_mtf_amd.ops import raw
 from homebrewnlp_mtf_amd.optim.fused import FusedOptimizer
 from homebrewnlp_mtf_amd.optim.reference import ReferenceOptimizer
 
@@ -28,8 +29,17 @@ def _pair(cfg, cuda):
     return m_cpu, m_gpu
 
 
-@pytest.mark.parametrize("variant", ["gpt", "gpt_d96", "revnet", "mixer"])
-def test_model_forward_backward(cuda, variant):
+@pytest.mark.parametrize("variant", ["gpt", "gpt_d96", "revnet", "mixer", "mixer_unfused"])
+def test_model_forward_backward(cuda, variant, monkeypatch):
+    """GPU model vs the fp32 CPU oracle. "mixer": the ctx32_mixer block pair under RevNet, whose stream updates ride
+    in the blocks' last GEMMs (F.StreamSink: the bottleneck out-projection and the token mixer) and whose stream
+    gradients ride in the opening norms' backward (F.GradSink) -- no mix_f32 pass; "mixer_unfused": the same with the
+    separate mix_f32 passes"""
+    from homebrewnlp_mtf_amd.models import reversible
+    mixes = []
+    real_mix = raw.mix_f32
+    monkeypatch.setattr(raw, "mix_f32", lambda *a, **k: (mixes.append(1), real_mix(*a, **k))[1])
+    monkeypatch.setattr(reversible, "_REV_FUSE", variant != "mixer_unfused")
     cfg = dict(GPT)
     if variant == "gpt_d96":     # GPT-Neo 20B-scale head dim
         cfg.update(features_per_head=96)
@@ -37,7 +47,7 @@ def test_model_forward_backward(cuda, variant):
         cfg.update(memory_reduction_strategy="revnet",
                    block_config=[{"layer": ["norm-shift-scale", "attention-dot_product-context"]},
                                  {"layer": ["norm-shift-scale-group", "feed_forward-in:relu"]}])
-    if variant == "mixer":
+    if variant.startswith("mixer"):
         cfg.update(memory_reduction_strategy="revnet", intermediate_feed_forward_multiplier=None,
                    block_config=[{"layer": ["norm-shift-scale-features-group",
                                             "bottleneck_group_linear-in:relu-mid:relu-mid:norm-mid:shift-mid:"
@@ -65,6 +75,11 @@ def test_model_forward_backward(cuda, variant):
         # reversible bodies reconstruct activations in bf16 (as the reference does): drift grows towards the input
         tol = 0.08 if variant.startswith("gpt") else 0.2
         assert rel < tol, f"{variant}: gradient of {name} off by {rel:.3f} (|g|={denom:.3g})"
+    if variant.startswith("mixer"):
+        nblk = 2 * cfg.get("depth", GPT.get("depth", 2))
+        # fused: the forward and reconstruction updates in the GEMMs, the gradient sums in the opening norms'
+        # backward -- no mix_f32 pass at all; unfused: three per block
+        assert len(mixes) == (0 if variant == "mixer" else 3 * nblk), (variant, len(mixes), nblk)
 
 
 @pytest.mark.parametrize("chain", ["adaptive_clip:0.003-sm3-momentum:0.9:1:1-learning_rate", "adam-learning_rate",
