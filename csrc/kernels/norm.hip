@@ -94,11 +94,13 @@ __device__ __forceinline__ void load_row(const bf16_t* x, int F, int sl, bool ok
 // The host sizes the grid so that the rows of one lane group (row, row + nw, ...) all belong to one parameter group
 // (nw % groups == 0): scale / shift are loaded into registers once, not re-fetched per row (with 256-wide group rows
 // the per-row parameter loads were 4x the row's own bytes)
-template <int NCH, int LPR>
-__global__ __launch_bounds__(NTH) void norm_fwd_kernel(const bf16_t* __restrict__ X, const float* __restrict__ scale,
-                                                       const float* __restrict__ shift, bf16_t* __restrict__ Y,
-                                                       float* __restrict__ rstd_out, long long rows, int F,
-                                                       int groups, float eps, const float* __restrict__ ext_stats) {
+// ACT: a following activation layer fused (Y = act(z)); its own instantiation, the plain kernel keeps its registers
+template <int NCH, int LPR, int AK>   // AK: 0 plain, > 0 that activation (compile-time), -1 the runtime `act`
+__device__ __forceinline__ void norm_fwd_body(const bf16_t* __restrict__ X, const float* __restrict__ scale,
+                                              const float* __restrict__ shift, bf16_t* __restrict__ Y,
+                                              float* __restrict__ rstd_out, long long rows, int F,
+                                              int groups, float eps, const float* __restrict__ ext_stats,
+                                              int act) {
   constexpr int RPW = 64 / LPR;
   constexpr int U = 1;   // (2-4 rows in flight per lane group measured 2 % slower than 1)
   const int lane = threadIdx.x & 63, sub = lane / LPR, sl = lane % LPR;
@@ -159,12 +161,33 @@ __global__ __launch_bounds__(NTH) void norm_fwd_kernel(const bf16_t* __restrict_
           float y0 = (v[c][2 * j] - mean) * rstd, y1 = (v[c][2 * j + 1] - mean) * rstd;
           if (scale) { y0 *= sc[c][2 * j]; y1 *= sc[c][2 * j + 1]; }
           if (shift) { y0 += sh[c][2 * j]; y1 += sh[c][2 * j + 1]; }
+          if constexpr (AK != 0) {   // the following activation layer
+            y0 = act_fwd(AK > 0 ? AK : act, y0);
+            y1 = act_fwd(AK > 0 ? AK : act, y1);
+          }
           o[j] = pack_bf16x2(y0, y1);
         }
         *reinterpret_cast<uint4*>(Y + row * F + col) = make_uint4(o[0], o[1], o[2], o[3]);
       }
     }
   }
+}
+
+#define NORM_FWD_PARAMS                                                                                       \
+  const bf16_t *__restrict__ X, const float *__restrict__ scale, const float *__restrict__ shift,             \
+      bf16_t *__restrict__ Y, float *__restrict__ rstd_out, long long rows, int F, int groups, float eps,     \
+      const float *__restrict__ ext_stats, int act
+template <int NCH, int LPR>
+__global__ __launch_bounds__(NTH) void norm_fwd_kernel(NORM_FWD_PARAMS) {
+  norm_fwd_body<NCH, LPR, 0>(X, scale, shift, Y, rstd_out, rows, F, groups, eps, ext_stats, act);
+}
+template <int NCH, int LPR>
+__global__ __launch_bounds__(NTH) void norm_fwd_act_kernel(NORM_FWD_PARAMS) {
+  norm_fwd_body<NCH, LPR, -1>(X, scale, shift, Y, rstd_out, rows, F, groups, eps, ext_stats, act);
+}
+template <int NCH, int LPR>
+__global__ __launch_bounds__(NTH) void norm_fwd_gelu_kernel(NORM_FWD_PARAMS) {
+  norm_fwd_body<NCH, LPR, ACT_GELU>(X, scale, shift, Y, rstd_out, rows, F, groups, eps, ext_stats, act);
 }
 
 // row partial sums for the TP path: out[row] = (sum x, sum x^2) over this rank's slice
@@ -207,6 +230,27 @@ __device__ __forceinline__ void scale8(int c, int sl, int F, bool ok, long long 
   }
 }
 
+// dy of a norm whose output went through a fused activation: dy * act'(z), z = xh * scale + shift recomputed
+template <int LPR, int AK, bool HSH>
+__device__ __forceinline__ void act_dy8(int c, int sl, int F, bool ok, long long poff, const float* __restrict__ scale,
+                                        const float* __restrict__ shift, int act, float mean, float rstd,
+                                        const float (&gsc)[8], const float (&hsh)[8], const float (&x)[8],
+                                        float (&dy)[8]) {
+  const int col0 = c * LPR * 8 + sl * 8;
+  float b[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if constexpr (HSH) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) b[j] = hsh[j];
+  } else {
+    if (shift && ok && col0 < F) load8f(shift + poff + col0, b);
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float z = (x[j] - mean) * rstd * (scale ? gsc[j] : 1.f) + b[j];
+    dy[j] *= act_grad(AK > 0 ? AK : act, z);
+  }
+}
+
 // backward. stats = (mean, rstd) per row. If `partial_out` is set, only writes per-row partial
 // (sum dxh, sum dxh*xh) for the TP all-reduce and returns (phase 1); with `ext_dsum` (phase 2) uses them.
 // Parameter gradients: per-lane register sums; the host sizes the grid so that (rows per grid step) % groups == 0,
@@ -227,7 +271,9 @@ __device__ __forceinline__ uint32_t pk2(float lo, float hi) {
 
 // F32R: the RevNet stream form (fp32 gradient R32 added, dx written in fp32 to DX32 and as its bf16 copy to DX) --
 // its own instantiation, so the plain kernel keeps its register budget
-template <int NCH, int LPR, bool F32R>
+// ACTF: the norm's output went through a fused activation (forward Y = act(z), z = xh * scale + shift): dy is taken
+// through act'(z) first, z recomputed from the row statistics and the parameters (its own instantiation)
+template <int NCH, int LPR, bool F32R, int AK>   // AK: 0 plain, > 0 that fused activation, -1 the runtime `act`
 __device__ __forceinline__ void norm_bwd_body(const bf16_t* __restrict__ X, const bf16_t* __restrict__ DY,
                                                        const float* __restrict__ scale, const float* __restrict__ stats,
                                                        bf16_t* __restrict__ DX, float* __restrict__ dscale,
@@ -235,8 +281,10 @@ __device__ __forceinline__ void norm_bwd_body(const bf16_t* __restrict__ X, cons
                                                        int Ffull, float* __restrict__ partial_out,
                                                        const float* __restrict__ ext_dsum,
                                                        const bf16_t* __restrict__ R, float* __restrict__ ws,
-                                                       const float* __restrict__ R32, float* __restrict__ DX32) {
+                                                       const float* __restrict__ R32, float* __restrict__ DX32,
+                                                       const float* __restrict__ shift, int act, int in_relu) {
   constexpr int RPW = 64 / LPR;
+  constexpr bool ACTF = AK != 0;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* red_s = reinterpret_cast<float*>(smem);           // [4 waves][F] dscale partials, then dshift
   // wide rows, one parameter group: scale staged once in LDS behind the reduction scratch (row reads by ds_read)
@@ -269,6 +317,18 @@ __device__ __forceinline__ void norm_bwd_body(const bf16_t* __restrict__ X, cons
     for (int c = 0; c < (HOIST ? NCH : 1); ++c) {
       const int col0 = c * LPR * 8 + sl * 8;
       if (col0 < F) load8f(scale + (long long)(rbase % groups) * F + col0, hsc[c]);
+    }
+  }
+  // the fused activation's shift, hoisted the same way (narrow rows)
+  constexpr bool HSH = ACTF && HOIST;
+  float hsh[HSH ? NCH : 1][8];
+  if constexpr (HSH) {
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) hsh[c][j] = 0.f;
+      const int col0 = c * LPR * 8 + sl * 8;
+      if (shift && col0 < F) load8f(shift + (long long)(rbase % groups) * F + col0, hsh[c]);
     }
   }
 #pragma unroll
@@ -308,6 +368,13 @@ __device__ __forceinline__ void norm_bwd_body(const bf16_t* __restrict__ X, cons
       scale8<NCH, LPR, HOIST>(c, sl, F, ok, poff, scale, sc_lds, sc_s, hsc, gsc);
       unpack8(cx[c], x);
       unpack8(cd[c], dy);
+      if constexpr (ACTF) {
+        if (AK > 0 || act) {
+          // dy through act'(z) once: pass 2 reads the product back from cd (bf16, as the separate pass stored it)
+          act_dy8<LPR, AK, HSH>(c, sl, F, ok, poff, scale, shift, act, mean, rstd, gsc, hsh[HSH ? c : 0], x, dy);
+          cd[c] = make_uint4(pk2(dy[0], dy[1]), pk2(dy[2], dy[3]), pk2(dy[4], dy[5]), pk2(dy[6], dy[7]));
+        }
+      }
       const int col0 = c * LPR * 8 + sl * 8;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -365,7 +432,14 @@ __device__ __forceinline__ void norm_bwd_body(const bf16_t* __restrict__ X, cons
         const float g0 = scale ? gsc[j0] : 1.f, g1 = scale ? gsc[j1] : 1.f;
         const float xh0 = (x[j0] - mean) * rstd, xh1 = (x[j1] - mean) * rstd;
         const float d0 = dy[j0] * g0, d1 = dy[j1] * g1;
-        o[j] = pk2(rstd * (d0 - m1 - xh0 * m2) + r[j0], rstd * (d1 - m1 - xh1 * m2) + r[j1]);
+        float v0 = rstd * (d0 - m1 - xh0 * m2) + r[j0], v1 = rstd * (d1 - m1 - xh1 * m2) + r[j1];
+        if constexpr (ACTF) {
+          if (in_relu) {   // the norm's input was relu(z): dz = dx * [x > 0] (the producing GEMM skips its pass)
+            v0 = x[j0] > 0.f ? v0 : 0.f;
+            v1 = x[j1] > 0.f ? v1 : 0.f;
+          }
+        }
+        o[j] = pk2(v0, v1);
       }
       *reinterpret_cast<uint4*>(DX + row * F + col) = make_uint4(o[0], o[1], o[2], o[3]);
     }
@@ -417,17 +491,29 @@ __device__ __forceinline__ void norm_bwd_body(const bf16_t* __restrict__ X, cons
       const float *__restrict__ stats, bf16_t *__restrict__ DX, float *__restrict__ dscale,                    \
       float *__restrict__ dshift, long long rows, int F, int groups, int Ffull, float *__restrict__ partial_out, \
       const float *__restrict__ ext_dsum, const bf16_t *__restrict__ R, float *__restrict__ ws,               \
-      const float *__restrict__ R32, float *__restrict__ DX32
-#define NORM_BWD_ARGS X, DY, scale, stats, DX, dscale, dshift, rows, F, groups, Ffull, partial_out, ext_dsum, R, ws, R32, DX32
+      const float *__restrict__ R32, float *__restrict__ DX32, const float *__restrict__ shift, int act, int in_relu
+#define NORM_BWD_ARGS \
+  X, DY, scale, stats, DX, dscale, dshift, rows, F, groups, Ffull, partial_out, ext_dsum, R, ws, R32, DX32, shift, act, \
+      in_relu
 
 template <int NCH, int LPR>
 __global__ __launch_bounds__(NTH, bwd_blocks_per_cu<NCH>()) void norm_bwd_kernel(NORM_BWD_PARAMS) {
-  norm_bwd_body<NCH, LPR, false>(NORM_BWD_ARGS);
+  norm_bwd_body<NCH, LPR, false, 0>(NORM_BWD_ARGS);
 }
 
 template <int NCH, int LPR>
 __global__ __launch_bounds__(NTH, bwd_blocks_per_cu<NCH>()) void norm_bwd32_kernel(NORM_BWD_PARAMS) {
-  norm_bwd_body<NCH, LPR, true>(NORM_BWD_ARGS);
+  norm_bwd_body<NCH, LPR, true, 0>(NORM_BWD_ARGS);
+}
+
+template <int NCH, int LPR>
+__global__ __launch_bounds__(NTH, bwd_blocks_per_cu<NCH>()) void norm_bwd_act_kernel(NORM_BWD_PARAMS) {
+  norm_bwd_body<NCH, LPR, false, -1>(NORM_BWD_ARGS);
+}
+
+template <int NCH, int LPR>
+__global__ __launch_bounds__(NTH, bwd_blocks_per_cu<NCH>()) void norm_bwd_gelu_kernel(NORM_BWD_PARAMS) {
+  norm_bwd_body<NCH, LPR, false, ACT_GELU>(NORM_BWD_ARGS);
 }
 
 // deterministic fold of the parameter-gradient slab: out[g][f] += sum over partial rows p = g, g + period, ... (in
@@ -488,6 +574,8 @@ struct ObstNormDesc {
   float* ws;                          // backward with parameter gradients: obst_norm_bwd_ws(desc) floats
   const float* R32;                   // backward: fp32 gradient added to DX (the RevNet stream gradient) or null
   float* DX32;                        // backward with R32: DX in fp32 (DX then holds its bf16 copy)
+  int act;                            // a following activation fused: forward Y = act(norm), backward dy *= act'(z)
+  int in_relu;                        // backward: the input was relu(z) of the producing GEMM, dx *= [x > 0]
 };
 
 #define NORM_DISPATCH_L(KERNEL, LPR, GRID, LDSB, ...)                                               \
@@ -524,9 +612,15 @@ static int group_aligned(int grid, int groups, int F) {
 
 OBST_API int obst_norm_fwd(const ObstNormDesc* d, hipStream_t st) {
   if (d->F % 8 || d->rows <= 0) return -1;
-  NORM_DISPATCH(norm_fwd_kernel, dim3(group_aligned(grid_for(d->rows), d->groups, d->F)), 0, (const bf16_t*)d->X,
-                d->scale, d->shift, (bf16_t*)d->Y,
-                d->stats, d->rows, d->F, d->groups, d->eps, d->ext);
+  if (d->act == ACT_GELU)
+    NORM_DISPATCH(norm_fwd_gelu_kernel, dim3(group_aligned(grid_for(d->rows), d->groups, d->F)), 0, (const bf16_t*)d->X,
+                  d->scale, d->shift, (bf16_t*)d->Y, d->stats, d->rows, d->F, d->groups, d->eps, d->ext, d->act);
+  else if (d->act)
+    NORM_DISPATCH(norm_fwd_act_kernel, dim3(group_aligned(grid_for(d->rows), d->groups, d->F)), 0, (const bf16_t*)d->X,
+                  d->scale, d->shift, (bf16_t*)d->Y, d->stats, d->rows, d->F, d->groups, d->eps, d->ext, d->act);
+  else
+    NORM_DISPATCH(norm_fwd_kernel, dim3(group_aligned(grid_for(d->rows), d->groups, d->F)), 0, (const bf16_t*)d->X,
+                  d->scale, d->shift, (bf16_t*)d->Y, d->stats, d->rows, d->F, d->groups, d->eps, d->ext, d->act);
   return (int)hipGetLastError();
 }
 
@@ -565,21 +659,22 @@ OBST_API long long obst_norm_bwd_ws(const ObstNormDesc* d) {
 
 OBST_API int obst_norm_bwd(const ObstNormDesc* d, hipStream_t st) {
   if (d->F % 8 || d->rows <= 0) return -1;
-  if ((d->R && d->R32) || (d->DX32 && !d->R32)) return -4;
+  if ((d->R && d->R32) || (d->DX32 && !d->R32) || ((d->act || d->in_relu) && d->R32)) return -4;
   const bool params = norm_bwd_params(d);
   if (params && !d->ws) return -3;
   // reduction scratch [8][LPR*8] floats (<= 16 KiB), plus the staged scale ([F] floats) for wide rows
   const int nch = (d->F + lanes_per_row(d->F) * 8 - 1) / (lanes_per_row(d->F) * 8);
   const size_t lds = (size_t)8 * lanes_per_row(d->F) * 8 * 4 + (nch > 2 && d->scale && d->groups == 1 ? d->F * 4 : 0);
   const int grid = norm_bwd_grid(d);
-  if (d->R32)
-    NORM_DISPATCH(norm_bwd32_kernel, dim3(grid), lds, (const bf16_t*)d->X, (const bf16_t*)d->DY, d->scale, d->stats,
-                  (bf16_t*)d->DX, d->dscale, d->dshift, d->rows, d->F, d->groups, d->Ffull, d->partial, d->ext,
-                  (const bf16_t*)d->R, d->ws, d->R32, d->DX32);
-  else
-    NORM_DISPATCH(norm_bwd_kernel, dim3(grid), lds, (const bf16_t*)d->X, (const bf16_t*)d->DY, d->scale, d->stats,
-                  (bf16_t*)d->DX, d->dscale, d->dshift, d->rows, d->F, d->groups, d->Ffull, d->partial, d->ext,
-                  (const bf16_t*)d->R, d->ws, d->R32, d->DX32);
+#define NORM_BWD_LAUNCH(KERNEL)                                                                                  \
+  NORM_DISPATCH(KERNEL, dim3(grid), lds, (const bf16_t*)d->X, (const bf16_t*)d->DY, d->scale, d->stats,           \
+                (bf16_t*)d->DX, d->dscale, d->dshift, d->rows, d->F, d->groups, d->Ffull, d->partial, d->ext,   \
+                (const bf16_t*)d->R, d->ws, d->R32, d->DX32, d->shift, d->act, d->in_relu)
+  if (d->R32) NORM_BWD_LAUNCH(norm_bwd32_kernel);
+  else if (d->act == ACT_GELU) NORM_BWD_LAUNCH(norm_bwd_gelu_kernel);
+  else if (d->act || d->in_relu) NORM_BWD_LAUNCH(norm_bwd_act_kernel);
+  else NORM_BWD_LAUNCH(norm_bwd_kernel);
+#undef NORM_BWD_LAUNCH
   if (params) {
     const long long parts = d->groups > 1 ? (long long)grid * 4 * (64 / lanes_per_row(d->F)) : grid;
     const long long nout = 2LL * d->groups * d->F;

@@ -167,6 +167,8 @@ class BlockArgs:
         self.residual: typing.Optional[Act] = None  # set by the frontend for fusable last layers of skip blocks
         self.stream_sink = None  # RevNet: the block's last layer may fuse the fp32 stream update (F.StreamSink)
         self.grad_sink = None    # RevNet: the block's opening norm may fuse the fp32 stream gradient (F.GradSink)
+        self.fused_act = None    # norm followed by an activation layer: applied in the norm kernel
+        self.fused_act_done = False
 
     def __call__(self, *args) -> "BlockArgs":
         new = BlockArgs(self.builder, self.tensor, self.name_extras[:], self.is_last)

@@ -28,6 +28,7 @@ def run_layers(builder: Builder, layers: typing.List[str], x: Act, residual: typ
     if (residual is not None and residual is x and n > 1 and layers[0].split('-')[0] == "norm"
             and layers[-1].split('-')[0] in _FUSABLE_LAST):
         carrier = F.ResidualGrad()
+    skip_act = False
     for idx, layer in enumerate(layers, 1):
         name, *extras = layer.split('-')
         if name not in LAYER_FUNCTIONS:
@@ -46,10 +47,27 @@ def run_layers(builder: Builder, layers: typing.List[str], x: Act, residual: typ
             args.stream_sink = stream_sink   # consumed (sink.out32 set) only by a layer that can fuse it
         if idx == 1 and grad_sink is not None and name == "norm":
             args.grad_sink = grad_sink       # the norm on the block input itself
+        if name == "norm" and idx < n:
+            args.fused_act = _fusable_act(layers[idx])
         with builder.scope(name + '_'):
-            out = LAYER_FUNCTIONS[name](args)
+            if skip_act:                     # applied by the preceding norm's kernel (variable-free layer)
+                skip_act = False
+            else:
+                out = LAYER_FUNCTIONS[name](args)
+        skip_act = getattr(args, "fused_act_done", False)
         consumed = consumed or getattr(args, "residual_consumed", False)
     return out, consumed
+
+
+def _fusable_act(layer: str) -> typing.Optional[str]:
+    """the activation of an `activation-<act>` layer that the norm kernels can apply (and differentiate) in place"""
+    from ..ops import raw
+    name, *extras = layer.split('-')
+    if name != "activation":
+        return None
+    from .layers import ACTIVATIONS
+    act = next((a for a in extras if a in ACTIVATIONS), None)
+    return act if act in raw.ACTS and raw.ACTS[act] != 0 else None
 
 
 def block_body(builder: Builder, config: BlockConfig, x: Act, stream_sink=None, grad_sink=None) -> Act:

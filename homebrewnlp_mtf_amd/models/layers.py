@@ -88,7 +88,7 @@ def anonymize(a: Act, dim: Dim) -> Act:
 # ================================================================================================================
 # linear (ref backend.py:108-118, basic.py:33-34)
 def linear(args: BlockArgs, old: typing.List[Dim], new: typing.List[Dim], act: typing.Optional[str] = None,
-           sink=None) -> Act:
+           sink=None, relu_grad=None) -> Act:
     x = args.tensor
     w = _scoped(args, "linear", orthogonal_var, args, list(old) + list(new), list(old))
     wdims = D.deduplicate(list(old) + list(new))
@@ -102,7 +102,7 @@ def linear(args: BlockArgs, old: typing.List[Dim], new: typing.List[Dim], act: t
         if act and plan.row_parallel and tp:   # all-reduce must precede the activation
             y = F.activation(F.linear(x.t, w, x.dims, wdims, odims), act)
         else:
-            y = F.linear(x.t, w, x.dims, wdims, odims, act=act, sink=sink)
+            y = F.linear(x.t, w, x.dims, wdims, odims, act=act, sink=sink, relu_grad=relu_grad)
         return Act(y, odims)
     hd = args.params.head_dim
     xt = x.t
@@ -197,10 +197,14 @@ def activated_linear(args: BlockArgs, prefix: str) -> Act:
         # the block's last product: the RevNet stream update rides in its epilogue (F.StreamSink)
         old, new = D.linear_shapes(args.params, args, args.tensor.dims)
         return linear(args, old, new, sink=sink)
+    # a relu product straight into a norm: the norm's backward applies relu' (F.ReluGrad)
+    rg = (F.ReluGrad() if act == "relu" and 'norm' in args and _plain([a for a in args if a != 'norm'])
+          else None)
     if ff is wrapped_linear and act is not None and act != "mtf_mish":
         old, new = D.linear_shapes(args.params, args, args.tensor.dims)
-        out = linear(args, old, new, act=act)   # activation fused into the GEMM epilogue
+        out = linear(args, old, new, act=act, relu_grad=rg)   # activation fused into the GEMM epilogue
     else:
+        rg = None
         out = activate(args(ff(args)))
     out = dropout(args(out))
     if 'glu' in args or 'glu_add' in args:
@@ -210,7 +214,7 @@ def activated_linear(args: BlockArgs, prefix: str) -> Act:
         extra = activate(args(ff(args)))
         out = Act(F.add(out.t, extra.t), out.dims)
     if 'norm' in args:
-        out = norm(args(out))
+        out = norm(args(out), relu_grad=rg)
     return out
 
 
@@ -388,7 +392,7 @@ def bottleneck_group_linear(args: BlockArgs) -> Act:
 NORM_ANY_LAYOUT = True
 
 
-def norm(args: BlockArgs, feature_shape: typing.Optional[typing.List[Dim]] = None) -> Act:
+def norm(args: BlockArgs, feature_shape: typing.Optional[typing.List[Dim]] = None, relu_grad=None) -> Act:
     p = args.params
     x = args.tensor
     feature_shape = list(D.linear_shapes(p, args, x.dims).old if feature_shape is None else feature_shape)
@@ -405,8 +409,11 @@ def norm(args: BlockArgs, feature_shape: typing.Optional[typing.List[Dim]] = Non
         Fsz = int(math.prod(d.size for d in normalized))
         groups = p.head_dim.size if group else 1
         tp_stats = (not group) and p.head_dim in normalized and pstate.tp_size() > 1
+        act = getattr(args, "fused_act", None) if not tp_stats else None
         y = F.norm(x.t, scale, shift, Fsz, groups, tp_stats=tp_stats,
-                   carrier=getattr(args, "norm_carrier", None), grad_sink=getattr(args, "grad_sink", None))
+                   carrier=getattr(args, "norm_carrier", None), grad_sink=getattr(args, "grad_sink", None), act=act,
+                   relu_grad=relu_grad)
+        args.fused_act_done = act is not None   # the frontend then skips the activation layer's own pass
         return Act(y, x.dims)
     # any other layout: permute to [others..., group?, normalized...] (row % groups = the group index), the same
     # kernel, permute back; parameters are permuted copies to [group?, normalized...] (their gradients flow back

@@ -65,7 +65,7 @@ class NormDesc(ctypes.Structure):
     _fields_ = [("X", c_p), ("scale", c_p), ("shift", c_p), ("Y", c_p), ("stats", c_p),
                 ("DY", c_p), ("DX", c_p), ("dscale", c_p), ("dshift", c_p), ("partial", c_p), ("ext", c_p),
                 ("rows", c_ll), ("F", c_i), ("groups", c_i), ("Ffull", c_i), ("eps", c_f), ("R", c_p), ("ws", c_p),
-                ("R32", c_p), ("DX32", c_p)]
+                ("R32", c_p), ("DX32", c_p), ("act", c_i), ("in_relu", c_i)]
 
 
 class EwDesc(ctypes.Structure):

@@ -237,9 +237,20 @@ class StreamSink:
         return y16
 
 
+class ReluGrad:
+    """A relu-activated product whose output feeds a norm: the norm backward multiplies its dx by [x > 0] (x = the
+    relu output it normalised, so that is relu'(z)) and marks ``applied``; the product's backward (which runs after)
+    then takes that gradient as dz and skips its own activation-backward pass."""
+    __slots__ = ("applied",)
+
+    def __init__(self):
+        self.applied = False
+
+
 class _Linear(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, plan: LinearPlan, act, sink: typing.Optional[StreamSink] = None):
+    def forward(ctx, x, w, plan: LinearPlan, act, sink: typing.Optional[StreamSink] = None,
+                relu_grad: typing.Optional[ReluGrad] = None):
         xc = x.permute(plan.x_perm).contiguous() if plan.x_perm is not None else x.contiguous()
         z = _empty(plan.canon_o_shape, xc) if act else None
         if plan.row_parallel and pstate.tp_size() > 1:
@@ -256,6 +267,7 @@ class _Linear(torch.autograd.Function):
             _fwd_gemm(xc, w, y, plan, act=act, Zout=z)
         ctx.save_for_backward(xc, w, z)
         ctx.plan, ctx.act = plan, act
+        ctx.relu_grad = relu_grad if act == "relu" else None
         if plan.o_perm is not None:
             y = y.permute(plan.o_perm)
         return y
@@ -268,10 +280,11 @@ class _Linear(torch.autograd.Function):
             inv = [plan.o_perm.index(i) for i in range(len(plan.o_perm))]
             dy = dy.permute(inv)
         dy = dy.contiguous()
-        if act:
+        if act and not (ctx.relu_grad is not None and ctx.relu_grad.applied):
             dz = torch.empty_like(dy)
             raw.elementwise("act_bwd", z, dz, z=dy, act=act)
             dy = dz
+        ctx.relu_grad = None
         dx = None
         pending = pstate._DONE
         if ctx.needs_input_grad[0]:
@@ -286,13 +299,14 @@ class _Linear(torch.autograd.Function):
         _wgrad_gemm(xc, dy, gw, plan, beta=beta)
         _done(w)
         pending.wait()
-        return dx, (None if is_main else gw.to(w.dtype)), None, None, None
+        return dx, (None if is_main else gw.to(w.dtype)), None, None, None, None
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, xdims: DimList, wdims: DimList, odims: DimList,
-           act: typing.Optional[str] = None, sink: typing.Optional[StreamSink] = None) -> torch.Tensor:
+           act: typing.Optional[str] = None, sink: typing.Optional[StreamSink] = None,
+           relu_grad: typing.Optional[ReluGrad] = None) -> torch.Tensor:
     plan = linear_plan(tuple(xdims), tuple(wdims), tuple(odims))
-    return _Linear.apply(x, w, plan, act, sink)
+    return _Linear.apply(x, w, plan, act, sink, relu_grad)
 
 
 class _TPReduce(torch.autograd.Function):
@@ -854,7 +868,7 @@ class GradSink:
 
 class _Norm(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, scale, shift, F, groups, tp_stats, carrier=None, grad_sink=None):
+    def forward(ctx, x, scale, shift, F, groups, tp_stats, carrier=None, grad_sink=None, act=None, relu_grad=None):
         xc = x.contiguous()
         rows = xc.numel() // F
         y = torch.empty_like(xc)
@@ -872,8 +886,12 @@ class _Norm(torch.autograd.Function):
             mean = p[:, 0] / Ffull
             var = (p[:, 1] / Ffull - mean * mean).clamp_min(0)
             ext = torch.stack([mean, torch.rsqrt(var + raw.EPS)], -1).reshape(-1).contiguous()
-        raw.norm_fwd(xc, sm32, sh32, y, stats, rows, F, groups, ext_stats=ext)
+        if act is not None and ext is not None:
+            raise NotImplementedError("activation fused into a TP-statistics norm")
+        raw.norm_fwd(xc, sm32, sh32, y, stats, rows, F, groups, ext_stats=ext, act=act)
         ctx.save_for_backward(xc, scale, shift, stats)
+        ctx.act, ctx.sh32 = act, sh32
+        ctx.relu_grad = relu_grad if ext is None else None
         ctx.cfg = (F, groups, rows, Ffull, tp_stats)
         ctx.sm32 = sm32
         ctx.carrier = carrier
@@ -899,7 +917,15 @@ class _Norm(torch.autograd.Function):
             R = ctx.carrier.grad.contiguous()
             ctx.carrier.grad = None
         sink = ctx.grad_sink
-        if sink is not None and R is None and ext is None and sink.usable(xc):
+        rg = ctx.relu_grad
+        ctx.relu_grad = None
+        if ctx.act is not None or (rg is not None and ext is None):
+            # the fused activation (dy through act'(z)) and / or the producer's relu (dx * [x > 0]) in the kernel
+            raw.norm_bwd(xc, dy, ctx.sm32, stats, dx, gsc, gsh, rows, F, groups, Ffull, R=R, shift=ctx.sh32,
+                         act=ctx.act, in_relu=rg is not None)
+            if rg is not None:
+                rg.applied = True
+        elif sink is not None and R is None and ext is None and sink.usable(xc):
             dx32 = torch.empty(xc.shape, dtype=torch.float32, device=xc.device)
             raw.norm_bwd(xc, dy, ctx.sm32, stats, dx, gsc, gsh, rows, F, groups, Ffull, R32=sink.g32, dx32=dx32)
             sink.out32, sink.ptr = dx32, dx.data_ptr()
@@ -910,12 +936,15 @@ class _Norm(torch.autograd.Function):
             if t is not None:
                 _done(t)
         return (dx, None if msc else gsc.view(scale.shape).to(scale.dtype),
-                None if msh else gsh.view(shift.shape).to(shift.dtype), None, None, None, None, None)
+                None if msh else gsh.view(shift.shape).to(shift.dtype), None, None, None, None, None, None, None)
 
 
 def norm(x, scale, shift, F: int, groups: int, tp_stats: bool = False, carrier: typing.Optional[ResidualGrad] = None,
-         grad_sink: typing.Optional[GradSink] = None):
-    return _Norm.apply(x, scale, shift, F, groups, tp_stats, carrier, grad_sink)
+         grad_sink: typing.Optional[GradSink] = None, act: typing.Optional[str] = None,
+         relu_grad: typing.Optional[ReluGrad] = None):
+    """act: the activation layer that follows the norm, applied in the norm kernel (and its derivative in the norm's
+    backward, from z recomputed out of the row statistics) instead of two elementwise passes"""
+    return _Norm.apply(x, scale, shift, F, groups, tp_stats, carrier, grad_sink, act, relu_grad)
 
 
 # ================================================================================================================

@@ -446,7 +446,9 @@ def attn_map_bwd(q, k, v, o, do, lse, delta, dq, dk, dv, bias, cmap, dbias, dcma
 EPS = 1e-5
 
 
-def norm_fwd(x, scale, shift, y, stats, rows: int, F: int, groups: int, ext_stats=None):
+def norm_fwd(x, scale, shift, y, stats, rows: int, F: int, groups: int, ext_stats=None, act=None):
+    """y = norm(x) * scale + shift per row (groups: row % groups selects the parameter row); act: a following
+    activation fused, y = act(...)"""
     if x.device.type == "meta":
         return None
     if on_gpu(x):
@@ -462,6 +464,7 @@ def norm_fwd(x, scale, shift, y, stats, rows: int, F: int, groups: int, ext_stat
                 _need(t, groups * F - 1, nm)
         d = L.NormDesc(x.data_ptr(), L.ptr(scale), L.ptr(shift), y.data_ptr(), L.ptr(stats), 0, 0, 0, 0, 0,
                        L.ptr(ext_stats), rows, F, groups, F, EPS)
+        d.act = ACTS[act]
         L.check(L.lib().obst_norm_fwd(d, L.stream_ptr()), "norm_fwd")
         return
     xv = _f(x.reshape(rows, F))
@@ -476,7 +479,7 @@ def norm_fwd(x, scale, shift, y, stats, rows: int, F: int, groups: int, ext_stat
         out = out * scale.reshape(groups, F)[g]
     if shift is not None:
         out = out + shift.reshape(groups, F)[g]
-    y.reshape(rows, F).copy_(out)
+    y.reshape(rows, F).copy_(act_fwd_t(act, out))
     if stats is not None:
         stats.view(rows, 2).copy_(torch.cat([mean, rstd], -1))
 
@@ -496,11 +499,13 @@ def norm_partial(x, out, rows: int, F: int):
 
 
 def norm_bwd(x, dy, scale, stats, dx, dscale, dshift, rows: int, F: int, groups: int, Ffull: int = 0,
-             partial=None, ext_dsum=None, R=None, R32=None, dx32=None):
+             partial=None, ext_dsum=None, R=None, R32=None, dx32=None, shift=None, act=None, in_relu=False):
     """dx (and parameter grads accumulated into fp32 dscale/dshift). With `partial` set, only the per-row partial
     sums (sum dxh, sum dxh*xh) are written (TP phase 1); phase 2 passes them back as `ext_dsum`. R (same layout as
     dx) is added to dx. R32 / dx32 (fp32, together, instead of R): dx32 = dx + R32 in fp32 and dx its bf16 copy (the
-    RevNet stream gradient, F.GradSink)."""
+    RevNet stream gradient, F.GradSink). act (with the forward's shift): the norm's output went through that
+    activation, dy is taken through act'(z) first (z recomputed from x, stats, scale, shift). in_relu: x was the
+    relu output of the producing product, dx *= [x > 0] (that product's activation backward)."""
     if x.device.type == "meta":
         return None
     Ffull = Ffull or F
@@ -517,8 +522,12 @@ def norm_bwd(x, dy, scale, stats, dx, dscale, dshift, rows: int, F: int, groups:
             if R.dtype != torch.bfloat16 or not R.is_contiguous():
                 raise L.KernelError("norm_bwd residual gradient must be contiguous bf16")
             _need(R, rows * F - 1, "R")
-        if (R32 is None) != (dx32 is None) or (R32 is not None and R is not None):
-            raise L.KernelError("norm_bwd: R32 and dx32 come together, without R")
+        if (R32 is None) != (dx32 is None) or (R32 is not None and (R is not None or act is not None or in_relu)):
+            raise L.KernelError("norm_bwd: R32 and dx32 come together, without R or an activation")
+        if act is not None and (partial is not None or ext_dsum is not None):
+            raise L.KernelError("norm_bwd: no fused activation on the TP statistics path")
+        if shift is not None:
+            _need(shift, groups * F - 1, "shift")
         for nm, t in (("R32", R32), ("dx32", dx32)):
             if t is not None:
                 if t.dtype != torch.float32 or not t.is_contiguous():
@@ -527,6 +536,7 @@ def norm_bwd(x, dy, scale, stats, dx, dscale, dshift, rows: int, F: int, groups:
         d = L.NormDesc(x.data_ptr(), L.ptr(scale), 0, 0, stats.data_ptr(), dy.data_ptr(), L.ptr(dx), L.ptr(dscale),
                        L.ptr(dshift), L.ptr(partial), L.ptr(ext_dsum), rows, F, groups, Ffull, EPS, L.ptr(R))
         d.R32, d.DX32 = L.ptr(R32), L.ptr(dx32)
+        d.shift, d.act, d.in_relu = L.ptr(shift), ACTS[act], int(bool(in_relu))
         nws = int(L.lib().obst_norm_bwd_ws(d))
         ws = torch.empty(max(nws, 1), dtype=torch.float32, device=x.device) if nws else None
         d.ws = L.ptr(ws)     # parameter-gradient partial slab, folded in a fixed order (no float atomics)
@@ -538,6 +548,9 @@ def norm_bwd(x, dy, scale, stats, dx, dscale, dshift, rows: int, F: int, groups:
     xh = (xv - st[:, 0:1]) * st[:, 1:2]
     g = torch.arange(rows, device=x.device) % groups
     gs = _f(scale.reshape(groups, F)[g]) if scale is not None else 1.0
+    if act is not None:
+        z = xh * gs + (_f(shift.reshape(groups, F)[g]) if shift is not None else 0.0)
+        dyv = dyv * act_grad_t(act, z)
     dxh = dyv * gs
     if partial is not None:
         partial.view(rows, 2).copy_(torch.stack([dxh.sum(-1), (dxh * xh).sum(-1)], -1))
@@ -553,6 +566,8 @@ def norm_bwd(x, dy, scale, stats, dx, dscale, dshift, rows: int, F: int, groups:
     out = st[:, 1:2] * (dxh - s1 / Ffull - xh * s2 / Ffull)
     if R is not None:
         out = out + _f(R.reshape(rows, F))
+    if in_relu:
+        out = out * (xv > 0).to(out.dtype)
     if R32 is not None:
         out = out + R32.reshape(rows, F).to(out.dtype)
         dx32.reshape(rows, F).copy_(out)

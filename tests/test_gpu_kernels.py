@@ -258,6 +258,55 @@ def test_norm(cuda, F_, groups, nrows):
         _close(g, c, 3e-2, 2e-2, f"norm F={F_} {name}")
 
 
+@pytest.mark.parametrize("act", ["gelu", "relu", "silu"])
+@pytest.mark.parametrize("F_,groups,nrows", [(256, 8, 300), (2048, 1, 96)])
+def test_norm_with_fused_activation(cuda, F_, groups, nrows, act):
+    """norm + the following activation layer in one kernel (forward y = act(z)); the backward takes dy through
+    act'(z) with z recomputed from the row statistics (its own kernel instantiation) -- against the fp32 oracle"""
+    torch.manual_seed(F_ + len(act))
+    rows = nrows * groups
+    x = (torch.randn(rows * F_) * 2 + 0.3).to(BF)
+    dy = torch.randn(rows * F_).to(BF)
+    sc = torch.randn(groups * F_) * 0.1 + 1
+    sh = torch.randn(groups * F_) * 0.3
+    res = {}
+    for dev in ("cpu", cuda):
+        y = torch.zeros(rows * F_, dtype=BF, device=dev)
+        st = torch.zeros(2 * rows, device=dev)
+        raw.norm_fwd(x.to(dev), sc.to(dev), sh.to(dev), y, st, rows, F_, groups, act=act)
+        dx = torch.zeros(rows * F_, dtype=BF, device=dev)
+        dsc = torch.zeros(groups * F_, device=dev)
+        dsh = torch.zeros(groups * F_, device=dev)
+        raw.norm_bwd(x.to(dev), dy.to(dev), sc.to(dev), st, dx, dsc, dsh, rows, F_, groups, shift=sh.to(dev), act=act)
+        res[str(dev)] = (y, dx, dsc, dsh)
+    torch.cuda.synchronize()
+    for name, g, c in zip(["y", "dx", "dscale", "dshift"], res[str(cuda)], res["cpu"]):
+        _close(g, c, 3e-2, 2e-2, f"norm+{act} F={F_} {name}")
+
+
+@pytest.mark.parametrize("F_,groups,nrows", [(512, 8, 200), (2048, 1, 96)])
+def test_norm_bwd_input_relu_mask(cuda, F_, groups, nrows):
+    """the norm of a relu product: its backward multiplies dx by [x > 0] (F.ReluGrad) in the kernel"""
+    torch.manual_seed(F_ + 1)
+    rows = nrows * groups
+    x = torch.relu(torch.randn(rows * F_) * 2).to(BF)
+    dy = torch.randn(rows * F_).to(BF)
+    sc = torch.randn(groups * F_) * 0.1 + 1
+    res = {}
+    for dev in ("cpu", cuda):
+        y = torch.zeros(rows * F_, dtype=BF, device=dev)
+        st = torch.zeros(2 * rows, device=dev)
+        raw.norm_fwd(x.to(dev), sc.to(dev), None, y, st, rows, F_, groups)
+        dx = torch.full((rows * F_,), float("nan"), dtype=BF, device=dev)
+        dsc = torch.zeros(groups * F_, device=dev)
+        raw.norm_bwd(x.to(dev), dy.to(dev), sc.to(dev), st, dx, dsc, None, rows, F_, groups, in_relu=True)
+        res[str(dev)] = (dx, dsc)
+    torch.cuda.synchronize()
+    for name, g, c in zip(["dx", "dscale"], res[str(cuda)], res["cpu"]):
+        _close(g, c, 3e-2, 2e-2, f"norm in_relu F={F_} {name}")
+    assert torch.all(res[str(cuda)][0].cpu()[x == 0] == 0)
+
+
 @pytest.mark.parametrize("F_,groups,nrows", [(256, 8, 300), (2048, 1, 96), (64, 4, 1000)])
 def test_norm_bwd_fp32_stream_gradient(cuda, F_, groups, nrows):
     """the RevNet stream-gradient form of the norm backward (F.GradSink): dx32 = dx + g32 in fp32 (its own kernel

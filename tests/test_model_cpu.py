@@ -608,3 +608,67 @@ def test_shared_key_value_modes(mixing, monkeypatch):
     a, b = res[(mixing, True)], res[(mixing, False)]
     assert abs(a[0] - b[0]) < 1e-6 and torch.allclose(a[1], b[1], atol=1e-6, rtol=1e-5)
     assert abs(res[(True, False)][0] - res[(False, False)][0]) > 1e-6
+
+
+@pytest.mark.parametrize("act", ["gelu", "relu", "silu"])
+@pytest.mark.parametrize("strategy", ["none", "revnet"])
+def test_norm_activation_fusion_matches_separate_layers(act, strategy, monkeypatch):
+    """a `norm-...` layer followed by `activation-<act>` runs as one norm kernel with the activation (and its
+    derivative, from z recomputed in the backward) fused; same loss and gradients as the two separate layers, and the
+    same variable names (the skipped layer still opens its scope)"""
+    from homebrewnlp_mtf_amd.models import frontend
+    cfg = dict(BASE, memory_reduction_strategy=strategy,
+               block_config=[{"layer": ["norm-shift-scale-features-group", f"activation-{act}",
+                                        "feed_forward-in:relu"]},
+                             {"layer": ["norm-shift-scale", "attention-dot_product-context"]}])
+    x = torch.randint(0, 50, (2, 8, 1), generator=torch.Generator().manual_seed(3))
+    y = torch.randint(0, 50, (2, 8, 1), generator=torch.Generator().manual_seed(4))
+    runs = []
+    for fuse in (True, False):
+        if not fuse:
+            monkeypatch.setattr(frontend, "_fusable_act", lambda layer: None)
+        torch.manual_seed(0)
+        m = Model(ModelParameter(cfg), "cpu")
+        out = m(x, y)
+        out["loss"].backward()
+        m.store.fold_leaf_grads()
+        runs.append((float(out["loss"]), m.store.grad.clone(), list(m.store.order)))
+    (la, ga, na), (lb, gb, nb) = runs
+    assert na == nb
+    assert abs(la - lb) < 1e-5 * max(1.0, abs(la)), (la, lb)
+    assert torch.allclose(ga, gb, rtol=1e-4, atol=1e-6), (ga - gb).abs().max()
+
+
+@pytest.mark.parametrize("strategy", ["none", "revnet"])
+def test_relu_into_norm_gradient_fusion(strategy, monkeypatch):
+    """the bottleneck's relu product feeding its mid norm: the norm backward applies relu' (dx * [x > 0], F.ReluGrad)
+    and the product skips its activation-backward pass -- same gradients as the separate passes"""
+    from homebrewnlp_mtf_amd.ops import functional as Fn
+    cfg = dict(BASE, memory_reduction_strategy=strategy, intermediate_feed_forward_multiplier=None,
+               block_config=[{"layer": ["norm-shift-scale-features-group",
+                                        "bottleneck_group_linear-in:relu-mid:relu-mid:norm-mid:shift-mid:scale-"
+                                        "mid:features"]}])
+    x = torch.randint(0, 50, (2, 8, 1), generator=torch.Generator().manual_seed(5))
+    applied = []
+    real = Fn.ReluGrad
+
+    class Spy(real):
+        __slots__ = ()
+
+        def __setattr__(self, k, v):
+            if k == "applied" and v:
+                applied.append(1)
+            real.__setattr__(self, k, v)
+    runs = []
+    for fuse in (True, False):
+        monkeypatch.setattr(Fn, "ReluGrad", Spy if fuse else (lambda: None))
+        torch.manual_seed(0)
+        m = Model(ModelParameter(cfg), "cpu")
+        out = m(x, x)
+        out["loss"].backward()
+        m.store.fold_leaf_grads()
+        runs.append((float(out["loss"]), m.store.grad.clone()))
+    assert applied, "the norm never applied the relu gradient"
+    (la, ga), (lb, gb) = runs
+    assert abs(la - lb) < 1e-6 * max(1.0, abs(la))
+    assert torch.allclose(ga, gb, rtol=1e-4, atol=1e-6), (ga - gb).abs().max()
