@@ -285,6 +285,26 @@ OBST_API long long obst_gemm4w_calls() { return g_4w_calls; }
 static unsigned long long* g_4w_stamps = nullptr;
 OBST_API void obst_gemm4w_stamps(unsigned long long* dev) { g_4w_stamps = dev; }
 
+// gemm4w dynamic tile queue (OBST_G4W_QUEUE, default 1): a ring of per-launch counter blocks (8 per-XCD counters
+// each), zeroed on the launch's stream just before it -- in-flight launches on other streams (and the slots baked
+// into a captured graph) keep their own block while the ring has not wrapped
+static int g4w_queue_env() {
+  static int v = [] { const char* e = getenv("OBST_G4W_QUEUE"); return e ? atoi(e) : 1; }();
+  return v;
+}
+static unsigned* g4w_queue_slot(hipStream_t stream) {
+  constexpr int RING = 256;
+  static unsigned* ring = nullptr;
+  static int next = 0;
+  if (!ring && hipMalloc(reinterpret_cast<void**>(&ring), RING * 8 * sizeof(unsigned)) != hipSuccess) {
+    ring = nullptr;
+    return nullptr;
+  }
+  unsigned* q = ring + (next++ % RING) * 8;
+  if (hipMemsetAsync(q, 0, 8 * sizeof(unsigned), stream) != hipSuccess) return nullptr;
+  return q;
+}
+
 // Every GEMM of the framework is one of two hand-written kernels: gemm4w (gemm4w.h: the one-wave-per-SIMD 256x256
 // persistent kernel -- every product with K % 64 == 0, including the triangular token mixer (tri 1 / 2), the masked
 // lower-triangle output (tri 3) and the split contraction index) and the 128x128 kernel above for what gemm4w does
@@ -311,6 +331,7 @@ OBST_API int obst_gemm(const ObstGemmDesc* d, hipStream_t stream) {
   a.alpha = d->alpha; a.beta = d->beta; a.act = d->act; a.mode = d->mode; a.tri = d->tri;
   a.kin = d->kin; a.a_sk = d->a_sk; a.b_sk = d->b_sk; a.kin_bps = 0;
   a.stamps = g_4w_stamps;
+  a.queue = nullptr;
   a.ksplit = 1;
   a.ws = nullptr;
   a.nbatch = 0;
@@ -361,6 +382,11 @@ OBST_API int obst_gemm(const ObstGemmDesc* d, hipStream_t stream) {
     if (d->tri == 3 && ks < 2) goto fallback;   // (no workspace: the 128x128 kernel masks in its epilogue)
     a.ksplit = ks;
     a.kin_bps = d->kin ? d->K / ks / d->kin : 0;
+    // the queue: dense products whose every tile has >= 3 K-tiles (the next tile is dequeued in a tile's first
+    // K-tile and the DMA cursor needs it by the end of K-tile nk - 3), more tiles than one per block, no stamps
+    if (g4w_queue_env() && d->tri == 0 && !d->kin && d->K / ks >= 192 && !g_4w_stamps &&
+        !(d->out_f32 && d->Zout) && tm * tn * batch * ks > 256)
+      a.queue = g4w_queue_slot(stream);
     e = gemm4w_launch(&a, d->a_t, d->b_t, d->out_f32, batch, stream);
     if (e == hipSuccess && d->out_f32 && a.ksplit > 1) {
       const long long mn = (long long)a.M * a.N;

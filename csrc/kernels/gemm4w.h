@@ -436,6 +436,10 @@ constexpr int idx(const int (&a)[8], int q) {
 #define G4W_OPT 0   // 4: LATE (row layout: epilogue 8.6k -> 6.5k clocks, +0.5-1 % per shape in the lab, but the
                     // step measured 137.2k vs 138.8k tokens/s: off); 1: RELAX
 #endif
+// the fp32 + bf16-copy (RevNet stream update) instantiation's options: its epilogue moves 10 bytes per output
+#ifndef G4W_ZCP_OPT
+#define G4W_ZCP_OPT G4W_OPT
+#endif
 // OPT bits (schedule options under A/B, tools/lab/g4w_sched.cpp):
 //   1 RELAX: the first K-tile of every tile is a separate (peeled) copy whose waits count the previous tile's
 //     direct-epilogue stores out (S = 32 bf16 / 64 fp32 stores per wave) instead of waiting for their write
@@ -445,7 +449,8 @@ constexpr int idx(const int (&a)[8], int q) {
 //   2 STAGGER: blocks start (slot & 7) / 8 of a tile apart (s_sleep), so the CUs' epilogue store bursts do not
 //     coincide on the fabric
 template <int A_T, int B_T, bool OUT_F32, bool PROF, int NWV = 4, int SCH = G4W_SCH, bool STG = (G4W_STG != 0),
-          int CPA = G4W_CPA, int CPB = G4W_CPB, int OPT = G4W_OPT, bool KINT = false, bool ZCP = false>
+          int CPA = G4W_CPA, int CPB = G4W_CPB, int OPT = G4W_OPT, bool KINT = false, bool ZCP = false,
+          bool QUE = false>
 __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   constexpr bool RELAX = (OPT & 1) != 0, STAGGER = (OPT & 2) != 0, LATE = (OPT & 4) != 0;
@@ -457,6 +462,13 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
   constexpr bool TLAY = B_T == 0 && NWV == 4 && (OPT & 256) == 0 && !ROWS;
   // fp32 output + its bf16 copy in Zout (the fused RevNet stream update): its own instantiation as well
   constexpr bool ZCOPY = ZCP && OUT_F32 && !ROWS;
+  // dynamic tile queue (its own instantiation): a block's first tile is dealt statically, every later one is taken
+  // from its XCD's counter (p.queue[xcd], zeroed before the launch) -- a block that starts late or runs slower
+  // because another kernel (RCCL's collectives at N > 1) holds CUs beside it simply takes fewer tiles. Wave 0
+  // dequeues the NEXT tile at the start of the current tile's first K-tile (one returning vector atomic), the
+  // K-tile's own vmcnt wait retires it, wave 0 passes it through LDS before that K-tile's barrier; the DMA cursor
+  // needs it by the end of K-tile nk - 3 (the host enables the queue only for dense products with nk >= 3).
+  constexpr bool QUEUE = QUE && !RELAX && !LATE && !KINT && !STG;
 
   static_assert(!(RELAX && LATE), "RELAX peels the first K-tile, LATE the last: not both");
   static_assert(SCH == 0 || NWV == 4, "the split schedule is laid out for one wave per SIMD");
@@ -529,6 +541,29 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
     r[3] = 0x00020000;
     return r;
   };
+  // QUEUE: the next tile (-1: none); static deal: tile 1 of the slot (q_next only steers the queue path)
+  long long q_next = -1;
+  unsigned q_ret = 0;
+  const unsigned q_slot = lds0 + 2 * Q_STAGE + 32768 - 16;   // LDS address: the end of the epilogue region
+  auto q_issue = [&]() {   // wave 0, lane 0: take the next index of this XCD's queue (returning vector atomic)
+    if (wave == 0 && lane == 0) {
+      unsigned* qp = p.queue + xcd;
+      asm volatile("global_atomic_add %0, %1, %2, off sc0" : "=v"(q_ret) : "v"(qp), "v"(1u) : "memory");
+    }
+  };
+  auto q_pin = [&]() { asm volatile("" : "+v"(q_ret)); };
+  // after the K-tile's vmcnt wait: the returned index into LDS before its barrier (asm LDS ops: the compiler would
+  // address a cast pointer generically, and a flat store waits for vmcnt(0), i.e. for every DMA in flight)
+  auto q_publish = [&]() {
+    if (wave == 0 && lane == 0) asm volatile("ds_write_b32 %0, %1" ::"v"(q_slot), "v"(q_ret) : "memory");
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the write is done before the barrier
+  };
+  auto q_take = [&]() {   // every wave: dynamic index i -> tile nslot + i of the XCD's range (the static tiles first)
+    unsigned v;
+    asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(q_slot) : "memory");
+    const long long i = (long long)__builtin_amdgcn_readfirstlane(v);
+    q_next = nslot + i < len ? start + nslot + i : -1;
+  };
   i32x4_t ra, rb;
   auto dma_setup = [&]() {   // resources of the cursor's K-tile
     ra = rsrc_of(cur_a, rem_a);
@@ -550,12 +585,12 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
         cur_b += bjump;
         rem_b -= bjump;
       }
-    } else if (d_rnd + 1 < ntiles) {
+    } else if (QUEUE ? q_next >= 0 : d_rnd + 1 < ntiles) {
       // once per tile: the volatile asm keeps the compiler from if-converting the decode into every K-tile
       asm volatile("");
       ++d_rnd;
       d_kt = 0;
-      cursor_tile(decode4<A_T, B_T, KIN>(p, logical(d_rnd)));
+      cursor_tile(decode4<A_T, B_T, KIN>(p, QUEUE ? q_next : logical(d_rnd)));
     }
   };
 
@@ -623,8 +658,9 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
     if constexpr (!LATE) static_for<NR>([&](auto rc) { read_sub(0, K0{}, rc, a0, b0); fence(); });   // loop order
 
     int pos = 0;   // flat position of the K-tile being multiplied (its stage is pos & 1)
-    for (int rnd = 0; rnd < ntiles; ++rnd) {
-      const Tile4 ct = decode4<A_T, B_T, KIN>(p, logical(rnd));
+    long long q_cur = logical(0);   // QUEUE: the tile being multiplied
+    for (int rnd = 0; QUEUE ? q_cur >= 0 : rnd < ntiles; ++rnd) {
+      const Tile4 ct = decode4<A_T, B_T, KIN>(p, QUEUE ? q_cur : logical(rnd));
       // Accumulator zeroing (VALU writes of AGPRs) -> first MFMA reading them needs wait states the compiler cannot
       // see through the asm MFMAs; the empty "+a" asms pin the zeros before the pad (no rematerialisation past it)
   #pragma unroll
@@ -644,7 +680,8 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
       // tile the previous tile's epilogue stores sit in between, so the same count also waits for the older stores
       // -- issued ~60 MFMAs earlier, they have retired by then; a relaxed count for that K-tile needs a runtime
       // branch at every wait or a second copy of the K-tile, and the copy's phi over the 256 accumulators spills.
-      auto ktile = [&](auto fc, auto lc, int s) {
+      auto ktile = [&](auto fc, auto lc, int s, auto hc) {
+        constexpr bool QH = decltype(hc)::value && QUEUE;   // this K-tile publishes the dequeued index
         constexpr bool FIRST = decltype(fc)::value && RELAX;
         constexpr bool NEXT0 = !(decltype(lc)::value && LATE);   // read pos+1's substep-0 fragments in this K-tile
         const unsigned sa = stage_a(s), sb = stage_b(s);
@@ -678,6 +715,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
               if constexpr (PROF) tw = __builtin_amdgcn_s_memtime();
               if constexpr (FIRST) vm_wait<V0F>();
               else vm_wait<2 * PPW>();
+              if constexpr (QH) q_publish();   // the dequeued index (retired by the wait above) to every wave
               if constexpr (!(G4W_EXP & 4)) __builtin_amdgcn_s_barrier();
               if constexpr (PROF) sync2 += __builtin_amdgcn_s_memtime() - tw;
             }
@@ -705,6 +743,9 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
               if constexpr (PROF) tw = __builtin_amdgcn_s_memtime();
               if constexpr (FIRST) vm_wait<q == g4s::WA ? VAF : VBF>();
               else vm_wait<q == g4s::WA ? VA : VB>();
+              // the atomic was issued before every DMA of this K-tile: at WB at most VB (< the K-tile's own pieces
+              // issued so far) are younger, so it has retired
+              if constexpr (QH && q == g4s::WB) q_publish();
               __builtin_amdgcn_s_barrier();
               if constexpr (PROF) sync2 += __builtin_amdgcn_s_memtime() - tw;
             }
@@ -714,30 +755,43 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
               b0[rb0] = frag_b<B_T, TLAY>(smem + (s ^ 1) * Q_STAGE + Q_OP, wn * WN, rb0, 0, lane);
           }
           fence();
+          // the dequeue's destination register has no hardware interlock: until the wait at WB retires the atomic,
+          // the empty asm at every slot keeps the value where the atomic writes it (no copy or spill reads it early)
+          if constexpr (QH && q < g4s::WB) q_pin();
         });
       };
 
       using T_ = std::true_type;
       using F_ = std::false_type;
       if constexpr (RELAX) {   // the first K-tile peeled (sequential copies: no phi over the accumulators)
-        ktile(T_{}, F_{}, pos & 1);
+        ktile(T_{}, F_{}, pos & 1, F_{});
         dma_advance();
         ++pos;
         for (int t = 1; t < ct.nk; ++t, ++pos) {
-          ktile(F_{}, F_{}, pos & 1);
+          ktile(F_{}, F_{}, pos & 1, F_{});
           dma_advance();
         }
       } else if constexpr (LATE) {   // the last K-tile peeled
         for (int t = 0; t < ct.nk - 1; ++t, ++pos) {
-          ktile(F_{}, F_{}, pos & 1);
+          ktile(F_{}, F_{}, pos & 1, F_{});
           dma_advance();
         }
-        ktile(F_{}, T_{}, pos & 1);
+        ktile(F_{}, T_{}, pos & 1, F_{});
         dma_advance();
         ++pos;
+      } else if constexpr (QUEUE) {
+        q_issue();   // the first K-tile peeled: it carries the dequeue (no runtime branch inside the MFMA stream)
+        ktile(F_{}, F_{}, pos & 1, T_{});
+        q_take();
+        dma_advance();
+        ++pos;
+        for (int t = 1; t < ct.nk; ++t, ++pos) {
+          ktile(F_{}, F_{}, pos & 1, F_{});
+          dma_advance();
+        }
       } else {
         for (int t = 0; t < ct.nk; ++t, ++pos) {
-          ktile(F_{}, F_{}, pos & 1);
+          ktile(F_{}, F_{}, pos & 1, F_{});
           dma_advance();
         }
       }
@@ -1193,6 +1247,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
         const unsigned long long now = __builtin_amdgcn_s_memtime();
         epi_clk += now - tmark;
       }
+      if constexpr (QUEUE) q_cur = q_next;
     }
   };
   if constexpr (STG) {
@@ -1236,11 +1291,25 @@ hipError_t launch4w(GemmArgs a, int batch, hipStream_t stream) {
   }
   if constexpr (F32 && A_T == 0) {
     if (a.Zout) {   // fp32 output + bf16 copy (RevNet stream update: A is the activation or the mixer weight)
-      k = gemm4w_kernel<A_T, B_T, F32, false, NWV, G4W_SCH, (G4W_STG != 0), G4W_CPA, G4W_CPB, G4W_OPT, false, true>;
+      k = gemm4w_kernel<A_T, B_T, F32, false, NWV, G4W_SCH, (G4W_STG != 0), G4W_CPA, G4W_CPB, G4W_ZCP_OPT, false,
+                        true>;
       which = 3;
     }
   }
-  static bool attr[4] = {false, false, false, false};
+  if constexpr (!(F32 && A_T == 0)) {
+    if (a.queue) {   // the dynamic tile queue (dense products, every tile >= 3 K-tiles: obst_gemm)
+      k = gemm4w_kernel<A_T, B_T, F32, false, NWV, G4W_SCH, (G4W_STG != 0), G4W_CPA, G4W_CPB, G4W_OPT, false, false,
+                        true>;
+      which = 4;
+    }
+  } else {
+    if (a.queue && !a.Zout) {
+      k = gemm4w_kernel<A_T, B_T, F32, false, NWV, G4W_SCH, (G4W_STG != 0), G4W_CPA, G4W_CPB, G4W_OPT, false, false,
+                        true>;
+      which = 4;
+    }
+  }
+  static bool attr[5] = {false, false, false, false, false};
   if (!attr[which]) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr[which] = true;

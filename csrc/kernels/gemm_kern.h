@@ -25,6 +25,7 @@ struct GemmArgs {
   int kin_bps;            // kin blocks per split-K slab (K / ksplit / kin; slabs start on block boundaries)
   int nbatch;             // gemm4w: batches x splits (the grid is one block per CU)
   unsigned long long* stamps;   // gemm4w diagnostics: per-block timestamps (null: off)
+  unsigned* queue;        // gemm4w dynamic tile queue: 8 per-XCD counters zeroed before the launch (null: static)
 };
 }  // namespace gemmk
 
