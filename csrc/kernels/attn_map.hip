@@ -70,6 +70,28 @@ __device__ __forceinline__ void load_rows(Rows<D>& r, const bf16_t* g, long long
     r.v[i] = ld16(g + (long long)(r0 + row) * ld + cc * 8, r0 + row < S);
   }
 }
+// full tiles (r0 + 64 <= S): the per-thread 32-bit offsets of its D / 32 pieces, computed once, on a uniform tile
+// base (global_load with an SGPR base and a VGPR offset: no 64-bit address VALU and no exec-masked branch per load)
+template <int D>
+__device__ __forceinline__ void row_offsets(int (&off)[D / 32], int ld, int tid) {
+  constexpr int CH = D / 8;
+#pragma unroll
+  for (int i = 0; i < D / 32; ++i) {
+    const int c = tid + 256 * i, row = c / CH, cc = c - row * CH;
+    off[i] = row * ld + cc * 8;
+  }
+}
+template <int D>
+__device__ __forceinline__ void load_tile(Rows<D>& r, const bf16_t* g, long long ld, int r0, int S, int tid,
+                                          const int (&off)[D / 32]) {
+  if (r0 + 64 <= S) {
+    const bf16_t* gt = g + (long long)r0 * ld;
+#pragma unroll
+    for (int i = 0; i < D / 32; ++i) r.v[i] = *reinterpret_cast<const uint4*>(gt + off[i]);
+  } else {
+    load_rows<D>(r, g, ld, r0, S, tid);
+  }
+}
 template <int D>
 __device__ __forceinline__ void store_rows(bf16_t* img, const Rows<D>& r, int tid) {
   constexpr int CH = D / 8;
@@ -117,7 +139,10 @@ __device__ __forceinline__ f32x4_t mfma(const bf16x8_t& a, const bf16x8_t& b, co
 }
 
 // ------------------------------------------------------------------------------------------------------------------
-template <int D>
+// HB / HC: a bias / scale map is present (separate instantiations: a runtime-null map load in a branch made the
+// compiler's wait at its use a vmcnt(0), which also waited for the next tile's K / V prefetch -- every tile paid a
+// full memory round trip, with or without a map). The next tile's map values are prefetched with its K / V rows.
+template <int D, bool HB, bool HC>
 __global__ __launch_bounds__(256) void attn_map_fwd_kernel(MapArgs a) {
   __shared__ __attribute__((aligned(16))) bf16_t kimg[64 * (D + PADR)];
   __shared__ __attribute__((aligned(16))) bf16_t vimg[64 * (D + PADR)];
@@ -140,18 +165,32 @@ __global__ __launch_bounds__(256) void attn_map_fwd_kernel(MapArgs a) {
   float m = -INFINITY, l = 0.f;
   const int nkt = a.causal ? qb + 1 : (S + TK - 1) / TK;
   Rows<D> nk, nv;
-  load_rows<D>(nk, a.k + base, ld, 0, S, tid);
-  load_rows<D>(nv, a.v + base, ld, 0, S, tid);
+  int roff[D / 32];
+  row_offsets<D>(roff, (int)ld, tid);
+  f32x4_t nb[4], nc[4];
+  auto fetch = [&](int k0) {
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      if constexpr (HB) nb[kb] = map4(a.bias + mrow, k0 + kb * 16 + 4 * g, S);
+      if constexpr (HC) nc[kb] = map4(a.cmap + mrow, k0 + kb * 16 + 4 * g, S);
+    }
+    load_tile<D>(nk, a.k + base, ld, k0, S, tid, roff);
+    load_tile<D>(nv, a.v + base, ld, k0, S, tid, roff);
+  };
+  fetch(0);
   for (int kt = 0; kt < nkt; ++kt) {
     const int k0 = kt * TK;
     __syncthreads();
     store_rows<D>(kimg, nk, tid);
     store_rows<D>(vimg, nv, tid);
-    __syncthreads();
-    if (kt + 1 < nkt) {
-      load_rows<D>(nk, a.k + base, ld, k0 + TK, S, tid);
-      load_rows<D>(nv, a.v + base, ld, k0 + TK, S, tid);
+    f32x4_t bv[4], cv[4];
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      if constexpr (HB) bv[kb] = nb[kb];
+      if constexpr (HC) cv[kb] = nc[kb];
     }
+    __syncthreads();
+    if (kt + 1 < nkt) fetch(k0 + TK);
     f32x4_t s[4];
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) {
@@ -159,40 +198,53 @@ __global__ __launch_bounds__(256) void attn_map_fwd_kernel(MapArgs a) {
 #pragma unroll
       for (int kk = 0; kk < D / 32; ++kk) s[kb] = mfma(frag_rm<D + PADR>(kimg, kb * 16, kk, lane), qf[kk], s[kb]);
     }
+    // masks only on the diagonal tile and the tile past S (uniform branch)
+    const bool edge = (a.causal && kt == nkt - 1) || k0 + TK > S;
     float mx = -INFINITY;
 #pragma unroll
-    for (int kb = 0; kb < 4; ++kb) {
-      const f32x4_t bv = a.bias != nullptr ? map4(a.bias + mrow, k0 + kb * 16 + 4 * g, S) : f32x4_t{0.f, 0.f, 0.f, 0.f};
+    for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int key = k0 + kb * 16 + 4 * g + r;
-        const bool ok = key < S && (!a.causal || key <= myq);
-        const float x = ok ? s[kb][r] * a.scale + bv[r] : -INFINITY;
+        float x = s[kb][r] * a.scale;
+        if constexpr (HB) x += bv[kb][r];
         s[kb][r] = x;
-        mx = fmaxf(mx, x);
       }
+    if (edge) {
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = k0 + kb * 16 + 4 * g + r;
+          if (!(key < S && (!a.causal || key <= myq))) s[kb][r] = -INFINITY;
+        }
     }
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) mx = fmaxf(mx, s[kb][r]);
     mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     const float mn = fmaxf(m, mx);   // finite: key k0 <= every query of a visited tile
     const float al = __expf(m - mn);
     float rs = 0.f;
 #pragma unroll
-    for (int kb = 0; kb < 4; ++kb) {
-      const f32x4_t cv = a.cmap != nullptr ? map4(a.cmap + mrow, k0 + kb * 16 + 4 * g, S) : f32x4_t{1.f, 1.f, 1.f, 1.f};
+    for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const float p = __expf(s[kb][r] - mn);
         rs += p;
-        s[kb][r] = p * cv[r];
+        s[kb][r] = HC ? p * cv[kb][r] : p;
       }
-    }
     rs += __shfl_xor(rs, 16, 64);
     rs += __shfl_xor(rs, 32, 64);
     l = l * al + rs;
-    m = mn;
+    // the output rescale only when some lane's max moved (exact; after the first tiles it rarely does): the
+    // accumulators live in AGPRs, and every rescale moved all of them through VGPRs and back
+    if (__any(mn > m)) {
 #pragma unroll
-    for (int i = 0; i < D / 16; ++i) acc[i] *= al;
+      for (int i = 0; i < D / 16; ++i) acc[i] *= al;
+    }
+    m = mn;
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       const bf16x8_t pb = frag_acc(s[2 * c], s[2 * c + 1]);
@@ -213,7 +265,7 @@ __global__ __launch_bounds__(256) void attn_map_fwd_kernel(MapArgs a) {
 
 // ------------------------------------------------------------------------------------------------------------------
 // dq per (query block, head, batch); writes delta_q = do_q . o_q first (the dk/dv kernel reads it)
-template <int D>
+template <int D, bool HB, bool HC>
 __global__ __launch_bounds__(256) void attn_map_dq_kernel(MapArgs a) {
   __shared__ __attribute__((aligned(16))) bf16_t kimg[64 * (D + PADR)];
   __shared__ __attribute__((aligned(16))) bf16_t vimg[64 * (D + PADR)];
@@ -250,18 +302,32 @@ __global__ __launch_bounds__(256) void attn_map_dq_kernel(MapArgs a) {
   for (int i = 0; i < D / 16; ++i) acc[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   const int nkt = a.causal ? qb + 1 : (S + TK - 1) / TK;
   Rows<D> nk, nv;
-  load_rows<D>(nk, a.k + base, ld, 0, S, tid);
-  load_rows<D>(nv, a.v + base, ld, 0, S, tid);
+  int roff[D / 32];
+  row_offsets<D>(roff, (int)ld, tid);
+  f32x4_t nb[4], nc[4];
+  auto fetch = [&](int k0) {
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      if constexpr (HB) nb[kb] = map4(a.bias + mrow, k0 + kb * 16 + 4 * g, S);
+      if constexpr (HC) nc[kb] = map4(a.cmap + mrow, k0 + kb * 16 + 4 * g, S);
+    }
+    load_tile<D>(nk, a.k + base, ld, k0, S, tid, roff);
+    load_tile<D>(nv, a.v + base, ld, k0, S, tid, roff);
+  };
+  fetch(0);
   for (int kti = 0; kti < nkt; ++kti) {
     const int k0 = kti * TK;
     __syncthreads();
     store_rows<D>(kimg, nk, tid);
     store_rows<D>(vimg, nv, tid);
-    __syncthreads();
-    if (kti + 1 < nkt) {
-      load_rows<D>(nk, a.k + base, ld, k0 + TK, S, tid);
-      load_rows<D>(nv, a.v + base, ld, k0 + TK, S, tid);
+    f32x4_t bv[4], cv[4];
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      if constexpr (HB) bv[kb] = nb[kb];
+      if constexpr (HC) cv[kb] = nc[kb];
     }
+    __syncthreads();
+    if (kti + 1 < nkt) fetch(k0 + TK);
     f32x4_t s[4], dp[4];
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) {
@@ -272,17 +338,20 @@ __global__ __launch_bounds__(256) void attn_map_dq_kernel(MapArgs a) {
         dp[kb] = mfma(frag_rm<D + PADR>(vimg, kb * 16, kk, lane), df[kk], dp[kb]);
       }
     }
+    // (rows of queries past S hold zero q / dO and lse 0: finite p, ds = 0; their dq is not stored)
+    const bool edge = (a.causal && kti == nkt - 1) || k0 + TK > S;
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) {
       const int key0 = k0 + kb * 16 + 4 * g;
-      const f32x4_t bv = a.bias != nullptr ? map4(a.bias + mrow, key0, S) : f32x4_t{0.f, 0.f, 0.f, 0.f};
-      const f32x4_t cv = a.cmap != nullptr ? map4(a.cmap + mrow, key0, S) : f32x4_t{1.f, 1.f, 1.f, 1.f};
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int key = key0 + r;
-        const bool ok = qok && key < S && (!a.causal || key <= myq);
-        const float p = ok ? __expf(s[kb][r] * a.scale + bv[r] - lse) : 0.f;
-        s[kb][r] = p * (cv[r] * dp[kb][r] - dl);
+        float x = s[kb][r] * a.scale - lse;
+        if constexpr (HB) x += bv[kb][r];
+        float p = __expf(x);
+        if (edge && !(key < S && (!a.causal || key <= myq))) p = 0.f;
+        const float c = HC ? cv[kb][r] : 1.f;
+        s[kb][r] = p * (c * dp[kb][r] - dl);
       }
     }
 #pragma unroll
@@ -304,7 +373,7 @@ __global__ __launch_bounds__(256) void attn_map_dq_kernel(MapArgs a) {
 
 // ------------------------------------------------------------------------------------------------------------------
 // dk / dv per (key block, head, batch slice); map gradients accumulated in place over the slice's batches
-template <int D>
+template <int D, bool HB, bool HC>
 __global__ __launch_bounds__(256) void attn_map_dkv_kernel(MapArgs a) {
   __shared__ __attribute__((aligned(16))) bf16_t qimg[64 * (D + PADR)];
   __shared__ __attribute__((aligned(16))) bf16_t dimg[64 * (D + PADR)];
@@ -315,11 +384,14 @@ __global__ __launch_bounds__(256) void attn_map_dkv_kernel(MapArgs a) {
   const long long ld = (long long)a.H * D;
   const int myk = kbk * TK + w * 16 + (lane & 15);
   const bool kok = myk < S;
+  const bool kedge = (kbk + 1) * TK > S;
   const int bper = (a.B + a.bsplit - 1) / a.bsplit;
   const int b0 = slice * bper, b1 = min(a.B, b0 + bper);
   const long long mbase = (long long)h * S * S;
   const long long pbase = (long long)slice * a.H * S * S + mbase;   // this slice's partial map gradients
   const int qb_first = a.causal ? kbk : 0;                            // query blocks holding a query >= a key here
+  int roff[D / 32];
+  row_offsets<D>(roff, (int)ld, tid);
   for (int b = b0; b < b1; ++b) {
     const long long base = (long long)b * S * ld + (long long)h * D;
     const long long srow = ((long long)b * a.H + h) * S;
@@ -335,34 +407,54 @@ __global__ __launch_bounds__(256) void attn_map_dkv_kernel(MapArgs a) {
     for (int i = 0; i < D / 16; ++i) dk[i] = dv[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
     Rows<D> nq, nd;
     float nl = 0.f, ndl = 0.f;
+    // the next tile's q / dO rows, statistics, map values and running map-gradient sums, one tile ahead (clamped
+    // addresses, unconditional loads: a load under a branch made its use wait for every younger load)
+    f32x4_t nbv[4], ncv[4], nob[4], noc[4];
     auto fetch = [&](int qbn) {
       const int qn = qbn * TQ;
-      load_rows<D>(nq, a.q + base, ld, qn, S, tid);
-      load_rows<D>(nd, a.dO + base, ld, qn, S, tid);
+#pragma unroll
+      for (int qi = 0; qi < 4; ++qi)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int qq = qn + qi * 16 + 4 * g + r;
+          const bool inb = kok && qq < S;
+          const long long mi = (long long)(inb ? qq : 0) * S + (kok ? myk : 0);
+          if constexpr (HB) {
+            const float x = a.bias[mbase + mi], y = a.dbias[pbase + mi];
+            nbv[qi][r] = inb ? x : 0.f;
+            nob[qi][r] = inb ? y : 0.f;
+          }
+          if constexpr (HC) {
+            const float x = a.cmap[mbase + mi], y = a.dcmap[pbase + mi];
+            ncv[qi][r] = inb ? x : 1.f;
+            noc[qi][r] = inb ? y : 0.f;
+          }
+        }
+      load_tile<D>(nq, a.q + base, ld, qn, S, tid, roff);
+      load_tile<D>(nd, a.dO + base, ld, qn, S, tid, roff);
       if (tid < TQ) {
         const bool ok = qn + tid < S;
-        nl = ok ? a.lse[srow + qn + tid] : 0.f;
-        ndl = ok ? a.delta[srow + qn + tid] : 0.f;
+        const long long i = srow + (ok ? qn + tid : 0);
+        const float x = a.lse[i], y = a.delta[i];
+        nl = ok ? x : 0.f;
+        ndl = ok ? y : 0.f;
       }
     };
     if (qb_first < nqb) fetch(qb_first);
     for (int qb = qb_first; qb < nqb; ++qb) {
       const int q0 = qb * TQ;
-      // this tile's map values and the running map-gradient sums, loaded before the staging and the score MFMAs so
-      // their latency hides under them (issued at their use, every read-modify-write paid a full memory round trip)
       f32x4_t bv[4], cv[4], ob[4], oc[4];
 #pragma unroll
-      for (int qi = 0; qi < 4; ++qi)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int qq = q0 + qi * 16 + 4 * g + r;
-          const bool inb = kok && qq < S;
-          const long long mi = (long long)(inb ? qq : 0) * S + (kok ? myk : 0);
-          bv[qi][r] = a.bias != nullptr && inb ? a.bias[mbase + mi] : 0.f;
-          cv[qi][r] = a.cmap != nullptr && inb ? a.cmap[mbase + mi] : 1.f;
-          ob[qi][r] = a.dbias != nullptr && inb ? a.dbias[pbase + mi] : 0.f;
-          oc[qi][r] = a.dcmap != nullptr && inb ? a.dcmap[pbase + mi] : 0.f;
+      for (int qi = 0; qi < 4; ++qi) {
+        if constexpr (HB) {
+          bv[qi] = nbv[qi];
+          ob[qi] = nob[qi];
         }
+        if constexpr (HC) {
+          cv[qi] = ncv[qi];
+          oc[qi] = noc[qi];
+        }
+      }
       __syncthreads();
       store_rows<D>(qimg, nq, tid);
       store_rows<D>(dimg, nd, tid);
@@ -383,20 +475,24 @@ __global__ __launch_bounds__(256) void attn_map_dkv_kernel(MapArgs a) {
           dp[qi] = mfma(frag_rm<D + PADR>(dimg, qi * 16, kk, lane), vf[kk], dp[qi]);
         }
       }
+      const bool edge = kedge || (a.causal && qb == kbk) || q0 + TQ > S;   // uniform: masks only here
 #pragma unroll
       for (int qi = 0; qi < 4; ++qi)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int ql = qi * 16 + 4 * g + r, qq = q0 + ql;
-          const bool inb = kok && qq < S;
-          const bool ok = inb && (!a.causal || myk <= qq);
+          const bool inb = !edge || (kok && qq < S);
+          const bool ok = !edge || (inb && (!a.causal || myk <= qq));
           const long long mi = (long long)qq * S + myk;
-          const float c = cv[qi][r];
-          const float p = ok ? __expf(s[qi][r] * a.scale + bv[qi][r] - lse_s[ql]) : 0.f;
+          const float c = HC ? cv[qi][r] : 1.f;
+          float x = s[qi][r] * a.scale - lse_s[ql];
+          if constexpr (HB) x += bv[qi][r];
+          const float e = __expf(x);
+          const float p = ok ? e : 0.f;
           const float ds = p * (c * dp[qi][r] - dl_s[ql]);
           if (inb) {
-            if (a.dbias != nullptr) a.dbias[pbase + mi] = ob[qi][r] + ds;
-            if (a.dcmap != nullptr) a.dcmap[pbase + mi] = oc[qi][r] + p * dp[qi][r];
+            if constexpr (HB) a.dbias[pbase + mi] = ob[qi][r] + ds;
+            if constexpr (HC) a.dcmap[pbase + mi] = oc[qi][r] + p * dp[qi][r];
           }
           s[qi][r] = p * c;
           dp[qi][r] = ds;
@@ -435,18 +531,29 @@ __global__ __launch_bounds__(256) void map_fold_kernel(const float* part, float*
   out[i] = v;
 }
 
-template <int D>
+template <int D, bool HB, bool HC>
 hipError_t launch_fwd(const MapArgs& a, hipStream_t st) {
   const int nqb = (a.S + TQ - 1) / TQ;
-  hipLaunchKernelGGL(attn_map_fwd_kernel<D>, dim3(nqb, a.H, a.B), dim3(256), 0, st, a);
+  hipLaunchKernelGGL((attn_map_fwd_kernel<D, HB, HC>), dim3(nqb, a.H, a.B), dim3(256), 0, st, a);
   return hipGetLastError();
 }
-template <int D>
+template <int D, bool HB, bool HC>
 hipError_t launch_bwd(const MapArgs& a, hipStream_t st) {
   const int nqb = (a.S + TQ - 1) / TQ;
-  hipLaunchKernelGGL(attn_map_dq_kernel<D>, dim3(nqb, a.H, a.B), dim3(256), 0, st, a);
-  hipLaunchKernelGGL(attn_map_dkv_kernel<D>, dim3(nqb, a.H, a.bsplit), dim3(256), 0, st, a);
+  hipLaunchKernelGGL((attn_map_dq_kernel<D, HB, HC>), dim3(nqb, a.H, a.B), dim3(256), 0, st, a);
+  hipLaunchKernelGGL((attn_map_dkv_kernel<D, HB, HC>), dim3(nqb, a.H, a.bsplit), dim3(256), 0, st, a);
   return hipGetLastError();
+}
+// the map-presence instantiations of one head dim
+template <int D>
+hipError_t launch_fwd_d(const MapArgs& a, hipStream_t st) {
+  if (a.bias) return a.cmap ? launch_fwd<D, true, true>(a, st) : launch_fwd<D, true, false>(a, st);
+  return a.cmap ? launch_fwd<D, false, true>(a, st) : launch_fwd<D, false, false>(a, st);
+}
+template <int D>
+hipError_t launch_bwd_d(const MapArgs& a, hipStream_t st) {
+  if (a.bias) return a.cmap ? launch_bwd<D, true, true>(a, st) : launch_bwd<D, true, false>(a, st);
+  return a.cmap ? launch_bwd<D, false, true>(a, st) : launch_bwd<D, false, false>(a, st);
 }
 
 }  // namespace
@@ -488,10 +595,10 @@ OBST_API int obst_attn_map_fwd(const ObstMapDesc* d, hipStream_t st) {
   if (fill(a, d) != 0) return -1;
   hipError_t e;
   switch (d->D) {
-    case 32: e = launch_fwd<32>(a, st); break;
-    case 64: e = launch_fwd<64>(a, st); break;
-    case 96: e = launch_fwd<96>(a, st); break;
-    case 128: e = launch_fwd<128>(a, st); break;
+    case 32: e = launch_fwd_d<32>(a, st); break;
+    case 64: e = launch_fwd_d<64>(a, st); break;
+    case 96: e = launch_fwd_d<96>(a, st); break;
+    case 128: e = launch_fwd_d<128>(a, st); break;
     default: return -2;
   }
   return (int)e;
@@ -500,12 +607,13 @@ OBST_API int obst_attn_map_fwd(const ObstMapDesc* d, hipStream_t st) {
 OBST_API int obst_attn_map_bwd(const ObstMapDesc* d, hipStream_t st) {
   MapArgs a;
   if (fill(a, d) != 0) return -1;
+  if ((a.bias && !a.dbias) || (a.cmap && !a.dcmap)) return -3;   // a present map always gets its gradient
   hipError_t e;
   switch (d->D) {
-    case 32: e = launch_bwd<32>(a, st); break;
-    case 64: e = launch_bwd<64>(a, st); break;
-    case 96: e = launch_bwd<96>(a, st); break;
-    case 128: e = launch_bwd<128>(a, st); break;
+    case 32: e = launch_bwd_d<32>(a, st); break;
+    case 64: e = launch_bwd_d<64>(a, st); break;
+    case 96: e = launch_bwd_d<96>(a, st); break;
+    case 128: e = launch_bwd_d<128>(a, st); break;
     default: return -2;
   }
   if (e != hipSuccess) return (int)e;

@@ -401,6 +401,14 @@ def attn_map_bwd(q, k, v, o, do, lse, delta, dq, dk, dv, bias, cmap, dbias, dcma
                 if t.dtype != torch.float32 or not t.is_contiguous():
                     raise L.KernelError(f"attention map {nm} must be contiguous fp32")
                 _need(t, H * S * S - 1, nm)
+        # the kernels accumulate the gradient of every present map (one instantiation per map set): a map whose
+        # gradient is not wanted gets a scratch output
+        if bias is not None and dbias is None:
+            dbias = torch.empty(H, S, S, device=q.device)
+            dbias_part = torch.zeros(bsplit, H, S, S, device=q.device) if bsplit > 1 else None
+        if cmap is not None and dcmap is None:
+            dcmap = torch.empty(H, S, S, device=q.device)
+            dcmap_part = torch.zeros(bsplit, H, S, S, device=q.device) if bsplit > 1 else None
         parts = []
         for nm, out, part in (("dbias", dbias, dbias_part), ("dcmap", dcmap, dcmap_part)):
             if out is None:
