@@ -24,6 +24,8 @@
 // once, row-major. The key-major dk/dv kernel does the same with queries and keys swapped.
 #include "common.h"
 
+#include <stdlib.h>
+
 namespace {
 
 constexpr int TQ = 64;    // queries per workgroup (16 per wave)
@@ -570,10 +572,18 @@ struct ObstMapDesc {
 };
 
 // batch slices of the dk/dv kernel: enough workgroups for 4 per CU, at most 4 partial maps
+static int map_wg_target() {   // OBST_MAP_WG: dk/dv workgroups to aim for (A/B)
+  static int v = [] { const char* e = getenv("OBST_MAP_WG"); return e ? atoi(e) : 1024; }();
+  return v;
+}
+static int map_max_split() {   // OBST_MAP_SPLIT: most partial maps
+  static int v = [] { const char* e = getenv("OBST_MAP_SPLIT"); return e ? atoi(e) : 4; }();
+  return v;
+}
 OBST_API int obst_attn_map_bsplit(int B, int S, int H) {
   const long long wg = (long long)((S + TK - 1) / TK) * H;
-  long long s = (1024 + wg - 1) / wg;
-  if (s > 4) s = 4;
+  long long s = (map_wg_target() + wg - 1) / wg;
+  if (s > map_max_split()) s = map_max_split();
   if (s > B) s = B;
   return (int)(s < 1 ? 1 : s);
 }

@@ -279,8 +279,9 @@ float* splitk_workspace(size_t bytes) {
 
 }  // namespace
 
-static long long g_4w_calls = 0;
+static long long g_4w_calls = 0, g_4w_queue_calls = 0;
 OBST_API long long obst_gemm4w_calls() { return g_4w_calls; }
+OBST_API long long obst_gemm4w_queue_calls() { return g_4w_queue_calls; }   // launches that took the tile queue
 // diagnostics: device buffer of 8 u64 per block (gemm4w.h) filled by the following gemm4w launches; null: off
 static unsigned long long* g_4w_stamps = nullptr;
 OBST_API void obst_gemm4w_stamps(unsigned long long* dev) { g_4w_stamps = dev; }
@@ -387,6 +388,7 @@ OBST_API int obst_gemm(const ObstGemmDesc* d, hipStream_t stream) {
     if (g4w_queue_env() && d->tri == 0 && !d->kin && d->K / ks >= 192 && !g_4w_stamps &&
         !(d->out_f32 && d->Zout) && tm * tn * batch * ks > 256)
       a.queue = g4w_queue_slot(stream);
+    if (a.queue) ++g_4w_queue_calls;
     e = gemm4w_launch(&a, d->a_t, d->b_t, d->out_f32, batch, stream);
     if (e == hipSuccess && d->out_f32 && a.ksplit > 1) {
       const long long mn = (long long)a.M * a.N;

@@ -514,6 +514,40 @@ def test_gemm4w_ragged(cuda, a_t, b_t, out_f32):
         assert torch.all(Cv[:, :, N:].float().cpu() == 7.0), "wrote past N into the ldc padding"
 
 
+def g4w_queue_calls() -> int:
+    import ctypes
+    f = L.lib().obst_gemm4w_queue_calls
+    f.restype = ctypes.c_longlong
+    return int(f())
+
+
+@pytest.mark.parametrize("a_t,b_t", [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("out_f32", [False, True])
+def test_gemm4w_tile_queue(cuda, a_t, b_t, out_f32):
+    """products with more tiles than blocks and >= 3 K-tiles take the dynamic per-XCD tile queue (OBST_G4W_QUEUE,
+    default on): every tile exactly once (ragged M, padded ldc) against the fp32 oracle, twice in a row (the
+    counters of the ring slot are zeroed per launch)"""
+    M, N, K, ldc = 8000, 2304, 448, 2304 + 8
+    torch.manual_seed(5)
+    A = (torch.randn(M * K) * 0.5).to(BF)
+    B = (torch.randn(N * K) * 0.5).to(BF)
+    av = A.view(M, K) if a_t == 0 else A.view(K, M).t()
+    bv = B.view(N, K).t() if b_t == 0 else B.view(K, N)
+    ref = av.float() @ bv.float()
+    dt = torch.float32 if out_f32 else BF
+    Ad, Bd = A.to(cuda), B.to(cuda)
+    for rep in range(2):
+        C = torch.full((M * ldc,), 7.0, dtype=dt, device=cuda)
+        c0, q0 = g4w_calls(), g4w_queue_calls()
+        raw.gemm(raw.Operand(Ad, a_t, K if a_t == 0 else M, M * K), raw.Operand(Bd, b_t, K if b_t == 0 else N, N * K),
+                 raw.Operand(C, 0, ldc, M * ldc), M, N, K)
+        torch.cuda.synchronize()
+        assert g4w_calls() - c0 == 1 and g4w_queue_calls() - q0 == 1, "the product did not take the tile queue"
+        Cv = C.view(M, ldc)
+        _close(Cv[:, :N], ref, 3e-2 * math.sqrt(K / 64), 2e-2, f"queued gemm4w {a_t}{b_t} f32={out_f32} rep {rep}")
+        assert torch.all(Cv[:, N:].float().cpu() == 7.0), "wrote past N into the ldc padding"
+
+
 @pytest.mark.parametrize("a_t,b_t,M,N,K", [(0, 0, 1024, 1536, 16384), (1, 1, 1024, 1536, 16384),
                                            (1, 0, 512, 768, 131072), (0, 1, 512, 768, 131072)])
 def test_gemm_splitk_wgrad(cuda, a_t, b_t, M, N, K):
