@@ -105,6 +105,11 @@ __device__ __forceinline__ void store_rows(bf16_t* img, const Rows<D>& r, int ti
 }
 
 // map values of keys key0 .. key0 + 3 on one query row (16-byte load when in range; zero past S)
+// (per-lane conditions: the compiler emits exec-masked branches around each load -- callers take map4_full, one
+// plain 16-byte load, on full tiles of a row length divisible by 4, a uniform condition)
+__device__ __forceinline__ f32x4_t map4_full(const float* row, int key0) {
+  return *reinterpret_cast<const f32x4_t*>(row + key0);
+}
 __device__ __forceinline__ f32x4_t map4(const float* row, int key0, int S) {
   if ((S & 3) == 0 && key0 + 3 < S) return *reinterpret_cast<const f32x4_t*>(row + key0);
   f32x4_t v;
@@ -171,10 +176,18 @@ __global__ __launch_bounds__(256) void attn_map_fwd_kernel(MapArgs a) {
   row_offsets<D>(roff, (int)ld, tid);
   f32x4_t nb[4], nc[4];
   auto fetch = [&](int k0) {
+    if ((S & 3) == 0 && k0 + TK <= S) {
 #pragma unroll
-    for (int kb = 0; kb < 4; ++kb) {
-      if constexpr (HB) nb[kb] = map4(a.bias + mrow, k0 + kb * 16 + 4 * g, S);
-      if constexpr (HC) nc[kb] = map4(a.cmap + mrow, k0 + kb * 16 + 4 * g, S);
+      for (int kb = 0; kb < 4; ++kb) {
+        if constexpr (HB) nb[kb] = map4_full(a.bias + mrow, k0 + kb * 16 + 4 * g);
+        if constexpr (HC) nc[kb] = map4_full(a.cmap + mrow, k0 + kb * 16 + 4 * g);
+      }
+    } else {
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) {
+        if constexpr (HB) nb[kb] = map4(a.bias + mrow, k0 + kb * 16 + 4 * g, S);
+        if constexpr (HC) nc[kb] = map4(a.cmap + mrow, k0 + kb * 16 + 4 * g, S);
+      }
     }
     load_tile<D>(nk, a.k + base, ld, k0, S, tid, roff);
     load_tile<D>(nv, a.v + base, ld, k0, S, tid, roff);
@@ -308,10 +321,18 @@ __global__ __launch_bounds__(256) void attn_map_dq_kernel(MapArgs a) {
   row_offsets<D>(roff, (int)ld, tid);
   f32x4_t nb[4], nc[4];
   auto fetch = [&](int k0) {
+    if ((S & 3) == 0 && k0 + TK <= S) {
 #pragma unroll
-    for (int kb = 0; kb < 4; ++kb) {
-      if constexpr (HB) nb[kb] = map4(a.bias + mrow, k0 + kb * 16 + 4 * g, S);
-      if constexpr (HC) nc[kb] = map4(a.cmap + mrow, k0 + kb * 16 + 4 * g, S);
+      for (int kb = 0; kb < 4; ++kb) {
+        if constexpr (HB) nb[kb] = map4_full(a.bias + mrow, k0 + kb * 16 + 4 * g);
+        if constexpr (HC) nc[kb] = map4_full(a.cmap + mrow, k0 + kb * 16 + 4 * g);
+      }
+    } else {
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) {
+        if constexpr (HB) nb[kb] = map4(a.bias + mrow, k0 + kb * 16 + 4 * g, S);
+        if constexpr (HC) nc[kb] = map4(a.cmap + mrow, k0 + kb * 16 + 4 * g, S);
+      }
     }
     load_tile<D>(nk, a.k + base, ld, k0, S, tid, roff);
     load_tile<D>(nv, a.v + base, ld, k0, S, tid, roff);
