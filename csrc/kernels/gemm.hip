@@ -293,6 +293,10 @@ static int g4w_queue_env() {
   static int v = [] { const char* e = getenv("OBST_G4W_QUEUE"); return e ? atoi(e) : 1; }();
   return v;
 }
+static int g4w_qsplit_env() {
+  static int v = [] { const char* e = getenv("OBST_G4W_QSPLIT"); return e ? atoi(e) : 0; }();
+  return v;
+}
 static unsigned* g4w_queue_slot(hipStream_t stream) {
   constexpr int RING = 256;
   static unsigned* ring = nullptr;
@@ -374,6 +378,18 @@ OBST_API int obst_gemm(const ObstGemmDesc* d, hipStream_t stream) {
         const double t = rounds * (d->K / c) * per_k +
                          (c > 1 ? (double)(c + (d->beta != 0.f ? 2 : 1)) * batch * d->M * d->N * 4.0 / 5e6 : 0.0);
         if (t < best * 0.98) { best = t; ks = c; }
+      }
+      // one tile per block leaves the tile queue nothing to balance: a block that starts late (beside the previous
+      // kernel's tail in the graph replay, or RCCL's kernels at N > 1) delays the whole product. Twice the split
+      // gives the queue two work items per block on average, for one more fold pass (OBST_G4W_QSPLIT=1; measured
+      // 148.9-149.1k vs 150.2k tokens/s without on the GPT-Neo-1.3B step: off)
+      if (g4w_qsplit_env() && g4w_queue_env() && d->tri == 0 && !d->kin && big_tiles * ks <= 256 &&
+          big_tiles * ks * 2 > 256) {
+        const int c = ks * 2;
+        const double fold = (double)(c + (d->beta != 0.f ? 2 : 1)) * batch * d->M * d->N * 4.0 / 5e6;
+        if (d->K % (64 * c) == 0 && d->K / c >= 512 && (size_t)c * batch * d->M * d->N * 4 <= (2ull << 30) &&
+            fold < 0.05 * (d->K / ks) * per_k)
+          ks = c;
       }
       if (ks > 1) {
         a.ws = splitk_workspace((size_t)ks * batch * d->M * d->N * sizeof(float));
