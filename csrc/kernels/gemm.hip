@@ -402,7 +402,7 @@ OBST_API int obst_gemm(const ObstGemmDesc* d, hipStream_t stream) {
     // the queue: dense products whose every tile has >= 3 K-tiles (the next tile is dequeued in a tile's first
     // K-tile and the DMA cursor needs it by the end of K-tile nk - 3), more tiles than one per block, no stamps
     if (g4w_queue_env() && d->tri == 0 && !d->kin && d->K / ks >= 192 && !g_4w_stamps &&
-        !(d->out_f32 && d->Zout) && tm * tn * batch * ks > 256)
+        tm * tn * batch * ks > 256)
       a.queue = g4w_queue_slot(stream);
     if (a.queue) ++g_4w_queue_calls;
     e = gemm4w_launch(&a, d->a_t, d->b_t, d->out_f32, batch, stream);

@@ -1307,9 +1307,13 @@ hipError_t launch4w(GemmArgs a, int batch, hipStream_t stream) {
       k = gemm4w_kernel<A_T, B_T, F32, false, NWV, G4W_SCH, (G4W_STG != 0), G4W_CPA, G4W_CPB, G4W_OPT, false, false,
                         true>;
       which = 4;
+    } else if (a.queue) {   // queued fp32 + bf16-copy products
+      k = gemm4w_kernel<A_T, B_T, F32, false, NWV, G4W_SCH, (G4W_STG != 0), G4W_CPA, G4W_CPB, G4W_ZCP_OPT, false,
+                        true, true>;
+      which = 5;
     }
   }
-  static bool attr[5] = {false, false, false, false, false};
+  static bool attr[6] = {false, false, false, false, false, false};
   if (!attr[which]) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr[which] = true;

@@ -736,7 +736,8 @@ def test_gemm_split_contraction_index(cuda, out_f32):
     _close(c.view(H, S, S).float().cpu(), ref, 3e-2, 2e-2, "split-index gemm")
 
 
-@pytest.mark.parametrize("b_t,tri,batch", [(0, 0, (3, 1)), (1, 1, (2, 3)), (1, 0, (1, 1))])
+@pytest.mark.parametrize("b_t,tri,batch", [(0, 0, (3, 1)), (1, 1, (2, 3)), (1, 0, (1, 1)), (0, 0, (150, 1)),
+                                           (1, 0, (75, 2))])
 @pytest.mark.parametrize("alpha", [1.0, -1.0])
 def test_gemm_fp32_stream_update_with_bf16_copy(cuda, b_t, tri, batch, alpha):
     """the fused RevNet stream update (F.StreamSink): C = R + alpha * A.B in fp32 with Zout = bf16(C), written by
@@ -753,12 +754,13 @@ def test_gemm_fp32_stream_update_with_bf16_copy(cuda, b_t, tri, batch, alpha):
     bs = bm.transpose(1, 2).contiguous() if b_t == 0 else bm     # stored [N][K] (K-contiguous) or [K][N]
     c = torch.full((nb, M, N), float("nan"), device=cuda)
     z = torch.full((nb, M, N), float("nan"), device=cuda).to(BF)
-    c0 = g4w_calls()
+    c0, q0 = g4w_calls(), g4w_queue_calls()
     raw.gemm(raw.Operand(a.to(cuda), 0, K, b2 * M * K, M * K),
              raw.Operand(bs.to(cuda), b_t, K if b_t == 0 else N, b2 * K * N, K * N),
              raw.Operand(c, 0, N, b2 * M * N, M * N), M, N, K, batch=batch, alpha=alpha, R=r.to(cuda), Zout=z, tri=tri)
     torch.cuda.synchronize()
     assert g4w_calls() - c0 == 1
+    assert g4w_queue_calls() - q0 == (1 if tri == 0 and nb * 2 > 256 else 0), "tile queue use"
     ref = r + alpha * torch.matmul(a.float(), bm.float())
     _close(c, ref, 2e-2, 1e-2, f"stream update b_t={b_t} tri={tri}")
     assert torch.equal(z.cpu(), c.cpu().to(BF)), "Zout is not the bf16 copy of C"
