@@ -15,7 +15,6 @@ all: $(PKG)/_kernels.so $(if $(RSRC),$(PKG)/_runtime.so,)
 # attention: no SLP vectorisation -- adjacent f32 adds / multiplies packed into v_pk_*_f32 cost more issue cycles
 # than two scalar ops beside MFMAs (MI355X_MICROARCH.md, 'price of one filler beside MFMAs')
 build/kernels/attention.o: HIPFLAGS += -fno-slp-vectorize
-build/kernels/attn_fwd64.o: HIPFLAGS += -fno-slp-vectorize
 # attention-map kernels: MFMAs in the VGPR form -- the AGPR form kept the output accumulators in VGPRs across the
 # key loop and moved all of them into AGPRs and back every tile (profiles/r5_attn_map.md)
 build/kernels/attn_map.o: HIPFLAGS += -mllvm -amdgpu-mfma-vgpr-form

@@ -5,7 +5,9 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config configs/gpt_neo_1.3b.json] [--batch-per-gpu B]
                     [--tp T]
 
-N > 1 is launched by the driver with ``torch.distributed.run`` (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* in the env).
+N > 1 is launched by the driver with ``torch.distributed.run`` (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* in the env). A bare
+``python bench.py --gpus N`` (no WORLD_SIZE) starts ``torch.distributed.run`` itself as a CHILD process, before anything
+touches the GPU, and exits with its status (as ``main.py --gpus N`` does).
 Weak scaling: every DP replica processes ``batch-per-gpu`` sequences per step (global batch = B x N / T). ``--tp T``
 builds the reference's 2-D mesh (``src/dataclass.py:247-252``): ``Mesh(dp=N/T, tp=T)``, heads sharded over T
 contiguous ranks -- BASELINE's GPT-Neo-2.7B at DP4 x TP2 and the 20B-scale config at TP8.
@@ -18,6 +20,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -36,6 +40,17 @@ PEAK_BF16_DENSE = 2.5e15  # MI355X dense bf16 MFMA peak (spec, no sparsity)
 TORCH_EAGER_1GPU = 80262.0  # tools/torch_baseline.py --batch 32 on one MI355X (profiles/r2_torch_baseline.md)
 
 
+def _self_launch(n: int) -> int:
+    """one process per GPU: ``torch.distributed.run`` as a child (never an exec: nothing here has touched the GPU)"""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -52,24 +67,37 @@ def main():
     ap.add_argument("--depth", type=int, default=0, help="(debug only: invalidates the headline number)")
     # the whole training step replayed as one hipGraph on a single GPU (1077 -> 1058 ms/step: the ~1500 launches of
     # a step no longer leave host-side gaps); with N > 1 ranks the step stays eager (RCCL all-reduces overlap it)
+    # unless --hip-graphs-dist 1 (then with the fp32 all-reduce wire, the one the capture probe replays exactly)
     ap.add_argument("--hip-graphs", type=int, default=1, help="1: replay the captured training step (1 GPU)")
     ap.add_argument("--hip-graphs-dist", type=int, default=0,
                     help="1: capture the step with N > 1 ranks too (RCCL collectives inside the graph; opt-in)")
+    ap.add_argument("--device", default="cuda", choices=("cuda", "cpu"),
+                    help="cpu: rehearse the launcher and the N-rank step on gloo (no GPU; not a measurement)")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(_self_launch(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one process per GPU)")
         raise SystemExit(f"WORLD_SIZE={world} != --gpus {args.gpus}")
+    cpu = args.device == "cpu"
     # OBST_DIST_BACKEND=gloo rehearses the N-rank code path with several ranks sharing the visible GPUs (RCCL needs
     # one GPU per rank); the measured numbers always use the default, RCCL ("nccl") with one process per GPU
-    backend = os.environ.get("OBST_DIST_BACKEND", "nccl")
-    local_dev = local_rank % max(torch.cuda.device_count(), 1) if backend != "nccl" else local_rank
-    torch.cuda.set_device(local_dev)
-    device = torch.device("cuda", local_dev)
+    backend = "gloo" if cpu else os.environ.get("OBST_DIST_BACKEND", "nccl")
+    if cpu:
+        args.hip_graphs = 0
+        local_dev = 0
+        device = torch.device("cpu")
+    else:
+        local_dev = local_rank % max(torch.cuda.device_count(), 1) if backend != "nccl" else local_rank
+        torch.cuda.set_device(local_dev)
+        device = torch.device("cuda", local_dev)
+
+    def sync():
+        if not cpu:
+            torch.cuda.synchronize()
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if backend == "nccl":
@@ -99,6 +127,10 @@ def main():
     if args.hip_graphs:
         overrides["use_hip_graphs"] = True
         overrides["hip_graphs_distributed"] = bool(args.hip_graphs_dist)
+        if args.hip_graphs_dist and dp > 1:
+            # the capturable DP wire: one fp32 all-reduce per bucket (the bf16 wire's all_to_all does not survive
+            # capture on this image, profiles/r6_rccl_capture.md)
+            overrides["allreduce_dtype"] = "float32"
     params = load_config(args.config, overrides)
     torch.manual_seed(1234 + rank)
     trainer = Trainer(params, device, mesh)
@@ -124,24 +156,25 @@ def main():
     for i in range(args.warmup):
         m = trainer.step(batches[i % len(batches)])
         if i == 0:
-            torch.cuda.synchronize()
+            sync()
             log(f"first step done ({time.time() - t_w:.1f}s) loss={float(m['loss']):.4f} "
-                f"peak mem {torch.cuda.max_memory_allocated(device) / 2**30:.1f} GiB")
+                f"peak mem {(0 if cpu else torch.cuda.max_memory_allocated(device)) / 2**30:.1f} GiB")
     trainer.prepare_graphs()    # record (not run) any step graph the warm-up has not captured: timed steps replay
     barrier()
-    torch.cuda.synchronize()
+    sync()
     obst_debug.comm_reset()
     t0 = time.perf_counter()
     for i in range(args.steps):
         m = trainer.step(batches[i % len(batches)])
-    torch.cuda.synchronize()
+    sync()
     barrier()
     t1 = time.perf_counter()
     elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=device)
     if world > 1:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     elapsed = float(elapsed)
-    peak = torch.tensor([torch.cuda.max_memory_allocated(device) / 2 ** 30], dtype=torch.float64, device=device)
+    peak = torch.tensor([0.0 if cpu else torch.cuda.max_memory_allocated(device) / 2 ** 30], dtype=torch.float64,
+                        device=device)
     if world > 1:
         dist.all_reduce(peak, op=dist.ReduceOp.MAX)
     peak = float(peak)

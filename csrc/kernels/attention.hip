@@ -1005,376 +1005,29 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd32_kernel(AttnArgs a)
   }
 }
 
-// D = 128 dK/dV with v_mfma_f32_32x32x16_bf16: block = 128 keys, wave w owns keys kw = kblk + 32w + [0, 32) (key
-// n = lane&31 on the lane, K and V of that key held in registers as B operands for the whole block). Per 32-query
-// sub-chunk: S = Q·Kᵀ and dP = dO·Vᵀ (queries on the 16 accumulator registers, A operands = Q / dO rows from LDS),
-// P = exp2(S·c2 - lse), dS = P·(dP - delta) (dP's accumulator starts at -delta), then dVᵀ += dOᵀ·P and dKᵀ += Qᵀ·dS
-// sum over the accumulators' ROW index, so P / dS feed the MFMA as B operands straight from the registers (permuted
-// k order) and the matching dOᵀ / Qᵀ A operands are read from the [q][d] LDS images with ds_read_b64_tr_b16.
-// Against the 16-keys-per-wave kernel this halves the LDS bytes per MFMA (every Q / dO fragment read from LDS now
-// serves 32 keys). Q, dO (64 rows), lse and delta (64 values) are double-buffered by LDS-DMA one chunk ahead.
-
-// S = Q·Kᵀ and dP = dO·Vᵀ - delta for one 32-query sub-chunk (accumulator register r <-> query row
-// 8(r>>2) + 4h + (r&3) of the sub-chunk)
-__device__ __forceinline__ void dkv32_scores(const char* sQ, const char* sD, const float* sDl, const Frag32& fo,
-                                             const bf16x8_t (&kf)[8], const bf16x8_t (&vf)[8], f32x16_t& s,
-                                             f32x16_t& dp, int sub, int lane) {
-  const int h = lane >> 5;
-  const int rb = sub * 32 * 256;
-  s = f32x16_t{};
-#pragma unroll
-  for (int a4 = 0; a4 < 4; ++a4) {
-    const float4 dl = *reinterpret_cast<const float4*>(sDl + sub * 32 + 8 * a4 + 4 * h);
-    dp[4 * a4 + 0] = -dl.x; dp[4 * a4 + 1] = -dl.y; dp[4 * a4 + 2] = -dl.z; dp[4 * a4 + 3] = -dl.w;
-  }
-#pragma unroll
-  for (int ks = 0; ks < 8; ++ks) {
-    const bf16x8_t qa = *reinterpret_cast<const bf16x8_t*>(sQ + fo.k[ks] + rb);
-    const bf16x8_t da = *reinterpret_cast<const bf16x8_t*>(sD + fo.k[ks] + rb);
-    s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, kf[ks], s, 0, 0, 0);
-    dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da, vf[ks], dp, 0, 0, 0);
-  }
-}
-
-// P = exp2(S·c2 - lse·log2e), dS = P·dP; then dVᵀ += dOᵀ·P, dKᵀ += Qᵀ·dS. Branch-free masking (a branch around
-// the MFMAs makes the compiler carry the dK/dV accumulators through VGPR<->AGPR copies): element r of the lane is
-// query row j = 8(r>>2) + (r&3) (+ the lane's 4h), so "key > q" is "j < tc" and "q >= S" is "j >= tq" with two
-// per-lane thresholds tc, tq and a compile-time j.
-__device__ __forceinline__ void dkv32_update(const char* sQ, const char* sD, const float* sL, const Frag32& fo,
-                                             f32x16_t& s, f32x16_t& dp, f32x16_t (&dk)[4], f32x16_t (&dv)[4],
-                                             int sub, int tc, int tq, float c2, int lane) {
-  const int h = lane >> 5;
-  const int rb = sub * 32 * 256;
-#pragma unroll
-  for (int a4 = 0; a4 < 4; ++a4) {
-    const float4 lv = *reinterpret_cast<const float4*>(sL + sub * 32 + 8 * a4 + 4 * h);
-    const float nl[4] = {-lv.x * LOG2E, -lv.y * LOG2E, -lv.z * LOG2E, -lv.w * LOG2E};
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      const int r = 4 * a4 + b, j = 8 * a4 + b;
-      float p = fexp2(__builtin_fmaf(s[r], c2, nl[b]));
-      p = (j < tc || j >= tq) ? 0.f : p;
-      s[r] = p;
-      dp[r] = p * dp[r];
-    }
-  }
-#pragma unroll
-  for (int st = 0; st < 2; ++st) {
-    const bf16x8_t pb = pack8(s, 8 * st);
-    const bf16x8_t sb = pack8(dp, 8 * st);
-    const int kb = rb + 16 * st * 256;
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      dv[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_pair(sD, fo.v[dt][0] + kb, fo.v[dt][1] + kb), pb, dv[dt],
-                                                       0, 0, 0);
-      dk[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_pair(sQ, fo.v[dt][0] + kb, fo.v[dt][1] + kb), sb, dk[dt],
-                                                       0, 0, 0);
-    }
-  }
-}
-
-// One 64-query chunk of the 32x32 dK/dV kernel as four MFMA phases of 16 MFMAs each, software-pipelined inside the
-// wave (the kernel runs one wave per SIMD: there is no partner wave to hide LDS latency or the softmax VALU):
-//   A: S/dP of sub-chunk 0          B: S/dP of sub-chunk 1  + softmax of sub-chunk 0 (2 elements per k-step)
-//   C: dV/dK update of sub-chunk 0  + softmax of sub-chunk 1        D: dV/dK update of sub-chunk 1
-// Every LDS fragment is read DKV32_PF steps ahead of its MFMA along the flat step sequence, and a sched_barrier per
-// step keeps the compiler from sinking the reads next to their use (the straight-line version waited out a full LDS
-// read in front of 45 of its 64 MFMAs).
-#ifndef DKV32_PF
-#define DKV32_PF 2
-#endif
-__device__ __forceinline__ void dkv32_softmax_pair(f32x16_t& s, f32x16_t& dp, const float (&nl)[16], int r0, int tc,
-                                                   int tq, float c2) {
-#pragma unroll
-  for (int r = r0; r < r0 + 2; ++r) {
-    const int j = 8 * (r >> 2) + (r & 3);
-    float p = fexp2(__builtin_fmaf(s[r], c2, nl[r]));
-    p = (j < tc || j >= tq) ? 0.f : p;
-    s[r] = p;
-    dp[r] = p * dp[r];
-  }
-}
-
-__device__ __forceinline__ void dkv32_chunk_pipe(const char* sQ, const char* sD, const float* sL, const float* sDl,
-                                                 const Frag32& fo, const bf16x8_t (&kf)[8], const bf16x8_t (&vf)[8],
-                                                 f32x16_t (&dk)[4], f32x16_t (&dv)[4], int tc0, int tq0, float c2,
-                                                 int lane) {
-  constexpr int PF = DKV32_PF, NB = PF + 1;
-  const int h = lane >> 5;
-  f32x16_t s[2], dp[2];
-  float nl[2][16];
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    s[u] = f32x16_t{};
-#pragma unroll
-    for (int a4 = 0; a4 < 4; ++a4) {
-      const float4 dl = *reinterpret_cast<const float4*>(sDl + u * 32 + 8 * a4 + 4 * h);
-      const float4 lv = *reinterpret_cast<const float4*>(sL + u * 32 + 8 * a4 + 4 * h);
-      dp[u][4 * a4 + 0] = -dl.x; dp[u][4 * a4 + 1] = -dl.y; dp[u][4 * a4 + 2] = -dl.z; dp[u][4 * a4 + 3] = -dl.w;
-      nl[u][4 * a4 + 0] = -lv.x * LOG2E; nl[u][4 * a4 + 1] = -lv.y * LOG2E;
-      nl[u][4 * a4 + 2] = -lv.z * LOG2E; nl[u][4 * a4 + 3] = -lv.w * LOG2E;
-    }
-  }
-  const int tc[2] = {tc0, tc0 - 32}, tq[2] = {tq0, tq0 - 32};
-  // phases A + B: 16 score steps t = 8u + ks
-  bf16x8_t qa[NB], da[NB];
-  auto ld_sc = [&](int t) {
-    const int o = fo.k[t & 7] + (t >> 3) * 32 * 256;
-    qa[t % NB] = *reinterpret_cast<const bf16x8_t*>(sQ + o);
-    da[t % NB] = *reinterpret_cast<const bf16x8_t*>(sD + o);
-  };
-#pragma unroll
-  for (int t = 0; t < PF; ++t) ld_sc(t);
-#pragma unroll
-  for (int t = 0; t < 16; ++t) {
-    if (t + PF < 16) ld_sc(t + PF);
-    __builtin_amdgcn_sched_barrier(0);
-    const int u = t >> 3, ks = t & 7;
-    s[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa[t % NB], kf[ks], s[u], 0, 0, 0);
-    dp[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da[t % NB], vf[ks], dp[u], 0, 0, 0);
-    if (u == 1) dkv32_softmax_pair(s[0], dp[0], nl[0], 2 * ks, tc[0], tq[0], c2);
-  }
-  // phases C + D: 16 update steps t = 8u + 4st + dt; the transposed Vᵀ-side operands: dOᵀ (for dV) and Qᵀ (for dK)
-  bf16x8_t ot[NB], qt[NB];
-  auto ld_up = [&](int t) {
-    const int u = t >> 3, st = (t >> 2) & 1, dt = t & 3;
-    const int kb = u * 32 * 256 + 16 * st * 256;
-    ot[t % NB] = tr_pair(sD, fo.v[dt][0] + kb, fo.v[dt][1] + kb);
-    qt[t % NB] = tr_pair(sQ, fo.v[dt][0] + kb, fo.v[dt][1] + kb);
-  };
-#pragma unroll
-  for (int t = 0; t < PF; ++t) ld_up(t);
-  bf16x8_t pb = pack8(s[0], 0), sb = pack8(dp[0], 0);
-#pragma unroll
-  for (int t = 0; t < 16; ++t) {
-    const int u = t >> 3, st = (t >> 2) & 1, dt = t & 3;
-    if (t + PF < 16) ld_up(t + PF);
-    if (dt == 0 && t > 0) {
-      pb = pack8(s[u], 8 * st);
-      sb = pack8(dp[u], 8 * st);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    dv[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ot[t % NB], pb, dv[dt], 0, 0, 0);
-    dk[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qt[t % NB], sb, dk[dt], 0, 0, 0);
-    if (u == 0) dkv32_softmax_pair(s[1], dp[1], nl[1], 2 * t, tc[1], tq[1], c2);
-  }
-}
-
-__global__ __launch_bounds__(NTH, 1) void attn_bwd_dkv32_kernel(AttnArgs a) {
-  constexpr int D = 128;
-  constexpr int QC = 64;
-  constexpr int TILE = QC * 256;
-  constexpr int STAGE = 2 * TILE + 2 * 256;   // Q, dO, lse[64], delta[64]
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  // an AGPR named in inline asm keeps the compiler from inferring "no AGPRs": the MFMAs are then selected in the
-  // AGPR-accumulator form, so the 128 dK/dV accumulator registers live in AGPRs instead of being shuttled between
-  // the VGPR and AGPR files (v_accvgpr_read/write) when the kernel's >256 live registers overflow the VGPRs
-  asm volatile("" ::: "a255");
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, n = lane & 31;
-  int bx, bh;
-  attn_block((a.S + 127) / 128, bx, bh);
-  const int b = bh / a.H, hd = bh % a.H;
-  const int kblk = bx * 128;
-  const int kw = kblk + w * 32;
-  const int key = kw + n;
-  const long long base = (long long)b * a.S * a.ld + hd * D;
-  const long long sbase = ((long long)b * a.H + hd) * a.S;
-  const bf16_t* Qb = a.Q + base;
-  const bf16_t* Db = a.dO + (long long)b * a.S * a.ld_o + hd * D;   // dO rows at their own stride (ld_o)
-  const int qstart = a.causal ? (kblk / QC) * QC : 0;
-  const int nqc = (a.S - qstart + QC - 1) / QC;
-  const int wu = __builtin_amdgcn_readfirstlane(w);
-  unsigned soff[4], soffo[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int row = (wu + 4 * i) * 4 + (lane >> 4);
-    soff[i] = (unsigned)(row * (int)a.ld + (((lane & 15) ^ swz<128>(row)) << 3)) * 2u;
-    soffo[i] = (unsigned)(row * (int)a.ld_o + (((lane & 15) ^ swz<128>(row)) << 3)) * 2u;
-  }
-  auto stage = [&](char* buf, int q0) {
-    q0 = __builtin_amdgcn_readfirstlane(q0);
-    if (q0 + QC <= a.S) {
-      stage_full64(buf, Qb + (long long)q0 * a.ld, soff, wu);
-      stage_full64(buf + TILE, Db + (long long)q0 * a.ld_o, soffo, wu);
-    } else {
-      stage_rows64_asm<4>(buf, Qb + (long long)q0 * a.ld, a.ld, a.S - q0, wu, lane);
-      stage_rows64_asm<4>(buf + TILE, Db + (long long)q0 * a.ld_o, a.ld_o, a.S - q0, wu, lane);
-    }
-    if (wu < 2) {   // wave 0: lse, wave 1: delta (64 x 4 B, lane-linear)
-      const float* src = (wu == 0 ? a.LSE : a.delta) + sbase;
-      const int qq = min(q0 + lane, a.S - 1);
-      glds4_asm(src + qq, buf + 2 * TILE + wu * 256);
-    }
-  };
-  if (nqc > 0) stage(smem, qstart);
-
-  bf16x8_t kf[8], vf[8];
-#pragma unroll
-  for (int ks = 0; ks < 8; ++ks) {
-    kf[ks] = load_frag_g(a.K + base + (long long)key * a.ld + ks * 16 + 8 * h, key < a.S);
-    vf[ks] = load_frag_g(a.V + base + (long long)key * a.ld + ks * 16 + 8 * h, key < a.S);
-  }
-#pragma unroll
-  for (int ks = 0; ks < 8; ++ks) asm volatile("" ::"v"(kf[ks]), "v"(vf[ks]));
-  Frag32 fo;
-  frag32_offsets(fo, lane);
-  f32x16_t dk[4], dv[4];
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt) dk[dt] = dv[dt] = f32x16_t{};
-  const float c2 = a.scale * LOG2E;
-  vm_wait<0>();
-  __syncthreads();
-  for (int c = 0; c < nqc; ++c) {
-    const int q0 = qstart + c * QC;
-    const char* sQ = smem + (c & 1) * STAGE;
-    const char* sD = sQ + TILE;
-    const float* sL = reinterpret_cast<const float*>(sQ + 2 * TILE);
-    const float* sDl = sL + 64;
-    if (c + 1 < nqc) stage(smem + ((c + 1) & 1) * STAGE, q0 + QC);
-    if (DKV32_PF > 0) {
-      const int rel = q0 + 4 * h;
-      dkv32_chunk_pipe(sQ, sD, sL, sDl, fo, kf, vf, dk, dv, a.causal ? key - rel : -1000000, a.S - rel, c2, lane);
-    } else {   // both sub-chunks straight-line: the score MFMAs of sub-chunk 1 overlap the softmax VALU of sub-chunk 0
-      f32x16_t s0, dp0, s1, dp1;
-      dkv32_scores(sQ, sD, sDl, fo, kf, vf, s0, dp0, 0, lane);
-      dkv32_scores(sQ, sD, sDl, fo, kf, vf, s1, dp1, 1, lane);
-      const int rel = q0 + 4 * h;                 // query of element j in sub-chunk u: rel + 32u + j
-      const int tc0 = a.causal ? key - rel : -1000000, tc1 = tc0 - 32;
-      const int tq0 = a.S - rel, tq1 = tq0 - 32;
-      dkv32_update(sQ, sD, sL, fo, s0, dp0, dk, dv, 0, tc0, tq0, c2, lane);
-      dkv32_update(sQ, sD, sL, fo, s1, dp1, dk, dv, 1, tc1, tq1, c2, lane);
-    }
-    vm_wait<0>();
-    __syncthreads();
-  }
-  if (key < a.S) {
-    bf16_t* krow = a.dK + base + (long long)key * a.ld;
-    bf16_t* vrow = a.dV + base + (long long)key * a.ld;
-    const float sc = a.scale;
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const int d = dt * 32 + 8 * g4 + 4 * h;
-        *reinterpret_cast<uint2*>(krow + d) =
-            make_uint2(pack_bf16x2(dk[dt][4 * g4] * sc, dk[dt][4 * g4 + 1] * sc),
-                       pack_bf16x2(dk[dt][4 * g4 + 2] * sc, dk[dt][4 * g4 + 3] * sc));
-        *reinterpret_cast<uint2*>(vrow + d) =
-            make_uint2(pack_bf16x2(dv[dt][4 * g4], dv[dt][4 * g4 + 1]), pack_bf16x2(dv[dt][4 * g4 + 2], dv[dt][4 * g4 + 3]));
-      }
-  }
-}
-
-static int attn_impl() {   // OBST_ATTN_IMPL=1 forces the 16x16x32 kernels (A/B comparisons)
-  static int v = [] { const char* e = getenv("OBST_ATTN_IMPL"); return e ? atoi(e) : 2; }();
-  return v;
-}
-
-// OBST_ATTN_BWD=2 selects the 32x32x16 dK/dV kernel; 3 (4 / 5: dQ / dK-dV only) the 8-wave blocks with 3-deep LDS
-// rings. A/B only: at B64 S2048 H16 D128 causal the default pair takes 5.23 ms, 3 / 4 / 5 take 5.86 / 5.68 / 5.61 ms
-// (the longer blocks lose more to the causal-diagonal imbalance than the deeper ring gains; r2 bench_attn_ab).
-// Round 3: the 32x32 dK/dV kernel software-pipelined (dkv32_chunk_pipe) and with dO at its own stride, so it also
-// runs on the step's interleaved k|q|v layout: 3.71 ms against 3.01 ms for the default 16x16 kernel at that shape
-// (rocprofv3, profiles/r3_attn_bwd_ab.md) -- one wave per SIMD, ~8k clocks per 64-query chunk for 2k of MFMA
-// OBST_ATTN_DKV_KG=2: two 16-key groups per dK/dV wave (half the LDS bytes per MFMA, ~490 registers: one wave per
-// SIMD). A/B only: B64 S2048 H16 D128 causal backward 5.24 -> 6.27 ms (3-deep ring: 6.33) -- without the partner
-// wave the softmax VALU and the LDS waits no longer hide under another wave's MFMAs (r2 tools/lab/gpu_attn_kg.sh)
-static int attn_dkv_kg() {
-  static int v = [] { const char* e = getenv("OBST_ATTN_DKV_KG"); return e ? atoi(e) : 1; }();
-  return v;
-}
-
-// OBST_ATTN_FWD_RING=4: forward over 32-key tiles in a 4-deep LDS-DMA ring. A/B only: B64 S2048 H16 D128 causal
-// 1.37 -> 1.47 ms (unlike the dQ kernel, the forward's 64-key tiles already cover the DMA latency; halving them
-// doubles the barriers and the row max / rescale work per key)
-static int attn_fwd_ring() {
-  static int v = [] { const char* e = getenv("OBST_ATTN_FWD_RING"); return e ? atoi(e) : 2; }();
-  return v;
-}
-
-// OBST_ATTN_FWD_NW=8: forward blocks of 8 waves / 256 queries (one block per CU) instead of 4 waves / 128 queries
-static int attn_fwd_nw() {
-  static int v = [] { const char* e = getenv("OBST_ATTN_FWD_NW"); return e ? atoi(e) : 4; }();
-  return v;
-}
-
-static int attn_dq_ring() {   // OBST_ATTN_DQ_RING=4: dQ kernel over 32-key tiles, 4-deep LDS-DMA ring
-  static int v = [] { const char* e = getenv("OBST_ATTN_DQ_RING"); return e ? atoi(e) : 4; }();
-  return v;
-}
-
-// OBST_ATTN_DKV_RING=4: dK/dV kernel over 32-query chunks in a 4-deep LDS-DMA ring. A/B only: B64 S2048 H16 D128
-// causal backward 4.98 -> 5.59 ms (the dK/dV loop is bound by its LDS reads, not by the DMA latency the deeper ring
-// hides; half-size chunks double its barriers and lse/delta reads). The dQ kernel's ring of 32-key tiles (default
-// since r2) took the backward 5.21 -> 4.99 ms.
-static int attn_dkv_ring() {
-  static int v = [] { const char* e = getenv("OBST_ATTN_DKV_RING"); return e ? atoi(e) : 2; }();
-  return v;
-}
-
-static int attn_bwd_impl() {
-  static int v = [] { const char* e = getenv("OBST_ATTN_BWD"); return e ? atoi(e) : 1; }();
-  return v;
-}
-
+// Dispatch. D = 128 (every shipped config) takes the 32x32x16 forward and the dQ kernel over 32-key tiles in a 4-deep
+// LDS-DMA ring; other head sizes take the 16x16x32 forward. Alternatives measured slower and removed in round 6 (the
+// numbers stay in git history and profiles/): the one-wave-per-SIMD forward attn_fwd64 (1.76 vs 1.42 ms,
+// profiles/r5_attn_fwd64.md), 8-wave forward / backward blocks with 3-deep rings (5.86 / 5.68 / 5.61 vs 5.23 ms), the
+// 32x32x16 dK/dV kernel (3.71 vs 3.01 ms, profiles/r3_attn_bwd_ab.md), two 16-key groups per dK/dV wave (6.27 vs
+// 5.24 ms), the forward over 32-key tiles (1.47 vs 1.37 ms) and dK/dV over 32-query chunks (5.59 vs 4.98 ms).
 template <int D>
 int launch_fwd(const AttnArgs& a, hipStream_t st) {
   dim3 grid((a.S + 127) / 128 * a.B * a.H);
-  if (D == 128 && attn_impl() == 3) {   // one wave per SIMD, 64 queries per wave, pipelined softmax
-    return attn_fwd64_launch(&a, st);
-  }
-  if (D == 128 && attn_impl() == 2) {
-    if (attn_fwd_nw() == 8) {
-      dim3 g8((a.S + 255) / 256 * a.B * a.H);
-      hipLaunchKernelGGL((attn_fwd32_kernel<64, 8>), g8, dim3(512), 2 * 2 * 64 * 256, st, a);
-    } else if (attn_fwd_ring() == 4) {
-      hipLaunchKernelGGL(attn_fwd32_kernel<32>, grid, dim3(NTH), 4 * 2 * 32 * 256, st, a);
-    } else {
-      hipLaunchKernelGGL(attn_fwd32_kernel<64>, grid, dim3(NTH), 2 * 2 * 64 * 256, st, a);
-    }
-    return (int)hipGetLastError();
-  }
-  hipLaunchKernelGGL(attn_fwd_kernel<D>, grid, dim3(NTH), 4 * 64 * Geo<D>::ROWB, st, a);
+  if (D == 128)
+    hipLaunchKernelGGL(attn_fwd32_kernel<64>, grid, dim3(NTH), 2 * 2 * 64 * 256, st, a);
+  else
+    hipLaunchKernelGGL(attn_fwd_kernel<D>, grid, dim3(NTH), 4 * 64 * Geo<D>::ROWB, st, a);
   return (int)hipGetLastError();
 }
 
 template <int D>
 int launch_bwd(const AttnArgs& a, hipStream_t st) {
   // dQ first: it also produces delta = rowsum(dO * O), which the dK/dV kernel reads
-  const int impl = attn_bwd_impl();
-  if (D == 128 && impl >= 3) {   // 8-wave blocks, 3-deep LDS rings (one block per CU): 3 both, 4 dQ only, 5 dK/dV only
-    if (impl != 5)
-      hipLaunchKernelGGL((attn_bwd_dq_kernel<D, 8, 3>), dim3((a.S + 255) / 256 * a.B * a.H), dim3(512),
-                         3 * 2 * 64 * Geo<D>::ROWB, st, a);
-    else
-      hipLaunchKernelGGL(attn_bwd_dq_kernel<D>, dim3((a.S + 127) / 128 * a.B * a.H), dim3(NTH),
-                         4 * 64 * Geo<D>::ROWB, st, a);
-    if (impl != 4)
-      hipLaunchKernelGGL((attn_bwd_dkv_kernel<D, 8, 3>), dim3((a.S + 127) / 128 * a.B * a.H), dim3(512),
-                         3 * (2 * 64 * Geo<D>::ROWB + 512), st, a);
-    else
-      hipLaunchKernelGGL(attn_bwd_dkv_kernel<D>, dim3((a.S + 63) / 64 * a.B * a.H), dim3(NTH),
-                         2 * (2 * 64 * Geo<D>::ROWB + 512), st, a);
-    return (int)hipGetLastError();
-  }
-  if (attn_dq_ring() == 4)   // 32-key K/V tiles in a 4-deep ring (same 64 KiB of LDS)
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<D, 4, 4, 32>), dim3((a.S + 127) / 128 * a.B * a.H), dim3(NTH),
-                       4 * 2 * 32 * Geo<D>::ROWB, st, a);
-  else
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<D>, dim3((a.S + 127) / 128 * a.B * a.H), dim3(NTH), 4 * 64 * Geo<D>::ROWB,
-                       st, a);
-  if (D == 128 && attn_bwd_impl() == 2)
-    hipLaunchKernelGGL(attn_bwd_dkv32_kernel, dim3((a.S + 127) / 128 * a.B * a.H), dim3(NTH), 2 * (2 * 64 * 256 + 512),
-                       st, a);
-  else if (attn_dkv_ring() == 4)   // 32-query chunks in a 4-deep ring (the same 66 KiB of LDS)
-    hipLaunchKernelGGL((attn_bwd_dkv_kernel<D, 4, 4, 1, 32>), dim3((a.S + 63) / 64 * a.B * a.H), dim3(NTH),
-                       4 * (2 * 32 * Geo<D>::ROWB + 512), st, a);
-  else if (attn_dkv_kg() == 2)
-    hipLaunchKernelGGL((attn_bwd_dkv_kernel<D, 4, 2, 2>), dim3((a.S + 127) / 128 * a.B * a.H), dim3(NTH),
-                       2 * (2 * 64 * Geo<D>::ROWB + 512), st, a);
-  else
-    hipLaunchKernelGGL(attn_bwd_dkv_kernel<D>, dim3((a.S + 63) / 64 * a.B * a.H), dim3(NTH),
-                       2 * (2 * 64 * Geo<D>::ROWB + 512), st, a);
+  hipLaunchKernelGGL((attn_bwd_dq_kernel<D, 4, 4, 32>), dim3((a.S + 127) / 128 * a.B * a.H), dim3(NTH),
+                     4 * 2 * 32 * Geo<D>::ROWB, st, a);
+  hipLaunchKernelGGL(attn_bwd_dkv_kernel<D>, dim3((a.S + 63) / 64 * a.B * a.H), dim3(NTH),
+                     2 * (2 * 64 * Geo<D>::ROWB + 512), st, a);
   return (int)hipGetLastError();
 }
 

@@ -1,6 +1,6 @@
-// Shared device helpers of the attention kernels (attention.hip, attn_fwd64.hip): LDS image swizzles, LDS-DMA
-// staging, fragment offsets, the XCD-aware block map, the kernel argument block. Included inside an anonymous
-// namespace by each translation unit; the argument block crosses TUs only by address (attn_fwd64_launch).
+// Shared device helpers of the attention kernels (attention.hip; the lab's attn_fwd64.hip): LDS image swizzles,
+// LDS-DMA staging, fragment offsets, the XCD-aware block map, the kernel argument block. Included inside an
+// anonymous namespace by each translation unit.
 #pragma once
 #include "common.h"
 #include <stdlib.h>
@@ -279,5 +279,3 @@ __device__ __forceinline__ void stage_rows64_asm(char* lds, const bf16_t* g, lon
 
 }  // namespace
 
-// forward kernel of attn_fwd64.hip (its own TU: built with the VGPR form of the MFMAs); `args` is an AttnArgs
-int attn_fwd64_launch(const void* args, hipStream_t st);

@@ -293,8 +293,8 @@ static int g4w_queue_env() {
   static int v = [] { const char* e = getenv("OBST_G4W_QUEUE"); return e ? atoi(e) : 1; }();
   return v;
 }
-static int g4w_qsplit_env() {
-  static int v = [] { const char* e = getenv("OBST_G4W_QSPLIT"); return e ? atoi(e) : 0; }();
+static int g4w_queue_tri_env() {   // the triangular (token-mixer) products on the queue too (0: static walk)
+  static int v = [] { const char* e = getenv("OBST_G4W_QUEUE_TRI"); return e ? atoi(e) : 1; }();
   return v;
 }
 static unsigned* g4w_queue_slot(hipStream_t stream) {
@@ -379,18 +379,8 @@ OBST_API int obst_gemm(const ObstGemmDesc* d, hipStream_t stream) {
                          (c > 1 ? (double)(c + (d->beta != 0.f ? 2 : 1)) * batch * d->M * d->N * 4.0 / 5e6 : 0.0);
         if (t < best * 0.98) { best = t; ks = c; }
       }
-      // one tile per block leaves the tile queue nothing to balance: a block that starts late (beside the previous
-      // kernel's tail in the graph replay, or RCCL's kernels at N > 1) delays the whole product. Twice the split
-      // gives the queue two work items per block on average, for one more fold pass (OBST_G4W_QSPLIT=1; measured
-      // 148.9-149.1k vs 150.2k tokens/s without on the GPT-Neo-1.3B step: off)
-      if (g4w_qsplit_env() && g4w_queue_env() && d->tri == 0 && !d->kin && big_tiles * ks <= 256 &&
-          big_tiles * ks * 2 > 256) {
-        const int c = ks * 2;
-        const double fold = (double)(c + (d->beta != 0.f ? 2 : 1)) * batch * d->M * d->N * 4.0 / 5e6;
-        if (d->K % (64 * c) == 0 && d->K / c >= 512 && (size_t)c * batch * d->M * d->N * 4 <= (2ull << 30) &&
-            fold < 0.05 * (d->K / ks) * per_k)
-          ks = c;
-      }
+      // (doubling ks so that one-tile-per-block products give the queue two items per block lost on the
+      // GPT-Neo-1.3B step, 148.9-149.1k vs 150.2k tokens/s: removed in round 6, profiles/r5_summary.md)
       if (ks > 1) {
         a.ws = splitk_workspace((size_t)ks * batch * d->M * d->N * sizeof(float));
         if (!a.ws) ks = 1;
@@ -399,10 +389,14 @@ OBST_API int obst_gemm(const ObstGemmDesc* d, hipStream_t stream) {
     if (d->tri == 3 && ks < 2) goto fallback;   // (no workspace: the 128x128 kernel masks in its epilogue)
     a.ksplit = ks;
     a.kin_bps = d->kin ? d->K / ks / d->kin : 0;
-    // the queue: dense products whose every tile has >= 3 K-tiles (the next tile is dequeued in a tile's first
-    // K-tile and the DMA cursor needs it by the end of K-tile nk - 3), more tiles than one per block, no stamps
-    if (g4w_queue_env() && d->tri == 0 && !d->kin && d->K / ks >= 192 && !g_4w_stamps &&
-        tm * tn * batch * ks > 256)
+    // the queue: products whose every tile has >= 3 K-tiles (the next tile is dequeued in a tile's first K-tile
+    // and the DMA cursor needs it by the end of K-tile nk - 3), more tiles than one per block, no stamps. Dense, or
+    // triangular A (the token mixer, OBST_G4W_QUEUE_TRI): tri 1 tile rows span min(K, m0 + 256), tri 2 K - m0 --
+    // the shortest is the first / last tile row
+    const bool tri_nk3 = (d->tri == 1 && (d->K < 256 ? d->K : 256) >= 192) ||
+                         (d->tri == 2 && d->K - (tm - 1) * 256 >= 192);
+    if (g4w_queue_env() && (d->tri == 0 || (tri_nk3 && g4w_queue_tri_env())) && !d->kin && d->K / ks >= 192 &&
+        !g_4w_stamps && tm * tn * batch * ks > 256)
       a.queue = g4w_queue_slot(stream);
     if (a.queue) ++g_4w_queue_calls;
     e = gemm4w_launch(&a, d->a_t, d->b_t, d->out_f32, batch, stream);

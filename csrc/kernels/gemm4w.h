@@ -467,7 +467,8 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
   // because another kernel (RCCL's collectives at N > 1) holds CUs beside it simply takes fewer tiles. Wave 0
   // dequeues the NEXT tile at the start of the current tile's first K-tile (one returning vector atomic), the
   // K-tile's own vmcnt wait retires it, wave 0 passes it through LDS before that K-tile's barrier; the DMA cursor
-  // needs it by the end of K-tile nk - 3 (the host enables the queue only for dense products with nk >= 3).
+  // needs it by the end of K-tile nk - 3 (the host enables the queue only when every tile has nk >= 3: dense
+  // products and the triangular token-mixer products, whose tiles are dequeued in decreasing-work order).
   constexpr bool QUEUE = QUE && !RELAX && !LATE && !KINT && !STG;
 
   static_assert(!(RELAX && LATE), "RELAX peels the first K-tile, LATE the last: not both");
@@ -490,16 +491,19 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
   const long long total = KIN ? tiles_total(p) : (long long)p.tiles_m * p.tiles_n * p.nbatch;
   const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3, nslot = gridDim.x >> 3;
   const long long Q = total >> 3, Rm = total & 7;
-  // dense: XCD x walks a contiguous run of tiles (L2 sharing of A / B panels); triangular A: block-cyclic over the
-  // whole grid (decode4 orders the tiles by work, so each round is balanced); tri 3: tiles of equal work, dense walk
+  // XCD x owns a run of logical tiles, its local index j -> tile gidx(j), walked by its blocks from slot (static
+  // deal: j = slot, slot + nslot, ...; the queue: the first tile static, then j = nslot + dequeued index).
+  // dense: a contiguous run (L2 sharing of A / B panels); triangular A: tiles x, x + 8, x + 16, ... -- decode4
+  // orders the tiles by decreasing work, so every XCD takes its tiles heaviest first and the 8 XCDs get equal work
+  // (the batch index runs fastest: XCD x keeps the heads of one residue class in its L2); tri 3: tiles of equal
+  // work, dense walk
   const bool cyc = KIN ? (p.tri == 1 || p.tri == 2) : p.tri != 0;
   const long long start = cyc ? 0 : xcd < Rm ? xcd * (Q + 1) : Rm * (Q + 1) + (xcd - Rm) * Q;
-  const long long len = cyc ? total : Q + (xcd < Rm ? 1 : 0);
-  const long long first = cyc ? blockIdx.x : slot;
-  const long long stride = cyc ? gridDim.x : nslot;
-  const int ntiles = (int)(len > first ? (len - first + stride - 1) / stride : 0);   // tiles of this block
+  const long long len = cyc ? (total > xcd ? (total - xcd + 7) >> 3 : 0) : Q + (xcd < Rm ? 1 : 0);
+  auto gidx = [&](long long j) { return cyc ? xcd + 8 * j : start + j; };
+  const int ntiles = (int)(len > slot ? (len - slot + nslot - 1) / nslot : 0);   // statically dealt tiles
   if (ntiles == 0) return;   // (a small launch: the grid is rounded up to the 8 XCDs)
-  auto logical = [&](int r) { return start + first + (long long)r * stride; };
+  auto logical = [&](int r) { return gidx(slot + (long long)r * nslot); };
   const long long astep = A_T == 0 ? 128 : 128 * p.lda;
   const long long bstep = B_T == 0 ? 128 : 128 * p.ldb;
 
@@ -562,7 +566,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
     unsigned v;
     asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(q_slot) : "memory");
     const long long i = (long long)__builtin_amdgcn_readfirstlane(v);
-    q_next = nslot + i < len ? start + nslot + i : -1;
+    q_next = nslot + i < len ? gidx(nslot + i) : -1;
   };
   i32x4_t ra, rb;
   auto dma_setup = [&]() {   // resources of the cursor's K-tile

@@ -610,6 +610,18 @@ def _mixer_fast_ok(args: BlockArgs, x: Act, dim: Dim) -> bool:
             x.dims[2:] == list(p.feature_dims))
 
 
+def _note_mixer(args: BlockArgs, dim: Dim, causal: bool, before) -> None:
+    """FLOP meter (models/model.py:count_flops_per_token): one token-mixer application costs 2 x features x (mixed
+    positions) FLOPs per token forward, 3x that for training -- not 6 x its weight, which depth-shared mixers reuse
+    at every application. Recorded once per application during the register pass."""
+    if before is None:
+        return
+    store = args.builder.store
+    n_t = (dim.size + 1) / 2 if causal else dim.size
+    store.mixer_flops = getattr(store, "mixer_flops", 0.0) + 3 * 2 * args.params.features * n_t
+    store.mixer_vars = getattr(store, "mixer_vars", set()) | (set(store.specs) - before)
+
+
 def attention(args: BlockArgs) -> Act:
     """ref spatial.py:42-81 (all variants). Fast path: dot_product + context (causal flash attention)."""
     p = args.params
@@ -655,14 +667,18 @@ def attention(args: BlockArgs) -> Act:
         kv = args.builder.kv
         if kv is not None and causal:
             return _mixer_kv(args, kv, x, dim, tmp, causal)
+        before = set(args.builder.store.specs) if args.builder.register else None
         bias = embed(args, [p.head_dim, dim, tmp])
+        _note_mixer(args, dim, causal, before)
         return Act(F.token_mixer(x.t, bias.t, causal, sink=getattr(args, "stream_sink", None)), x.dims)
     fold = _fold_of(p, x.dims, dim) if FLASH_MAPS else None
     if (fold is not None and not fold.identity and args.builder.kv is None and 'biased_attention_map' in args
             and 'input_as_value' in args and not any(k in args for k in ('dot_product', 'biased_softmax',
                                                                            'scale_attention_map'))):
         # the learned token mixer over a non-sequence axis: the same K03 kernel on the folded input
+        before = set(args.builder.store.specs) if args.builder.register else None
         bias = embed(args, [p.head_dim, dim, tmp])
+        _note_mixer(args, dim, causal, before)
         return Act(fold.back(F.token_mixer(fold.fwd(x.t), bias.t, causal)), x.dims)
     if args.builder.kv is not None:
         args.builder.kv.unsupported = True     # the composable path below has no incremental form

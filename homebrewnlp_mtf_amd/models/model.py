@@ -437,9 +437,13 @@ def _bcast(pe: Act, like: Act) -> torch.Tensor:
 
 
 def count_flops_per_token(params: ModelParameter, store) -> float:
-    """training FLOPs per token: 6 x (matmul parameters touched per token) + attention score/value products."""
+    """training FLOPs per token: 6 x (matmul parameters touched per token) + attention score/value products + the
+    learned token mixers, counted per application (layers._note_mixer: 3 x 2 x features x mixed positions, the
+    causal half) and not as 6 x their weight -- a depth-shared [heads, S, S] mixer weight is one variable that
+    every block applies."""
     p = params
-    n_mm = sum(s.numel for s in store.specs.values() if len(s.local_shape) >= 2)
+    mixer_vars = getattr(store, "mixer_vars", set())
+    n_mm = sum(s.numel for n, s in store.specs.items() if len(s.local_shape) >= 2 and n not in mixer_vars)
     emb = sum(s.numel for n, s in store.specs.items() if "gather" in n)
     attn = 0
     for cfg in p.block_configs:
@@ -450,4 +454,4 @@ def count_flops_per_token(params: ModelParameter, store) -> float:
     d = p.features
     # causal: half the S x S products; fwd 2 products x 2 FLOP, bwd 2x fwd
     attn_flops = attn * p.depth * 3 * 2 * 2 * S * d / 2
-    return 6.0 * (n_mm - emb) + attn_flops
+    return 6.0 * (n_mm - emb) + attn_flops + float(getattr(store, "mixer_flops", 0.0))

@@ -109,7 +109,7 @@ class Trainer:
 
     # ---------------------------------------------------------------------------------------------------------------
     # Whole-step hipGraph (``use_hip_graphs``): the device work of a training step -- forward, backward (every HIP
-    # kernel, hipBLASLt GEMM and allocation of the step), the fused optimizer -- is captured once and replayed, so
+    # kernel, gemm4w GEMM and allocation of the step), the fused optimizer -- is captured once and replayed, so
     # the host issues one graph launch per step instead of ~1000 kernel launches. The values that change between
     # steps live on the device (input tokens copied into static buffers, [lr, step] read by the optimizer kernels);
     # the SM3 accumulators alternate between two buffers, so one graph is captured per parity.
@@ -117,9 +117,12 @@ class Trainer:
         p = self.params
         dropout = p.input_dropout > 0 or "dropout" in str(p.block_config)
         # world > 1: RCCL collectives can be captured (async all-reduce + wait become graph nodes), but only on the
-        # nccl backend and only as an opt-in (hip_graphs_distributed): gloo runs on the host and cannot be captured
+        # nccl backend and only as an opt-in (hip_graphs_distributed): gloo runs on the host and cannot be captured.
+        # The bf16 DP wire's all_to_all crashes inside hipStreamEndCapture on this image (round 6 probe:
+        # profiles/r6_rccl_capture.md), so a captured multi-rank step needs the fp32 all-reduce wire
         multi_ok = self.mesh.world == 1 or (bool(getattr(p, "hip_graphs_distributed", False)) and dist.is_initialized()
-                                            and dist.get_backend() == "nccl")
+                                            and dist.get_backend() == "nccl"
+                                            and (self.mesh.dp == 1 or p.allreduce_dtype == "float32"))
         return (self.device.type == "cuda" and isinstance(self.opt, fused_opt.FusedOptimizer)
                 and multi_ok and int(p.grad_accumulation) == 1 and not dropout
                 and not getattr(self.store, "leaf_grads_seen", False) and not debug.CHECK)
@@ -161,7 +164,11 @@ class Trainer:
         graph = torch.cuda.CUDAGraph()
         torch.cuda.synchronize(self.device)
         before = debug.comm_bytes()
-        with torch.cuda.graph(graph, pool=g["pool"]):
+        # OBST_CAPTURE_MODE (global | thread_local | relaxed): what other host threads may do while this one captures.
+        # Multi-rank captures default to thread_local: ProcessGroupNCCL's watchdog polls its events from its own
+        # thread, which a global-mode capture turns into an error (tools/graph_capture_probe.py)
+        mode = os.environ.get("OBST_CAPTURE_MODE", "thread_local" if self.mesh.world > 1 else "global")
+        with torch.cuda.graph(graph, pool=g["pool"], capture_error_mode=mode):
             out = self._step_body(g["inputs"], lr)
         # collectives recorded while capturing = what every replay issues (replays run no host code to count them)
         after = debug.comm_bytes()

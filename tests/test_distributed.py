@@ -320,3 +320,24 @@ def test_adafactor_checkpoint_tp2_restores_at_tp1(tmp_path):
     l_new = float(tr.step(b)["loss"])
     assert abs(l_ref - l_new) < 1e-4 * abs(l_ref)
     assert (tr.store.master - ref.store.master).abs().max().item() < 5e-5
+
+
+def test_bench_bare_gpus2_self_launches():
+    """``python bench.py --gpus 2`` with no launcher env: bench.py starts torch.distributed.run as a child (one
+    process per rank), the ranks step over gloo on the CPU, and rank 0 prints the one JSON line"""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--device", "cpu",
+                        "--config", "configs/gpt_neo_125m_cpu.json", "--depth", "2", "--batch-per-gpu", "2",
+                        "--steps", "2", "--warmup", "1"],
+                       capture_output=True, text=True, env=env, timeout=600, cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rows = [json.loads(line) for line in r.stdout.splitlines() if line.startswith("{")]
+    assert len(rows) == 1, r.stdout[-2000:]
+    row = rows[0]
+    assert row["n_gpus"] == 2 and row["steps"] == 2 and row["warmup"] == 1 and row["value"] > 0
+    assert row["config"]["parallelism"] == "dp2" and row["config"]["global_batch"] == 4
+    assert row["config"]["dp_wire"] == "bfloat16" and row["config"]["comm_mib_per_step"]["dp_all_to_all"] > 0

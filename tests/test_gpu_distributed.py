@@ -131,24 +131,25 @@ def test_rccl_collectives_world1():
     assert len(rows) == 8 and all(x["backend"] == "nccl" and x["world"] == 1 and x["us"] > 0 for x in rows)
 
 
-@pytest.mark.parametrize("part", ["all_gather"])
-def test_rccl_graph_capture_world1(part):
-    """RCCL inside a captured graph on a one-rank nccl group (tools/graph_capture_probe.py): an async all_gather +
-    wait captured and replayed equals eager. The probe's other parts (all_reduce, all_to_all, the bf16 wire's
-    side-stream shape, the Trainer's whole-step capture) abort or crash inside RCCL at world 1 on this image
-    (SIGABRT / SIGSEGV, gpurun_out/r5c/capture.txt; docs/KNOBS.md), which is why the N > 1 step stays eager
-    (hip_graphs_distributed off); they are not run here because a crashing subprocess is an abort on the box."""
+@pytest.mark.parametrize("part,mode", [("all_reduce", "global"), ("all_reduce", "thread_local"),
+                                       ("all_gather", "thread_local"), ("trainer_fp32", "thread_local")])
+def test_rccl_graph_capture_world1(part, mode):
+    """RCCL inside a captured graph on a one-rank nccl group (tools/graph_capture_probe.py, launcher-free so the
+    child's own stderr is kept): an async all_reduce / all_gather + wait captured and replayed equals eager, and the
+    Trainer's whole-step capture with the fp32 all-reduce DP wire inside (GradSync forced on at world 1) replays the
+    eager run's losses and weights exactly. all_to_all (the bf16 wire and its side-stream shape) crashes inside
+    hipStreamEndCapture on this image (SIGSEGV in torch.cuda.graph's capture_end, profiles/r6_rccl_capture.md) and is
+    not run here: a crashing subprocess is an abort on the box. Multi-rank captures therefore use the fp32 wire."""
     import json
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, PYTHONPATH=root, HSA_ENABLE_IPC_MODE_LEGACY="0")
-    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "1", "--master-addr",
-                        "127.0.0.1", "--master-port", str(_free_port()),
-                        os.path.join(root, "tools", "graph_capture_probe.py"), "--part", part],
-                       capture_output=True, text=True, env=env, timeout=240)
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(PYTHONPATH=root, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run([sys.executable, os.path.join(root, "tools", "graph_capture_probe.py"), "--part", part,
+                        "--capture-mode", mode], capture_output=True, text=True, env=env, timeout=240)
     rows = [json.loads(line) for line in r.stdout.splitlines() if line.startswith("{")]
-    assert rows, f"exit {r.returncode} (no result line: the process died inside the capture)\n" + r.stderr[-1500:]
+    assert rows, f"exit {r.returncode} (no result line: the process died inside the capture)\n" + r.stderr[-3000:]
     print(rows[0])
     assert r.returncode == 0 and rows[0]["ok"], rows[0]
 

@@ -658,12 +658,14 @@ def test_token_mixer_big_tiles(cuda, causal, B, S):
     w = (torch.randn(H, S, S) * 0.05).to(BF)
     dy = (torch.randn(B, S, H, Fd) * 0.5).to(BF)
     xg, wg = x.to(cuda).requires_grad_(True), w.to(cuda).requires_grad_(True)
-    c0 = g4w_calls()
+    c0, q0 = g4w_calls(), g4w_queue_calls()
     y = F.token_mixer(xg, wg, causal)
     y.backward(dy.to(cuda))
     torch.cuda.synchronize()
     # y, dx and dW: all three products on gemm4w (no phase kernel left)
     assert g4w_calls() - c0 == (2 if causal and B % 2 else 3)
+    # y and dx (triangular A when causal) take the tile queue once they have more tiles than blocks; dW never does
+    assert g4w_queue_calls() - q0 == (2 if B * H * (S // 256) > 256 else 0)
     xf, wf = x.float().requires_grad_(True), w.float().requires_grad_(True)
     wm = torch.tril(wf) if causal else wf
     ref = torch.einsum("hst,bthf->bshf", wm, xf)

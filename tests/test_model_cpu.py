@@ -2,6 +2,7 @@
 grammar, initialisation statistics (the reference's own tests: tests/basic_linear_square_test.py,
 tests/basic_pointwise_test.py, tests/variable_test.py), and exact fp64 gradient checks of every body variant."""
 import math
+import os
 
 import pytest
 import torch
@@ -672,3 +673,20 @@ def test_relu_into_norm_gradient_fusion(strategy, monkeypatch):
     (la, ga), (lb, gb) = runs
     assert abs(la - lb) < 1e-6 * max(1.0, abs(la))
     assert torch.allclose(ga, gb, rtol=1e-4, atol=1e-6), (ga - gb).abs().max()
+
+
+def test_flop_meter_counts_every_token_mixer_application():
+    """ctx32_mixer (the reference's 32ctx_mixer config): the depth-shared [heads, S, S] mixer weights are counted per
+    application (2 per block x 32 blocks, 3 x S x d FLOPs per token each, causal half), not as 6 x their numel"""
+    from homebrewnlp_mtf_amd.config import load_config
+    from homebrewnlp_mtf_amd.models.model import Model, count_flops_per_token
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = load_config(os.path.join(root, "configs", "ctx32_mixer.json"), {"train_batch_size": 1})
+    store = Model(p, "cpu", finalize=False).builder.store
+    assert len(store.mixer_vars) == 2
+    S, d = p.sequence_length, p.features
+    dense = sum(s.numel for n, s in store.specs.items()
+                if len(s.local_shape) >= 2 and n not in store.mixer_vars and "gather" not in n)
+    expect = 6.0 * dense + 2 * p.depth * 3 * 2 * d * (S + 1) / 2
+    assert abs(count_flops_per_token(p, store) - expect) < 1e-6 * expect
+    assert 1.30e9 < count_flops_per_token(p, store) < 1.33e9

@@ -6,9 +6,15 @@ same code with ``--hip-graphs-dist 1``):
      the whole training step captured by ``Trainer`` (``use_hip_graphs`` + ``hip_graphs_distributed``, GradSync forced
      on at world 1) give the eager Trainer's losses and weights.
 
+  python tools/graph_capture_probe.py [--part P]          (one rank, no launcher: the child's own stderr is kept)
   python -m torch.distributed.run --nproc-per-node 1 --master-addr 127.0.0.1 tools/graph_capture_probe.py [--part P]
 
---part: all_reduce | all_to_all | all_gather | side_stream | trainer | all (default). Prints one JSON line per part as
+Without a launcher the probe sets RANK / WORLD_SIZE / MASTER_* itself, so a crash inside RCCL leaves its own text (not
+the elastic agent's ChildFailedError) on stderr; faulthandler prints the Python stack of a SIGSEGV / SIGABRT. Run it
+with NCCL_DEBUG=INFO TORCH_SHOW_CPP_STACKTRACES=1 for RCCL's and PyTorch's own account.
+
+--part: all_reduce | all_to_all | all_gather | side_stream | trainer | trainer_fp32 (the fp32 all-reduce wire) | all
+(default). Prints one JSON line per part as
 it completes (a crash inside a capture still leaves the earlier lines); exit status 1 when one fails.
 """
 from __future__ import annotations
@@ -24,6 +30,14 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def main():
+    import faulthandler
+    faulthandler.enable(all_threads=True)
+    if "WORLD_SIZE" not in os.environ:
+        import socket
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+        os.environ.update(RANK="0", LOCAL_RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     from homebrewnlp_mtf_amd.config import ModelParameter
     from homebrewnlp_mtf_amd.parallel import state as pstate
     from homebrewnlp_mtf_amd.run.trainer import Trainer
@@ -31,7 +45,14 @@ def main():
     import argparse
     ap = argparse.ArgumentParser()
     ap.add_argument("--part", default="all")
-    part = ap.parse_args().part
+    ap.add_argument("--capture-mode", default=os.environ.get("OBST_CAPTURE_MODE", "global"),
+                    choices=("global", "thread_local", "relaxed"),
+                    help="torch.cuda.graph capture_error_mode (the Trainer reads OBST_CAPTURE_MODE)")
+    args = ap.parse_args()
+    part = args.part
+    global CAPTURE_MODE
+    CAPTURE_MODE = args.capture_mode
+    os.environ["OBST_CAPTURE_MODE"] = CAPTURE_MODE
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
@@ -39,25 +60,30 @@ def main():
     ok_all = True
     for name, fn in (("all_reduce", _capture_all_reduce), ("all_to_all", _capture_all_to_all),
                      ("all_gather", _capture_all_gather), ("side_stream", _capture_side_stream),
-                     ("trainer", lambda d, o: _capture_trainer(d, o, ModelParameter, pstate, Trainer))):
+                     ("trainer", lambda d, o: _capture_trainer(d, o, ModelParameter, pstate, Trainer)),
+                     ("trainer_fp32", lambda d, o: _capture_trainer(d, o, ModelParameter, pstate, Trainer,
+                                                                    "float32"))):
         if part not in ("all", name):
             continue
-        out = {"part": name}
+        out = {"part": name, "capture_mode": CAPTURE_MODE}
         try:
             fn(dev, out)
         except Exception:
             import traceback
             out["error"] = traceback.format_exc()[-2500:]
-        if name == "trainer":
+        if name.startswith("trainer"):
             out["ok"] = bool("error" not in out and out.get("graphs_captured") == 2
                              and out.get("max_loss_diff", 1) < 1e-3 and out.get("max_weight_diff", 1) < 1e-4
-                             and "dp_all_to_all" in out.get("graph_comm", {}))
+                             and ("dp_all_to_all" in out.get("graph_comm", {}) or name == "trainer_fp32"))
         else:
             out["ok"] = bool("error" not in out and out.get("equal"))
         ok_all &= out["ok"]
         print(json.dumps(out), flush=True)
     dist.destroy_process_group()
     sys.exit(0 if ok_all else 1)
+
+
+CAPTURE_MODE = "global"
 
 
 def _capture(dev, fn):
@@ -69,7 +95,7 @@ def _capture(dev, fn):
     torch.cuda.current_stream().wait_stream(s)
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
+    with torch.cuda.graph(g, capture_error_mode=CAPTURE_MODE):
         fn()
     torch.cuda.synchronize()
     g.replay()
@@ -133,7 +159,7 @@ def _capture_all_reduce(dev, out):
         dist.all_reduce(y, async_op=True).wait()
     torch.cuda.current_stream().wait_stream(s)
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
+    with torch.cuda.graph(g, capture_error_mode=CAPTURE_MODE):
         y.copy_(x * 3.0)
         w = dist.all_reduce(y, async_op=True)
         w.wait()
@@ -144,13 +170,13 @@ def _capture_all_reduce(dev, out):
     out["equal"] = bool(torch.equal(z, eager + 1.0))
 
 
-def _capture_trainer(dev, out, ModelParameter, pstate, Trainer):
+def _capture_trainer(dev, out, ModelParameter, pstate, Trainer, wire="bfloat16"):
     # 2. Trainer step captured with the DP collectives inside (world 1, GradSync forced on)
     cfg = dict(model_mode="gpt", use_video=False, use_language=True, heads=4, features_per_head=64, depth=2,
                sequence_length=128, train_batch_size=4, vocab_size=512, intermediate_feed_forward_multiplier=2,
                memory_reduction_strategy="none", calculation_dtype="bfloat16", learning_rate=1e-4,
                optimizer="adaptive_clip:0.003-sm3-momentum:0.9:1:1-learning_rate", grad_bucket_mb=0.25,
-               force_grad_sync=True, allreduce_dtype="bfloat16",
+               force_grad_sync=True, allreduce_dtype=wire,
                block_config=[{"layer": ["norm-shift-scale", "attention-dot_product-context"], "skip": True},
                              {"layer": ["norm-shift-scale", "feed_forward-in:gelu"], "skip": True}])
     gen = torch.Generator().manual_seed(5)

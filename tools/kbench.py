@@ -11,6 +11,8 @@
 * attn_map  -- the biased_softmax / scale_attention_map kernels (csrc/kernels/attn_map.hip) at the same shape.
 * norm      -- norm fwd / bwd (+ residual gradient, + parameter gradients): GB/s of the bytes each must move.
 * ew        -- the streaming elementwise kernels (gelu fwd / bwd, add): GB/s.
+* gate      -- one row per hot-kernel family (GATE), each between its own two calibrations: the perf gate that
+               tests/test_gpu_perf_gate.py runs inside `pytest -m gpu`.
 
 Timing: every number is the MEDIAN of --reps (default 20) individually timed calls after two warm-up calls; where
 two implementations are compared their samples are interleaved call by call (cdna guide §5.4 rule 24).
@@ -167,7 +169,7 @@ def check(rows, floors: dict, tol: float = 0.03, ratios: typing.Optional[dict] =
     return bad
 
 
-def bench_gemm(T: int, reps: int):
+def bench_gemm(T: int, reps: int, only=None):
     d, i4, V = 2048, 8192, 50304
     shapes = [  # name, M, N, K, a_t, b_t, out_f32 (layouts as the step issues them)
         ("fwd d->4d", T, i4, d, 0, 0, False), ("fwd 4d->d", T, d, i4, 0, 0, False),
@@ -178,6 +180,8 @@ def bench_gemm(T: int, reps: int):
     ]
     dev = torch.device("cuda")
     for name, M, N, K, at, bt, f32 in shapes:
+        if only is not None and name not in only:
+            continue
         A = (torch.randn(M * K, device=dev) * 0.5).to(BF)
         B = (torch.randn(N * K, device=dev) * 0.5).to(BF)
         C = torch.zeros(M * N, device=dev, dtype=torch.float32 if f32 else BF)
@@ -189,7 +193,7 @@ def bench_gemm(T: int, reps: int):
         del A, B, C
 
 
-def bench_mixer(reps: int):
+def bench_mixer(reps: int, only=None):
     """the learned token mixer's GEMMs (K03, ctx32_mixer: 32 x 2048 tokens, 8 heads x 256) on gemm4w: y = tril(W) x
     (tri 1), dx = tril(W)^T dy (tri 2) and the weight gradient dW = dy . x^T over the split (batch, feature)
     contraction index into the lower-triangle tiles (kin = F, tri 3); effective TF/s count only the causal half"""
@@ -202,6 +206,9 @@ def bench_mixer(reps: int):
     hf = H * Fd
     fl = B * H * S * S * Fd   # 2 * S * S / 2 per (batch, head, feature)
     for name, a_t, tri in (("mixer y=tril(W)x", 0, 1), ("mixer dx=tril(W)^T dy", 1, 2)):
+        if only is not None and name not in only:
+            continue
+
         def run():
             raw.gemm(raw.Operand(w, a_t, S, 0, S * S), raw.Operand(x, 1, hf, S * hf, Fd),
                      raw.Operand(y, 0, hf, S * hf, Fd), S, Fd, S, batch=(B, H), tri=tri)
@@ -211,6 +218,8 @@ def bench_mixer(reps: int):
     def wgrad():
         raw.gemm(raw.Operand(y, 0, hf, 0, Fd), raw.Operand(x, 0, hf, 0, Fd), raw.Operand(gw, 0, S, 0, S * S),
                  S, S, B * Fd, batch=(1, H), beta=1.0, tri=3, kin=Fd, a_sk=S * hf, b_sk=S * hf)
+    if only is not None and "mixer dW=dy.x^T (kin, tri 3)" not in only:
+        return
     us = timed(wgrad, reps)
     emit(kernel="gemm", shape="mixer dW=dy.x^T (kin, tri 3)", us_gemm4w=round(us, 1),
          tflops_gemm4w=round(fl / us / 1e6, 1))
@@ -268,7 +277,7 @@ def bench_attn_map(B: int, reps: int):
          bias_grad_slices=bs)
 
 
-def bench_norm(T: int, reps: int):
+def bench_norm(T: int, reps: int, only=None):
     F = 2048
     dev = torch.device("cuda")
     x = (torch.randn(T * F, device=dev) * 2).to(BF)
@@ -277,16 +286,21 @@ def bench_norm(T: int, reps: int):
     y, dx = torch.empty_like(x), torch.empty_like(x)
     stats = torch.empty(2 * T, device=dev)
     dsc, dsh = torch.zeros(F, device=dev), torch.zeros(F, device=dev)
-    us = timed(lambda: raw.norm_fwd(x, sc, sh, y, stats, T, F, 1), reps)
-    emit(kernel="norm_fwd", rows=T, F=F, us=round(us, 1), gbps=round(2 * T * F * 2 / us / 1e3, 1))
+    if only is None or "norm_fwd" in only:
+        us = timed(lambda: raw.norm_fwd(x, sc, sh, y, stats, T, F, 1), reps)
+        emit(kernel="norm_fwd", rows=T, F=F, us=round(us, 1), gbps=round(2 * T * F * 2 / us / 1e3, 1))
+    else:   # the backward reads the forward's statistics
+        raw.norm_fwd(x, sc, sh, y, stats, T, F, 1)
     for name, R, params in (("norm_bwd+R+params", r, True), ("norm_bwd+R", r, False), ("norm_bwd", None, False)):
+        if only is not None and name not in only:
+            continue
         args = (dsc, dsh) if params else (None, None)
         us = timed(lambda: raw.norm_bwd(x, dy, sc, stats, dx, args[0], args[1], T, F, 1, F, R=R), reps)
         nbytes = (3 + (1 if R is not None else 0)) * T * F * 2
         emit(kernel=name, rows=T, F=F, us=round(us, 1), gbps=round(nbytes / us / 1e3, 1))
 
 
-def bench_ew(T: int, reps: int):
+def bench_ew(T: int, reps: int, only=None):
     n = T * 8192
     dev = torch.device("cuda")
     x, z = ((torch.randn(n, device=dev)).to(BF) for _ in range(2))
@@ -294,13 +308,44 @@ def bench_ew(T: int, reps: int):
     for name, fn, streams in (("gelu_fwd", lambda: raw.elementwise("act", x, y, act="gelu"), 2),
                               ("gelu_bwd", lambda: raw.elementwise("act_bwd", x, y, z=z, act="gelu"), 3),
                               ("add", lambda: raw.elementwise("add", x, y, z=z), 3)):
+        if only is not None and name not in only:
+            continue
         us = timed(fn, reps)
         emit(kernel=name, elements=n, us=round(us, 1), gbps=round(streams * n * 2 / us / 1e3, 1))
 
 
+# The in-suite perf gate (tests/test_gpu_perf_gate.py, `kbench gate`): one row per hot-kernel family, each timed
+# between its own two calibrations (short kernels drifted ~3 % against a per-section calibration in round 5)
+GATE = (("gemm", "fwd d->4d"), ("gemm", "wgrad logits"), ("mixer", "mixer y=tril(W)x"), ("attn", None),
+        ("norm", "norm_bwd"), ("ew", "gelu_bwd"))
+
+
+def bench_gate(tokens: int, batch: int, reps: int):
+    for sec, name in GATE:
+        cal0 = calibrate()
+        only = None if name is None else {name}
+        if sec == "gemm":
+            bench_gemm(tokens, reps, only)
+        elif sec == "mixer":
+            bench_mixer(reps, only)
+        elif sec == "attn":
+            bench_attn(batch, reps)
+        elif sec == "norm":
+            bench_norm(tokens, reps, only)
+        else:
+            bench_ew(tokens, reps, only)
+        flush_rows(section_calib(cal0, calibrate()))
+        torch.cuda.empty_cache()
+
+
+def gate_keys():
+    return {("attention" if sec == "attn" else (f"gemm {name}" if sec in ("gemm", "mixer") else name))
+            for sec, name in GATE}
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", nargs="?", default="all", choices=["gemm", "mixer", "attn", "attn_map", "norm", "ew", "all"])
+    ap.add_argument("what", nargs="?", default="all", choices=["gemm", "mixer", "attn", "attn_map", "norm", "ew", "all", "gate"])
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--tokens", type=int, default=131072, help="tokens per step (GPT-Neo-1.3B: 64 x 2048)")
     ap.add_argument("--batch", type=int, default=64, help="attention batch at S 2048")
@@ -309,6 +354,9 @@ def main(argv=None):
     ap.add_argument("--write-floors", default=None, help="write the observed ratios as a floor file")
     a = ap.parse_args(argv)
     todo = ["gemm", "mixer", "attn", "attn_map", "norm", "ew"] if a.what == "all" else [a.what]
+    if a.what == "gate":
+        bench_gate(a.tokens, a.batch, a.reps)
+        todo = []
     for w in todo:
         cal0 = calibrate()
         if w == "gemm":
@@ -344,7 +392,7 @@ def main(argv=None):
         seen = {line_key(r) for r in EMITTED}
         for key, metric, v, floor in bad:
             print(f"REGRESSION {key}: {metric} {v} < floor {floor} - {a.tol:.0%}", flush=True)
-        gone = missing(floors, seen, todo)
+        gone = missing(floors, seen, todo) if a.what != "gate" else sorted(gate_keys() - seen)
         for key in gone:
             print(f"MISSING {key}: floored but not emitted by its section", flush=True)
         n = sum(len(m) for k, m in floors.items() if k in seen)

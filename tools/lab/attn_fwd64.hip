@@ -1,3 +1,5 @@
+// LAB ONLY (round 6): moved out of the product -- slower than attn_fwd32_kernel (profiles/r5_attn_fwd64.md). It
+// declared its launcher in attn_common.h; building it again needs that declaration back.
 // D = 128 causal / full attention forward, one wave per SIMD, 64 queries per wave, the softmax software-pipelined
 // beside the MFMAs (K04 forward, same contract as attn_fwd32_kernel in attention.hip: ref src/model/spatial.py:44-81).
 //
