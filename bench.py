@@ -71,6 +71,8 @@ def main():
     ap.add_argument("--hip-graphs", type=int, default=1, help="1: replay the captured training step (1 GPU)")
     ap.add_argument("--hip-graphs-dist", type=int, default=0,
                     help="1: capture the step with N > 1 ranks too (RCCL collectives inside the graph; opt-in)")
+    ap.add_argument("--set", nargs="*", default=[], help="config overrides key=json_value (e.g. "
+                    "revnet_stream_dtype=\"calculation\")")
     ap.add_argument("--device", default="cuda", choices=("cuda", "cpu"),
                     help="cpu: rehearse the launcher and the N-rank step on gloo (no GPU; not a measurement)")
     args = ap.parse_args()
@@ -124,6 +126,12 @@ def main():
     overrides["mesh"] = {"dp": dp, "tp": tp}
     if args.depth:
         overrides["depth"] = args.depth
+    for item in args.set:
+        k, _, v = item.partition("=")
+        try:
+            overrides[k] = json.loads(v)
+        except json.JSONDecodeError:
+            overrides[k] = v
     if args.hip_graphs:
         overrides["use_hip_graphs"] = True
         overrides["hip_graphs_distributed"] = bool(args.hip_graphs_dist)
@@ -212,6 +220,9 @@ def main():
             "config": {"model": os.path.basename(args.config).replace(".json", "") +
                                 (f"-depth{args.depth}(debug)" if args.depth else ""),
                        "global_batch": params.train_batch_size, "seq_len": S,
+                       "set": args.set or None,
+                       "revnet_stream": (params.revnet_stream_dtype if params.memory_reduction_strategy == "revnet"
+                                         else None),
                        "parallelism": f"dp{dp}" + (f"xtp{tp}" if tp > 1 else ""),
                        "params": trainer.store.global_numel(), "optimizer": params.optimizer,
                        "hip_graphs": graphs,

@@ -12,7 +12,7 @@
 //    (2 x 128 VGPRs), so the LDS image of tile t is dead as soon as its substep-1 fragments are read -- after 16
 //    of the tile's 128 MFMAs. From then on the same LDS stage receives tile t+2 by LDS-DMA (buffer_load ... lds,
 //    16 B per lane, 1 KiB per wave-instruction, source address = SGPR resource + one constant per-lane offset).
-//    Two LDS stages of 64 KiB. Default schedule (SCH 1, the K-loop structure of hipBLASLt's 256x256x64 gfx950 kernel
+//    Two LDS stages of 64 KiB. Default schedule (SCH 1, the K-loop structure of the vendor library's 256x256x64 gfx950 kernel
 //    as read from its code object, profiles/r4_gemm_sched.md): per-operand barrier pairs -- A / B image of stage s
 //    free (lgkmcnt(0) + barrier), then DMA bursts into it; A / B of tile t+1 landed (counted vmcnt + barrier), then
 //    its substep-0 fragments are read under the last MFMAs of tile t. SCH 0 is the round-3 two-barrier schedule.

@@ -1,5 +1,5 @@
 // Host-side GEMM descriptor of the MFMA kernels (gemm.hip, gemm4w.h); the ctypes mirror is GemmDesc in
-// homebrewnlp_mtf_amd/ops/_lib.py. (tools/lab/blaslt.cpp, the hipBLASLt A/B harness, takes the same descriptor.)
+// homebrewnlp_mtf_amd/ops/_lib.py. (tools/lab/blaslt.cpp, the vendor-library A/B harness, takes the same descriptor.)
 #pragma once
 struct ObstGemmDesc {
   const void* A; const void* B; void* C; const void* R; void* Zout; const void* Zin;
@@ -15,5 +15,5 @@ struct ObstGemmDesc {
   long long a_sk, b_sk;
 };
 
-// (tools/lab only) the same products through hipBLASLt: 0 done, 1 not eligible, < 0 hipBLASLt error
+// (tools/lab only) the same products through the vendor GEMM library: 0 done, 1 not eligible, < 0 library error
 int obst_blaslt_gemm(const ObstGemmDesc* d, hipStream_t stream);

@@ -101,6 +101,10 @@ _DEFAULTS: typing.Dict[str, typing.Any] = dict(
     allreduce_dtype="bfloat16",  # DP wire dtype: bf16 with fp32 accumulation (all-to-all + sum + all-gather), or
                                  # "float32" (one fp32 all-reduce per bucket)
     force_grad_sync=False,       # run the DP collectives at world 1 too (tests of the capture path on one GPU)
+    # RevNet residual streams: "float32" (exact-to-fp32 reconstruction x1 = y2 - F(x2)) or "calculation" (the streams in
+    # calculation_dtype, as the reference's RevGradOp keeps them: ref src/model/revnet.py:23,69 -- a third of the
+    # stream bytes, bf16 reconstruction error over the depth; profiles/r6_revnet_stream.md)
+    revnet_stream_dtype="float32",
     use_hip_graphs=False,        # capture the whole training step in hipGraphs (Trainer._graph_step; 1 GPU, no dropout)
     # also capture with world > 1 (the RCCL all-reduces inside the graph; opt-in: RCCL graph capture is exercised only
     # where several GPUs are visible, which the 1-GPU test boxes are not)

@@ -44,7 +44,7 @@ def run_layers(builder: Builder, layers: typing.List[str], x: Act, residual: typ
         if idx == 1 and carrier is not None:
             args.norm_carrier = carrier
         if idx == n and stream_sink is not None:
-            args.stream_sink = stream_sink   # consumed (sink.out32 set) only by a layer that can fuse it
+            args.stream_sink = stream_sink   # consumed (sink.out set) only by a layer that can fuse it
         if idx == 1 and grad_sink is not None and name == "norm":
             args.grad_sink = grad_sink       # the norm on the block input itself
         if name == "norm" and idx < n:

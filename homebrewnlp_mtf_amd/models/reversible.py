@@ -45,8 +45,18 @@ def _sink(r32: torch.Tensor, alpha: float):
     return F.StreamSink(r32, alpha) if _REV_FUSE and raw.on_gpu(r32) else None
 
 
-def _stream_dtype(dt: torch.dtype) -> torch.dtype:
+def _stream_dtype(dt: torch.dtype, calc: bool = False) -> torch.dtype:
+    """fp32 streams (fp64 for the fp64 oracle); ``calc`` (revnet_stream_dtype "calculation"): the compute dtype"""
+    if calc:
+        return dt
     return torch.float64 if dt == torch.float64 else torch.float32
+
+
+def _add(a, b, beta: float = 1.0):
+    """a + beta * b in a's dtype (one elementwise pass)"""
+    if raw.on_gpu(a) and a.dtype == torch.bfloat16:
+        return _axpby(a, b, 1.0, beta)
+    return a + beta * b
 
 
 def _axpby(x, z, alpha, beta):
@@ -56,18 +66,30 @@ def _axpby(x, z, alpha, beta):
 
 
 class _RevStack(torch.autograd.Function):
-    """The residual streams (x1, x2) / (x, v) are carried in fp32 -- RevNet keeps no per-layer activations, so
-    this costs two activation-sized buffers -- while every block F runs in the compute dtype. Reconstruction
-    x1 = y2 - F(x2) is then exact to fp32 rounding instead of accumulating bf16 error over the depth."""
+    """The residual streams (x1, x2) / (x, v) are carried in fp32 by default -- RevNet keeps no per-layer
+    activations, so this costs two activation-sized buffers -- while every block F runs in the compute dtype.
+    Reconstruction x1 = y2 - F(x2) is then exact to fp32 rounding instead of accumulating bf16 error over the depth.
+    ``revnet_stream_dtype`` "calculation" keeps the RevNet streams in the compute dtype, as the reference does (its
+    RevGradOp adds and subtracts in the activations' dtype, src/model/revnet.py:23,69): 4 instead of 10 bytes per
+    element in every fused stream update (profiles/r6_revnet_stream.md)."""
 
     @staticmethod
-    def forward(ctx, x1, x2, blocks: typing.List[Block], mode: str, alpha: float):
+    def forward(ctx, x1, x2, blocks: typing.List[Block], mode: str, alpha: float, calc: bool = False):
         dt = x1.dtype
-        sd = _stream_dtype(dt)
+        calc = calc and mode == "revnet"
+        sd = _stream_dtype(dt, calc)
         x1, x2 = x1.to(sd), x2.to(sd)
         low = dt != sd                      # fused fp32 <- fp32 + bf16 kernels on the GPU
         with torch.no_grad():
-            if mode == "revnet" and low:
+            if calc:
+                # streams in the compute dtype (the reference's RevGradOp): y2 = x1 + F(x2) from the block's last
+                # GEMM's epilogue (F.StreamSink with a bf16 residual), else one elementwise add
+                for f in blocks:
+                    sink = _sink(x1, 1.0)
+                    fx = f(x2, sink)
+                    nx2 = sink.out if sink is not None and sink.out is not None else _add(x1, fx)
+                    x1, x2 = x2, nx2
+            elif mode == "revnet" and low:
                 x2b = raw.to_bf16(x2)
                 for f in blocks:
                     # y2 = x1 + F(x2) and its bf16 copy: from the block's last GEMM when it can take the update
@@ -87,7 +109,7 @@ class _RevStack(torch.autograd.Function):
                     else:  # momentum: (x, v) -> (x + v', v'), v' = a v + (1-a) F(x)
                         v = x2 * alpha + f(x1.to(dt)).to(sd) * (1.0 - alpha)
                         x1, x2 = x1 + v, v
-        ctx.blocks, ctx.mode, ctx.alpha, ctx.dt = blocks, mode, alpha, dt
+        ctx.blocks, ctx.mode, ctx.alpha, ctx.dt, ctx.calc = blocks, mode, alpha, dt, calc
         ctx.save_for_backward(x1, x2)
         return x1, x2
 
@@ -95,11 +117,31 @@ class _RevStack(torch.autograd.Function):
     def backward(ctx, g1, g2):
         y1, y2 = ctx.saved_tensors
         mode, alpha, dt = ctx.mode, ctx.alpha, ctx.dt
-        sd = _stream_dtype(dt)
-        g1 = torch.zeros_like(y1) if g1 is None else g1.to(sd)
-        g2 = torch.zeros_like(y2) if g2 is None else g2.to(sd)
+        sd = _stream_dtype(dt, ctx.calc)
+        g1 = torch.zeros_like(y1) if g1 is None else g1.to(sd).contiguous()
+        g2 = torch.zeros_like(y2) if g2 is None else g2.to(sd).contiguous()
         y1b = g2b = None    # bf16 copies of y1 / g2, written by the previous block's fused fp32 mixes
         for f in reversed(ctx.blocks):
+            if ctx.calc:
+                # y1 = x2, y2 = x1 + F(x2), all in the compute dtype: the recomputed F's last GEMM writes
+                # x1 = y2 - F(x2) (F.StreamSink, alpha -1) and the block's opening norm adds g1 into its dx
+                # (F.GradSink); autograd still sees dL/dF = g2 for that last op
+                sink = _sink(y2, -1.0)
+                gsink = F.GradSink(g1) if sink is not None else None
+                with torch.enable_grad():
+                    x2 = y1.detach().requires_grad_(True)
+                    fx = f(x2, sink, gsink)
+                torch.autograd.backward(fx, g2)
+                x1 = sink.out if sink is not None and sink.out is not None else _add(y2, fx.detach(), -1.0)
+                if x2.grad is None:
+                    dx2 = g1
+                elif gsink is not None and gsink.out is not None:
+                    # the norm's dx already holds g1; if another gradient reached x2 as well, autograd summed it in
+                    dx2 = x2.grad
+                else:
+                    dx2 = _add(g1, x2.grad)
+                y1, y2, g1, g2 = x1, y1, g2, dx2.contiguous()
+                continue
             if mode == "revnet":
                 # y1 = x2, y2 = x1 + F(x2)
                 bf = dt == torch.bfloat16
@@ -149,7 +191,7 @@ class _RevStack(torch.autograd.Function):
                 v = (y2 - fx.detach().to(sd) * (1.0 - alpha)) / alpha
                 gx = g1 if xr.grad is None else g1 + xr.grad.to(sd)
                 y1, y2, g1, g2 = x, v, gx, gv_tot * alpha
-        return g1.to(dt), g2.to(dt), None, None, None
+        return g1.to(dt), g2.to(dt), None, None, None, None
 
 
 class _Checkpoint(torch.autograd.Function):
@@ -171,6 +213,13 @@ class _Checkpoint(torch.autograd.Function):
         return xr.grad, None
 
 
+def _calc_stream(builder: Builder) -> bool:
+    v = str(getattr(builder.params, "revnet_stream_dtype", "float32"))
+    if v not in ("float32", "calculation"):
+        raise ValueError(f"revnet_stream_dtype must be 'float32' or 'calculation', not {v!r}")
+    return v == "calculation"
+
+
 def run_body(builder: Builder, src: Act, strategy: str, configs, depth: int) -> Act:
     stack = builder.scope.snapshot()
     dims = src.dims
@@ -179,7 +228,7 @@ def run_body(builder: Builder, src: Act, strategy: str, configs, depth: int) -> 
         # registration / inference: plain forward through the same blocks
         if strategy in ("revnet", "momentum"):
             dt = src.t.dtype
-            sd = _stream_dtype(dt)
+            sd = _stream_dtype(dt, strategy == "revnet" and _calc_stream(builder))
             x1 = x2 = src.t.to(sd)
             for f in blocks:
                 if strategy == "revnet":
@@ -194,7 +243,8 @@ def run_body(builder: Builder, src: Act, strategy: str, configs, depth: int) -> 
             x = f(x)
         return Act(x, dims)
     if strategy in ("revnet", "momentum"):
-        y1, y2 = _RevStack.apply(src.t, src.t, blocks, strategy, builder.params.momentumnet_alpha)
+        y1, y2 = _RevStack.apply(src.t, src.t, blocks, strategy, builder.params.momentumnet_alpha,
+                                 _calc_stream(builder))
         return Act((y1 + y2).to(src.t.dtype), dims)
     x = src.t
     for f in blocks:

@@ -46,8 +46,8 @@ def _acc_grad(w: torch.Tensor) -> typing.Tuple[torch.Tensor, bool]:
 
 def _acc_grad_beta(w: torch.Tensor) -> typing.Tuple[torch.Tensor, bool, float]:
     """like ``_acc_grad`` plus the GEMM beta: 0 (overwrite) for the first contribution of the step to a flat-buffer
-    gradient, 1 (accumulate) after that. hipBLASLt's fp32 weight-gradient GEMM runs up to 13 % faster without the
-    C read-back (tools/lab/bench_wgrad.py, profiles/r2_wgrad_layouts.txt)."""
+    gradient, 1 (accumulate) after that: an fp32 weight-gradient GEMM without the C read-back ran up to 13 % faster
+    (round 2, tools/lab/bench_wgrad.py, profiles/r2_wgrad_layouts.txt)."""
     mg = getattr(w, "main_grad", None)
     if mg is None:
         return torch.zeros(w.shape, dtype=torch.float32, device=w.device), False, 0.0
@@ -203,7 +203,7 @@ def _wgrad_gemm(x2, dy2, gw, plan: LinearPlan, xT=None, dyT=None, beta: float = 
         raw.gemm(raw.Operand(xT, 0, M, K * M), raw.Operand(dyT, 0, M, N * M), raw.Operand(gw, 0, N, K * N),
                  K, N, M, batch=(H, 1), beta=beta)
         return
-    if xT is not None:      # shared token-contiguous x (hipBLASLt: NT runs ~25 % faster than TT at T = 32k)
+    if xT is not None:      # shared token-contiguous x (round 2: NT ran ~25 % faster than TT at T = 32k)
         raw.gemm(raw.Operand(xT, 0, M, K * M), raw.Operand(dy2, 1, H * N, N), raw.Operand(gw, 0, N, K * N),
                  K, N, M, batch=(H, 1), beta=beta)
         return
@@ -212,28 +212,33 @@ def _wgrad_gemm(x2, dy2, gw, plan: LinearPlan, xT=None, dyT=None, beta: float = 
 
 
 class StreamSink:
-    """The RevNet stream update of a block fused into the block's last GEMM (ref src/model/revnet.py:20-49):
-    out32 = r32 + alpha * F(x) in fp32 and its bf16 copy come out of that GEMM's epilogue, replacing the separate
-    mix_f32 pass over the fp32 stream (forward: y2 = x1 + F(x2), alpha 1; backward reconstruction x1 = y2 - F(x2),
-    alpha -1). The op that takes it returns the bf16 copy as its output -- a value autograd never reads: the RevNet
-    stack back-propagates dL/dF through that op explicitly -- and leaves the fp32 tensor in ``out32``."""
+    """The RevNet stream update of a block fused into the block's last GEMM (ref src/model/revnet.py:20-49): forward
+    y2 = x1 + F(x2) (alpha 1), backward reconstruction x1 = y2 - F(x2) (alpha -1), out of that GEMM's epilogue instead
+    of a separate pass over the stream. fp32 stream: ``out32`` = r + alpha * F in fp32 plus its bf16 copy, which the op
+    returns -- a value autograd never reads: the RevNet stack back-propagates dL/dF through that op explicitly. bf16
+    stream (``revnet_stream_dtype`` "calculation"): r + alpha * F in bf16 is the op's output itself. Either way
+    ``out`` holds the updated stream once an op has consumed the sink."""
 
-    def __init__(self, r32: torch.Tensor, alpha: float):
-        self.r32, self.alpha = r32, float(alpha)
+    def __init__(self, r: torch.Tensor, alpha: float):
+        self.r, self.alpha = r, float(alpha)
         self.out32: typing.Optional[torch.Tensor] = None
+        self.out: typing.Optional[torch.Tensor] = None
 
     def usable(self, y_shape, device) -> bool:
-        """a fresh fp32 [.., y] buffer of the op's output shape on the GPU, nothing consumed yet"""
-        return (self.out32 is None and raw.on_gpu(self.r32) and self.r32.dtype == torch.float32
-                and self.r32.is_contiguous() and self.r32.numel() == math.prod(y_shape)
-                and self.r32.device == device)
+        """a fresh fp32 / bf16 stream buffer of the op's output shape on the GPU, nothing consumed yet"""
+        return (self.out is None and raw.on_gpu(self.r) and self.r.dtype in (torch.float32, torch.bfloat16)
+                and self.r.is_contiguous() and self.r.numel() == math.prod(y_shape) and self.r.device == device)
 
     def run(self, y_shape, device, gemm) -> torch.Tensor:
-        """gemm(out32, out16): the fused product; returns the bf16 copy"""
+        """gemm(y, R, Zout, alpha): the fused product; returns the op's bf16 output"""
         y16 = torch.empty(y_shape, dtype=torch.bfloat16, device=device)
+        if self.r.dtype == torch.bfloat16:
+            gemm(y16, self.r, None, self.alpha)
+            self.out = y16
+            return y16
         y32 = torch.empty(y_shape, dtype=torch.float32, device=device)
-        gemm(y32, y16)
-        self.out32 = y32
+        gemm(y32, self.r, y16, self.alpha)
+        self.out32 = self.out = y32
         return y16
 
 
@@ -261,7 +266,7 @@ class _Linear(torch.autograd.Function):
         elif (sink is not None and act is None and plan.o_perm is None
               and sink.usable(plan.canon_o_shape, xc.device)):
             y = sink.run(plan.canon_o_shape, xc.device,
-                         lambda y32, y16: _fwd_gemm(xc, w, y32, plan, R=sink.r32, Zout=y16, alpha=sink.alpha))
+                         lambda yo, R, Z, a: _fwd_gemm(xc, w, yo, plan, R=R, Zout=Z, alpha=a))
         else:
             y = _empty(plan.canon_o_shape, xc)
             _fwd_gemm(xc, w, y, plan, act=act, Zout=z)
@@ -634,7 +639,7 @@ class _TokenMixer(torch.autograd.Function):
                      raw.Operand(y, 0, hf, S * hf, Fd), S, Fd, S, batch=(B, H), tri=1 if causal else 0,
                      R=R, Zout=Zout, alpha=alpha)
         if sink is not None and sink.usable(xc.shape, xc.device):
-            y = sink.run(xc.shape, xc.device, lambda y32, y16: product(y32, R=sink.r32, Zout=y16, alpha=sink.alpha))
+            y = sink.run(xc.shape, xc.device, lambda yo, R, Z, a: product(yo, R=R, Zout=Z, alpha=a))
         else:
             y = torch.empty_like(xc)
             product(y)
@@ -851,19 +856,21 @@ class ResidualGrad:
 
 
 class GradSink:
-    """The RevNet stream gradient of a block input (ref src/model/revnet.py:51-120): the norm opening the block
-    adds the fp32 stream gradient g32 into its dx inside the backward kernel and writes the sum in fp32 (``out32``)
-    plus the bf16 copy it returns as dx -- replacing the separate dx2 = g1 + dF/dx2 mix_f32 pass. ``ptr`` is that
-    bf16 tensor's address: the stack checks that the input's .grad is exactly it (no other gradient was summed in)."""
+    """The RevNet stream gradient of a block input (ref src/model/revnet.py:51-120): the norm opening the block adds
+    the stream gradient g into its dx inside the backward kernel -- fp32 stream: the sum in fp32 (``out32``) plus the
+    bf16 copy it returns as dx; bf16 stream: dx itself -- replacing the separate dx2 = g1 + dF/dx2 pass. ``out`` holds
+    the summed stream gradient; ``ptr`` is the address of the bf16 dx the norm returned: the stack checks that the
+    input's .grad is exactly it (no other gradient was summed in)."""
 
-    def __init__(self, g32: torch.Tensor):
-        self.g32 = g32
+    def __init__(self, g: torch.Tensor):
+        self.g = g
         self.out32: typing.Optional[torch.Tensor] = None
+        self.out: typing.Optional[torch.Tensor] = None
         self.ptr = 0
 
     def usable(self, x: torch.Tensor) -> bool:
-        return (self.out32 is None and raw.on_gpu(self.g32) and self.g32.dtype == torch.float32
-                and self.g32.is_contiguous() and self.g32.numel() == x.numel() and self.g32.device == x.device)
+        return (self.out is None and raw.on_gpu(self.g) and self.g.dtype in (torch.float32, torch.bfloat16)
+                and self.g.is_contiguous() and self.g.numel() == x.numel() and self.g.device == x.device)
 
 
 class _Norm(torch.autograd.Function):
@@ -926,9 +933,14 @@ class _Norm(torch.autograd.Function):
             if rg is not None:
                 rg.applied = True
         elif sink is not None and R is None and ext is None and sink.usable(xc):
-            dx32 = torch.empty(xc.shape, dtype=torch.float32, device=xc.device)
-            raw.norm_bwd(xc, dy, ctx.sm32, stats, dx, gsc, gsh, rows, F, groups, Ffull, R32=sink.g32, dx32=dx32)
-            sink.out32, sink.ptr = dx32, dx.data_ptr()
+            if sink.g.dtype == torch.bfloat16:   # bf16 stream: dx = norm gradient + stream gradient
+                raw.norm_bwd(xc, dy, ctx.sm32, stats, dx, gsc, gsh, rows, F, groups, Ffull, R=sink.g)
+                sink.out = dx
+            else:
+                dx32 = torch.empty(xc.shape, dtype=torch.float32, device=xc.device)
+                raw.norm_bwd(xc, dy, ctx.sm32, stats, dx, gsc, gsh, rows, F, groups, Ffull, R32=sink.g, dx32=dx32)
+                sink.out32 = sink.out = dx32
+            sink.ptr = dx.data_ptr()
         else:
             raw.norm_bwd(xc, dy, ctx.sm32, stats, dx, gsc, gsh, rows, F, groups, Ffull, ext_dsum=ext, R=R)
         ctx.grad_sink = None

@@ -163,6 +163,10 @@ class Trainer:
         self.opt.flip = parity
         graph = torch.cuda.CUDAGraph()
         torch.cuda.synchronize(self.device)
+        if dist.is_initialized() and dist.get_backend() == "nccl":
+            # ProcessGroupNCCL's watchdog polls the events of finished eager collectives from its own thread (~every
+            # 100 ms); a poll inside the capture aborts the process (profiles/r6_rccl_capture.md): let it reap them
+            time.sleep(0.5)
         before = debug.comm_bytes()
         # OBST_CAPTURE_MODE (global | thread_local | relaxed): what other host threads may do while this one captures.
         # Multi-rank captures default to thread_local: ProcessGroupNCCL's watchdog polls its events from its own

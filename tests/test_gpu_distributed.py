@@ -135,7 +135,10 @@ def test_rccl_collectives_world1():
                                        ("all_gather", "thread_local"), ("trainer_fp32", "thread_local")])
 def test_rccl_graph_capture_world1(part, mode):
     """RCCL inside a captured graph on a one-rank nccl group (tools/graph_capture_probe.py, launcher-free so the
-    child's own stderr is kept): an async all_reduce / all_gather + wait captured and replayed equals eager, and the
+    child's own stderr is kept). ProcessGroupNCCL's watchdog thread polls the events of finished eager collectives;
+    a poll that lands inside a capture raises (WorkNCCL::isCompleted -> HIPEvent query) and aborts the process in
+    either capture mode -- a race, the round-5 SIGABRT. The probe (and Trainer._capture) let the watchdog reap them
+    first. An async all_reduce / all_gather + wait captured and replayed equals eager, and the
     Trainer's whole-step capture with the fp32 all-reduce DP wire inside (GradSync forced on at world 1) replays the
     eager run's losses and weights exactly. all_to_all (the bf16 wire and its side-stream shape) crashes inside
     hipStreamEndCapture on this image (SIGSEGV in torch.cuda.graph's capture_end, profiles/r6_rccl_capture.md) and is

@@ -135,7 +135,7 @@ def test_gemm_plain_paths(cuda, case):
 @pytest.mark.parametrize("with_r", [False, True])
 @pytest.mark.parametrize("act", ["gelu", "relu"])
 def test_gemm_activation_split(cuda, act_bwd, with_r, act):
-    """activation GEMMs as the model issues them (contiguous, unbatched): hipBLASLt + elementwise or fused MFMA
+    """activation GEMMs as the model issues them (contiguous, unbatched): gemm4w + elementwise or fused MFMA
     (gelu and relu take gemm4w's direct epilogue without a residual; ragged N = 520 masks columns per lane)"""
     torch.manual_seed(9)
     M, K, N = 384, 256, 520
@@ -488,7 +488,7 @@ def test_gemm_big_tile(cuda, a_t, b_t, K):
 @pytest.mark.parametrize("a_t,b_t", [(0, 0), (0, 1), (1, 0), (1, 1)])
 @pytest.mark.parametrize("out_f32", [False, True])
 def test_gemm4w_ragged(cuda, a_t, b_t, out_f32):
-    """gemm4w directly (hipBLASLt off) on ragged M / N -- 1, 17, 255, 257 rows (decode-sized products up to one row
+    """gemm4w directly on ragged M / N -- 1, 17, 255, 257 rows (decode-sized products up to one row
     past a tile), padded ldc -- bf16 and fp32 outputs, batched, against the fp32 oracle"""
     for M, N, K, nb in ((1, 264, 128, 3), (17, 8, 64, 2), (255, 520, 192, 1), (257, 256, 320, 2)):
         if a_t == 1 and M % 8:

@@ -29,17 +29,21 @@ def _pair(cfg, cuda):
     return m_cpu, m_gpu
 
 
-@pytest.mark.parametrize("variant", ["gpt", "gpt_d96", "revnet", "mixer", "mixer_unfused"])
+@pytest.mark.parametrize("variant", ["gpt", "gpt_d96", "revnet", "mixer", "mixer_unfused", "mixer_bf16stream",
+                                     "mixer_bf16stream_unfused"])
 def test_model_forward_backward(cuda, variant, monkeypatch):
     """GPU model vs the fp32 CPU oracle. "mixer": the ctx32_mixer block pair under RevNet, whose stream updates ride
     in the blocks' last GEMMs (F.StreamSink: the bottleneck out-projection and the token mixer) and whose stream
     gradients ride in the opening norms' backward (F.GradSink) -- no mix_f32 pass; "mixer_unfused": the same with the
-    separate mix_f32 passes"""
+    separate mix_f32 passes; "mixer_bf16stream": the streams in bf16 (revnet_stream_dtype "calculation", the
+    reference's numerics) -- the same fusions with a bf16 residual, no stream pass at all (unfused: bf16 axpby passes)"""
     from homebrewnlp_mtf_amd.models import reversible
-    mixes = []
-    real_mix = raw.mix_f32
+    mixes, axpbys = [], []
+    real_mix, real_ew = raw.mix_f32, raw.elementwise
     monkeypatch.setattr(raw, "mix_f32", lambda *a, **k: (mixes.append(1), real_mix(*a, **k))[1])
-    monkeypatch.setattr(reversible, "_REV_FUSE", variant != "mixer_unfused")
+    monkeypatch.setattr(raw, "elementwise",
+                        lambda op, *a, **k: ((axpbys.append(1) if op == "axpby" else None), real_ew(op, *a, **k))[1])
+    monkeypatch.setattr(reversible, "_REV_FUSE", not variant.endswith("_unfused"))
     cfg = dict(GPT)
     if variant == "gpt_d96":     # GPT-Neo 20B-scale head dim
         cfg.update(features_per_head=96)
@@ -54,6 +58,8 @@ def test_model_forward_backward(cuda, variant, monkeypatch):
                                             "scale-mid:features"]},
                                  {"layer": ["norm-shift-scale-features-group",
                                             "attention-biased_attention_map-absolute-input_as_value-shared"]}])
+    if "bf16stream" in variant:
+        cfg.update(revnet_stream_dtype="calculation")
     torch.manual_seed(0)
     m_cpu, m_gpu = _pair(cfg, cuda)
     x = torch.randint(0, 500, (2, 128, 1))
@@ -78,8 +84,12 @@ def test_model_forward_backward(cuda, variant, monkeypatch):
     if variant.startswith("mixer"):
         nblk = 2 * cfg.get("depth", GPT.get("depth", 2))
         # fused: the forward and reconstruction updates in the GEMMs, the gradient sums in the opening norms'
-        # backward -- no mix_f32 pass at all; unfused: three per block
-        assert len(mixes) == (0 if variant == "mixer" else 3 * nblk), (variant, len(mixes), nblk)
+        # backward -- no mix_f32 pass at all; unfused: three per block (bf16 streams: three bf16 axpby passes)
+        passes = 0 if not variant.endswith("_unfused") else 3 * nblk
+        if "bf16stream" in variant:
+            assert len(mixes) == 0 and len(axpbys) == passes, (variant, len(mixes), len(axpbys), nblk)
+        else:
+            assert len(mixes) == passes, (variant, len(mixes), nblk)
 
 
 @pytest.mark.parametrize("chain", ["adaptive_clip:0.003-sm3-momentum:0.9:1:1-learning_rate", "adam-learning_rate",

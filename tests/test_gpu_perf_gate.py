@@ -2,9 +2,10 @@
 forward GEMM and its worst product (the logits weight gradient), the token mixer's triangular forward, flash
 attention forward + backward, the norm backward and the gelu backward -- timed by ``tools/kbench.py gate`` (median
 of individually timed calls, each row between its own two same-process calibrations) and checked against the
-calibration-ratio floors of ``profiles/kbench_floor.json``. A kernel that gets slower than its floor by more than TOL
-fails the GPU suite; ``OBST_EW_CAP=2048`` (the round-1 grid-stride elementwise launch, ~35 % slower gelu backward)
-is the deliberately slowed build the gate was checked against (profiles/r6_perf_gate.md)."""
+calibration-ratio floors of ``profiles/kbench_gate_floor.json`` (the gate's own runs: a row timed alone reads
+slower than inside its full kbench section, e.g. norm_bwd 370-378 vs 343 us). A kernel that gets slower than its
+floor by more than TOL fails the GPU suite; ``OBST_EW_CAP=2048`` (the round-1 grid-stride elementwise launch, ~20 %
+slower gelu backward) is the deliberately slowed build the gate was checked against (profiles/r6_perf_gate.md)."""
 import json
 import os
 import sys
@@ -24,7 +25,7 @@ def test_hot_kernels_meet_their_floors(cuda):
     kbench.EMITTED.clear()
     kbench.PENDING.clear()
     kbench.bench_gate(131072, 64, reps=9)
-    with open(os.path.join(ROOT, "profiles", "kbench_floor.json")) as f:
+    with open(os.path.join(ROOT, "profiles", "kbench_gate_floor.json")) as f:
         spec = json.load(f)
     rows = list(kbench.EMITTED)
     seen = {kbench.line_key(r) for r in rows}
@@ -32,5 +33,10 @@ def test_hot_kernels_meet_their_floors(cuda):
     assert all(k in spec["floors"] for k in kbench.gate_keys()), "a gate row has no floor"
     for r in rows:
         print(json.dumps(r))
-    bad = kbench.check(rows, spec["floors"], TOL, spec.get("ratios", {}))
+    # compute rows: the ratio to the same-process MFMA loop (tracks the box's clock). Memory rows: the ratio to a
+    # torch device copy, or the absolute GB/s -- the copy itself read 4.6-5.3 TB/s across boxes at equal kernel GB/s
+    # (profiles/r6_perf_gate.md), so a memory row fails only when it misses both
+    bad_ratio = kbench.check(rows, spec["floors"], TOL, spec.get("ratios", {}))
+    bad_abs = {(k, m.replace("ratio_", "")) for k, m, _, _ in kbench.check(rows, spec["floors"], TOL)}
+    bad = [b for b in bad_ratio if not b[1].startswith("ratio_gbps") or (b[0], "gbps") in bad_abs]
     assert not bad, "perf regression: " + "; ".join(f"{k} {m} {v} < floor {fl} - {TOL:.0%}" for k, m, v, fl in bad)

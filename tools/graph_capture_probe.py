@@ -86,6 +86,16 @@ def main():
 CAPTURE_MODE = "global"
 
 
+def _quiesce():
+    """let ProcessGroupNCCL's watchdog reap the completed eager collectives before a capture starts: it polls its
+    work queue's events from its own thread (~every 100 ms), and a hipEventQuery that lands inside the capture raises
+    in WorkNCCL::isCompleted and aborts the process (HIPEvent.h:109 from Watchdog::runLoop, both capture modes on this
+    image; profiles/r6_rccl_capture.md)"""
+    import time
+    torch.cuda.synchronize()
+    time.sleep(0.5)
+
+
 def _capture(dev, fn):
     """warm fn up eagerly on a side stream, capture it, replay once"""
     s = torch.cuda.Stream()
@@ -93,7 +103,7 @@ def _capture(dev, fn):
     with torch.cuda.stream(s):
         fn()
     torch.cuda.current_stream().wait_stream(s)
-    torch.cuda.synchronize()
+    _quiesce()
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g, capture_error_mode=CAPTURE_MODE):
         fn()
@@ -158,6 +168,7 @@ def _capture_all_reduce(dev, out):
         y.copy_(x * 3.0)
         dist.all_reduce(y, async_op=True).wait()
     torch.cuda.current_stream().wait_stream(s)
+    _quiesce()
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g, capture_error_mode=CAPTURE_MODE):
         y.copy_(x * 3.0)

@@ -5,8 +5,12 @@ set -o pipefail
 out=$1
 mkdir -p "$out"
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest -x -v --timeout 240 --timeout-method thread -s tests/test_gpu_perf_gate.py \
+timeout -k 10 120 python -u tools/kbench.py norm > "$out/kb_norm.jsonl" 2>&1; timeout -k 10 300 python -u -m pytest -x -v --timeout 240 --timeout-method thread -s tests/test_gpu_perf_gate.py \
     > "$out/gate.log" 2>&1; echo "gate exit $?"; grep -E "passed|failed|REGRESS|regression" "$out/gate.log" | tail -3
+# the deliberately slowed build: the round-1 grid-stride elementwise launch (must FAIL the gate)
+OBST_EW_CAP=2048 timeout -k 10 300 python -u -m pytest -x -v --timeout 240 --timeout-method thread -s \
+    tests/test_gpu_perf_gate.py > "$out/gate_slowed.log" 2>&1; echo "slowed gate exit $? (expected 1)"
+grep -E "passed|failed|regression" "$out/gate_slowed.log" | tail -2 | cut -c1-300
 timeout -k 10 600 python -u -m pytest -x -v --timeout 250 --timeout-method thread tests/test_gpu_distributed.py \
     -k capture > "$out/capture_tests.log" 2>&1 || { tail -30 "$out/capture_tests.log"; exit 1; }
 tail -2 "$out/capture_tests.log"
