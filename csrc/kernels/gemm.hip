@@ -365,7 +365,10 @@ OBST_API int obst_gemm(const ObstGemmDesc* d, hipStream_t stream) {
     // batched products too (the per-head group-linear weight gradients: few tiles per batch); C batch strides must
     // keep 16-byte alignment for the fold. The folds index float4s of rows (m = e / N, e < M * N / 4): N and ldc
     // must be multiples of 4 (the entry checks already require 8; restated here so the fold's own contract is local)
-    if ((big_tiles < 512 || d->tri == 3) && d->out_f32 && !d->R && !d->Zout && !d->act && d->mode == 0 &&
+    // (also long-K products with many tiles: the logits weight gradient, 8 x 197 tiles of 2048 K-tiles each, ran 7
+    // rounds of which the last held 40 of 256 CUs -- split 4 ways it runs 25 rounds and one 0.4 GB fold)
+    if ((big_tiles < 512 || d->tri == 3 || d->K >= 32768) && d->out_f32 && !d->R && !d->Zout && !d->act &&
+        d->mode == 0 &&
         (d->tri == 0 || d->tri == 3) && d->N % 4 == 0 && d->ldc % 4 == 0 &&
         (batch == 1 || (d->c_s1 % 4 == 0 && d->c_s2 % 4 == 0))) {
       const double per_k = 1.25 / 64.0;   // us per K element of one tile

@@ -7,7 +7,7 @@ out=$1
 mkdir -p "$out"
 export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_model.py \
-    -k "forward_backward" > "$out/model_tests.log" 2>&1 || { tail -30 "$out/model_tests.log"; exit 1; }
+    -k "forward_backward" -s > "$out/model_tests.log" 2>&1; grep -E "rel |passed|failed" "$out/model_tests.log" | tail -40
 tail -1 "$out/model_tests.log"
 timeout -k 10 600 python -u -m pytest -x -v --timeout 250 --timeout-method thread tests/test_gpu_distributed.py \
     -k capture > "$out/capture_tests.log" 2>&1 || { grep -E "PASS|FAIL" "$out/capture_tests.log"; exit 1; }
