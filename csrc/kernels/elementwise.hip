@@ -285,6 +285,20 @@ __global__ __launch_bounds__(NTH) void cast_f32_bf16_kernel(const float* __restr
   }
 }
 
+// y(bf16) = x1(fp32) + x2(fp32) in one pass: the reversible body's output (y1 + y2) and the embedding's gradient out of
+// it (g1 + g2), instead of an fp32 add plus a cast (18 -> 10 bytes per element)
+__global__ __launch_bounds__(NTH) void add2_f32_bf16_kernel(const float* __restrict__ X1, const float* __restrict__ X2,
+                                                            bf16_t* __restrict__ Y, long long n) {
+  for (long long v = (long long)blockIdx.x * NTH + threadIdx.x; v * 4 < n; v += (long long)gridDim.x * NTH) {
+    if (v * 4 + 3 < n) {
+      const float4 a = reinterpret_cast<const float4*>(X1)[v], b = reinterpret_cast<const float4*>(X2)[v];
+      reinterpret_cast<uint2*>(Y)[v] = make_uint2(pack_bf16x2(a.x + b.x, a.y + b.y), pack_bf16x2(a.z + b.z, a.w + b.w));
+    } else {
+      for (long long j = v * 4; j < n; ++j) Y[j] = f2bf(X1[j] + X2[j]);
+    }
+  }
+}
+
 // y(fp32) = alpha * x(fp32) + beta * z(bf16); optional bf16 copy of y (the reversible bodies' residual streams)
 __global__ __launch_bounds__(NTH) void mix_f32_kernel(const float* __restrict__ X, const bf16_t* __restrict__ Z,
                                                       float* __restrict__ Y, bf16_t* __restrict__ Yb, long long nvec,
@@ -386,6 +400,11 @@ OBST_API int obst_cumsum(const void* X, void* Y, long long outer, int S, long lo
                          int grad, hipStream_t st) {
   hipLaunchKernelGGL(cumsum_kernel, dim3(grid_for(outer * inner)), dim3(NTH), 0, st, (const bf16_t*)X, (bf16_t*)Y,
                      outer, S, inner, reverse, mean, grad);
+  return (int)hipGetLastError();
+}
+
+OBST_API int obst_add2_f32_bf16(const float* X1, const float* X2, void* Y, long long n, hipStream_t st) {
+  hipLaunchKernelGGL(add2_f32_bf16_kernel, dim3(grid_ew((n + 3) / 4)), dim3(NTH), 0, st, X1, X2, (bf16_t*)Y, n);
   return (int)hipGetLastError();
 }
 

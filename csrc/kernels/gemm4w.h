@@ -342,7 +342,7 @@ __device__ __forceinline__ Tile4 decode4(const GemmArgs& p, long long L64) {
     const int gsz = min(p.tiles_m - first_m, GROUP);
     tm = first_m + (bid % per_group) % gsz;
     tn = (bid % per_group) / gsz;
-  } else {
+  } else if (p.tri_group == 0) {
     // triangular A (tri 1: A[m][k] = 0 for k > m, tri 2: for k < m): tile rows in order of decreasing K range,
     // the slowest index, so every round of the block-cyclic walk (logical4) holds tiles of equal work
     const unsigned per_row = (unsigned)p.tiles_n * (unsigned)p.nbatch;
@@ -351,6 +351,20 @@ __device__ __forceinline__ Tile4 decode4(const GemmArgs& p, long long L64) {
     ybat = rest / (unsigned)p.tiles_n;
     tn = (int)(rest % (unsigned)p.tiles_n);
     tm = p.tri == 1 ? p.tiles_m - 1 - tmr : tmr;
+  } else {
+    // grouped order (tri_group G > 0): batches in groups of G, and inside a group the tile rows heaviest first with
+    // the batch next -- the B operand of one batch (the token mixer's x[b, :, h, :]) is re-read by its tile rows
+    // within one group's span instead of one whole sweep over the batch apart (L2 / MALL reuse). G a multiple of 8
+    // keeps the XCD interleave (tile x + 8 j on XCD x) on the batches of one residue class.
+    const unsigned G = (unsigned)p.tri_group, tmn = (unsigned)p.tiles_m, tnn = (unsigned)p.tiles_n;
+    const unsigned block = tmn * G * tnn;
+    const unsigned yg = L / block, r = L - yg * block;
+    const unsigned left = (unsigned)p.nbatch - yg * G;
+    const unsigned gsz = left < G ? left : G;   // (the last group may be short)
+    const unsigned tmr = r / (gsz * tnn), r2 = r - tmr * (gsz * tnn);
+    ybat = yg * G + r2 / tnn;
+    tn = (int)(r2 % tnn);
+    tm = p.tri == 1 ? p.tiles_m - 1 - (int)tmr : (int)tmr;
   }
   T.m0 = tm * 256;
   T.n0 = tn * 256;

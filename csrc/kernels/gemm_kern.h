@@ -26,6 +26,7 @@ struct GemmArgs {
   int nbatch;             // gemm4w: batches x splits (the grid is one block per CU)
   unsigned long long* stamps;   // gemm4w diagnostics: per-block timestamps (null: off)
   unsigned* queue;        // gemm4w dynamic tile queue: 8 per-XCD counters zeroed before the launch (null: static)
+  int tri_group;          // gemm4w tri 1 / 2: batches per tile-row group of the work order (0: tile rows slowest)
 };
 }  // namespace gemmk
 

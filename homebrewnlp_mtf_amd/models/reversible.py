@@ -59,6 +59,13 @@ def _add(a, b, beta: float = 1.0):
     return a + beta * b
 
 
+def _sum_to(a, b, dt):
+    """(a + b) in dtype dt: one fused fp32 + fp32 -> bf16 pass on the GPU (raw.add_to_bf16)"""
+    if dt == torch.bfloat16 and a.dtype == torch.float32 and raw.on_gpu(a):
+        return raw.add_to_bf16(a, b)
+    return (a + b).to(dt)
+
+
 def _axpby(x, z, alpha, beta):
     y = torch.empty_like(x)
     raw.elementwise("axpby", x.contiguous(), y, z=z.contiguous(), alpha=alpha, beta=beta)
@@ -74,11 +81,12 @@ class _RevStack(torch.autograd.Function):
     element in every fused stream update (profiles/r6_revnet_stream.md)."""
 
     @staticmethod
-    def forward(ctx, x1, x2, blocks: typing.List[Block], mode: str, alpha: float, calc: bool = False):
-        dt = x1.dtype
+    def forward(ctx, x, blocks: typing.List[Block], mode: str, alpha: float, calc: bool = False):
+        """both streams start as the body input x; returns the body output y1 + y2 in x's dtype"""
+        dt = x.dtype
         calc = calc and mode == "revnet"
         sd = _stream_dtype(dt, calc)
-        x1, x2 = x1.to(sd), x2.to(sd)
+        x1 = x2 = x.to(sd)
         low = dt != sd                      # fused fp32 <- fp32 + bf16 kernels on the GPU
         with torch.no_grad():
             if calc:
@@ -111,15 +119,14 @@ class _RevStack(torch.autograd.Function):
                         x1, x2 = x1 + v, v
         ctx.blocks, ctx.mode, ctx.alpha, ctx.dt, ctx.calc = blocks, mode, alpha, dt, calc
         ctx.save_for_backward(x1, x2)
-        return x1, x2
+        return _sum_to(x1, x2, dt)
 
     @staticmethod
-    def backward(ctx, g1, g2):
+    def backward(ctx, g):
         y1, y2 = ctx.saved_tensors
         mode, alpha, dt = ctx.mode, ctx.alpha, ctx.dt
         sd = _stream_dtype(dt, ctx.calc)
-        g1 = torch.zeros_like(y1) if g1 is None else g1.to(sd).contiguous()
-        g2 = torch.zeros_like(y2) if g2 is None else g2.to(sd).contiguous()
+        g1 = g2 = g.to(sd).contiguous()     # d(y1 + y2): the same gradient reaches both streams
         y1b = g2b = None    # bf16 copies of y1 / g2, written by the previous block's fused fp32 mixes
         for f in reversed(ctx.blocks):
             if ctx.calc:
@@ -191,7 +198,8 @@ class _RevStack(torch.autograd.Function):
                 v = (y2 - fx.detach().to(sd) * (1.0 - alpha)) / alpha
                 gx = g1 if xr.grad is None else g1 + xr.grad.to(sd)
                 y1, y2, g1, g2 = x, v, gx, gv_tot * alpha
-        return g1.to(dt), g2.to(dt), None, None, None, None
+        # the body input fed both streams: its gradient is the sum, rounded once
+        return _sum_to(g1, g2, dt), None, None, None, None
 
 
 class _Checkpoint(torch.autograd.Function):
@@ -243,9 +251,8 @@ def run_body(builder: Builder, src: Act, strategy: str, configs, depth: int) -> 
             x = f(x)
         return Act(x, dims)
     if strategy in ("revnet", "momentum"):
-        y1, y2 = _RevStack.apply(src.t, src.t, blocks, strategy, builder.params.momentumnet_alpha,
-                                 _calc_stream(builder))
-        return Act((y1 + y2).to(src.t.dtype), dims)
+        y = _RevStack.apply(src.t, blocks, strategy, builder.params.momentumnet_alpha, _calc_stream(builder))
+        return Act(y, dims)
     x = src.t
     for f in blocks:
         if strategy == "checkpoint":

@@ -104,6 +104,7 @@ _SIGS = {
     "obst_scatter_ws": [c_ll, c_i],
     "obst_cumsum": [c_p, c_p, c_ll, c_i, c_ll, c_i, c_i, c_i, c_p],
     "obst_cast_f32_bf16": [c_p, c_p, c_ll, c_p],
+    "obst_add2_f32_bf16": [c_p, c_p, c_p, c_ll, c_p],
     "obst_transpose": [c_p, c_p, c_ll, c_ll, c_ll, c_ll, c_i, c_ll, c_ll, c_p],
     "obst_mix_f32": [c_p, c_p, c_p, c_p, c_ll, c_f, c_f, c_p],
     "obst_xent_fwd": [c_p, c_p, c_p, c_p, c_p, c_ll, c_i, c_i, c_f, c_p],

@@ -686,6 +686,21 @@ def mix_f32(x, z, alpha: float, beta: float, y=None, yb=None):
     return y
 
 
+def add_to_bf16(a, b, out=None):
+    """bf16(a + b) of two fp32 tensors in one pass on the GPU (HIP add2 kernel); a + b then a cast elsewhere"""
+    if out is None:
+        out = torch.empty(a.shape, dtype=torch.bfloat16, device=a.device)
+    if a.device.type == "meta":
+        return out
+    if on_gpu(a) and a.dtype == torch.float32 and b.dtype == torch.float32 and a.shape == b.shape:
+        a, b = a.contiguous(), b.contiguous()
+        L.check(L.lib().obst_add2_f32_bf16(a.data_ptr(), b.data_ptr(), out.data_ptr(), a.numel(), L.stream_ptr()),
+                "add2_f32_bf16")
+        return out
+    out.copy_(a + b)
+    return out
+
+
 def to_bf16(x, out=None):
     """fp32 -> bf16 copy through the HIP cast kernel on the GPU"""
     if out is None:
