@@ -293,15 +293,18 @@ static int g4w_queue_env() {
   static int v = [] { const char* e = getenv("OBST_G4W_QUEUE"); return e ? atoi(e) : 1; }();
   return v;
 }
-// OBST_G4W_TRI_GROUP (default 8): work order of the triangular (token-mixer) products -- G > 0: batches in groups of
+// OBST_G4W_TRI_GROUP (default: auto, below): work order of the triangular (token-mixer) products -- G > 0: batches in groups of
 // G, the tile rows of a group heaviest first inside it (gemm4w.h decode4), so the B operand of a (batch, head) --
 // x[b, :, h, :], re-read by each of its 8 tile rows -- stays in L2 / MALL between its reads; 0: tile rows slowest
 // (each x re-read one whole sweep over the 2048 (batch, head) products later). ctx32_mixer at batch 256: 1862-1869
 // vs 1934-1938 ms/step (G = 32: 1870; kbench's 32-batch mixer, which fits the MALL either way: equal;
 // tools/lab/r6_tri_group.sh)
-static int g4w_tri_group_env() {
-  static int v = [] { const char* e = getenv("OBST_G4W_TRI_GROUP"); return e ? atoi(e) : 8; }();
-  return v < 0 ? 0 : v;
+// Auto (unset): 8 when the B operands of the launch exceed 512 MiB (past the 256 MiB MALL), else 0 -- kbench's
+// 32-batch mixer (268 MB of x) ran 3-5 % slower grouped
+static int g4w_tri_group_env(long long b_bytes) {
+  static int v = [] { const char* e = getenv("OBST_G4W_TRI_GROUP"); return e ? atoi(e) : -1; }();
+  if (v >= 0) return v;
+  return b_bytes > (512ll << 20) ? 8 : 0;
 }
 static int g4w_queue_tri_env() {   // the triangular (token-mixer) products on the queue too (0: static walk)
   static int v = [] { const char* e = getenv("OBST_G4W_QUEUE_TRI"); return e ? atoi(e) : 1; }();
@@ -347,7 +350,8 @@ OBST_API int obst_gemm(const ObstGemmDesc* d, hipStream_t stream) {
   a.kin = d->kin; a.a_sk = d->a_sk; a.b_sk = d->b_sk; a.kin_bps = 0;
   a.stamps = g_4w_stamps;
   a.queue = nullptr;
-  a.tri_group = (d->tri == 1 || d->tri == 2) ? g4w_tri_group_env() : 0;
+  a.tri_group = (d->tri == 1 || d->tri == 2)
+                    ? g4w_tri_group_env((long long)d->batch1 * d->batch2 * d->K * d->N * 2) : 0;
   a.ksplit = 1;
   a.ws = nullptr;
   a.nbatch = 0;

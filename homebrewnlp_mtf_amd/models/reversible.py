@@ -81,7 +81,8 @@ class _RevStack(torch.autograd.Function):
     element in every fused stream update (profiles/r6_revnet_stream.md)."""
 
     @staticmethod
-    def forward(ctx, x, blocks: typing.List[Block], mode: str, alpha: float, calc: bool = False):
+    def forward(ctx, x, blocks: typing.List[Block], mode: str, alpha: float, calc: bool = False,
+                gcalc: bool = False):
         """both streams start as the body input x; returns the body output y1 + y2 in x's dtype"""
         dt = x.dtype
         calc = calc and mode == "revnet"
@@ -118,6 +119,8 @@ class _RevStack(torch.autograd.Function):
                         v = x2 * alpha + f(x1.to(dt)).to(sd) * (1.0 - alpha)
                         x1, x2 = x1 + v, v
         ctx.blocks, ctx.mode, ctx.alpha, ctx.dt, ctx.calc = blocks, mode, alpha, dt, calc
+        # gradient streams in the compute dtype under fp32 activation streams (revnet_grad_stream_dtype)
+        ctx.gcalc = gcalc and mode == "revnet" and not calc and dt == torch.bfloat16 and dt != _stream_dtype(dt)
         ctx.save_for_backward(x1, x2)
         return _sum_to(x1, x2, dt)
 
@@ -126,7 +129,8 @@ class _RevStack(torch.autograd.Function):
         y1, y2 = ctx.saved_tensors
         mode, alpha, dt = ctx.mode, ctx.alpha, ctx.dt
         sd = _stream_dtype(dt, ctx.calc)
-        g1 = g2 = g.to(sd).contiguous()     # d(y1 + y2): the same gradient reaches both streams
+        gd = dt if ctx.gcalc else sd
+        g1 = g2 = g.to(gd).contiguous()     # d(y1 + y2): the same gradient reaches both streams
         y1b = g2b = None    # bf16 copies of y1 / g2, written by the previous block's fused fp32 mixes
         for f in reversed(ctx.blocks):
             if ctx.calc:
@@ -147,6 +151,31 @@ class _RevStack(torch.autograd.Function):
                     dx2 = x2.grad
                 else:
                     dx2 = _add(g1, x2.grad)
+                y1, y2, g1, g2 = x1, y1, g2, dx2.contiguous()
+                continue
+            if ctx.gcalc:
+                # fp32 activation streams (exact reconstruction x1 = y2 - F(x2) from the fused fp32 sink), bf16
+                # gradient streams: the opening norm adds the bf16 g1 into its dx (F.GradSink with a bf16 R), and
+                # dx2 / g2 stay bf16 -- the mixed-precision convention for activation gradients
+                y1b = raw.to_bf16(y1) if y1b is None else y1b
+                sink = _sink(y2, -1.0)
+                gsink = F.GradSink(g1) if sink is not None else None
+                with torch.enable_grad():
+                    x2 = y1b.detach().requires_grad_(True)
+                    fx = f(x2, sink, gsink)
+                torch.autograd.backward(fx, g2)
+                if sink is not None and sink.out32 is not None:
+                    x1, nb1 = sink.out32, fx.detach()
+                else:
+                    nb1 = torch.empty_like(y1b)
+                    x1 = raw.mix_f32(y2, fx.detach(), 1.0, -1.0, yb=nb1)
+                if x2.grad is None:
+                    dx2 = g1
+                elif gsink is not None and gsink.out is not None:
+                    dx2 = x2.grad            # the norm's dx already holds g1 (and anything else autograd summed in)
+                else:
+                    dx2 = _add(g1, x2.grad)
+                y1b = nb1
                 y1, y2, g1, g2 = x1, y1, g2, dx2.contiguous()
                 continue
             if mode == "revnet":
@@ -199,7 +228,7 @@ class _RevStack(torch.autograd.Function):
                 gx = g1 if xr.grad is None else g1 + xr.grad.to(sd)
                 y1, y2, g1, g2 = x, v, gx, gv_tot * alpha
         # the body input fed both streams: its gradient is the sum, rounded once
-        return _sum_to(g1, g2, dt), None, None, None, None
+        return _sum_to(g1, g2, dt), None, None, None, None, None
 
 
 class _Checkpoint(torch.autograd.Function):
@@ -228,6 +257,13 @@ def _calc_stream(builder: Builder) -> bool:
     return v == "calculation"
 
 
+def _calc_grad_stream(builder: Builder) -> bool:
+    v = str(getattr(builder.params, "revnet_grad_stream_dtype", "float32"))
+    if v not in ("float32", "calculation"):
+        raise ValueError(f"revnet_grad_stream_dtype must be 'float32' or 'calculation', not {v!r}")
+    return v == "calculation"
+
+
 def run_body(builder: Builder, src: Act, strategy: str, configs, depth: int) -> Act:
     stack = builder.scope.snapshot()
     dims = src.dims
@@ -251,7 +287,8 @@ def run_body(builder: Builder, src: Act, strategy: str, configs, depth: int) -> 
             x = f(x)
         return Act(x, dims)
     if strategy in ("revnet", "momentum"):
-        y = _RevStack.apply(src.t, blocks, strategy, builder.params.momentumnet_alpha, _calc_stream(builder))
+        y = _RevStack.apply(src.t, blocks, strategy, builder.params.momentumnet_alpha, _calc_stream(builder),
+                            _calc_grad_stream(builder))
         return Act(y, dims)
     x = src.t
     for f in blocks:

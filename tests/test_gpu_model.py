@@ -30,7 +30,7 @@ def _pair(cfg, cuda):
 
 
 @pytest.mark.parametrize("variant", ["gpt", "gpt_d96", "revnet", "mixer", "mixer_unfused", "mixer_bf16stream",
-                                     "mixer_bf16stream_unfused"])
+                                     "mixer_bf16stream_unfused", "mixer_bf16grad"])
 def test_model_forward_backward(cuda, variant, monkeypatch):
     """GPU model vs the fp32 CPU oracle. "mixer": the ctx32_mixer block pair under RevNet, whose stream updates ride
     in the blocks' last GEMMs (F.StreamSink: the bottleneck out-projection and the token mixer) and whose stream
@@ -60,6 +60,8 @@ def test_model_forward_backward(cuda, variant, monkeypatch):
                                             "attention-biased_attention_map-absolute-input_as_value-shared"]}])
     if "bf16stream" in variant:
         cfg.update(revnet_stream_dtype="calculation")
+    if variant == "mixer_bf16grad":   # fp32 activation streams, bf16 gradient streams
+        cfg.update(revnet_grad_stream_dtype="calculation")
     torch.manual_seed(0)
     m_cpu, m_gpu = _pair(cfg, cuda)
     x = torch.randint(0, 500, (2, 128, 1))
@@ -93,7 +95,7 @@ def test_model_forward_backward(cuda, variant, monkeypatch):
         # fused: the forward and reconstruction updates in the GEMMs, the gradient sums in the opening norms'
         # backward -- no mix_f32 pass at all; unfused: three per block (bf16 streams: three bf16 axpby passes)
         passes = 0 if not variant.endswith("_unfused") else 3 * nblk
-        if "bf16stream" in variant:
+        if "bf16stream" in variant or variant == "mixer_bf16grad":
             assert len(mixes) == 0 and len(axpbys) == passes, (variant, len(mixes), len(axpbys), nblk)
         else:
             assert len(mixes) == passes, (variant, len(mixes), nblk)

@@ -694,28 +694,29 @@ def test_flop_meter_counts_every_token_mixer_application():
 
 @pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
 def test_revnet_calculation_dtype_streams(dtype):
-    """revnet_stream_dtype "calculation" (the reference's RevGradOp numerics): the RevNet streams in the compute dtype.
-    fp32 compute: identical to the default fp32 streams. bf16 compute: same loss and gradients as the fp32-stream run
-    to within the bf16 reconstruction error"""
+    """revnet_stream_dtype "calculation" (the reference's RevGradOp numerics): the RevNet streams in the compute dtype;
+    revnet_grad_stream_dtype "calculation": only the gradient streams. fp32 compute: identical to the default fp32
+    streams. bf16 compute: same loss and gradients as the fp32-stream run to within bf16 error"""
     cfg = dict(BASE, depth=2, memory_reduction_strategy="revnet", calculation_dtype=dtype,
                block_config=[{"layer": ["norm-shift-scale-features-group", "feed_forward-in:relu"]},
                              {"layer": ["norm-shift-scale", "attention-dot_product-context"]}])
     x = torch.randint(0, 50, (2, 8, 1), generator=torch.Generator().manual_seed(3))
     y = torch.randint(0, 50, (2, 8, 1), generator=torch.Generator().manual_seed(4))
     runs = []
-    for stream in ("float32", "calculation"):
+    for stream, gstream in (("float32", "float32"), ("calculation", "float32"), ("float32", "calculation")):
         torch.manual_seed(0)
-        m = Model(ModelParameter(dict(cfg, revnet_stream_dtype=stream)), "cpu")
+        m = Model(ModelParameter(dict(cfg, revnet_stream_dtype=stream, revnet_grad_stream_dtype=gstream)), "cpu")
         out = m(x, y)
         out["loss"].backward()
         m.store.fold_leaf_grads()
         runs.append((float(out["loss"]), m.store.grad.clone()))
-    (la, ga), (lb, gb) = runs
-    if dtype == "float32":
-        assert la == lb and torch.equal(ga, gb)
-    else:
-        assert abs(la - lb) < 2e-2 * max(1.0, abs(la)), (la, lb)
-        assert (ga - gb).norm() < 0.1 * ga.norm(), ((ga - gb).norm(), ga.norm())
+    (la, ga), *others = runs
+    for lb, gb in others:   # bf16 activation streams / bf16 gradient streams under fp32 activation streams
+        if dtype == "float32":
+            assert la == lb and torch.equal(ga, gb)
+        else:
+            assert abs(la - lb) < 2e-2 * max(1.0, abs(la)), (la, lb)
+            assert (ga - gb).norm() < 0.1 * ga.norm(), ((ga - gb).norm(), ga.norm())
     with pytest.raises(ValueError):
         m = Model(ModelParameter(dict(cfg, revnet_stream_dtype="float16")), "cpu")
         m(x, y)["loss"].backward()

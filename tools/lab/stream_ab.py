@@ -41,8 +41,10 @@ def main():
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     curves = {}
-    for stream in ("float32", "calculation"):
-        p = load_config(a.config, {"train_batch_size": a.batch, "revnet_stream_dtype": stream, "use_hip_graphs": True})
+    combos = (("float32", "float32"), ("calculation", "float32"), ("float32", "calculation"))
+    for stream, gstream in combos:
+        p = load_config(a.config, {"train_batch_size": a.batch, "revnet_stream_dtype": stream,
+                                   "revnet_grad_stream_dtype": gstream, "use_hip_graphs": True})
         torch.manual_seed(1234)
         tr = Trainer(p, dev)
         data = batches(8, a.batch, p.sequence_length, dev)
@@ -51,13 +53,14 @@ def main():
             m = tr.step(data[i % len(data)])
             if i % 10 == 9 or i == 0:
                 losses.append(round(float(m["loss"]), 4))
-        curves[stream] = losses
-        print(json.dumps({"stream": stream, "batch": a.batch, "loss_every_10": losses}), flush=True)
+        curves[(stream, gstream)] = losses
+        print(json.dumps({"stream": stream, "grad_stream": gstream, "batch": a.batch, "loss_every_10": losses}),
+              flush=True)
         del tr
         torch.cuda.empty_cache()
-    for stream in ("float32", "calculation", "float32", "calculation"):
+    for stream, gstream in combos + combos:
         p = load_config(a.config, {"train_batch_size": a.time_batch, "revnet_stream_dtype": stream,
-                                   "use_hip_graphs": True})
+                                   "revnet_grad_stream_dtype": gstream, "use_hip_graphs": True})
         torch.manual_seed(1234)
         tr = Trainer(p, dev)
         data = batches(2, a.time_batch, p.sequence_length, dev)
@@ -70,7 +73,8 @@ def main():
             tr.step(data[i % 2])
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / a.time_steps
-        print(json.dumps({"stream": stream, "batch": a.time_batch, "ms_per_step": round(dt * 1e3, 1),
+        print(json.dumps({"stream": stream, "grad_stream": gstream, "batch": a.time_batch,
+                          "ms_per_step": round(dt * 1e3, 1),
                           "tokens_per_s": round(a.time_batch * p.sequence_length / dt, 1)}), flush=True)
         del tr
         torch.cuda.empty_cache()
