@@ -301,8 +301,11 @@ static int g4w_queue_env() {
 // tools/lab/r6_tri_group.sh)
 // Auto (unset): 8 when the B operands of the launch exceed 512 MiB (past the 256 MiB MALL), else 0 -- kbench's
 // 32-batch mixer (268 MB of x) ran 3-5 % slower grouped
+static int g_tri_group_force = -1;   // obst_gemm4w_tri_group (tests): >= 0 overrides the env / auto choice
+OBST_API void obst_gemm4w_tri_group(int g) { g_tri_group_force = g; }
 static int g4w_tri_group_env(long long b_bytes) {
   static int v = [] { const char* e = getenv("OBST_G4W_TRI_GROUP"); return e ? atoi(e) : -1; }();
+  if (g_tri_group_force >= 0) return g_tri_group_force;
   if (v >= 0) return v;
   return b_bytes > (512ll << 20) ? 8 : 0;
 }

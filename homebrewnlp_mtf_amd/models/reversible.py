@@ -146,7 +146,7 @@ class _RevStack(torch.autograd.Function):
                 x1 = sink.out if sink is not None and sink.out is not None else _add(y2, fx.detach(), -1.0)
                 if x2.grad is None:
                     dx2 = g1
-                elif gsink is not None and gsink.out is not None:
+                elif gsink is not None and gsink.fused:
                     # the norm's dx already holds g1; if another gradient reached x2 as well, autograd summed it in
                     dx2 = x2.grad
                 else:
@@ -171,7 +171,7 @@ class _RevStack(torch.autograd.Function):
                     x1 = raw.mix_f32(y2, fx.detach(), 1.0, -1.0, yb=nb1)
                 if x2.grad is None:
                     dx2 = g1
-                elif gsink is not None and gsink.out is not None:
+                elif gsink is not None and gsink.fused:
                     dx2 = x2.grad            # the norm's dx already holds g1 (and anything else autograd summed in)
                 else:
                     dx2 = _add(g1, x2.grad)

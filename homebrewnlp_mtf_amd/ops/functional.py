@@ -858,18 +858,20 @@ class ResidualGrad:
 class GradSink:
     """The RevNet stream gradient of a block input (ref src/model/revnet.py:51-120): the norm opening the block adds
     the stream gradient g into its dx inside the backward kernel -- fp32 stream: the sum in fp32 (``out32``) plus the
-    bf16 copy it returns as dx; bf16 stream: dx itself -- replacing the separate dx2 = g1 + dF/dx2 pass. ``out`` holds
-    the summed stream gradient; ``ptr`` is the address of the bf16 dx the norm returned: the stack checks that the
-    input's .grad is exactly it (no other gradient was summed in)."""
+    bf16 copy it returns as dx; bf16 stream: dx itself -- replacing the separate dx2 = g1 + dF/dx2 pass. ``out32`` holds
+    the fp32 sum; ``ptr`` is the address of the bf16 dx the norm returned: the stack checks that the
+    input's .grad is exactly it (no other gradient was summed in). ``fused``: the norm consumed the sink (bf16
+    stream: the sum is the input's .grad itself)."""
 
     def __init__(self, g: torch.Tensor):
         self.g = g
         self.out32: typing.Optional[torch.Tensor] = None
         self.out: typing.Optional[torch.Tensor] = None
+        self.fused = False
         self.ptr = 0
 
     def usable(self, x: torch.Tensor) -> bool:
-        return (self.out is None and raw.on_gpu(self.g) and self.g.dtype in (torch.float32, torch.bfloat16)
+        return (not self.fused and raw.on_gpu(self.g) and self.g.dtype in (torch.float32, torch.bfloat16)
                 and self.g.is_contiguous() and self.g.numel() == x.numel() and self.g.device == x.device)
 
 
@@ -935,11 +937,14 @@ class _Norm(torch.autograd.Function):
         elif sink is not None and R is None and ext is None and sink.usable(xc):
             if sink.g.dtype == torch.bfloat16:   # bf16 stream: dx = norm gradient + stream gradient
                 raw.norm_bwd(xc, dy, ctx.sm32, stats, dx, gsc, gsh, rows, F, groups, Ffull, R=sink.g)
-                sink.out = dx
+                # (no reference to dx kept here: autograd's AccumulateGrad steals a gradient only when nothing else
+                # holds it, else it copies it into .grad -- 0.76 ms per block at ctx32_mixer's batch 256)
+                sink.fused = True
             else:
                 dx32 = torch.empty(xc.shape, dtype=torch.float32, device=xc.device)
                 raw.norm_bwd(xc, dy, ctx.sm32, stats, dx, gsc, gsh, rows, F, groups, Ffull, R32=sink.g, dx32=dx32)
                 sink.out32 = sink.out = dx32
+            sink.fused = True
             sink.ptr = dx.data_ptr()
         else:
             raw.norm_bwd(xc, dy, ctx.sm32, stats, dx, gsc, gsh, rows, F, groups, Ffull, ext_dsum=ext, R=R)

@@ -352,6 +352,17 @@ def test_elementwise(cuda, op, act):
     _close(out[str(cuda)], out["cpu"], 2e-2, 2e-2, f"{op}/{act}")
 
 
+@pytest.mark.parametrize("n", [4096 + 8, 4099])
+def test_add_to_bf16(cuda, n):
+    """bf16(a + b) of two fp32 tensors in one pass (the reversible body's output and input gradient, HIP add2
+    kernel), ragged tail included, against the fp32 sum rounded once on the CPU"""
+    torch.manual_seed(5)
+    a, b = torch.randn(n) * 3, torch.randn(n)
+    got = raw.add_to_bf16(a.to(cuda), b.to(cuda))
+    torch.cuda.synchronize()
+    assert got.dtype == BF and torch.equal(got.cpu(), (a + b).to(BF))
+
+
 def test_xent(cuda):
     torch.manual_seed(11)
     rows, V, Vp = 64, 1000, 1024
@@ -673,6 +684,38 @@ def test_token_mixer_big_tiles(cuda, causal, B, S):
     _close(y, ref, 5e-2, 3e-2, "mixer y")
     _close(xg.grad, xf.grad, 5e-2, 3e-2, "mixer dx")
     _close(wg.grad, wf.grad, 1e-1, 3e-2, "mixer dw")
+
+
+@pytest.mark.parametrize("group", [0, 8, 3])
+def test_token_mixer_work_orders(cuda, group):
+    """the triangular products' work orders (obst_gemm4w_tri_group; production: auto, 8 past 512 MiB of B operands):
+    tile rows slowest (0), batch groups of 8 with the XCD interleave on one residue class, and groups of 3 whose last
+    group is short (B x H = 80 = 26 x 3 + 2) -- every tile exactly once, on the tile queue (320 tiles), against the
+    fp32 oracle"""
+    import ctypes
+    from homebrewnlp_mtf_amd.ops import functional as F
+    setg = L.lib().obst_gemm4w_tri_group
+    setg.argtypes = [ctypes.c_int]
+    torch.manual_seed(7)
+    B, S, H, Fd = 10, 1024, 8, 256
+    x = (torch.randn(B, S, H, Fd) * 0.5).to(BF)
+    w = (torch.randn(H, S, S) * 0.05).to(BF)
+    dy = (torch.randn(B, S, H, Fd) * 0.5).to(BF)
+    xg, wg = x.to(cuda).requires_grad_(True), w.to(cuda).requires_grad_(True)
+    setg(group)
+    try:
+        q0 = g4w_queue_calls()
+        y = F.token_mixer(xg, wg, True)
+        y.backward(dy.to(cuda))
+        torch.cuda.synchronize()
+    finally:
+        setg(-1)
+    assert g4w_queue_calls() - q0 == 2, "y and dx did not take the tile queue"
+    xf, wf = x.float().requires_grad_(True), w.float().requires_grad_(True)
+    ref = torch.einsum("hst,bthf->bshf", torch.tril(wf), xf)
+    ref.backward(dy.float())
+    _close(y, ref, 5e-2, 3e-2, f"mixer y, order {group}")
+    _close(xg.grad, xf.grad, 5e-2, 3e-2, f"mixer dx, order {group}")
 
 
 @pytest.mark.parametrize("M,K,N", [(1, 2048, 2048), (7, 96, 64), (16, 2048, 8192), (32, 8192, 2048),

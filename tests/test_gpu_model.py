@@ -60,8 +60,10 @@ def test_model_forward_backward(cuda, variant, monkeypatch):
                                             "attention-biased_attention_map-absolute-input_as_value-shared"]}])
     if "bf16stream" in variant:
         cfg.update(revnet_stream_dtype="calculation")
-    if variant == "mixer_bf16grad":   # fp32 activation streams, bf16 gradient streams
+    if variant == "mixer_bf16grad":   # fp32 activation streams, bf16 gradient streams (the default)
         cfg.update(revnet_grad_stream_dtype="calculation")
+    elif variant.startswith("mixer"):  # the other mixer variants pin the fp32 gradient streams
+        cfg.update(revnet_grad_stream_dtype="float32")
     torch.manual_seed(0)
     m_cpu, m_gpu = _pair(cfg, cuda)
     x = torch.randint(0, 500, (2, 128, 1))
