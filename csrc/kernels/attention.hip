@@ -765,14 +765,25 @@ __global__ __launch_bounds__(NW * 64, KG == 1 ? 2 : 1) void attn_bwd_dkv_kernel(
 #endif
 
 // one 64-key tile for a wave's 32 queries (query n = lane&31 is `q`); l is this lane's partial row sum
-template <bool MASK, int NKT = 2>
+// BIAS (biased_softmax, ref src/model/spatial.py:65-66,74-75): brow is this lane's query row of the [H][S][S] fp32 map;
+// its 16 values per 32-key sub-tile (keys 8a + 4h + b: four 16-byte loads) are loaded before the score MFMAs and
+// added to the scaled logits after them, so the softmax below runs on scale q.k + b (in log2 units)
+template <bool MASK, int NKT = 2, bool BIAS = false>
 __device__ __forceinline__ void fwd32_tile(const char* sK, const char* sV, const bf16x8_t (&qf)[8],
                                            f32x16_t (&o)[4], float& m, float& l, int k0, int q, int S, int causal,
-                                           float c2, int lane, int prio = 0) {
+                                           float c2, int lane, int prio = 0, const float* brow = nullptr) {
   const int h = lane >> 5;
   Frag32 fo;
   frag32_offsets(fo, lane);
   f32x16_t s[NKT];
+  f32x4_t bv[BIAS ? NKT * 4 : 1];
+  if constexpr (BIAS) {
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+      for (int a4 = 0; a4 < 4; ++a4)
+        bv[kt * 4 + a4] = *reinterpret_cast<const f32x4_t*>(brow + k0 + kt * 32 + 8 * a4 + 4 * h);
+  }
   if (prio) __builtin_amdgcn_s_setprio(1);
   // the NKT score chains interleaved k-step by k-step, K fragments read FWD_KPF k-steps ahead of their MFMA: with
   // one chain at a time the compiler re-used one fragment register and every MFMA waited out a full LDS read
@@ -798,6 +809,13 @@ __device__ __forceinline__ void fwd32_tile(const char* sK, const char* sV, const
       s[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[ks % (PF + 1)][kt], qf[ks], s[kt], 0, 0, 0);
   }
   if (prio) __builtin_amdgcn_s_setprio(0);
+  if constexpr (BIAS) {   // logits in log2 units: scale q.k log2(e) + b log2(e); the softmax below then takes c2 = 1
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s[kt][r] = __builtin_fmaf(s[kt][r], c2, bv[kt * 4 + (r >> 2)][r & 3] * LOG2E);
+    c2 = 1.f;
+  }
   float mx = -INFINITY;
 #pragma unroll
   for (int kt = 0; kt < NKT; ++kt)
@@ -855,7 +873,7 @@ __device__ __forceinline__ void fwd32_tile(const char* sK, const char* sV, const
 // the tile loop is unrolled by two so both buffers' fragment addresses are immediates
 // KT = 32: 32-key tiles in a 4-deep ring (the same 64 KiB), the next three tiles in flight instead of one
 // NW = 8: 256 queries per block, one block per CU -- the K/V tiles each CU streams from L2 halve (A/B knob)
-template <int KT = 64, int NW = 4>
+template <int KT = 64, int NW = 4, bool BIAS = false>
 __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd32_kernel(AttnArgs a) {
   constexpr int D = 128;
   constexpr int TILE = KT * 256;
@@ -908,6 +926,8 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd32_kernel(AttnArgs a)
   for (int dt = 0; dt < 4; ++dt) o[dt] = f32x16_t{};
   float m = NEG_BIG, l = 0.f;
   const float c2 = a.scale * LOG2E;
+  // BIAS: this lane's query row of the map (rows past S read the last row; their outputs are not stored)
+  const float* brow = BIAS ? a.bias + ((long long)hd * a.S + min(q, a.S - 1)) * a.S : nullptr;
   vm_wait<0>();
   __syncthreads();
   // key tiles in two branch-free runs, unmasked then the block's masked band (as in the backward kernels): the
@@ -921,7 +941,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd32_kernel(AttnArgs a)
     const char* sV = sK + TILE;
     const int kn = kb + NS - 1;   // its slot was last read in iteration kb - 1 (behind the barrier)
     if (kn < nkb) stage(smem + (kn % NS) * 2 * TILE, kn * KT);
-    fwd32_tile<MK, KT / 32>(sK, sV, qf, o, m, l, k0, q, a.S, a.causal, c2, lane, a.prio & 4);
+    fwd32_tile<MK, KT / 32, BIAS>(sK, sV, qf, o, m, l, k0, q, a.S, a.causal, c2, lane, a.prio & 4, brow);
     // tile kb + 1 has landed; tiles kb + 2 .. kb + NS - 2 may stay in flight (2 NP pieces per wave per tile)
     const int ahead = min(NS - 2, nkb - 2 - kb);
     if (NS >= 4 && ahead >= 2) vm_wait<4 * NP>();
@@ -1054,6 +1074,7 @@ static bool fill(AttnArgs& a, const ObstAttnDesc* d) {
   a.B = d->B; a.S = d->S; a.H = d->H; a.ld = d->ld; a.scale = d->scale; a.causal = d->causal;
   a.ld_o = d->ld_o ? d->ld_o : d->ld;
   a.Res = (const bf16_t*)d->Res; a.Sum = (bf16_t*)d->Sum;
+  a.bias = nullptr;
   if ((a.Res == nullptr) != (a.Sum == nullptr)) return false;
   static const int prio = [] { const char* e = getenv("OBST_ATTN_PRIO"); return e ? atoi(e) : 3; }();
   a.prio = prio;
@@ -1071,6 +1092,19 @@ OBST_API int obst_attn_fwd(const ObstAttnDesc* d, hipStream_t st) {
     case 128: return launch_fwd<128>(a, st);
     default: return -2;
   }
+}
+
+// biased_softmax forward on the flash schedule (D = 128, S % 128 == 0): attn_fwd32_kernel over 32-key tiles in a
+// 4-deep ring (185 VGPRs: room for the 16 map values per lane and tile that the 64-key kernel's 239 do not leave),
+// the [H][S][S] fp32 map added to the scaled logits. O and LSE as the map kernels of attn_map.hip write them, so
+// their backward consumes this forward unchanged.
+OBST_API int obst_attn_fwd_bias(const ObstAttnDesc* d, const float* bias, hipStream_t st) {
+  AttnArgs a;
+  if (!fill(a, d) || d->D != 128 || !bias || d->S % 128 || a.Sum) return -1;
+  a.bias = bias;
+  dim3 grid(d->S / 128 * d->B * d->H);
+  hipLaunchKernelGGL((attn_fwd32_kernel<32, 4, true>), grid, dim3(NTH), 4 * 2 * 32 * 256, st, a);
+  return (int)hipGetLastError();
 }
 
 OBST_API int obst_attn_bwd(const ObstAttnDesc* d, hipStream_t st) {

@@ -87,6 +87,7 @@ _SIGS = {
     "obst_gemm": [ctypes.POINTER(GemmDesc), c_p],
     "obst_attn_fwd": [ctypes.POINTER(AttnDesc), c_p],
     "obst_attn_bwd": [ctypes.POINTER(AttnDesc), c_p],
+    "obst_attn_fwd_bias": [ctypes.POINTER(AttnDesc), c_p, c_p],
     "obst_attn_map_fwd": [ctypes.POINTER(MapDesc), c_p],
     "obst_attn_map_bwd": [ctypes.POINTER(MapDesc), c_p],
     "obst_attn_map_bsplit": [c_i, c_i, c_i],

@@ -353,6 +353,11 @@ def _map_logits(q, k, bias, B, S, H, D, scale, causal):
     return s
 
 
+# OBST_MAP_FLASH (default 1): the bias-only D = 128 map forward (S % 128 == 0) on the flash kernel; 0: attn_map.hip
+_MAP_FLASH = __import__("os").environ.get("OBST_MAP_FLASH", "1") != "0"
+map_flash_calls = 0   # (tests: forwards that took the flash path)
+
+
 def attn_map_fwd(q, k, v, o, lse, bias, cmap, B, S, H, D, scale: float, causal: bool):
     if q.device.type == "meta":
         return None
@@ -369,6 +374,15 @@ def attn_map_fwd(q, k, v, o, lse, bias, cmap, B, S, H, D, scale: float, causal: 
                     raise L.KernelError(f"attention map {nm} must be contiguous fp32")
                 _need(t, H * S * S - 1, nm)
         _need(lse, B * H * S - 1, "lse")
+        if _MAP_FLASH and bias is not None and cmap is None and D == 128 and S % 128 == 0:
+            # biased_softmax on the flash forward (attention.hip attn_fwd32_kernel with the map hook); the map
+            # kernels' backward consumes its o / lse unchanged
+            global map_flash_calls
+            map_flash_calls += 1
+            d = L.AttnDesc(q.data_ptr(), k.data_ptr(), v.data_ptr(), 0, 0, o.data_ptr(), 0, 0, 0, lse.data_ptr(), 0,
+                           B, S, H, D, H * D, float(scale), int(causal), H * D, 0, 0)
+            L.check(L.lib().obst_attn_fwd_bias(d, bias.data_ptr(), L.stream_ptr()), "attn_fwd_bias")
+            return
         d = L.MapDesc(q.data_ptr(), k.data_ptr(), v.data_ptr(), 0, 0, o.data_ptr(), 0, 0, 0, L.ptr(bias), L.ptr(cmap),
                       0, 0, 0, 0, lse.data_ptr(), 0, B, S, H, D, 1, float(scale), int(causal))
         L.check(L.lib().obst_attn_map_fwd(d, L.stream_ptr()), "attn_map_fwd")

@@ -71,8 +71,11 @@ def test_attn_map_single_batch_slice(cuda):
 
 
 def test_attn_map_training_shape_class(cuda):
-    """multi-block causal paths at S = 2048 (32 query / key blocks), head dim 128"""
+    """multi-block causal paths at S = 2048 (32 query / key blocks), head dim 128; the bias-only forward runs on the
+    flash kernel with the map hook (attention.hip, obst_attn_fwd_bias)"""
+    n0 = raw.map_flash_calls
     _case(cuda, 2, 2048, 2, 128, True, "bias", seed=7)
+    assert raw.map_flash_calls == n0 + 1, "the D = 128 bias forward did not take the flash kernel"
 
 
 def test_attn_map_deterministic(cuda):

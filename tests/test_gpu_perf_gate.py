@@ -33,10 +33,7 @@ def test_hot_kernels_meet_their_floors(cuda):
     assert all(k in spec["floors"] for k in kbench.gate_keys()), "a gate row has no floor"
     for r in rows:
         print(json.dumps(r))
-    # compute rows: the ratio to the same-process MFMA loop (tracks the box's clock). Memory rows: the ratio to a
-    # torch device copy, or the absolute GB/s -- the copy itself read 4.6-5.3 TB/s across boxes at equal kernel GB/s
-    # (profiles/r6_perf_gate.md), so a memory row fails only when it misses both
-    bad_ratio = kbench.check(rows, spec["floors"], TOL, spec.get("ratios", {}))
-    bad_abs = {(k, m.replace("ratio_", "")) for k, m, _, _ in kbench.check(rows, spec["floors"], TOL)}
-    bad = [b for b in bad_ratio if not b[1].startswith("ratio_gbps") or (b[0], "gbps") in bad_abs]
+    # a row fails only when it misses both its calibration ratio and its absolute floor: the same-process
+    # calibrations move between boxes (MFMA loop 1904-2091 TF/s, copy 4.6-5.3 TB/s) at equal kernel numbers
+    bad = kbench.check_either(rows, spec["floors"], TOL, spec.get("ratios", {}))
     assert not bad, "perf regression: " + "; ".join(f"{k} {m} {v} < floor {fl} - {TOL:.0%}" for k, m, v, fl in bad)

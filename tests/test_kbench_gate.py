@@ -57,3 +57,14 @@ def test_rows_get_calibration_ratios():
     r = kbench.EMITTED[-1]
     assert r["ratio_pflops_fwd"] == 0.4 and r["ratio_gbps"] == 0.6
     kbench.EMITTED.clear()
+
+
+def test_check_either_needs_both_floors_missed():
+    """a row regresses only when it misses its ratio floor AND its absolute floor (box calibration drift alone does
+    not fail it; a slower kernel fails both)"""
+    floors = {"k": {"gbps": 100.0}}
+    ratios = {"k": {"gbps": 1.0}}
+    fast_calib = {"kernel": "k", "gbps": 101.0, "ratio_gbps": 0.9}    # calibration read high: ratio misses only
+    assert kbench.check_either([fast_calib], floors, 0.03, ratios) == []
+    slow = {"kernel": "k", "gbps": 90.0, "ratio_gbps": 0.9}
+    assert kbench.check_either([slow], floors, 0.03, ratios) != []

@@ -24,9 +24,9 @@ metrics (GB/s) over the copy. Devices differ by up to ~12 % on an MFMA loop at t
 'DVFS give-back' item 5), so the gate compares ratios.
 
 --check FLOOR.json (the perf-regression gate of tools/gpu_final.sh): every emitted line whose key (kernel, shape) has
-floors in the file must reach each floored ratio (``ratios``; the absolute ``floors`` where a key has no ratio)
-within --tol (default 3 %), and every floored key of a section that ran must have been emitted; the exit status is
-1 otherwise. --write-floors PATH writes the observed ratios as a new floor file.
+floors in the file must reach, within --tol (default 3 %), its floored calibration ratio (``ratios``) OR its absolute
+floor (``floors``) -- a metric regresses only when it misses both (check_either) -- and every floored key of a
+section that ran must have been emitted; the exit status is 1 otherwise. --write-floors PATH writes the observed ratios as a new floor file.
 
 The profiles under profiles/ quote these numbers; the one-off A/B scripts next to it (bench_*.py, gpu_*.sh) are the
 lab notes behind individual measurements (tools/README.md).
@@ -147,6 +147,17 @@ def missing(floors: dict, seen: set, sections) -> list:
     """floor keys of the sections that ran but that no emitted row carries (a renamed / dropped kernel or shape
     must not silently skip its floor)"""
     return sorted(k for k in floors if section_of(k) in sections and k not in seen)
+
+
+def check_either(rows, floors: dict, tol: float = 0.03, ratios: typing.Optional[dict] = None):
+    """the gate's rule: a metric regresses only when it misses BOTH its calibration-ratio floor and its absolute
+    floor. The same-process calibrations themselves move between boxes (MFMA loop 1904-2091 TF/s, device copy
+    4.6-5.3 TB/s in rounds 5-6) while the kernels' own numbers do not, so either one alone flags healthy boxes
+    (profiles/r6_perf_gate.md); a kernel that really got slower misses both."""
+    bad_r = check(rows, floors, tol, ratios)
+    bad_a = {(k, m) for k, m, _, _ in check(rows, floors, tol)}
+    return [b for b in bad_r if not b[1].startswith("ratio_") or (b[0], b[1][len("ratio_"):]) in bad_a
+            or b[0] not in floors]
 
 
 def check(rows, floors: dict, tol: float = 0.03, ratios: typing.Optional[dict] = None):
@@ -388,7 +399,7 @@ def main(argv=None):
         with open(a.check) as f:
             spec = json.load(f)
         floors, ratios = spec["floors"], spec.get("ratios", {})
-        bad = check(EMITTED, floors, a.tol, ratios)
+        bad = check_either(EMITTED, floors, a.tol, ratios)
         seen = {line_key(r) for r in EMITTED}
         for key, metric, v, floor in bad:
             print(f"REGRESSION {key}: {metric} {v} < floor {floor} - {a.tol:.0%}", flush=True)
