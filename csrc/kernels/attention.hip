@@ -222,18 +222,34 @@ __global__ __launch_bounds__(NTH) void attn_delta_kernel(AttnArgs a) {
 #define DKV_PF 2   // score-loop fragment prefetch distance of dq_tile / dkv_chunk (0: the plain loops)
 #endif
 
+// backward map hook (biased_softmax): 1 loads a tile's map values after its score MFMAs instead of before them (their
+// registers are then not live across the MFMA loop of the kernels that already use all 256 VGPRs)
+#ifndef BIAS_LATE
+#define BIAS_LATE 1
+#endif
+
 // one 64-key tile of the dQ kernel for a wave's 32 queries (two 32-key halves: P needs only the stored LSE, so no
 // state crosses the halves). dP starts from -delta (the accumulator init), so dS = P * dP.
-template <int D, bool MASK, int HALVES = 2>
+// BIAS (biased_softmax): bq = this lane's query row (qt = 0) of the [H][S][S] map; its 4 keys per 16-key sub-tile are
+// one 16-byte load, issued before the score MFMAs and added to the scaled logits after them
+template <int D, bool MASK, int HALVES = 2, bool BIAS = false>
 __device__ __forceinline__ void dq_tile(const char* sK, const char* sV, const bf16x8_t (&qf)[2][Geo<D>::DS],
                                         const bf16x8_t (&df)[2][Geo<D>::DS], const float (&lse2)[2],
                                         const float (&dlt)[2], f32x4_t (&acc)[Geo<D>::DT][2], int k0, int qw, int S,
-                                        int causal, float c2, int lane, int prio = 0) {
+                                        int causal, float c2, int lane, int prio = 0, const float* bq = nullptr) {
   using G = Geo<D>;
   const int g = lane >> 4, i = lane & 15;
 #pragma unroll
   for (int st = 0; st < HALVES; ++st) {
-    f32x4_t sc[2][2], dp[2][2];
+    f32x4_t sc[2][2], dp[2][2], bv[2][2];
+    auto load_bias = [&]() {
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+          bv[qt][kk] = *reinterpret_cast<const f32x4_t*>(bq + (long long)qt * 16 * S + k0 + (2 * st + kk) * 16 + 4 * g);
+    };
+    if constexpr (BIAS && !BIAS_LATE) load_bias();
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt)
 #pragma unroll
@@ -280,6 +296,7 @@ __device__ __forceinline__ void dq_tile(const char* sK, const char* sV, const bf
     }
     }
     if (prio) __builtin_amdgcn_s_setprio(0);
+    if constexpr (BIAS && BIAS_LATE) load_bias();
     bf16x8_t sf[2];
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) {
@@ -289,7 +306,9 @@ __device__ __forceinline__ void dq_tile(const char* sK, const char* sV, const bf
       for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
-          float p = fexp2(__builtin_fmaf(sc[qt][kk][v], c2, nl));
+          float x = __builtin_fmaf(sc[qt][kk][v], c2, nl);
+          if constexpr (BIAS) x = __builtin_fmaf(bv[qt][kk][v], LOG2E, x);
+          float p = fexp2(x);
           if (MASK) {
             const int key = k0 + (2 * st + kk) * 16 + 4 * g + v;
             p = (key >= S || (causal && key > q)) ? 0.f : p;
@@ -329,7 +348,7 @@ __device__ __forceinline__ void dq_tile(const char* sK, const char* sV, const bf
 // dQ: block = NW x 32 queries; recompute Sᵀ, Pᵀ, dPᵀ = V·dOᵀ, dSᵀ, dQᵀ += Kᵀ·dSᵀ. K/V tiles in an NS-deep LDS ring
 // filled by LDS-DMA NS - 1 tiles ahead (NW = 8, NS = 3: one block per CU, every wave's DMA share of a tile is 4
 // pieces, a tile has two tiles' time to land instead of one).
-template <int D, int NW = 4, int NS = 2, int KT = 64>
+template <int D, int NW = 4, int NS = 2, int KT = 64, bool BIAS = false>
 __global__ __launch_bounds__(NW * 64, 2) void attn_bwd_dq_kernel(AttnArgs a) {
   using G = Geo<D>;
   constexpr int TILE = KT * G::ROWB;                   // KT keys per K / V tile (64, or 32 in a 4-deep ring)
@@ -398,6 +417,7 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_bwd_dq_kernel(AttnArgs a) {
 #pragma unroll
   for (int dt = 0; dt < G::DT; ++dt) acc[dt][0] = acc[dt][1] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   const float c2 = a.scale * LOG2E;
+  const float* bq = BIAS ? a.bias + ((long long)h * a.S + qw + i) * a.S : nullptr;
   vm_wait<0>();   // staged tiles (asm LDS-DMA: the compiler does not track them) have landed
   __syncthreads();
   // key tiles in two branch-free runs: unmasked, then masked (the causal diagonal band of the whole block, and a ragged
@@ -411,7 +431,7 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_bwd_dq_kernel(AttnArgs a) {
     const char* sV = sK + TILE;
     const int kn = kb + NS - 1;   // tile issued now; its slot was last read in iteration kb - 1 (behind a barrier)
     if (kn < nkb) stage_kv(smem + (kn % NS) * 2 * TILE, kn);
-    dq_tile<D, MK, KT / 32>(sK, sV, qf, df, lse2, dlt, acc, k0, qw, a.S, a.causal, c2, lane, a.prio & 2);
+    dq_tile<D, MK, KT / 32, BIAS>(sK, sV, qf, df, lse2, dlt, acc, k0, qw, a.S, a.causal, c2, lane, a.prio & 2, bq);
     // tile kb + 1 must have landed; tiles kb + 2 .. kb + NS - 2 may stay in flight across the barrier (counted
     // wait: the only vector-memory ops of this loop are the DMA pieces, PPW per wave per tile)
     const int ahead = min(NS - 2, nkb - 2 - kb);
@@ -464,14 +484,34 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_bwd_dq_kernel(AttnArgs a) {
 // dVᵀ and dKᵀ as B operands straight from the accumulators). dP starts from -delta[q] (read from LDS as one f32x4 per
 // tile). Every Q / dO fragment read from LDS feeds KG MFMAs: with KG = 2 the LDS bytes per MFMA halve (at KG = 1 the
 // 104 LDS reads of a chunk take ~2300 LDS cycles per CU against ~2050 MFMA cycles per SIMD: LDS-bound).
-template <int D, bool MASK, int KG, int NQT = 4>
+// BIAS (biased_softmax, KG = 1): bcol / dcol = this head's [S][S] map and this batch's partial map gradient (uniform
+// bases, 32-bit per-lane offsets q * S + key). The 16 map values of a chunk (queries 4g + v of each 16-query tile) are loaded before the score MFMAs;
+// dS is stored to dcol for every query of the chunk (masked entries as 0) -- the dK/dV kernel visits every (query,
+// key) pair of the causal triangle exactly once per batch, so the partial maps need no zeroing or accumulation
+template <int D, bool MASK, int KG, int NQT = 4, bool BIAS = false>
 __device__ __forceinline__ void dkv_chunk(const char* sQ, const char* sD, const float* sL, const float* sDl,
                                           const bf16x8_t (&kf)[KG][Geo<D>::DS], const bf16x8_t (&vf)[KG][Geo<D>::DS],
                                           f32x4_t (&dk)[KG][Geo<D>::DT], f32x4_t (&dv)[KG][Geo<D>::DT], int q0,
-                                          int key, int S, int causal, float c2, int lane, int prio) {
+                                          int key, int S, int causal, float c2, int lane, int prio,
+                                          const float* bcol = nullptr, float* dcol = nullptr) {
   using G = Geo<D>;
+  static_assert(!BIAS || KG == 1, "the map hook covers one 16-key group per wave");
   const int g = lane >> 4;
   f32x4_t sc[KG][NQT], dp[KG][NQT];
+  float bv[BIAS ? NQT : 1][4];
+  // buffer accesses: one lane offset for the whole kernel ((4g S + key) * 4 bytes) plus a uniform SGPR offset per
+  // (tile, row) -- no per-access 64-bit address registers in a kernel already at 256 VGPRs
+  const int voff = (4 * g * S + key) * 4;
+  const int nrec = S * S * 4;
+  auto load_bias = [&]() {
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(bcol), 0, nrec, 0x00020000);
+#pragma unroll
+    for (int qt = 0; qt < NQT; ++qt)
+#pragma unroll
+      for (int v = 0; v < 4; ++v)
+        bv[qt][v] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, voff, (q0 + qt * 16 + v) * S * 4, 0));
+  };
+  if constexpr (BIAS && !BIAS_LATE) load_bias();
 #pragma unroll
   for (int qt = 0; qt < NQT; ++qt) {
     const float4 dl = *reinterpret_cast<const float4*>(sDl + qt * 16 + 4 * g);
@@ -520,6 +560,7 @@ __device__ __forceinline__ void dkv_chunk(const char* sQ, const char* sD, const 
   }
   }
   if (prio) __builtin_amdgcn_s_setprio(0);
+  if constexpr (BIAS && BIAS_LATE) load_bias();
   // sc[j][qt][v] = S[q = q0 + qt*16 + 4g + v][key + 16 j]
 #pragma unroll
   for (int qt = 0; qt < NQT; ++qt) {
@@ -529,13 +570,21 @@ __device__ __forceinline__ void dkv_chunk(const char* sQ, const char* sD, const 
     for (int j = 0; j < KG; ++j)
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
-        float pv = fexp2(__builtin_fmaf(sc[j][qt][v], c2, nl[v]));
+        float x = __builtin_fmaf(sc[j][qt][v], c2, nl[v]);
+        if constexpr (BIAS) x = __builtin_fmaf(bv[qt][v], LOG2E, x);
+        float pv = fexp2(x);
         if (MASK) {
           const int q = q0 + qt * 16 + 4 * g + v, kj = key + 16 * j;
           pv = (q >= S || kj >= S || (causal && kj > q)) ? 0.f : pv;
         }
         sc[j][qt][v] = pv;
         dp[j][qt][v] = pv * dp[j][qt][v];
+        if constexpr (BIAS) {
+          // a plain store: the raw_buffer_store builtin with per-row SGPR offsets compiled to one value stored to all
+          // four rows of a lane (ROCm 7.2 clang; the loads above are unaffected -- checked in the device assembly)
+          char* row = reinterpret_cast<char*>(dcol + (long long)(q0 + qt * 16 + v) * S);
+          *reinterpret_cast<float*>(row + (unsigned)voff) = dp[j][qt][v];
+        }
       }
   }
   if (prio) __builtin_amdgcn_s_setprio(1);
@@ -594,7 +643,7 @@ __device__ __forceinline__ void dkv_chunk(const char* sQ, const char* sD, const 
 // ----------------------------------------------------------------------------------------------------------------
 // dK/dV: block = NW x KG x 16 keys; wave w owns keys k0 + 16 KG w + [0, 16 KG). Loop over 64-query chunks (Q, dO, lse,
 // delta) in an NS-deep LDS ring filled by LDS-DMA NS - 1 chunks ahead. KG = 2 holds ~300 registers: one wave per SIMD.
-template <int D, int NW = 4, int NS = 2, int KG = 1, int QC = 64>
+template <int D, int NW = 4, int NS = 2, int KG = 1, int QC = 64, bool BIAS = false>
 __global__ __launch_bounds__(NW * 64, KG == 1 ? 2 : 1) void attn_bwd_dkv_kernel(AttnArgs a) {
   using G = Geo<D>;
   constexpr int TILE = QC * G::ROWB;
@@ -662,6 +711,8 @@ __global__ __launch_bounds__(NW * 64, KG == 1 ? 2 : 1) void attn_bwd_dkv_kernel(
     for (int dt = 0; dt < G::DT; ++dt) dk[j][dt] = dv[j][dt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   const float c2 = a.scale * LOG2E;
   const int key = kw + i;
+  const float* bcol = BIAS ? a.bias + (long long)h * a.S * a.S : nullptr;
+  float* dcol = BIAS ? a.dbias + ((long long)b * a.H + h) * a.S * a.S : nullptr;
   vm_wait<0>();   // staged tiles (asm LDS-DMA: the compiler does not track them) have landed
   __syncthreads();
   // Chunks in three branch-free runs: masked (causal diagonal band of the whole block, or every chunk when the block's
@@ -681,7 +732,8 @@ __global__ __launch_bounds__(NW * 64, KG == 1 ? 2 : 1) void attn_bwd_dkv_kernel(
     const float* sDl = sL + 64;
     const int cn = c + NS - 1;
     if (cn < nqc) stage(smem + (cn % NS) * STAGE, qstart + cn * QC);
-    dkv_chunk<D, MK, KG, QC / 16>(sQ, sD, sL, sDl, kf, vf, dk, dv, q0, key, a.S, a.causal, c2, lane, a.prio & 1);
+    dkv_chunk<D, MK, KG, QC / 16, BIAS>(sQ, sD, sL, sDl, kf, vf, dk, dv, q0, key, a.S, a.causal, c2, lane,
+                                        a.prio & 1, bcol, dcol);
     // chunk c + 1 must have landed; chunks c + 2 .. c + NS - 2 may stay in flight across the barrier. Per chunk a
     // wave issues PPW pieces, plus the lse / delta pieces: NW = 4 wave 0 issues both, NW = 8 waves 0 and 1 one each
     const int ahead = min(NS - 2, nqc - 2 - c);
@@ -1051,6 +1103,24 @@ int launch_bwd(const AttnArgs& a, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
+// dbias[h][q][k] = sum over b (in order) of part[b][h][q][k]; 0 above the diagonal when causal (never written there)
+__global__ __launch_bounds__(NTH) void bias_fold_kernel(const float* __restrict__ part, float* __restrict__ out, int B,
+                                                        long long n, int S, int causal) {
+  for (long long v = (long long)blockIdx.x * NTH + threadIdx.x; v * 4 < n; v += (long long)gridDim.x * NTH) {
+    const long long e = v * 4;
+    const int k = (int)(e % S), q = (int)((e / S) % S);
+    f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+    if (!causal || k <= q) {
+      for (int b = 0; b < B; ++b) acc += *reinterpret_cast<const f32x4_t*>(part + b * n + e);
+      if (causal) {
+#pragma unroll
+        for (int j = 1; j < 4; ++j) acc[j] = k + j > q ? 0.f : acc[j];
+      }
+    }
+    *reinterpret_cast<f32x4_t*>(out + e) = acc;
+  }
+}
+
 }  // namespace
 
 struct ObstAttnDesc {
@@ -1075,6 +1145,7 @@ static bool fill(AttnArgs& a, const ObstAttnDesc* d) {
   a.ld_o = d->ld_o ? d->ld_o : d->ld;
   a.Res = (const bf16_t*)d->Res; a.Sum = (bf16_t*)d->Sum;
   a.bias = nullptr;
+  a.dbias = nullptr;
   if ((a.Res == nullptr) != (a.Sum == nullptr)) return false;
   static const int prio = [] { const char* e = getenv("OBST_ATTN_PRIO"); return e ? atoi(e) : 3; }();
   a.prio = prio;
@@ -1104,6 +1175,25 @@ OBST_API int obst_attn_fwd_bias(const ObstAttnDesc* d, const float* bias, hipStr
   a.bias = bias;
   dim3 grid(d->S / 128 * d->B * d->H);
   hipLaunchKernelGGL((attn_fwd32_kernel<32, 4, true>), grid, dim3(NTH), 4 * 2 * 32 * 256, st, a);
+  return (int)hipGetLastError();
+}
+
+// biased_softmax backward on the flash schedule (D = 128, S % 128 == 0): the dQ and dK/dV kernels with the map hook;
+// the dK/dV kernel writes dS per batch into part ([B][H][S][S] fp32, no zeroing needed), bias_fold_kernel sums the
+// batches in order into dbias ([H][S][S]) -- deterministic, no atomics
+OBST_API int obst_attn_bwd_bias(const ObstAttnDesc* d, const float* bias, float* part, float* dbias, hipStream_t st) {
+  AttnArgs a;
+  if (!fill(a, d) || d->D != 128 || !bias || !part || !dbias || d->S % 128) return -1;
+  a.bias = bias;
+  a.dbias = part;
+  hipLaunchKernelGGL((attn_bwd_dq_kernel<128, 4, 4, 32, true>), dim3(d->S / 128 * d->B * d->H), dim3(NTH),
+                     4 * 2 * 32 * Geo<128>::ROWB, st, a);
+  hipLaunchKernelGGL((attn_bwd_dkv_kernel<128, 4, 2, 1, 64, true>), dim3(d->S / 64 * d->B * d->H), dim3(NTH),
+                     2 * (2 * 64 * Geo<128>::ROWB + 512), st, a);
+  const long long n = (long long)d->H * d->S * d->S;
+  const long long nv = n / 4;
+  const unsigned g = (unsigned)(nv / NTH + 1 < 8192 ? nv / NTH + 1 : 8192);
+  hipLaunchKernelGGL(bias_fold_kernel, dim3(g), dim3(NTH), 0, st, part, dbias, d->B, n, d->S, d->causal);
   return (int)hipGetLastError();
 }
 

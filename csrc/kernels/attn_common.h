@@ -169,7 +169,8 @@ struct AttnArgs {
   int prio;       // s_setprio(1) around the MFMA clusters: bit 0 dK/dV kernel (default on: -2 %), bit 1 dQ (+1 %: off)
   const bf16_t* Res;   // forward, optional: Sum = bf16(O) + Res, the block's residual add (O's layout, row stride ld_o)
   bf16_t* Sum;
-  const float* bias;   // forward, optional (obst_attn_fwd_bias): [H][S][S] fp32 added to the scaled logits
+  const float* bias;   // optional (obst_attn_fwd_bias / obst_attn_bwd_bias): [H][S][S] fp32 added to the scaled logits
+  float* dbias;        // backward with bias: per-batch partial map gradients [B][H][S][S] (dS of the dK/dV kernel)
 };
 
 // the forward epilogue's 4-element store of O (and, with a residual, of O + residual from the rounded O values)

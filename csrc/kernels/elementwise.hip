@@ -285,6 +285,17 @@ __global__ __launch_bounds__(NTH) void cast_f32_bf16_kernel(const float* __restr
   }
 }
 
+// y(fp32) = x(bf16): the reversible body's fp32 streams out of its bf16 input
+__global__ __launch_bounds__(NTH) void cast_bf16_f32_kernel(const bf16_t* __restrict__ X, float* __restrict__ Y,
+                                                            long long nvec) {
+  for (long long v = (long long)blockIdx.x * NTH + threadIdx.x; v < nvec; v += (long long)gridDim.x * NTH) {
+    float r[8];
+    unpack8(reinterpret_cast<const uint4*>(X)[v], r);
+    reinterpret_cast<float4*>(Y)[2 * v] = make_float4(r[0], r[1], r[2], r[3]);
+    reinterpret_cast<float4*>(Y)[2 * v + 1] = make_float4(r[4], r[5], r[6], r[7]);
+  }
+}
+
 // y(bf16) = x1(fp32) + x2(fp32) in one pass: the reversible body's output (y1 + y2) and the embedding's gradient out of
 // it (g1 + g2), instead of an fp32 add plus a cast (18 -> 10 bytes per element)
 __global__ __launch_bounds__(NTH) void add2_f32_bf16_kernel(const float* __restrict__ X1, const float* __restrict__ X2,
@@ -410,6 +421,13 @@ OBST_API int obst_add2_f32_bf16(const float* X1, const float* X2, void* Y, long 
 
 OBST_API int obst_cast_f32_bf16(const float* X, void* Y, long long n, hipStream_t st) {
   hipLaunchKernelGGL(cast_f32_bf16_kernel, dim3(grid_ew((n + 3) / 4)), dim3(NTH), 0, st, X, (bf16_t*)Y, n);
+  return (int)hipGetLastError();
+}
+
+OBST_API int obst_cast_bf16_f32(const void* X, float* Y, long long n, hipStream_t st) {
+  if (n % 8) return -1;
+  if ((((uintptr_t)X) | ((uintptr_t)Y)) & 15) return -2;
+  hipLaunchKernelGGL(cast_bf16_f32_kernel, dim3(grid_ew(n / 8)), dim3(NTH), 0, st, (const bf16_t*)X, Y, n / 8);
   return (int)hipGetLastError();
 }
 

@@ -60,10 +60,21 @@ def _add(a, b, beta: float = 1.0):
 
 
 def _sum_to(a, b, dt):
-    """(a + b) in dtype dt: one fused fp32 + fp32 -> bf16 pass on the GPU (raw.add_to_bf16)"""
-    if dt == torch.bfloat16 and a.dtype == torch.float32 and raw.on_gpu(a):
-        return raw.add_to_bf16(a, b)
+    """(a + b) in dtype dt: one fused fp32 + fp32 -> bf16 pass on the GPU (raw.add_to_bf16), bf16 + bf16 through
+    the HIP axpby"""
+    if dt == torch.bfloat16 and raw.on_gpu(a):
+        if a.dtype == torch.float32 and b.dtype == torch.float32:
+            return raw.add_to_bf16(a, b)
+        if a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16:
+            return _add(a, b)
     return (a + b).to(dt)
+
+
+def _to_stream(x, sd):
+    """the body input as a stream: bf16 -> fp32 through the HIP cast kernel on the GPU"""
+    if sd == torch.float32 and x.dtype == torch.bfloat16 and raw.on_gpu(x):
+        return raw.to_f32(x)
+    return x.to(sd)
 
 
 def _axpby(x, z, alpha, beta):
@@ -87,7 +98,7 @@ class _RevStack(torch.autograd.Function):
         dt = x.dtype
         calc = calc and mode == "revnet"
         sd = _stream_dtype(dt, calc)
-        x1 = x2 = x.to(sd)
+        x1 = x2 = _to_stream(x, sd)
         low = dt != sd                      # fused fp32 <- fp32 + bf16 kernels on the GPU
         with torch.no_grad():
             if calc:
@@ -99,7 +110,8 @@ class _RevStack(torch.autograd.Function):
                     nx2 = sink.out if sink is not None and sink.out is not None else _add(x1, fx)
                     x1, x2 = x2, nx2
             elif mode == "revnet" and low:
-                x2b = raw.to_bf16(x2)
+                # the bf16 copy of the fp32 stream is the (bf16) input itself: bf16 -> fp32 -> bf16 is exact
+                x2b = x.contiguous() if x.dtype == torch.bfloat16 else raw.to_bf16(x2)
                 for f in blocks:
                     # y2 = x1 + F(x2) and its bf16 copy: from the block's last GEMM when it can take the update
                     # (F.StreamSink), else one mix_f32 pass

@@ -269,7 +269,8 @@ class ParamStore:
         return hit[1]
 
     def zero_grad(self):
-        self.grad.zero_()
+        from ..ops import raw
+        raw.zero_(self.grad)
         # variables whose gradient has received no contribution yet this step: their first weight-gradient GEMM
         # may overwrite (beta = 0) instead of accumulating (ops/functional.py::_acc_grad_beta)
         self.fresh = set(self.order)

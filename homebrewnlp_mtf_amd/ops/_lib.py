@@ -88,6 +88,7 @@ _SIGS = {
     "obst_attn_fwd": [ctypes.POINTER(AttnDesc), c_p],
     "obst_attn_bwd": [ctypes.POINTER(AttnDesc), c_p],
     "obst_attn_fwd_bias": [ctypes.POINTER(AttnDesc), c_p, c_p],
+    "obst_attn_bwd_bias": [ctypes.POINTER(AttnDesc), c_p, c_p, c_p, c_p],
     "obst_attn_map_fwd": [ctypes.POINTER(MapDesc), c_p],
     "obst_attn_map_bwd": [ctypes.POINTER(MapDesc), c_p],
     "obst_attn_map_bsplit": [c_i, c_i, c_i],
@@ -106,6 +107,10 @@ _SIGS = {
     "obst_cumsum": [c_p, c_p, c_ll, c_i, c_ll, c_i, c_i, c_i, c_p],
     "obst_cast_f32_bf16": [c_p, c_p, c_ll, c_p],
     "obst_add2_f32_bf16": [c_p, c_p, c_p, c_ll, c_p],
+    "obst_cast_bf16_f32": [c_p, c_p, c_ll, c_p],
+    "obst_tril": [c_p, c_p, c_ll, c_ll, c_p],
+    "obst_zero": [c_p, c_ll, c_p],
+    "obst_copy2d": [c_p, c_p, c_ll, c_ll, c_ll, c_ll, c_i, c_ll, c_ll, c_p],
     "obst_transpose": [c_p, c_p, c_ll, c_ll, c_ll, c_ll, c_i, c_ll, c_ll, c_p],
     "obst_mix_f32": [c_p, c_p, c_p, c_p, c_ll, c_f, c_f, c_p],
     "obst_xent_fwd": [c_p, c_p, c_p, c_p, c_p, c_ll, c_i, c_i, c_f, c_p],

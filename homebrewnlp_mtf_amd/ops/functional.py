@@ -558,6 +558,13 @@ class _DotAttention(torch.autograd.Function):
                 dres, None, None)
 
 
+def _kqv_cat(w, K: int, N: int):
+    """[K][3N] row interleave of the stacked [3][K][N] q / k / v weights (one strided-copy kernel)"""
+    cat = torch.empty((K, 3 * N), dtype=w.dtype, device=w.device)
+    raw.copy2d(w, cat, K, N, N, 3 * N, batch=3, sx=K * N, sy=N)
+    return cat
+
+
 def _stacked(ws) -> bool:
     """the three weights are equal-sized blocks adjacent in the flat buffer, in order (registration order)"""
     w0 = ws[0]
@@ -594,9 +601,7 @@ def _kqv_dgrad(dkqv, ws, dbase, p: LinearPlan, act, z):
     w0 = ws[0]
     store = getattr(w0, "store", None)
     if raw.on_gpu(dkqv) and store is not None and _stacked(ws):
-        cat = store.derived(w0.var_name, f"kqv_cat@{w0.data_ptr()}",
-                            lambda: torch.as_strided(w0.detach(), (3, K, N), (K * N, N, 1)).permute(1, 0, 2)
-                            .contiguous().view(K, 3 * N))
+        cat = store.derived(w0.var_name, f"kqv_cat@{w0.data_ptr()}", lambda: _kqv_cat(w0.detach(), K, N))
         raw.gemm(raw.Operand(dkqv, 0, 3 * N), raw.Operand(cat, 0, 3 * N), raw.Operand(dbase, 0, K), M, K, 3 * N,
                  act=act, act_bwd=act is not None, Zin=z if act else None)
         return
@@ -629,7 +634,7 @@ class _TokenMixer(torch.autograd.Function):
         store = getattr(w, "store", None)
         if causal and store is not None and w.device.type == "cuda":
             # the masked weight of a depth-shared mixer is built once per step (ParamStore.derived)
-            wm = store.derived(w.var_name, f"tril@{w.data_ptr()}", lambda: torch.tril(w.detach()))
+            wm = store.derived(w.var_name, f"tril@{w.data_ptr()}", lambda: raw.tril(w.detach()))
         else:
             wm = torch.tril(w) if causal else w.contiguous()
         hf = H * Fd
@@ -795,7 +800,10 @@ class _AttnMap(torch.autograd.Function):
         db = torch.empty(H, S, S, dtype=md, device=q.device) if need_b else None
         dc = torch.empty(H, S, S, dtype=md, device=q.device) if need_c else None
         pb = pc = None
-        if raw.on_gpu(q) and (need_b or need_c):
+        if raw.on_gpu(q) and raw.attn_map_flash_bwd(B, S, H, D, b32 is not None, c32 is not None):
+            # flash backward with the map hook: dS per batch, written whole (no zeroing), folded by the kernel
+            pb = _map_workspace(q.device, B * H * S * S).view(B, H, S, S)
+        elif raw.on_gpu(q) and (need_b or need_c):
             bs = raw.attn_map_bsplit(B, S, H)
             if bs > 1:
                 # the per-batch-slice partial map gradients live in one cached workspace (reused by every layer's

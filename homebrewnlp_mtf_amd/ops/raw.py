@@ -355,6 +355,7 @@ def _map_logits(q, k, bias, B, S, H, D, scale, causal):
 
 # OBST_MAP_FLASH (default 1): the bias-only D = 128 map forward (S % 128 == 0) on the flash kernel; 0: attn_map.hip
 _MAP_FLASH = __import__("os").environ.get("OBST_MAP_FLASH", "1") != "0"
+map_flash_bwd_calls = 0
 map_flash_calls = 0   # (tests: forwards that took the flash path)
 
 
@@ -396,6 +397,13 @@ def attn_map_fwd(q, k, v, o, lse, bias, cmap, B, S, H, D, scale: float, causal: 
     lse.view(B, H, S).copy_(m)
 
 
+def attn_map_flash_bwd(B: int, S: int, H: int, D: int, has_bias: bool, has_cmap: bool) -> bool:
+    """biased_softmax backward on the flash kernels (attention.hip, map hook): bias only, D = 128, S % 128 == 0, and
+    the per-batch partial map gradients ([B, H, S, S] fp32) within 16 GiB"""
+    return (_MAP_FLASH and has_bias and not has_cmap and D == 128 and S % 128 == 0
+            and B * H * S * S * 4 <= 16 << 30)
+
+
 def attn_map_bwd(q, k, v, o, do, lse, delta, dq, dk, dv, bias, cmap, dbias, dcmap, B, S, H, D, scale: float,
                  causal: bool, dbias_part=None, dcmap_part=None):
     """dbias / dcmap: [H, S, S] fp32 outputs (None: not needed); *_part: zeroed [bsplit, H, S, S] partial maps the
@@ -415,6 +423,26 @@ def attn_map_bwd(q, k, v, o, do, lse, delta, dq, dk, dv, bias, cmap, dbias, dcma
                 if t.dtype != torch.float32 or not t.is_contiguous():
                     raise L.KernelError(f"attention map {nm} must be contiguous fp32")
                 _need(t, H * S * S - 1, nm)
+        if attn_map_flash_bwd(B, S, H, D, bias is not None, cmap is not None):
+            # dQ and dK/dV kernels of the main flash backward with the map hook; dS per batch into dbias_part
+            # ([B, H, S, S], written whole over the causal triangle: no zeroing), folded over the batch in order
+            global map_flash_bwd_calls
+            map_flash_bwd_calls += 1
+            if dbias is None:
+                dbias = torch.empty(H, S, S, device=q.device)
+            if dbias_part is None or dbias_part.numel() < B * H * S * S:
+                dbias_part = torch.empty(B, H, S, S, device=q.device)
+            if dbias_part.dtype != torch.float32 or not dbias_part.is_contiguous():
+                raise L.KernelError("attention map dbias_part must be contiguous fp32")
+            _need(dbias_part, B * H * S * S - 1, "dbias_part")
+            _need(lse, B * H * S - 1, "lse")
+            _need(delta, B * H * S - 1, "delta")
+            d = L.AttnDesc(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), do.data_ptr(), 0, dq.data_ptr(),
+                           dk.data_ptr(), dv.data_ptr(), lse.data_ptr(), delta.data_ptr(), B, S, H, D, H * D,
+                           float(scale), int(causal), H * D, 0, 0)
+            L.check(L.lib().obst_attn_bwd_bias(d, bias.data_ptr(), dbias_part.data_ptr(), dbias.data_ptr(),
+                                               L.stream_ptr()), "attn_bwd_bias")
+            return
         # the kernels accumulate the gradient of every present map (one instantiation per map set): a map whose
         # gradient is not wanted gets a scratch output
         if bias is not None and dbias is None:
@@ -715,6 +743,40 @@ def add_to_bf16(a, b, out=None):
     return out
 
 
+def to_f32(x, out=None):
+    """bf16 -> fp32 copy through the HIP cast kernel on the GPU"""
+    if out is None:
+        out = torch.empty(x.shape, dtype=torch.float32, device=x.device)
+    if on_gpu(x) and x.dtype == torch.bfloat16 and x.numel() % 8 == 0:
+        x = x.contiguous()
+        L.check(L.lib().obst_cast_bf16_f32(x.data_ptr(), out.data_ptr(), x.numel(), L.stream_ptr()), "cast")
+        return out
+    out.copy_(x)
+    return out
+
+
+def tril(x):
+    """lower triangle (diagonal included) of the trailing S x S of x: one HIP pass for bf16 on the GPU"""
+    S = x.shape[-1]
+    if on_gpu(x) and x.dtype == torch.bfloat16 and x.shape[-2] == S and S % 8 == 0:
+        x = x.contiguous()
+        y = torch.empty_like(x)
+        L.check(L.lib().obst_tril(x.data_ptr(), y.data_ptr(), S, x.numel() // (S * S), L.stream_ptr()), "tril")
+        return y
+    return torch.tril(x)
+
+
+_ZERO_MEMSET = __import__("os").environ.get("OBST_ZERO_MEMSET", "1") != "0"
+
+
+def zero_(t):
+    """t[:] = 0 (contiguous): the runtime's memset on the GPU (OBST_ZERO_MEMSET=0: torch's fill)"""
+    if _ZERO_MEMSET and on_gpu(t) and t.is_contiguous():
+        L.check(L.lib().obst_zero(t.data_ptr(), t.numel() * t.element_size(), L.stream_ptr()), "zero")
+        return t
+    return t.zero_()
+
+
 def to_bf16(x, out=None):
     """fp32 -> bf16 copy through the HIP cast kernel on the GPU"""
     if out is None:
@@ -742,6 +804,23 @@ def transpose(x, y, rows: int, cols: int, ldx: int, ldy: int, batch: int = 1, sx
     xv = torch.as_strided(x, (batch, rows, cols), (sx, ldx, 1), x.storage_offset())
     yv = torch.as_strided(y, (batch, cols, rows), (sy, ldy, 1), y.storage_offset())
     yv.copy_(xv.transpose(1, 2))
+
+
+def copy2d(x, y, rows: int, cols: int, ldx: int, ldy: int, batch: int = 1, sx: int = 0, sy: int = 0):
+    """y[b][r][c] = x[b][r][c] between strided layouts (bf16 HIP kernel on the GPU; any dtype on the CPU)"""
+    if x.device.type == "meta":
+        return None
+    if on_gpu(x):
+        if x.dtype != torch.bfloat16 or y.dtype != torch.bfloat16:
+            raise L.KernelError("copy2d is bf16")
+        _need(x, (batch - 1) * sx + (rows - 1) * ldx + cols - 1, "x")
+        _need(y, (batch - 1) * sy + (rows - 1) * ldy + cols - 1, "y")
+        L.check(L.lib().obst_copy2d(x.data_ptr(), y.data_ptr(), rows, cols, ldx, ldy, batch, sx, sy,
+                                    L.stream_ptr()), "copy2d")
+        return
+    xv = torch.as_strided(x, (batch, rows, cols), (sx, ldx, 1), x.storage_offset())
+    yv = torch.as_strided(y, (batch, rows, cols), (sy, ldy, 1), y.storage_offset())
+    yv.copy_(xv)
 
 
 def gather(idx, table, out, T: int, F: int, V: int):

@@ -73,9 +73,19 @@ def test_attn_map_single_batch_slice(cuda):
 def test_attn_map_training_shape_class(cuda):
     """multi-block causal paths at S = 2048 (32 query / key blocks), head dim 128; the bias-only forward runs on the
     flash kernel with the map hook (attention.hip, obst_attn_fwd_bias)"""
-    n0 = raw.map_flash_calls
+    n0, n1 = raw.map_flash_calls, raw.map_flash_bwd_calls
     _case(cuda, 2, 2048, 2, 128, True, "bias", seed=7)
     assert raw.map_flash_calls == n0 + 1, "the D = 128 bias forward did not take the flash kernel"
+    assert raw.map_flash_bwd_calls == n1 + 1, "the D = 128 bias backward did not take the flash kernels"
+
+
+@pytest.mark.parametrize("causal", [True, False])
+def test_attn_map_flash_bwd_odd_batch(cuda, causal):
+    """the flash backward's per-batch dS slabs folded over an odd batch count, causal (the fold zeroes the never
+    written upper triangle) and full"""
+    n1 = raw.map_flash_bwd_calls
+    _case(cuda, 3, 384, 2, 128, causal, "bias", seed=11)
+    assert raw.map_flash_bwd_calls == n1 + 1
 
 
 def test_attn_map_deterministic(cuda):

@@ -363,6 +363,29 @@ def test_add_to_bf16(cuda, n):
     assert got.dtype == BF and torch.equal(got.cpu(), (a + b).to(BF))
 
 
+def test_to_f32_and_copy2d(cuda):
+    """bf16 -> fp32 cast (the RevNet body's fp32 streams) is exact; the strided copy interleaves the stacked
+    [3][K][N] q / k / v weights into [K][3N] exactly as the permute + contiguous it replaces"""
+    torch.manual_seed(6)
+    x = torch.randn(4096 * 8).to(BF)
+    y = raw.to_f32(x.to(cuda))
+    K, N = 96, 40
+    w = torch.randn(3, K, N).to(BF)
+    cat = torch.empty(K, 3 * N, dtype=BF, device=cuda)
+    raw.copy2d(w.to(cuda), cat, K, N, N, 3 * N, batch=3, sx=K * N, sy=N)
+    torch.cuda.synchronize()
+    assert y.dtype == torch.float32 and torch.equal(y.cpu(), x.float())
+    assert torch.equal(cat.cpu(), w.permute(1, 0, 2).reshape(K, 3 * N))
+    m = torch.randn(3, 72, 72).to(BF)
+    z = torch.randn(1000 * 8 + 8)
+    zg = z.to(cuda)
+    raw.zero_(zg[8:])
+    got = raw.tril(m.to(cuda))
+    torch.cuda.synchronize()
+    assert torch.equal(got.cpu(), torch.tril(m))
+    assert torch.equal(zg[:8].cpu(), z[:8]) and not zg[8:].any()
+
+
 def test_xent(cuda):
     torch.manual_seed(11)
     rows, V, Vp = 64, 1000, 1024

@@ -98,7 +98,9 @@ def test_model_forward_backward(cuda, variant, monkeypatch):
         # backward -- no mix_f32 pass at all; unfused: three per block (bf16 streams: three bf16 axpby passes)
         passes = 0 if not variant.endswith("_unfused") else 3 * nblk
         if "bf16stream" in variant or variant == "mixer_bf16grad":
-            assert len(mixes) == 0 and len(axpbys) == passes, (variant, len(mixes), len(axpbys), nblk)
+            # plus the bf16 sums of the two streams: the body output (bf16 streams) and its input gradient
+            sums = 2 if "bf16stream" in variant else 1
+            assert len(mixes) == 0 and len(axpbys) == passes + sums, (variant, len(mixes), len(axpbys), nblk)
         else:
             assert len(mixes) == passes, (variant, len(mixes), nblk)
 

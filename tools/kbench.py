@@ -8,7 +8,8 @@
                The per-tile clock breakdown of gemm4w lives in the C++ harness (tools/gemm_bench.cpp, STAMPS=1).
 * attn      -- flash attention fwd / bwd (B, S 2048, H 16, D 128, causal, interleaved k|q|v as in the step):
                effective causal PF/s (fwd 2 units, bwd 5 units of B*H*S*S/2*D*2 FLOPs).
-* attn_map  -- the biased_softmax / scale_attention_map kernels (csrc/kernels/attn_map.hip) at the same shape.
+* attn_map  -- biased_softmax at the same shape: the flash kernels with the map hook (attention.hip) by default,
+               the attn_map.hip kernels with OBST_MAP_FLASH=0.
 * norm      -- norm fwd / bwd (+ residual gradient, + parameter gradients): GB/s of the bytes each must move.
 * ew        -- the streaming elementwise kernels (gelu fwd / bwd, add): GB/s.
 * gate      -- one row per hot-kernel family (GATE), each between its own two calibrations: the perf gate that
@@ -272,20 +273,22 @@ def bench_attn_map(B: int, reps: int):
     dq, dk, dv = (torch.empty_like(q) for _ in range(3))
     delta = torch.empty_like(lse)
     db = torch.empty(H, S, S, device=dev)
-    bs = raw.attn_map_bsplit(B, S, H)
+    flash = raw.attn_map_flash_bwd(B, S, H, D, True, False)
+    # flash backward: per-batch dS slabs, written whole (no zeroing); map kernels: zeroed per-slice partial sums
+    bs = B if flash else raw.attn_map_bsplit(B, S, H)
     pb = torch.zeros(bs, H, S, S, device=dev) if bs > 1 else None
     sc = D ** -0.5
     unit = B * H * S * S / 2 * D * 2
     f = timed(lambda: raw.attn_map_fwd(q, k, v, o, lse, bias, None, B, S, H, D, sc, True), reps)
 
     def bwd():
-        if pb is not None:
+        if pb is not None and not flash:
             pb.zero_()
         raw.attn_map_bwd(q, k, v, o, do, lse, delta, dq, dk, dv, bias, None, db, None, B, S, H, D, sc, True, pb)
     b = timed(bwd, reps)
     emit(kernel="attention_map(biased_softmax)", B=B, S=S, H=H, D=D, causal=True, us_fwd=round(f, 1),
          us_bwd=round(b, 1), pflops_fwd=round(2 * unit / f / 1e9, 3), pflops_bwd=round(5 * unit / b / 1e9, 3),
-         bias_grad_slices=bs)
+         bias_grad_slices=bs, flash_bwd=flash)
 
 
 def bench_norm(T: int, reps: int, only=None):
