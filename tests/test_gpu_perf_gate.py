@@ -18,7 +18,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 import kbench  # noqa: E402
 
-TOL = 0.05   # ratio to the floor; box-to-box spread of the calibration ratios is ~3 % (profiles/r5_summary.md)
+TOL = 0.08   # a healthy box read gelu_bwd 5.8 % under its absolute floor and 3.6 % under its ratio floor (round-6
+# final kbench, profiles/r6/kbench_final_check.log); the deliberately slowed launch is ~20 % slower
 
 
 def test_hot_kernels_meet_their_floors(cuda):
