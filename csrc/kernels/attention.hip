@@ -360,7 +360,7 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_bwd_dq_kernel(AttnArgs a) {
   const int nx = (a.S + QB - 1) / QB;
   int bx, bh;
   attn_block(nx, bx, bh);
-  const int b = bh / a.H, h = bh % a.H;
+  const int b = BIAS ? bh % a.B : bh / a.H, h = BIAS ? bh / a.B : bh % a.H;   // BIAS: batch-major (bias_order)
   const int qblk = (a.causal ? (nx - 1 - bx) : bx) * QB;  // heaviest first
   const int qw = qblk + w * 32;
   const long long base = (long long)b * a.S * a.ld + h * D;
@@ -656,7 +656,7 @@ __global__ __launch_bounds__(NW * 64, KG == 1 ? 2 : 1) void attn_bwd_dkv_kernel(
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, i = lane & 15;
   int bx, bh;
   attn_block((a.S + KB - 1) / KB, bx, bh);
-  const int b = bh / a.H, h = bh % a.H;
+  const int b = BIAS ? bh % a.B : bh / a.H, h = BIAS ? bh / a.B : bh % a.H;   // BIAS: batch-major (bias_order)
   const int kblk = bx * KB;
   const int kw = kblk + w * KW;
   const long long base = (long long)b * a.S * a.ld + h * D;
@@ -937,7 +937,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd32_kernel(AttnArgs a)
   const int nx = (a.S + QB - 1) / QB;
   int bx, bh;
   attn_block(nx, bx, bh);
-  const int b = bh / a.H, hd = bh % a.H;
+  const int b = BIAS ? bh % a.B : bh / a.H, hd = BIAS ? bh / a.B : bh % a.H;   // BIAS: batch-major (bias_order)
   const int qblk = (a.causal ? (nx - 1 - bx) : bx) * QB;
   const int qw = qblk + w * 32;
   const int q = qw + n;

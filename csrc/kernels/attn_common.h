@@ -154,6 +154,10 @@ __device__ __forceinline__ void attn_block(int nx, int& bx, int& bh) {
   bh = L / nx;
 }
 
+// bias_order: the map-hooked kernels (BIAS) take (b, h) = (bh % B, bh / B) instead of (bh / H, bh % H), so the
+// consecutive logical blocks one XCD runs are the batches of one head, which read the same [S][S] map rows: the map
+// is fetched from HBM about once per head and re-read from L2 / MALL, instead of once per (batch, head)
+
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr float NEG_BIG = -1e30f;
 
