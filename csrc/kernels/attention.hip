@@ -817,25 +817,18 @@ __global__ __launch_bounds__(NW * 64, KG == 1 ? 2 : 1) void attn_bwd_dkv_kernel(
 #endif
 
 // one 64-key tile for a wave's 32 queries (query n = lane&31 is `q`); l is this lane's partial row sum
-// BIAS (biased_softmax, ref src/model/spatial.py:65-66,74-75): brow is this lane's query row of the [H][S][S] fp32 map;
-// its 16 values per 32-key sub-tile (keys 8a + 4h + b: four 16-byte loads) are loaded before the score MFMAs and
-// added to the scaled logits after them, so the softmax below runs on scale q.k + b (in log2 units)
+// BIAS (biased_softmax, ref src/model/spatial.py:65-66,74-75; 32-key tiles): bv holds this lane's 16 map values of
+// the tile (keys 8a + 4h + b of its query row, loaded one tile ahead by the kernel), added to the scaled logits after
+// the score MFMAs, so the softmax below runs on scale q.k + b (in log2 units)
 template <bool MASK, int NKT = 2, bool BIAS = false>
 __device__ __forceinline__ void fwd32_tile(const char* sK, const char* sV, const bf16x8_t (&qf)[8],
                                            f32x16_t (&o)[4], float& m, float& l, int k0, int q, int S, int causal,
-                                           float c2, int lane, int prio = 0, const float* brow = nullptr) {
+                                           float c2, int lane, int prio, const f32x4_t (&bv)[4]) {
+  static_assert(!BIAS || NKT == 1, "the map hook runs on 32-key tiles");
   const int h = lane >> 5;
   Frag32 fo;
   frag32_offsets(fo, lane);
   f32x16_t s[NKT];
-  f32x4_t bv[BIAS ? NKT * 4 : 1];
-  if constexpr (BIAS) {
-#pragma unroll
-    for (int kt = 0; kt < NKT; ++kt)
-#pragma unroll
-      for (int a4 = 0; a4 < 4; ++a4)
-        bv[kt * 4 + a4] = *reinterpret_cast<const f32x4_t*>(brow + k0 + kt * 32 + 8 * a4 + 4 * h);
-  }
   if (prio) __builtin_amdgcn_s_setprio(1);
   // the NKT score chains interleaved k-step by k-step, K fragments read FWD_KPF k-steps ahead of their MFMA: with
   // one chain at a time the compiler re-used one fragment register and every MFMA waited out a full LDS read
@@ -978,41 +971,82 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd32_kernel(AttnArgs a)
   for (int dt = 0; dt < 4; ++dt) o[dt] = f32x16_t{};
   float m = NEG_BIG, l = 0.f;
   const float c2 = a.scale * LOG2E;
-  // BIAS: this lane's query row of the map (rows past S read the last row; their outputs are not stored)
-  const float* brow = BIAS ? a.bias + ((long long)hd * a.S + min(q, a.S - 1)) * a.S : nullptr;
+  // BIAS: this lane's query row of the map (rows past S read the last row; their outputs are not stored). The 16
+  // values of tile kb + 1 are loaded during tile kb by inline asm, ahead of that iteration's K/V DMA: a compiler-
+  // visible load would get a vmcnt wait in front of its first use that also drains the K/V DMA issued after it (the
+  // compiler does not count the asm LDS-DMA), i.e. every tile would wait for the tile three ahead to land. The
+  // iteration's closing wait covers them instead (only the newer DMA of tile kb + 3 may stay in flight).
+  const float* brow = BIAS ? a.bias + ((long long)hd * a.S + min(q, a.S - 1)) * a.S + 4 * h : nullptr;
+  f32x4_t bcur[4], bnx[4];
+  auto bias_load = [&](f32x4_t (&dst)[4], int k0) {
+    if constexpr (BIAS) {
+      const float* p = brow + k0;
+      asm volatile(
+          "global_load_dwordx4 %0, %4, off\n\t"
+          "global_load_dwordx4 %1, %4, off offset:32\n\t"
+          "global_load_dwordx4 %2, %4, off offset:64\n\t"
+          "global_load_dwordx4 %3, %4, off offset:96"
+          : "=&v"(dst[0]), "=&v"(dst[1]), "=&v"(dst[2]), "=&v"(dst[3])
+          : "v"(p)
+          : "memory");
+    }
+  };
+  auto bias_pin = [&](f32x4_t (&r)[4]) {   // after the wait: the values are in place from here on
+    if constexpr (BIAS) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(r[i]));
+    }
+  };
+  if constexpr (BIAS) {
+    static_assert(KT == 32 && NS == 4, "the map pipeline is laid out for the 32-key, 4-deep ring");
+    bias_load(bcur, 0);   // (issued after the prologue's DMA: the wait below covers both)
+  }
   vm_wait<0>();
+  bias_pin(bcur);
   __syncthreads();
   // key tiles in two branch-free runs, unmasked then the block's masked band (as in the backward kernels): the
   // per-tile branch merged O, m and l of its two arms. Fully masked tiles of the lower waves add exactly nothing (the
   // first tile, key 0, makes every row's running max finite) and run while those waves would wait at the barrier.
   const int kbm = a.causal ? min(nkb, (qblk + 1) / KT) : ((nkb * KT > a.S) ? nkb - 1 : nkb);
+  // the ring step of iteration kb: (BIAS: map values of tile kb + 1,) the DMA of tile kb + NS - 1, [the tile's work],
+  // then the wait for tile kb + 1 (and its map values) and the barrier
+  auto issue = [&](int kb) {
+    bias_load(bnx, min(kb + 1, nkb - 1) * KT);
+    const int kn = kb + NS - 1;   // its slot was last read in iteration kb - 1 (behind the barrier)
+    if (kn < nkb) stage(smem + (kn % NS) * 2 * TILE, kn * KT);
+  };
+  auto retire = [&](int kb) {
+    if constexpr (BIAS) {   // the map loads sit between tile kb + 2's DMA and tile kb + 3's: only the latter may stay
+      if (kb + NS - 1 < nkb) vm_wait<2 * NP>();
+      else vm_wait<0>();
+      bias_pin(bnx);   // (ordered after the wait: the copy below cannot be hoisted above it)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) bcur[i] = bnx[i];
+    } else {
+      // tile kb + 1 has landed; tiles kb + 2 .. kb + NS - 2 may stay in flight (2 NP pieces per wave per tile)
+      const int ahead = min(NS - 2, nkb - 2 - kb);
+      if (NS >= 4 && ahead >= 2) vm_wait<4 * NP>();
+      else if (NS >= 3 && ahead >= 1) vm_wait<2 * NP>();
+      else vm_wait<0>();
+    }
+    __syncthreads();
+  };
   auto tile = [&](int kb, auto mk) {
     constexpr bool MK = decltype(mk)::value;
     const int k0 = kb * KT;
     const char* sK = smem + (kb % NS) * 2 * TILE;
     const char* sV = sK + TILE;
-    const int kn = kb + NS - 1;   // its slot was last read in iteration kb - 1 (behind the barrier)
-    if (kn < nkb) stage(smem + (kn % NS) * 2 * TILE, kn * KT);
-    fwd32_tile<MK, KT / 32, BIAS>(sK, sV, qf, o, m, l, k0, q, a.S, a.causal, c2, lane, a.prio & 4, brow);
-    // tile kb + 1 has landed; tiles kb + 2 .. kb + NS - 2 may stay in flight (2 NP pieces per wave per tile)
-    const int ahead = min(NS - 2, nkb - 2 - kb);
-    if (NS >= 4 && ahead >= 2) vm_wait<4 * NP>();
-    else if (NS >= 3 && ahead >= 1) vm_wait<2 * NP>();
-    else vm_wait<0>();
-    __syncthreads();
+    issue(kb);
+    fwd32_tile<MK, KT / 32, BIAS>(sK, sV, qf, o, m, l, k0, q, a.S, a.causal, c2, lane, a.prio & 4, bcur);
+    retire(kb);
   };
   if (!(a.prio & 16)) {   // default: the per-tile branch with its skip of the tiles past a wave's queries (bit 4,
     // the branch-free runs, measured within 1 %: profiles/r4_attn_branchfree_ab.txt)
     for (int kb = 0; kb < nkb; ++kb) {
       const int k0 = kb * KT;
       if (a.causal && k0 > qw + 31) {   // nothing of this tile for this wave: keep the ring's staging and barrier
-        const int kn = kb + NS - 1;
-        if (kn < nkb) stage(smem + (kn % NS) * 2 * TILE, kn * KT);
-        const int ahead = min(NS - 2, nkb - 2 - kb);
-        if (NS >= 4 && ahead >= 2) vm_wait<4 * NP>();
-        else if (NS >= 3 && ahead >= 1) vm_wait<2 * NP>();
-        else vm_wait<0>();
-        __syncthreads();
+        issue(kb);
+        retire(kb);
       } else if ((a.causal && k0 + KT - 1 > qw) || k0 + KT > a.S) {
         tile(kb, std::true_type{});
       } else {
