@@ -11,17 +11,85 @@
 // norm when `heads` is split across ranks (collective X05).
 #include "common.h"
 
+#include <mutex>
+#include <unordered_map>
+
 namespace {
 
 constexpr int NTH = 256;
 
+// one-chunk rows (F <= 8 x lanes per row: ctx32_mixer's 256- and 512-wide head groups): forward rows in flight per lane
+// group, backward rows in flight and blocks per CU (the backward's grid: one resident wave of blocks)
+#ifndef NORM_FWD_U1
+#define NORM_FWD_U1 1
+#endif
+#ifndef NORM_FWD_U64
+#define NORM_FWD_U64 2
+#endif
+#ifndef NORM_BWD_U1
+#define NORM_BWD_U1 4
+#endif
+#ifndef NORM_BWD_BPC1
+#define NORM_BWD_BPC1 2
+#endif
+// the one-chunk backward (norm_bwd1_kernel): blocks per CU (its grid: one resident wave of them); 0 turns it off
+#ifndef NORM_BWD1_BPC
+#define NORM_BWD1_BPC 4
+#endif
+
 // LPR lanes per row (64 for F > 256; 32 / 16 / 8 for short rows so a wave covers 64/LPR rows at once),
 // NCH chunks of LPR*8 elements per row
-template <int LPR>
+// row sums by DPP (quad permutes, half-row / row mirrors) and the gfx950 row swaps (v_permlane16/32_swap) instead of
+// one ds_bpermute round trip through the LDS unit per step: every step adds a lane's value to its partner's in both
+// lanes' order-independent form (a + b == b + a), so every lane of the row ends with the same bits
+#ifndef NORM_DPP
+#define NORM_DPP 1
+#endif
+// forward streaming hints: bit 0 nontemporal row loads, bit 1 nontemporal output stores
+#ifndef NORM_NT
+#define NORM_NT 0
+#endif
+// whole-wave rows (64 lanes): 1 the two row swaps, 0 ds_bpermute, 2 row broadcasts + readlane
+#ifndef NORM_DPP64
+#define NORM_DPP64 1
+#endif
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xf, 0xf, false));
+}
+template <int LPR, bool DPP = (NORM_DPP != 0)>
 __device__ __forceinline__ float row_sum(float v) {
+  if constexpr (DPP) {
+    static_assert(LPR >= 8 && LPR <= 64, "rows of 8 to 64 lanes");
+    v += dpp_mov<0xB1>(v);    // quad_perm [1, 0, 3, 2]: lane ^ 1
+    v += dpp_mov<0x4E>(v);    // quad_perm [2, 3, 0, 1]: lane ^ 2
+    v += dpp_mov<0x141>(v);   // row_half_mirror: the other quad of the 8-lane half
+    if constexpr (LPR >= 16) v += dpp_mov<0x140>(v);   // row_mirror: the other half of the 16-lane row
+    if constexpr (LPR == 64 && NORM_DPP64 == 0) {   // the ds_bpermute steps for the whole wave
+      v += __shfl_xor(v, 16, 64);
+      return v + __shfl_xor(v, 32, 64);
+    }
+    if constexpr (LPR == 64 && NORM_DPP64 == 2) {
+      // whole wave: row 1 += row 0 and row 3 += row 2 (row_bcast:15), rows 2, 3 += row 1 (row_bcast:31), lane 63
+      // broadcast through an SGPR
+      v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x142, 0xa, 0xf, false));
+      v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x143, 0xc, 0xf, false));
+      return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
+    }
+    if constexpr (LPR >= 32) {   // lane ^ 16
+      const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+      v = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+    }
+    if constexpr (LPR >= 64) {   // lane ^ 32
+      const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+      v = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+    }
+    return v;
+  } else {
 #pragma unroll
-  for (int o = LPR / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+    for (int o = LPR / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+  }
 }
 
 template <int LPR>
@@ -42,7 +110,13 @@ __device__ __forceinline__ void load_raw(const bf16_t* x, int F, int sl, bool ok
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
     const int col = c * LPR * 8 + sl * 8;
-    u[c] = (ok && col < F) ? *reinterpret_cast<const uint4*>(x + col) : make_uint4(0, 0, 0, 0);
+    if constexpr (NORM_NT & 1) {
+      typedef unsigned v4u __attribute__((ext_vector_type(4)));
+      const v4u t = (ok && col < F) ? __builtin_nontemporal_load(reinterpret_cast<const v4u*>(x + col)) : v4u{0u, 0u, 0u, 0u};
+      u[c] = make_uint4(t[0], t[1], t[2], t[3]);
+    } else {
+      u[c] = (ok && col < F) ? *reinterpret_cast<const uint4*>(x + col) : make_uint4(0, 0, 0, 0);
+    }
   }
 }
 
@@ -102,7 +176,9 @@ __device__ __forceinline__ void norm_fwd_body(const bf16_t* __restrict__ X, cons
                                               int groups, float eps, const float* __restrict__ ext_stats,
                                               int act) {
   constexpr int RPW = 64 / LPR;
-  constexpr int U = 1;   // (2-4 rows in flight per lane group measured 2 % slower than 1)
+  // rows in flight per lane group (F 2048: 2-4 measured 2 % slower than 1; one-chunk rows: 2 at 64 lanes per row,
+  // 1930 -> 1750 us at ctx32_mixer's 512-wide groups, but 1010 -> 1250 us at 32 lanes, 256-wide)
+  constexpr int U = NCH == 1 ? (LPR == 64 ? NORM_FWD_U64 : NORM_FWD_U1) : 1;
   const int lane = threadIdx.x & 63, sub = lane / LPR, sl = lane % LPR;
   const long long nw = (long long)gridDim.x * 4 * RPW;
   long long r0 = ((long long)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
@@ -167,7 +243,12 @@ __device__ __forceinline__ void norm_fwd_body(const bf16_t* __restrict__ X, cons
           }
           o[j] = pack_bf16x2(y0, y1);
         }
-        *reinterpret_cast<uint4*>(Y + row * F + col) = make_uint4(o[0], o[1], o[2], o[3]);
+        if constexpr (NORM_NT & 2) {
+          typedef unsigned v4u __attribute__((ext_vector_type(4)));
+          __builtin_nontemporal_store(v4u{o[0], o[1], o[2], o[3]}, reinterpret_cast<v4u*>(Y + row * F + col));
+        } else {
+          *reinterpret_cast<uint4*>(Y + row * F + col) = make_uint4(o[0], o[1], o[2], o[3]);
+        }
       }
     }
   }
@@ -261,7 +342,7 @@ __device__ __forceinline__ void act_dy8(int c, int sl, int F, bool ok, long long
 // the output pairs are packed with the scalar conversions (pk2 below): 411 us per call at 131072 x 2048 against
 // 596 us with one block per CU and 833 us with the ~60 VGPRs the vector-convert pack spilled.
 template <int NCH>
-constexpr int bwd_blocks_per_cu() { return NCH >= 8 ? 1 : 2; }
+constexpr int bwd_blocks_per_cu() { return NCH >= 8 ? 1 : NCH == 1 ? NORM_BWD_BPC1 : 2; }
 
 // two floats -> packed bf16 pair through two scalar conversions: the vector convert (common.h pack_bf16x2) costs
 // this kernel ~60 VGPRs of spills at F = 2048 (register allocation around the v_cvt_pk_bf16_f32 pairs)
@@ -304,7 +385,7 @@ __device__ __forceinline__ void norm_bwd_body(const bf16_t* __restrict__ X, cons
     for (int j = 0; j < 8; ++j) gs[c][j] = gb[c][j] = 0.f;
   const long long nw = (long long)gridDim.x * 4 * RPW;
   const long long first = ((long long)blockIdx.x * 4 + w) * RPW + sub;
-  constexpr int U = NCH == 1 ? 4 : NCH == 2 ? 2 : 1;   // rows per lane group in flight
+  constexpr int U = NCH == 1 ? NORM_BWD_U1 : NCH == 2 ? 2 : 1;   // rows per lane group in flight
   // next rows (x, dy, the residual gradient and the row statistics) in flight while this one is processed
   uint4 nx[U][NCH], nd[U][NCH];
   float2 nst[U];
@@ -389,8 +470,8 @@ __device__ __forceinline__ void norm_bwd_body(const bf16_t* __restrict__ X, cons
         }
       }
     }
-    s1 = row_sum<LPR>(s1);
-    s2 = row_sum<LPR>(s2);
+    s1 = row_sum<LPR, false>(s1);
+    s2 = row_sum<LPR, false>(s2);
     if (!ok) continue;
     if (partial_out) {
       if (sl == 0) { partial_out[2 * row] = s1; partial_out[2 * row + 1] = s2; }
@@ -516,6 +597,98 @@ __global__ __launch_bounds__(NTH, bwd_blocks_per_cu<NCH>()) void norm_bwd_gelu_k
   norm_bwd_body<NCH, LPR, false, ACT_GELU>(NORM_BWD_ARGS);
 }
 
+// One-chunk rows (F <= 8 x LPR: ctx32_mixer's 256-wide head groups and 512-wide bottleneck groups), the plain, bf16
+// residual, fused-activation and input-relu forms of the backward without the TP / fp32-stream paths: each lane holds
+// 8 columns of one row; the next row's x, dy and statistics are in flight while this one is processed, the residual
+// gradient is loaded for this row ahead of the first pass. The general body held 100-130 VGPRs at one chunk (64-bit
+// address pairs of its generic paths): two waves per SIMD, too few to cover the gelu form's VALU and the loads (3.4
+// TB/s). This one fits four blocks per CU. Parameter gradients: per-lane-group partial slabs (row `first` of a [lane
+// groups][2F] slab, every group count, groups == 1 too), folded in order by norm_fold_kernel.
+// AK: 0 plain, ACT_GELU, -1 the runtime `act`
+template <int LPR, int AK>
+__global__ __launch_bounds__(NTH, NORM_BWD1_BPC) void norm_bwd1_kernel(
+    const bf16_t* __restrict__ X, const bf16_t* __restrict__ DY, const float* __restrict__ scale,
+    const float* __restrict__ shift, const float* __restrict__ stats, bf16_t* __restrict__ DX,
+    const bf16_t* __restrict__ R, float* __restrict__ ws, long long rows, int F, int groups, int act, int in_relu) {
+  constexpr int RPW = 64 / LPR;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, sub = lane / LPR, sl = lane % LPR;
+  const int col = sl * 8;
+  const bool colok = col < F;
+  const int ccol = colok ? col : 0;   // lanes past F re-read column 0 (their values are never used)
+  const long long nw = (long long)gridDim.x * 4 * RPW;
+  const long long first = ((long long)blockIdx.x * 4 + w) * RPW + sub;
+  const long long poff = (first % groups) * F + ccol;
+  float sc[8], sh[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { sc[j] = 1.f; sh[j] = 0.f; }
+  if (scale) load8f(scale + poff, sc);
+  if (AK != 0 && shift) load8f(shift + poff, sh);
+  float gs[8], gb[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) gs[j] = gb[j] = 0.f;
+  const float inv_f = 1.f / (float)F;
+  long long row = first;
+  long long rc = row < rows ? row : rows - 1;
+  uint4 nx = *reinterpret_cast<const uint4*>(X + rc * F + ccol);
+  uint4 nd = *reinterpret_cast<const uint4*>(DY + rc * F + ccol);
+  float2 nst = *reinterpret_cast<const float2*>(stats + 2 * rc);
+#pragma nounroll
+  for (; row < rows; row += nw) {
+    const uint4 cx = nx, cd = nd;
+    const float mean = nst.x, rstd = nst.y;
+    uint4 cr = make_uint4(0u, 0u, 0u, 0u);
+    if (R) cr = *reinterpret_cast<const uint4*>(R + row * F + ccol);
+    const long long nrow = row + nw, nrc = nrow < rows ? nrow : rows - 1;
+    nx = *reinterpret_cast<const uint4*>(X + nrc * F + ccol);
+    nd = *reinterpret_cast<const uint4*>(DY + nrc * F + ccol);
+    nst = *reinterpret_cast<const float2*>(stats + 2 * nrc);
+    float x[8], dy[8], xh[8];
+    unpack8(cx, x);
+    unpack8(cd, dy);
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      xh[j] = (x[j] - mean) * rstd;
+      if constexpr (AK != 0) {
+        if (AK > 0 || act) dy[j] *= act_grad(AK > 0 ? AK : act, __builtin_fmaf(xh[j], sc[j], sh[j]));
+      }
+      const float dxh = dy[j] * sc[j];
+      s1 += dxh;
+      s2 += dxh * xh[j];
+      gs[j] += dy[j] * xh[j];
+      gb[j] += dy[j];
+    }
+    if (!colok) s1 = s2 = 0.f;
+    // (the activation forms keep the ds_bpermute steps: DPP measured 2-5 % slower there, 3-7 % faster elsewhere)
+    s1 = row_sum<LPR, NORM_DPP != 0 && AK == 0>(s1) * inv_f;
+    s2 = row_sum<LPR, NORM_DPP != 0 && AK == 0>(s2) * inv_f;
+    float r[8];
+    unpack8(cr, r);
+    uint32_t o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int j0 = 2 * j, j1 = 2 * j + 1;
+      float v0 = rstd * (dy[j0] * sc[j0] - s1 - xh[j0] * s2) + r[j0];
+      float v1 = rstd * (dy[j1] * sc[j1] - s1 - xh[j1] * s2) + r[j1];
+      if (AK != 0 && in_relu) {   // the norm's input was relu(z): dz = dx * [x > 0]
+        v0 = x[j0] > 0.f ? v0 : 0.f;
+        v1 = x[j1] > 0.f ? v1 : 0.f;
+      }
+      o[j] = pk2(v0, v1);
+    }
+    if (colok) *reinterpret_cast<uint4*>(DX + row * F + col) = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+  if (ws && colok) {
+    // lanes of groups past the last row hold zeros; a lane group that saw a row past `rows` summed nothing for it
+    // (its loop exited), so every slab row is exactly its lane group's sum
+    float* wr = ws + first * 2 * F;
+    *reinterpret_cast<float4*>(wr + col) = make_float4(gs[0], gs[1], gs[2], gs[3]);
+    *reinterpret_cast<float4*>(wr + col + 4) = make_float4(gs[4], gs[5], gs[6], gs[7]);
+    *reinterpret_cast<float4*>(wr + F + col) = make_float4(gb[0], gb[1], gb[2], gb[3]);
+    *reinterpret_cast<float4*>(wr + F + col + 4) = make_float4(gb[4], gb[5], gb[6], gb[7]);
+  }
+}
+
 // deterministic fold of the parameter-gradient slab: out[g][f] += sum over partial rows p = g, g + period, ... (in
 // order) of ws[p][which * F + f] for the scale (which 0) and shift (which 1) halves. Block = 32 output columns x 8
 // segments of the partial rows; the 8 segment sums are added in segment order.
@@ -558,11 +731,6 @@ __global__ __launch_bounds__(NTH) void norm_fold_kernel(const float* __restrict_
   }
 }
 
-int grid_for(long long rows) {
-  long long g = (rows + 3) / 4;
-  return (int)(g < 2048 ? g : 2048);
-}
-
 }  // namespace
 
 struct ObstNormDesc {
@@ -591,9 +759,18 @@ struct ObstNormDesc {
 
 static int lanes_per_row(int F) { return F <= 64 ? 8 : F <= 128 ? 16 : F <= 256 ? 32 : 64; }
 
-#define NORM_DISPATCH(KERNEL, GRID, LDSB, ...)                                                      \
+// the forward's lanes per row: NORM_FWD_NARROW halves them for 128 < F <= 512 (two 16-byte chunks per lane and row)
+#ifndef NORM_FWD_NARROW
+#define NORM_FWD_NARROW 0
+#endif
+static int fwd_lanes_per_row(int F) {
+  return (NORM_FWD_NARROW && F > 128 && F <= 512) ? lanes_per_row(F) / 2 : lanes_per_row(F);
+}
+
+#define NORM_DISPATCH(KERNEL, GRID, LDSB, ...) NORM_DISPATCH_F(lanes_per_row, KERNEL, GRID, LDSB, __VA_ARGS__)
+#define NORM_DISPATCH_F(LPRF, KERNEL, GRID, LDSB, ...)                                              \
   do {                                                                                              \
-    switch (lanes_per_row(d->F)) {                                                                  \
+    switch (LPRF(d->F)) {                                                                           \
       case 8: NORM_DISPATCH_L(KERNEL, 8, GRID, LDSB, __VA_ARGS__); break;                           \
       case 16: NORM_DISPATCH_L(KERNEL, 16, GRID, LDSB, __VA_ARGS__); break;                         \
       case 32: NORM_DISPATCH_L(KERNEL, 32, GRID, LDSB, __VA_ARGS__); break;                         \
@@ -601,26 +778,70 @@ static int lanes_per_row(int F) { return F <= 64 ? 8 : F <= 128 ? 16 : F <= 256 
     }                                                                                               \
   } while (0)
 
-static int group_aligned(int grid, int groups, int F) {
+static int group_aligned(int grid, int groups, int F, int lpr) {
   // rows per grid step (4 waves x 64/LPR rows per block) must be a multiple of groups
   if (groups <= 1) return grid;
-  int a = groups, b = 4 * (64 / lanes_per_row(F));
+  int a = groups, b = 4 * (64 / lpr);
   while (b) { const int t = a % b; a = b; b = t; }
   const int q = groups / a;                 // blocks per group period
   return grid < q ? q : grid / q * q;
 }
 
+// The forward's grid: one resident wave of blocks (the occupancy of that instantiation x the CUs), grid-striding over
+// the rows. A fixed 2048-block grid left a tail whenever an instantiation fit fewer than 8 blocks per CU (72 VGPRs: 7
+// per CU, 1792 blocks in the first round and 256 in a second one).
+static int resident_blocks(const void* fn) {
+  static std::mutex mu;
+  static std::unordered_map<const void*, int> cache;
+  static int ncu = 0;
+  std::lock_guard<std::mutex> lk(mu);
+  if (ncu == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                 hipSuccess || ncu <= 0)
+      ncu = 256;
+  }
+  auto it = cache.find(fn);
+  if (it != cache.end()) return it->second;
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, NTH, 0) != hipSuccess || per_cu <= 0) per_cu = 8;
+  return cache[fn] = per_cu * ncu;
+}
+
+template <int LPR, typename K>
+static void fwd_launch(K kern, const ObstNormDesc* d, hipStream_t st) {
+  const long long need = (d->rows + 4 * (64 / LPR) - 1) / (4 * (64 / LPR));
+  const int cap = resident_blocks(reinterpret_cast<const void*>(kern));
+  const int grid = group_aligned((int)(need < cap ? need : cap), d->groups, d->F, LPR);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(NTH), 0, st, (const bf16_t*)d->X, d->scale, d->shift, (bf16_t*)d->Y,
+                     d->stats, d->rows, d->F, d->groups, d->eps, d->ext, d->act);
+}
+
+#define NORM_FWD_L(KERNEL, LPR)                                                         \
+  do {                                                                                  \
+    const int nch = (d->F + LPR * 8 - 1) / (LPR * 8);                                   \
+    if (nch <= 1) fwd_launch<LPR>(KERNEL<1, LPR>, d, st);                               \
+    else if (nch <= 2) fwd_launch<LPR>(KERNEL<2, LPR>, d, st);                          \
+    else if (nch <= 4) fwd_launch<LPR>(KERNEL<4, LPR>, d, st);                          \
+    else if (nch <= 8) fwd_launch<LPR>(KERNEL<8, LPR>, d, st);                          \
+    else if (nch <= 16) fwd_launch<LPR>(KERNEL<16, LPR>, d, st);                        \
+    else return -2;                                                                     \
+  } while (0)
+#define NORM_FWD_DISPATCH(KERNEL)                                                       \
+  do {                                                                                  \
+    switch (fwd_lanes_per_row(d->F)) {                                                  \
+      case 8: NORM_FWD_L(KERNEL, 8); break;                                             \
+      case 16: NORM_FWD_L(KERNEL, 16); break;                                           \
+      case 32: NORM_FWD_L(KERNEL, 32); break;                                           \
+      default: NORM_FWD_L(KERNEL, 64); break;                                           \
+    }                                                                                   \
+  } while (0)
+
 OBST_API int obst_norm_fwd(const ObstNormDesc* d, hipStream_t st) {
   if (d->F % 8 || d->rows <= 0) return -1;
-  if (d->act == ACT_GELU)
-    NORM_DISPATCH(norm_fwd_gelu_kernel, dim3(group_aligned(grid_for(d->rows), d->groups, d->F)), 0, (const bf16_t*)d->X,
-                  d->scale, d->shift, (bf16_t*)d->Y, d->stats, d->rows, d->F, d->groups, d->eps, d->ext, d->act);
-  else if (d->act)
-    NORM_DISPATCH(norm_fwd_act_kernel, dim3(group_aligned(grid_for(d->rows), d->groups, d->F)), 0, (const bf16_t*)d->X,
-                  d->scale, d->shift, (bf16_t*)d->Y, d->stats, d->rows, d->F, d->groups, d->eps, d->ext, d->act);
-  else
-    NORM_DISPATCH(norm_fwd_kernel, dim3(group_aligned(grid_for(d->rows), d->groups, d->F)), 0, (const bf16_t*)d->X,
-                  d->scale, d->shift, (bf16_t*)d->Y, d->stats, d->rows, d->F, d->groups, d->eps, d->ext, d->act);
+  if (d->act == ACT_GELU) NORM_FWD_DISPATCH(norm_fwd_gelu_kernel);
+  else if (d->act) NORM_FWD_DISPATCH(norm_fwd_act_kernel);
+  else NORM_FWD_DISPATCH(norm_fwd_kernel);
   return (int)hipGetLastError();
 }
 
@@ -631,11 +852,19 @@ OBST_API int obst_norm_partial(const ObstNormDesc* d, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
+// the one-chunk backward serves the row (F <= 8 x lanes per row), plain / bf16-residual / activation forms
+static bool norm_bwd_one_chunk(const ObstNormDesc* d) {
+  return NORM_BWD1_BPC > 0 && d->F <= 8 * lanes_per_row(d->F) && !d->partial && !d->ext && !d->R32 && !d->DX32;
+}
+
 static int norm_bwd_grid(const ObstNormDesc* d) {
-  // one resident wave of blocks (2 blocks of 4 waves per CU; wide rows: 1, bwd_blocks_per_cu) grid-strides over the
-  // rows; more blocks only grow the parameter-gradient slab that norm_fold_kernel reads back (2048 blocks: 103 us)
+  // one resident wave of blocks (2 blocks of 4 waves per CU; wide rows: 1, bwd_blocks_per_cu; the one-chunk kernel:
+  // NORM_BWD1_BPC) grid-strides over the rows; more blocks only grow the parameter-gradient slab that
+  // norm_fold_kernel reads back (2048 blocks: 103 us)
   const int lpr = lanes_per_row(d->F);
-  const int cap = (d->F + lpr * 8 - 1) / (lpr * 8) > 4 ? 256 : 512;
+  const int nch = (d->F + lpr * 8 - 1) / (lpr * 8);
+  const int cap = norm_bwd_one_chunk(d) ? 256 * (NORM_BWD1_BPC > 0 ? NORM_BWD1_BPC : 1)
+                  : nch > 4 ? 256 : nch == 1 ? 256 * NORM_BWD_BPC1 : 512;
   long long g = (d->rows + 15) / 16;
   int grid = (int)(g < cap ? (g < 1 ? 1 : g) : cap);
   if (d->groups > 1) {   // rows per grid step (4 waves x 64/LPR rows per block) must be a multiple of groups
@@ -649,12 +878,17 @@ static int norm_bwd_grid(const ObstNormDesc* d) {
 
 static bool norm_bwd_params(const ObstNormDesc* d) { return (d->dscale || d->dshift) && !d->partial; }
 
+// rows of the parameter-gradient slab: one per lane group (grouped rows, and every one-chunk launch), else one per
+// block
+static long long norm_bwd_parts(const ObstNormDesc* d) {
+  const long long grid = norm_bwd_grid(d);
+  return (d->groups > 1 || norm_bwd_one_chunk(d)) ? grid * 4 * (64 / lanes_per_row(d->F)) : grid;
+}
+
 // floats of the parameter-gradient slab obst_norm_bwd needs in desc->ws (0: no parameter gradients)
 OBST_API long long obst_norm_bwd_ws(const ObstNormDesc* d) {
   if (!norm_bwd_params(d) || d->F <= 0 || d->rows <= 0) return 0;
-  const long long grid = norm_bwd_grid(d);
-  const long long parts = d->groups > 1 ? grid * 4 * (64 / lanes_per_row(d->F)) : grid;
-  return parts * 2 * d->F;
+  return norm_bwd_parts(d) * 2 * d->F;
 }
 
 OBST_API int obst_norm_bwd(const ObstNormDesc* d, hipStream_t st) {
@@ -670,13 +904,33 @@ OBST_API int obst_norm_bwd(const ObstNormDesc* d, hipStream_t st) {
   NORM_DISPATCH(KERNEL, dim3(grid), lds, (const bf16_t*)d->X, (const bf16_t*)d->DY, d->scale, d->stats,           \
                 (bf16_t*)d->DX, d->dscale, d->dshift, d->rows, d->F, d->groups, d->Ffull, d->partial, d->ext,   \
                 (const bf16_t*)d->R, d->ws, d->R32, d->DX32, d->shift, d->act, d->in_relu)
-  if (d->R32) NORM_BWD_LAUNCH(norm_bwd32_kernel);
+  if (norm_bwd_one_chunk(d)) {
+#define NORM_BWD1_LAUNCH(AK)                                                                                     \
+  do {                                                                                                          \
+    const dim3 gr(grid), bl(NTH);                                                                               \
+    float* ws = params ? d->ws : nullptr;                                                                       \
+    switch (lanes_per_row(d->F)) {                                                                              \
+      case 8: hipLaunchKernelGGL((norm_bwd1_kernel<8, AK>), gr, bl, 0, st, NORM_BWD1_ARGS); break;             \
+      case 16: hipLaunchKernelGGL((norm_bwd1_kernel<16, AK>), gr, bl, 0, st, NORM_BWD1_ARGS); break;           \
+      case 32: hipLaunchKernelGGL((norm_bwd1_kernel<32, AK>), gr, bl, 0, st, NORM_BWD1_ARGS); break;           \
+      default: hipLaunchKernelGGL((norm_bwd1_kernel<64, AK>), gr, bl, 0, st, NORM_BWD1_ARGS); break;           \
+    }                                                                                                           \
+  } while (0)
+#define NORM_BWD1_ARGS                                                                                           \
+  (const bf16_t*)d->X, (const bf16_t*)d->DY, d->scale, d->shift, d->stats, (bf16_t*)d->DX, (const bf16_t*)d->R, \
+      ws, d->rows, d->F, d->groups, d->act, d->in_relu
+    if (d->act == ACT_GELU) NORM_BWD1_LAUNCH(ACT_GELU);
+    else if (d->act || d->in_relu) NORM_BWD1_LAUNCH(-1);
+    else NORM_BWD1_LAUNCH(0);
+#undef NORM_BWD1_LAUNCH
+#undef NORM_BWD1_ARGS
+  } else if (d->R32) NORM_BWD_LAUNCH(norm_bwd32_kernel);
   else if (d->act == ACT_GELU) NORM_BWD_LAUNCH(norm_bwd_gelu_kernel);
   else if (d->act || d->in_relu) NORM_BWD_LAUNCH(norm_bwd_act_kernel);
   else NORM_BWD_LAUNCH(norm_bwd_kernel);
 #undef NORM_BWD_LAUNCH
   if (params) {
-    const long long parts = d->groups > 1 ? (long long)grid * 4 * (64 / lanes_per_row(d->F)) : grid;
+    const long long parts = norm_bwd_parts(d);
     const long long nout = 2LL * d->groups * d->F;
     // a lane group's rows are p, p + nw, ... so partial row p belongs to group p % groups (nw % groups == 0)
     hipLaunchKernelGGL(norm_fold_kernel, dim3((unsigned)((nout + 31) / 32)), dim3(NTH), 0, st, d->ws, parts,
