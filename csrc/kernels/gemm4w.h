@@ -179,6 +179,12 @@ __device__ __forceinline__ void store16_nc(const V& v, int voff, const i32x4_t& 
 #pragma clang diagnostic pop
 
 __device__ __forceinline__ void fence() { __builtin_amdgcn_sched_barrier(0); }
+// 16-byte buffer load straight into an accumulator's AGPRs, invisible to the compiler's wait model: the caller waits
+// with an explicit counted vmcnt and then agpr_opaque()s the value before reading it (emit_zpipe)
+template <int IMM>
+__device__ __forceinline__ void load16_agpr(f32x4_t& dst, int voff, const i32x4_t& rs) {
+  asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen offset:%3" : "=a"(dst) : "v"(voff), "s"(rs), "n"(IMM) : "memory");
+}
 // makes c an asm-produced AGPR value (no later rematerialisation of what it was computed from)
 __device__ __forceinline__ void agpr_opaque(f32x4_t& c) { asm volatile("" : "+a"(c)); }
 
@@ -449,6 +455,11 @@ constexpr int idx(const int (&a)[8], int q) {
 #ifndef G4W_OPT
 #define G4W_OPT 0   // 4: LATE (row layout: epilogue 8.6k -> 6.5k clocks, +0.5-1 % per shape in the lab, but the
                     // step measured 137.2k vs 138.8k tokens/s: off); 1: RELAX
+#endif
+// the stream-update epilogue with the next fragment row's residual loads ahead of this row's stores (emit_zpipe);
+// 0: the plain per-row loads
+#ifndef G4W_ZPIPE
+#define G4W_ZPIPE 1
 #endif
 // the fp32 + bf16-copy (RevNet stream update) instantiation's options: its epilogue moves 10 bytes per output
 #ifndef G4W_ZCP_OPT
@@ -1189,6 +1200,64 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
           // skipped past N on an edge tile only shorten the queue the K loop's counted waits were derived for.)
           if constexpr (EX || AC == 2 || (RELAX && (ED || AC != 0))) __builtin_amdgcn_s_waitcnt(0x0f70);
         };
+        // The RevNet stream update (fp32 C = R + alpha acc, its bf16 copy in Zout) with the residual loads of fragment
+        // row i + 1 issued ahead of row i's stores. In the plain EX loop each row's residual loads were issued behind
+        // the previous row's 12 stores and consumed at once: vmcnt completes in order, so every row waited for the
+        // previous row's stores to be written AND for its own loads -- 8 serialized round trips per tile (the token
+        // mixer's stream-update product ran 4.1 ms against 2.1 ms for the same product without the update). Here row
+        // i + 1's loads go to acc[i]'s AGPRs (dead once row i's outputs are formed) by inline asm BEFORE row i's
+        // stores, and row i + 1 waits with vmcnt(12): row i's stores may stay in flight. Row 0's loads are the
+        // compiler's own. Full tiles only (edge tiles skip stores and would break the count).
+        auto emit_zpipe = [&]() {
+          const i32x4_t rr4 = make_rsrc(reinterpret_cast<const char*>(p.R) + ct.coff * ES + corg, cext);
+          static_for<8>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            const int vrow = voff + i * 16 * ES * ldcs;
+            f32x4_t r[8];
+            if constexpr (i == 0) {
+              static_for<4>([&](auto pc) {
+                constexpr int pp = decltype(pc)::value;
+                r[2 * pp] = __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rr, vrow + pp * 128, 0, 0));
+                r[2 * pp + 1] =
+                    __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rr, vrow + pp * 128 + 16, 0, 0));
+              });
+            } else {
+              asm volatile("s_waitcnt vmcnt(12)" ::: "memory");   // row i's residual landed (row i-1's stores: 12)
+              static_for<8>([&](auto jc) {
+                constexpr int j = decltype(jc)::value;
+                agpr_opaque(acc[i - 1][j]);   // the loaded values from here on
+                r[j] = acc[i - 1][j];
+              });
+            }
+            static_for<8>([&](auto jc) {   // in place: no second set of 32 VGPRs (the queue's LDS slot spilled)
+              constexpr int j = decltype(jc)::value;
+              r[j] = alpha * acc[i][j] + r[j];
+            });
+            if constexpr (i + 1 < 8) {   // row i + 1's residual into acc[i] (its accumulators are consumed)
+              const int vnext = vrow + 16 * ES * ldcs;
+              asm volatile("s_nop 4" ::: "memory");   // resource SGPRs possibly just written by VALU
+              static_for<4>([&](auto pc) {
+                constexpr int pp = decltype(pc)::value;
+                load16_agpr<pp * 128>(acc[i][2 * pp], vnext, rr4);
+                load16_agpr<pp * 128 + 16>(acc[i][2 * pp + 1], vnext, rr4);
+              });
+            }
+            static_for<4>([&](auto pc) {   // 12 stores per row (the count the next row's wait assumes)
+              constexpr int pp = decltype(pc)::value;
+              const f32x4_t va = r[2 * pp], vb = r[2 * pp + 1];
+              store16_padded<pp * 128, SC>(va, vrow, rc4, std::integral_constant<int, pp * 128>{});
+              store16_padded<pp * 128 + 16, SC>(vb, vrow, rc4, std::integral_constant<int, pp * 128 + 16>{});
+              store16_padded<pp * 64, SC>(v4u32_t{pack_bf16x2(va[0], va[1]), pack_bf16x2(va[2], va[3]),
+                                                  pack_bf16x2(vb[0], vb[1]), pack_bf16x2(vb[2], vb[3])},
+                                          vrow >> 1, rz4, std::integral_constant<int, pp * 64>{});
+            });
+            fence();
+          });
+          if constexpr (PROF) {
+            if (stamp) epi_issue += __builtin_amdgcn_s_memtime() - tmark;
+          }
+          // (no vmcnt drain: every asm load was waited for; the stores drain under the next tile's first K-tile)
+        };
         using A0 = std::integral_constant<int, 0>;
         if constexpr (!OUT_F32) {
           if (gelu_direct && p.act == ACT_GELU) {
@@ -1213,7 +1282,13 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
           }
         } else {
           if (extra) {
-            if (edge) emit(T_{}, T_{}, A0{}); else emit(T_{}, F_{}, A0{});
+            if constexpr (ZCOPY && !TLAY && G4W_ZPIPE != 0) {
+              if (!edge && beta == 0.f && zout && p.R != nullptr) emit_zpipe();
+              else if (edge) emit(T_{}, T_{}, A0{});
+              else emit(T_{}, F_{}, A0{});
+            } else {
+              if (edge) emit(T_{}, T_{}, A0{}); else emit(T_{}, F_{}, A0{});
+            }
           } else {
             if (edge) emit(F_{}, T_{}, A0{}); else emit(F_{}, F_{}, A0{});
           }

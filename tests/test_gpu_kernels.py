@@ -258,8 +258,35 @@ def test_norm(cuda, F_, groups, nrows):
         _close(g, c, 3e-2, 2e-2, f"norm F={F_} {name}")
 
 
+@pytest.mark.parametrize("F_,groups,nrows", [(256, 8, 500), (192, 1, 700), (512, 8, 100), (96, 3, 1000),
+                                           (2048, 1, 64)])
+def test_norm_bwd_residual_one_chunk(cuda, F_, groups, nrows):
+    """the backward with the bf16 residual / stream gradient added (F.GradSink, bf16 streams) and parameter
+    gradients: rows of one 16-byte chunk per lane take norm_bwd1_kernel (lanes past F idle at F 192 / 96; per-lane-
+    group parameter slabs for every group count), 2048-wide rows the general body -- against the fp32 oracle"""
+    torch.manual_seed(F_ + groups)
+    rows = nrows * groups
+    x = (torch.randn(rows * F_) * 2 + 0.3).to(BF)
+    dy = torch.randn(rows * F_).to(BF)
+    r = torch.randn(rows * F_).to(BF)
+    sc = torch.randn(groups * F_) * 0.1 + 1
+    res = {}
+    for dev in ("cpu", cuda):
+        y = torch.zeros(rows * F_, dtype=BF, device=dev)
+        st = torch.zeros(2 * rows, device=dev)
+        raw.norm_fwd(x.to(dev), sc.to(dev), None, y, st, rows, F_, groups)
+        dx = torch.full((rows * F_,), float("nan"), dtype=BF, device=dev)
+        dsc = torch.zeros(groups * F_, device=dev)
+        dsh = torch.zeros(groups * F_, device=dev)
+        raw.norm_bwd(x.to(dev), dy.to(dev), sc.to(dev), st, dx, dsc, dsh, rows, F_, groups, R=r.to(dev))
+        res[str(dev)] = (y, dx, dsc, dsh)
+    torch.cuda.synchronize()
+    for name, g, c in zip(["y", "dx", "dscale", "dshift"], res[str(cuda)], res["cpu"]):
+        _close(g, c, 3e-2, 2e-2, f"norm+R F={F_} groups={groups} {name}")
+
+
 @pytest.mark.parametrize("act", ["gelu", "relu", "silu"])
-@pytest.mark.parametrize("F_,groups,nrows", [(256, 8, 300), (2048, 1, 96)])
+@pytest.mark.parametrize("F_,groups,nrows", [(256, 8, 300), (2048, 1, 96), (128, 1, 2000)])
 def test_norm_with_fused_activation(cuda, F_, groups, nrows, act):
     """norm + the following activation layer in one kernel (forward y = act(z)); the backward takes dy through
     act'(z) with z recomputed from the row statistics (its own kernel instantiation) -- against the fp32 oracle"""

@@ -1,0 +1,6 @@
+set -o pipefail
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+bash tools/profile.sh r6s_ctx32 --config configs/ctx32_mixer.json --steps 6 --warmup 3 > /dev/null || exit 1
+head -20 gpurun_out/prof_r6s_ctx32/steps.md
+bash tools/profile.sh r6s_neo --steps 6 --warmup 3 > /dev/null || exit 1
+head -12 gpurun_out/prof_r6s_neo/steps.md
