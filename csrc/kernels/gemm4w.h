@@ -182,7 +182,12 @@ __device__ __forceinline__ void fence() { __builtin_amdgcn_sched_barrier(0); }
 // 16-byte buffer load straight into an accumulator's AGPRs, invisible to the compiler's wait model: the caller waits
 // with an explicit counted vmcnt and then agpr_opaque()s the value before reading it (emit_zpipe)
 template <int IMM>
-__device__ __forceinline__ void load16_agpr(f32x4_t& dst, int voff, const i32x4_t& rs) {
+__device__ __forceinline__ void load16_agpr(f32x4_t& dst, int voff, const i32x4_t& rs_) {
+  i32x4_t rs;   // uniform by construction; read back into SGPRs as store16_nc does (the caller's s_nop covers the hazard)
+  rs[0] = __builtin_amdgcn_readfirstlane(rs_[0]);
+  rs[1] = __builtin_amdgcn_readfirstlane(rs_[1]);
+  rs[2] = __builtin_amdgcn_readfirstlane(rs_[2]);
+  rs[3] = __builtin_amdgcn_readfirstlane(rs_[3]);
   asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen offset:%3" : "=a"(dst) : "v"(voff), "s"(rs), "n"(IMM) : "memory");
 }
 // makes c an asm-produced AGPR value (no later rematerialisation of what it was computed from)
@@ -460,6 +465,9 @@ constexpr int idx(const int (&a)[8], int q) {
 // 0: the plain per-row loads
 #ifndef G4W_ZPIPE
 #define G4W_ZPIPE 1
+#endif
+#ifndef G4W_TPM
+#define G4W_TPM 3   // bit 0 residual, bit 1 gelu', bit 2 relu' (with all three the kernel hits "illegal VGPR to SGPR copy")
 #endif
 // the fp32 + bf16-copy (RevNet stream update) instantiation's options: its epilogue moves 10 bytes per output
 #ifndef G4W_ZCP_OPT
@@ -1258,13 +1266,93 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
           }
           // (no vmcnt drain: every asm load was waited for; the stores drain under the next tile's first K-tile)
         };
+        // The same pipelining on the row-layout (TLAY) bf16 epilogues with one 16-byte side input per row: the
+        // block output projections' residual (AC_ 0, R) and the activation backward of the FFN-in dgrad (AC_ 2 / 4,
+        // gelu' / relu' of Zin). Measured on GPT-Neo-1.3B's shapes the side input cost +23 % (131072 x 2048 x 2048
+        // + R) and +34 % (131072 x 8192 x 2048 with gelu', 3.22 -> 4.32 ms; tools/lab/epi_side_ab.py) -- 8 rows x
+        // (the previous row's 4 stores + this row's loads) of exposed latency per tile. Row i + 1's side rows go to
+        // acc[i][0..3] (consumed) ahead of row i's 4 stores; row i + 1 waits with vmcnt(4). Full tiles only.
+        auto emit_tpipe = [&](auto acc_) {
+          constexpr int AC_ = decltype(acc_)::value;
+          constexpr bool ACT = AC_ != 0;
+          constexpr int ACTK = AC_ >= 3 ? ACT_RELU : ACT_GELU;
+          const char* sbase = ACT ? reinterpret_cast<const char*>(p.Zin) + ct.coff * 2 + corg
+                                  : reinterpret_cast<const char*>(p.R) + ct.coff * ES + corg;
+          const i32x4_t rs4 = make_rsrc(sbase, cext);
+          const __amdgpu_buffer_rsrc_t rsb = ACT ? rzi : rr;
+          const int vt = ((wm * 128 + 4 * gq) * ldcs + wn * WN + 8 * ml) * ES;
+          static_for<8>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            int vro[4];
+            v4u32_t side[4];
+            static_for<4>([&](auto rk) {
+              constexpr int r = decltype(rk)::value;
+              vro[r] = vt + (16 * i + r) * ES * ldcs;
+            });
+            if constexpr (i == 0) {
+              static_for<4>([&](auto rk) {
+                constexpr int r = decltype(rk)::value;
+                side[r] = __builtin_amdgcn_raw_buffer_load_b128(rsb, vro[r], 0, 0);
+              });
+            } else {
+              asm volatile("s_waitcnt vmcnt(4)" ::: "memory");   // row i's side rows landed (row i-1's stores: 4)
+              static_for<4>([&](auto rk) {
+                constexpr int r = decltype(rk)::value;
+                agpr_opaque(acc[i - 1][r]);
+                side[r] = __builtin_bit_cast(v4u32_t, acc[i - 1][r]);
+              });
+            }
+            v4u32_t o0[4];
+            static_for<4>([&](auto rk) {
+              constexpr int r = decltype(rk)::value;
+              float x[8];
+              static_for<8>([&](auto jc) {
+                constexpr int j = decltype(jc)::value;
+                x[j] = alpha * acc[i][j][r];
+              });
+              static_for<4>([&](auto tc) {
+                constexpr int t = decltype(tc)::value;
+                const float lo = bf2f(side[r][t] & 0xffff), hi = bf2f(side[r][t] >> 16);
+                if constexpr (ACT) {
+                  x[2 * t] *= act_grad(ACTK, lo);
+                  x[2 * t + 1] *= act_grad(ACTK, hi);
+                } else {
+                  x[2 * t] += lo;
+                  x[2 * t + 1] += hi;
+                }
+              });
+              o0[r] = v4u32_t{pack_bf16x2(x[0], x[1]), pack_bf16x2(x[2], x[3]), pack_bf16x2(x[4], x[5]),
+                              pack_bf16x2(x[6], x[7])};
+            });
+            if constexpr (i + 1 < 8) {   // row i + 1's side rows into acc[i][0..3]
+              asm volatile("s_nop 4" ::: "memory");
+              static_for<4>([&](auto rk) {
+                constexpr int r = decltype(rk)::value;
+                load16_agpr<0>(acc[i][r], vt + (16 * (i + 1) + r) * ES * ldcs, rs4);
+              });
+            }
+            static_for<4>([&](auto rk) {   // 4 stores per row (the count the next row's wait assumes)
+              constexpr int r = decltype(rk)::value;
+              store16_nc<SC>(o0[r], vro[r], rc4);
+            });
+            fence();
+          });
+          if constexpr (PROF) {
+            if (stamp) epi_issue += __builtin_amdgcn_s_memtime() - tmark;
+          }
+        };
         using A0 = std::integral_constant<int, 0>;
+        const bool tfull = TLAY && G4W_ZPIPE != 0 && ct.n0 + 256 <= p.N;
         if constexpr (!OUT_F32) {
           if (gelu_direct && p.act == ACT_GELU) {
             using A1 = std::integral_constant<int, 1>;
             using A2 = std::integral_constant<int, 2>;
             if (p.mode == 1) {
-              if (edge) emit(F_{}, T_{}, A2{}); else emit(F_{}, F_{}, A2{});
+              if constexpr (TLAY) {
+                if ((G4W_TPM & 2) && tfull) emit_tpipe(A2{}); else emit(F_{}, F_{}, A2{});
+              } else {
+                if (edge) emit(F_{}, T_{}, A2{}); else emit(F_{}, F_{}, A2{});
+              }
             } else {
               if (edge) emit(F_{}, T_{}, A1{}); else emit(F_{}, F_{}, A1{});
             }
@@ -1272,11 +1360,18 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
             if constexpr (TLAY) {
               using A3 = std::integral_constant<int, 3>;
               using A4 = std::integral_constant<int, 4>;
-              if (p.mode == 1) emit(F_{}, F_{}, A4{});
-              else emit(F_{}, F_{}, A3{});
+              if (p.mode == 1) {
+                if ((G4W_TPM & 4) && tfull) emit_tpipe(A4{}); else emit(F_{}, F_{}, A4{});
+              } else {
+                emit(F_{}, F_{}, A3{});
+              }
             }
           } else if (extra) {
-            if (edge) emit(T_{}, T_{}, A0{}); else emit(T_{}, F_{}, A0{});
+            if constexpr (TLAY) {
+              if ((G4W_TPM & 1) && tfull) emit_tpipe(A0{}); else emit(T_{}, F_{}, A0{});
+            } else {
+              if (edge) emit(T_{}, T_{}, A0{}); else emit(T_{}, F_{}, A0{});
+            }
           } else {
             if (edge) emit(F_{}, T_{}, A0{}); else emit(F_{}, F_{}, A0{});
           }

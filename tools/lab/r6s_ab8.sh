@@ -1,0 +1,15 @@
+set -o pipefail
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+mkdir -p gpurun_out/r6s
+timeout -k 10 400 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_model.py -m gpu -x -q -k "gemm or stream or ffn or attention or model or residual or gelu" --timeout 120 --timeout-method thread > gpurun_out/r6s/tpipe_tests.log 2>&1 || { tail -30 gpurun_out/r6s/tpipe_tests.log; exit 1; }
+tail -1 gpurun_out/r6s/tpipe_tests.log
+for v in tree zpipe0; do
+  if [ $v = tree ]; then unset OBST_KERNELS; else export OBST_KERNELS=$PWD/lab_so/k_$v.so; fi
+  timeout -k 10 200 python -u tools/lab/epi_side_ab.py >> gpurun_out/r6s/epi_side_ab8.jsonl 2>/dev/null || exit 1
+done
+cat gpurun_out/r6s/epi_side_ab8.jsonl
+for v in tree zpipe0 tree; do
+  if [ $v = tree ]; then unset OBST_KERNELS; else export OBST_KERNELS=$PWD/lab_so/k_$v.so; fi
+  timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > gpurun_out/r6s/bench_ab8_$v.log 2>&1 || exit 1
+  echo "$v $(tail -1 gpurun_out/r6s/bench_ab8_$v.log | cut -c1-140)"
+done
