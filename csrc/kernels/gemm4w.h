@@ -181,6 +181,18 @@ __device__ __forceinline__ void store16_nc(const V& v, int voff, const i32x4_t& 
 __device__ __forceinline__ void fence() { __builtin_amdgcn_sched_barrier(0); }
 // 16-byte buffer load straight into an accumulator's AGPRs, invisible to the compiler's wait model: the caller waits
 // with an explicit counted vmcnt and then agpr_opaque()s the value before reading it (emit_zpipe)
+// emit_tpipe's side-row schedule: row i (i < 4) issues rows 2i + 1 and 2i + 2 (row 3: row 7) after forming its
+// outputs, then its 4 stores; row k waits until only the ops issued after its side rows are pending:
+//   k 1: R2 S0 | 2: S0 R3 R4 S1 | 3: R4 S1 R5 R6 S2 | 4: S1 R5 R6 S2 R7 S3 | 5: R6 S2 R7 S3 S4 | 6: S2 R7 S3 S4 S5 |
+//   7: S3 S4 S5 S6   (4 ops each)
+template <int K>
+__device__ __forceinline__ void tpipe_wait() {
+  static_assert(K >= 1 && K <= 7, "rows 1..7");
+  if constexpr (K == 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if constexpr (K == 2 || K == 7) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else if constexpr (K == 4) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+}
 template <int IMM>
 __device__ __forceinline__ void load16_agpr(f32x4_t& dst, int voff, const i32x4_t& rs_) {
   i32x4_t rs;   // uniform by construction; read back into SGPRs as store16_nc does (the caller's s_nop covers the hazard)
@@ -1295,11 +1307,13 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
                 side[r] = __builtin_amdgcn_raw_buffer_load_b128(rsb, vro[r], 0, 0);
               });
             } else {
-              asm volatile("s_waitcnt vmcnt(4)" ::: "memory");   // row i's side rows landed (row i-1's stores: 4)
+              // row i's side rows landed: the VMEM ops issued after them (TPIPE_W) may stay in flight
+              tpipe_wait<i>();
+              constexpr int lr = (i - 1) / 2, lj = (i & 1) ? 0 : 4;   // where row i's side rows were loaded
               static_for<4>([&](auto rk) {
                 constexpr int r = decltype(rk)::value;
-                agpr_opaque(acc[i - 1][r]);
-                side[r] = __builtin_bit_cast(v4u32_t, acc[i - 1][r]);
+                agpr_opaque(acc[lr][lj + r]);
+                side[r] = __builtin_bit_cast(v4u32_t, acc[lr][lj + r]);
               });
             }
             v4u32_t o0[4];
@@ -1324,11 +1338,15 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
               o0[r] = v4u32_t{pack_bf16x2(x[0], x[1]), pack_bf16x2(x[2], x[3]), pack_bf16x2(x[4], x[5]),
                               pack_bf16x2(x[6], x[7])};
             });
-            if constexpr (i + 1 < 8) {   // row i + 1's side rows into acc[i][0..3]
+            if constexpr (i < 4) {   // rows 2i + 1 (and 2i + 2) into acc[i][0..3] (and [4..7]): consumed
+              constexpr int k0 = 2 * i + 1, nk = i < 3 ? 2 : 1;
               asm volatile("s_nop 4" ::: "memory");
-              static_for<4>([&](auto rk) {
-                constexpr int r = decltype(rk)::value;
-                load16_agpr<0>(acc[i][r], vt + (16 * (i + 1) + r) * ES * ldcs, rs4);
+              static_for<nk>([&](auto hc) {
+                constexpr int h = decltype(hc)::value;
+                static_for<4>([&](auto rk) {
+                  constexpr int r = decltype(rk)::value;
+                  load16_agpr<0>(acc[i][4 * h + r], vt + (16 * (k0 + h) + r) * ES * ldcs, rs4);
+                });
               });
             }
             static_for<4>([&](auto rk) {   // 4 stores per row (the count the next row's wait assumes)

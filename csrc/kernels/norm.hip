@@ -45,6 +45,11 @@ constexpr int NTH = 256;
 #ifndef NORM_DPP
 #define NORM_DPP 1
 #endif
+// forward grid: 1 one resident wave of blocks (occupancy x CUs), 0 the fixed 2048-block grid of rounds 1-5 (1 measured
+// 1.5 % slower at GPT-Neo-1.3B's 2048-wide rows and equal elsewhere, profiles/r6s/norm_ab9.jsonl)
+#ifndef NORM_FWD_RESIDENT
+#define NORM_FWD_RESIDENT 0
+#endif
 // forward streaming hints: bit 0 nontemporal row loads, bit 1 nontemporal output stores
 #ifndef NORM_NT
 #define NORM_NT 0
@@ -787,9 +792,8 @@ static int group_aligned(int grid, int groups, int F, int lpr) {
   return grid < q ? q : grid / q * q;
 }
 
-// The forward's grid: one resident wave of blocks (the occupancy of that instantiation x the CUs), grid-striding over
-// the rows. A fixed 2048-block grid left a tail whenever an instantiation fit fewer than 8 blocks per CU (72 VGPRs: 7
-// per CU, 1792 blocks in the first round and 256 in a second one).
+// The forward's grid (NORM_FWD_RESIDENT): one resident wave of blocks (the occupancy of that instantiation x the CUs)
+// or the fixed 2048 blocks, grid-striding over the rows.
 static int resident_blocks(const void* fn) {
   static std::mutex mu;
   static std::unordered_map<const void*, int> cache;
@@ -811,7 +815,7 @@ static int resident_blocks(const void* fn) {
 template <int LPR, typename K>
 static void fwd_launch(K kern, const ObstNormDesc* d, hipStream_t st) {
   const long long need = (d->rows + 4 * (64 / LPR) - 1) / (4 * (64 / LPR));
-  const int cap = resident_blocks(reinterpret_cast<const void*>(kern));
+  const int cap = NORM_FWD_RESIDENT ? resident_blocks(reinterpret_cast<const void*>(kern)) : 2048;
   const int grid = group_aligned((int)(need < cap ? need : cap), d->groups, d->F, LPR);
   hipLaunchKernelGGL(kern, dim3(grid), dim3(NTH), 0, st, (const bf16_t*)d->X, d->scale, d->shift, (bf16_t*)d->Y,
                      d->stats, d->rows, d->F, d->groups, d->eps, d->ext, d->act);
