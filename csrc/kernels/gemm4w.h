@@ -193,6 +193,16 @@ __device__ __forceinline__ void tpipe_wait() {
   else if constexpr (K == 4) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
   else asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
 }
+// emit_zpipe's schedule (8 loads R per row, 12 stores S): row k waits until only the ops issued after its rows are
+// pending -- k 1: S0 | 2: R3 S1 | 3: S1 R4 S2 | 4: S2 R5 S3 | 5: S3 R6 S4 | 6: S4 R7 S5 | 7: S5 S6
+template <int K>
+__device__ __forceinline__ void zpipe_wait() {
+  static_assert(K >= 1 && K <= 7, "rows 1..7");
+  if constexpr (K == 1) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else if constexpr (K == 2) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+  else if constexpr (K == 7) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+}
 template <int IMM>
 __device__ __forceinline__ void load16_agpr(f32x4_t& dst, int voff, const i32x4_t& rs_) {
   i32x4_t rs;   // uniform by construction; read back into SGPRs as store16_nc does (the caller's s_nop covers the hazard)
@@ -1242,25 +1252,39 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm4w_kernel(GemmArgs p) {
                     __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rr, vrow + pp * 128 + 16, 0, 0));
               });
             } else {
-              asm volatile("s_waitcnt vmcnt(12)" ::: "memory");   // row i's residual landed (row i-1's stores: 12)
+              zpipe_wait<i>();   // row i's residual landed; the ops issued after it may stay in flight
+              constexpr int b = (i + 1) % 2;   // rows 1, 3, 5, 7 in acc[0], rows 2, 4, 6 in acc[1]
               static_for<8>([&](auto jc) {
                 constexpr int j = decltype(jc)::value;
-                agpr_opaque(acc[i - 1][j]);   // the loaded values from here on
-                r[j] = acc[i - 1][j];
+                agpr_opaque(acc[b][j]);   // the loaded values from here on
+                r[j] = acc[b][j];
               });
             }
             static_for<8>([&](auto jc) {   // in place: no second set of 32 VGPRs (the queue's LDS slot spilled)
               constexpr int j = decltype(jc)::value;
               r[j] = alpha * acc[i][j] + r[j];
             });
-            if constexpr (i + 1 < 8) {   // row i + 1's residual into acc[i] (its accumulators are consumed)
-              const int vnext = vrow + 16 * ES * ldcs;
-              asm volatile("s_nop 4" ::: "memory");   // resource SGPRs possibly just written by VALU
+            // two rows ahead: row 0 issues row 1 (acc[0]); row 1 rows 2 (acc[1]) and 3 (acc[0]); row i >= 2 row i + 2
+            // into the buffer row i was read from
+            auto issue = [&](auto kc, auto bc) {
+              constexpr int k = decltype(kc)::value, bb = decltype(bc)::value;
+              const int vk = voff + k * 16 * ES * ldcs;
               static_for<4>([&](auto pc) {
                 constexpr int pp = decltype(pc)::value;
-                load16_agpr<pp * 128>(acc[i][2 * pp], vnext, rr4);
-                load16_agpr<pp * 128 + 16>(acc[i][2 * pp + 1], vnext, rr4);
+                load16_agpr<pp * 128>(acc[bb][2 * pp], vk, rr4);
+                load16_agpr<pp * 128 + 16>(acc[bb][2 * pp + 1], vk, rr4);
               });
+            };
+            if constexpr (i == 0) {
+              asm volatile("s_nop 4" ::: "memory");   // resource SGPRs possibly just written by VALU
+              issue(std::integral_constant<int, 1>{}, std::integral_constant<int, 0>{});
+            } else if constexpr (i == 1) {
+              asm volatile("s_nop 4" ::: "memory");
+              issue(std::integral_constant<int, 2>{}, std::integral_constant<int, 1>{});
+              issue(std::integral_constant<int, 3>{}, std::integral_constant<int, 0>{});
+            } else if constexpr (i + 2 < 8) {
+              asm volatile("s_nop 4" ::: "memory");
+              issue(std::integral_constant<int, i + 2>{}, std::integral_constant<int, (i + 1) % 2>{});
             }
             static_for<4>([&](auto pc) {   // 12 stores per row (the count the next row's wait assumes)
               constexpr int pp = decltype(pc)::value;
